@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: committed msgs/s of the Partition-Raft append+CRC+commit path (BASELINE.json).
+
+Workload (BASELINE.json configs[2], the metric's configuration): per GPU, 4096 partitions,
+RF = 3 replicas co-located, Zipf(s = 1.1) partition load over a random permutation of ranks,
+100-byte records in 65536-record batches. One step = one rmq_append of one batch: stable
+partition sort, offsets, CRC32C, three replica copies, sparse index, quorum commit, high
+watermark. Inputs are resident in HBM before timing (a pool of distinct batches larger than the
+256 MiB Infinity Cache, so payload reads come from HBM).
+
+Multi-GPU: one process per GPU (torch.distributed.run); partitions shard by GPU (4096 per GPU,
+config C's layout) with no data-path collective -> weak scaling. The barrier and the max-over-
+ranks of the timed region use torch.distributed over gloo (host side); the engine itself never
+touches torch.
+
+roofline: achieved = algorithmic bytes per append launch / mean append-kernel duration, timed
+with HIP events on the engine's own stream inside the timed region; algorithmic bytes per record
+= (8 + L) read + RF * (16 + L) written, plus RF*8 + 16 per partition per batch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+# Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
+from ripplemq_amd.engine import Engine, EngineConfig  # noqa: E402
+from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(n: int, L: int, rf: int, P: int) -> int:
+    return n * ((8 + L) + rf * (16 + L)) + P * (rf * 8 + 16)
+
+
+def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float) -> dict:
+    """Time the C oracle (sequential restatement, SSE4.2 CRC) on a bounded sample of the workload."""
+    from oracle.oracle import OracleEngine  # cpu_baseline leg only
+
+    cfg = EngineConfig(num_partitions=spec.partitions, replication_factor=rf, segment_bytes=seg,
+                       index_interval=1024, max_batch_records=spec.records)
+    batches = [make_batch(spec, 10_000 + i) for i in range(4)]
+    recs, t_cpu, nb = 0, 0.0, 0
+    with OracleEngine(cfg) as ora:
+        while t_cpu < budget_s and nb < 400:
+            b = batches[nb % len(batches)]
+            t0 = time.perf_counter()
+            ora.append(b.pidx, b.lens, b.payload)
+            t_cpu += time.perf_counter() - t0
+            recs += b.n
+            nb += 1
+    return {"value": recs / t_cpu, "unit": "msgs/s", "cores": 1, "kind": "port",
+            "sample": f"{nb} batches x {spec.records} records (config B stream, {spec.partitions} "
+                      f"partitions, RF={rf}) through oracle/ripple_oracle.c ro_append, 1 thread, "
+                      f"{t_cpu:.1f} s"}
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
+    ap.add_argument("--segment-mb", type=int, default=8)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # host-side barrier / max only (gloo)
+
+        dist.init_process_group("gloo")
+
+    spec = CONFIGS[args.config]
+    rf = 3
+    L = spec.size if isinstance(spec.size, int) else None
+    cfg = EngineConfig(num_partitions=spec.partitions, replication_factor=rf,
+                       segment_bytes=args.segment_mb << 20, index_interval=1024,
+                       max_batch_records=spec.records, max_batch_bytes=64 << 20,
+                       pipeline_depth=3, device=local_rank, rank=0)
+    eng = Engine(cfg)
+    dev_name, cus = eng.device_info()
+
+    # resident input pool: distinct batches per rank (rank-salted stream keys)
+    pool = []
+    for q in range(args.pool):
+        b = make_batch(spec, 1_000_000 * rank + q)
+        d_pidx = eng.device_alloc(b.n * 4)
+        d_len = eng.device_alloc(b.n * 4)
+        d_pay = eng.device_alloc(max(b.payload.nbytes, 4))
+        eng.h2d(d_pidx, b.pidx)
+        eng.h2d(d_len, b.lens)
+        eng.h2d(d_pay, b.payload)
+        pool.append((b.n, d_pidx, d_len, d_pay, int(b.payload.nbytes), record_bytes(b.lens)))
+    d_out = [eng.device_alloc(spec.records * 8) for _ in range(4)]
+
+    def step(k: int) -> int:
+        n, dp, dl, dpay, pb, _ = pool[k % len(pool)]
+        return eng.append_device(n, dp, dl, dpay, pb, d_out[k % len(d_out)])
+
+    def barrier():
+        eng.sync()
+        if dist is not None:
+            dist.barrier()
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    eng.profile(True)
+    t0 = time.perf_counter()
+    last = 0
+    for k in range(args.steps):
+        last = step(args.warmup + k)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = eng.wait(last) if last else {}
+    n_app, app_ms = eng.profile_query(0)
+    n_sort, sort_ms = eng.profile_query(1)
+    eng.profile(False)
+
+    t_max = elapsed
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+
+    n = spec.records
+    total_records = n * args.steps * world
+    msgs_per_s = total_records / t_max
+    out = None
+    if rank == 0:
+        alg = algorithmic_bytes(n, L or 0, rf, spec.partitions)
+        mean_app_s = app_ms / 1e3 / max(n_app, 1)
+        achieved = alg / mean_app_s / 1e9 if n_app else 0.0
+        out = {
+            "metric": "committed msgs/sec (node) + HBM GB/s, 100B msgs, 4096 partitions RF=3",
+            "value": msgs_per_s,
+            "unit": "msgs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": t_max * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"config {args.config}: {spec.partitions} partitions/GPU, RF={rf}, "
+                                   f"{spec.mode}{'(s=%.1f)' % spec.zipf_s if spec.mode == 'zipf' else ''}, "
+                                   f"{L} B records, {n} records/batch",
+                       "partitions_per_gpu": spec.partitions, "replication_factor": rf,
+                       "records_per_batch": n, "record_payload_bytes": L,
+                       "parallelism": f"partition-sharded x{world}"},
+            "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "rmq::append_kernel", "algorithmic_bytes_per_launch": alg,
+                         "mean_kernel_us": mean_app_s * 1e6},
+            "kernels_us": {"append_mean": mean_app_s * 1e6,
+                           "sort_passes_mean": sort_ms * 1e3 / max(n_sort, 1)},
+            "append_stats_last": st,
+            "device": dev_name,
+            "cu_count": cus,
+        }
+    for _, dp, dl, dpay, _, _ in pool:
+        eng.device_free(dp)
+        eng.device_free(dl)
+        eng.device_free(dpay)
+    for d in d_out:
+        eng.device_free(d)
+    eng.close()
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(spec, rf, args.segment_mb << 20, args.cpu_budget)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,181 @@
+"""ctypes handle over the C oracle (oracle/libripple_oracle.so) — TEST INFRASTRUCTURE ONLY.
+
+Same method names and return shapes as ripplemq_amd.engine.Engine so a parity test can run one
+scenario through both and compare everything. Importable only from tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg; the product package never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from ripplemq_amd import _abi as A
+from ripplemq_amd.engine import FETCH_RES_DTYPE, EngineConfig, state_to_dict
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libripple_oracle.so")
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    lib = C.CDLL(LIB)
+    vp, u32, u64 = C.c_void_p, C.c_uint32, C.c_uint64
+    sigs = {
+        "ro_crc32c_bitwise": (u32, [vp, C.c_size_t]),
+        "ro_crc32c": (u32, [vp, C.c_size_t]),
+        "ro_crc32c_hw_available": (C.c_int, []),
+        "ro_create": (vp, [C.POINTER(A.RmqConfig)]),
+        "ro_destroy": (None, [vp]),
+        "ro_set_replicas": (C.c_int, [vp, u32, vp, u32, u32]),
+        "ro_become_leader": (C.c_int, [vp, u32, u64]),
+        "ro_append": (C.c_int, [vp, u32, vp, vp, vp, vp, u64, vp, C.POINTER(A.RmqAppendStats)]),
+        "ro_ack": (C.c_int, [vp, vp, vp, vp, u32]),
+        "ro_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp]),
+        "ro_fetch": (C.c_int, [vp, vp, u32, vp, u64, vp, C.POINTER(u64)]),
+        "ro_get_partition_state": (C.c_int, [vp, u32, C.POINTER(A.RmqPartitionState)]),
+        "ro_read_segment": (C.c_int, [vp, u32, u32, u64, u64, vp]),
+        "ro_read_index": (C.c_int, [vp, u32, u64, u64, vp]),
+        "ro_read_consumer_offsets": (C.c_int, [vp, u32, vp]),
+        "ro_record_pos": (C.c_int, [vp, u32, u64, C.POINTER(u64)]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def crc32c(data: bytes, bitwise: bool = False) -> int:
+    lib = load()
+    buf = (C.c_uint8 * max(len(data), 1)).from_buffer_copy(data or b"\0")
+    fn = lib.ro_crc32c_bitwise if bitwise else lib.ro_crc32c
+    return int(fn(buf, len(data)))
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+class OracleEngine:
+    """Sequential CPU restatement with the Engine's Python surface."""
+
+    def __init__(self, cfg: EngineConfig):
+        self.lib = load()
+        self.cfg = cfg
+        c = cfg.to_c()
+        self.h = self.lib.ro_create(C.byref(c))
+        if not self.h:
+            raise ValueError("invalid oracle config")
+
+    def close(self):
+        if self.h:
+            self.lib.ro_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_replicas(self, pidx, ranks, leader_slot):
+        r = (C.c_uint32 * len(ranks))(*ranks)
+        rc = self.lib.ro_set_replicas(self.h, pidx, r, len(ranks), leader_slot)
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+
+    def become_leader(self, pidx, term):
+        rc = self.lib.ro_become_leader(self.h, pidx, term)
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+
+    def append(self, pidx, lens, payload, payload_off=None):
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        lens = np.ascontiguousarray(lens, np.uint32)
+        payload = np.ascontiguousarray(payload, np.uint8)
+        if payload_off is not None:
+            payload_off = np.ascontiguousarray(payload_off, np.uint64)
+        out = np.empty(len(pidx), np.uint64)
+        st = A.RmqAppendStats()
+        rc = self.lib.ro_append(self.h, len(pidx), _p(pidx), _p(lens), _p(payload_off),
+                                _p(payload) if payload.size else None, payload.size, _p(out), C.byref(st))
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+        return out, {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_ if f != "reserved"}
+
+    def ack(self, pidx, slot, match):
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        slot = np.ascontiguousarray(slot, np.uint32)
+        match = np.ascontiguousarray(match, np.uint64)
+        rc = self.lib.ro_ack(self.h, _p(pidx), _p(slot), _p(match), len(pidx))
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+
+    def commit_consumer_offset(self, pidx, consumer, offset):
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        consumer = np.ascontiguousarray(consumer, np.uint32)
+        offset = np.ascontiguousarray(offset, np.uint64)
+        status = np.zeros(len(pidx), np.int32)
+        rc = self.lib.ro_commit_consumer_offset(self.h, _p(pidx), _p(consumer), _p(offset), len(pidx), _p(status))
+        return rc, status
+
+    def fetch(self, pidx, consumer, max_records, out_cap=None):
+        n = len(pidx)
+        req = np.zeros((n, 4), np.uint32)
+        req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
+        res = np.zeros(n, FETCH_RES_DTYPE)
+        used = C.c_uint64()
+        if out_cap is None:
+            self.lib.ro_fetch(self.h, _p(req), n, None, 0, _p(res), C.byref(used))
+            out_cap = int(used.value)
+        out = np.zeros(max(out_cap, 1), np.uint8)
+        rc = self.lib.ro_fetch(self.h, _p(req), n, _p(out), out_cap, _p(res), C.byref(used))
+        return rc, res, out[:out_cap], int(used.value)
+
+    def state(self, pidx):
+        s = A.RmqPartitionState()
+        rc = self.lib.ro_get_partition_state(self.h, pidx, C.byref(s))
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+        return state_to_dict(s, self.cfg.replication_factor)
+
+    def read_segment(self, replica, pidx, ring_off=0, n=None):
+        n = self.cfg.segment_bytes - ring_off if n is None else n
+        out = np.empty(n, np.uint8)
+        rc = self.lib.ro_read_segment(self.h, replica, pidx, ring_off, n, _p(out))
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+        return out
+
+    def read_index(self, pidx, m_first, count):
+        out = np.empty((count, 2), np.uint64)
+        rc = self.lib.ro_read_index(self.h, pidx, m_first, count, _p(out))
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+        return out
+
+    def consumer_offsets(self, pidx):
+        out = np.empty(self.cfg.max_consumers, np.uint64)
+        self.lib.ro_read_consumer_offsets(self.h, pidx, _p(out))
+        return out
+
+    def record_pos(self, pidx, offset):
+        v = C.c_uint64()
+        rc = self.lib.ro_record_pos(self.h, pidx, offset, C.byref(v))
+        if rc:
+            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+        return int(v.value)

@@ -1,0 +1,525 @@
+/*
+ * ripple_oracle.c — sequential CPU restatement of the reference partition state machine plus the
+ * FORMAT.md byte layout. TEST INFRASTRUCTURE ONLY (see ripple_oracle.h for what it restates and
+ * how it is pinned). Plain C99, one record at a time in apply order; no attempt to mirror how the
+ * GPU engine computes anything (no sort, no scans, no sparse-index walk for lookups).
+ */
+#include "ripple_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+#if defined(__x86_64__) && defined(__SSE4_2__)
+#include <nmmintrin.h>
+#define RO_HAVE_SSE42 1
+#else
+#define RO_HAVE_SSE42 0
+#endif
+
+#define RO_POLY 0x82F63B78u /* CRC32C (Castagnoli), reflected */
+
+/* ------------------------------------------------------------------------------------------ */
+/* CRC32C                                                                                      */
+/* ------------------------------------------------------------------------------------------ */
+
+uint32_t ro_crc32c_bitwise(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) {
+    c ^= p[i];
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (RO_POLY & (0u - (c & 1u)));
+  }
+  return c ^ 0xFFFFFFFFu;
+}
+
+static uint32_t ro_tab[8][256];
+static int ro_tab_ready = 0;
+
+static void ro_tab_init(void) {
+  if (ro_tab_ready) return;
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (RO_POLY & (0u - (c & 1u)));
+    ro_tab[0][b] = c;
+  }
+  for (uint32_t b = 0; b < 256; ++b)
+    for (int t = 1; t < 8; ++t) ro_tab[t][b] = (ro_tab[t - 1][b] >> 8) ^ ro_tab[0][ro_tab[t - 1][b] & 0xFF];
+  ro_tab_ready = 1;
+}
+
+int ro_crc32c_hw_available(void) { return RO_HAVE_SSE42; }
+
+uint32_t ro_crc32c(const uint8_t* p, size_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+#if RO_HAVE_SSE42
+  uint64_t c64 = c;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    c64 = _mm_crc32_u64(c64, v);
+    p += 8;
+    n -= 8;
+  }
+  c = (uint32_t)c64;
+  while (n--) c = _mm_crc32_u8(c, *p++);
+  return c ^ 0xFFFFFFFFu;
+#else
+  ro_tab_init();
+  while (n >= 8) {
+    uint32_t lo, hi;
+    memcpy(&lo, p, 4);
+    memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = ro_tab[7][lo & 0xFF] ^ ro_tab[6][(lo >> 8) & 0xFF] ^ ro_tab[5][(lo >> 16) & 0xFF] ^
+        ro_tab[4][lo >> 24] ^ ro_tab[3][hi & 0xFF] ^ ro_tab[2][(hi >> 8) & 0xFF] ^
+        ro_tab[1][(hi >> 16) & 0xFF] ^ ro_tab[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = (c >> 8) ^ ro_tab[0][(c ^ *p++) & 0xFF];
+  return c ^ 0xFFFFFFFFu;
+#endif
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* State                                                                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+  uint64_t* v;
+  uint64_t n, cap;
+} u64vec;
+
+static int vec_push(u64vec* a, uint64_t x) {
+  if (a->n == a->cap) {
+    uint64_t nc = a->cap ? a->cap * 2 : 1024;
+    uint64_t* nv = (uint64_t*)realloc(a->v, nc * sizeof(uint64_t));
+    if (!nv) return -1;
+    a->v = nv;
+    a->cap = nc;
+  }
+  a->v[a->n++] = x;
+  return 0;
+}
+
+typedef struct {
+  uint64_t leo, used, start_off, start_pos, commit, hw, term, term_start;
+  uint64_t match[RMQ_MAX_RF];
+  uint32_t ranks[RMQ_MAX_RF];
+  uint32_t leader_slot, is_leader;
+  u64vec idx_off, idx_pos; /* sparse index entries E[m], m = 0.. (unbounded, logical) */
+  u64vec rec_pos;          /* dense logical position of every record (oracle-only lookup) */
+  uint64_t* cons;          /* consumer offsets (reference: HashMap<String,Long>, default 0) */
+} ro_part;
+
+struct ro_engine {
+  rmq_config cfg;
+  ro_part* parts;
+  uint8_t** rings; /* [replica][partition] -> segment_bytes */
+  uint8_t* touched;
+};
+
+static int cfg_ok(const rmq_config* c) {
+  if (!c || c->num_partitions == 0 || c->replication_factor == 0 || c->replication_factor > RMQ_MAX_RF)
+    return 0;
+  if (c->index_interval < 64 || (c->index_interval & (c->index_interval - 1))) return 0;
+  if (c->segment_bytes == 0 || c->segment_bytes % c->index_interval) return 0;
+  if (c->segment_bytes <= 2ull * c->index_interval) return 0;
+  if (c->max_consumers == 0) return 0;
+  return 1;
+}
+
+ro_engine* ro_create(const rmq_config* cfg) {
+  if (!cfg_ok(cfg)) return NULL;
+  ro_tab_init();
+  ro_engine* e = (ro_engine*)calloc(1, sizeof(ro_engine));
+  if (!e) return NULL;
+  e->cfg = *cfg;
+  uint32_t P = cfg->num_partitions, RF = cfg->replication_factor;
+  e->parts = (ro_part*)calloc(P, sizeof(ro_part));
+  e->touched = (uint8_t*)calloc(P, 1);
+  e->rings = (uint8_t**)calloc((size_t)P * RF, sizeof(uint8_t*));
+  if (!e->parts || !e->touched || !e->rings) {
+    ro_destroy(e);
+    return NULL;
+  }
+  for (uint32_t p = 0; p < P; ++p) {
+    ro_part* s = &e->parts[p];
+    for (uint32_t r = 0; r < RF; ++r) s->ranks[r] = cfg->rank; /* all replicas co-located */
+    s->leader_slot = 0;
+    s->is_leader = 1; /* this engine leads every partition it hosts, term 1 */
+    s->term = 1;
+    s->term_start = 0;
+    s->cons = (uint64_t*)calloc(cfg->max_consumers, sizeof(uint64_t));
+    if (!s->cons || vec_push(&s->idx_off, 0) || vec_push(&s->idx_pos, 0)) { /* E[0] = (0, 0) */
+      ro_destroy(e);
+      return NULL;
+    }
+  }
+  for (size_t k = 0; k < (size_t)P * RF; ++k) {
+    e->rings[k] = (uint8_t*)calloc(cfg->segment_bytes, 1);
+    if (!e->rings[k]) {
+      ro_destroy(e);
+      return NULL;
+    }
+  }
+  return e;
+}
+
+void ro_destroy(ro_engine* e) {
+  if (!e) return;
+  uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  if (e->parts)
+    for (uint32_t p = 0; p < P; ++p) {
+      free(e->parts[p].idx_off.v);
+      free(e->parts[p].idx_pos.v);
+      free(e->parts[p].rec_pos.v);
+      free(e->parts[p].cons);
+    }
+  if (e->rings)
+    for (size_t k = 0; k < (size_t)P * RF; ++k) free(e->rings[k]);
+  free(e->rings);
+  free(e->parts);
+  free(e->touched);
+  free(e);
+}
+
+static uint8_t* ring_of(ro_engine* e, uint32_t replica, uint32_t p) {
+  return e->rings[(size_t)replica * e->cfg.num_partitions + p];
+}
+
+static void ring_write(ro_engine* e, uint8_t* ring, uint64_t pos, const uint8_t* src, uint64_t n) {
+  uint64_t S = e->cfg.segment_bytes;
+  while (n) {
+    uint64_t o = pos % S, k = S - o < n ? S - o : n;
+    memcpy(ring + o, src, k);
+    pos += k;
+    src += k;
+    n -= k;
+  }
+}
+
+static void ring_read(ro_engine* e, const uint8_t* ring, uint64_t pos, uint8_t* dst, uint64_t n) {
+  uint64_t S = e->cfg.segment_bytes;
+  while (n) {
+    uint64_t o = pos % S, k = S - o < n ? S - o : n;
+    memcpy(dst, ring + o, k);
+    pos += k;
+    dst += k;
+    n -= k;
+  }
+}
+
+/* Raft quorum commit: N = k-th largest match, k = RF/2 + 1; commit moves to N only
+   if N > commit and the N-th record belongs to the current term (N > term_start). */
+static void commit_eval(ro_engine* e, ro_part* s) {
+  uint32_t RF = e->cfg.replication_factor, k = RF / 2 + 1;
+  uint64_t m[RMQ_MAX_RF];
+  for (uint32_t r = 0; r < RF; ++r) m[r] = s->match[r];
+  for (uint32_t i = 1; i < RF; ++i) /* insertion sort, descending */
+    for (uint32_t j = i; j > 0 && m[j - 1] < m[j]; --j) {
+      uint64_t t = m[j];
+      m[j] = m[j - 1];
+      m[j - 1] = t;
+    }
+  uint64_t N = m[k - 1];
+  if (N > s->commit && N > s->term_start) s->commit = N;
+  s->hw = s->commit;
+}
+
+/* Size retention (FORMAT.md §4): evaluated once per append batch. */
+static void retention_eval(ro_engine* e, ro_part* s) {
+  uint64_t S = e->cfg.segment_bytes, I = e->cfg.index_interval;
+  if (s->used - s->start_pos <= S) return;
+  uint64_t m = (s->used - S + I - 1) / I;
+  s->start_off = s->idx_off.v[m];
+  s->start_pos = s->idx_pos.v[m];
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Control                                                                                     */
+/* ------------------------------------------------------------------------------------------ */
+
+int ro_set_replicas(ro_engine* e, uint32_t p, const uint32_t* ranks, uint32_t rf, uint32_t leader_slot) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  if (!ranks || rf != e->cfg.replication_factor || leader_slot >= rf) return RMQ_EINVAL;
+  ro_part* s = &e->parts[p];
+  for (uint32_t r = 0; r < rf; ++r) s->ranks[r] = ranks[r];
+  s->leader_slot = leader_slot;
+  s->is_leader = ranks[leader_slot] == e->cfg.rank;
+  return RMQ_OK;
+}
+
+static int become_leader_one(ro_engine* e, uint32_t p, uint64_t term) {
+  ro_part* s = &e->parts[p];
+  uint32_t RF = e->cfg.replication_factor, slot = RF;
+  if (term < s->term) return RMQ_EINVAL;
+  for (uint32_t r = 0; r < RF; ++r)
+    if (s->ranks[r] == e->cfg.rank) {
+      slot = r;
+      break;
+    }
+  if (slot == RF) return RMQ_EINVAL; /* no replica of p lives here */
+  s->leader_slot = slot;
+  s->is_leader = 1;
+  s->term = term;
+  s->term_start = s->leo; /* jraft: pendingIndex = lastLogIndex + 1 at leader start */
+  for (uint32_t r = 0; r < RF; ++r) s->match[r] = s->ranks[r] == e->cfg.rank ? s->leo : 0;
+  return RMQ_OK;
+}
+
+int ro_become_leader(ro_engine* e, uint32_t p, uint64_t term) {
+  if (p == RMQ_ALL_PARTITIONS) {
+    for (uint32_t q = 0; q < e->cfg.num_partitions; ++q) {
+      int rc = become_leader_one(e, q, term);
+      if (rc) return rc;
+    }
+    return RMQ_OK;
+  }
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  return become_leader_one(e, p, term);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Append: PartitionStateMachine.onApply -> handleMessageAppendRequest (messages.addAll)       */
+/* ------------------------------------------------------------------------------------------ */
+
+int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* len,
+              const uint64_t* payload_off, const uint8_t* payload, uint64_t payload_bytes,
+              uint64_t* out_offsets, rmq_append_stats* stats) {
+  const rmq_config* c = &e->cfg;
+  uint32_t P = c->num_partitions, RF = c->replication_factor;
+  uint64_t I = c->index_interval;
+  rmq_append_stats st;
+  memset(&st, 0, sizeof st);
+  st.records = n;
+  if (n && (!pidx || !len || !out_offsets)) return RMQ_EINVAL;
+
+  /* validate payload ranges; compute the batch's record bytes (all records, FORMAT.md §3) */
+  uint64_t run = 0, out_bytes = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t off = payload_off ? payload_off[i] : run;
+    if (len[i] && (!payload || off > payload_bytes || len[i] > payload_bytes - off)) return RMQ_EINVAL;
+    run += len[i];
+    out_bytes += RMQ_RECORD_HEADER_BYTES + ((len[i] + 3u) & ~3ull);
+  }
+  if (out_bytes > c->segment_bytes - I) {
+    for (uint32_t i = 0; i < n; ++i) out_offsets[i] = RMQ_OFFSET_NONE;
+    st.rejected_no_space = n;
+    if (stats) *stats = st;
+    return RMQ_OK;
+  }
+
+  memset(e->touched, 0, P);
+  uint8_t* rec = NULL;
+  uint64_t rec_cap = 0;
+  run = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t off = payload_off ? payload_off[i] : run;
+    run += len[i];
+    uint32_t p = pidx[i];
+    if (p >= P) {
+      out_offsets[i] = RMQ_OFFSET_NONE;
+      st.rejected_no_partition++;
+      continue;
+    }
+    ro_part* s = &e->parts[p];
+    if (!s->is_leader) {
+      out_offsets[i] = RMQ_OFFSET_NONE;
+      st.rejected_not_leader++;
+      continue;
+    }
+    uint32_t L = len[i];
+    uint64_t rs = RMQ_RECORD_HEADER_BYTES + ((L + 3u) & ~3ull);
+    if (rs > rec_cap) {
+      uint8_t* nr = (uint8_t*)realloc(rec, rs);
+      if (!nr) {
+        free(rec);
+        return RMQ_ENOMEM;
+      }
+      rec = nr;
+      rec_cap = rs;
+    }
+    uint64_t o = s->leo, pos = s->used;
+    uint32_t crc = ro_crc32c(payload + off, L);
+    memcpy(rec, &o, 8); /* little-endian host */
+    memcpy(rec + 8, &L, 4);
+    memcpy(rec + 12, &crc, 4);
+    if (L) memcpy(rec + 16, payload + off, L);
+    memset(rec + 16 + L, 0, rs - 16 - L);
+    for (uint32_t r = 0; r < RF; ++r)
+      if (s->ranks[r] == c->rank) ring_write(e, ring_of(e, r, p), pos, rec, rs);
+    /* sparse index: every multiple m*I in (pos, pos + rs] now names the next record */
+    for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m) {
+      if (vec_push(&s->idx_off, o + 1) || vec_push(&s->idx_pos, pos + rs)) {
+        free(rec);
+        return RMQ_ENOMEM;
+      }
+    }
+    if (vec_push(&s->rec_pos, pos)) {
+      free(rec);
+      return RMQ_ENOMEM;
+    }
+    s->leo = o + 1;
+    s->used = pos + rs;
+    out_offsets[i] = o;
+    st.appended++;
+    e->touched[p] = 1;
+  }
+  free(rec);
+  for (uint32_t p = 0; p < P; ++p) {
+    if (!e->touched[p]) continue;
+    ro_part* s = &e->parts[p];
+    for (uint32_t r = 0; r < RF; ++r)
+      if (s->ranks[r] == c->rank) s->match[r] = s->leo; /* co-located replicas persisted */
+    commit_eval(e, s);
+    retention_eval(e, s);
+  }
+  if (stats) *stats = st;
+  return RMQ_OK;
+}
+
+int ro_ack(ro_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n) {
+  uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (pidx[i] >= P) return RMQ_ENOPART;
+    if (slot[i] >= RF) return RMQ_EINVAL;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    ro_part* s = &e->parts[pidx[i]];
+    uint64_t m = match[i] < s->leo ? match[i] : s->leo; /* matchIndex <= leader's last index */
+    if (m > s->match[slot[i]]) s->match[slot[i]] = m;
+  }
+  for (uint32_t i = 0; i < n; ++i) commit_eval(e, &e->parts[pidx[i]]);
+  return RMQ_OK;
+}
+
+/* PartitionStateMachine.handleConsumerOffsetUpdateRequest: put, last writer wins, unchecked. */
+int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t* consumer,
+                              const uint64_t* offset, uint32_t n, int32_t* status) {
+  int rc = RMQ_OK;
+  for (uint32_t i = 0; i < n; ++i) {
+    int st = RMQ_OK;
+    if (pidx[i] >= e->cfg.num_partitions)
+      st = RMQ_ENOPART;
+    else if (!e->parts[pidx[i]].is_leader)
+      st = RMQ_ENOTLEADER;
+    else if (consumer[i] >= e->cfg.max_consumers)
+      st = RMQ_EINVAL;
+    else
+      e->parts[pidx[i]].cons[consumer[i]] = offset[i];
+    if (status) status[i] = st;
+    if (st && !rc) rc = st;
+  }
+  return rc;
+}
+
+/* PartitionStateMachine.handleBatchRead: off = consumerOffsets.getOrDefault(id, 0);
+   returns messages[off, min(off + max, size)) with size = applied (committed) records. */
+int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, uint64_t out_cap,
+             rmq_fetch_res* res, uint64_t* bytes_used) {
+  uint64_t cursor = 0;
+  int rc = RMQ_OK;
+  for (uint32_t r = 0; r < n; ++r) {
+    rmq_fetch_res* x = &res[r];
+    memset(x, 0, sizeof *x);
+    x->out_pos = cursor;
+    uint32_t p = reqs[r].pidx;
+    if (p >= e->cfg.num_partitions) {
+      x->status = RMQ_ENOPART;
+      continue;
+    }
+    ro_part* s = &e->parts[p];
+    if (!s->is_leader) {
+      x->status = RMQ_ENOTLEADER;
+      continue;
+    }
+    if (reqs[r].consumer >= e->cfg.max_consumers) {
+      x->status = RMQ_EINVAL;
+      continue;
+    }
+    uint64_t off = s->cons[reqs[r].consumer];
+    x->start_offset = off;
+    uint64_t lim = off + reqs[r].max_records;
+    if (lim < off) lim = UINT64_MAX;
+    uint64_t end = lim < s->hw ? lim : s->hw;
+    if (off >= end) continue; /* empty list */
+    if (off < s->start_off) {
+      x->status = RMQ_EOFFSET;
+      continue;
+    }
+    uint64_t p0 = s->rec_pos.v[off];
+    uint64_t p1 = end < s->leo ? s->rec_pos.v[end] : s->used;
+    uint64_t nb = p1 - p0;
+    if (cursor + nb > out_cap) {
+      x->status = RMQ_ENOSPC;
+      cursor += nb;
+      rc = RMQ_ENOSPC;
+      continue;
+    }
+    if (out) ring_read(e, ring_of(e, s->leader_slot, p), p0, out + cursor, nb);
+    x->count = (uint32_t)(end - off);
+    x->bytes = (uint32_t)nb;
+    cursor += nb;
+  }
+  if (bytes_used) *bytes_used = cursor;
+  return rc;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Read-back                                                                                   */
+/* ------------------------------------------------------------------------------------------ */
+
+int ro_get_partition_state(ro_engine* e, uint32_t p, rmq_partition_state* o) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  ro_part* s = &e->parts[p];
+  memset(o, 0, sizeof *o);
+  o->log_end_offset = s->leo;
+  o->log_end_pos = s->used;
+  o->log_start_offset = s->start_off;
+  o->log_start_pos = s->start_pos;
+  o->commit = s->commit;
+  o->high_watermark = s->hw;
+  o->term = s->term;
+  o->term_start = s->term_start;
+  for (uint32_t r = 0; r < RMQ_MAX_RF; ++r) {
+    o->match[r] = r < e->cfg.replication_factor ? s->match[r] : 0;
+    o->replica_rank[r] = r < e->cfg.replication_factor ? s->ranks[r] : 0;
+  }
+  o->leader_slot = s->leader_slot;
+  o->is_leader = s->is_leader;
+  return RMQ_OK;
+}
+
+int ro_read_segment(ro_engine* e, uint32_t replica, uint32_t p, uint64_t ring_off, uint64_t len, uint8_t* out) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  if (replica >= e->cfg.replication_factor || ring_off > e->cfg.segment_bytes ||
+      len > e->cfg.segment_bytes - ring_off)
+    return RMQ_EINVAL;
+  memcpy(out, ring_of(e, replica, p) + ring_off, len);
+  return RMQ_OK;
+}
+
+int ro_read_index(ro_engine* e, uint32_t p, uint64_t m_first, uint64_t count, uint64_t* out) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  ro_part* s = &e->parts[p];
+  if (m_first > s->idx_off.n || count > s->idx_off.n - m_first) return RMQ_EINVAL;
+  for (uint64_t k = 0; k < count; ++k) {
+    out[2 * k] = s->idx_off.v[m_first + k];
+    out[2 * k + 1] = s->idx_pos.v[m_first + k];
+  }
+  return RMQ_OK;
+}
+
+int ro_read_consumer_offsets(ro_engine* e, uint32_t p, uint64_t* out) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  memcpy(out, e->parts[p].cons, e->cfg.max_consumers * sizeof(uint64_t));
+  return RMQ_OK;
+}
+
+int ro_record_pos(ro_engine* e, uint32_t p, uint64_t offset, uint64_t* pos) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  ro_part* s = &e->parts[p];
+  if (offset > s->leo) return RMQ_EINVAL;
+  *pos = offset == s->leo ? s->used : s->rec_pos.v[offset];
+  return RMQ_OK;
+}

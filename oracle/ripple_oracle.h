@@ -1,0 +1,69 @@
+/*
+ * ripple_oracle.h — CPU restatement of RippleMQ's partition state machine (TEST INFRASTRUCTURE).
+ *
+ * This is the parity oracle for the MI355X engine. It is NOT part of the product: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it, and only as the checker
+ * (or as the timed CPU baseline). The engine library never links or calls it.
+ *
+ * It restates, record by record in apply order, what the reference computes:
+ *   - PartitionStateMachine.handleMessageAppendRequest: messages.addAll(batch), so the record j of
+ *     an applied entry gets offset size_before + j  (mq-broker/src/main/java/metadata/raft/
+ *     PartitionStateMachine.java:64-69; apply loop :38-62);
+ *   - handleConsumerOffsetUpdateRequest: consumerOffsets.put(id, off), last writer wins (:71-77);
+ *   - handleBatchRead: off = getOrDefault(id, 0); messages[off, min(off + max, size)) (:85-110);
+ *   - the "Not leader" gate of the three processors (MessageAppendRequestProcessor.java:29-32,
+ *     MessageBatchReadRequestProcessor.java:29-33, ConsumerOffsetUpdateRequestProcessor.java:31-35),
+ *     as a documented divergence: the engine rejects instead of continuing;
+ *   - the Raft quorum-commit rule that jraft's BallotBox implements (third-party
+ *     com.alipay.sofa:jraft-core:1.3.15, not present in the container — restated from the Raft
+ *     paper: commit = max(commit, k-th largest matchIndex, k = RF/2+1) gated on the current term).
+ * plus the build-defined byte format of FORMAT.md (record header, CRC32C, ring segments, sparse
+ * offset index, size retention), which has no reference counterpart.
+ *
+ * Parity pins: CRC32C against the RFC 3720 §B.4 known-answer vectors; offsets / fetch slices /
+ * consumer offsets against a literal Python restatement of PartitionStateMachine.java
+ * (tests/refmodel.py); commit indices vs jraft are UNPINNED (no JVM, no jraft jar here).
+ */
+#ifndef RIPPLE_ORACLE_H
+#define RIPPLE_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../include/ripplemq_engine.h" /* shared result structs only */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ro_engine ro_engine;
+
+uint32_t ro_crc32c_bitwise(const uint8_t* p, size_t n); /* definitional, 1 bit per step */
+uint32_t ro_crc32c(const uint8_t* p, size_t n);         /* table (or SSE4.2) implementation */
+int ro_crc32c_hw_available(void);
+
+ro_engine* ro_create(const rmq_config* cfg);
+void ro_destroy(ro_engine* e);
+int ro_set_replicas(ro_engine* e, uint32_t pidx, const uint32_t* ranks, uint32_t rf, uint32_t leader_slot);
+int ro_become_leader(ro_engine* e, uint32_t pidx, uint64_t term);
+int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* len,
+              const uint64_t* payload_off, const uint8_t* payload, uint64_t payload_bytes,
+              uint64_t* out_offsets, rmq_append_stats* stats);
+int ro_ack(ro_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n);
+int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t* consumer,
+                              const uint64_t* offset, uint32_t n, int32_t* status);
+int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, uint64_t out_cap,
+             rmq_fetch_res* res, uint64_t* bytes_used);
+
+int ro_get_partition_state(ro_engine* e, uint32_t pidx, rmq_partition_state* out);
+int ro_read_segment(ro_engine* e, uint32_t replica, uint32_t pidx, uint64_t ring_off, uint64_t len,
+                    uint8_t* out);
+int ro_read_index(ro_engine* e, uint32_t pidx, uint64_t m_first, uint64_t count, uint64_t* out);
+int ro_read_consumer_offsets(ro_engine* e, uint32_t pidx, uint64_t* out);
+/* Logical position of record `offset` (dense, for cross-checking the sparse index). */
+int ro_record_pos(ro_engine* e, uint32_t pidx, uint64_t offset, uint64_t* pos);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,37 @@
+// partition_ops.hpp — per-partition state transitions shared by the append and control kernels.
+#pragma once
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace rmq {
+
+// Raft quorum commit (jraft BallotBox semantics; restated from the Raft paper since
+// jraft-core 1.3.15 is not in the container): N = k-th largest matchIndex of the partition's
+// replica row, k = RF/2 + 1 (the median for odd RF), held in registers and ordered by a
+// compare-exchange network; commit advances to N only if N > commit and the N-th record was
+// appended in the current term (N > term_start). hw (consumer-visible end) = commit.
+__device__ __forceinline__ void commit_rule(const DevState& st, u32 p) {
+  const u32 RF = st.RF, k = RF / 2 + 1;
+  u64 m[kMaxRF];
+#pragma unroll
+  for (u32 r = 0; r < kMaxRF; ++r) m[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
+  // k-th largest of the row in registers: insertion network, descending
+#pragma unroll
+  for (u32 i = 1; i < kMaxRF; ++i)
+#pragma unroll
+    for (u32 j = i; j > 0; --j) {
+      const u64 a = m[j - 1], b = m[j];
+      m[j - 1] = a > b ? a : b;
+      m[j] = a > b ? b : a;
+    }
+  u64 N = 0;
+#pragma unroll
+  for (u32 r = 0; r < kMaxRF; ++r) N = (r == k - 1) ? m[r] : N;
+  u64 c = st.commit[p];
+  if (N > c && N > st.term_start[p]) c = N;
+  st.commit[p] = c;
+  st.hw[p] = c;
+}
+
+
+}  // namespace rmq

@@ -1,0 +1,245 @@
+"""Python handle over the C-ABI engine (numpy in, numpy out).
+
+Thin host glue for tests, tools and bench.py: every call goes straight to
+``libripplemq_engine.so``; nothing here computes the data path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi as A
+
+
+class EngineError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {A.STATUS_NAMES.get(status, status)}")
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise EngineError(rc, what)
+    return rc
+
+
+def _ptr(a: np.ndarray | None) -> int | None:
+    return None if a is None else a.ctypes.data
+
+
+FETCH_RES_DTYPE = np.dtype([
+    ("start_offset", "<u8"), ("out_pos", "<u8"), ("count", "<u4"), ("bytes", "<u4"),
+    ("status", "<i4"), ("reserved", "<u4"),
+])
+STATE_FIELDS = ("log_end_offset", "log_end_pos", "log_start_offset", "log_start_pos", "commit",
+                "high_watermark", "term", "term_start")
+
+
+@dataclass
+class EngineConfig:
+    num_partitions: int
+    replication_factor: int = 3
+    segment_bytes: int = 1 << 20
+    index_interval: int = 1024
+    max_consumers: int = 8
+    max_batch_records: int = 65536
+    pipeline_depth: int = 3
+    max_batch_bytes: int = 64 << 20
+    device: int = 0
+    rank: int = 0
+
+    def to_c(self) -> A.RmqConfig:
+        c = A.RmqConfig()
+        for f, _ in A.RmqConfig._fields_:
+            setattr(c, f, getattr(self, f))
+        return c
+
+
+def state_to_dict(s: A.RmqPartitionState, rf: int) -> dict:
+    d = {f: int(getattr(s, f)) for f in STATE_FIELDS}
+    d["match"] = [int(s.match[r]) for r in range(rf)]
+    d["replica_rank"] = [int(s.replica_rank[r]) for r in range(rf)]
+    d["leader_slot"] = int(s.leader_slot)
+    d["is_leader"] = int(s.is_leader)
+    return d
+
+
+class Engine:
+    """One engine = one HIP device, P partitions, RF co-located or placed replicas."""
+
+    def __init__(self, cfg: EngineConfig, lib_path: str | None = None):
+        self.lib = A.load(lib_path) if lib_path else A.load()
+        self.cfg = cfg
+        h = C.c_void_p()
+        c = cfg.to_c()
+        _check(self.lib.rmq_create(C.byref(c), C.byref(h)), "rmq_create")
+        self.h = h
+        self._keep: dict[int, tuple] = {}
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.rmq_destroy(self.h)
+            self.h = None
+            self._keep.clear()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- control
+    def set_replicas(self, pidx: int, ranks, leader_slot: int) -> None:
+        r = (C.c_uint32 * len(ranks))(*ranks)
+        _check(self.lib.rmq_set_replicas(self.h, pidx, r, len(ranks), leader_slot), "rmq_set_replicas")
+
+    def become_leader(self, pidx: int, term: int) -> None:
+        _check(self.lib.rmq_become_leader(self.h, pidx, term), "rmq_become_leader")
+
+    # ---- append
+    def append_async(self, pidx: np.ndarray, lens: np.ndarray, payload: np.ndarray,
+                     payload_off: np.ndarray | None = None) -> tuple[int, np.ndarray]:
+        pidx = np.ascontiguousarray(pidx, dtype=np.uint32)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        if payload_off is not None:
+            payload_off = np.ascontiguousarray(payload_off, dtype=np.uint64)
+        out = np.empty(len(pidx), dtype=np.uint64)
+        b = A.RmqBatch(len(pidx), A.RMQ_MEM_HOST, _ptr(pidx), _ptr(lens), _ptr(payload_off),
+                       _ptr(payload) if payload.size else None, payload.size)
+        t = C.c_uint64()
+        _check(self.lib.rmq_append(self.h, C.byref(b), _ptr(out), C.byref(t)), "rmq_append")
+        self._keep[t.value] = (pidx, lens, payload, payload_off, out)
+        return t.value, out
+
+    def append_device(self, n: int, d_pidx: int, d_len: int, d_payload: int, payload_bytes: int,
+                      d_out: int, d_payload_off: int | None = None) -> int:
+        b = A.RmqBatch(n, A.RMQ_MEM_DEVICE, d_pidx, d_len, d_payload_off, d_payload, payload_bytes)
+        t = C.c_uint64()
+        _check(self.lib.rmq_append(self.h, C.byref(b), d_out, C.byref(t)), "rmq_append")
+        return t.value
+
+    def poll(self, ticket: int, want_commit: bool = False):
+        P = self.cfg.num_partitions
+        commit = np.empty(P, np.uint64) if want_commit else None
+        hw = np.empty(P, np.uint64) if want_commit else None
+        rc = _check(self.lib.rmq_poll_commit(self.h, ticket, _ptr(commit), _ptr(hw)), "rmq_poll_commit")
+        if rc == A.RMQ_PENDING:
+            return None
+        self._keep.pop(ticket, None)
+        return (commit, hw) if want_commit else True
+
+    def wait(self, ticket: int) -> dict:
+        st = A.RmqAppendStats()
+        _check(self.lib.rmq_ticket_stats(self.h, ticket, C.byref(st)), "rmq_ticket_stats")
+        self._keep.pop(ticket, None)
+        return {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_ if f != "reserved"}
+
+    def append(self, pidx, lens, payload, payload_off=None) -> tuple[np.ndarray, dict]:
+        t, out = self.append_async(pidx, lens, payload, payload_off)
+        stats = self.wait(t)
+        return out, stats
+
+    def sync(self) -> None:
+        _check(self.lib.rmq_sync(self.h), "rmq_sync")
+
+    def ack(self, pidx, slot, match) -> None:
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        slot = np.ascontiguousarray(slot, np.uint32)
+        match = np.ascontiguousarray(match, np.uint64)
+        _check(self.lib.rmq_ack(self.h, _ptr(pidx), _ptr(slot), _ptr(match), len(pidx)), "rmq_ack")
+
+    def commit_consumer_offset(self, pidx, consumer, offset) -> tuple[int, np.ndarray]:
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        consumer = np.ascontiguousarray(consumer, np.uint32)
+        offset = np.ascontiguousarray(offset, np.uint64)
+        status = np.zeros(len(pidx), np.int32)
+        rc = self.lib.rmq_commit_consumer_offset(self.h, _ptr(pidx), _ptr(consumer), _ptr(offset),
+                                                 len(pidx), _ptr(status))
+        if rc in (A.RMQ_EDEVICE, A.RMQ_ENOMEM):
+            raise EngineError(rc, "rmq_commit_consumer_offset")
+        return rc, status
+
+    def fetch(self, pidx, consumer, max_records, out_cap: int | None = None):
+        n = len(pidx)
+        req = np.zeros((n, 4), np.uint32)
+        req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
+        res = np.zeros(n, FETCH_RES_DTYPE)
+        if out_cap is None:
+            used = C.c_uint64()
+            rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, None, 0, _ptr(res), C.byref(used))
+            if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
+                raise EngineError(rc, "rmq_fetch")
+            out_cap = int(used.value)
+        out = np.zeros(max(out_cap, 1), np.uint8)
+        used = C.c_uint64()
+        rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, _ptr(out), out_cap, _ptr(res), C.byref(used))
+        if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
+            raise EngineError(rc, "rmq_fetch")
+        return rc, res, out[:out_cap], int(used.value)
+
+    # ---- read-back
+    def state(self, pidx: int) -> dict:
+        s = A.RmqPartitionState()
+        _check(self.lib.rmq_get_partition_state(self.h, pidx, C.byref(s)), "rmq_get_partition_state")
+        return state_to_dict(s, self.cfg.replication_factor)
+
+    def read_segment(self, replica: int, pidx: int, ring_off: int = 0, n: int | None = None) -> np.ndarray:
+        n = self.cfg.segment_bytes - ring_off if n is None else n
+        out = np.empty(n, np.uint8)
+        _check(self.lib.rmq_read_segment(self.h, replica, pidx, ring_off, n, _ptr(out)), "rmq_read_segment")
+        return out
+
+    def read_index(self, pidx: int, m_first: int, count: int) -> np.ndarray:
+        out = np.empty((count, 2), np.uint64)
+        _check(self.lib.rmq_read_index(self.h, pidx, m_first, count, _ptr(out)), "rmq_read_index")
+        return out
+
+    def consumer_offsets(self, pidx: int) -> np.ndarray:
+        out = np.empty(self.cfg.max_consumers, np.uint64)
+        _check(self.lib.rmq_read_consumer_offsets(self.h, pidx, _ptr(out)), "rmq_read_consumer_offsets")
+        return out
+
+    # ---- device memory / timing
+    def device_alloc(self, nbytes: int) -> int:
+        p = C.c_void_p()
+        _check(self.lib.rmq_device_alloc(self.h, nbytes, C.byref(p)), "rmq_device_alloc")
+        return p.value
+
+    def device_free(self, p: int) -> None:
+        _check(self.lib.rmq_device_free(self.h, p), "rmq_device_free")
+
+    def h2d(self, dst: int, src: np.ndarray) -> None:
+        src = np.ascontiguousarray(src)
+        _check(self.lib.rmq_memcpy(self.h, dst, _ptr(src), src.nbytes, 0), "rmq_memcpy")
+
+    def d2h(self, dst: np.ndarray, src: int) -> None:
+        _check(self.lib.rmq_memcpy(self.h, _ptr(dst), src, dst.nbytes, 1), "rmq_memcpy")
+
+    def profile(self, enable: bool) -> None:
+        _check(self.lib.rmq_profile_enable(self.h, 1 if enable else 0), "rmq_profile_enable")
+
+    def profile_query(self, kernel: int) -> tuple[int, float]:
+        n, ms = C.c_uint64(), C.c_double()
+        _check(self.lib.rmq_profile_query(self.h, kernel, C.byref(n), C.byref(ms)), "rmq_profile_query")
+        return int(n.value), float(ms.value)
+
+    def device_info(self) -> tuple[str, int]:
+        buf = C.create_string_buffer(256)
+        cu = C.c_uint32()
+        _check(self.lib.rmq_device_info(self.h, buf, 256, C.byref(cu)), "rmq_device_info")
+        return buf.value.decode(), int(cu.value)
+
+
+def parse_records(buf: np.ndarray) -> list[tuple[int, int, bytes]]:
+    """Split FORMAT.md records: [(offset, crc, payload), ...]."""
+    out, pos, b = [], 0, buf.tobytes()
+    while pos + 16 <= len(b):
+        off = int.from_bytes(b[pos:pos + 8], "little")
+        ln = int.from_bytes(b[pos + 8:pos + 12], "little")
+        crc = int.from_bytes(b[pos + 12:pos + 16], "little")
+        out.append((off, crc, b[pos + 16:pos + 16 + ln]))
+        pos += 16 + ((ln + 3) & ~3)
+    return out

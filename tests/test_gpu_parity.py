@@ -1,0 +1,165 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle, bit for bit.
+
+Every test runs the same op list through both (tests/parity.py) and compares offsets, stats,
+partition state, ring bytes, sparse index, consumer offsets and fetch output.
+"""
+import numpy as np
+import pytest
+
+from parity import compare_state, run_ops
+from ripplemq_amd.engine import Engine, EngineConfig
+from ripplemq_amd.workload import Batch, StreamSpec, make_batch
+
+pytestmark = pytest.mark.gpu
+
+
+def pair(oracle_mod, **kw):
+    cfg = EngineConfig(**kw)
+    return cfg, Engine(cfg), oracle_mod.OracleEngine(cfg)
+
+
+def test_small_mixed_sizes(oracle_mod):
+    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=3, segment_bytes=1 << 16,
+                         index_interval=256, max_batch_records=4096)
+    with dev, ora:
+        spec = StreamSpec(8, 300, "uniform", size=(0, 700), config_index=11)
+        ops = [("append", make_batch(spec, b)) for b in range(6)]
+        run_ops(dev, ora, cfg, ops, full_rings=True)
+
+
+@pytest.mark.parametrize("P,mode", [(1, "rr"), (7, "uniform"), (256, "rr"), (300, "zipf"), (4096, "zipf")])
+def test_partition_counts(oracle_mod, P, mode):
+    cfg, dev, ora = pair(oracle_mod, num_partitions=P, replication_factor=3, segment_bytes=1 << 20,
+                         index_interval=1024, max_batch_records=20000)
+    with dev, ora:
+        spec = StreamSpec(P, 5000, mode, size=100, config_index=12)
+        ops = [("append", make_batch(spec, b)) for b in range(3)]
+        run_ops(dev, ora, cfg, ops, full_rings=P <= 8)
+
+
+def test_retention_wraps_ring(oracle_mod):
+    # hot Zipf partitions wrap their 256 KB rings many times; log start follows the index rule
+    cfg, dev, ora = pair(oracle_mod, num_partitions=64, replication_factor=3, segment_bytes=1 << 18,
+                         index_interval=1024, max_batch_records=4096)
+    with dev, ora:
+        spec = StreamSpec(64, 2000, "zipf", size=(50, 150), config_index=13)
+        ops = [("append", make_batch(spec, b)) for b in range(12)]
+        run_ops(dev, ora, cfg, ops, full_rings=True)
+        starts = [ora.state(p)["log_start_offset"] for p in range(64)]
+        assert max(starts) > 0, "scenario must exercise retention"
+
+
+def test_large_records_direct_path(oracle_mod):
+    # log-uniform 64 B..16 KB (config D sizes): tiles overflow the LDS image -> direct path,
+    # long payloads -> whole-wave CRC with GF(2) shift-combine
+    cfg, dev, ora = pair(oracle_mod, num_partitions=16, replication_factor=5, segment_bytes=1 << 23,
+                         index_interval=1024, max_batch_records=4096, max_batch_bytes=32 << 20)
+    with dev, ora:
+        spec = StreamSpec(16, 700, "uniform", size=(64, 16384), config_index=14)
+        ops = [("append", make_batch(spec, b)) for b in range(3)]
+        run_ops(dev, ora, cfg, ops)
+
+
+def test_rejections_and_leadership(oracle_mod):
+    cfg, dev, ora = pair(oracle_mod, num_partitions=16, replication_factor=3, segment_bytes=1 << 16,
+                         index_interval=256, max_batch_records=4096)
+    with dev, ora:
+        spec = StreamSpec(16, 1500, "uniform", size=(1, 200), config_index=15, invalid_frac=0.05)
+        ops = [("append", make_batch(spec, 0)),
+               ("set_replicas", 3, [1, 0, 2], 0),        # partition 3 led by rank 1: not leader
+               ("set_replicas", 5, [0, 1, 2], 0),        # partition 5: only slot 0 local
+               ("become_leader", 5, 2),
+               ("append", make_batch(spec, 1)),
+               ("ack", [5], [1], [10]),                  # quorum needs 2 of 3: commit -> min(leo,10)
+               ("ack", [5, 5], [2, 1], [7, 3]),          # max() keeps slot 1 at 10
+               ("append", make_batch(spec, 2)),
+               ("become_leader", 5, 3),                  # new term: prior entries wait for a new one
+               ("ack", [5, 5], [1, 2], [10 ** 6, 10 ** 6]),
+               ("append", make_batch(spec, 3)),
+               ("ack", [5], [1], [10 ** 6]),
+               ("fetch", np.arange(16), np.zeros(16), np.full(16, 10))]
+        run_ops(dev, ora, cfg, ops, full_rings=True)
+
+
+def test_no_space_and_edge_batches(oracle_mod):
+    cfg, dev, ora = pair(oracle_mod, num_partitions=4, replication_factor=1, segment_bytes=1 << 12,
+                         index_interval=64, max_batch_records=4096)
+    with dev, ora:
+        empty = Batch(np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+        one = Batch(np.array([2], np.uint32), np.array([5], np.uint32), np.arange(5, dtype=np.uint8))
+        big = make_batch(StreamSpec(4, 400, "uniform", size=20, config_index=16), 0)  # > 4 KB - 64
+        ok = make_batch(StreamSpec(4, 100, "uniform", size=(0, 20), config_index=16), 1)
+        run_ops(dev, ora, cfg, [("append", empty), ("append", one), ("append", big), ("append", ok),
+                                ("append", ok), ("append", big)], full_rings=True)
+
+
+def test_explicit_payload_offsets(oracle_mod):
+    # caller-provided payload_off with gaps and unaligned starts
+    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=2, segment_bytes=1 << 16,
+                         index_interval=256, max_batch_records=4096)
+    with dev, ora:
+        g = np.random.default_rng(7)
+        n = 900
+        lens = g.integers(0, 300, n).astype(np.uint32)
+        gaps = g.integers(0, 9, n).astype(np.uint64)
+        off = np.cumsum(gaps + np.r_[0, lens[:-1]].astype(np.uint64)).astype(np.uint64)
+        payload = g.integers(0, 256, int(off[-1] + lens[-1] + 16), dtype=np.uint8)
+        b = Batch(g.integers(0, 8, n).astype(np.uint32), lens, payload)
+        run_ops(dev, ora, cfg, [("append", b, off, payload)], full_rings=True)
+
+
+def test_consumer_fetch_paths(oracle_mod):
+    cfg, dev, ora = pair(oracle_mod, num_partitions=32, replication_factor=3, segment_bytes=1 << 16,
+                         index_interval=256, max_consumers=4, max_batch_records=8192)
+    with dev, ora:
+        spec = StreamSpec(32, 3000, "zipf", size=(1, 180), config_index=17)
+        g = np.random.default_rng(3)
+        ops = []
+        for b in range(8):
+            ops.append(("append", make_batch(spec, b)))
+            n = 200
+            p = g.integers(0, 33, n)            # includes an unknown partition (32)
+            c = g.integers(0, 5, n)             # includes an invalid consumer id (4)
+            o = g.integers(0, 1200, n)          # lagging, current, beyond hw, evicted
+            ops.append(("consumer_commit", p, c, o))
+            ops.append(("fetch", p, c, g.integers(0, 40, n)))
+            ops.append(("fetch", p, c, np.full(n, 1024), 5000))  # output buffer too small
+        ops.append(("set_replicas", 9, [2, 0, 1], 0))
+        ops.append(("fetch", np.arange(32), np.zeros(32), np.full(32, 10)))
+        run_ops(dev, ora, cfg, ops, full_rings=True)
+
+
+def test_read_then_commit_consume_loop(oracle_mod):
+    # ConsumerClientImpl.consume: read max 10, commit offset + n, until drained
+    cfg, dev, ora = pair(oracle_mod, num_partitions=3, replication_factor=3, segment_bytes=1 << 16,
+                         index_interval=256, max_batch_records=4096)
+    with dev, ora:
+        b = make_batch(StreamSpec(3, 95, "rr", size=12, config_index=18), 0)
+        run_ops(dev, ora, cfg, [("append", b)])
+        for _ in range(12):
+            for eng in (dev, ora):
+                _, res, _, _ = eng.fetch([0, 1, 2], [0, 0, 0], [10, 10, 10])
+                eng.commit_consumer_offset([0, 1, 2], [0, 0, 0], res["start_offset"] + res["count"])
+        compare_state(dev, ora, cfg)
+        assert [int(dev.consumer_offsets(p)[0]) for p in range(3)] == [32, 32, 31]
+
+
+def test_config_B_full_batches(oracle_mod):
+    # BASELINE configs[2] at full size: 4096 partitions, Zipf s=1.1, 64k x 100 B, RF=3
+    cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 23,
+                         index_interval=1024, max_batch_records=65536)
+    with dev, ora:
+        spec = StreamSpec(4096, 65536, "zipf", size=100, config_index=2)
+        ops = [("append", make_batch(spec, b)) for b in range(3)]
+        run_ops(dev, ora, cfg, ops, check=False)
+        hot = np.argsort([-ora.state(p)["log_end_offset"] for p in range(4096)])
+        compare_state(dev, ora, cfg, parts=list(hot[:64]) + list(range(0, 4096, 97)))
+
+
+def test_config_A_full_batches(oracle_mod):
+    cfg, dev, ora = pair(oracle_mod, num_partitions=256, replication_factor=3, segment_bytes=1 << 23,
+                         index_interval=1024, max_batch_records=65536)
+    with dev, ora:
+        spec = StreamSpec(256, 65536, "rr", size=100, config_index=1)
+        run_ops(dev, ora, cfg, [("append", make_batch(spec, b)) for b in range(3)], check=False)
+        compare_state(dev, ora, cfg)
