@@ -9,54 +9,54 @@
 //   jraft BallotBox quorum commit: commit = max(commit, k-th largest matchIndex,
 //   k = RF/2+1) when that entry is from the current term.
 //
-// Input: the batch in the sort's partition-major order (slot s -> record svals[s] of partition
-// skeys[s], stable). One workgroup = 256 slots ("tile"), tiles taken from a monotonic ticket so
-// every predecessor a tile waits for has already started.
+// Input: the sort's slot records {pidx, record, len, payload offset} in stable partition-major
+// order. One WAVE = one tile of 64 slots (no workgroup barriers on the hot loop); waves take
+// tiles from a monotonic ticket, so every tile a wave waits on has already started.
 //
 // Per tile:
-//  1. segmented block scan of (record count, record bytes) over the slots -> rank and byte offset
-//     of every record inside its partition run;
-//  2. the head of each run reads the partition's log end (offset, byte position) from state; a
-//     run continued from earlier tiles gets its absolute base from a decoupled look-back over
-//     {epoch|status|count} granules (wave-wide 64-tile window);
-//  3. payloads are gathered into an LDS image laid out exactly as the log records (FORMAT.md:
-//     u64 offset | u32 len | u32 crc32c | payload | pad to 4), CRC32C computed from LDS with
-//     slicing-by-8 tables (one lane per record; one wave per record above 512 B, GF(2) combine);
-//  4. the image is streamed to every local replica ring with dword stores that are contiguous
-//     across lanes inside a partition run;
-//  5. the slot that ends a run finalizes the partition: log end, local matchIndex, quorum commit,
-//     high watermark, size retention.
-// Tiles whose record bytes exceed the LDS image go through a wave-per-record direct path.
+//  1. wave segmented scan of (record count, record bytes) keyed by partition -> rank and byte
+//     offset of each record inside its partition run;
+//  2. the head of each run reads the partition's log end from state; a run continued from
+//     earlier tiles gets its absolute base from a decoupled look-back over {epoch|status|count}
+//     granules (64-tile window per probe);
+//  3. the records are laid out in an LDS image exactly as in the log (FORMAT.md: u64 offset |
+//     u32 len | u32 crc32c | payload | pad to 4); payload dwords arrive by LDS-DMA
+//     (global_load_lds_dword, one wave-instruction per 256 image bytes, all in flight at once);
+//  4. CRC32C from LDS, slicing-by-8 tables in LDS, one lane per record (a whole wave with GF(2)
+//     shift-combine for payloads over 512 B);
+//  5. the image streams to every local replica ring: dword stores contiguous across lanes inside
+//     a run; the lane that ends a run finalizes the partition (log end, matchIndex, quorum commit,
+//     high watermark, retention).
+// Tiles whose records overflow the wave's LDS image, or with unaligned payloads, take a
+// wave-per-record path with register staging.
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "partition_ops.hpp"
 
 namespace rmq {
 
-constexpr u32 kT = kAppendThreads;
-constexpr u32 kTW = kT / 64;
-constexpr u32 kImgDw = kAppendImageBytes / 4;
-constexpr u32 kLongCrc = 512;  // payloads above this are CRC'd by a whole wave
+constexpr u32 kWaves = kAppendThreads / 64;        // waves per workgroup
+constexpr u32 kImgDw = kAppendImageBytes / 4;      // image dwords per wave
+constexpr u32 kLongCrc = 512;                      // payloads above this: whole-wave CRC
 constexpr u32 kStAgg = 1u, kStIncl = 2u;
+constexpr u32 kBadPart = 0x80000000u;              // slot len flag: pidx >= P
+
+struct WaveSmem {
+  u32 img[kImgDw];
+  uint8_t map[kImgDw];
+  u64 pos[64];
+  u64 rb_off[65];
+  u64 rb_pos[65];
+  u32 key[64];
+  u32 imgoff[64];
+  u32 len[64];
+  u32 so[64];
+  u32 mask[64];
+};
 
 struct AppendSmem {
   u32 crc[8][256];
-  u32 img[kImgDw];
-  uint8_t map[kImgDw];
-  u64 rb_off[kT + 1];  // absolute base per run id (0 = run continued from earlier tiles)
-  u64 rb_pos[kT + 1];
-  u64 so[kT];          // payload source offset per slot
-  u64 pos[kT];         // absolute logical byte position of the record
-  u32 len[kT];
-  u32 key[kT];
-  u32 mask[kT];
-  u32 imgoff[kT];
-  u32 crcv[kT];
-  u32 wsum[3][kTW];
-  u32 wflag[kTW];
-  u32 scan[kTW];
-  u32 misc[8];
-  u32 longlist[kT];
+  WaveSmem wv[kWaves];
 };
 
 __device__ __forceinline__ u32 load_payload_dw(const uint8_t* payload, u64 byte, u32 nb) {
@@ -80,7 +80,8 @@ __device__ __forceinline__ u32 crc_shift(const CrcConsts* cc, u32 crc, u32 n) {
 }
 
 // Whole-wave CRC32C of a payload. Lane l takes bytes [l*c, min((l+1)*c, L)), c = ceil(L/64)
-// rounded to 4; partial CRCs are shifted by the bytes that follow them and XOR-reduced.
+// rounded to 4; partial CRCs are shifted by the bytes that follow them and XOR-reduced
+// (crc(A||B) = crc(A) * x^(8|B|) ^ crc(B), linear in each part).
 template <bool kFromLds>
 __device__ u32 wave_crc32c(const u32 (*t)[256], const CrcConsts* cc, const u32* lds_dw,
                            const uint8_t* payload, u64 src, u32 L) {
@@ -104,8 +105,9 @@ __device__ u32 wave_crc32c(const u32 (*t)[256], const CrcConsts* cc, const u32* 
   return crc;
 }
 
-__device__ __forceinline__ void finalize_partition(const DevState& st, u32 p, u64 end_off, u64 end_pos) {
-  if (end_off == st.leo[p]) return;  // no record of this run was appended
+__device__ __forceinline__ void finalize_partition(const DevState& st, u32 p, u64 end_off, u64 end_pos,
+                                                   u64 leo_before) {
+  if (end_off == leo_before) return;  // no record of this run was appended
   st.leo[p] = end_off;
   st.used[p] = end_pos;
   const u32 lm = st.local_mask[p];
@@ -122,124 +124,77 @@ __device__ __forceinline__ void finalize_partition(const DevState& st, u32 p, u6
   }
 }
 
-__global__ __launch_bounds__(kT, 2) void append_kernel(AppendArgs a) {
+__global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   AppendSmem& S = *reinterpret_cast<AppendSmem*>(smem_raw);
-  const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  WaveSmem& W = S.wv[wv];
   const DevState& st = a.st;
   const u64 nospace_limit = ((u64)a.nospace_limit_hi << 32) | a.nospace_limit_lo;
   const bool nospace = a.batch_info[0] > nospace_limit;
 
-  for (u32 k = tid; k < 8 * 256; k += kT) (&S.crc[0][0])[k] = a.crc->table[k >> 8][k & 255];
+  for (u32 k = threadIdx.x; k < 8 * 256; k += kAppendThreads) (&S.crc[0][0])[k] = a.crc->table[k >> 8][k & 255];
+  __syncthreads();
 
   for (;;) {
-    __syncthreads();
-    if (tid == 0) S.misc[0] = (u32)(atomicAdd((unsigned long long*)a.tile_counter, 1ull) - a.tile_base);
-    __syncthreads();
-    const u32 tile = S.misc[0];
+    // Control values must be provably wave-uniform (readfirstlane / readlane), or the compiler
+    // structurizes the loop per lane and a __shfl can read a lane that already left it.
+    // every lane adds 1 (a uniform increment: one wave atomic of 64), no divergent branch at the
+    // loop head; the wave's ticket is lane 0's old value / 64
+    const u64 tk = atomicAdd((unsigned long long*)a.tile_counter, 1ull);
+    const u32 tile = __builtin_amdgcn_readfirstlane((u32)((tk - a.tile_base) >> 6));
     if (tile >= a.tiles) break;
 
-    const u32 s0 = tile * kT;
-    const u32 s = s0 + tid;
+    const u32 s0 = tile * 64u, s = s0 + lane;
     const bool in = s < a.n;
-    const u32 last_slot = (s0 + kT < a.n ? s0 + kT : a.n) - 1 - s0;  // tid of the tile's last slot
+    const u32 nin = a.n - s0 < 64u ? a.n - s0 : 64u;  // valid slots in this tile
+    const u32 last = nin - 1;
 
-    // ---- 1. per-slot record metadata
-    u32 key = 0, rec = 0, L = 0, praw = 0;
-    u64 so = 0;
-    bool range_ok = false;
-    if (in) {
-      key = a.skeys[s];
-      rec = a.svals[s];
-      if (rec < a.n && key < st.P) {
-        praw = a.pidx[rec];
-        L = a.len[rec];
-        so = a.src_off64 ? a.src_off64[rec] : (u64)a.src_off32[rec];
-        range_ok = so <= a.payload_bytes && L <= a.payload_bytes - so;
-      } else {
-        rec = 0;
-        key = 0;
-        praw = 0xFFFFFFFFu;
-        atomicOr(a.err, 2u);
-      }
-    }
-    const bool okp = in && praw < st.P;
-    const bool ok = okp && range_ok && st.is_leader[key] && !nospace;
+    // ---- 1. slot records (one 16-byte load per lane) and validity
+    uint4 sr = make_uint4(0, 0, 0, 0);
+    if (in) sr = a.slots[s];
+    const u32 key = sr.x, rec = sr.y, L = sr.z & ~kBadPart, so = sr.w;
+    u32 prev_key = __shfl_up(key, 1, 64), next_key = __shfl_down(key, 1, 64);
+    if (lane == 0) prev_key = s ? a.slots[s - 1].x : 0xFFFFFFFFu;
+    if (lane == last) next_key = s + 1 < a.n ? a.slots[s + 1].x : 0xFFFFFFFFu;
+    const bool okp = in && !(sr.z & kBadPart);
+    const bool range_ok = (u64)so + L <= a.payload_bytes;
+    const bool lead = in && st.is_leader[key];
+    const bool ok = okp && range_ok && lead && !nospace;
     const u32 cnt = ok ? 1u : 0u;
     const u32 rs = ok ? 16u + ((L + 3u) & ~3u) : 0u;
-    S.key[tid] = key;
-    __syncthreads();
-    u32 prev_key = 0, next_key = 0xFFFFFFFFu;
-    if (in) {
-      prev_key = tid ? S.key[tid - 1] : (s ? a.skeys[s - 1] : 0xFFFFFFFFu);
-      if (s + 1 < a.n) next_key = tid + 1 < kT ? S.key[tid + 1] : a.skeys[s + 1];
-    }
     const u32 head = in && (s == 0 || prev_key != key) ? 1u : 0u;
     const bool run_end = in && (s + 1 == a.n || next_key != key);
 
     if (nospace) {
       if (in) a.out_offsets[rec] = ~0ull;
-      const u64 bm = __ballot(in);
-      if (lane == 0 && bm) atomicAdd(&a.stats[3], (u32)__popcll(bm));
+      if (lane == 0) a.tile_stats[tile] = make_uint4(0, 0, 0, nin);
       continue;
     }
 
-    // ---- 2. segmented scan of (cnt, bytes) with run heads; inclusive count of heads = run id
-    u32 f = head, c_inc = cnt, b_inc = rs;
-    {
-      u32 f2 = head;
-      wave_seg_incl_scan(f, c_inc);
-      wave_seg_incl_scan(f2, b_inc);
-    }
-    u32 h_inc = wave_incl_scan(head);
-    if (lane == 63) {
-      S.wsum[0][w] = c_inc;
-      S.wsum[1][w] = b_inc;
-      S.wsum[2][w] = h_inc;
-      S.wflag[w] = f;
-    }
-    __syncthreads();
-    {
-      u32 cc = 0, cb = 0, ch = 0;
-      for (u32 k = 0; k < w; ++k) {
-        if (S.wflag[k]) {
-          cc = S.wsum[0][k];
-          cb = S.wsum[1][k];
-        } else {
-          cc += S.wsum[0][k];
-          cb += S.wsum[1][k];
-        }
-        ch += S.wsum[2][k];
-      }
-      if (!f) {
-        c_inc += cc;
-        b_inc += cb;
-      }
-      h_inc += ch;
-    }
+    // early load for the run-finalizing lanes (latency hides under the staging below)
+    u64 leo_before = 0;
+    if (run_end) leo_before = st.leo[key];
+
+    // ---- 2. segmented wave scan: rank / byte offset inside the run; run ids
+    u32 fc = head, fb = head, c_inc = cnt, b_inc = rs;
+    wave_seg_incl_scan(fc, c_inc);
+    wave_seg_incl_scan(fb, b_inc);
+    const u32 run_id = wave_incl_scan(head);  // 0: run continued from the previous tile
     const u32 c_exc = c_inc - cnt, b_exc = b_inc - rs;
-    const u32 run_id = h_inc;  // 0: the run continued from the previous tile
-    u32 tile_heads;
-    if (tid == last_slot) S.misc[1] = h_inc;
-    if (tid == 0) S.misc[3] = head;
-
-    // ---- 3. run heads read the partition log end
+    const u32 tile_heads = __builtin_amdgcn_readlane(run_id, last);
+    const bool cont = __builtin_amdgcn_readfirstlane(head) == 0u;
     if (head) {
-      S.rb_off[run_id] = st.leo[key];
-      S.rb_pos[run_id] = st.used[key];
+      W.rb_off[run_id] = st.leo[key];
+      W.rb_pos[run_id] = st.used[key];
     }
-    S.len[tid] = L;
-    S.so[tid] = so;
-    S.mask[tid] = ok ? st.local_mask[key] : 0u;
-    __syncthreads();
-    tile_heads = S.misc[1];
-    const bool cont = S.misc[3] == 0u;  // slot s0 continues a run of the previous tile
+    __builtin_amdgcn_wave_barrier();
 
-    // publish the tile's state for the look-back of later tiles
-    if (tid == last_slot) {
+    // publish this tile for the look-back of later tiles
+    if (lane == last) {
       if (tile_heads) {
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 0], S.rb_off[run_id] + c_inc);
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 1], S.rb_pos[run_id] + b_inc);
+        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 0], W.rb_off[run_id] + c_inc);
+        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 1], W.rb_pos[run_id] + b_inc);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         gran_store(&a.lb_status[tile], a.epoch, (kStIncl << 30) | c_inc);
       } else {
@@ -249,63 +204,61 @@ __global__ __launch_bounds__(kT, 2) void append_kernel(AppendArgs a) {
       }
     }
 
-    // ---- image layout (non-segmented prefix of record bytes)
-    u32 tb;
-    const u32 ioff = block_excl_scan<kTW>(rs, S.scan, &tb);
-    S.imgoff[tid] = ioff;
-    const bool image = tb <= kAppendImageBytes;
-
+    // ---- image layout
+    const u32 ioff = wave_incl_scan(rs) - rs;
+    const u32 tb = __builtin_amdgcn_readlane(ioff + rs, 63);
+    const bool aligned = __all(!ok || (so & 3u) == 0u);
+    const bool image = tb <= kAppendImageBytes && aligned;
+    W.key[lane] = key;
+    W.len[lane] = L;
+    W.so[lane] = so;
+    W.imgoff[lane] = ioff;
+    W.mask[lane] = ok ? st.local_mask[key] : 0u;
+    const u32 ndw = tb >> 2;
     if (image) {
-      for (u32 d = 0; d < rs / 4; ++d) S.map[ioff / 4 + d] = (uint8_t)tid;
-      __syncthreads();
-      // ---- 4a. gather payloads into the image (lanes walk consecutive dwords of a record)
-      const u32 ndw = tb / 4;
-      for (u32 dw = tid; dw < ndw; dw += kT) {
-        const u32 k = S.map[dw];
-        const u32 rel = dw - S.imgoff[k] / 4;
-        if (rel >= 4) {
-          const u32 b = 4 * (rel - 4), Lk = S.len[k];
-          S.img[dw] = b < Lk ? load_payload_dw(a.payload, S.so[k] + b, Lk - b < 4 ? Lk - b : 4) : 0u;
+      for (u32 d = 0; d < rs / 4; ++d) W.map[ioff / 4 + d] = (uint8_t)lane;
+      __builtin_amdgcn_wave_barrier();
+      // ---- 3. LDS-DMA gather of the payload dwords into the image
+      if (a.debug & 1u) {
+        for (u32 dw = lane; dw < ndw; dw += 64) {
+          const u32 k = W.map[dw];
+          const u32 rel = dw - (W.imgoff[k] >> 2);
+          if (rel >= 4) W.img[dw] = *reinterpret_cast<const u32*>(a.payload + W.so[k] + 4u * (rel - 4u));
         }
-      }
-      __syncthreads();
-      // ---- 4b. CRC32C from LDS: one lane per short record, one wave per long record
-      u32 crc = 0;
-      if (ok && L <= kLongCrc) crc = crc32c_lds(S.crc, &S.img[ioff / 4 + 4], L);
-      S.crcv[tid] = crc;
-      {
-        if (tid == 0) S.misc[2] = 0;
-        __syncthreads();
-        if (ok && L > kLongCrc) S.longlist[atomicAdd(&S.misc[2], 1u)] = tid;
-        __syncthreads();
-        const u32 nlong = S.misc[2];
-        for (u32 q = w; q < nlong; q += kTW) {
-          const u32 k = S.longlist[q];
-          const u32 cr = wave_crc32c<true>(S.crc, a.crc, &S.img[S.imgoff[k] / 4 + 4], nullptr, 0, S.len[k]);
-          if (lane == 0) S.crcv[k] = cr;
+      } else
+      for (u32 c = 0; c * 64 < ndw; ++c) {
+        const u32 dw = c * 64 + lane;
+        const uint8_t* src = a.payload;
+        if (dw < ndw) {
+          const u32 k = W.map[dw];
+          const u32 rel = dw - (W.imgoff[k] >> 2);
+          if (rel >= 4) src = a.payload + W.so[k] + 4u * (rel - 4u);
         }
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)&W.img[c * 64], 4, 0, 0);
       }
     }
 
-    // ---- 2b. look-back for a run continued from earlier tiles (wave 0)
-    if (cont && w == 0) {
+    // ---- 2b. look-back for a run continued from earlier tiles (overlaps the DMA)
+    if (cont && (a.debug & 2u)) {
+      if (lane == 0) {
+        W.rb_off[0] = 0;
+        W.rb_pos[0] = 0;
+      }
+    } else if (cont) {
       u64 acc_c = 0, acc_b = 0;
       long look = (long)tile - 1;
-      u32 spins = 0;
-      for (;;) {
+      for (u32 spins = 0;;) {
         const long t = look - (long)lane;
-        u64 x = 0;
-        if (t >= 0) x = gran_load(&a.lb_status[t]);
+        const u64 tc = t >= 0 ? (u64)t : 0ull;  // predicated, not branched (see the loop head)
+        const u64 x = gran_load(&a.lb_status[tc]);
         const bool ready = t >= 0 && (u32)(x >> 32) == a.epoch;
         const u32 stt = ((u32)x) >> 30;
         const u64 stop = __ballot(!ready || stt == kStIncl);
         const u32 fl = stop ? (u32)__ffsll((long long)stop) - 1u : 64u;
-        // lanes below the first stop lane are aggregates: add them
-        u64 ab = 0, ac = 0;
-        if (lane < fl) {
-          ac = ((u32)x) & 0x3FFFFFFFu;
-          ab = load_sc1_u64(&a.lb_abs[(u64)t * 4 + 2]);
-        }
+        const u64 ab_raw = load_sc1_u64(&a.lb_abs[tc * 4 + 2]);
+        u64 ac = lane < fl ? (u64)(((u32)x) & 0x3FFFFFFFu) : 0ull;
+        u64 ab = lane < fl ? ab_raw : 0ull;
         for (int d = 32; d >= 1; d >>= 1) {
           ac += __shfl_xor(ac, d, 64);
           ab += __shfl_xor(ab, d, 64);
@@ -316,49 +269,39 @@ __global__ __launch_bounds__(kT, 2) void append_kernel(AppendArgs a) {
           look -= 64;
           continue;
         }
-        const u32 fready = __shfl(ready ? 1u : 0u, fl, 64);
-        if (fready) {
+        if (__builtin_amdgcn_readlane(ready ? 1u : 0u, fl)) {
           const long tf = look - (long)fl;
-          u64 bo = 0, bp = 0;
-          if (lane == 0) {
-            bo = load_sc1_u64(&a.lb_abs[(u64)tf * 4 + 0]);
-            bp = load_sc1_u64(&a.lb_abs[(u64)tf * 4 + 1]);
-          }
-          bo = __shfl(bo, 0, 64);
-          bp = __shfl(bp, 0, 64);
-          if (lane == 0) {
-            S.rb_off[0] = bo + acc_c;
-            S.rb_pos[0] = bp + acc_b;
-          }
+          const u64 bo = load_sc1_u64(&a.lb_abs[(u64)tf * 4 + 0]) + acc_c;
+          const u64 bp = load_sc1_u64(&a.lb_abs[(u64)tf * 4 + 1]) + acc_b;
+          W.rb_off[0] = bo;  // every lane stores the same value
+          W.rb_pos[0] = bp;
           break;
         }
-        look -= (long)fl;  // consumed fl aggregates; wait for the not-yet-published tile
-        if (++spins >= kSpinLimit) {
-          if (lane == 0) {
-            atomicOr(a.err, kErrSpinTimeout);
-            S.rb_off[0] = 0;
-            S.rb_pos[0] = 0;
-          }
+        look -= (long)fl;  // consumed fl aggregates; wait for the unpublished tile
+        if (++spins >= a.spin_limit) {
+          atomicOr(a.err, kErrSpinTimeout);
+          W.rb_off[0] = 0;
+          W.rb_pos[0] = 0;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      __builtin_amdgcn_wave_barrier();
+      if (!tile_heads && lane == last) {
+        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 0], W.rb_off[0] + c_inc);
+        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 1], W.rb_pos[0] + b_inc);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gran_store(&a.lb_status[tile], a.epoch, (kStIncl << 30) | c_inc);
+      }
     }
-    __syncthreads();
-    if (cont && !tile_heads && tid == last_slot) {
-      store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 0], S.rb_off[0] + c_inc);
-      store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 1], S.rb_pos[0] + b_inc);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      gran_store(&a.lb_status[tile], a.epoch, (kStIncl << 30) | c_inc);
-    }
+    __builtin_amdgcn_wave_barrier();
 
     // ---- absolute offset / position of every record
-    const u64 off_abs = S.rb_off[run_id] + c_exc;
-    const u64 pos_abs = S.rb_pos[run_id] + b_exc;
-    S.pos[tid] = pos_abs;
+    const u64 off_abs = W.rb_off[run_id] + c_exc;
+    const u64 pos_abs = W.rb_pos[run_id] + b_exc;
+    W.pos[lane] = pos_abs;
     if (in) a.out_offsets[rec] = ok ? off_abs : ~0ull;
-    if (ok) {
-      // sparse offset index: multiples m*I in (pos, pos + rs] name the next record
+    if (ok) {  // sparse offset index: multiples m*I in (pos, pos + rs] name the next record
       const u64 end = pos_abs + rs;
       for (u64 m = (pos_abs >> st.interval_log2) + 1; (m << st.interval_log2) <= end; ++m) {
         u64* e = st.index + ((u64)key * st.icap + m % st.icap) * 2;
@@ -366,84 +309,87 @@ __global__ __launch_bounds__(kT, 2) void append_kernel(AppendArgs a) {
         e[1] = end;
       }
     }
-    __syncthreads();
 
+    const u64 segmask = st.seg - 1;
+    const u64 rstride = (u64)st.P * st.seg;
     if (image) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
+      __builtin_amdgcn_wave_barrier();
+      // ---- 4. CRC32C from LDS (zero the pad bytes of the last payload dword first)
+      if (ok && (L & 3u)) W.img[ioff / 4 + 4 + L / 4] &= (1u << (8 * (L & 3u))) - 1u;
+      __builtin_amdgcn_wave_barrier();
+      u32 crc = 0;
+      if (ok && L <= kLongCrc) crc = crc32c_lds(S.crc, &W.img[ioff / 4 + 4], L);
+      u64 longs = __ballot(ok && L > kLongCrc);
+      while (longs) {
+        const u32 k = (u32)__ffsll((long long)longs) - 1u;
+        longs &= longs - 1;
+        const u32 cr = wave_crc32c<true>(S.crc, a.crc, &W.img[W.imgoff[k] / 4 + 4], nullptr, 0, W.len[k]);
+        if (lane == k) crc = cr;
+      }
       if (ok) {
         const u32 d0 = ioff / 4;
-        S.img[d0 + 0] = (u32)off_abs;
-        S.img[d0 + 1] = (u32)(off_abs >> 32);
-        S.img[d0 + 2] = L;
-        S.img[d0 + 3] = S.crcv[tid];
+        W.img[d0 + 0] = (u32)off_abs;
+        W.img[d0 + 1] = (u32)(off_abs >> 32);
+        W.img[d0 + 2] = L;
+        W.img[d0 + 3] = crc;
       }
-      __syncthreads();
-      // ---- 4c. stream the image into every local replica ring
-      const u32 ndw = tb / 4;
-      const u64 segmask = st.seg - 1;
-      const u64 rstride = (u64)st.P * st.seg;
-      for (u32 dw = tid; dw < ndw; dw += kT) {
-        const u32 k = S.map[dw];
-        const u32 v = S.img[dw];
-        const u64 lp = S.pos[k] + (u64)(dw * 4 - S.imgoff[k]);
-        uint8_t* dst = st.logs + (u64)S.key[k] * st.seg + (lp & segmask);
-        const u32 msk = S.mask[k];
+      __builtin_amdgcn_wave_barrier();
+      // ---- 5. stream the image into every local replica ring
+      for (u32 dw = lane; dw < ndw; dw += 64) {
+        const u32 k = W.map[dw];
+        const u32 v = W.img[dw];
+        const u64 lp = W.pos[k] + (u64)(dw * 4u - W.imgoff[k]);
+        uint8_t* dst = st.logs + (u64)W.key[k] * st.seg + (lp & segmask);
+        const u32 msk = W.mask[k];
         for (u32 r = 0; r < st.RF; ++r)
           if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v;
       }
     } else {
-      // ---- direct path: one wave per record (tiles holding more bytes than the LDS image)
-      const u64 segmask = st.seg - 1;
-      const u64 rstride = (u64)st.P * st.seg;
-      for (u32 k = w; k < kT; k += kTW) {
-        const u32 msk = S.mask[k];
+      // ---- wave-per-record path (large or unaligned payloads)
+      for (u32 k = 0; k < nin; ++k) {
+        const u32 msk = __builtin_amdgcn_readfirstlane(W.mask[k]);
         if (!msk) continue;
-        const u32 Lk = S.len[k];
-        const u64 sk = S.so[k], P0 = S.pos[k];
+        const u32 Lk = __builtin_amdgcn_readfirstlane(W.len[k]);
+        const u64 sk = W.so[k], P0 = W.pos[k];
         const u32 cr = wave_crc32c<false>(S.crc, a.crc, nullptr, a.payload, sk, Lk);
-        uint8_t* base = st.logs + (u64)S.key[k] * st.seg;
+        uint8_t* rb = st.logs + (u64)W.key[k] * st.seg;
         const u32 pdw = (Lk + 3u) >> 2;
-        for (u32 d = lane; d < pdw; d += 64) {
-          const u32 b = 4 * d;
-          const u32 v = load_payload_dw(a.payload, sk + b, Lk - b < 4 ? Lk - b : 4);
-          const u64 lp = P0 + 16 + b;
+        const u64 ko = ((u64)__builtin_amdgcn_readlane((u32)(off_abs >> 32), k) << 32) |
+                       __builtin_amdgcn_readlane((u32)off_abs, k);
+        for (u32 d = lane; d < pdw + 4; d += 64) {
+          u32 v;
+          if (d >= 4) {
+            const u32 b = 4 * (d - 4);
+            v = load_payload_dw(a.payload, sk + b, Lk - b < 4 ? Lk - b : 4);
+          } else {
+            v = d == 0 ? (u32)ko : d == 1 ? (u32)(ko >> 32) : d == 2 ? Lk : cr;
+          }
+          const u64 lp = P0 + 4ull * d;
           for (u32 r = 0; r < st.RF; ++r)
-            if (msk >> r & 1u) *reinterpret_cast<u32*>(base + r * rstride + (lp & segmask)) = v;
-        }
-        if (lane == 0) S.crcv[k] = cr;
-      }
-      __syncthreads();
-      if (ok) {  // headers: the owner thread writes its record's 4 header dwords
-        uint8_t* base = st.logs + (u64)key * st.seg;
-        const u32 h[4] = {(u32)off_abs, (u32)(off_abs >> 32), L, S.crcv[tid]};
-        const u32 msk = S.mask[tid];
-        for (u32 d = 0; d < 4; ++d) {
-          const u64 lp = pos_abs + 4ull * d;
-          for (u32 r = 0; r < st.RF; ++r)
-            if (msk >> r & 1u) *reinterpret_cast<u32*>(base + r * rstride + (lp & segmask)) = h[d];
+            if (msk >> r & 1u) *reinterpret_cast<u32*>(rb + r * rstride + (lp & segmask)) = v;
         }
       }
     }
 
-    // ---- 5. finalize partitions whose run ends in this tile
-    if (run_end) finalize_partition(st, key, off_abs + cnt, pos_abs + rs);
+    // ---- 6. the lane that ends a run finalizes its partition
+    if (run_end) finalize_partition(st, key, off_abs + cnt, pos_abs + rs, leo_before);
 
-    // ---- stats
+    // ---- per-tile stats (no atomics): appended, not leader, unknown partition, no space
     {
-      const u64 m_app = __ballot(ok), m_nl = __ballot(okp && range_ok && !st.is_leader[key]),
-                m_np = __ballot(in && !okp);
-      if (lane == 0) {
-        if (m_app) atomicAdd(&a.stats[0], (u32)__popcll(m_app));
-        if (m_nl) atomicAdd(&a.stats[1], (u32)__popcll(m_nl));
-        if (m_np) atomicAdd(&a.stats[2], (u32)__popcll(m_np));
-      }
+      const u32 n_app = (u32)__popcll(__ballot(ok));
+      const u32 n_nl = (u32)__popcll(__ballot(okp && range_ok && !lead));
+      const u32 n_np = (u32)__popcll(__ballot(in && !okp));
+      if (lane == 0) a.tile_stats[tile] = make_uint4(n_app, n_nl, n_np, 0);
     }
   }
 }
 
 int append_blocks_per_cu() { return 2; }
+int append_waves_per_block() { return (int)kWaves; }
 
 void launch_append(const AppendArgs& a, uint32_t grid, hipStream_t s) {
-  hipLaunchKernelGGL(append_kernel, dim3(grid), dim3(kT), sizeof(AppendSmem), s, a);
+  hipLaunchKernelGGL(append_kernel, dim3(grid), dim3(kAppendThreads), sizeof(AppendSmem), s, a);
 }
 
 }  // namespace rmq

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -23,8 +24,8 @@ using namespace rmq;
 
 namespace {
 
-constexpr uint32_t kStatsRing = 1024;
-constexpr uint32_t kMaxSortTiles = 64;
+constexpr uint32_t kStatsRing = 64;                               // tickets whose stats stay readable
+constexpr uint32_t kMaxSortTiles = 256;                           // all sort tiles must be co-resident
 constexpr uint32_t kMaxBatchRecords = kMaxSortTiles * kSortTile;  // 262144
 
 struct EvPair {
@@ -37,10 +38,14 @@ struct Slot {
   uint64_t* d_poff = nullptr;
   uint8_t* d_payload = nullptr;
   uint64_t* d_out = nullptr;
-  uint32_t* keys[2] = {nullptr, nullptr};
+  uint32_t* keys[2] = {nullptr, nullptr};  // intermediate radix passes (P > 4096 only)
   uint32_t* vals[2] = {nullptr, nullptr};
-  uint32_t* src_off = nullptr;
+  uint32_t* src_off = nullptr;             // packed payload offsets (multi-pass only)
+  uint4* slots = nullptr;                  // sorted slot records for the append kernel
   uint64_t* batch_info = nullptr;
+  uint64_t* hist_gran = nullptr;           // sort look-back granules [tiles][4096]
+  uint64_t* len_gran = nullptr;
+  uint64_t* len_val = nullptr;
   hipEvent_t prep_done = nullptr, append_done = nullptr;
   uint64_t ticket = 0;
   bool used = false;
@@ -59,10 +64,8 @@ struct rmq_engine {
   CrcConsts* d_crc = nullptr;
   uint64_t* d_winner = nullptr;
   uint32_t* d_err = nullptr;
-  uint32_t* d_stats = nullptr;  // [kStatsRing][4]
-  uint64_t* d_hist_gran = nullptr;
-  uint64_t* d_len_gran = nullptr;
-  uint64_t* d_rb_gran = nullptr;
+  uint4* d_tile_stats = nullptr;  // [kStatsRing][max append tiles]
+  uint32_t max_app_tiles = 0;
   uint64_t* d_lb_status = nullptr;
   uint64_t* d_lb_abs = nullptr;
   uint64_t* d_tile_counter = nullptr;
@@ -75,7 +78,7 @@ struct rmq_engine {
   std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
   std::vector<uint64_t> term;
   // sort plan
-  uint32_t passes = 1, pass_shift[3] = {0, 0, 0}, pass_bits[3] = {1, 0, 0};
+  uint32_t passes = 1, pass_shift[2] = {0, 0}, pass_bits[2] = {1, 0}, pass_ndig[2] = {1, 0};
   // fetch scratch
   uint32_t* d_req = nullptr;
   uint64_t* d_res = nullptr;
@@ -88,6 +91,10 @@ struct rmq_engine {
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;
   uint32_t ctl_cap = 0;
+  // RMQ_DEBUG_SKIP bit 0: skip the sort launch, bit 1: skip the append launch (bisecting only)
+  uint32_t debug_skip = 0;
+  uint32_t debug_flags = 0;   // RMQ_DEBUG_FLAGS -> AppendArgs.debug
+  uint32_t spin_limit = 1u << 22;
   // profiling
   bool profile = false;
   std::vector<EvPair> prof[5];
@@ -202,14 +209,15 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   void* bufs[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match,
                   s.is_leader, s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner,
-                  e->d_err, e->d_stats, e->d_hist_gran, e->d_len_gran, e->d_rb_gran,
+                  e->d_err, e->d_tile_stats,
                   e->d_lb_status, e->d_lb_abs, e->d_tile_counter, e->d_req, e->d_res, e->d_aux,
                   e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64};
   for (void* b : bufs)
     if (b) hipFree(b);
   for (Slot& sl : e->slots) {
     void* sb[] = {sl.d_pidx, sl.d_len, sl.d_poff, sl.d_payload, sl.d_out, sl.keys[0], sl.keys[1],
-                  sl.vals[0], sl.vals[1], sl.src_off, sl.batch_info};
+                  sl.vals[0], sl.vals[1], sl.src_off, sl.slots, sl.batch_info, sl.hist_gran,
+                  sl.len_gran, sl.len_val};
     for (void* b : sb)
       if (b) hipFree(b);
     if (sl.prep_done) hipEventDestroy(sl.prep_done);
@@ -287,6 +295,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (!e) return RMQ_ENOMEM;
   e->cfg = *cfg;
   if (!e->cfg.pipeline_depth) e->cfg.pipeline_depth = 3;
+  if (const char* dbg = std::getenv("RMQ_DEBUG_SKIP")) e->debug_skip = (uint32_t)std::atoi(dbg);
+  if (const char* dbg = std::getenv("RMQ_DEBUG_FLAGS")) e->debug_flags = (uint32_t)std::atoi(dbg);
+  if (const char* dbg = std::getenv("RMQ_SPIN_LIMIT")) e->spin_limit = (uint32_t)std::atoi(dbg);
   e->device = cfg->device;
 #define CREATE_TRY(x)      \
   do {                     \
@@ -328,14 +339,11 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&e->d_winner, (size_t)P * C));
   CREATE_TRY(dalloc(&e->d_err, 1));
-  CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * 4));
   const uint32_t max_sort_tiles = (cfg->max_batch_records + kSortTile - 1) / kSortTile;
-  const uint32_t max_app_tiles = (cfg->max_batch_records + kAppendThreads - 1) / kAppendThreads;
-  CREATE_TRY(dalloc(&e->d_hist_gran, (size_t)max_sort_tiles * 256));
-  CREATE_TRY(dalloc(&e->d_len_gran, max_sort_tiles));
-  CREATE_TRY(dalloc(&e->d_rb_gran, max_sort_tiles));
-  CREATE_TRY(dalloc(&e->d_lb_status, max_app_tiles));
-  CREATE_TRY(dalloc(&e->d_lb_abs, (size_t)max_app_tiles * 4));
+  e->max_app_tiles = (cfg->max_batch_records + kAppendTile - 1) / kAppendTile;
+  CREATE_TRY(dalloc(&e->d_tile_stats, (size_t)kStatsRing * e->max_app_tiles));
+  CREATE_TRY(dalloc(&e->d_lb_status, e->max_app_tiles));
+  CREATE_TRY(dalloc(&e->d_lb_abs, (size_t)e->max_app_tiles * 4));
   CREATE_TRY(dalloc(&e->d_tile_counter, 1));
   {
     CrcConsts h;
@@ -354,26 +362,31 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->term.assign(P, 1ull);
   e->ticket_n.assign(kStatsRing, 0u);
 
-  // radix plan over the partition-id bit width
+  // radix plan: 12-bit digits of the partition id (one pass for P <= 4096)
   uint32_t bits = ilog2((uint64_t)P);  // keys in [0, P-1]
   if (bits == 0) bits = 1;
-  e->passes = (bits + 7) / 8;
+  e->passes = (bits + 11) / 12;
   const uint32_t dw = (bits + e->passes - 1) / e->passes;
   for (uint32_t k = 0; k < e->passes; ++k) {
     e->pass_shift[k] = k * dw;
     e->pass_bits[k] = std::min(dw, bits - k * dw);
+    e->pass_ndig[k] = k + 1 == e->passes ? ((P - 1) >> e->pass_shift[k]) + 1 : 1u << e->pass_bits[k];
   }
 
   const uint32_t D = e->cfg.pipeline_depth;
   e->slots.resize(D);
   const uint32_t NB = cfg->max_batch_records;
   for (Slot& sl : e->slots) {
-    CREATE_TRY(dalloc(&sl.keys[0], NB));
-    CREATE_TRY(dalloc(&sl.keys[1], NB));
-    CREATE_TRY(dalloc(&sl.vals[0], NB));
-    CREATE_TRY(dalloc(&sl.vals[1], NB));
-    CREATE_TRY(dalloc(&sl.src_off, NB));
+    if (e->passes > 1) {
+      CREATE_TRY(dalloc(&sl.keys[0], NB));
+      CREATE_TRY(dalloc(&sl.vals[0], NB));
+      CREATE_TRY(dalloc(&sl.src_off, NB));
+    }
+    CREATE_TRY(dalloc(&sl.slots, NB));
     CREATE_TRY(dalloc(&sl.batch_info, 4));
+    CREATE_TRY(dalloc(&sl.hist_gran, (size_t)max_sort_tiles * kMaxDigits));
+    CREATE_TRY(dalloc(&sl.len_gran, max_sort_tiles));
+    CREATE_TRY(dalloc(&sl.len_val, (size_t)max_sort_tiles * 2));
     CREATE_HIP(hipEventCreateWithFlags(&sl.prep_done, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&sl.append_done, hipEventDisableTiming));
   }
@@ -465,7 +478,6 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   sl.used = true;
   sl.ticket = t;
   if (n == 0) {
-    HIP_TRY(hipMemsetAsync(e->d_stats + (t % kStatsRing) * 4, 0, 16, e->main_s));
     HIP_TRY(hipEventRecord(sl.append_done, e->main_s));
     return RMQ_OK;
   }
@@ -497,7 +509,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     d_out = sl.d_out;
   }
 
-  // ---- prep stream: stable partition-major sort of the batch (1-3 radix passes)
+  // ---- prep stream: stable partition-major sort of the batch into slot records
   const uint32_t sort_tiles = (n + kSortTile - 1) / kSortTile;
   hipEvent_t ps0 = nullptr, ps1 = nullptr;
   if (e->profile) {
@@ -510,27 +522,31 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   for (uint32_t k = 0; k < e->passes; ++k) {
     SortPassArgs a{};
     a.keys_in = kin;
+    a.pidx_raw = pidx;
     a.vals_in = vin;
-    a.keys_out = sl.keys[k & 1];
-    a.vals_out = sl.vals[k & 1];
-    a.n = n;
-    a.shift = e->pass_shift[k];
-    a.bits = e->pass_bits[k];
-    a.P = e->cfg.num_partitions;
-    a.first = k == 0;
-    a.epoch = ++e->epoch;
-    a.hist_gran = e->d_hist_gran;
-    a.tiles = sort_tiles;
-    a.len_gran = e->d_len_gran;
-    a.rb_gran = e->d_rb_gran;
+    a.keys_out = sl.keys[0];
+    a.vals_out = sl.vals[0];
+    a.slots = sl.slots;
     a.len = len;
+    a.payload_off = poff;
     a.src_off = poff ? nullptr : sl.src_off;
     a.batch_info = sl.batch_info;
-    a.stats = e->d_stats + (t % kStatsRing) * 4;
+    a.hist_gran = sl.hist_gran;
+    a.len_gran = sl.len_gran;
+    a.len_val = sl.len_val;
+    a.n = n;
+    a.tiles = sort_tiles;
+    a.shift = e->pass_shift[k];
+    a.bits = e->pass_bits[k];
+    a.ndig = e->pass_ndig[k];
+    a.P = e->cfg.num_partitions;
+    a.first = k == 0;
+    a.last = k + 1 == e->passes;
+    a.epoch = ++e->epoch;
     a.err = e->d_err;
-    launch_sort_pass(a, sort_tiles, e->prep_s);
-    kin = a.keys_out;
-    vin = a.vals_out;
+    if (!(e->debug_skip & 1u)) launch_sort_pass(a, sort_tiles, e->prep_s);
+    kin = sl.keys[0];
+    vin = sl.vals[0];
   }
   HIP_TRY(hipGetLastError());
   if (e->profile) {
@@ -543,38 +559,36 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   HIP_TRY(hipStreamWaitEvent(e->main_s, sl.prep_done, 0));
   AppendArgs a{};
   a.st = e->st;
-  a.skeys = kin;
-  a.svals = vin;
-  a.pidx = pidx;
-  a.len = len;
-  a.src_off32 = poff ? nullptr : sl.src_off;
-  a.src_off64 = poff;
+  a.slots = sl.slots;
   a.payload = payload;
   a.payload_bytes = b->payload_bytes;
   a.out_offsets = d_out;
   a.batch_info = sl.batch_info;
-  a.stats = e->d_stats + (t % kStatsRing) * 4;
+  a.tile_stats = e->d_tile_stats + (size_t)(t % kStatsRing) * e->max_app_tiles;
   a.lb_status = e->d_lb_status;
   a.lb_abs = e->d_lb_abs;
   a.tile_counter = e->d_tile_counter;
   a.tile_base = e->tile_base;
   a.n = n;
-  a.tiles = (n + kAppendThreads - 1) / kAppendThreads;
+  a.tiles = (n + kAppendTile - 1) / kAppendTile;
   a.epoch = ++e->epoch;
   const uint64_t lim = e->cfg.segment_bytes - e->cfg.index_interval;
   a.nospace_limit_lo = (uint32_t)lim;
   a.nospace_limit_hi = (uint32_t)(lim >> 32);
   a.crc = e->d_crc;
   a.err = e->d_err;
-  const uint32_t grid = std::min<uint32_t>(a.tiles, e->cu_count * (uint32_t)append_blocks_per_cu());
-  e->tile_base += (uint64_t)a.tiles + grid;
+  a.spin_limit = e->spin_limit;
+  a.debug = e->debug_flags;
+  const uint32_t wpb = (uint32_t)append_waves_per_block();
+  const uint32_t grid = std::min<uint32_t>((a.tiles + wpb - 1) / wpb, e->cu_count * (uint32_t)append_blocks_per_cu());
+  e->tile_base += 64ull * ((uint64_t)a.tiles + (uint64_t)grid * wpb);  // 64 per ticket; one failing ticket per wave
   hipEvent_t pa0 = nullptr, pa1 = nullptr;
   if (e->profile) {
     pa0 = pool_event(e);
     pa1 = pool_event(e);
     HIP_TRY(hipEventRecord(pa0, e->main_s));
   }
-  launch_append(a, grid, e->main_s);
+  if (!(e->debug_skip & 2u)) launch_append(a, grid, e->main_s);
   HIP_TRY(hipGetLastError());
   if (e->profile) {
     HIP_TRY(hipEventRecord(pa1, e->main_s));
@@ -645,14 +659,20 @@ int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out) {
   HIP_TRY(hipSetDevice(e->device));
   Slot& sl = e->slots[ticket % e->slots.size()];
   if (sl.ticket == ticket) HIP_TRY(hipEventSynchronize(sl.append_done));
-  uint32_t v[4];
-  HIP_TRY(hipMemcpy(v, e->d_stats + (ticket % kStatsRing) * 4, 16, hipMemcpyDeviceToHost));
+  const uint32_t n = e->ticket_n[ticket % kStatsRing];
+  const uint32_t tiles = (n + kAppendTile - 1) / kAppendTile;
+  std::vector<uint4> ts(tiles ? tiles : 1);
+  if (tiles)
+    HIP_TRY(hipMemcpy(ts.data(), e->d_tile_stats + (size_t)(ticket % kStatsRing) * e->max_app_tiles,
+                      tiles * sizeof(uint4), hipMemcpyDeviceToHost));
   std::memset(out, 0, sizeof *out);
-  out->records = e->ticket_n[ticket % kStatsRing];
-  out->appended = v[0];
-  out->rejected_not_leader = v[1];
-  out->rejected_no_partition = v[2];
-  out->rejected_no_space = v[3];
+  out->records = n;
+  for (uint32_t k = 0; k < tiles; ++k) {
+    out->appended += ts[k].x;
+    out->rejected_not_leader += ts[k].y;
+    out->rejected_no_partition += ts[k].z;
+    out->rejected_no_space += ts[k].w;
+  }
   return check_err(e);
 }
 

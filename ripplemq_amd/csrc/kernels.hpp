@@ -6,11 +6,13 @@
 
 namespace rmq {
 
-constexpr uint32_t kSortThreads = 512;
-constexpr uint32_t kSortItems = 8;
+constexpr uint32_t kSortThreads = 256;
+constexpr uint32_t kSortItems = 4;
+constexpr uint32_t kMaxDigits = 4096;                      // 12-bit digits per sort pass
 constexpr uint32_t kSortTile = kSortThreads * kSortItems;  // keys per sort tile
-constexpr uint32_t kAppendThreads = 256;                    // = slots per append tile
-constexpr uint32_t kAppendImageBytes = 32768;               // LDS image budget per tile
+constexpr uint32_t kAppendThreads = 256;                    // 4 waves; one 64-slot tile per wave
+constexpr uint32_t kAppendTile = 64;
+constexpr uint32_t kAppendImageBytes = 8192;                // LDS record image per wave
 constexpr uint32_t kMaxRF = 8;
 
 struct CrcConsts;
@@ -37,51 +39,49 @@ struct DevState {
   uint32_t pad;
 };
 
-// One append batch after the sort: slot s (sorted order) holds record vals[s] of partition keys[s].
+// One stable sort pass over the partition ids of a batch (see sort.hip).
 struct SortPassArgs {
-  const uint32_t* keys_in;   // pass 0: raw pidx of the input batch
-  const uint32_t* vals_in;   // pass 0: nullptr (identity)
-  uint32_t* keys_out;
+  const uint32_t* keys_in;      // first pass: raw pidx of the input batch
+  const uint32_t* pidx_raw;     // raw pidx of the input batch (last pass of a multi-pass sort)
+  const uint32_t* vals_in;      // later passes: record indices
+  uint32_t* keys_out;           // intermediate passes
   uint32_t* vals_out;
-  uint32_t n;
-  uint32_t shift, bits;      // digit = (key >> shift) & ((1 << bits) - 1)
-  uint32_t P;                // pass 0 clamps key = min(pidx, P-1)
-  uint32_t first;            // 1 on pass 0
+  uint4* slots;                 // last pass: {pidx, record, len, payload offset} per slot
+  const uint32_t* len;          // record payload lengths (input order)
+  const uint64_t* payload_off;  // caller payload offsets, or nullptr (packed)
+  uint32_t* src_off;            // packed payload offsets written by the first pass of a multi-pass sort
+  uint64_t* batch_info;         // first pass: [0] record bytes, [1] payload bytes of the batch
+  uint64_t* hist_gran;          // [tiles][ndig] look-back granules {epoch | flag | count}
+  uint64_t* len_gran;           // [tiles] look-back flags of the input-order length chain
+  uint64_t* len_val;            // [tiles][2] {aggregate, inclusive} of {record bytes:32 | payload:32}
+  uint32_t n, tiles;
+  uint32_t shift, bits, ndig;   // digit = (key >> shift) & ((1 << bits) - 1), ndig digits used
+  uint32_t P;
+  uint32_t first, last;
   uint32_t epoch;
-  uint64_t* hist_gran;       // [tiles][256]
-  uint32_t tiles;
-  uint64_t* len_gran;        // [tiles] payload bytes per tile (pass 0)
-  uint64_t* rb_gran;         // [tiles] record bytes per tile (pass 0)
-  const uint32_t* len;       // pass 0: record payload lengths
-  uint32_t* src_off;         // pass 0: packed payload offsets out (nullptr if caller gave payload_off)
-  uint64_t* batch_info;      // pass 0: [0] total record bytes
-  uint32_t* stats;           // pass 0: zeroed stats slot [4]
   uint32_t* err;
 };
 
 struct AppendArgs {
   DevState st;
-  const uint32_t* skeys;     // sorted keys [n]
-  const uint32_t* svals;     // sorted record indices [n]
-  const uint32_t* pidx;      // input order
-  const uint32_t* len;
-  const uint32_t* src_off32; // packed payload offsets (or nullptr)
-  const uint64_t* src_off64; // caller payload offsets (or nullptr)
+  const uint4* slots;        // sorted slot records {pidx, record, len | bad-partition flag, payload off}
   const uint8_t* payload;
   uint64_t payload_bytes;
   uint64_t* out_offsets;     // input order
   const uint64_t* batch_info;
-  uint32_t* stats;           // [4] appended, not_leader, no_partition, no_space
+  uint4* tile_stats;         // [tiles] {appended, not leader, unknown partition, no space}
   uint64_t* lb_status;       // [tiles] look-back granules
-  uint64_t* lb_abs;          // [tiles][2] absolute {offset, pos} at tile end (INCLUSIVE)
+  uint64_t* lb_abs;          // [tiles][4] {offset, pos} at tile end (INCL), aggregate bytes (AGG)
   uint64_t* tile_counter;    // monotonic dynamic tile ticket
   uint64_t tile_base;        // value of *tile_counter at launch
   uint32_t n;
-  uint32_t tiles;
+  uint32_t tiles;            // 64-slot tiles
   uint32_t epoch;
   uint32_t nospace_limit_lo, nospace_limit_hi;  // segment - interval (u64 split)
   const CrcConsts* crc;
   uint32_t* err;
+  uint32_t spin_limit;
+  uint32_t debug;            // bit 0: register staging instead of LDS-DMA, bit 1: no look-back
 };
 
 struct FetchArgs {
@@ -124,5 +124,6 @@ void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev_resolve0, hip
                   hipEvent_t ev_gather0, hipEvent_t ev_gather1);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 int append_blocks_per_cu();
+int append_waves_per_block();
 
 }  // namespace rmq

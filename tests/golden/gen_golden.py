@@ -24,10 +24,10 @@ OUT = os.path.dirname(os.path.abspath(__file__))
 
 SCENARIOS = {
     # BASELINE configs at fixture scale: A (rr, 256 p), B (Zipf, 4096 p), D (RF 5, 64 B..16 KB)
-    "rr_256p": dict(cfg=dict(num_partitions=256, replication_factor=3, segment_bytes=1 << 16,
+    "rr_256p": dict(cfg=dict(num_partitions=256, replication_factor=3, segment_bytes=1 << 18,
                              index_interval=1024, max_batch_records=4096),
                     spec=StreamSpec(256, 1024, "rr", size=100, config_index=1), batches=3),
-    "zipf_4096p": dict(cfg=dict(num_partitions=4096, replication_factor=3, segment_bytes=1 << 16,
+    "zipf_4096p": dict(cfg=dict(num_partitions=4096, replication_factor=3, segment_bytes=1 << 19,
                                 index_interval=1024, max_batch_records=4096),
                        spec=StreamSpec(4096, 2048, "zipf", size=100, config_index=2), batches=2),
     "mixed_rf5": dict(cfg=dict(num_partitions=64, replication_factor=5, segment_bytes=1 << 22,
@@ -110,5 +110,7 @@ if __name__ == "__main__":
         fx = make_inputs(name, sc)
         with OracleEngine(fx["cfg"]) as ora:
             obs = run(ora, fx)
+        for b in range(fx["batches"]):  # stats keys sorted: appended first
+            assert obs[f"stats{b}"][0] > 0, f"{name}: batch {b} appended nothing (degenerate fixture)"
         save(name, fx, obs)
         print(name, os.path.getsize(os.path.join(OUT, f"{name}.npz")), "bytes")

@@ -14,6 +14,7 @@ NAMES = sorted(G.SCENARIOS)
 
 def check(obs, exp):
     assert set(obs) == set(exp)
+    assert all(exp[k][0] > 0 for k in exp if k.startswith("stats")), "fixture must append records"
     for k in sorted(exp):
         assert np.array_equal(np.asarray(obs[k]).reshape(exp[k].shape).astype(exp[k].dtype), exp[k]), k
 

@@ -163,3 +163,16 @@ def test_config_A_full_batches(oracle_mod):
         spec = StreamSpec(256, 65536, "rr", size=100, config_index=1)
         run_ops(dev, ora, cfg, [("append", make_batch(spec, b)) for b in range(3)], check=False)
         compare_state(dev, ora, cfg)
+
+
+@pytest.mark.parametrize("P", [4097, 20000])
+def test_multi_pass_sort(oracle_mod, P):
+    # P > 4096: two 12-bit radix passes before the slot records
+    cfg, dev, ora = pair(oracle_mod, num_partitions=P, replication_factor=2, segment_bytes=1 << 18,
+                         index_interval=1024, max_batch_records=8192)
+    with dev, ora:
+        spec = StreamSpec(P, 1500, "zipf", size=(1, 120), config_index=19, invalid_frac=0.02)
+        ops = [("append", make_batch(spec, b)) for b in range(3)]
+        run_ops(dev, ora, cfg, ops, check=False)
+        parts = sorted({int(p) for b in range(3) for p in make_batch(spec, b).pidx if p < P})[:300]
+        compare_state(dev, ora, cfg, parts=parts)
