@@ -38,7 +38,7 @@ namespace rmq {
 constexpr u32 kWaves = kAppendThreads / 64;        // waves per workgroup
 constexpr u32 kImgDw = kAppendImageBytes / 4;      // image dwords per wave
 constexpr u32 kLongCrc = 512;                      // payloads above this: whole-wave CRC
-constexpr u32 kStAgg = 1u, kStIncl = 2u;
+constexpr u32 kStAgg = 1u, kStIncl = 2u;  // look-back granule tag = epoch << 2 | status
 constexpr u32 kBadPart = 0x80000000u;              // slot len flag: pidx >= P
 
 struct WaveSmem {
@@ -105,66 +105,55 @@ __device__ u32 wave_crc32c(const u32 (*t)[256], const CrcConsts* cc, const u32* 
   return crc;
 }
 
-__device__ __forceinline__ void finalize_partition(const DevState& st, u32 p, u64 end_off, u64 end_pos,
-                                                   u64 leo_before) {
-  if (end_off == leo_before) return;  // no record of this run was appended
-  st.leo[p] = end_off;
-  st.used[p] = end_pos;
-  const u32 lm = st.local_mask[p];
-  for (u32 r = 0; r < st.RF; ++r)
-    if (lm >> r & 1u) st.match[(u64)p * st.RF + r] = end_off;
-  commit_rule(st, p);
-  const u64 sp = st.start_pos[p];
-  if (end_pos - sp > st.seg) {  // size retention, FORMAT.md §4
-    const u64 I = 1ull << st.interval_log2;
-    const u64 m = (end_pos - st.seg + I - 1) >> st.interval_log2;
-    const u64* e = st.index + ((u64)p * st.icap + m % st.icap) * 2;
-    st.start_off[p] = e[0];
-    st.start_pos[p] = e[1];
-  }
-}
-
 __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   AppendSmem& S = *reinterpret_cast<AppendSmem*>(smem_raw);
-  const u32 lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const u32 lane = threadIdx.x & 63;
+  const u32 wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   WaveSmem& W = S.wv[wv];
   const DevState& st = a.st;
   const u64 nospace_limit = ((u64)a.nospace_limit_hi << 32) | a.nospace_limit_lo;
   const bool nospace = a.batch_info[0] > nospace_limit;
+  const u32 RF = st.RF;
 
   for (u32 k = threadIdx.x; k < 8 * 256; k += kAppendThreads) (&S.crc[0][0])[k] = a.crc->table[k >> 8][k & 255];
   __syncthreads();
 
-  for (;;) {
-    // Control values must be provably wave-uniform (readfirstlane / readlane), or the compiler
-    // structurizes the loop per lane and a __shfl can read a lane that already left it.
-    // every lane adds 1 (a uniform increment: one wave atomic of 64), no divergent branch at the
-    // loop head; the wave's ticket is lane 0's old value / 64
-    const u64 tk = atomicAdd((unsigned long long*)a.tile_counter, 1ull);
-    const u32 tile = __builtin_amdgcn_readfirstlane((u32)((tk - a.tile_base) >> 6));
-    if (tile >= a.tiles) break;
-
+  // Static tile assignment: wave gw takes tiles gw, gw + nw, ...; every wave of the grid is
+  // resident (<= 2 workgroups per CU), and a wave only ever waits on lower tiles, which their
+  // owners reach first, so the look-back cannot deadlock.
+  const u32 nw = gridDim.x * kWaves;
+  for (u32 tile = blockIdx.x * kWaves + wv; tile < a.tiles; tile += nw) {
     const u32 s0 = tile * 64u, s = s0 + lane;
     const bool in = s < a.n;
     const u32 nin = a.n - s0 < 64u ? a.n - s0 : 64u;  // valid slots in this tile
     const u32 last = nin - 1;
 
-    // ---- 1. slot records (one 16-byte load per lane) and validity
-    uint4 sr = make_uint4(0, 0, 0, 0);
-    if (in) sr = a.slots[s];
+    // ---- 1. every load the tile needs, issued up front and unbranched (clamped indices)
+    const uint4 sr = a.slots[in ? s : a.n - 1];
+    const u32 e_prev = a.slots[s0 ? s0 - 1 : 0].x;
+    const u32 e_next = a.slots[s0 + nin < a.n ? s0 + nin : a.n - 1].x;
     const u32 key = sr.x, rec = sr.y, L = sr.z & ~kBadPart, so = sr.w;
+    const u32 lead = st.is_leader[key];
+    const u32 lmask = st.local_mask[key];
+    // batch-start state of the record's partition. Safe to read here: the partition's finalizer
+    // (this or a later tile) writes it only after this tile's look-back granules are published.
+    const u64 base_off = st.leo[key], base_pos = st.used[key];
+    const u64 f_start = st.start_pos[key], f_term = st.term_start[key], f_commit = st.commit[key];
+    u64 row[kMaxRF];
+#pragma unroll
+    for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)key * RF + r] : 0ull;
+
     u32 prev_key = __shfl_up(key, 1, 64), next_key = __shfl_down(key, 1, 64);
-    if (lane == 0) prev_key = s ? a.slots[s - 1].x : 0xFFFFFFFFu;
-    if (lane == last) next_key = s + 1 < a.n ? a.slots[s + 1].x : 0xFFFFFFFFu;
+    prev_key = lane == 0 ? (s0 ? e_prev : 0xFFFFFFFFu) : prev_key;
+    next_key = lane == last ? (s0 + nin < a.n ? e_next : 0xFFFFFFFFu) : next_key;
     const bool okp = in && !(sr.z & kBadPart);
     const bool range_ok = (u64)so + L <= a.payload_bytes;
-    const bool lead = in && st.is_leader[key];
     const bool ok = okp && range_ok && lead && !nospace;
     const u32 cnt = ok ? 1u : 0u;
     const u32 rs = ok ? 16u + ((L + 3u) & ~3u) : 0u;
     const u32 head = in && (s == 0 || prev_key != key) ? 1u : 0u;
-    const bool run_end = in && (s + 1 == a.n || next_key != key);
+    const bool run_end = in && next_key != key;
 
     if (nospace) {
       if (in) a.out_offsets[rec] = ~0ull;
@@ -172,11 +161,7 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
       continue;
     }
 
-    // early load for the run-finalizing lanes (latency hides under the staging below)
-    u64 leo_before = 0;
-    if (run_end) leo_before = st.leo[key];
-
-    // ---- 2. segmented wave scan: rank / byte offset inside the run; run ids
+    // ---- 2. segmented wave scan: count / bytes relative to the run start (or the tile start)
     u32 fc = head, fb = head, c_inc = cnt, b_inc = rs;
     wave_seg_incl_scan(fc, c_inc);
     wave_seg_incl_scan(fb, b_inc);
@@ -184,24 +169,15 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     const u32 c_exc = c_inc - cnt, b_exc = b_inc - rs;
     const u32 tile_heads = __builtin_amdgcn_readlane(run_id, last);
     const bool cont = __builtin_amdgcn_readfirstlane(head) == 0u;
-    if (head) {
-      W.rb_off[run_id] = st.leo[key];
-      W.rb_pos[run_id] = st.used[key];
-    }
-    __builtin_amdgcn_wave_barrier();
 
-    // publish this tile for the look-back of later tiles
+    // publish {count, bytes} of the tile's last run relative to its batch start: INCL when the
+    // run starts here, AGG (the tile's whole contribution) when it continued from before.
+    // Waiting for the state loads first is what orders them before any finalizer's writes.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == last) {
-      if (tile_heads) {
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 0], W.rb_off[run_id] + c_inc);
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 1], W.rb_pos[run_id] + b_inc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        gran_store(&a.lb_status[tile], a.epoch, (kStIncl << 30) | c_inc);
-      } else {
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 2], b_inc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        gran_store(&a.lb_status[tile], a.epoch, (kStAgg << 30) | c_inc);
-      }
+      const u32 tag = (a.epoch << 2) | (tile_heads ? kStIncl : kStAgg);
+      gran_store(&a.lb_cnt[tile], tag, c_inc);
+      gran_store(&a.lb_bytes[tile], tag, b_inc);
     }
 
     // ---- image layout
@@ -213,52 +189,45 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     W.len[lane] = L;
     W.so[lane] = so;
     W.imgoff[lane] = ioff;
-    W.mask[lane] = ok ? st.local_mask[key] : 0u;
+    W.mask[lane] = ok ? lmask : 0u;
     const u32 ndw = tb >> 2;
     if (image) {
       for (u32 d = 0; d < rs / 4; ++d) W.map[ioff / 4 + d] = (uint8_t)lane;
       __builtin_amdgcn_wave_barrier();
-      // ---- 3. LDS-DMA gather of the payload dwords into the image
+      // ---- 3. LDS-DMA gather of the payload dwords into the image (all in flight at once)
       if (a.debug & 1u) {
         for (u32 dw = lane; dw < ndw; dw += 64) {
           const u32 k = W.map[dw];
           const u32 rel = dw - (W.imgoff[k] >> 2);
           if (rel >= 4) W.img[dw] = *reinterpret_cast<const u32*>(a.payload + W.so[k] + 4u * (rel - 4u));
         }
-      } else
-      for (u32 c = 0; c * 64 < ndw; ++c) {
-        const u32 dw = c * 64 + lane;
-        const uint8_t* src = a.payload;
-        if (dw < ndw) {
-          const u32 k = W.map[dw];
+      } else {
+        for (u32 c = 0; c * 64 < ndw; ++c) {
+          const u32 dw = c * 64 + lane;
+          const u32 k = W.map[dw < ndw ? dw : 0];
           const u32 rel = dw - (W.imgoff[k] >> 2);
-          if (rel >= 4) src = a.payload + W.so[k] + 4u * (rel - 4u);
+          const uint8_t* src = (dw < ndw && rel >= 4) ? a.payload + W.so[k] + 4u * (rel - 4u) : a.payload;
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                           (__attribute__((address_space(3))) void*)&W.img[c * 64], 4, 0, 0);
         }
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)&W.img[c * 64], 4, 0, 0);
       }
     }
 
-    // ---- 2b. look-back for a run continued from earlier tiles (overlaps the DMA)
-    if (cont && (a.debug & 2u)) {
-      if (lane == 0) {
-        W.rb_off[0] = 0;
-        W.rb_pos[0] = 0;
-      }
-    } else if (cont) {
-      u64 acc_c = 0, acc_b = 0;
+    // ---- 2b. look-back: relative count/bytes of the run before this tile (overlaps the DMA)
+    u32 carry_c = 0, carry_b = 0;
+    if (cont) {
+      u32 acc_c = 0, acc_b = 0;
       long look = (long)tile - 1;
       for (u32 spins = 0;;) {
         const long t = look - (long)lane;
-        const u64 tc = t >= 0 ? (u64)t : 0ull;  // predicated, not branched (see the loop head)
-        const u64 x = gran_load(&a.lb_status[tc]);
-        const bool ready = t >= 0 && (u32)(x >> 32) == a.epoch;
-        const u32 stt = ((u32)x) >> 30;
-        const u64 stop = __ballot(!ready || stt == kStIncl);
+        const u64 tc = t >= 0 ? (u64)t : 0ull;  // predicated, not branched
+        const u64 xc = gran_load(&a.lb_cnt[tc]);
+        const u64 xb = gran_load(&a.lb_bytes[tc]);
+        const u32 tag = (u32)(xc >> 32);
+        const bool ready = t >= 0 && (tag >> 2) == a.epoch && (u32)(xb >> 32) == tag;
+        const u64 stop = __ballot(!ready || (tag & 3u) == kStIncl);
         const u32 fl = stop ? (u32)__ffsll((long long)stop) - 1u : 64u;
-        const u64 ab_raw = load_sc1_u64(&a.lb_abs[tc * 4 + 2]);
-        u64 ac = lane < fl ? (u64)(((u32)x) & 0x3FFFFFFFu) : 0ull;
-        u64 ab = lane < fl ? ab_raw : 0ull;
+        u32 ac = lane < fl ? (u32)xc : 0u, ab = lane < fl ? (u32)xb : 0u;
         for (int d = 32; d >= 1; d >>= 1) {
           ac += __shfl_xor(ac, d, 64);
           ab += __shfl_xor(ab, d, 64);
@@ -270,35 +239,29 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
           continue;
         }
         if (__builtin_amdgcn_readlane(ready ? 1u : 0u, fl)) {
-          const long tf = look - (long)fl;
-          const u64 bo = load_sc1_u64(&a.lb_abs[(u64)tf * 4 + 0]) + acc_c;
-          const u64 bp = load_sc1_u64(&a.lb_abs[(u64)tf * 4 + 1]) + acc_b;
-          W.rb_off[0] = bo;  // every lane stores the same value
-          W.rb_pos[0] = bp;
+          carry_c = acc_c + __builtin_amdgcn_readlane((u32)xc, fl);
+          carry_b = acc_b + __builtin_amdgcn_readlane((u32)xb, fl);
           break;
         }
         look -= (long)fl;  // consumed fl aggregates; wait for the unpublished tile
         if (++spins >= a.spin_limit) {
           atomicOr(a.err, kErrSpinTimeout);
-          W.rb_off[0] = 0;
-          W.rb_pos[0] = 0;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_wave_barrier();
       if (!tile_heads && lane == last) {
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 0], W.rb_off[0] + c_inc);
-        store_sc1_u64(&a.lb_abs[(u64)tile * 4 + 1], W.rb_pos[0] + b_inc);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        gran_store(&a.lb_status[tile], a.epoch, (kStIncl << 30) | c_inc);
+        const u32 tag = (a.epoch << 2) | kStIncl;
+        gran_store(&a.lb_cnt[tile], tag, carry_c + c_inc);
+        gran_store(&a.lb_bytes[tile], tag, carry_b + b_inc);
       }
     }
-    __builtin_amdgcn_wave_barrier();
 
     // ---- absolute offset / position of every record
-    const u64 off_abs = W.rb_off[run_id] + c_exc;
-    const u64 pos_abs = W.rb_pos[run_id] + b_exc;
+    const u32 rel_c = (run_id ? 0u : carry_c) + c_exc;
+    const u32 rel_b = (run_id ? 0u : carry_b) + b_exc;
+    const u64 off_abs = base_off + rel_c;
+    const u64 pos_abs = base_pos + rel_b;
     W.pos[lane] = pos_abs;
     if (in) a.out_offsets[rec] = ok ? off_abs : ~0ull;
     if (ok) {  // sparse offset index: multiples m*I in (pos, pos + rs] name the next record
@@ -309,6 +272,7 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         e[1] = end;
       }
     }
+    __builtin_amdgcn_wave_barrier();
 
     const u64 segmask = st.seg - 1;
     const u64 rstride = (u64)st.P * st.seg;
@@ -325,7 +289,7 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         const u32 k = (u32)__ffsll((long long)longs) - 1u;
         longs &= longs - 1;
         const u32 cr = wave_crc32c<true>(S.crc, a.crc, &W.img[W.imgoff[k] / 4 + 4], nullptr, 0, W.len[k]);
-        if (lane == k) crc = cr;
+        crc = lane == k ? cr : crc;
       }
       if (ok) {
         const u32 d0 = ioff / 4;
@@ -342,7 +306,7 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         const u64 lp = W.pos[k] + (u64)(dw * 4u - W.imgoff[k]);
         uint8_t* dst = st.logs + (u64)W.key[k] * st.seg + (lp & segmask);
         const u32 msk = W.mask[k];
-        for (u32 r = 0; r < st.RF; ++r)
+        for (u32 r = 0; r < RF; ++r)
           if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v;
       }
     } else {
@@ -366,14 +330,35 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
             v = d == 0 ? (u32)ko : d == 1 ? (u32)(ko >> 32) : d == 2 ? Lk : cr;
           }
           const u64 lp = P0 + 4ull * d;
-          for (u32 r = 0; r < st.RF; ++r)
+          for (u32 r = 0; r < RF; ++r)
             if (msk >> r & 1u) *reinterpret_cast<u32*>(rb + r * rstride + (lp & segmask)) = v;
         }
       }
     }
 
-    // ---- 6. the lane that ends a run finalizes its partition
-    if (run_end) finalize_partition(st, key, off_abs + cnt, pos_abs + rs, leo_before);
+    // ---- 6. the lane that ends a run finalizes its partition (state prefetched in step 1)
+    const u32 end_c = rel_c + cnt;
+    if (run_end && end_c) {
+      const u64 end_off = base_off + end_c, end_pos = base_pos + rel_b + rs;
+      st.leo[key] = end_off;
+      st.used[key] = end_pos;
+#pragma unroll
+      for (u32 r = 0; r < kMaxRF; ++r)
+        if (r < RF && (lmask >> r & 1u)) {
+          row[r] = end_off;
+          st.match[(u64)key * RF + r] = end_off;
+        }
+      const u64 c = quorum_commit(row, RF, f_commit, f_term);
+      st.commit[key] = c;
+      st.hw[key] = c;
+      if (end_pos - f_start > st.seg) {  // size retention, FORMAT.md §4
+        const u64 I = 1ull << st.interval_log2;
+        const u64 m = (end_pos - st.seg + I - 1) >> st.interval_log2;
+        const u64* e = st.index + ((u64)key * st.icap + m % st.icap) * 2;
+        st.start_off[key] = e[0];
+        st.start_pos[key] = e[1];
+      }
+    }
 
     // ---- per-tile stats (no atomics): appended, not leader, unknown partition, no space
     {

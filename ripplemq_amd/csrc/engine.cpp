@@ -25,7 +25,7 @@ using namespace rmq;
 namespace {
 
 constexpr uint32_t kStatsRing = 64;                               // tickets whose stats stay readable
-constexpr uint32_t kMaxSortTiles = 256;                           // all sort tiles must be co-resident
+constexpr uint32_t kMaxSortTiles = 128;                           // all sort tiles must be co-resident
 constexpr uint32_t kMaxBatchRecords = kMaxSortTiles * kSortTile;  // 262144
 
 struct EvPair {
@@ -43,9 +43,9 @@ struct Slot {
   uint32_t* src_off = nullptr;             // packed payload offsets (multi-pass only)
   uint4* slots = nullptr;                  // sorted slot records for the append kernel
   uint64_t* batch_info = nullptr;
-  uint64_t* hist_gran = nullptr;           // sort look-back granules [tiles][4096]
+  uint64_t* hist_gran = nullptr;           // sort tile histograms [tiles][256]
   uint64_t* len_gran = nullptr;
-  uint64_t* len_val = nullptr;
+  uint64_t* rb_gran = nullptr;
   hipEvent_t prep_done = nullptr, append_done = nullptr;
   uint64_t ticket = 0;
   bool used = false;
@@ -59,17 +59,16 @@ struct rmq_engine {
   int device = 0;
   uint32_t cu_count = 0;
   char dev_name[256] = {0};
-  hipStream_t main_s = nullptr, prep_s = nullptr;
+  hipStream_t main_s = nullptr;
+  hipStream_t prep[2] = {nullptr, nullptr};  // batch sorts alternate between two prep streams
   DevState st{};
   CrcConsts* d_crc = nullptr;
   uint64_t* d_winner = nullptr;
   uint32_t* d_err = nullptr;
   uint4* d_tile_stats = nullptr;  // [kStatsRing][max append tiles]
   uint32_t max_app_tiles = 0;
-  uint64_t* d_lb_status = nullptr;
-  uint64_t* d_lb_abs = nullptr;
-  uint64_t* d_tile_counter = nullptr;
-  uint64_t tile_base = 0;
+  uint64_t* d_lb_cnt = nullptr;
+  uint64_t* d_lb_bytes = nullptr;
   uint32_t epoch = 0;
   std::vector<Slot> slots;
   uint64_t last_ticket = 0;
@@ -78,7 +77,7 @@ struct rmq_engine {
   std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
   std::vector<uint64_t> term;
   // sort plan
-  uint32_t passes = 1, pass_shift[2] = {0, 0}, pass_bits[2] = {1, 0}, pass_ndig[2] = {1, 0};
+  uint32_t passes = 1, pass_shift[3] = {0, 0, 0}, pass_bits[3] = {1, 0, 0}, pass_ndig[3] = {1, 0, 0};
   // fetch scratch
   uint32_t* d_req = nullptr;
   uint64_t* d_res = nullptr;
@@ -91,10 +90,12 @@ struct rmq_engine {
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;
   uint32_t ctl_cap = 0;
-  // RMQ_DEBUG_SKIP bit 0: skip the sort launch, bit 1: skip the append launch (bisecting only)
+  // RMQ_DEBUG_SKIP bit 0: skip the sort launch, bit 1: skip the append launch, bit 2: run each
+  // batch's sort after the previous append (no overlap; to time the kernels alone)
   uint32_t debug_skip = 0;
   uint32_t debug_flags = 0;   // RMQ_DEBUG_FLAGS -> AppendArgs.debug
   uint32_t spin_limit = 1u << 22;
+  hipEvent_t last_append_done = nullptr;
   // profiling
   bool profile = false;
   std::vector<EvPair> prof[5];
@@ -171,7 +172,8 @@ int check_err(rmq_engine* e) {
 }
 
 int drain(rmq_engine* e) {
-  HIP_TRY(hipStreamSynchronize(e->prep_s));
+  HIP_TRY(hipStreamSynchronize(e->prep[0]));
+  HIP_TRY(hipStreamSynchronize(e->prep[1]));
   HIP_TRY(hipStreamSynchronize(e->main_s));
   return check_err(e);
 }
@@ -205,19 +207,20 @@ void free_engine(rmq_engine* e) {
   if (!e) return;
   hipSetDevice(e->device);
   if (e->main_s) hipStreamSynchronize(e->main_s);
-  if (e->prep_s) hipStreamSynchronize(e->prep_s);
+  for (hipStream_t ps : e->prep)
+    if (ps) hipStreamSynchronize(ps);
   DevState& s = e->st;
   void* bufs[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match,
                   s.is_leader, s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner,
                   e->d_err, e->d_tile_stats,
-                  e->d_lb_status, e->d_lb_abs, e->d_tile_counter, e->d_req, e->d_res, e->d_aux,
+                  e->d_lb_cnt, e->d_lb_bytes, e->d_req, e->d_res, e->d_aux,
                   e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64};
   for (void* b : bufs)
     if (b) hipFree(b);
   for (Slot& sl : e->slots) {
     void* sb[] = {sl.d_pidx, sl.d_len, sl.d_poff, sl.d_payload, sl.d_out, sl.keys[0], sl.keys[1],
                   sl.vals[0], sl.vals[1], sl.src_off, sl.slots, sl.batch_info, sl.hist_gran,
-                  sl.len_gran, sl.len_val};
+                  sl.len_gran, sl.rb_gran};
     for (void* b : sb)
       if (b) hipFree(b);
     if (sl.prep_done) hipEventDestroy(sl.prep_done);
@@ -230,7 +233,8 @@ void free_engine(rmq_engine* e) {
     }
   for (hipEvent_t ev : e->ev_pool) hipEventDestroy(ev);
   if (e->main_s) hipStreamDestroy(e->main_s);
-  if (e->prep_s) hipStreamDestroy(e->prep_s);
+  for (hipStream_t ps : e->prep)
+    if (ps) hipStreamDestroy(ps);
   delete e;
 }
 
@@ -314,7 +318,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->cu_count = (uint32_t)prop.multiProcessorCount;
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
-  CREATE_HIP(hipStreamCreateWithFlags(&e->prep_s, hipStreamNonBlocking));
+  CREATE_HIP(hipStreamCreateWithFlags(&e->prep[0], hipStreamNonBlocking));
+  CREATE_HIP(hipStreamCreateWithFlags(&e->prep[1], hipStreamNonBlocking));
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
   DevState& s = e->st;
@@ -342,9 +347,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   const uint32_t max_sort_tiles = (cfg->max_batch_records + kSortTile - 1) / kSortTile;
   e->max_app_tiles = (cfg->max_batch_records + kAppendTile - 1) / kAppendTile;
   CREATE_TRY(dalloc(&e->d_tile_stats, (size_t)kStatsRing * e->max_app_tiles));
-  CREATE_TRY(dalloc(&e->d_lb_status, e->max_app_tiles));
-  CREATE_TRY(dalloc(&e->d_lb_abs, (size_t)e->max_app_tiles * 4));
-  CREATE_TRY(dalloc(&e->d_tile_counter, 1));
+  CREATE_TRY(dalloc(&e->d_lb_cnt, e->max_app_tiles));
+  CREATE_TRY(dalloc(&e->d_lb_bytes, e->max_app_tiles));
   {
     CrcConsts h;
     build_crc_consts(&h);
@@ -362,10 +366,10 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->term.assign(P, 1ull);
   e->ticket_n.assign(kStatsRing, 0u);
 
-  // radix plan: 12-bit digits of the partition id (one pass for P <= 4096)
+  // radix plan: <= 8-bit digits of the partition id (one pass for P <= 256)
   uint32_t bits = ilog2((uint64_t)P);  // keys in [0, P-1]
   if (bits == 0) bits = 1;
-  e->passes = (bits + 11) / 12;
+  e->passes = (bits + kSortDigitBits - 1) / kSortDigitBits;
   const uint32_t dw = (bits + e->passes - 1) / e->passes;
   for (uint32_t k = 0; k < e->passes; ++k) {
     e->pass_shift[k] = k * dw;
@@ -384,9 +388,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     }
     CREATE_TRY(dalloc(&sl.slots, NB));
     CREATE_TRY(dalloc(&sl.batch_info, 4));
-    CREATE_TRY(dalloc(&sl.hist_gran, (size_t)max_sort_tiles * kMaxDigits));
+    CREATE_TRY(dalloc(&sl.hist_gran, (size_t)max_sort_tiles * 256));
     CREATE_TRY(dalloc(&sl.len_gran, max_sort_tiles));
-    CREATE_TRY(dalloc(&sl.len_val, (size_t)max_sort_tiles * 2));
+    CREATE_TRY(dalloc(&sl.rb_gran, max_sort_tiles));
     CREATE_HIP(hipEventCreateWithFlags(&sl.prep_done, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&sl.append_done, hipEventDisableTiming));
   }
@@ -472,6 +476,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   *ticket = t;
   e->ticket_n[t % kStatsRing] = n;
   Slot& sl = e->slots[t % e->slots.size()];
+  hipStream_t prep_s = e->prep[t & 1];
   if (sl.used) {
     HIP_TRY(hipEventSynchronize(sl.append_done));  // scratch of ticket t - depth is free again
   }
@@ -497,11 +502,11 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
       if (!rc) rc = dalloc(&sl.d_payload, e->cfg.max_batch_bytes + 8);
       if (rc) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(sl.d_pidx, pidx, n * 4ull, hipMemcpyHostToDevice, e->prep_s));
-    HIP_TRY(hipMemcpyAsync(sl.d_len, len, n * 4ull, hipMemcpyHostToDevice, e->prep_s));
-    if (poff) HIP_TRY(hipMemcpyAsync(sl.d_poff, poff, n * 8ull, hipMemcpyHostToDevice, e->prep_s));
+    HIP_TRY(hipMemcpyAsync(sl.d_pidx, pidx, n * 4ull, hipMemcpyHostToDevice, prep_s));
+    HIP_TRY(hipMemcpyAsync(sl.d_len, len, n * 4ull, hipMemcpyHostToDevice, prep_s));
+    if (poff) HIP_TRY(hipMemcpyAsync(sl.d_poff, poff, n * 8ull, hipMemcpyHostToDevice, prep_s));
     if (b->payload_bytes)
-      HIP_TRY(hipMemcpyAsync(sl.d_payload, payload, b->payload_bytes, hipMemcpyHostToDevice, e->prep_s));
+      HIP_TRY(hipMemcpyAsync(sl.d_payload, payload, b->payload_bytes, hipMemcpyHostToDevice, prep_s));
     pidx = sl.d_pidx;
     len = sl.d_len;
     poff = poff ? sl.d_poff : nullptr;
@@ -509,13 +514,15 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     d_out = sl.d_out;
   }
 
+  if ((e->debug_skip & 4u) && e->last_append_done)
+    HIP_TRY(hipStreamWaitEvent(prep_s, e->last_append_done, 0));
   // ---- prep stream: stable partition-major sort of the batch into slot records
   const uint32_t sort_tiles = (n + kSortTile - 1) / kSortTile;
   hipEvent_t ps0 = nullptr, ps1 = nullptr;
   if (e->profile) {
     ps0 = pool_event(e);
     ps1 = pool_event(e);
-    HIP_TRY(hipEventRecord(ps0, e->prep_s));
+    HIP_TRY(hipEventRecord(ps0, prep_s));
   }
   const uint32_t* kin = pidx;
   const uint32_t* vin = nullptr;
@@ -533,7 +540,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     a.batch_info = sl.batch_info;
     a.hist_gran = sl.hist_gran;
     a.len_gran = sl.len_gran;
-    a.len_val = sl.len_val;
+    a.rb_gran = sl.rb_gran;
     a.n = n;
     a.tiles = sort_tiles;
     a.shift = e->pass_shift[k];
@@ -544,16 +551,16 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     a.last = k + 1 == e->passes;
     a.epoch = ++e->epoch;
     a.err = e->d_err;
-    if (!(e->debug_skip & 1u)) launch_sort_pass(a, sort_tiles, e->prep_s);
+    if (!(e->debug_skip & 1u)) launch_sort_pass(a, sort_tiles, prep_s);
     kin = sl.keys[0];
     vin = sl.vals[0];
   }
   HIP_TRY(hipGetLastError());
   if (e->profile) {
-    HIP_TRY(hipEventRecord(ps1, e->prep_s));
+    HIP_TRY(hipEventRecord(ps1, prep_s));
     e->prof[1].push_back({ps0, ps1});
   }
-  HIP_TRY(hipEventRecord(sl.prep_done, e->prep_s));
+  HIP_TRY(hipEventRecord(sl.prep_done, prep_s));
 
   // ---- main stream: fused append
   HIP_TRY(hipStreamWaitEvent(e->main_s, sl.prep_done, 0));
@@ -565,10 +572,8 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   a.out_offsets = d_out;
   a.batch_info = sl.batch_info;
   a.tile_stats = e->d_tile_stats + (size_t)(t % kStatsRing) * e->max_app_tiles;
-  a.lb_status = e->d_lb_status;
-  a.lb_abs = e->d_lb_abs;
-  a.tile_counter = e->d_tile_counter;
-  a.tile_base = e->tile_base;
+  a.lb_cnt = e->d_lb_cnt;
+  a.lb_bytes = e->d_lb_bytes;
   a.n = n;
   a.tiles = (n + kAppendTile - 1) / kAppendTile;
   a.epoch = ++e->epoch;
@@ -581,7 +586,6 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   a.debug = e->debug_flags;
   const uint32_t wpb = (uint32_t)append_waves_per_block();
   const uint32_t grid = std::min<uint32_t>((a.tiles + wpb - 1) / wpb, e->cu_count * (uint32_t)append_blocks_per_cu());
-  e->tile_base += 64ull * ((uint64_t)a.tiles + (uint64_t)grid * wpb);  // 64 per ticket; one failing ticket per wave
   hipEvent_t pa0 = nullptr, pa1 = nullptr;
   if (e->profile) {
     pa0 = pool_event(e);
@@ -597,6 +601,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   if (b->mem == RMQ_MEM_HOST)
     HIP_TRY(hipMemcpyAsync(out_offsets, d_out, n * 8ull, hipMemcpyDeviceToHost, e->main_s));
   HIP_TRY(hipEventRecord(sl.append_done, e->main_s));
+  e->last_append_done = sl.append_done;
   return RMQ_OK;
 }
 

@@ -7,8 +7,8 @@
 namespace rmq {
 
 constexpr uint32_t kSortThreads = 256;
-constexpr uint32_t kSortItems = 4;
-constexpr uint32_t kMaxDigits = 4096;                      // 12-bit digits per sort pass
+constexpr uint32_t kSortItems = 8;
+constexpr uint32_t kSortDigitBits = 8;                     // <= 256 buckets per radix pass
 constexpr uint32_t kSortTile = kSortThreads * kSortItems;  // keys per sort tile
 constexpr uint32_t kAppendThreads = 256;                    // 4 waves; one 64-slot tile per wave
 constexpr uint32_t kAppendTile = 64;
@@ -51,9 +51,9 @@ struct SortPassArgs {
   const uint64_t* payload_off;  // caller payload offsets, or nullptr (packed)
   uint32_t* src_off;            // packed payload offsets written by the first pass of a multi-pass sort
   uint64_t* batch_info;         // first pass: [0] record bytes, [1] payload bytes of the batch
-  uint64_t* hist_gran;          // [tiles][ndig] look-back granules {epoch | flag | count}
-  uint64_t* len_gran;           // [tiles] look-back flags of the input-order length chain
-  uint64_t* len_val;            // [tiles][2] {aggregate, inclusive} of {record bytes:32 | payload:32}
+  uint64_t* hist_gran;          // [tiles][256] tile digit counts {epoch | count}
+  uint64_t* len_gran;           // [tiles] tile payload bytes {epoch | bytes}
+  uint64_t* rb_gran;            // [tiles] tile record bytes {epoch | bytes}
   uint32_t n, tiles;
   uint32_t shift, bits, ndig;   // digit = (key >> shift) & ((1 << bits) - 1), ndig digits used
   uint32_t P;
@@ -70,10 +70,8 @@ struct AppendArgs {
   uint64_t* out_offsets;     // input order
   const uint64_t* batch_info;
   uint4* tile_stats;         // [tiles] {appended, not leader, unknown partition, no space}
-  uint64_t* lb_status;       // [tiles] look-back granules
-  uint64_t* lb_abs;          // [tiles][4] {offset, pos} at tile end (INCL), aggregate bytes (AGG)
-  uint64_t* tile_counter;    // monotonic dynamic tile ticket
-  uint64_t tile_base;        // value of *tile_counter at launch
+  uint64_t* lb_cnt;          // [tiles] look-back granules {epoch<<2|status : record count}
+  uint64_t* lb_bytes;        // [tiles] look-back granules {epoch<<2|status : record bytes}
   uint32_t n;
   uint32_t tiles;            // 64-slot tiles
   uint32_t epoch;

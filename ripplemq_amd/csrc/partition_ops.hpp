@@ -10,28 +10,32 @@ namespace rmq {
 // replica row, k = RF/2 + 1 (the median for odd RF), held in registers and ordered by a
 // compare-exchange network; commit advances to N only if N > commit and the N-th record was
 // appended in the current term (N > term_start). hw (consumer-visible end) = commit.
-__device__ __forceinline__ void commit_rule(const DevState& st, u32 p) {
-  const u32 RF = st.RF, k = RF / 2 + 1;
+__device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u64 commit, u64 term_start) {
   u64 m[kMaxRF];
 #pragma unroll
-  for (u32 r = 0; r < kMaxRF; ++r) m[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
-  // k-th largest of the row in registers: insertion network, descending
+  for (u32 r = 0; r < kMaxRF; ++r) m[r] = r < RF ? row[r] : 0ull;
 #pragma unroll
   for (u32 i = 1; i < kMaxRF; ++i)
 #pragma unroll
-    for (u32 j = i; j > 0; --j) {
+    for (u32 j = i; j > 0; --j) {  // compare-exchange network, descending
       const u64 a = m[j - 1], b = m[j];
       m[j - 1] = a > b ? a : b;
       m[j] = a > b ? b : a;
     }
+  const u32 k = RF / 2 + 1;
   u64 N = 0;
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) N = (r == k - 1) ? m[r] : N;
-  u64 c = st.commit[p];
-  if (N > c && N > st.term_start[p]) c = N;
+  return (N > commit && N > term_start) ? N : commit;
+}
+
+__device__ __forceinline__ void commit_rule(const DevState& st, u32 p) {
+  u64 row[kMaxRF];
+#pragma unroll
+  for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < st.RF ? st.match[(u64)p * st.RF + r] : 0ull;
+  const u64 c = quorum_commit(row, st.RF, st.commit[p], st.term_start[p]);
   st.commit[p] = c;
   st.hw[p] = c;
 }
-
 
 }  // namespace rmq

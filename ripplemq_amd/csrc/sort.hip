@@ -3,53 +3,119 @@
 // Reference semantics (mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:64-69):
 // the records of one partition are applied in batch order and get consecutive offsets. The append
 // kernel consumes the batch reordered partition-major, *stably*, as 16-byte slot records
-// {pidx, record index, payload length, payload offset}; this file produces them.
+// {pidx, record index, payload length | bad-partition flag, payload offset}; this file makes them.
 //
-// One launch per 12-bit digit of the partition id (one launch for P <= 4096, two up to 2^24).
-// One workgroup = one tile of 1024 keys; wave w owns the contiguous keys [base + 256w, +256) and
-// reads them in rounds k of 64 (key j = base + 256w + 64k + lane), so (w, k, lane) is key order.
-//  * in-tile stable rank: per wave, rounds of 64 keys are ballot-matched on the digit bits; a
-//    per-wave LDS counter per digit carries ranks across rounds; waves are then prefixed per digit;
-//  * cross-tile prefix: decoupled look-back per digit over {epoch | AGG/INCL | count} granules
-//    (each thread owns 16 consecutive digits and walks them in lock-step, loads in flight together);
-//  * global digit starts: every tile reads the LAST tile's inclusive prefix (= the digit totals)
-//    once published — no histogram kernel and no memset between batches;
-//  * the first pass also scans {payload bytes, record bytes} in input order with a one-value
-//    look-back: packed payload offsets and the batch record-byte total (ENOSPC rule) for free.
-// Every tile waits on predecessors and on the last tile, so all tiles must be resident together:
-// the grid is capped at 256 workgroups of 256 threads (engine.cpp).
+// LSD radix over the partition id, one launch per digit of <= 8 bits (1 launch for P <= 256,
+// 2 for P <= 65536). One workgroup = one tile of 2048 keys; wave w owns the contiguous keys
+// [base + 512w, +512) and reads them in 8 rounds of 64 lanes, so (wave, round, lane) is key order.
+//  * in-tile stable rank: ballot-match the digit bits per 64-key round; a per-wave LDS counter per
+//    digit carries ranks across rounds; the 4 waves are then prefixed per digit;
+//  * cross-tile prefix and digit totals: every tile publishes its <= 256 counts as {epoch|count}
+//    granules and reads every tile's counts back (tiles^2 * 2 KB; 2 MB at a 64k-record batch).
+//    The loads of a poll are issued together (no serial look-back walk, which degenerates when
+//    all tiles start at once);
+//  * the first pass also sums {payload bytes, record bytes} per tile in input order and exchanges
+//    those sums the same way: packed payload offsets and the batch record-byte total (ENOSPC).
+// Tiles wait on each other, so all must be resident: <= 128 workgroups of 256 threads.
 #include "device_common.hpp"
 #include "kernels.hpp"
 
 namespace rmq {
 
-constexpr u32 kST = kSortThreads;       // 256
-constexpr u32 kSI = kSortItems;         // 4
-constexpr u32 kSW = kST / 64;           // waves per tile
-constexpr u32 kDPT = kMaxDigits / kST;  // digits owned per thread (16)
-constexpr u32 kAgg = 1u, kIncl = 2u;
+constexpr u32 kST = kSortThreads;     // 256
+constexpr u32 kSI = kSortItems;       // 8 keys per thread
+constexpr u32 kSW = kST / 64;         // 4 waves
+constexpr u32 kWK = kSortTile / kSW;  // keys per wave (512)
+
+// Sum a column of {epoch|value} granules over all tiles and over tiles < `tile`. The loads of a
+// sweep are issued 16 at a time before any is inspected; the sweep repeats until every tag
+// matches (bounded).
+__device__ __forceinline__ bool sweep_column(const u64* g, u32 stride, u32 tiles, u32 tile, u32 epoch,
+                                             u32* before, u32* total) {
+  for (u32 spins = 0; spins < kSpinLimit; ++spins) {
+    u32 b = 0, t = 0;
+    bool ok = true;
+    for (u32 t0 = 0; t0 < tiles; t0 += 16) {
+      u64 x[16];
+#pragma unroll
+      for (u32 i = 0; i < 16; ++i) x[i] = gran_load(g + (u64)(t0 + i < tiles ? t0 + i : 0) * stride);
+#pragma unroll
+      for (u32 i = 0; i < 16; ++i) {
+        const bool in = t0 + i < tiles;
+        ok &= !in || (u32)(x[i] >> 32) == epoch;
+        const u32 c = in ? (u32)x[i] : 0u;
+        t += c;
+        b += t0 + i < tile ? c : 0u;
+      }
+    }
+    if (ok) {
+      *before = b;
+      *total = t;
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
+
+// Two unit-stride columns swept together (payload bytes and record bytes per tile).
+__device__ __forceinline__ bool sweep_column2(const u64* g0, const u64* g1, u32 tiles, u32 tile, u32 epoch,
+                                              u32* b0, u32* t0_, u32* b1, u32* t1_) {
+  for (u32 spins = 0; spins < kSpinLimit; ++spins) {
+    u32 sb0 = 0, st0 = 0, sb1 = 0, st1 = 0;
+    bool ok = true;
+    for (u32 t0 = 0; t0 < tiles; t0 += 8) {
+      u64 x[8], y[8];
+#pragma unroll
+      for (u32 i = 0; i < 8; ++i) {
+        const u32 t = t0 + i < tiles ? t0 + i : 0;
+        x[i] = gran_load(g0 + t);
+        y[i] = gran_load(g1 + t);
+      }
+#pragma unroll
+      for (u32 i = 0; i < 8; ++i) {
+        const bool in = t0 + i < tiles;
+        ok &= !in || ((u32)(x[i] >> 32) == epoch && (u32)(y[i] >> 32) == epoch);
+        const u32 c0 = in ? (u32)x[i] : 0u, c1 = in ? (u32)y[i] : 0u;
+        st0 += c0;
+        st1 += c1;
+        sb0 += t0 + i < tile ? c0 : 0u;
+        sb1 += t0 + i < tile ? c1 : 0u;
+      }
+    }
+    if (ok) {
+      *b0 = sb0;
+      *t0_ = st0;
+      *b1 = sb1;
+      *t1_ = st1;
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return false;
+}
 
 __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
-  __shared__ uint16_t s_wcnt[kSW][kMaxDigits];  // per-wave digit counters, then per-wave bases
-  __shared__ u32 s_start[kMaxDigits];           // this tile's global position base per digit
-  __shared__ u64 s_scan64[kSW];
+  __shared__ uint16_t s_wcnt[kSW][256];  // per-wave digit counters, then per-wave bases
+  __shared__ u32 s_start[256];           // this tile's global position base per digit
   __shared__ u32 s_scan[kSW];
-  __shared__ u64 s_pre_len;
+  __shared__ u64 s_wtot[kSW];
+  __shared__ u32 s_pre_len;
 
   const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const u32 tile = blockIdx.x, tiles = a.tiles, nd = a.ndig;
-  const u32 base = tile * kSortTile;
+  const u32 base = tile * kSortTile + w * kWK;
   const u32 dmask = (1u << a.bits) - 1u;
   const u64 lt = (1ull << lane) - 1ull;
-  const u32 d0 = tid * kDPT;  // first digit owned by this thread
 
-  for (u32 k = tid; k < kSW * kMaxDigits / 2; k += kST) reinterpret_cast<u32*>(&s_wcnt[0][0])[k] = 0;
+  reinterpret_cast<u32*>(&s_wcnt[0][0])[tid] = 0;  // kSW * 256 u16 = 2 u32 per thread
+  reinterpret_cast<u32*>(&s_wcnt[0][0])[tid + kST] = 0;
 
   u32 key[kSI], val[kSI], rnk[kSI], len_[kSI], so_[kSI];
   u32 bad = 0;  // bit k: record k of this thread names a partition >= P
 #pragma unroll
   for (u32 k = 0; k < kSI; ++k) {
-    const u32 j = base + w * 256u + k * 64u + lane;
+    const u32 j = base + k * 64u + lane;
     u32 kk = 0, v = 0, L = 0;
     if (j < a.n) {
       kk = a.keys_in[j];
@@ -68,74 +134,40 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
     so_[k] = 0;
   }
 
-  // ---- first pass: input-order scan of {record bytes : payload bytes}, one-value look-back
+  // ---- first pass: input-order scan of {record bytes : payload bytes} inside the tile
   if (a.first) {
-    // wave-contiguous keys: scan per wave over its rounds, then prefix the 4 wave totals
     u64 wcarry = 0;
 #pragma unroll
     for (u32 k = 0; k < kSI; ++k) {
-      const u32 j = base + w * 256u + k * 64u + lane;
+      const u32 j = base + k * 64u + lane;
       const u64 v = j < a.n ? ((u64)(16u + ((len_[k] + 3u) & ~3u)) << 32) | len_[k] : 0ull;
       const u64 inc = wave_incl_scan(v);
       so_[k] = (u32)(wcarry + inc - v);
-      wcarry += ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32) | __builtin_amdgcn_readlane((u32)inc, 63);
+      wcarry += ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32) |
+                __builtin_amdgcn_readlane((u32)inc, 63);
     }
-    if (lane == 0) s_scan64[w] = wcarry;
+    if (lane == 0) s_wtot[w] = wcarry;
     __syncthreads();
-    u64 carry = 0, wpre = 0;
+    u64 wpre = 0, tile_sum = 0;
 #pragma unroll
     for (u32 ww = 0; ww < kSW; ++ww) {
-      const u64 t = s_scan64[ww];
+      const u64 t = s_wtot[ww];
       wpre += ww < w ? t : 0ull;
-      carry += t;
+      tile_sum += t;
     }
 #pragma unroll
     for (u32 k = 0; k < kSI; ++k) so_[k] += (u32)wpre;
     if (tid == 0) {
-      u64 pre = 0;
-      if (tile == 0) {
-        store_sc1_u64(&a.len_val[1], carry);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        gran_store(&a.len_gran[0], a.epoch, kIncl);
-      } else {
-        store_sc1_u64(&a.len_val[2 * tile], carry);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        gran_store(&a.len_gran[tile], a.epoch, kAgg);
-        long t = (long)tile - 1;
-        for (u32 spins = 0;;) {
-          const u64 x = gran_load(&a.len_gran[t]);
-          if ((u32)(x >> 32) == a.epoch) {
-            if ((u32)x == kIncl) {
-              pre += load_sc1_u64(&a.len_val[2 * t + 1]);
-              break;
-            }
-            pre += load_sc1_u64(&a.len_val[2 * t]);
-            --t;
-            continue;
-          }
-          if (++spins >= kSpinLimit) {
-            atomicOr(a.err, kErrSpinTimeout);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        store_sc1_u64(&a.len_val[2 * tile + 1], pre + carry);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        gran_store(&a.len_gran[tile], a.epoch, kIncl);
-      }
-      s_pre_len = pre;
-      if (tile == tiles - 1) {
-        a.batch_info[0] = (pre + carry) >> 32;          // record bytes of the batch
-        a.batch_info[1] = (u32)(pre + carry);           // payload bytes of the batch
-      }
+      gran_store(&a.len_gran[tile], a.epoch, (u32)tile_sum);
+      gran_store(&a.rb_gran[tile], a.epoch, (u32)(tile_sum >> 32));
     }
   }
 
-  // ---- in-tile stable ranking per wave (rounds k = 0..3 are in key order)
+  // ---- in-tile stable ranking per wave
   __syncthreads();
 #pragma unroll
   for (u32 k = 0; k < kSI; ++k) {
-    const u32 j = base + w * 256u + k * 64u + lane;
+    const u32 j = base + k * 64u + lane;
     const bool valid = j < a.n;
     const u32 d = (key[k] >> a.shift) & dmask;
     u64 peers = __ballot(valid);
@@ -152,105 +184,44 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   }
   __syncthreads();
 
-  // ---- owned digits: wave bases, tile count; publish AGG (INCL on tile 0)
-  u32 cnt[kDPT], pre[kDPT];
+  // ---- per digit: wave bases and the tile count, published as a granule
+  u32 cnt = 0;
+  if (tid < nd) {
 #pragma unroll
-  for (u32 i = 0; i < kDPT; ++i) {
-    const u32 d = d0 + i;
-    u32 run = 0;
-    if (d < nd) {
-#pragma unroll
-      for (u32 ww = 0; ww < kSW; ++ww) {
-        const u32 c = s_wcnt[ww][d];
-        s_wcnt[ww][d] = (uint16_t)run;
-        run += c;
-      }
-      gran_store(&a.hist_gran[(u64)tile * nd + d], a.epoch, ((tile ? kAgg : kIncl) << 30) | run);
+    for (u32 ww = 0; ww < kSW; ++ww) {
+      const u32 c = s_wcnt[ww][tid];
+      s_wcnt[ww][tid] = (uint16_t)cnt;
+      cnt += c;
     }
-    cnt[i] = run;
-    pre[i] = 0;
+    gran_store(&a.hist_gran[(u64)tile * 256 + tid], a.epoch, cnt);
   }
 
-  // ---- decoupled look-back, the 16 owned digits in lock-step
-  if (tile) {
-    long t[kDPT];
-    u32 live = 0;
-#pragma unroll
-    for (u32 i = 0; i < kDPT; ++i) {
-      t[i] = (long)tile - 1;
-      if (d0 + i < nd) live |= 1u << i;
-    }
-    for (u32 spins = 0; live;) {
-      u64 x[kDPT];
-#pragma unroll
-      for (u32 i = 0; i < kDPT; ++i) x[i] = (live >> i & 1u) ? gran_load(&a.hist_gran[(u64)t[i] * nd + d0 + i]) : 0ull;
-      bool progress = false;
-#pragma unroll
-      for (u32 i = 0; i < kDPT; ++i) {
-        if (!(live >> i & 1u) || (u32)(x[i] >> 32) != a.epoch) continue;
-        progress = true;
-        pre[i] += ((u32)x[i]) & 0x3FFFFFFFu;
-        if ((((u32)x[i]) >> 30) == kIncl)
-          live &= ~(1u << i);
-        else
-          --t[i];
-      }
-      if (!progress) {
-        if (++spins >= kSpinLimit) {
-          atomicOr(a.err, kErrSpinTimeout);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-#pragma unroll
-    for (u32 i = 0; i < kDPT; ++i)
-      if (d0 + i < nd) gran_store(&a.hist_gran[(u64)tile * nd + d0 + i], a.epoch, (kIncl << 30) | (pre[i] + cnt[i]));
-  }
-
-  // ---- digit totals = the last tile's inclusive prefix; exclusive scan over digits
-  u32 tot[kDPT];
-  if (tile == tiles - 1) {
-#pragma unroll
-    for (u32 i = 0; i < kDPT; ++i) tot[i] = pre[i] + cnt[i];
-  } else {
-    for (u32 spins = 0;;) {
-      bool all = true;
-#pragma unroll
-      for (u32 i = 0; i < kDPT; ++i) {
-        tot[i] = 0;
-        if (d0 + i >= nd) continue;
-        const u64 x = gran_load(&a.hist_gran[(u64)(tiles - 1) * nd + d0 + i]);
-        all &= (u32)(x >> 32) == a.epoch && (((u32)x) >> 30) == kIncl;
-        tot[i] = ((u32)x) & 0x3FFFFFFFu;
-      }
-      if (all) break;
-      if (++spins >= kSpinLimit) {
-        atomicOr(a.err, kErrSpinTimeout);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
+  // ---- all-to-all: counts of earlier tiles and digit totals (batched polls)
+  u32 before = 0, total = 0;
+  if (tid < nd && !sweep_column(a.hist_gran + tid, 256, tiles, tile, a.epoch, &before, &total))
+    atomicOr(a.err, kErrSpinTimeout);
+  if (a.first && tid == kST - 1) {  // the length sums, polled by the last lane
+    u32 lb = 0, ltot = 0, rb = 0, rtot = 0;
+    if (!sweep_column2(a.len_gran, a.rb_gran, tiles, tile, a.epoch, &lb, &ltot, &rb, &rtot))
+      atomicOr(a.err, kErrSpinTimeout);
+    s_pre_len = lb;
+    if (tile == tiles - 1) {
+      a.batch_info[0] = rtot;  // record bytes of the batch
+      a.batch_info[1] = ltot;  // payload bytes of the batch
     }
   }
   {
-    u32 mine = 0;
-#pragma unroll
-    for (u32 i = 0; i < kDPT; ++i) mine += tot[i];
     u32 all_tot;
-    u32 run = block_excl_scan<kSW>(mine, s_scan, &all_tot);
-#pragma unroll
-    for (u32 i = 0; i < kDPT; ++i) {
-      if (d0 + i < nd) s_start[d0 + i] = run + pre[i];
-      run += tot[i];
-    }
+    const u32 dexcl = block_excl_scan<kSW>(tid < nd ? total : 0u, s_scan, &all_tot);
+    if (tid < nd) s_start[tid] = dexcl + before;
   }
   __syncthreads();
 
   // ---- scatter
-  const u32 pre_len = a.first ? (u32)s_pre_len : 0u;
+  const u32 pre_len = a.first ? s_pre_len : 0u;
 #pragma unroll
   for (u32 k = 0; k < kSI; ++k) {
-    const u32 j = base + w * 256u + k * 64u + lane;
+    const u32 j = base + k * 64u + lane;
     if (j >= a.n) continue;
     const u32 d = (key[k] >> a.shift) & dmask;
     const u32 pos = s_start[d] + s_wcnt[w][d] + rnk[k];
@@ -276,7 +247,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   if (a.first && !a.last && a.src_off) {
 #pragma unroll
     for (u32 k = 0; k < kSI; ++k) {
-      const u32 j = base + w * 256u + k * 64u + lane;
+      const u32 j = base + k * 64u + lane;
       if (j < a.n) a.src_off[j] = pre_len + so_[k];
     }
   }
