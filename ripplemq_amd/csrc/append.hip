@@ -41,12 +41,14 @@ constexpr u32 kLongCrc = 512;                      // payloads above this: whole
 constexpr u32 kStAgg = 1u, kStIncl = 2u;  // look-back granule tag = epoch << 2 | status
 constexpr u32 kBadPart = 0x80000000u;              // slot len flag: pidx >= P
 
+constexpr u32 kDmaChunks = kImgDw / 64;             // LDS-DMA wave-instructions per tile
+
 struct WaveSmem {
   u32 img[kImgDw];
   uint8_t map[kImgDw];
   u64 pos[64];
-  u64 rb_off[65];
-  u64 rb_pos[65];
+  u64 ra[64];   // pos - imgoff: ring position of image byte 0 as seen by the record's dwords
+  u32 km[64];   // key | local replica mask << 24 (P <= 2^24, RF <= 8)
   u32 key[64];
   u32 imgoff[64];
   u32 len[64];
@@ -56,6 +58,7 @@ struct WaveSmem {
 
 struct AppendSmem {
   u32 crc[8][256];
+  u32 pow8[kCrcPow8];
   WaveSmem wv[kWaves];
 };
 
@@ -105,6 +108,15 @@ __device__ u32 wave_crc32c(const u32 (*t)[256], const CrcConsts* cc, const u32* 
   return crc;
 }
 
+// Phase stamps for the diagnostic run (RMQ_STAMPS): never read by the kernel itself.
+#define RMQ_STAMP(i)                                                                  \
+  do {                                                                                \
+    if (a.stamps) {                                                                   \
+      const u64 t_ = __builtin_amdgcn_s_memrealtime();                                \
+      if (lane == 0) a.stamps[(u64)tile * 8 + (i)] = t_;                              \
+    }                                                                                 \
+  } while (0)
+
 __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   AppendSmem& S = *reinterpret_cast<AppendSmem*>(smem_raw);
@@ -117,6 +129,7 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
   const u32 RF = st.RF;
 
   for (u32 k = threadIdx.x; k < 8 * 256; k += kAppendThreads) (&S.crc[0][0])[k] = a.crc->table[k >> 8][k & 255];
+  for (u32 k = threadIdx.x; k < kCrcPow8; k += kAppendThreads) S.pow8[k] = a.crc->pow8[k];
   __syncthreads();
 
   // Static tile assignment: wave gw takes tiles gw, gw + nw, ...; every wave of the grid is
@@ -128,8 +141,9 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     const bool in = s < a.n;
     const u32 nin = a.n - s0 < 64u ? a.n - s0 : 64u;  // valid slots in this tile
     const u32 last = nin - 1;
+    RMQ_STAMP(0);
 
-    // ---- 1. every load the tile needs, issued up front and unbranched (clamped indices)
+    // ---- 1. slot records, then the partition state (clamped indices, unbranched)
     const uint4 sr = a.slots[in ? s : a.n - 1];
     const u32 e_prev = a.slots[s0 ? s0 - 1 : 0].x;
     const u32 e_next = a.slots[s0 + nin < a.n ? s0 + nin : a.n - 1].x;
@@ -137,23 +151,15 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     const u32 lead = st.is_leader[key];
     const u32 lmask = st.local_mask[key];
     // batch-start state of the record's partition. Safe to read here: the partition's finalizer
-    // (this or a later tile) writes it only after this tile's look-back granules are published.
+    // (this or a later tile) writes it only after this tile's look-back granules are published,
+    // and those are published only after these loads have returned (vmcnt below).
     const u64 base_off = st.leo[key], base_pos = st.used[key];
     const u64 f_start = st.start_pos[key], f_term = st.term_start[key], f_commit = st.commit[key];
     u64 row[kMaxRF];
 #pragma unroll
     for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)key * RF + r] : 0ull;
-
-    u32 prev_key = __shfl_up(key, 1, 64), next_key = __shfl_down(key, 1, 64);
-    prev_key = lane == 0 ? (s0 ? e_prev : 0xFFFFFFFFu) : prev_key;
-    next_key = lane == last ? (s0 + nin < a.n ? e_next : 0xFFFFFFFFu) : next_key;
-    const bool okp = in && !(sr.z & kBadPart);
-    const bool range_ok = (u64)so + L <= a.payload_bytes;
-    const bool ok = okp && range_ok && lead && !nospace;
-    const u32 cnt = ok ? 1u : 0u;
-    const u32 rs = ok ? 16u + ((L + 3u) & ~3u) : 0u;
-    const u32 head = in && (s == 0 || prev_key != key) ? 1u : 0u;
-    const bool run_end = in && next_key != key;
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 
     if (nospace) {
       if (in) a.out_offsets[rec] = ~0ull;
@@ -161,7 +167,55 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
       continue;
     }
 
-    // ---- 2. segmented wave scan: count / bytes relative to the run start (or the tile start)
+    // ---- 2. image layout of every record with a valid partition and payload range (leadership
+    // is not known yet; rejected records occupy image space but are never stored)
+    const bool okp = in && !(sr.z & kBadPart);
+    const bool range_ok = (u64)so + L <= a.payload_bytes;
+    const bool img_rec = okp && range_ok;
+    const u32 rs_img = img_rec ? 16u + ((L + 3u) & ~3u) : 0u;
+    const u32 ioff = wave_incl_scan(rs_img) - rs_img;
+    const u32 tb = __builtin_amdgcn_readlane(ioff + rs_img, 63);
+    const bool aligned = __all(!img_rec || (so & 3u) == 0u);
+    const bool image = tb <= kAppendImageBytes && aligned;
+    const u32 ndw = tb >> 2;
+    if (image) {
+      // map: image dword -> owning lane (store pass); the image slots themselves carry each
+      // payload dword's source offset until the DMA overwrites them (header slots: dummy 0)
+      const u32 d0 = ioff / 4;
+      for (u32 d = 0; d < rs_img / 4; ++d) {
+        W.map[d0 + d] = (uint8_t)lane;
+        W.img[d0 + d] = d < 4 ? 0u : so + 4u * (d - 4u);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- 3. LDS-DMA gather: always exactly kDmaChunks wave-instructions (dummy source when not
+    // needed), so `vmcnt(kDmaChunks)` below waits for the state loads alone. All source offsets
+    // are read in one batch before the first DMA; DMA c overwrites only the slots of chunk c.
+    {
+      u32 srcoff[kDmaChunks];
+#pragma unroll
+      for (u32 c = 0; c < kDmaChunks; ++c) srcoff[c] = W.img[c * 64 + lane];
+      const u32 imgm = 0u - (u32)image;
+#pragma unroll
+      for (u32 c = 0; c < kDmaChunks; ++c) {
+        const u32 use = imgm & (0u - (u32)(c * 64 + lane < ndw));
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(a.payload + (srcoff[c] & use)),
+                                         (__attribute__((address_space(3))) void*)&W.img[c * 64], 4, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kDmaChunks) : "memory");
+    RMQ_STAMP(1);
+
+    // ---- 4. segmented wave scans: count / bytes relative to the run start (or the tile start)
+    u32 prev_key = __shfl_up(key, 1, 64), next_key = __shfl_down(key, 1, 64);
+    prev_key = lane == 0 ? (s0 ? e_prev : 0xFFFFFFFFu) : prev_key;
+    next_key = lane == last ? (s0 + nin < a.n ? e_next : 0xFFFFFFFFu) : next_key;
+    const bool ok = img_rec && lead;
+    const u32 cnt = ok ? 1u : 0u;
+    const u32 rs = ok ? rs_img : 0u;
+    const u32 head = in && (s == 0 || prev_key != key) ? 1u : 0u;
+    const bool run_end = in && next_key != key;
     u32 fc = head, fb = head, c_inc = cnt, b_inc = rs;
     wave_seg_incl_scan(fc, c_inc);
     wave_seg_incl_scan(fb, b_inc);
@@ -172,48 +226,37 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
 
     // publish {count, bytes} of the tile's last run relative to its batch start: INCL when the
     // run starts here, AGG (the tile's whole contribution) when it continued from before.
-    // Waiting for the state loads first is what orders them before any finalizer's writes.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == last) {
       const u32 tag = (a.epoch << 2) | (tile_heads ? kStIncl : kStAgg);
       gran_store(&a.lb_cnt[tile], tag, c_inc);
       gran_store(&a.lb_bytes[tile], tag, b_inc);
     }
-
-    // ---- image layout
-    const u32 ioff = wave_incl_scan(rs) - rs;
-    const u32 tb = __builtin_amdgcn_readlane(ioff + rs, 63);
-    const bool aligned = __all(!ok || (so & 3u) == 0u);
-    const bool image = tb <= kAppendImageBytes && aligned;
     W.key[lane] = key;
     W.len[lane] = L;
     W.so[lane] = so;
     W.imgoff[lane] = ioff;
     W.mask[lane] = ok ? lmask : 0u;
-    const u32 ndw = tb >> 2;
+
+    // ---- 5. CRC32C from the LDS image (pad bytes zeroed first: they are log bytes too)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
+    RMQ_STAMP(2);
+    u32 crc = 0;
     if (image) {
-      for (u32 d = 0; d < rs / 4; ++d) W.map[ioff / 4 + d] = (uint8_t)lane;
       __builtin_amdgcn_wave_barrier();
-      // ---- 3. LDS-DMA gather of the payload dwords into the image (all in flight at once)
-      if (a.debug & 1u) {
-        for (u32 dw = lane; dw < ndw; dw += 64) {
-          const u32 k = W.map[dw];
-          const u32 rel = dw - (W.imgoff[k] >> 2);
-          if (rel >= 4) W.img[dw] = *reinterpret_cast<const u32*>(a.payload + W.so[k] + 4u * (rel - 4u));
-        }
-      } else {
-        for (u32 c = 0; c * 64 < ndw; ++c) {
-          const u32 dw = c * 64 + lane;
-          const u32 k = W.map[dw < ndw ? dw : 0];
-          const u32 rel = dw - (W.imgoff[k] >> 2);
-          const uint8_t* src = (dw < ndw && rel >= 4) ? a.payload + W.so[k] + 4u * (rel - 4u) : a.payload;
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                           (__attribute__((address_space(3))) void*)&W.img[c * 64], 4, 0, 0);
-        }
+      if (ok && (L & 3u)) W.img[ioff / 4 + 4 + L / 4] &= (1u << (8 * (L & 3u))) - 1u;
+      __builtin_amdgcn_wave_barrier();
+      if (ok && L <= kLongCrc) crc = crc32c_lds4(S.crc, S.pow8, &W.img[ioff / 4 + 4], L);
+      u64 longs = __ballot(ok && L > kLongCrc);
+      while (longs) {
+        const u32 k = (u32)__ffsll((long long)longs) - 1u;
+        longs &= longs - 1;
+        const u32 cr = wave_crc32c<true>(S.crc, a.crc, &W.img[W.imgoff[k] / 4 + 4], nullptr, 0, W.len[k]);
+        crc = lane == k ? cr : crc;
       }
     }
+    RMQ_STAMP(3);
 
-    // ---- 2b. look-back: relative count/bytes of the run before this tile (overlaps the DMA)
+    // ---- 6. look-back: relative count/bytes of the run before this tile
     u32 carry_c = 0, carry_b = 0;
     if (cont) {
       u32 acc_c = 0, acc_b = 0;
@@ -256,8 +299,9 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         gran_store(&a.lb_bytes[tile], tag, carry_b + b_inc);
       }
     }
+    RMQ_STAMP(4);
 
-    // ---- absolute offset / position of every record
+    // ---- 7. absolute offset / position of every record, offsets out, sparse index
     const u32 rel_c = (run_id ? 0u : carry_c) + c_exc;
     const u32 rel_b = (run_id ? 0u : carry_b) + b_exc;
     const u64 off_abs = base_off + rel_c;
@@ -272,25 +316,12 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         e[1] = end;
       }
     }
-    __builtin_amdgcn_wave_barrier();
 
     const u64 segmask = st.seg - 1;
     const u64 rstride = (u64)st.P * st.seg;
     if (image) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA landed
-      __builtin_amdgcn_wave_barrier();
-      // ---- 4. CRC32C from LDS (zero the pad bytes of the last payload dword first)
-      if (ok && (L & 3u)) W.img[ioff / 4 + 4 + L / 4] &= (1u << (8 * (L & 3u))) - 1u;
-      __builtin_amdgcn_wave_barrier();
-      u32 crc = 0;
-      if (ok && L <= kLongCrc) crc = crc32c_lds(S.crc, &W.img[ioff / 4 + 4], L);
-      u64 longs = __ballot(ok && L > kLongCrc);
-      while (longs) {
-        const u32 k = (u32)__ffsll((long long)longs) - 1u;
-        longs &= longs - 1;
-        const u32 cr = wave_crc32c<true>(S.crc, a.crc, &W.img[W.imgoff[k] / 4 + 4], nullptr, 0, W.len[k]);
-        crc = lane == k ? cr : crc;
-      }
+      W.ra[lane] = pos_abs - ioff;  // ring position of image byte 0 for this record's dwords
+      W.km[lane] = key | (ok ? lmask << 24 : 0u);
       if (ok) {
         const u32 d0 = ioff / 4;
         W.img[d0 + 0] = (u32)off_abs;
@@ -299,17 +330,38 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         W.img[d0 + 3] = crc;
       }
       __builtin_amdgcn_wave_barrier();
-      // ---- 5. stream the image into every local replica ring
-      for (u32 dw = lane; dw < ndw; dw += 64) {
-        const u32 k = W.map[dw];
-        const u32 v = W.img[dw];
-        const u64 lp = W.pos[k] + (u64)(dw * 4u - W.imgoff[k]);
-        uint8_t* dst = st.logs + (u64)W.key[k] * st.seg + (lp & segmask);
-        const u32 msk = W.mask[k];
-        for (u32 r = 0; r < RF; ++r)
-          if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v;
+      RMQ_STAMP(5);
+      // ---- 8. stream the image into every local replica ring, 8 chunks of 64 dwords per batch:
+      // all LDS reads of a batch (owner, then the owner's ring address and key|mask) are issued
+      // before any store, so a batch costs two LDS round trips instead of two per dword.
+      const u32 nchunks = (ndw + 63u) >> 6;
+      for (u32 c0 = 0; c0 < nchunks; c0 += 8) {
+        u32 k[8], v[8], km[8];
+        u64 ra[8];
+#pragma unroll
+        for (u32 j = 0; j < 8; ++j) k[j] = W.map[(c0 + j) * 64 + lane];
+#pragma unroll
+        for (u32 j = 0; j < 8; ++j) {
+          v[j] = W.img[(c0 + j) * 64 + lane];
+          ra[j] = W.ra[k[j] & 63u];
+          km[j] = W.km[k[j] & 63u];
+        }
+#pragma unroll
+        for (u32 j = 0; j < 8; ++j) {
+          const u32 dw = (c0 + j) * 64 + lane;
+          u32 msk = dw < ndw ? km[j] >> 24 : 0u;
+          if (a.debug & 12u) msk = (a.debug & 4u) ? 0u : (msk & 1u);  // diagnostics: no stores / one replica
+          if (msk) {
+            const u64 lp = ra[j] + 4ull * dw;
+            uint8_t* dst = st.logs + (u64)(km[j] & 0xFFFFFFu) * st.seg + (lp & segmask);
+            for (u32 r = 0; r < RF; ++r)
+              if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v[j];
+          }
+        }
       }
     } else {
+      __builtin_amdgcn_wave_barrier();
+      RMQ_STAMP(5);
       // ---- wave-per-record path (large or unaligned payloads)
       for (u32 k = 0; k < nin; ++k) {
         const u32 msk = __builtin_amdgcn_readfirstlane(W.mask[k]);
@@ -336,7 +388,8 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
       }
     }
 
-    // ---- 6. the lane that ends a run finalizes its partition (state prefetched in step 1)
+    RMQ_STAMP(6);
+    // ---- 9. the lane that ends a run finalizes its partition (state prefetched in step 1)
     const u32 end_c = rel_c + cnt;
     if (run_end && end_c) {
       const u64 end_off = base_off + end_c, end_pos = base_pos + rel_b + rs;
@@ -367,6 +420,8 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
       const u32 n_np = (u32)__popcll(__ballot(in && !okp));
       if (lane == 0) a.tile_stats[tile] = make_uint4(n_app, n_nl, n_np, 0);
     }
+    if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RMQ_STAMP(7);
   }
 }
 

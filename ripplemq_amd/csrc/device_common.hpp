@@ -20,11 +20,13 @@ typedef __attribute__((address_space(1))) u32 gu32;
 constexpr u32 kCrcPoly = 0x82F63B78u;
 constexpr u32 kSpinLimit = 1u << 22;  // polls before a hand-off is declared dead (~seconds)
 constexpr u32 kErrSpinTimeout = 1u;
+constexpr u32 kCrcPow8 = 520;         // pow8[n] = x^(8n) mod P for n < kCrcPow8 (4-chain CRC merge)
 
 // Device constants: CRC tables and GF(2) shift constants, filled by the host at engine creation.
 struct CrcConsts {
   u32 table[8][256];   // slicing-by-8: table[k][b] = CRC register after byte b then k zero bytes
   u32 shift_pow2[32];  // shift_pow2[j] = x^(8 * 2^j) mod P (reflected): "append 2^j zero bytes"
+  u32 pow8[kCrcPow8];  // pow8[n] = x^(8n) mod P: "append n zero bytes"
 };
 
 __device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
@@ -64,6 +66,49 @@ __device__ __forceinline__ u32 crc_step8(const u32 (*t)[256], u32 c, u32 lo, u32
 
 __device__ __forceinline__ u32 crc_step1(const u32 (*t)[256], u32 c, u32 byte) {
   return (c >> 8) ^ t[0][(c ^ byte) & 0xFF];
+}
+
+// CRC register after k in [0, 8] more bytes (lo = bytes 0..3, hi = bytes 4..7; bytes >= k
+// ignored): c' = (c >> 8k) ^ XOR_{i<k} table[k-1-i][byte i of (c ^ data)], one round of lookups.
+__device__ __forceinline__ u32 crc_stepn(const u32 (*t)[256], u32 c, u32 lo, u32 hi, u32 k) {
+  const u32 x = lo ^ c;
+  u32 r = k == 0 ? c : (k < 4 ? c >> (8 * k) : 0u);
+#pragma unroll
+  for (u32 i = 0; i < 8; ++i) {
+    const u32 b = i < 4 ? (x >> (8 * i)) & 0xFF : (hi >> (8 * (i - 4))) & 0xFF;
+    const u32 v = t[(k - 1 - i) & 7][b];
+    r ^= i < k ? v : 0u;
+  }
+  return r;
+}
+
+// Finalized CRC32C of `len` bytes in LDS as four independent chains over contiguous quarters
+// (8-byte blocks split as evenly as possible, the last chain also takes the 0..7 tail bytes),
+// merged by linearity: reg(A||B) = reg(A) * x^(8|B|) ^ reg0(B). One wave per SIMD is LDS-latency
+// bound; four chains keep four lookup rounds in flight (tools/lds_bench.hip: 2.5x over one chain
+// reading its payload from LDS).
+__device__ __forceinline__ u32 crc32c_lds4(const u32 (*t)[256], const u32* pow8, const u32* w, u32 len) {
+  const u32 n8 = len >> 3, q = n8 >> 2, r = n8 & 3u;
+  const u32 s1 = q + (r > 0), s2 = s1 + q + (r > 1), s3 = s2 + q + (r > 2);
+  u32 c0 = 0xFFFFFFFFu, c1 = 0, c2 = 0, c3 = 0;
+  for (u32 i = 0; i < s1; ++i) {
+    const u32 i1 = s1 + i, i2 = s2 + i, i3 = s3 + i;
+    const bool a1 = i1 < s2, a2 = i2 < s3, a3 = i3 < n8;
+    const u32 j1 = a1 ? i1 : 0u, j2 = a2 ? i2 : 0u, j3 = a3 ? i3 : 0u;
+    const u32 x0 = w[2 * i], y0 = w[2 * i + 1];
+    const u32 x1 = w[2 * j1], y1 = w[2 * j1 + 1];
+    const u32 x2 = w[2 * j2], y2 = w[2 * j2 + 1];
+    const u32 x3 = w[2 * j3], y3 = w[2 * j3 + 1];
+    c0 = crc_step8(t, c0, x0, y0);
+    const u32 n1 = crc_step8(t, c1, x1, y1), n2 = crc_step8(t, c2, x2, y2), n3 = crc_step8(t, c3, x3, y3);
+    c1 = a1 ? n1 : c1;
+    c2 = a2 ? n2 : c2;
+    c3 = a3 ? n3 : c3;
+  }
+  c3 = crc_stepn(t, c3, w[2 * n8], w[2 * n8 + 1], len & 7u);
+  const u32 m = gf2_mulmod(pow8[len - 8 * s1], c0) ^ gf2_mulmod(pow8[len - 8 * s2], c1) ^
+                gf2_mulmod(pow8[len - 8 * s3], c2);
+  return ~(m ^ c3);
 }
 
 // Finalized CRC32C of `len` bytes held in LDS starting at a 4-byte aligned dword pointer.

@@ -96,6 +96,9 @@ struct rmq_engine {
   uint32_t debug_flags = 0;   // RMQ_DEBUG_FLAGS -> AppendArgs.debug
   uint32_t spin_limit = 1u << 22;
   hipEvent_t last_append_done = nullptr;
+  uint64_t* d_stamps = nullptr;     // RMQ_STAMPS=<csv path>: append phase stamps of the last batch
+  const char* stamps_path = nullptr;
+  uint32_t stamps_tiles = 0;
   // profiling
   bool profile = false;
   std::vector<EvPair> prof[5];
@@ -151,6 +154,8 @@ void build_crc_consts(CrcConsts* c) {
   x2n[0] = 0x40000000u;  // x^1 in the reflected representation
   for (int k = 1; k < 40; ++k) x2n[k] = host_mulmod(x2n[k - 1], x2n[k - 1]);
   for (int j = 0; j < 32; ++j) c->shift_pow2[j] = x2n[j + 3];  // x^(8 * 2^j)
+  c->pow8[0] = 0x80000000u;                                     // x^0
+  for (uint32_t n = 1; n < kCrcPow8; ++n) c->pow8[n] = host_mulmod(c->pow8[n - 1], x2n[3]);
 }
 
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
@@ -203,10 +208,28 @@ int ensure_ctl(rmq_engine* e, uint32_t n) {
   return RMQ_OK;
 }
 
+void dump_stamps(rmq_engine* e) {
+  if (!e->stamps_path || !e->d_stamps || !e->stamps_tiles) return;
+  std::vector<uint64_t> h((size_t)e->stamps_tiles * 8);
+  if (hipMemcpy(h.data(), e->d_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  FILE* f = std::fopen(e->stamps_path, "w");
+  if (!f) return;
+  std::fprintf(f, "tile,t0,t1,t2,t3,t4,t5,t6,t7\n");
+  for (uint32_t t = 0; t < e->stamps_tiles; ++t) {
+    std::fprintf(f, "%u", t);
+    for (int k = 0; k < 8; ++k) std::fprintf(f, ",%llu", (unsigned long long)h[(size_t)t * 8 + k]);
+    std::fprintf(f, "\n");
+  }
+  std::fclose(f);
+}
+
 void free_engine(rmq_engine* e) {
   if (!e) return;
   hipSetDevice(e->device);
   if (e->main_s) hipStreamSynchronize(e->main_s);
+  for (hipStream_t ps : e->prep)
+    if (ps) hipStreamSynchronize(ps);
+  dump_stamps(e);
   for (hipStream_t ps : e->prep)
     if (ps) hipStreamSynchronize(ps);
   DevState& s = e->st;
@@ -214,7 +237,7 @@ void free_engine(rmq_engine* e) {
                   s.is_leader, s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner,
                   e->d_err, e->d_tile_stats,
                   e->d_lb_cnt, e->d_lb_bytes, e->d_req, e->d_res, e->d_aux,
-                  e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64};
+                  e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (void* b : bufs)
     if (b) hipFree(b);
   for (Slot& sl : e->slots) {
@@ -302,6 +325,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* dbg = std::getenv("RMQ_DEBUG_SKIP")) e->debug_skip = (uint32_t)std::atoi(dbg);
   if (const char* dbg = std::getenv("RMQ_DEBUG_FLAGS")) e->debug_flags = (uint32_t)std::atoi(dbg);
   if (const char* dbg = std::getenv("RMQ_SPIN_LIMIT")) e->spin_limit = (uint32_t)std::atoi(dbg);
+  e->stamps_path = std::getenv("RMQ_STAMPS");
   e->device = cfg->device;
 #define CREATE_TRY(x)      \
   do {                     \
@@ -584,6 +608,14 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   a.err = e->d_err;
   a.spin_limit = e->spin_limit;
   a.debug = e->debug_flags;
+  if (e->stamps_path) {
+    if (!e->d_stamps) {
+      int rc = dalloc(&e->d_stamps, (size_t)e->max_app_tiles * 8);
+      if (rc) return rc;
+    }
+    a.stamps = e->d_stamps;
+    e->stamps_tiles = a.tiles;
+  }
   const uint32_t wpb = (uint32_t)append_waves_per_block();
   const uint32_t grid = std::min<uint32_t>((a.tiles + wpb - 1) / wpb, e->cu_count * (uint32_t)append_blocks_per_cu());
   hipEvent_t pa0 = nullptr, pa1 = nullptr;

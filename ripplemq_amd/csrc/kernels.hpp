@@ -79,7 +79,8 @@ struct AppendArgs {
   const CrcConsts* crc;
   uint32_t* err;
   uint32_t spin_limit;
-  uint32_t debug;            // bit 0: register staging instead of LDS-DMA, bit 1: no look-back
+  uint32_t debug;            // diagnostics (RMQ_DEBUG_FLAGS): bit 2 no ring stores, bit 3 replica 0 only
+  uint64_t* stamps;          // diagnostic build only: [tiles][8] s_memrealtime per phase, or null
 };
 
 struct FetchArgs {
