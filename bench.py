@@ -32,6 +32,7 @@ sys.path.insert(0, REPO)
 
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
 from ripplemq_amd.engine import Engine, EngineConfig  # noqa: E402
+from ripplemq_amd.sharding import max_over_ranks  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -131,13 +132,7 @@ def main() -> None:
     n_sort, sort_ms = eng.profile_query(1)
     eng.profile(False)
 
-    t_max = elapsed
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
+    t_max = max_over_ranks(elapsed, dist)
 
     n = spec.records
     total_records = n * args.steps * world

@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 from ripplemq_amd import _abi as A
-from ripplemq_amd.engine import FETCH_RES_DTYPE, EngineConfig, state_to_dict
+from ripplemq_amd.engine import FETCH_RES_DTYPE, EngineConfig, EngineError, state_to_dict
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libripple_oracle.so")
@@ -96,12 +96,12 @@ class OracleEngine:
         r = (C.c_uint32 * len(ranks))(*ranks)
         rc = self.lib.ro_set_replicas(self.h, pidx, r, len(ranks), leader_slot)
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
 
     def become_leader(self, pidx, term):
         rc = self.lib.ro_become_leader(self.h, pidx, term)
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
 
     def append(self, pidx, lens, payload, payload_off=None):
         pidx = np.ascontiguousarray(pidx, np.uint32)
@@ -114,7 +114,7 @@ class OracleEngine:
         rc = self.lib.ro_append(self.h, len(pidx), _p(pidx), _p(lens), _p(payload_off),
                                 _p(payload) if payload.size else None, payload.size, _p(out), C.byref(st))
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
         return out, {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_ if f != "reserved"}
 
     def ack(self, pidx, slot, match):
@@ -123,7 +123,7 @@ class OracleEngine:
         match = np.ascontiguousarray(match, np.uint64)
         rc = self.lib.ro_ack(self.h, _p(pidx), _p(slot), _p(match), len(pidx))
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
 
     def commit_consumer_offset(self, pidx, consumer, offset):
         pidx = np.ascontiguousarray(pidx, np.uint32)
@@ -150,7 +150,7 @@ class OracleEngine:
         s = A.RmqPartitionState()
         rc = self.lib.ro_get_partition_state(self.h, pidx, C.byref(s))
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
         return state_to_dict(s, self.cfg.replication_factor)
 
     def read_segment(self, replica, pidx, ring_off=0, n=None):
@@ -158,14 +158,14 @@ class OracleEngine:
         out = np.empty(n, np.uint8)
         rc = self.lib.ro_read_segment(self.h, replica, pidx, ring_off, n, _p(out))
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
         return out
 
     def read_index(self, pidx, m_first, count):
         out = np.empty((count, 2), np.uint64)
         rc = self.lib.ro_read_index(self.h, pidx, m_first, count, _p(out))
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
         return out
 
     def consumer_offsets(self, pidx):
@@ -177,5 +177,5 @@ class OracleEngine:
         v = C.c_uint64()
         rc = self.lib.ro_record_pos(self.h, pidx, offset, C.byref(v))
         if rc:
-            raise RuntimeError(A.STATUS_NAMES.get(rc, rc))
+            raise EngineError(rc, "oracle")
         return int(v.value)

@@ -354,8 +354,13 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
           if (msk) {
             const u64 lp = ra[j] + 4ull * dw;
             uint8_t* dst = st.logs + (u64)(km[j] & 0xFFFFFFu) * st.seg + (lp & segmask);
-            for (u32 r = 0; r < RF; ++r)
-              if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v[j];
+            if (a.debug & 16u) {
+              for (u32 r = 0; r < RF; ++r)
+                if (msk >> r & 1u) __builtin_nontemporal_store(v[j], reinterpret_cast<u32*>(dst + r * rstride));
+            } else {
+              for (u32 r = 0; r < RF; ++r)
+                if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v[j];
+            }
           }
         }
       }

@@ -28,19 +28,19 @@ constexpr u32 kSW = kST / 64;         // 4 waves
 constexpr u32 kWK = kSortTile / kSW;  // keys per wave (512)
 
 // Sum a column of {epoch|value} granules over all tiles and over tiles < `tile`. The loads of a
-// sweep are issued 16 at a time before any is inspected; the sweep repeats until every tag
-// matches (bounded).
+// sweep are issued 32 at a time before any is inspected (one round trip for <= 32 tiles); the
+// sweep repeats until every tag matches (bounded).
 __device__ __forceinline__ bool sweep_column(const u64* g, u32 stride, u32 tiles, u32 tile, u32 epoch,
                                              u32* before, u32* total) {
   for (u32 spins = 0; spins < kSpinLimit; ++spins) {
     u32 b = 0, t = 0;
     bool ok = true;
-    for (u32 t0 = 0; t0 < tiles; t0 += 16) {
-      u64 x[16];
+    for (u32 t0 = 0; t0 < tiles; t0 += 32) {
+      u64 x[32];
 #pragma unroll
-      for (u32 i = 0; i < 16; ++i) x[i] = gran_load(g + (u64)(t0 + i < tiles ? t0 + i : 0) * stride);
+      for (u32 i = 0; i < 32; ++i) x[i] = gran_load(g + (u64)(t0 + i < tiles ? t0 + i : 0) * stride);
 #pragma unroll
-      for (u32 i = 0; i < 16; ++i) {
+      for (u32 i = 0; i < 32; ++i) {
         const bool in = t0 + i < tiles;
         ok &= !in || (u32)(x[i] >> 32) == epoch;
         const u32 c = in ? (u32)x[i] : 0u;
@@ -58,41 +58,47 @@ __device__ __forceinline__ bool sweep_column(const u64* g, u32 stride, u32 tiles
   return false;
 }
 
-// Two unit-stride columns swept together (payload bytes and record bytes per tile).
-__device__ __forceinline__ bool sweep_column2(const u64* g0, const u64* g1, u32 tiles, u32 tile, u32 epoch,
-                                              u32* b0, u32* t0_, u32* b1, u32* t1_) {
-  for (u32 spins = 0; spins < kSpinLimit; ++spins) {
-    u32 sb0 = 0, st0 = 0, sb1 = 0, st1 = 0;
+// Payload-byte and record-byte sums of all tiles, by one whole wave: lane l holds tiles l and
+// l + 64 (<= 128 tiles). The first poll's loads are issued by the caller early (`x`, `y`), so their
+// latency overlaps the ranking; lanes re-poll only until every tag matches (bounded).
+__device__ __forceinline__ bool sweep_lenrb_wave(const u64* g0, const u64* g1, u32 tiles, u32 tile, u32 epoch,
+                                                 u32 lane, u64 (&x)[2], u64 (&y)[2], u32* pre_len,
+                                                 u32* tot_len, u32* tot_rb) {
+  for (u32 spins = 0;; ++spins) {
     bool ok = true;
-    for (u32 t0 = 0; t0 < tiles; t0 += 8) {
-      u64 x[8], y[8];
 #pragma unroll
-      for (u32 i = 0; i < 8; ++i) {
-        const u32 t = t0 + i < tiles ? t0 + i : 0;
-        x[i] = gran_load(g0 + t);
-        y[i] = gran_load(g1 + t);
-      }
-#pragma unroll
-      for (u32 i = 0; i < 8; ++i) {
-        const bool in = t0 + i < tiles;
-        ok &= !in || ((u32)(x[i] >> 32) == epoch && (u32)(y[i] >> 32) == epoch);
-        const u32 c0 = in ? (u32)x[i] : 0u, c1 = in ? (u32)y[i] : 0u;
-        st0 += c0;
-        st1 += c1;
-        sb0 += t0 + i < tile ? c0 : 0u;
-        sb1 += t0 + i < tile ? c1 : 0u;
-      }
+    for (u32 h = 0; h < 2; ++h) {
+      const u32 t = lane + 64 * h;
+      ok &= t >= tiles || ((u32)(x[h] >> 32) == epoch && (u32)(y[h] >> 32) == epoch);
     }
-    if (ok) {
-      *b0 = sb0;
-      *t0_ = st0;
-      *b1 = sb1;
-      *t1_ = st1;
-      return true;
-    }
+    if (__all(ok)) break;
+    if (spins >= kSpinLimit) return false;
     __builtin_amdgcn_s_sleep(2);
+#pragma unroll
+    for (u32 h = 0; h < 2; ++h) {
+      const u32 t = lane + 64 * h < tiles ? lane + 64 * h : 0;
+      x[h] = gran_load(g0 + t);
+      y[h] = gran_load(g1 + t);
+    }
   }
-  return false;
+  u32 pl = 0, tl = 0, tr = 0;
+#pragma unroll
+  for (u32 h = 0; h < 2; ++h) {
+    const u32 t = lane + 64 * h;
+    const u32 c0 = t < tiles ? (u32)x[h] : 0u, c1 = t < tiles ? (u32)y[h] : 0u;
+    tl += c0;
+    tr += c1;
+    pl += t < tile ? c0 : 0u;
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    pl += __shfl_xor(pl, d, 64);
+    tl += __shfl_xor(tl, d, 64);
+    tr += __shfl_xor(tr, d, 64);
+  }
+  *pre_len = pl;
+  *tot_len = tl;
+  *tot_rb = tr;
+  return true;
 }
 
 __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
@@ -162,6 +168,16 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
       gran_store(&a.rb_gran[tile], a.epoch, (u32)(tile_sum >> 32));
     }
   }
+  // first poll of every tile's {payload, record} byte sums: issued now, inspected after ranking
+  u64 lx[2] = {0, 0}, ly[2] = {0, 0};
+  if (a.first && w == 0) {
+#pragma unroll
+    for (u32 h = 0; h < 2; ++h) {
+      const u32 t = lane + 64 * h < tiles ? lane + 64 * h : 0;
+      lx[h] = gran_load(a.len_gran + t);
+      ly[h] = gran_load(a.rb_gran + t);
+    }
+  }
 
   // ---- in-tile stable ranking per wave
   __syncthreads();
@@ -200,14 +216,17 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   u32 before = 0, total = 0;
   if (tid < nd && !sweep_column(a.hist_gran + tid, 256, tiles, tile, a.epoch, &before, &total))
     atomicOr(a.err, kErrSpinTimeout);
-  if (a.first && tid == kST - 1) {  // the length sums, polled by the last lane
-    u32 lb = 0, ltot = 0, rb = 0, rtot = 0;
-    if (!sweep_column2(a.len_gran, a.rb_gran, tiles, tile, a.epoch, &lb, &ltot, &rb, &rtot))
-      atomicOr(a.err, kErrSpinTimeout);
-    s_pre_len = lb;
-    if (tile == tiles - 1) {
-      a.batch_info[0] = rtot;  // record bytes of the batch
-      a.batch_info[1] = ltot;  // payload bytes of the batch
+  if (a.first && w == 0) {  // the byte sums, by wave 0
+    u32 lb = 0, ltot = 0, rtot = 0;
+    if (!sweep_lenrb_wave(a.len_gran, a.rb_gran, tiles, tile, a.epoch, lane, lx, ly, &lb, &ltot, &rtot)) {
+      if (lane == 0) atomicOr(a.err, kErrSpinTimeout);
+    }
+    if (lane == 0) {
+      s_pre_len = lb;
+      if (tile == tiles - 1) {
+        a.batch_info[0] = rtot;  // record bytes of the batch
+        a.batch_info[1] = ltot;  // payload bytes of the batch
+      }
     }
   }
   {

@@ -1,0 +1,71 @@
+"""Partition sharding across GPUs (host routing).
+
+Partitions are independent Raft groups (reference: one ``PartitionRaftServer`` per
+``topic-partitionId``, ``mq-broker/src/main/java/metadata/PartitionManager.java:111-176``), so a
+node with W GPUs gives GPU ``g`` the contiguous global partition range
+``[g * P_local, (g + 1) * P_local)`` and routes each produced record to the GPU that leads its
+partition. Routing keeps batch order within every partition, which is all the reference's
+apply-order semantics needs (offsets are per partition). Payload bytes are not copied: each
+shard gets explicit payload offsets into the caller's buffer (``rmq_batch.payload_off``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+
+@dataclass
+class Shard:
+    rank: int
+    records: np.ndarray      # positions of this shard's records in the original batch (ascending)
+    pidx: np.ndarray         # local partition index, u32
+    lens: np.ndarray         # u32
+    payload_off: np.ndarray  # u64 byte offsets into the original payload buffer
+
+
+def owner(pidx: np.ndarray, parts_per_rank: int) -> np.ndarray:
+    return (np.asarray(pidx, np.uint64) // np.uint64(parts_per_rank)).astype(np.int64)
+
+
+def packed_offsets(lens: np.ndarray) -> np.ndarray:
+    off = np.zeros(len(lens), np.uint64)
+    if len(lens) > 1:
+        np.cumsum(np.asarray(lens[:-1], np.uint64), out=off[1:])
+    return off
+
+
+def split_batch(pidx: np.ndarray, lens: np.ndarray, world: int, parts_per_rank: int,
+                payload_off: np.ndarray | None = None) -> list[Shard]:
+    """Route a global batch to its owning ranks, order-preserving. Records whose partition lies
+    beyond ``world * parts_per_rank`` go to no shard (the caller answers them as unknown)."""
+    pidx = np.asarray(pidx, np.uint32)
+    lens = np.asarray(lens, np.uint32)
+    offs = packed_offsets(lens) if payload_off is None else np.asarray(payload_off, np.uint64)
+    own = owner(pidx, parts_per_rank)
+    out = []
+    for r in range(world):
+        sel = np.flatnonzero(own == r)
+        out.append(Shard(r, sel, (pidx[sel] - np.uint32(r * parts_per_rank)).astype(np.uint32),
+                         lens[sel], offs[sel]))
+    return out
+
+
+def merge_offsets(n: int, shards: list[Shard], shard_offsets: list[np.ndarray]) -> np.ndarray:
+    """Per-record offsets in original batch order; records no shard took stay RMQ_OFFSET_NONE."""
+    out = np.full(n, np.iinfo(np.uint64).max, np.uint64)
+    for s, o in zip(shards, shard_offsets):
+        out[s.records] = o
+    return out
+
+
+def max_over_ranks(value: float, dist=None) -> float:
+    """Max of a host-side scalar over the process group (the bench's timed-region rule); identity
+    without a group. Uses the group's own backend (gloo on CPU)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(value)
+    import torch
+
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
