@@ -52,6 +52,7 @@ extern "C" {
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
 #define RMQ_RECORD_HEADER_BYTES 16u
+#define RMQ_RECORD_ALIGN 16u /* records start and end on 16-byte boundaries (FORMAT.md §1) */
 
 /* Status codes. Negative = error; RMQ_PENDING is a non-error poll result. */
 enum {
@@ -158,7 +159,7 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
    the high watermark. Asynchronous: returns a ticket; caller buffers must stay valid until
    rmq_poll_commit(ticket) returns RMQ_OK. out_offsets (same memory kind as the batch) gets the
    offset of each record, or RMQ_OFFSET_NONE if it was rejected (not leader / unknown pidx).
-   If the batch's total record bytes (sum of 16 + align4(len)) exceed segment_bytes -
+   If the batch's total record bytes (sum of 16 + align16(len)) exceed segment_bytes -
    index_interval, no record is appended (rmq_ticket_stats reports rejected_no_space). */
 int rmq_append(rmq_engine* e, const rmq_batch* batch, uint64_t* out_offsets, uint64_t* ticket);
 

@@ -300,7 +300,7 @@ int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* le
     uint64_t off = payload_off ? payload_off[i] : run;
     if (len[i] && (!payload || off > payload_bytes || len[i] > payload_bytes - off)) return RMQ_EINVAL;
     run += len[i];
-    out_bytes += RMQ_RECORD_HEADER_BYTES + ((len[i] + 3u) & ~3ull);
+    out_bytes += RMQ_RECORD_HEADER_BYTES + ((len[i] + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
   }
   if (out_bytes > c->segment_bytes - I) {
     for (uint32_t i = 0; i < n; ++i) out_offsets[i] = RMQ_OFFSET_NONE;
@@ -329,7 +329,7 @@ int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* le
       continue;
     }
     uint32_t L = len[i];
-    uint64_t rs = RMQ_RECORD_HEADER_BYTES + ((L + 3u) & ~3ull);
+    uint64_t rs = RMQ_RECORD_HEADER_BYTES + ((L + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
     if (rs > rec_cap) {
       uint8_t* nr = (uint8_t*)realloc(rec, rs);
       if (!nr) {

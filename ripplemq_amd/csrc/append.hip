@@ -43,7 +43,7 @@ constexpr u32 kBadPart = 0x80000000u;              // slot len flag: pidx >= P
 
 constexpr u32 kDmaChunks = kImgDw / 64;             // LDS-DMA wave-instructions per tile
 
-struct WaveSmem {
+struct alignas(16) WaveSmem {
   u32 img[kImgDw];
   uint8_t map[kImgDw];
   u64 pos[64];
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     const bool okp = in && !(sr.z & kBadPart);
     const bool range_ok = (u64)so + L <= a.payload_bytes;
     const bool img_rec = okp && range_ok;
-    const u32 rs_img = img_rec ? 16u + ((L + 3u) & ~3u) : 0u;
+    const u32 rs_img = img_rec ? record_bytes(L) : 0u;
     const u32 ioff = wave_incl_scan(rs_img) - rs_img;
     const u32 tb = __builtin_amdgcn_readlane(ioff + rs_img, 63);
     const bool aligned = __all(!img_rec || (so & 3u) == 0u);
@@ -181,10 +181,10 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     if (image) {
       // map: image dword -> owning lane (store pass); the image slots themselves carry each
       // payload dword's source offset until the DMA overwrites them (header slots: dummy 0)
-      const u32 d0 = ioff / 4;
+      const u32 d0 = ioff / 4, pend = 4u + ((L + 3u) >> 2);  // payload dwords [4, pend)
       for (u32 d = 0; d < rs_img / 4; ++d) {
         W.map[d0 + d] = (uint8_t)lane;
-        W.img[d0 + d] = d < 4 ? 0u : so + 4u * (d - 4u);
+        W.img[d0 + d] = (d < 4 || d >= pend) ? 0u : so + 4u * (d - 4u);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -243,7 +243,11 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
     u32 crc = 0;
     if (image) {
       __builtin_amdgcn_wave_barrier();
-      if (ok && (L & 3u)) W.img[ioff / 4 + 4 + L / 4] &= (1u << (8 * (L & 3u))) - 1u;
+      if (ok) {  // pad bytes: the tail of the last payload dword, then whole pad dwords
+        const u32 d0 = ioff / 4, pend = 4u + ((L + 3u) >> 2);
+        if (L & 3u) W.img[d0 + 4 + L / 4] &= (1u << (8 * (L & 3u))) - 1u;
+        for (u32 d = pend; d < rs / 4; ++d) W.img[d0 + d] = 0u;
+      }
       __builtin_amdgcn_wave_barrier();
       if (ok && L <= kLongCrc) crc = crc32c_lds4(S.crc, S.pow8, &W.img[ioff / 4 + 4], L);
       u64 longs = __ballot(ok && L > kLongCrc);
@@ -331,36 +335,33 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
       }
       __builtin_amdgcn_wave_barrier();
       RMQ_STAMP(5);
-      // ---- 8. stream the image into every local replica ring, 8 chunks of 64 dwords per batch:
-      // all LDS reads of a batch (owner, then the owner's ring address and key|mask) are issued
-      // before any store, so a batch costs two LDS round trips instead of two per dword.
-      const u32 nchunks = (ndw + 63u) >> 6;
-      for (u32 c0 = 0; c0 < nchunks; c0 += 8) {
-        u32 k[8], v[8], km[8];
-        u64 ra[8];
+      // ---- 8. stream the image into every local replica ring in 16-B pieces (records are
+      // 16-B aligned in the image and in the ring, so a piece never straddles records or the
+      // ring end): one dwordx4 store per lane per replica per KiB; all LDS reads of a batch of 4
+      // chunks are issued before any store.
+      const u32 npc = ndw >> 2;
+      for (u32 c0 = 0; c0 * 64 < npc; c0 += 4) {
+        u32 k[4], km[4];
+        u64 ra[4];
+        uint4 v[4];
 #pragma unroll
-        for (u32 j = 0; j < 8; ++j) k[j] = W.map[(c0 + j) * 64 + lane];
+        for (u32 j = 0; j < 4; ++j) k[j] = W.map[(((c0 + j) * 64 + lane) * 4) & (kImgDw - 1)];
 #pragma unroll
-        for (u32 j = 0; j < 8; ++j) {
-          v[j] = W.img[(c0 + j) * 64 + lane];
+        for (u32 j = 0; j < 4; ++j) {
+          v[j] = *reinterpret_cast<const uint4*>(&W.img[(((c0 + j) * 64 + lane) * 4) & (kImgDw - 1)]);
           ra[j] = W.ra[k[j] & 63u];
           km[j] = W.km[k[j] & 63u];
         }
 #pragma unroll
-        for (u32 j = 0; j < 8; ++j) {
-          const u32 dw = (c0 + j) * 64 + lane;
-          u32 msk = dw < ndw ? km[j] >> 24 : 0u;
+        for (u32 j = 0; j < 4; ++j) {
+          const u32 q = (c0 + j) * 64 + lane;
+          u32 msk = q < npc ? km[j] >> 24 : 0u;
           if (a.debug & 12u) msk = (a.debug & 4u) ? 0u : (msk & 1u);  // diagnostics: no stores / one replica
           if (msk) {
-            const u64 lp = ra[j] + 4ull * dw;
-            uint8_t* dst = st.logs + (u64)(km[j] & 0xFFFFFFu) * st.seg + (lp & segmask);
-            if (a.debug & 16u) {
-              for (u32 r = 0; r < RF; ++r)
-                if (msk >> r & 1u) __builtin_nontemporal_store(v[j], reinterpret_cast<u32*>(dst + r * rstride));
-            } else {
-              for (u32 r = 0; r < RF; ++r)
-                if (msk >> r & 1u) *reinterpret_cast<u32*>(dst + r * rstride) = v[j];
-            }
+            const u64 lp = (ra[j] + 16ull * q) & segmask;
+            uint8_t* dst = st.logs + (u64)(km[j] & 0xFFFFFFu) * st.seg + lp;
+            for (u32 r = 0; r < RF; ++r)
+              if (msk >> r & 1u) *reinterpret_cast<uint4*>(dst + r * rstride) = v[j];
           }
         }
       }
@@ -375,12 +376,14 @@ __global__ __launch_bounds__(kAppendThreads, 2) void append_kernel(AppendArgs a)
         const u64 sk = W.so[k], P0 = W.pos[k];
         const u32 cr = wave_crc32c<false>(S.crc, a.crc, nullptr, a.payload, sk, Lk);
         uint8_t* rb = st.logs + (u64)W.key[k] * st.seg;
-        const u32 pdw = (Lk + 3u) >> 2;
+        const u32 pdw = (Lk + 3u) >> 2, rdw = record_bytes(Lk) >> 2;
         const u64 ko = ((u64)__builtin_amdgcn_readlane((u32)(off_abs >> 32), k) << 32) |
                        __builtin_amdgcn_readlane((u32)off_abs, k);
-        for (u32 d = lane; d < pdw + 4; d += 64) {
+        for (u32 d = lane; d < rdw; d += 64) {
           u32 v;
-          if (d >= 4) {
+          if (d >= 4 + pdw) {
+            v = 0u;  // pad dwords
+          } else if (d >= 4) {
             const u32 b = 4 * (d - 4);
             v = load_payload_dw(a.payload, sk + b, Lk - b < 4 ? Lk - b : 4);
           } else {

@@ -20,6 +20,7 @@ typedef __attribute__((address_space(1))) u32 gu32;
 constexpr u32 kCrcPoly = 0x82F63B78u;
 constexpr u32 kSpinLimit = 1u << 22;  // polls before a hand-off is declared dead (~seconds)
 constexpr u32 kErrSpinTimeout = 1u;
+constexpr u32 kRecAlign = 16;         // FORMAT.md §1: records padded to 16 bytes
 constexpr u32 kCrcPow8 = 520;         // pow8[n] = x^(8n) mod P for n < kCrcPow8 (4-chain CRC merge)
 
 // Device constants: CRC tables and GF(2) shift constants, filled by the host at engine creation.
@@ -28,6 +29,11 @@ struct CrcConsts {
   u32 shift_pow2[32];  // shift_pow2[j] = x^(8 * 2^j) mod P (reflected): "append 2^j zero bytes"
   u32 pow8[kCrcPow8];  // pow8[n] = x^(8n) mod P: "append n zero bytes"
 };
+
+// FORMAT.md §1 record size: 16-byte header + payload padded to kRecAlign.
+__host__ __device__ __forceinline__ constexpr u32 record_bytes(u32 len) {
+  return 16u + ((len + kRecAlign - 1u) & ~(kRecAlign - 1u));
+}
 
 __device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 

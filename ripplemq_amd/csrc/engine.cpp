@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "../../include/ripplemq_engine.h"
@@ -97,6 +98,8 @@ struct rmq_engine {
   uint32_t spin_limit = 1u << 22;
   hipEvent_t last_append_done = nullptr;
   uint64_t* d_stamps = nullptr;     // RMQ_STAMPS=<csv path>: append phase stamps of the last batch
+  uint64_t* d_sort_stamps = nullptr;  // [pass][tiles][8] sort phase stamps of the last batch
+  uint32_t sort_stamps_tiles = 0, sort_stamps_passes = 0;
   const char* stamps_path = nullptr;
   uint32_t stamps_tiles = 0;
   // profiling
@@ -221,6 +224,21 @@ void dump_stamps(rmq_engine* e) {
     std::fprintf(f, "\n");
   }
   std::fclose(f);
+  if (!e->d_sort_stamps || !e->sort_stamps_tiles) return;
+  std::vector<uint64_t> g((size_t)3 * kMaxSortTiles * 8);
+  if (hipMemcpy(g.data(), e->d_sort_stamps, g.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  std::string sp = std::string(e->stamps_path) + ".sort.csv";
+  f = std::fopen(sp.c_str(), "w");
+  if (!f) return;
+  std::fprintf(f, "pass,tile,t0,t1,t2,t3,t4,t5,t6,t7\n");
+  for (uint32_t k = 0; k < e->sort_stamps_passes; ++k)
+    for (uint32_t t = 0; t < e->sort_stamps_tiles; ++t) {
+      std::fprintf(f, "%u,%u", k, t);
+      for (int q = 0; q < 8; ++q)
+        std::fprintf(f, ",%llu", (unsigned long long)g[((size_t)k * kMaxSortTiles + t) * 8 + q]);
+      std::fprintf(f, "\n");
+    }
+  std::fclose(f);
 }
 
 void free_engine(rmq_engine* e) {
@@ -237,7 +255,7 @@ void free_engine(rmq_engine* e) {
                   s.is_leader, s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner,
                   e->d_err, e->d_tile_stats,
                   e->d_lb_cnt, e->d_lb_bytes, e->d_req, e->d_res, e->d_aux,
-                  e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64, e->d_stamps};
+                  e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_sort_stamps};
   for (void* b : bufs)
     if (b) hipFree(b);
   for (Slot& sl : e->slots) {
@@ -575,6 +593,15 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     a.last = k + 1 == e->passes;
     a.epoch = ++e->epoch;
     a.err = e->d_err;
+    if (e->stamps_path) {
+      if (!e->d_sort_stamps) {
+        int rc = dalloc(&e->d_sort_stamps, (size_t)3 * kMaxSortTiles * 8);
+        if (rc) return rc;
+      }
+      a.stamps = e->d_sort_stamps + (size_t)k * kMaxSortTiles * 8;
+      e->sort_stamps_tiles = sort_tiles;
+      e->sort_stamps_passes = e->passes;
+    }
     if (!(e->debug_skip & 1u)) launch_sort_pass(a, sort_tiles, prep_s);
     kin = sl.keys[0];
     vin = sl.vals[0];

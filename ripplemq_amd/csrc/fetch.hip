@@ -42,7 +42,7 @@ __device__ u64 record_pos(const DevState& st, u32 p, const PartView& v, u64 t) {
   const u64 mask = st.seg - 1;
   for (u32 guard = 0; c_off < t && guard < (1u << 20); ++guard) {  // at most ~I / 16 records
     const u32 L = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 8) & mask));
-    c_pos += 16ull + ((L + 3ull) & ~3ull);
+    c_pos += record_bytes(L);
     ++c_off;
   }
   return c_pos;

@@ -60,6 +60,7 @@ struct SortPassArgs {
   uint32_t first, last;
   uint32_t epoch;
   uint32_t* err;
+  uint64_t* stamps;             // diagnostic build only: [tiles][8] s_memrealtime per phase, or null
 };
 
 struct AppendArgs {

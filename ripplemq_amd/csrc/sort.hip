@@ -101,6 +101,15 @@ __device__ __forceinline__ bool sweep_lenrb_wave(const u64* g0, const u64* g1, u
   return true;
 }
 
+// Phase stamps for the diagnostic run (RMQ_STAMPS): never read by the kernel itself.
+#define SORT_STAMP(i)                                                                 \
+  do {                                                                                \
+    if (a.stamps) {                                                                   \
+      const u64 t_ = __builtin_amdgcn_s_memrealtime();                                \
+      if (tid == 0) a.stamps[(u64)tile * 8 + (i)] = t_;                               \
+    }                                                                                 \
+  } while (0)
+
 __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   __shared__ uint16_t s_wcnt[kSW][256];  // per-wave digit counters, then per-wave bases
   __shared__ u32 s_start[256];           // this tile's global position base per digit
@@ -114,6 +123,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   const u32 dmask = (1u << a.bits) - 1u;
   const u64 lt = (1ull << lane) - 1ull;
 
+  SORT_STAMP(0);
   reinterpret_cast<u32*>(&s_wcnt[0][0])[tid] = 0;  // kSW * 256 u16 = 2 u32 per thread
   reinterpret_cast<u32*>(&s_wcnt[0][0])[tid + kST] = 0;
 
@@ -140,13 +150,15 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
     so_[k] = 0;
   }
 
+  if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SORT_STAMP(1);
   // ---- first pass: input-order scan of {record bytes : payload bytes} inside the tile
   if (a.first) {
     u64 wcarry = 0;
 #pragma unroll
     for (u32 k = 0; k < kSI; ++k) {
       const u32 j = base + k * 64u + lane;
-      const u64 v = j < a.n ? ((u64)(16u + ((len_[k] + 3u) & ~3u)) << 32) | len_[k] : 0ull;
+      const u64 v = j < a.n ? ((u64)record_bytes(len_[k]) << 32) | len_[k] : 0ull;
       const u64 inc = wave_incl_scan(v);
       so_[k] = (u32)(wcarry + inc - v);
       wcarry += ((u64)__builtin_amdgcn_readlane((u32)(inc >> 32), 63) << 32) |
@@ -181,6 +193,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
 
   // ---- in-tile stable ranking per wave
   __syncthreads();
+  SORT_STAMP(2);
 #pragma unroll
   for (u32 k = 0; k < kSI; ++k) {
     const u32 j = base + k * 64u + lane;
@@ -200,6 +213,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   }
   __syncthreads();
 
+  SORT_STAMP(3);
   // ---- per digit: wave bases and the tile count, published as a granule
   u32 cnt = 0;
   if (tid < nd) {
@@ -212,6 +226,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
     gran_store(&a.hist_gran[(u64)tile * 256 + tid], a.epoch, cnt);
   }
 
+  SORT_STAMP(4);
   // ---- all-to-all: counts of earlier tiles and digit totals (batched polls)
   u32 before = 0, total = 0;
   if (tid < nd && !sweep_column(a.hist_gran + tid, 256, tiles, tile, a.epoch, &before, &total))
@@ -229,6 +244,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
       }
     }
   }
+  SORT_STAMP(5);
   {
     u32 all_tot;
     const u32 dexcl = block_excl_scan<kSW>(tid < nd ? total : 0u, s_scan, &all_tot);
@@ -236,6 +252,7 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
   }
   __syncthreads();
 
+  SORT_STAMP(6);
   // ---- scatter
   const u32 pre_len = a.first ? s_pre_len : 0u;
 #pragma unroll
@@ -270,6 +287,8 @@ __global__ __launch_bounds__(kST) void sort_pass_kernel(SortPassArgs a) {
       if (j < a.n) a.src_off[j] = pre_len + so_[k];
     }
   }
+  if (a.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  SORT_STAMP(7);
 }
 
 void launch_sort_pass(const SortPassArgs& a, uint32_t tiles, hipStream_t s) {

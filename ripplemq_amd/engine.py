@@ -241,5 +241,5 @@ def parse_records(buf: np.ndarray) -> list[tuple[int, int, bytes]]:
         ln = int.from_bytes(b[pos + 8:pos + 12], "little")
         crc = int.from_bytes(b[pos + 12:pos + 16], "little")
         out.append((off, crc, b[pos + 16:pos + 16 + ln]))
-        pos += 16 + ((ln + 3) & ~3)
+        pos += 16 + ((ln + 15) & ~15)
     return out

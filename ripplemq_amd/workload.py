@@ -93,8 +93,8 @@ def make_batch(spec: StreamSpec, b: int) -> Batch:
 
 
 def record_bytes(lens: np.ndarray) -> int:
-    """Sum of FORMAT.md record sizes (16-byte header + payload padded to 4)."""
-    return int((16 + ((lens.astype(np.uint64) + 3) & ~np.uint64(3))).sum())
+    """Sum of FORMAT.md record sizes (16-byte header + payload padded to 16)."""
+    return int((16 + ((lens.astype(np.uint64) + 15) & ~np.uint64(15))).sum())
 
 
 # BASELINE.json configs[1..4] as stream specs (configs[0] is the Java docker plumbing run).

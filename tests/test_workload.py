@@ -31,5 +31,5 @@ def test_zipf_skew():
 def test_sizes_and_record_bytes():
     b = make_batch(StreamSpec(4, 5000, "uniform", size=(64, 16384)), 0)
     assert b.lens.min() >= 64 and b.lens.max() <= 16384
-    assert record_bytes(np.array([100, 1, 0])) == 116 + 20 + 16
+    assert record_bytes(np.array([100, 1, 0])) == 128 + 32 + 16
     assert b.payload.size == int(b.lens.sum())

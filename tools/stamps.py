@@ -25,6 +25,26 @@ def main(path):
           f"p90 {np.percentile(e, 90):7.2f}  max {e.max():7.2f} us")
 
 
+
+
+SORT_NAMES = ["loads", "first-pass byte scan", "ranking", "hist publish", "digit sweep",
+              "byte sums + block scan", "scatter"]
+
+
+def main_sort(path):
+    a = np.loadtxt(path, delimiter=",", skiprows=1, dtype=np.int64)
+    base = a[:, 2:].min()
+    for k in sorted(set(a[:, 0].tolist())):
+        r = a[a[:, 0] == k]
+        t = (r[:, 2:] - base).astype(np.float64) * 10e-3
+        print(f"{path} pass {k}: tiles={len(r)} start min {t[:, 0].min():.2f} max {t[:, 0].max():.2f}  "
+              f"end max {t[:, 7].max():.2f} us")
+        for q in range(7):
+            d = t[:, q + 1] - t[:, q]
+            print(f"  {SORT_NAMES[q]:>24s}: p10 {np.percentile(d, 10):7.2f}  p50 {np.percentile(d, 50):7.2f}  "
+                  f"p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f} us")
+
+
 if __name__ == "__main__":
     for p in sys.argv[1:]:
-        main(p)
+        (main_sort if p.endswith(".sort.csv") else main)(p)
