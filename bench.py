@@ -54,7 +54,8 @@ def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float) -> dict:
         while t_cpu < budget_s and nb < 400:
             b = batches[nb % len(batches)]
             t0 = time.perf_counter()
-            ora.append(b.pidx, b.lens, b.payload)
+            _, st = ora.append(b.pidx, b.lens, b.payload)
+            assert st["appended"] == b.n, st
             t_cpu += time.perf_counter() - t0
             recs += b.n
             nb += 1
@@ -71,7 +72,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
-    ap.add_argument("--segment-mb", type=int, default=8)
+    ap.add_argument("--segment-mb", type=int, default=16,
+                    help="ring bytes per (replica, partition); a 64k x 128 B batch needs > 8 MiB")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -128,6 +130,8 @@ def main() -> None:
     barrier()
     elapsed = time.perf_counter() - t0
     st = eng.wait(last) if last else {}
+    if st and st.get("appended") != spec.records:
+        raise SystemExit(f"bench: last batch not fully appended ({st}); the measurement would be void")
     n_app, app_ms = eng.profile_query(0)
     n_sort, sort_ms = eng.profile_query(1)
     eng.profile(False)

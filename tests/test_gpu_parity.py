@@ -146,22 +146,25 @@ def test_read_then_commit_consume_loop(oracle_mod):
 
 def test_config_B_full_batches(oracle_mod):
     # BASELINE configs[2] at full size: 4096 partitions, Zipf s=1.1, 64k x 100 B, RF=3
-    cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 23,
+    # (16 MiB rings: a 64k x 128 B batch is exactly 8 MiB, over the 8 MiB - interval batch limit)
+    cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,
                          index_interval=1024, max_batch_records=65536)
     with dev, ora:
         spec = StreamSpec(4096, 65536, "zipf", size=100, config_index=2)
         ops = [("append", make_batch(spec, b)) for b in range(3)]
-        run_ops(dev, ora, cfg, ops, check=False)
+        log = run_ops(dev, ora, cfg, ops, check=False)
+        assert all(st["appended"] == 65536 for _, st in log), log
         hot = np.argsort([-ora.state(p)["log_end_offset"] for p in range(4096)])
         compare_state(dev, ora, cfg, parts=list(hot[:64]) + list(range(0, 4096, 97)))
 
 
 def test_config_A_full_batches(oracle_mod):
-    cfg, dev, ora = pair(oracle_mod, num_partitions=256, replication_factor=3, segment_bytes=1 << 23,
+    cfg, dev, ora = pair(oracle_mod, num_partitions=256, replication_factor=3, segment_bytes=1 << 24,
                          index_interval=1024, max_batch_records=65536)
     with dev, ora:
         spec = StreamSpec(256, 65536, "rr", size=100, config_index=1)
-        run_ops(dev, ora, cfg, [("append", make_batch(spec, b)) for b in range(3)], check=False)
+        log = run_ops(dev, ora, cfg, [("append", make_batch(spec, b)) for b in range(3)], check=False)
+        assert all(st["appended"] == 65536 for _, st in log), log
         compare_state(dev, ora, cfg)
 
 
