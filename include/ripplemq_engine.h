@@ -71,7 +71,7 @@ enum {
 enum { RMQ_MEM_HOST = 0, RMQ_MEM_DEVICE = 1 };
 
 typedef struct rmq_config {
-  uint32_t num_partitions;     /* P: dense pidx in [0, P) */
+  uint32_t num_partitions;     /* P: dense pidx in [0, P), P <= 65536 per engine */
   uint32_t replication_factor; /* RF in [1, RMQ_MAX_RF]; quorum = RF/2 + 1 */
   uint64_t segment_bytes;      /* ring bytes per (replica, partition) log; multiple of index_interval */
   uint32_t index_interval;     /* sparse offset-index interval in bytes; power of two in [64, 1<<20] */
@@ -132,7 +132,8 @@ typedef struct rmq_append_stats {
   uint32_t rejected_not_leader;
   uint32_t rejected_no_partition;
   uint32_t rejected_no_space;  /* whole batch rejected: sum of record sizes > segment - interval */
-  uint32_t reserved;
+  uint32_t rejected_invalid;   /* device batches only: whole batch rejected, a payload range lies
+                                  outside payload_bytes (host batches get RMQ_EINVAL instead) */
 } rmq_append_stats;
 
 typedef struct rmq_engine rmq_engine;
@@ -160,7 +161,10 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
    rmq_poll_commit(ticket) returns RMQ_OK. out_offsets (same memory kind as the batch) gets the
    offset of each record, or RMQ_OFFSET_NONE if it was rejected (not leader / unknown pidx).
    If the batch's total record bytes (sum of 16 + align16(len)) exceed segment_bytes -
-   index_interval, no record is appended (rmq_ticket_stats reports rejected_no_space). */
+   index_interval, no record is appended (rmq_ticket_stats reports rejected_no_space).
+   Each call issues one kernel launch that also advances the two batches submitted before it;
+   a batch is applied by the second launch after its own, or when rmq_poll_commit /
+   rmq_ticket_stats / rmq_sync / any control call flushes the pipeline. */
 int rmq_append(rmq_engine* e, const rmq_batch* batch, uint64_t* out_offsets, uint64_t* ticket);
 
 /* External replica acks (followers on other ranks): match[slot] = max(match[slot],
@@ -201,7 +205,8 @@ int rmq_read_consumer_offsets(rmq_engine* e, uint32_t pidx, uint64_t* out /* max
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out);
 int rmq_device_free(rmq_engine* e, void* p);
 int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int kind /*0 h2d,1 d2h,2 d2d*/);
-/* Kernel timing with HIP events on the engine's own streams. kernel: 0 append, 1 sort pass,
+/* Kernel timing with HIP events on the engine's stream. enable = N > 0 brackets every N-th
+   pipeline launch with an event pair (0 = off). kernel: 0 pipeline launch, 1 unused,
    2 commit, 3 fetch-resolve, 4 fetch-gather. */
 int rmq_profile_enable(rmq_engine* e, int enable);
 int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* total_ms);

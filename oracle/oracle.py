@@ -115,7 +115,7 @@ class OracleEngine:
                                 _p(payload) if payload.size else None, payload.size, _p(out), C.byref(st))
         if rc:
             raise EngineError(rc, "oracle")
-        return out, {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_ if f != "reserved"}
+        return out, {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_}
 
     def ack(self, pidx, slot, match):
         pidx = np.ascontiguousarray(pidx, np.uint32)

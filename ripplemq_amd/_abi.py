@@ -13,7 +13,7 @@ import re
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
-LIB_PATH = os.path.join(HERE, "libripplemq_engine.so")
+LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
 RMQ_ABI_VERSION = 1
 RMQ_MAX_RF = 8
@@ -84,7 +84,7 @@ class RmqPartitionState(C.Structure):
 class RmqAppendStats(C.Structure):
     _fields_ = [
         ("records", u32), ("appended", u32), ("rejected_not_leader", u32),
-        ("rejected_no_partition", u32), ("rejected_no_space", u32), ("reserved", u32),
+        ("rejected_no_partition", u32), ("rejected_no_space", u32), ("rejected_invalid", u32),
     ]
 
 

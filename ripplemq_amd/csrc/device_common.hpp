@@ -26,7 +26,9 @@ constexpr u32 kCrcPow8 = 520;         // pow8[n] = x^(8n) mod P for n < kCrcPow8
 // Device constants: CRC tables and GF(2) shift constants, filled by the host at engine creation.
 struct CrcConsts {
   u32 table[8][256];   // slicing-by-8: table[k][b] = CRC register after byte b then k zero bytes
+  u32 zshift[3][4][256];  // zshift[k][i][b] = (b << 8i) * x^(8 * 16 * 2^k): register shift past 16<<k zero bytes
   u32 shift_pow2[32];  // shift_pow2[j] = x^(8 * 2^j) mod P (reflected): "append 2^j zero bytes"
+  u32 inv_pad[16];     // inv_pad[n] = x^(-8n) mod P: "remove n trailing zero bytes"
   u32 pow8[kCrcPow8];  // pow8[n] = x^(8n) mod P: "append n zero bytes"
 };
 
@@ -68,6 +70,11 @@ __device__ __forceinline__ u32 crc_step8(const u32 (*t)[256], u32 c, u32 lo, u32
   lo ^= c;
   return t[7][lo & 0xFF] ^ t[6][(lo >> 8) & 0xFF] ^ t[5][(lo >> 16) & 0xFF] ^ t[4][lo >> 24] ^
          t[3][hi & 0xFF] ^ t[2][(hi >> 8) & 0xFF] ^ t[1][(hi >> 16) & 0xFF] ^ t[0][hi >> 24];
+}
+
+// Register shift past 16 << k zero bytes (k = 0, 1, 2) by a 4 x 256 table (linearity in the register).
+__device__ __forceinline__ u32 crc_zshift(const u32 (*z)[256], u32 c) {
+  return z[0][c & 0xFF] ^ z[1][(c >> 8) & 0xFF] ^ z[2][(c >> 16) & 0xFF] ^ z[3][c >> 24];
 }
 
 __device__ __forceinline__ u32 crc_step1(const u32 (*t)[256], u32 c, u32 byte) {

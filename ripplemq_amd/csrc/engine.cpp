@@ -1,11 +1,14 @@
 // engine.cpp — host side of the C-ABI (include/ripplemq_engine.h).
 //
 // Owns all device memory of one engine (one HIP device): per-(replica, partition) ring segments,
-// the sparse offset index, per-partition Raft state and consumer offsets. Orchestrates, per
-// append batch, the batch-local partition sort on a prep stream and the fused append kernel on
-// the main stream, with `pipeline_depth` batches in flight so the sort of batch k+1 overlaps the
-// append of batch k. Control-plane calls (leadership, replicas, acks, consumer offsets, fetch)
-// drain both streams first and run synchronously: they are rare next to the append stream.
+// the sparse offset index, per-partition Raft state and consumer offsets. Each rmq_append issues
+// exactly ONE kernel launch (pipeline.hip): it ranks the new batch (stage 1), scans the previous
+// batch (stage 2) and applies the one before (stage 3). A batch is therefore complete two launches
+// after its own; rmq_poll_commit / rmq_sync / any control call flush the pipeline with up to two
+// launches that carry only stages 2-3. No host synchronisation and no HIP events sit on the
+// append path: launch k reports launch k-1 complete through a host-visible word, and the tail is
+// read with hipStreamQuery. Control-plane calls (leadership, replicas, acks, consumer offsets,
+// fetch) flush and drain first and run synchronously: they are rare next to the append stream.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,31 +28,30 @@ using namespace rmq;
 
 namespace {
 
-constexpr uint32_t kStatsRing = 64;                               // tickets whose stats stay readable
-constexpr uint32_t kMaxSortTiles = 128;                           // all sort tiles must be co-resident
-constexpr uint32_t kMaxBatchRecords = kMaxSortTiles * kSortTile;  // 262144
+constexpr uint32_t kStatsRing = 64;                                // tickets whose stats stay readable
+constexpr uint32_t kMaxBatchRecords = kMaxTiles * kTileRecs;       // 262144
+constexpr uint32_t kSets = 3;                                      // pipeline scratch sets
 
 struct EvPair {
   hipEvent_t a = nullptr, b = nullptr;
 };
 
-struct Slot {
-  uint32_t* d_pidx = nullptr;  // staging for host batches
+// Device staging of host-memory batches.
+struct Staging {
+  uint32_t* d_pidx = nullptr;
   uint32_t* d_len = nullptr;
   uint64_t* d_poff = nullptr;
   uint8_t* d_payload = nullptr;
   uint64_t* d_out = nullptr;
-  uint32_t* keys[2] = {nullptr, nullptr};  // intermediate radix passes (P > 4096 only)
-  uint32_t* vals[2] = {nullptr, nullptr};
-  uint32_t* src_off = nullptr;             // packed payload offsets (multi-pass only)
-  uint4* slots = nullptr;                  // sorted slot records for the append kernel
-  uint64_t* batch_info = nullptr;
-  uint64_t* hist_gran = nullptr;           // sort tile histograms [tiles][256]
-  uint64_t* len_gran = nullptr;
-  uint64_t* rb_gran = nullptr;
-  hipEvent_t prep_done = nullptr, append_done = nullptr;
+  uint64_t ticket = 0;  // last ticket that used it
+};
+
+// A batch inside the launch pipeline.
+struct InFlight {
   uint64_t ticket = 0;
-  bool used = false;
+  PipeBatch b{};
+  uint32_t set = 0;             // scratch set = ticket % kSets
+  uint64_t* host_out = nullptr;  // host batches: caller's out_offsets
 };
 
 }  // namespace
@@ -61,24 +63,33 @@ struct rmq_engine {
   uint32_t cu_count = 0;
   char dev_name[256] = {0};
   hipStream_t main_s = nullptr;
-  hipStream_t prep[2] = {nullptr, nullptr};  // batch sorts alternate between two prep streams
-  DevState st{};
+  DevState st{};            // leo/used/start_off/start_pos point at sets[applied & 1]
+  StateSet sets[2]{};
+  uint64_t applied = 0;     // stage-3 launches issued
   CrcConsts* d_crc = nullptr;
   uint64_t* d_winner = nullptr;
   uint32_t* d_err = nullptr;
-  uint4* d_tile_stats = nullptr;  // [kStatsRing][max append tiles]
-  uint32_t max_app_tiles = 0;
-  uint64_t* d_lb_cnt = nullptr;
-  uint64_t* d_lb_bytes = nullptr;
+  uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
+  uint32_t max_tasks = 0;
+  uint32_t max_tiles = 0;
+  uint32_t key_passes = 0;
   uint32_t epoch = 0;
-  std::vector<Slot> slots;
+  PipeScratch scratch[kSets]{};
+  std::vector<Staging> staging;
+  // pipeline
+  bool has1 = false, has2 = false;  // batch ranked (needs stage 2) / scanned (needs stage 3)
+  InFlight st1, st2;
+  uint64_t launch_seq = 0;
+  uint64_t* done_host = nullptr;     // pinned: launch k-1 complete, written by launch k
+  uint64_t* done_dev = nullptr;
   uint64_t last_ticket = 0;
-  std::vector<uint32_t> ticket_n;  // [kStatsRing]
+  uint64_t last_nonempty = 0;
+  std::vector<uint32_t> ticket_n;        // [kStatsRing]
+  std::vector<uint64_t> ticket_launch;   // [kStatsRing] launch applying the ticket (0: not yet)
+  std::vector<uint64_t> ticket_dep;      // [kStatsRing] empty batches: the ticket they wait for
   // host mirrors of control state
   std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
   std::vector<uint64_t> term;
-  // sort plan
-  uint32_t passes = 1, pass_shift[3] = {0, 0, 0}, pass_bits[3] = {1, 0, 0}, pass_ndig[3] = {1, 0, 0};
   // fetch scratch
   uint32_t* d_req = nullptr;
   uint64_t* d_res = nullptr;
@@ -91,21 +102,16 @@ struct rmq_engine {
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;
   uint32_t ctl_cap = 0;
-  // RMQ_DEBUG_SKIP bit 0: skip the sort launch, bit 1: skip the append launch, bit 2: run each
-  // batch's sort after the previous append (no overlap; to time the kernels alone)
-  uint32_t debug_skip = 0;
-  uint32_t debug_flags = 0;   // RMQ_DEBUG_FLAGS -> AppendArgs.debug
-  uint32_t spin_limit = 1u << 22;
-  hipEvent_t last_append_done = nullptr;
-  uint64_t* d_stamps = nullptr;     // RMQ_STAMPS=<csv path>: append phase stamps of the last batch
-  uint64_t* d_sort_stamps = nullptr;  // [pass][tiles][8] sort phase stamps of the last batch
-  uint32_t sort_stamps_tiles = 0, sort_stamps_passes = 0;
-  const char* stamps_path = nullptr;
-  uint32_t stamps_tiles = 0;
-  // profiling
-  bool profile = false;
+  // profiling: HIP event pairs around every `profile`-th pipeline launch (0 = off)
+  uint32_t profile = 0;
+  uint64_t prof_count = 0;
   std::vector<EvPair> prof[5];
   std::vector<hipEvent_t> ev_pool;
+  // diagnostics: RMQ_STAMPS=<csv> records per-wave phase stamps of launch RMQ_STAMPS_AT (default 100)
+  const char* stamps_path = nullptr;
+  uint64_t stamps_at = 100;
+  uint64_t* d_stamps = nullptr;
+  uint32_t stamps_wg[3] = {0, 0, 0};
 };
 
 namespace {
@@ -144,6 +150,42 @@ uint32_t host_mulmod(uint32_t a, uint32_t b) {
   return p;
 }
 
+// Inverse of a in GF(2)[x] mod P (reflected), by Gaussian elimination of y -> y * a.
+uint32_t host_inverse(uint32_t a) {
+  uint32_t col[32];
+  for (int k = 0; k < 32; ++k) col[k] = host_mulmod(1u << k, a);  // image of basis vector bit k
+  // solve sum_k y_k col[k] = one (x^0 = 0x80000000): rows = output bits
+  uint32_t rows[32];  // rows[b]: bit k = bit b of col[k]; bit 32 handled separately
+  uint32_t rhs = 0;
+  for (int bb = 0; bb < 32; ++bb) {
+    rows[bb] = 0;
+    for (int k = 0; k < 32; ++k) rows[bb] |= ((col[k] >> bb) & 1u) << k;
+    rhs |= ((0x80000000u >> bb) & 1u) << bb;
+  }
+  int r = 0;
+  int piv[32];
+  for (int k = 0; k < 32 && r < 32; ++k) {
+    int sel = -1;
+    for (int bb = r; bb < 32; ++bb)
+      if ((rows[bb] >> k) & 1u) { sel = bb; break; }
+    if (sel < 0) continue;
+    std::swap(rows[sel], rows[r]);
+    const uint32_t t = (rhs >> sel) & 1u, u = (rhs >> r) & 1u;
+    rhs = (rhs & ~((1u << sel) | (1u << r))) | (u << sel) | (t << r);
+    for (int bb = 0; bb < 32; ++bb)
+      if (bb != r && ((rows[bb] >> k) & 1u)) {
+        rows[bb] ^= rows[r];
+        rhs ^= ((rhs >> r) & 1u) << bb;
+      }
+    piv[r] = k;
+    ++r;
+  }
+  uint32_t y = 0;
+  for (int q = 0; q < r; ++q)
+    if ((rhs >> q) & 1u) y |= 1u << piv[q];
+  return y;
+}
+
 void build_crc_consts(CrcConsts* c) {
   for (uint32_t b = 0; b < 256; ++b) {
     uint32_t x = b;
@@ -159,6 +201,10 @@ void build_crc_consts(CrcConsts* c) {
   for (int j = 0; j < 32; ++j) c->shift_pow2[j] = x2n[j + 3];  // x^(8 * 2^j)
   c->pow8[0] = 0x80000000u;                                     // x^0
   for (uint32_t n = 1; n < kCrcPow8; ++n) c->pow8[n] = host_mulmod(c->pow8[n - 1], x2n[3]);
+  for (uint32_t k = 0; k < 3; ++k)  // shift past 16 << k zero bytes = multiply by x^(2^(7+k))
+    for (uint32_t i = 0; i < 4; ++i)
+      for (uint32_t b = 0; b < 256; ++b) c->zshift[k][i][b] = host_mulmod(b << (8 * i), x2n[7 + k]);
+  for (uint32_t n = 0; n < 16; ++n) c->inv_pad[n] = n ? host_inverse(c->pow8[n]) : 0x80000000u;
 }
 
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
@@ -173,17 +219,10 @@ int check_err(rmq_engine* e) {
   uint32_t err = 0;
   HIP_TRY(hipMemcpy(&err, e->d_err, 4, hipMemcpyDeviceToHost));
   if (err) {
-    std::fprintf(stderr, "ripplemq: device hand-off timeout (err=%u)\n", err);
+    std::fprintf(stderr, "ripplemq: device error word %u\n", err);
     return RMQ_EDEVICE;
   }
   return RMQ_OK;
-}
-
-int drain(rmq_engine* e) {
-  HIP_TRY(hipStreamSynchronize(e->prep[0]));
-  HIP_TRY(hipStreamSynchronize(e->prep[1]));
-  HIP_TRY(hipStreamSynchronize(e->main_s));
-  return check_err(e);
 }
 
 hipEvent_t pool_event(rmq_engine* e) {
@@ -195,6 +234,116 @@ hipEvent_t pool_event(rmq_engine* e) {
   hipEvent_t ev = nullptr;
   if (hipEventCreate(&ev) != hipSuccess) return nullptr;
   return ev;
+}
+
+// One pipeline launch: stage 1 on `s1`, stage 2 on `s2`, stage 3 on `s3` (each may be null).
+int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const InFlight* s3) {
+  PipeArgs a{};
+  const uint32_t P = e->cfg.num_partitions;
+  const StateSet cur = e->sets[e->applied & 1u], nxt = e->sets[(e->applied + 1) & 1u];
+  a.st = e->st;
+  a.cur = cur;
+  a.nxt = nxt;
+  a.key_passes = e->key_passes;
+  a.nospace_limit = e->cfg.segment_bytes - e->cfg.index_interval;
+  a.crc = e->d_crc;
+  a.done_word = e->done_dev;
+  if (s1) {
+    a.b1 = s1->b;
+    a.s1 = e->scratch[s1->set];
+    a.wg1 = s1->b.tiles;
+  }
+  if (s2) {
+    a.b2 = s2->b;
+    a.s2 = e->scratch[s2->set];
+    a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + kPipeThreads - 1) / kPipeThreads, 2u * e->cu_count));
+  }
+  if (s3) {
+    a.b3 = s3->b;
+    a.s3 = e->scratch[s3->set];
+    const uint32_t tasks = (s3->b.n + kTaskRecs - 1) / kTaskRecs;
+    const uint32_t wpb = kPipeThreads / 64;
+    const uint32_t want = std::max((tasks + wpb - 1) / wpb, (P + kPipeThreads - 1) / kPipeThreads);
+    // fill the chip next to the stage-1/2 workgroups of this launch (resident workgroups per CU
+    // from the kernel's launch bounds)
+    const uint32_t slots = pipeline_wgs_per_cu() * e->cu_count;
+    const uint32_t room = slots > a.wg1 + a.wg2 + e->cu_count ? slots - a.wg1 - a.wg2 : e->cu_count;
+    a.wg3 = std::max<uint32_t>(1u, std::min<uint32_t>(want, room));
+    a.stats3 = e->d_stats + (size_t)(s3->ticket % kStatsRing) * e->max_tasks;
+  }
+  a.launch_seq = ++e->launch_seq;
+  if (e->d_stamps && a.launch_seq == e->stamps_at) {
+    a.stamps = e->d_stamps;
+    e->stamps_wg[0] = a.wg1;
+    e->stamps_wg[1] = a.wg2;
+    e->stamps_wg[2] = a.wg3;
+  }
+  const bool prof = e->profile && (e->prof_count++ % e->profile) == 0;
+  EvPair ev;
+  if (prof) {
+    ev.a = pool_event(e);
+    ev.b = pool_event(e);
+    HIP_TRY(hipEventRecord(ev.a, e->main_s));
+  }
+  launch_pipeline(a, e->main_s);
+  HIP_TRY(hipGetLastError());
+  if (prof) {
+    HIP_TRY(hipEventRecord(ev.b, e->main_s));
+    e->prof[0].push_back(ev);
+  }
+  if (s3) {
+    e->applied++;
+    e->st.leo = nxt.leo;
+    e->st.used = nxt.used;
+    e->st.start_off = nxt.start_off;
+    e->st.start_pos = nxt.start_pos;
+    e->ticket_launch[s3->ticket % kStatsRing] = e->launch_seq;
+    if (s3->host_out && s3->b.n)
+      HIP_TRY(hipMemcpyAsync(s3->host_out, s3->b.out_offsets, s3->b.n * 8ull, hipMemcpyDeviceToHost, e->main_s));
+  }
+  return RMQ_OK;
+}
+
+// Push everything in the pipeline through stage 3 (at most two launches).
+int flush(rmq_engine* e) {
+  while (e->has1 || e->has2) {
+    int rc = launch_stages(e, nullptr, e->has1 ? &e->st1 : nullptr, e->has2 ? &e->st2 : nullptr);
+    if (rc) return rc;
+    e->has2 = e->has1;
+    e->st2 = e->st1;
+    e->has1 = false;
+  }
+  return RMQ_OK;
+}
+
+int drain(rmq_engine* e) {
+  int rc = flush(e);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->main_s));
+  return check_err(e);
+}
+
+// Has the launch with sequence number L completed?
+bool launch_done(rmq_engine* e, uint64_t L) {
+  if (L <= __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE)) return true;
+  return hipStreamQuery(e->main_s) == hipSuccess;
+}
+
+// The ticket whose completion `t` stands for (empty batches wait for the last non-empty one).
+uint64_t resolve_ticket(rmq_engine* e, uint64_t t) {
+  return e->ticket_n[t % kStatsRing] ? t : e->ticket_dep[t % kStatsRing];
+}
+
+// Block until ticket t (non-empty, issued) is applied and complete.
+int wait_ticket(rmq_engine* e, uint64_t t) {
+  if (!t) return RMQ_OK;
+  if (!e->ticket_launch[t % kStatsRing]) {
+    int rc = flush(e);
+    if (rc) return rc;
+  }
+  const uint64_t L = e->ticket_launch[t % kStatsRing];
+  if (!launch_done(e, L)) HIP_TRY(hipStreamSynchronize(e->main_s));
+  return RMQ_OK;
 }
 
 int ensure_ctl(rmq_engine* e, uint32_t n) {
@@ -212,61 +361,54 @@ int ensure_ctl(rmq_engine* e, uint32_t n) {
 }
 
 void dump_stamps(rmq_engine* e) {
-  if (!e->stamps_path || !e->d_stamps || !e->stamps_tiles) return;
-  std::vector<uint64_t> h((size_t)e->stamps_tiles * 8);
+  const uint32_t nwg = e->stamps_wg[0] + e->stamps_wg[1] + e->stamps_wg[2];
+  if (!e->stamps_path || !e->d_stamps || !nwg) return;
+  std::vector<uint64_t> h((size_t)nwg * 64);
   if (hipMemcpy(h.data(), e->d_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
   FILE* f = std::fopen(e->stamps_path, "w");
   if (!f) return;
-  std::fprintf(f, "tile,t0,t1,t2,t3,t4,t5,t6,t7\n");
-  for (uint32_t t = 0; t < e->stamps_tiles; ++t) {
-    std::fprintf(f, "%u", t);
-    for (int k = 0; k < 8; ++k) std::fprintf(f, ",%llu", (unsigned long long)h[(size_t)t * 8 + k]);
-    std::fprintf(f, "\n");
-  }
-  std::fclose(f);
-  if (!e->d_sort_stamps || !e->sort_stamps_tiles) return;
-  std::vector<uint64_t> g((size_t)3 * kMaxSortTiles * 8);
-  if (hipMemcpy(g.data(), e->d_sort_stamps, g.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-  std::string sp = std::string(e->stamps_path) + ".sort.csv";
-  f = std::fopen(sp.c_str(), "w");
-  if (!f) return;
-  std::fprintf(f, "pass,tile,t0,t1,t2,t3,t4,t5,t6,t7\n");
-  for (uint32_t k = 0; k < e->sort_stamps_passes; ++k)
-    for (uint32_t t = 0; t < e->sort_stamps_tiles; ++t) {
-      std::fprintf(f, "%u,%u", k, t);
-      for (int q = 0; q < 8; ++q)
-        std::fprintf(f, ",%llu", (unsigned long long)g[((size_t)k * kMaxSortTiles + t) * 8 + q]);
+  std::fprintf(f, "wg,wave,stage,t0,t1,t2,t3,t4,t5,t6,t7\n");
+  for (uint32_t g = 0; g < nwg; ++g) {
+    const int stage = g < e->stamps_wg[0] ? 1 : g < e->stamps_wg[0] + e->stamps_wg[1] ? 2 : 3;
+    for (uint32_t w = 0; w < 8; ++w) {
+      std::fprintf(f, "%u,%u,%d", g, w, stage);
+      for (int k = 0; k < 8; ++k) std::fprintf(f, ",%llu", (unsigned long long)h[((size_t)g * 8 + w) * 8 + k]);
       std::fprintf(f, "\n");
     }
+  }
   std::fclose(f);
 }
 
 void free_engine(rmq_engine* e) {
   if (!e) return;
   hipSetDevice(e->device);
-  if (e->main_s) hipStreamSynchronize(e->main_s);
-  for (hipStream_t ps : e->prep)
-    if (ps) hipStreamSynchronize(ps);
-  dump_stamps(e);
-  for (hipStream_t ps : e->prep)
-    if (ps) hipStreamSynchronize(ps);
-  DevState& s = e->st;
-  void* bufs[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match,
-                  s.is_leader, s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner,
-                  e->d_err, e->d_tile_stats,
-                  e->d_lb_cnt, e->d_lb_bytes, e->d_req, e->d_res, e->d_aux,
-                  e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_sort_stamps};
-  for (void* b : bufs)
-    if (b) hipFree(b);
-  for (Slot& sl : e->slots) {
-    void* sb[] = {sl.d_pidx, sl.d_len, sl.d_poff, sl.d_payload, sl.d_out, sl.keys[0], sl.keys[1],
-                  sl.vals[0], sl.vals[1], sl.src_off, sl.slots, sl.batch_info, sl.hist_gran,
-                  sl.len_gran, sl.rb_gran};
-    for (void* b : sb)
-      if (b) hipFree(b);
-    if (sl.prep_done) hipEventDestroy(sl.prep_done);
-    if (sl.append_done) hipEventDestroy(sl.append_done);
+  if (e->main_s) {
+    flush(e);  // every submitted batch is applied before the memory goes away
+    hipStreamSynchronize(e->main_s);
+    dump_stamps(e);
   }
+  DevState& s = e->st;
+  std::vector<void*> bufs = {s.commit, s.hw, s.term_start, s.match, s.is_leader, s.local_mask, s.index,
+                             s.logs, s.cons, e->d_crc, e->d_winner, e->d_err, e->d_stats, e->d_req,
+                             e->d_res, e->d_aux, e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64,
+                             e->d_stamps};
+  for (const StateSet& z : e->sets) {
+    bufs.push_back(z.leo);
+    bufs.push_back(z.used);
+    bufs.push_back(z.start_off);
+    bufs.push_back(z.start_pos);
+  }
+  for (const PipeScratch& x : e->scratch) {
+    void* xs[] = {x.hist, x.excl, x.totals, x.crank, x.pre, x.tsum, x.tile_base, x.binfo};
+    for (void* p : xs) bufs.push_back(p);
+  }
+  for (const Staging& sg : e->staging) {
+    void* xs[] = {sg.d_pidx, sg.d_len, sg.d_poff, sg.d_payload, sg.d_out};
+    for (void* p : xs) bufs.push_back(p);
+  }
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (e->done_host) hipHostFree(e->done_host);
   for (auto& v : e->prof)
     for (EvPair& p : v) {
       if (p.a) hipEventDestroy(p.a);
@@ -274,14 +416,12 @@ void free_engine(rmq_engine* e) {
     }
   for (hipEvent_t ev : e->ev_pool) hipEventDestroy(ev);
   if (e->main_s) hipStreamDestroy(e->main_s);
-  for (hipStream_t ps : e->prep)
-    if (ps) hipStreamDestroy(ps);
   delete e;
 }
 
 int validate_cfg(const rmq_config* c) {
   if (!c) return RMQ_EINVAL;
-  if (c->num_partitions == 0 || c->num_partitions > (1u << 24)) return RMQ_EINVAL;
+  if (c->num_partitions == 0 || c->num_partitions > kMaxPartitions) return RMQ_EINVAL;
   if (c->replication_factor == 0 || c->replication_factor > RMQ_MAX_RF) return RMQ_EINVAL;
   if (!is_pow2(c->index_interval) || c->index_interval < 64 || c->index_interval > (1u << 20))
     return RMQ_EINVAL;
@@ -340,11 +480,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (!e) return RMQ_ENOMEM;
   e->cfg = *cfg;
   if (!e->cfg.pipeline_depth) e->cfg.pipeline_depth = 3;
-  if (const char* dbg = std::getenv("RMQ_DEBUG_SKIP")) e->debug_skip = (uint32_t)std::atoi(dbg);
-  if (const char* dbg = std::getenv("RMQ_DEBUG_FLAGS")) e->debug_flags = (uint32_t)std::atoi(dbg);
-  if (const char* dbg = std::getenv("RMQ_SPIN_LIMIT")) e->spin_limit = (uint32_t)std::atoi(dbg);
-  e->stamps_path = std::getenv("RMQ_STAMPS");
   e->device = cfg->device;
+  e->stamps_path = std::getenv("RMQ_STAMPS");
+  if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
     int _r = (x);          \
@@ -360,8 +498,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->cu_count = (uint32_t)prop.multiProcessorCount;
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
-  CREATE_HIP(hipStreamCreateWithFlags(&e->prep[0], hipStreamNonBlocking));
-  CREATE_HIP(hipStreamCreateWithFlags(&e->prep[1], hipStreamNonBlocking));
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
   DevState& s = e->st;
@@ -371,10 +507,16 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   s.seg = cfg->segment_bytes;
   s.interval_log2 = ilog2(cfg->index_interval);
   s.icap = (uint32_t)(cfg->segment_bytes / cfg->index_interval + 2);
-  CREATE_TRY(dalloc(&s.leo, P));
-  CREATE_TRY(dalloc(&s.used, P));
-  CREATE_TRY(dalloc(&s.start_off, P));
-  CREATE_TRY(dalloc(&s.start_pos, P));
+  for (StateSet& z : e->sets) {
+    CREATE_TRY(dalloc(&z.leo, P));
+    CREATE_TRY(dalloc(&z.used, P));
+    CREATE_TRY(dalloc(&z.start_off, P));
+    CREATE_TRY(dalloc(&z.start_pos, P));
+  }
+  s.leo = e->sets[0].leo;
+  s.used = e->sets[0].used;
+  s.start_off = e->sets[0].start_off;
+  s.start_pos = e->sets[0].start_pos;
   CREATE_TRY(dalloc(&s.commit, P));
   CREATE_TRY(dalloc(&s.hw, P));
   CREATE_TRY(dalloc(&s.term_start, P));
@@ -386,11 +528,24 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&e->d_winner, (size_t)P * C));
   CREATE_TRY(dalloc(&e->d_err, 1));
-  const uint32_t max_sort_tiles = (cfg->max_batch_records + kSortTile - 1) / kSortTile;
-  e->max_app_tiles = (cfg->max_batch_records + kAppendTile - 1) / kAppendTile;
-  CREATE_TRY(dalloc(&e->d_tile_stats, (size_t)kStatsRing * e->max_app_tiles));
-  CREATE_TRY(dalloc(&e->d_lb_cnt, e->max_app_tiles));
-  CREATE_TRY(dalloc(&e->d_lb_bytes, e->max_app_tiles));
+  e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
+  e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
+  CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));
+  for (PipeScratch& x : e->scratch) {
+    const size_t TP = (size_t)e->max_tiles * P;
+    CREATE_TRY(dalloc(&x.hist, TP));
+    CREATE_TRY(dalloc(&x.excl, TP));
+    CREATE_TRY(dalloc(&x.totals, P));
+    CREATE_TRY(dalloc(&x.crank, cfg->max_batch_records));
+    CREATE_TRY(dalloc(&x.pre, cfg->max_batch_records));
+    CREATE_TRY(dalloc(&x.tsum, (size_t)e->max_tiles * 4));
+    CREATE_TRY(dalloc(&x.tile_base, e->max_tiles));
+    CREATE_TRY(dalloc(&x.binfo, 4));
+  }
+  if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(4u * e->cu_count + 2u * kMaxTiles) * 64));
+  CREATE_HIP(hipHostMalloc((void**)&e->done_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
+  *e->done_host = 0;
+  CREATE_HIP(hipHostGetDevicePointer((void**)&e->done_dev, e->done_host, 0));
   {
     CrcConsts h;
     build_crc_consts(&h);
@@ -407,35 +562,14 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->ranks.assign((size_t)P * RF, cfg->rank);
   e->term.assign(P, 1ull);
   e->ticket_n.assign(kStatsRing, 0u);
-
-  // radix plan: <= 8-bit digits of the partition id (one pass for P <= 256)
-  uint32_t bits = ilog2((uint64_t)P);  // keys in [0, P-1]
-  if (bits == 0) bits = 1;
-  e->passes = (bits + kSortDigitBits - 1) / kSortDigitBits;
-  const uint32_t dw = (bits + e->passes - 1) / e->passes;
-  for (uint32_t k = 0; k < e->passes; ++k) {
-    e->pass_shift[k] = k * dw;
-    e->pass_bits[k] = std::min(dw, bits - k * dw);
-    e->pass_ndig[k] = k + 1 == e->passes ? ((P - 1) >> e->pass_shift[k]) + 1 : 1u << e->pass_bits[k];
+  e->ticket_launch.assign(kStatsRing, 0ull);
+  e->ticket_dep.assign(kStatsRing, 0ull);
+  {
+    uint32_t bits = 0;
+    while ((1u << bits) < P) ++bits;  // keys in [0, P)
+    e->key_passes = bits == 0 ? 0u : bits <= 8 ? 1u : 2u;
   }
-
-  const uint32_t D = e->cfg.pipeline_depth;
-  e->slots.resize(D);
-  const uint32_t NB = cfg->max_batch_records;
-  for (Slot& sl : e->slots) {
-    if (e->passes > 1) {
-      CREATE_TRY(dalloc(&sl.keys[0], NB));
-      CREATE_TRY(dalloc(&sl.vals[0], NB));
-      CREATE_TRY(dalloc(&sl.src_off, NB));
-    }
-    CREATE_TRY(dalloc(&sl.slots, NB));
-    CREATE_TRY(dalloc(&sl.batch_info, 4));
-    CREATE_TRY(dalloc(&sl.hist_gran, (size_t)max_sort_tiles * 256));
-    CREATE_TRY(dalloc(&sl.len_gran, max_sort_tiles));
-    CREATE_TRY(dalloc(&sl.rb_gran, max_sort_tiles));
-    CREATE_HIP(hipEventCreateWithFlags(&sl.prep_done, hipEventDisableTiming));
-    CREATE_HIP(hipEventCreateWithFlags(&sl.append_done, hipEventDisableTiming));
-  }
+  e->staging.resize(std::max<uint32_t>(e->cfg.pipeline_depth, kSets) + 1);
   CREATE_HIP(hipDeviceSynchronize());
   *out = e;
   return RMQ_OK;
@@ -517,150 +651,57 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   const uint64_t t = ++e->last_ticket;
   *ticket = t;
   e->ticket_n[t % kStatsRing] = n;
-  Slot& sl = e->slots[t % e->slots.size()];
-  hipStream_t prep_s = e->prep[t & 1];
-  if (sl.used) {
-    HIP_TRY(hipEventSynchronize(sl.append_done));  // scratch of ticket t - depth is free again
-  }
-  sl.used = true;
-  sl.ticket = t;
-  if (n == 0) {
-    HIP_TRY(hipEventRecord(sl.append_done, e->main_s));
-    return RMQ_OK;
-  }
+  e->ticket_launch[t % kStatsRing] = 0;
+  e->ticket_dep[t % kStatsRing] = e->last_nonempty;
+  if (n == 0) return RMQ_OK;  // completes with the last non-empty batch before it
+  e->last_nonempty = t;
 
-  const uint32_t* pidx = b->pidx;
-  const uint32_t* len = b->len;
-  const uint64_t* poff = b->payload_off;
-  const uint8_t* payload = b->payload;
-  uint64_t* d_out = out_offsets;
+  InFlight f;
+  f.ticket = t;
+  f.set = (uint32_t)(t % kSets);
+  f.b.pidx = b->pidx;
+  f.b.len = b->len;
+  f.b.poff = b->payload_off;
+  f.b.payload = b->payload;
+  f.b.payload_bytes = b->payload_bytes;
+  f.b.out_offsets = out_offsets;
+  f.b.n = n;
+  f.b.tiles = (n + kTileRecs - 1) / kTileRecs;
   if (b->mem == RMQ_MEM_HOST) {
+    Staging& sg = e->staging[t % e->staging.size()];
+    if (sg.ticket) {  // the batch that used this staging slot must be complete
+      int rc = wait_ticket(e, sg.ticket);
+      if (rc) return rc;
+    }
     const uint32_t NB = e->cfg.max_batch_records;
-    if (!sl.d_pidx) {
-      int rc = dalloc(&sl.d_pidx, NB);
-      if (!rc) rc = dalloc(&sl.d_len, NB);
-      if (!rc) rc = dalloc(&sl.d_poff, NB);
-      if (!rc) rc = dalloc(&sl.d_out, NB);
-      if (!rc) rc = dalloc(&sl.d_payload, e->cfg.max_batch_bytes + 8);
+    if (!sg.d_pidx) {
+      int rc = dalloc(&sg.d_pidx, NB);
+      if (!rc) rc = dalloc(&sg.d_len, NB);
+      if (!rc) rc = dalloc(&sg.d_poff, NB);
+      if (!rc) rc = dalloc(&sg.d_out, NB);
+      if (!rc) rc = dalloc(&sg.d_payload, e->cfg.max_batch_bytes + 32);
       if (rc) return rc;
     }
-    HIP_TRY(hipMemcpyAsync(sl.d_pidx, pidx, n * 4ull, hipMemcpyHostToDevice, prep_s));
-    HIP_TRY(hipMemcpyAsync(sl.d_len, len, n * 4ull, hipMemcpyHostToDevice, prep_s));
-    if (poff) HIP_TRY(hipMemcpyAsync(sl.d_poff, poff, n * 8ull, hipMemcpyHostToDevice, prep_s));
+    sg.ticket = t;
+    HIP_TRY(hipMemcpyAsync(sg.d_pidx, b->pidx, n * 4ull, hipMemcpyHostToDevice, e->main_s));
+    HIP_TRY(hipMemcpyAsync(sg.d_len, b->len, n * 4ull, hipMemcpyHostToDevice, e->main_s));
+    if (b->payload_off)
+      HIP_TRY(hipMemcpyAsync(sg.d_poff, b->payload_off, n * 8ull, hipMemcpyHostToDevice, e->main_s));
     if (b->payload_bytes)
-      HIP_TRY(hipMemcpyAsync(sl.d_payload, payload, b->payload_bytes, hipMemcpyHostToDevice, prep_s));
-    pidx = sl.d_pidx;
-    len = sl.d_len;
-    poff = poff ? sl.d_poff : nullptr;
-    payload = sl.d_payload;
-    d_out = sl.d_out;
+      HIP_TRY(hipMemcpyAsync(sg.d_payload, b->payload, b->payload_bytes, hipMemcpyHostToDevice, e->main_s));
+    f.b.pidx = sg.d_pidx;
+    f.b.len = sg.d_len;
+    f.b.poff = b->payload_off ? sg.d_poff : nullptr;
+    f.b.payload = sg.d_payload;
+    f.b.out_offsets = sg.d_out;
+    f.host_out = out_offsets;
   }
-
-  if ((e->debug_skip & 4u) && e->last_append_done)
-    HIP_TRY(hipStreamWaitEvent(prep_s, e->last_append_done, 0));
-  // ---- prep stream: stable partition-major sort of the batch into slot records
-  const uint32_t sort_tiles = (n + kSortTile - 1) / kSortTile;
-  hipEvent_t ps0 = nullptr, ps1 = nullptr;
-  if (e->profile) {
-    ps0 = pool_event(e);
-    ps1 = pool_event(e);
-    HIP_TRY(hipEventRecord(ps0, prep_s));
-  }
-  const uint32_t* kin = pidx;
-  const uint32_t* vin = nullptr;
-  for (uint32_t k = 0; k < e->passes; ++k) {
-    SortPassArgs a{};
-    a.keys_in = kin;
-    a.pidx_raw = pidx;
-    a.vals_in = vin;
-    a.keys_out = sl.keys[0];
-    a.vals_out = sl.vals[0];
-    a.slots = sl.slots;
-    a.len = len;
-    a.payload_off = poff;
-    a.src_off = poff ? nullptr : sl.src_off;
-    a.batch_info = sl.batch_info;
-    a.hist_gran = sl.hist_gran;
-    a.len_gran = sl.len_gran;
-    a.rb_gran = sl.rb_gran;
-    a.n = n;
-    a.tiles = sort_tiles;
-    a.shift = e->pass_shift[k];
-    a.bits = e->pass_bits[k];
-    a.ndig = e->pass_ndig[k];
-    a.P = e->cfg.num_partitions;
-    a.first = k == 0;
-    a.last = k + 1 == e->passes;
-    a.epoch = ++e->epoch;
-    a.err = e->d_err;
-    if (e->stamps_path) {
-      if (!e->d_sort_stamps) {
-        int rc = dalloc(&e->d_sort_stamps, (size_t)3 * kMaxSortTiles * 8);
-        if (rc) return rc;
-      }
-      a.stamps = e->d_sort_stamps + (size_t)k * kMaxSortTiles * 8;
-      e->sort_stamps_tiles = sort_tiles;
-      e->sort_stamps_passes = e->passes;
-    }
-    if (!(e->debug_skip & 1u)) launch_sort_pass(a, sort_tiles, prep_s);
-    kin = sl.keys[0];
-    vin = sl.vals[0];
-  }
-  HIP_TRY(hipGetLastError());
-  if (e->profile) {
-    HIP_TRY(hipEventRecord(ps1, prep_s));
-    e->prof[1].push_back({ps0, ps1});
-  }
-  HIP_TRY(hipEventRecord(sl.prep_done, prep_s));
-
-  // ---- main stream: fused append
-  HIP_TRY(hipStreamWaitEvent(e->main_s, sl.prep_done, 0));
-  AppendArgs a{};
-  a.st = e->st;
-  a.slots = sl.slots;
-  a.payload = payload;
-  a.payload_bytes = b->payload_bytes;
-  a.out_offsets = d_out;
-  a.batch_info = sl.batch_info;
-  a.tile_stats = e->d_tile_stats + (size_t)(t % kStatsRing) * e->max_app_tiles;
-  a.lb_cnt = e->d_lb_cnt;
-  a.lb_bytes = e->d_lb_bytes;
-  a.n = n;
-  a.tiles = (n + kAppendTile - 1) / kAppendTile;
-  a.epoch = ++e->epoch;
-  const uint64_t lim = e->cfg.segment_bytes - e->cfg.index_interval;
-  a.nospace_limit_lo = (uint32_t)lim;
-  a.nospace_limit_hi = (uint32_t)(lim >> 32);
-  a.crc = e->d_crc;
-  a.err = e->d_err;
-  a.spin_limit = e->spin_limit;
-  a.debug = e->debug_flags;
-  if (e->stamps_path) {
-    if (!e->d_stamps) {
-      int rc = dalloc(&e->d_stamps, (size_t)e->max_app_tiles * 8);
-      if (rc) return rc;
-    }
-    a.stamps = e->d_stamps;
-    e->stamps_tiles = a.tiles;
-  }
-  const uint32_t wpb = (uint32_t)append_waves_per_block();
-  const uint32_t grid = std::min<uint32_t>((a.tiles + wpb - 1) / wpb, e->cu_count * (uint32_t)append_blocks_per_cu());
-  hipEvent_t pa0 = nullptr, pa1 = nullptr;
-  if (e->profile) {
-    pa0 = pool_event(e);
-    pa1 = pool_event(e);
-    HIP_TRY(hipEventRecord(pa0, e->main_s));
-  }
-  if (!(e->debug_skip & 2u)) launch_append(a, grid, e->main_s);
-  HIP_TRY(hipGetLastError());
-  if (e->profile) {
-    HIP_TRY(hipEventRecord(pa1, e->main_s));
-    e->prof[0].push_back({pa0, pa1});
-  }
-  if (b->mem == RMQ_MEM_HOST)
-    HIP_TRY(hipMemcpyAsync(out_offsets, d_out, n * 8ull, hipMemcpyDeviceToHost, e->main_s));
-  HIP_TRY(hipEventRecord(sl.append_done, e->main_s));
-  e->last_append_done = sl.append_done;
+  int rc = launch_stages(e, &f, e->has1 ? &e->st1 : nullptr, e->has2 ? &e->st2 : nullptr);
+  if (rc) return rc;
+  e->has2 = e->has1;
+  e->st2 = e->st1;
+  e->has1 = true;
+  e->st1 = f;
   return RMQ_OK;
 }
 
@@ -695,21 +736,22 @@ int rmq_ack(rmq_engine* e, const uint32_t* pidx, const uint32_t* slot, const uin
 int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64_t* hw_out) {
   if (!e) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
-  if (ticket > e->last_ticket) return RMQ_EINVAL;
+  if (ticket > e->last_ticket || (ticket && e->last_ticket - ticket >= kStatsRing)) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  if (ticket) {
-    Slot& sl = e->slots[ticket % e->slots.size()];
-    if (sl.ticket == ticket) {
-      hipError_t q = hipEventQuery(sl.append_done);
-      if (q == hipErrorNotReady) return RMQ_PENDING;
-      if (q != hipSuccess) return hip_fail(q);
+  const uint64_t t = ticket ? resolve_ticket(e, ticket) : 0;
+  if (t) {
+    if (!e->ticket_launch[t % kStatsRing]) {
+      int rc = flush(e);  // a poll pushes the batch through the remaining stages
+      if (rc) return rc;
     }
+    if (!launch_done(e, e->ticket_launch[t % kStatsRing])) return RMQ_PENDING;
   }
   int rc = check_err(e);
   if (rc) return rc;
   const size_t P = e->cfg.num_partitions;
   if (commit_out || hw_out) {
-    HIP_TRY(hipStreamSynchronize(e->main_s));  // snapshot after everything submitted so far
+    rc = drain(e);  // snapshot after everything submitted so far
+    if (rc) return rc;
     if (commit_out) HIP_TRY(hipMemcpy(commit_out, e->st.commit, P * 8, hipMemcpyDeviceToHost));
     if (hw_out) HIP_TRY(hipMemcpy(hw_out, e->st.hw, P * 8, hipMemcpyDeviceToHost));
   }
@@ -721,21 +763,22 @@ int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out) {
   std::lock_guard<std::mutex> g(e->mu);
   if (!ticket || ticket > e->last_ticket || e->last_ticket - ticket >= kStatsRing) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  Slot& sl = e->slots[ticket % e->slots.size()];
-  if (sl.ticket == ticket) HIP_TRY(hipEventSynchronize(sl.append_done));
+  int rc = wait_ticket(e, resolve_ticket(e, ticket));
+  if (rc) return rc;
   const uint32_t n = e->ticket_n[ticket % kStatsRing];
-  const uint32_t tiles = (n + kAppendTile - 1) / kAppendTile;
-  std::vector<uint4> ts(tiles ? tiles : 1);
-  if (tiles)
-    HIP_TRY(hipMemcpy(ts.data(), e->d_tile_stats + (size_t)(ticket % kStatsRing) * e->max_app_tiles,
-                      tiles * sizeof(uint4), hipMemcpyDeviceToHost));
+  const uint32_t tasks = (n + kTaskRecs - 1) / kTaskRecs;
+  std::vector<uint4> ts(tasks ? tasks : 1);
+  if (tasks)
+    HIP_TRY(hipMemcpy(ts.data(), e->d_stats + (size_t)(ticket % kStatsRing) * e->max_tasks,
+                      tasks * sizeof(uint4), hipMemcpyDeviceToHost));
   std::memset(out, 0, sizeof *out);
   out->records = n;
-  for (uint32_t k = 0; k < tiles; ++k) {
+  for (uint32_t k = 0; k < tasks; ++k) {
     out->appended += ts[k].x;
     out->rejected_not_leader += ts[k].y;
     out->rejected_no_partition += ts[k].z;
-    out->rejected_no_space += ts[k].w;
+    out->rejected_no_space += ts[k].w & 0xFFFFu;
+    out->rejected_invalid += ts[k].w >> 16;
   }
   return check_err(e);
 }
@@ -998,7 +1041,8 @@ int rmq_profile_enable(rmq_engine* e, int enable) {
     }
     v.clear();
   }
-  e->profile = enable != 0;
+  e->profile = enable > 0 ? (uint32_t)enable : 0u;
+  e->prof_count = 0;
   return RMQ_OK;
 }
 

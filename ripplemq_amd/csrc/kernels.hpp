@@ -6,19 +6,20 @@
 
 namespace rmq {
 
-constexpr uint32_t kSortThreads = 256;
-constexpr uint32_t kSortItems = 8;
-constexpr uint32_t kSortDigitBits = 8;                     // <= 256 buckets per radix pass
-constexpr uint32_t kSortTile = kSortThreads * kSortItems;  // keys per sort tile
-constexpr uint32_t kAppendThreads = 256;                    // 4 waves; one 64-slot tile per wave
-constexpr uint32_t kAppendTile = 64;
-constexpr uint32_t kAppendImageBytes = 8192;                // LDS record image per wave
+constexpr uint32_t kPipeThreads = 512;   // 8 waves per workgroup, every role of the pipeline launch
+constexpr uint32_t kTileRecs = 1024;     // records per ranking tile (stage 1)
+constexpr uint32_t kTileIdxBits = 10;    // log2(kTileRecs)
+constexpr uint32_t kMaxTiles = 256;      // max_batch_records <= kMaxTiles * kTileRecs
+constexpr uint32_t kScanLanes = 8;       // stage 2: threads per partition column
+constexpr uint32_t kTaskRecs = 8;        // records per apply task (one wave, 8 lanes per record)
+constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-bit LDS radix passes)
 constexpr uint32_t kMaxRF = 8;
 
 struct CrcConsts;
 
 // Per-partition device state (SoA, [P] unless noted). Owned by the engine.
 struct DevState {
+  // leo / used / start_off / start_pos point at the CURRENT state set (see StateSet)
   uint64_t* leo;         // log end offset (next offset)
   uint64_t* used;        // log end byte position (logical)
   uint64_t* start_off;   // retained log start
@@ -39,49 +40,55 @@ struct DevState {
   uint32_t pad;
 };
 
-// One stable sort pass over the partition ids of a batch (see sort.hip).
-struct SortPassArgs {
-  const uint32_t* keys_in;      // first pass: raw pidx of the input batch
-  const uint32_t* pidx_raw;     // raw pidx of the input batch (last pass of a multi-pass sort)
-  const uint32_t* vals_in;      // later passes: record indices
-  uint32_t* keys_out;           // intermediate passes
-  uint32_t* vals_out;
-  uint4* slots;                 // last pass: {pidx, record, len, payload offset} per slot
-  const uint32_t* len;          // record payload lengths (input order)
-  const uint64_t* payload_off;  // caller payload offsets, or nullptr (packed)
-  uint32_t* src_off;            // packed payload offsets written by the first pass of a multi-pass sort
-  uint64_t* batch_info;         // first pass: [0] record bytes, [1] payload bytes of the batch
-  uint64_t* hist_gran;          // [tiles][256] tile digit counts {epoch | count}
-  uint64_t* len_gran;           // [tiles] tile payload bytes {epoch | bytes}
-  uint64_t* rb_gran;            // [tiles] tile record bytes {epoch | bytes}
-  uint32_t n, tiles;
-  uint32_t shift, bits, ndig;   // digit = (key >> shift) & ((1 << bits) - 1), ndig digits used
-  uint32_t P;
-  uint32_t first, last;
-  uint32_t epoch;
-  uint32_t* err;
-  uint64_t* stamps;             // diagnostic build only: [tiles][8] s_memrealtime per phase, or null
+// Double-buffered per-partition log-position state: apply #a reads set a&1 and writes set (a+1)&1,
+// so records can read their partition's batch-start state while its new state is being written.
+struct StateSet {
+  uint64_t* leo;
+  uint64_t* used;
+  uint64_t* start_off;
+  uint64_t* start_pos;
 };
 
-struct AppendArgs {
-  DevState st;
-  const uint4* slots;        // sorted slot records {pidx, record, len | bad-partition flag, payload off}
+// One append batch as the pipeline sees it (device pointers).
+struct PipeBatch {
+  const uint32_t* pidx;
+  const uint32_t* len;
+  const uint64_t* poff;        // caller payload offsets, or nullptr (packed)
   const uint8_t* payload;
   uint64_t payload_bytes;
-  uint64_t* out_offsets;     // input order
-  const uint64_t* batch_info;
-  uint4* tile_stats;         // [tiles] {appended, not leader, unknown partition, no space}
-  uint64_t* lb_cnt;          // [tiles] look-back granules {epoch<<2|status : record count}
-  uint64_t* lb_bytes;        // [tiles] look-back granules {epoch<<2|status : record bytes}
+  uint64_t* out_offsets;       // input order
   uint32_t n;
-  uint32_t tiles;            // 64-slot tiles
-  uint32_t epoch;
-  uint32_t nospace_limit_lo, nospace_limit_hi;  // segment - interval (u64 split)
+  uint32_t tiles;              // ceil(n / kTileRecs)
+};
+
+// Batch-local scratch of one pipeline set (three sets rotate: a batch is ranked in launch k,
+// scanned in launch k+1 and applied in launch k+2).
+struct PipeScratch {
+  uint64_t* hist;       // [tiles][P] tile aggregate {count << 40 | bytes/16}; 0 = absent (stage 2 clears)
+  uint64_t* excl;       // [tiles][P] exclusive prefix of the aggregates over tiles (present entries only)
+  uint64_t* totals;     // [P] batch aggregate per partition
+  uint2* crank;         // [n] {rank in tile run | flags << 29, bytes/16 before it in the tile run}
+  uint32_t* pre;        // [n] payload bytes before the record inside its tile (packed payloads)
+  uint64_t* tsum;       // [tiles][4] {payload bytes, record bytes, invalid records, 0}
+  uint64_t* tile_base;  // [tiles] payload offset of the tile's first record (packed payloads)
+  uint64_t* binfo;      // [4] {reject flags (1 no space, 2 invalid), record bytes, payload bytes, 0}
+};
+
+// The single per-batch launch: stage 1 (rank tiles of batch k), stage 2 (column scans of batch
+// k-1), stage 3 (apply batch k-2). Any stage may be absent (count 0).
+struct PipeArgs {
+  DevState st;
+  StateSet cur, nxt;    // stage 3: read cur, write nxt
+  PipeBatch b1, b2, b3;
+  PipeScratch s1, s2, s3;
+  uint32_t wg1, wg2, wg3;  // workgroups per stage, in this order along blockIdx.x
+  uint32_t key_passes;     // 1 (P <= 256) or 2
+  uint64_t nospace_limit;  // segment - interval
   const CrcConsts* crc;
-  uint32_t* err;
-  uint32_t spin_limit;
-  uint32_t debug;            // diagnostics (RMQ_DEBUG_FLAGS): bit 2 no ring stores, bit 3 replica 0 only
-  uint64_t* stamps;          // diagnostic build only: [tiles][8] s_memrealtime per phase, or null
+  uint4* stats3;           // [tasks] {appended, not leader, unknown partition, no space | invalid << 16}
+  uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
+  uint64_t launch_seq;
+  uint64_t* stamps;        // diagnostic only (RMQ_STAMPS): [workgroup][wave][8] s_memrealtime, or null
 };
 
 struct FetchArgs {
@@ -115,15 +122,14 @@ struct AckArgs {
 };
 
 // launchers (defined in the .hip files)
-void launch_sort_pass(const SortPassArgs& a, uint32_t tiles, hipStream_t s);
-void launch_append(const AppendArgs& a, uint32_t grid, hipStream_t s);
+void launch_pipeline(const PipeArgs& a, hipStream_t s);
+uint32_t pipeline_lds_bytes();
+uint32_t pipeline_wgs_per_cu();
 void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev_resolve0, hipEvent_t ev_resolve1,
                   hipEvent_t ev_gather0, hipEvent_t ev_gather1);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
-int append_blocks_per_cu();
-int append_waves_per_block();
 
 }  // namespace rmq

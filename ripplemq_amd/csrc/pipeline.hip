@@ -1,0 +1,653 @@
+// pipeline.hip — the append path as ONE launch per batch: a three-stage software pipeline whose
+// stages work on three different batches at once, so no stage waits on another inside a launch.
+//
+// Reference semantics restated (file:line relative to the reference root):
+//   PartitionStateMachine.onApply / handleMessageAppendRequest — messages.addAll(batch): record j of
+//   an applied entry gets offset size_before + j, per partition, in apply order
+//   (mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:38-69);
+//   MessageAppendRequestProcessor "Not leader" gate (.../processor/MessageAppendRequestProcessor.java:29-32);
+//   jraft BallotBox quorum commit: commit = k-th largest matchIndex, k = RF/2 + 1,
+//   when that entry is from the current term. Log bytes, index and retention: FORMAT.md.
+//
+// Stage 1 (batch k, workgroup per 1024-record tile, no inter-workgroup traffic): stable LDS radix
+//   sort of the tile by partition id (two 8-bit passes, ballot-match ranks), a segmented scan of
+//   {1, record bytes/16} over the sorted tile, which gives every record its count / byte rank
+//   inside its partition's run in the tile, and the tile aggregate of each present partition,
+//   written sparsely into hist[tile][p]. Also the tile's payload prefix (packed payloads) and sums.
+// Stage 2 (batch k-1, 8 threads per partition): exclusive scan of hist[.][p] over the tiles ->
+//   excl[tile][p] and totals[p]; clears hist for reuse. Workgroup 0 scans the tile sums
+//   (payload bases, batch record bytes -> the no-space rule).
+// Stage 3 (batch k-2, wave per 32-record task): offset = log end + excl + rank, position likewise,
+//   out offsets, sparse index, then the records' 16-byte pieces are spread over the 64 lanes:
+//   coalesced-per-record payload loads, CRC32C of each piece from LDS tables (shifted into place
+//   by zero-byte tables, XOR-reduced per record), 16-byte stores into every local replica ring;
+//   headers last. Thread per partition: new log end, matchIndex, quorum commit, high watermark,
+//   retention — into the other state set, so no record ever reads a half-updated partition.
+//
+// Launch k starts only after launch k-1 has finished (one stream), so every hand-off between
+// stages crosses a kernel boundary. Launch k's first lane reports launch k-1 complete to the host.
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "partition_ops.hpp"
+
+namespace rmq {
+
+constexpr u32 kPT = kPipeThreads;   // 512
+constexpr u32 kPW = kPT / 64;       // 8 waves
+constexpr u32 kTR = kTileRecs;      // 2048
+constexpr u32 kTI = kTR / kPT;      // 2 records per thread in stage 1
+constexpr u32 kWR = kTR / kPW;      // 128 records per wave in stage 1
+constexpr u32 kIB = kTileIdxBits;   // 10
+constexpr u32 kFlagShift = 29;
+constexpr u32 kRankMask = (1u << kFlagShift) - 1u;
+// stage-1 flags (leadership is per partition, so it cannot change another partition's ranks:
+// stage 3 checks it)
+constexpr u32 kFlNoPart = 1u, kFlInvalid = 4u, kFlJunk = 7u;
+constexpr u64 kLow40 = (1ull << 40) - 1ull;
+constexpr u64 kOne40 = 1ull << 40;
+constexpr u32 kRejNoSpace = 1u, kRejInvalid = 2u;
+
+// Diagnostic phase stamps (RMQ_STAMPS): stamps[(workgroup * 8 + wave) * 8 + k], s_memrealtime
+// (100 MHz). Never read by the kernel.
+#define PIPE_STAMP(k)                                                                         \
+  do {                                                                                        \
+    if (A.stamps) {                                                                           \
+      const u64 t_ = __builtin_amdgcn_s_memrealtime();                                        \
+      if ((threadIdx.x & 63) == 0) A.stamps[((u64)blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+    }                                                                                         \
+  } while (0)
+
+struct Stage1Smem {
+  u32 items[2][kTR];   // key << 11 | position in tile (ping-pong between radix passes)
+  u32 cnt[kPW][256];   // per-wave digit counters, then per-wave digit bases
+  u32 dbase[256];      // digit totals, then digit bases
+  u32 info[kTR];       // record bytes/16 | flags << 29, by input position in the tile
+  u64 wsum[kPW][2];
+  u64 wtail[kPW];
+  u32 whead[kPW];
+  u32 scan[kPW];
+};
+
+struct Stage3Smem {
+  u32 t8[8][256];       // slicing-by-8 CRC32C tables
+  u32 z[3][4][256];     // register shift past 16, 32, 64 zero bytes
+};
+
+constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
+
+__device__ __forceinline__ u64 wave_incl_scan_u64(u64 v) {
+  const u32 l = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const u64 o = __shfl_up(v, d, 64);
+    if (l >= (u32)d) v += o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ u32 record_rs16(u32 L) {  // (16 + align16(L)) / 16 without overflow
+  return (L >> 4) + ((L & 15u) ? 1u : 0u) + 1u;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 1: rank one tile
+// ------------------------------------------------------------------------------------------
+__device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
+  const PipeBatch& b = A.b1;
+  const PipeScratch& x = A.s1;
+  const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const u32 base = t * kTR;
+  const u32 P = A.st.P;
+  const u64 lt = (1ull << lane) - 1ull;
+  const u32 nin = b.n - base < kTR ? b.n - base : kTR;
+  PIPE_STAMP(0);
+
+  // ---- loads (input position q = 256w + 64r + lane)
+  u32 item[kTI], lenv[kTI], fl[kTI];
+  u32 pc[kTI];
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 q = w * kWR + r * 64u + lane;
+    const bool in = q < nin;
+    const u32 p = in ? b.pidx[base + q] : 0u;
+    lenv[r] = in ? b.len[base + q] : 0u;
+    const bool bad = in && p >= P;
+    pc[r] = (in && !bad) ? p : 0u;
+    fl[r] = !in ? kFlJunk : bad ? kFlNoPart : 0u;
+  }
+  u64 inv_cnt = 0;
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 q = w * kWR + r * 64u + lane;
+    if (fl[r] != kFlJunk && b.poff) {  // explicit payload offsets: per-record range check
+      const u64 o = b.poff[base + q];
+      const u32 L = lenv[r];
+      if (L && (o > b.payload_bytes || (u64)L > b.payload_bytes - o)) {
+        inv_cnt += 1;
+        if (fl[r] == 0u) fl[r] = kFlInvalid;
+      }
+    }
+    const u32 rs16 = fl[r] == kFlJunk ? 0u : record_rs16(lenv[r]);
+    S.info[q] = rs16 | (fl[r] << kFlagShift);
+    item[r] = (pc[r] << kIB) | q;
+  }
+
+  // ---- input-order scans: payload prefix per record, tile sums {payload, record bytes}
+  {
+    u64 carry = 0, rb = 0;
+    u32 pre_r[kTI];
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) {
+      const u64 v = lenv[r];
+      const u64 inc = wave_incl_scan_u64(v);
+      pre_r[r] = (u32)(carry + inc - v);
+      carry += __shfl(inc, 63, 64);
+      rb += fl[r] == kFlJunk ? 0ull : 16ull * record_rs16(lenv[r]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      rb += __shfl_xor(rb, d, 64);
+      inv_cnt += __shfl_xor(inv_cnt, d, 64);
+    }
+    if (lane == 0) {
+      S.wsum[w][0] = carry;
+      S.wsum[w][1] = rb | (inv_cnt << 48);
+    }
+    __syncthreads();
+    u64 wpre = 0;
+#pragma unroll
+    for (u32 ww = 0; ww < kPW; ++ww) wpre += ww < w ? S.wsum[ww][0] : 0ull;
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) {
+      const u32 q = w * kWR + r * 64u + lane;
+      if (q < nin) x.pre[base + q] = (u32)wpre + pre_r[r];
+    }
+    if (tid == 0) {
+      u64 ps = 0, rs = 0, ic = 0;
+      for (u32 ww = 0; ww < kPW; ++ww) {
+        ps += S.wsum[ww][0];
+        rs += S.wsum[ww][1] & ((1ull << 48) - 1ull);
+        ic += S.wsum[ww][1] >> 48;
+      }
+      x.tsum[(u64)t * 4 + 0] = ps;
+      x.tsum[(u64)t * 4 + 1] = rs;
+      x.tsum[(u64)t * 4 + 2] = ic;
+      x.tsum[(u64)t * 4 + 3] = 0;
+    }
+  }
+
+  PIPE_STAMP(1);
+  // ---- stable LDS radix sort of the tile by partition id, 8-bit digits
+  u32 buf = 0;
+  for (u32 pass = 0; pass < A.key_passes; ++pass) {
+    const u32 sh = kIB + 8u * pass;
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) S.cnt[w][lane + 64u * k] = 0u;
+    __builtin_amdgcn_wave_barrier();
+    u32 rk[kTI];
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) {
+      const u32 d = (item[r] >> sh) & 0xFFu;
+      u64 peers = ~0ull;
+#pragma unroll
+      for (u32 bb = 0; bb < 8; ++bb) {
+        const bool bit = (d >> bb) & 1u;
+        const u64 m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      const u32 c = S.cnt[w][d];
+      const u64 below = peers & lt;
+      rk[r] = c + (u32)__popcll(below);
+      __builtin_amdgcn_wave_barrier();
+      if (below == 0ull) S.cnt[w][d] = c + (u32)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    if (tid < 256) {
+      u32 run = 0;
+#pragma unroll
+      for (u32 ww = 0; ww < kPW; ++ww) {
+        const u32 c = S.cnt[ww][tid];
+        S.cnt[ww][tid] = run;
+        run += c;
+      }
+      const u32 inc = wave_incl_scan(run);
+      if (lane == 63) S.scan[w] = inc;
+      S.dbase[tid] = inc - run;
+    }
+    __syncthreads();
+    if (tid < 256) {
+      u32 add = 0;
+      for (u32 ww = 0; ww < w; ++ww) add += S.scan[ww];
+      S.dbase[tid] += add;
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) {
+      const u32 d = (item[r] >> sh) & 0xFFu;
+      S.items[buf][S.dbase[d] + S.cnt[w][d] + rk[r]] = item[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) item[r] = S.items[buf][w * kWR + r * 64u + lane];
+    buf ^= 1u;
+  }
+  if (A.key_passes == 0) {  // single partition: input order is already sorted
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) S.items[buf][w * kWR + r * 64u + lane] = item[r];
+    __syncthreads();
+    buf ^= 1u;
+  }
+  const u32* sorted = S.items[buf ^ 1u];
+  PIPE_STAMP(2);
+
+  // ---- segmented scan of {1, rs16} over the sorted tile (segments = partitions)
+  u64 val[kTI], inc[kTI];
+  u32 hb[kTI];
+  u64 carry = 0;
+  u32 any_head = 0;
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 s = w * kWR + r * 64u + lane;
+    const u32 key = item[r] >> kIB, q = item[r] & (kTR - 1u);
+    const u32 info = S.info[q];
+    const u32 f = info >> kFlagShift;
+    val[r] = f == 0u ? (kOne40 | (info & kRankMask)) : 0ull;
+    const u32 pkey = s ? (sorted[s - 1] >> kIB) : 0xFFFFFFFFu;
+    u32 head = pkey != key ? 1u : 0u;
+    u64 v = val[r];
+    wave_seg_incl_scan(head, v);
+    if (!head) v += carry;
+    carry = __shfl(v, 63, 64);
+    hb[r] = head | any_head;
+    any_head |= __ballot(head) ? 1u : 0u;
+    inc[r] = v;
+  }
+  if (lane == 63) {
+    S.wtail[w] = carry;
+    S.whead[w] = any_head;
+  }
+  __syncthreads();
+  u64 cin = 0;
+  for (int ww = (int)w - 1; ww >= 0; --ww) {
+    cin += S.wtail[ww];
+    if (S.whead[ww]) break;
+  }
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 s = w * kWR + r * 64u + lane;
+    const u32 key = item[r] >> kIB, q = item[r] & (kTR - 1u);
+    const u64 v = inc[r] + (hb[r] ? 0ull : cin);
+    const u32 f = S.info[q] >> kFlagShift;
+    if (q < nin) {
+      const u64 ex = v - val[r];
+      x.crank[base + q] = make_uint2((u32)(ex >> 40) | (f << kFlagShift), (u32)(ex & kLow40));
+    }
+    const u32 nkey = s + 1 < kTR ? (sorted[s + 1] >> kIB) : 0xFFFFFFFFu;
+    if (nkey != key && (v >> 40)) x.hist[(u64)t * P + key] = v;
+  }
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(3);
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 2: column scans over the tiles, tile payload bases, batch rules
+// ------------------------------------------------------------------------------------------
+__device__ void stage2(const PipeArgs& A, u32 wg) {
+  const PipeBatch& b = A.b2;
+  const PipeScratch& x = A.s2;
+  const u32 P = A.st.P, T = b.tiles;
+  PIPE_STAMP(0);
+  // kScanLanes consecutive threads share a partition column: thread s takes tiles [s*ts, s*ts+ts)
+  const u32 ts = (T + kScanLanes - 1) / kScanLanes;
+  const u32 s = threadIdx.x % kScanLanes;
+  for (u32 g = wg * kPT + threadIdx.x; g < P * kScanLanes; g += A.wg2 * kPT) {  // uniform trip count
+    const u32 p = g / kScanLanes;
+    const u32 ta = s * ts;
+    const u32 tn = ta >= T ? 0u : (T - ta < ts ? T - ta : ts);  // tiles of this thread
+    u64* const col = x.hist + (u64)ta * P + p;
+    u64* const ecol = x.excl + (u64)ta * P + p;
+    u64 loc = 0;
+    for (u32 k0 = 0; k0 < tn; k0 += 4) {
+      u64 h[4];
+#pragma unroll
+      for (u32 k = 0; k < 4; ++k) h[k] = k0 + k < tn ? col[(size_t)(k0 + k) * P] : 0ull;
+#pragma unroll
+      for (u32 k = 0; k < 4; ++k) loc += h[k];
+    }
+    // exclusive prefix of the segment sums across the kScanLanes threads of the column
+    u64 inc = loc;
+#pragma unroll
+    for (u32 d = 1; d < kScanLanes; d <<= 1) {
+      const u64 o = __shfl_up(inc, d, kScanLanes);
+      if (s >= d) inc += o;
+    }
+    u64 run = inc - loc;
+    if (s == kScanLanes - 1) x.totals[p] = inc;
+    for (u32 k = 0; k < tn; ++k) {  // second sweep (L2-hot): prefixes, clear for reuse
+      const u64 h = col[(size_t)k * P];
+      if (h) {
+        ecol[(size_t)k * P] = run;
+        col[(size_t)k * P] = 0ull;
+        run += h;
+      }
+    }
+  }
+  if (wg == 0) {
+    __shared__ u64 s_w[kPW][3];
+    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const bool in = tid < T;
+    const u64 pay = in ? x.tsum[(u64)tid * 4 + 0] : 0ull;
+    const u64 rb = in ? x.tsum[(u64)tid * 4 + 1] : 0ull;
+    const u64 ic = in ? x.tsum[(u64)tid * 4 + 2] : 0ull;
+    const u64 pinc = wave_incl_scan_u64(pay);
+    u64 rsum = rb, isum = ic;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      rsum += __shfl_xor(rsum, d, 64);
+      isum += __shfl_xor(isum, d, 64);
+    }
+    if (lane == 63) s_w[w][0] = pinc;
+    if (lane == 0) {
+      s_w[w][1] = rsum;
+      s_w[w][2] = isum;
+    }
+    __syncthreads();
+    u64 wpre = 0, ptot = 0, rtot = 0, itot = 0;
+    for (u32 ww = 0; ww < kPW; ++ww) {
+      wpre += ww < w ? s_w[ww][0] : 0ull;
+      ptot += s_w[ww][0];
+      rtot += s_w[ww][1];
+      itot += s_w[ww][2];
+    }
+    if (in) x.tile_base[tid] = wpre + pinc - pay;
+    if (tid == 0) {
+      u32 rej = 0;
+      if (itot || (!b.poff && ptot > b.payload_bytes)) rej |= kRejInvalid;
+      if (rtot > A.nospace_limit) rej |= kRejNoSpace;
+      x.binfo[0] = rej;
+      x.binfo[1] = rtot;
+      x.binfo[2] = ptot;
+      x.binfo[3] = 0;
+    }
+  }
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(1);
+}
+
+// ------------------------------------------------------------------------------------------
+// Stage 3: apply
+// ------------------------------------------------------------------------------------------
+
+// The aligned 16-byte blocks holding payload bytes [addr, addr + nb), nb in [1, 16]: the block of
+// addr and, if the range crosses into it, the next one (never touches a block without a
+// requested byte, so never a page without one).
+__device__ __forceinline__ void load_blocks(const uint8_t* payload, u64 addr, u32 nb, uint4& b0, uint4& b1) {
+  const u64 ua = reinterpret_cast<u64>(payload + addr);
+  const u32 s = (u32)(ua & 15u);
+  b0 = *reinterpret_cast<const uint4*>(ua - s);
+  b1 = make_uint4(0, 0, 0, 0);
+  if (s + nb > 16u) b1 = *reinterpret_cast<const uint4*>(ua - s + 16u);
+}
+
+// Bytes [s, s + nb) of b0 || b1 as 4 little-endian dwords, zero-padded past nb. 64-bit funnel
+// shifts with two-way selects (no dynamically indexed array, which would go to scratch).
+__device__ __forceinline__ uint4 extract_piece(uint4 b0, uint4 b1, u32 s, u32 nb) {
+  const u64 q0 = ((u64)b0.y << 32) | b0.x, q1 = ((u64)b0.w << 32) | b0.z;
+  const u64 q2 = ((u64)b1.y << 32) | b1.x, q3 = ((u64)b1.w << 32) | b1.z;
+  const bool h = s >= 8u;
+  const u64 a0 = h ? q1 : q0, a1 = h ? q2 : q1, a2 = h ? q3 : q2;
+  const u32 sh = (s & 7u) * 8u;
+  u64 lo = sh ? (a0 >> sh) | (a1 << (64u - sh)) : a0;
+  u64 hi = sh ? (a1 >> sh) | (a2 << (64u - sh)) : a1;
+  if (nb < 16u) {
+    if (nb <= 8u) {
+      hi = 0;
+      lo = nb == 8u ? lo : lo & ((1ull << (8u * nb)) - 1ull);
+    } else {
+      hi &= (1ull << (8u * (nb - 8u))) - 1ull;
+    }
+  }
+  return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
+}
+
+__device__ __forceinline__ u32 crc_piece16(const u32 (*t)[256], uint4 v) {
+  return crc_step8(t, crc_step8(t, 0u, v.x, v.y), v.z, v.w);
+}
+
+// XOR over each aligned group of 8 lanes; lane 8g + 7 (and 8g + 4..6) receive the group total.
+__device__ __forceinline__ u32 group8_xor_to_top(u32 v) {
+  v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+  return v;
+}
+
+// One task = 8 records, one per 8-lane group: lane j of a group carries the record's payload
+// pieces j, j + 8, ... (16 bytes each); lane 7 also writes the header once the group's CRC
+// registers are XOR-reduced into it.
+struct TaskRec {  // round-1 words of a task's record (the same in all 8 lanes of its group)
+  u32 p, L;
+  uint2 cr;
+  u64 src;
+};
+
+__device__ __forceinline__ TaskRec stage3_load(const PipeArgs& A, u32 task) {
+  const PipeBatch& b = A.b3;
+  const PipeScratch& x = A.s3;
+  const u32 i = task * kTaskRecs + ((threadIdx.x & 63) >> 3);
+  const u32 t = (task * kTaskRecs) / kTR;
+  TaskRec r{0u, 0u, make_uint2(kFlJunk << kFlagShift, 0u), 0ull};
+  if (i < b.n) {
+    r.p = b.pidx[i];
+    r.L = b.len[i];
+    r.cr = x.crank[i];
+    r.src = b.poff ? b.poff[i] : x.tile_base[t] + x.pre[i];
+  }
+  return r;
+}
+
+__device__ void stage3_task(const PipeArgs& A, const Stage3Smem& S, u32 task, const TaskRec& R, uint4& stat_out) {
+  const PipeBatch& b = A.b3;
+  const PipeScratch& x = A.s3;
+  const DevState& st = A.st;
+  const u32 lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+  const u32 P = st.P, RF = st.RF;
+  const u32 i = task * kTaskRecs + g;
+  const bool in = i < b.n;
+  const u32 t = (task * kTaskRecs) / kTR;
+  PIPE_STAMP(0);
+  const u32 rej = (u32)x.binfo[0];
+  const u32 p = R.p, L = R.L;
+  const uint2 cr = R.cr;
+  const u64 src = R.src;
+  const u32 fl = cr.x >> kFlagShift;
+  const bool cand = in && fl == 0u && rej == 0u;
+  // ---- round 2: partition state and payload, issued together
+  u64 ex = 0, tot = 0, leo = 0, used = 0, spos = 0;
+  u32 lm = 0, lead = 0;
+  if (cand) {
+    lead = st.is_leader[p];
+    ex = x.excl[(u64)t * P + p];
+    tot = x.totals[p];
+    leo = A.cur.leo[p];
+    used = A.cur.used[p];
+    spos = A.cur.start_pos[p];
+    lm = st.local_mask[p];
+  }
+  const bool ok = cand && lead != 0u;
+  const u32 m = (L + 15u) >> 4;  // payload pieces
+  const u32 nck = ok ? (m + 7u) >> 3 : 0u;
+  PIPE_STAMP(1);
+  const u64 segmask = st.seg - 1ull;
+  const u64 rstride = (u64)P * st.seg;
+  const u64 off = leo + (ex >> 40) + (cr.x & kRankMask);
+  const u64 pos = used + 16ull * ((ex & kLow40) + cr.y);
+  uint8_t* const ring = st.logs + (u64)p * st.seg;
+  u32 acc = 0;
+  for (u32 c = 0; __any(c < nck); ++c) {
+    const u32 jp = 8u * c + j;
+    const bool act = c < nck && jp < m;
+    if (act) {
+      const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
+      const u64 addr = src + 16ull * jp;
+      uint4 b0, b1;
+      load_blocks(b.payload, addr, nb, b0, b1);
+      const uint4 v = extract_piece(b0, b1, (u32)(reinterpret_cast<u64>(b.payload + addr) & 15u), nb);
+      uint4 vc = v;
+      if (jp == 0) vc.x ^= 0xFFFFFFFFu;  // CRC init folded into the first payload dword
+      u32 cc = crc_piece16(S.t8, vc);
+      const u32 d = m - 1u - jp;  // 16-byte pieces after this one (< 2^28)
+      if (d & 1u) cc = crc_zshift(S.z[0], cc);
+      if (d & 2u) cc = crc_zshift(S.z[1], cc);
+      if (d & 4u) cc = crc_zshift(S.z[2], cc);
+      for (u32 bb = 3; bb < 28u && (d >> bb) != 0u; ++bb)
+        if ((d >> bb) & 1u) cc = gf2_mulmod(A.crc->shift_pow2[bb + 4], cc);
+      acc ^= cc;
+      uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
+      for (u32 r = 0; r < RF; ++r)
+        if ((lm >> r) & 1u) *reinterpret_cast<uint4*>(dst + r * rstride) = v;
+    }
+  }
+  PIPE_STAMP(2);
+  acc = group8_xor_to_top(acc);
+
+  // ---- header (lane 7), out offset (lane 0), sparse index (lane 1), retention crossing (lane 2)
+  if (ok && j == 7) {
+    u32 crc = 0;
+    if (L) {  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad))
+      const u32 pad = 16u * m - L;
+      crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
+    }
+    const uint4 h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
+    uint8_t* dst = ring + (pos & segmask);
+    for (u32 r = 0; r < RF; ++r)
+      if ((lm >> r) & 1u) *reinterpret_cast<uint4*>(dst + r * rstride) = h;
+  }
+  if (in && j == 0) b.out_offsets[i] = ok ? off : ~0ull;
+  const u32 ilog = st.interval_log2;
+  const u64 end = pos + 16ull * (1ull + m);
+  if (ok && j == 1) {
+    for (u64 mm = (pos >> ilog) + 1; (mm << ilog) <= end; ++mm) {
+      u64* e = st.index + ((u64)p * st.icap + mm % st.icap) * 2;
+      e[0] = off + 1;
+      e[1] = end;
+    }
+  }
+  if (ok && j == 2) {  // retention (FORMAT.md §4): the record whose range holds m* * I names E[m*]
+    const u64 fin = used + 16ull * (tot & kLow40);
+    if (fin - spos > st.seg) {
+      const u64 ms = (fin - st.seg + (1ull << ilog) - 1) >> ilog;
+      const u64 X = ms << ilog;
+      if (pos < X && X <= end) {
+        A.nxt.start_off[p] = off + 1;
+        A.nxt.start_pos[p] = end;
+      }
+    }
+  }
+  {
+    const bool h = j == 0;
+    const u32 n_in = (u32)__popcll(__ballot(h && in));
+    const u32 n_app = (u32)__popcll(__ballot(h && ok));
+    const u32 n_nl = (u32)__popcll(__ballot(h && cand && !lead));
+    const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h && in && fl == kFlNoPart));
+    const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
+    const u32 n_ns = (rej & kRejInvalid) ? 0u : (rej & kRejNoSpace) ? n_in : 0u;
+    stat_out = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
+  }
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(3);
+}
+
+// Thread per partition: the batch's new log end, matchIndex, quorum commit, high watermark and
+// retention, into the next state set.
+__device__ void stage3_partition(const PipeArgs& A, u32 p) {
+  const DevState& st = A.st;
+  const u32 rej = (u32)A.s3.binfo[0];
+  const u64 tot = rej ? 0ull : A.s3.totals[p];
+  const u64 tc = tot >> 40, tb = 16ull * (tot & kLow40);
+  const u64 leo = A.cur.leo[p], used = A.cur.used[p];
+  const u64 so = A.cur.start_off[p], sp = A.cur.start_pos[p];
+  const u64 nleo = leo + tc, nused = used + tb;
+  A.nxt.leo[p] = nleo;
+  A.nxt.used[p] = nused;
+  bool copy_start = true;
+  if (tc) {
+    const u32 RF = st.RF, lm = st.local_mask[p];
+    u64 row[kMaxRF];
+#pragma unroll
+    for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
+#pragma unroll
+    for (u32 r = 0; r < kMaxRF; ++r)
+      if (r < RF && ((lm >> r) & 1u)) {
+        row[r] = nleo;
+        st.match[(u64)p * RF + r] = nleo;
+      }
+    const u64 c = quorum_commit(row, RF, st.commit[p], st.term_start[p]);
+    st.commit[p] = c;
+    st.hw[p] = c;
+    if (nused - sp > st.seg) {
+      const u32 ilog = st.interval_log2;
+      const u64 ms = (nused - st.seg + (1ull << ilog) - 1) >> ilog;
+      if ((ms << ilog) <= used) {  // crossing record from an earlier batch: E[m*] is in the index
+        const u64* e = st.index + ((u64)p * st.icap + ms % st.icap) * 2;
+        A.nxt.start_off[p] = e[0];
+        A.nxt.start_pos[p] = e[1];
+      }
+      copy_start = false;  // otherwise the crossing record of this batch writes the new start
+    }
+  }
+  if (copy_start) {
+    A.nxt.start_off[p] = so;
+    A.nxt.start_pos[p] = sp;
+  }
+}
+
+#ifndef RMQ_PIPE_WAVES_PER_SIMD
+#define RMQ_PIPE_WAVES_PER_SIMD 6  // 75 VGPRs, no spills: 3 resident workgroups per CU
+#endif
+__global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(PipeArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
+    __hip_atomic_store(A.done_word, A.launch_seq - 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  u32 wg = blockIdx.x;
+  if (wg < A.wg1) {
+    stage1_tile(A, wg, *reinterpret_cast<Stage1Smem*>(smem_raw));
+    return;
+  }
+  wg -= A.wg1;
+  if (wg < A.wg2) {
+    stage2(A, wg);
+    return;
+  }
+  wg -= A.wg2;
+  Stage3Smem& S = *reinterpret_cast<Stage3Smem*>(smem_raw);
+  const u32 tasks = (A.b3.n + kTaskRecs - 1) / kTaskRecs;
+  u32 task = wg * kPW + (threadIdx.x >> 6);
+  TaskRec R = stage3_load(A, task < tasks ? task : 0u);  // in flight during the table fill
+  for (u32 k = threadIdx.x; k < 8 * 256; k += kPT) (&S.t8[0][0])[k] = (&A.crc->table[0][0])[k];
+  for (u32 k = threadIdx.x; k < 3 * 4 * 256; k += kPT) (&S.z[0][0][0])[k] = (&A.crc->zshift[0][0][0])[k];
+  __syncthreads();
+  const u32 lane = threadIdx.x & 63;
+  for (; task < tasks; task += A.wg3 * kPW) {
+    uint4 so;
+    stage3_task(A, S, task, R, so);
+    if (lane == 0) A.stats3[task] = so;
+    const u32 nt = task + A.wg3 * kPW;
+    if (nt < tasks) R = stage3_load(A, nt);
+  }
+  for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wg3 * kPT) stage3_partition(A, p);
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(4);
+}
+
+uint32_t pipeline_lds_bytes() { return (uint32_t)kSmemBytes; }
+uint32_t pipeline_wgs_per_cu() { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (kPT / 64u); }
+
+void launch_pipeline(const PipeArgs& a, hipStream_t s) {
+  const u32 grid = a.wg1 + a.wg2 + a.wg3;
+  if (!grid) return;
+  hipLaunchKernelGGL(pipeline_kernel, dim3(grid), dim3(kPT), kSmemBytes, s, a);
+}
+
+}  // namespace rmq

@@ -135,7 +135,7 @@ class Engine:
         st = A.RmqAppendStats()
         _check(self.lib.rmq_ticket_stats(self.h, ticket, C.byref(st)), "rmq_ticket_stats")
         self._keep.pop(ticket, None)
-        return {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_ if f != "reserved"}
+        return {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_}
 
     def append(self, pidx, lens, payload, payload_off=None) -> tuple[np.ndarray, dict]:
         t, out = self.append_async(pidx, lens, payload, payload_off)
@@ -219,7 +219,7 @@ class Engine:
         _check(self.lib.rmq_memcpy(self.h, _ptr(dst), src, dst.nbytes, 1), "rmq_memcpy")
 
     def profile(self, enable: bool) -> None:
-        _check(self.lib.rmq_profile_enable(self.h, 1 if enable else 0), "rmq_profile_enable")
+        _check(self.lib.rmq_profile_enable(self.h, int(enable)), "rmq_profile_enable")
 
     def profile_query(self, kernel: int) -> tuple[int, float]:
         n, ms = C.c_uint64(), C.c_double()

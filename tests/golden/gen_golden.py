@@ -44,7 +44,7 @@ def run(eng, fx):
     for b in range(fx["batches"]):
         off, st = eng.append(fx[f"pidx{b}"], fx[f"lens{b}"], fx[f"payload{b}"])
         obs[f"offsets{b}"] = off
-        obs[f"stats{b}"] = np.array([st[k] for k in sorted(st)], np.uint64)
+        obs[f"stats{b}"] = np.array([st[k] for k in sorted(st) if k != "rejected_invalid"], np.uint64)
         rc, status = eng.commit_consumer_offset(fx[f"cc_p{b}"], fx[f"cc_c{b}"], fx[f"cc_o{b}"])
         obs[f"cc_status{b}"] = status
         rc, res, buf, used = eng.fetch(fx[f"f_p{b}"], fx[f"f_c{b}"], fx[f"f_m{b}"])

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Summarise pipeline-launch phase stamps (RMQ_STAMPS=<csv>, one launch: RMQ_STAMPS_AT).
+
+Rows: workgroup, wave, stage (1 rank tiles, 2 column scans, 3 apply), t0..t7 s_memrealtime
+(100 MHz -> 10 ns). Stage 1/2 stamps are per workgroup (wave 0); stage 3 per wave (one task).
+Prints, per stage, start/end spread relative to the first stamp of the launch and per-phase
+percentiles."""
+import sys
+
+import numpy as np
+
+PHASES = {
+    1: ["loads+input scans", "radix passes", "seg scan+writes"],
+    2: ["column scans+tile scan"],
+    3: ["records+state issue", "payload, crc, ring stores", "headers/index/offsets",
+        "partition threads (+later tasks)"],
+}
+
+
+def main(path):
+    a = np.loadtxt(path, delimiter=",", skiprows=1, dtype=np.int64)
+    t0 = a[:, 3][a[:, 3] > 0].min()
+    print(f"{path}: launch span {(a[:, 3:][a[:, 3:] > 0].max() - t0) * 0.01:.2f} us")
+    for stage, names in PHASES.items():
+        r = a[a[:, 2] == stage]
+        if stage in (1, 2):
+            r = r[r[:, 1] == 0]
+        if not len(r):
+            continue
+        t = (r[:, 3:3 + len(names) + 1] - t0).astype(np.float64) * 0.01
+        valid = (r[:, 3:3 + len(names) + 1] > 0).all(axis=1)
+        t = t[valid]
+        if not len(t):
+            continue
+        print(f" stage {stage}: {len(t)} rows, start p0 {t[:, 0].min():.2f} p50 {np.median(t[:, 0]):.2f} "
+              f"max {t[:, 0].max():.2f} | end p50 {np.median(t[:, -1]):.2f} max {t[:, -1].max():.2f} us")
+        for k, n in enumerate(names):
+            d = t[:, k + 1] - t[:, k]
+            print(f"   {n:>26s}: p10 {np.percentile(d, 10):7.2f} p50 {np.percentile(d, 50):7.2f} "
+                  f"p90 {np.percentile(d, 90):7.2f} max {d.max():7.2f} us")
+
+
+if __name__ == "__main__":
+    for p in sys.argv[1:]:
+        main(p)
