@@ -37,6 +37,22 @@ __host__ __device__ __forceinline__ constexpr u32 record_bytes(u32 len) {
   return 16u + ((len + kRecAlign - 1u) & ~(kRecAlign - 1u));
 }
 
+typedef u32 u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte log store. RMQ_RING_NT=1: non-temporal (streams past L2, nothing left dirty for the
+// end-of-kernel writeback); 0: default policy.
+#ifndef RMQ_RING_NT
+#define RMQ_RING_NT 1
+#endif
+__device__ __forceinline__ void store_log16(uint8_t* dst, uint4 v) {
+#if RMQ_RING_NT
+  const u32x4 x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(dst));
+#else
+  *reinterpret_cast<uint4*>(dst) = v;
+#endif
+}
+
 __device__ __forceinline__ u32 lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 // ---------------------------------------------------------------------------------------------

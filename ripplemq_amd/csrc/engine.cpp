@@ -112,6 +112,7 @@ struct rmq_engine {
   uint64_t stamps_at = 100;
   uint64_t* d_stamps = nullptr;
   uint32_t stamps_wg[3] = {0, 0, 0};
+  uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
 };
 
 namespace {
@@ -248,6 +249,7 @@ int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const I
   a.nospace_limit = e->cfg.segment_bytes - e->cfg.index_interval;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
+  a.debug = e->debug;
   if (s1) {
     a.b1 = s1->b;
     a.s1 = e->scratch[s1->set];
@@ -482,6 +484,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (!e->cfg.pipeline_depth) e->cfg.pipeline_depth = 3;
   e->device = cfg->device;
   e->stamps_path = std::getenv("RMQ_STAMPS");
+  if (const char* v = std::getenv("RMQ_DEBUG")) e->debug = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \

@@ -11,7 +11,7 @@ constexpr uint32_t kTileRecs = 1024;     // records per ranking tile (stage 1)
 constexpr uint32_t kTileIdxBits = 10;    // log2(kTileRecs)
 constexpr uint32_t kMaxTiles = 256;      // max_batch_records <= kMaxTiles * kTileRecs
 constexpr uint32_t kScanLanes = 8;       // stage 2: threads per partition column
-constexpr uint32_t kTaskRecs = 8;        // records per apply task (one wave, 8 lanes per record)
+constexpr uint32_t kTaskRecs = 32;       // records per apply task (one wave, 2 lanes per record)
 constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-bit LDS radix passes)
 constexpr uint32_t kMaxRF = 8;
 
@@ -88,6 +88,9 @@ struct PipeArgs {
   uint4* stats3;           // [tasks] {appended, not leader, unknown partition, no space | invalid << 16}
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
   uint64_t launch_seq;
+  uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
+                           // stores, 2 no CRC lookups, 4 no payload loads
+  uint32_t pad0;
   uint64_t* stamps;        // diagnostic only (RMQ_STAMPS): [workgroup][wave][8] s_memrealtime, or null
 };
 

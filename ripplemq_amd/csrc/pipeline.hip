@@ -71,6 +71,8 @@ struct Stage1Smem {
 struct Stage3Smem {
   u32 t8[8][256];       // slicing-by-8 CRC32C tables
   u32 z[3][4][256];     // register shift past 16, 32, 64 zero bytes
+  uint4 img[kPW][kTaskRecs][8];  // per wave: the task's records as laid out in the log (<= 128 B each)
+  uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16}
 };
 
 constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
@@ -298,40 +300,38 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
   const PipeScratch& x = A.s2;
   const u32 P = A.st.P, T = b.tiles;
   PIPE_STAMP(0);
-  // kScanLanes consecutive threads share a partition column: thread s takes tiles [s*ts, s*ts+ts)
-  const u32 ts = (T + kScanLanes - 1) / kScanLanes;
+  // kScanLanes consecutive threads share a partition column; per block of 8 * kScanLanes tiles,
+  // thread s holds tiles [8s, 8s + 8) of the block in registers (one load round per block)
   const u32 s = threadIdx.x % kScanLanes;
-  for (u32 g = wg * kPT + threadIdx.x; g < P * kScanLanes; g += A.wg2 * kPT) {  // uniform trip count
+  for (u32 g = wg * kPT + threadIdx.x; g < P * kScanLanes; g += A.wg2 * kPT) {  // whole columns per group
     const u32 p = g / kScanLanes;
-    const u32 ta = s * ts;
-    const u32 tn = ta >= T ? 0u : (T - ta < ts ? T - ta : ts);  // tiles of this thread
-    u64* const col = x.hist + (u64)ta * P + p;
-    u64* const ecol = x.excl + (u64)ta * P + p;
-    u64 loc = 0;
-    for (u32 k0 = 0; k0 < tn; k0 += 4) {
-      u64 h[4];
+    u64 carry = 0;
+    for (u32 B = 0; B < T; B += 8u * kScanLanes) {
+      const u32 ta = B + 8u * s;
+      u64 h[8];
 #pragma unroll
-      for (u32 k = 0; k < 4; ++k) h[k] = k0 + k < tn ? col[(size_t)(k0 + k) * P] : 0ull;
+      for (u32 k = 0; k < 8; ++k) h[k] = ta + k < T ? x.hist[(u64)(ta + k) * P + p] : 0ull;
+      u64 loc = 0;
 #pragma unroll
-      for (u32 k = 0; k < 4; ++k) loc += h[k];
-    }
-    // exclusive prefix of the segment sums across the kScanLanes threads of the column
-    u64 inc = loc;
+      for (u32 k = 0; k < 8; ++k) loc += h[k];
+      u64 inc = loc;
 #pragma unroll
-    for (u32 d = 1; d < kScanLanes; d <<= 1) {
-      const u64 o = __shfl_up(inc, d, kScanLanes);
-      if (s >= d) inc += o;
-    }
-    u64 run = inc - loc;
-    if (s == kScanLanes - 1) x.totals[p] = inc;
-    for (u32 k = 0; k < tn; ++k) {  // second sweep (L2-hot): prefixes, clear for reuse
-      const u64 h = col[(size_t)k * P];
-      if (h) {
-        ecol[(size_t)k * P] = run;
-        col[(size_t)k * P] = 0ull;
-        run += h;
+      for (u32 d = 1; d < kScanLanes; d <<= 1) {
+        const u64 o = __shfl_up(inc, d, kScanLanes);
+        if (s >= d) inc += o;
+      }
+      u64 run = carry + inc - loc;
+      carry += __shfl(inc, kScanLanes - 1, kScanLanes);
+#pragma unroll
+      for (u32 k = 0; k < 8; ++k) {
+        if (h[k]) {
+          x.excl[(u64)(ta + k) * P + p] = run;
+          x.hist[(u64)(ta + k) * P + p] = 0ull;  // clear for the set's next batch
+          run += h[k];
+        }
       }
     }
+    if (s == 0) x.totals[p] = carry;
   }
   if (wg == 0) {
     __shared__ u64 s_w[kPW][3];
@@ -415,27 +415,38 @@ __device__ __forceinline__ u32 crc_piece16(const u32 (*t)[256], uint4 v) {
   return crc_step8(t, crc_step8(t, 0u, v.x, v.y), v.z, v.w);
 }
 
-// XOR over each aligned group of 8 lanes; lane 8g + 7 (and 8g + 4..6) receive the group total.
-__device__ __forceinline__ u32 group8_xor_to_top(u32 v) {
-  v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
-  v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
-  v ^= (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
-  return v;
+// Stage 3 works on tasks of kTaskRecs = 32 records, one per lane pair. The pair loads the
+// record's payload as aligned 16-byte blocks (lane j takes blocks j, j + 2, ...; 8 pieces = up
+// to 9 blocks per round) and each lane builds its pieces (j, j + 2, j + 4, j + 6 of the round)
+// from its own block and its partner's (DPP swap); lane 1 writes the header once the pair's
+// CRC registers are XOR-reduced.
+constexpr u32 kPL = 2;          // lanes per record
+constexpr u32 kPR = 8;          // pieces per record per round
+constexpr u32 kBL = 5;          // blocks per lane per round (9 blocks cover 8 misaligned pieces)
+
+__device__ __forceinline__ u32 pair_swap(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint4 pair_swap4(uint4 v) {
+  return make_uint4(pair_swap(v.x), pair_swap(v.y), pair_swap(v.z), pair_swap(v.w));
 }
 
-// One task = 8 records, one per 8-lane group: lane j of a group carries the record's payload
-// pieces j, j + 8, ... (16 bytes each); lane 7 also writes the header once the group's CRC
-// registers are XOR-reduced into it.
-struct TaskRec {  // round-1 words of a task's record (the same in all 8 lanes of its group)
+struct TaskRec {  // round 1: the record (the same words in both lanes of its pair)
   u32 p, L;
   uint2 cr;
   u64 src;
 };
 
-__device__ __forceinline__ TaskRec stage3_load(const PipeArgs& A, u32 task) {
+struct TaskState {  // round 2: partition state of the record and its first round of payload blocks
+  u64 ex, tot, leo, used, spos;
+  u32 lm, lead;
+  uint4 blk[kBL];
+};
+
+__device__ __forceinline__ TaskRec stage3_r1(const PipeArgs& A, u32 task) {
   const PipeBatch& b = A.b3;
   const PipeScratch& x = A.s3;
-  const u32 i = task * kTaskRecs + ((threadIdx.x & 63) >> 3);
+  const u32 i = task * kTaskRecs + ((threadIdx.x & 63) >> 1);
   const u32 t = (task * kTaskRecs) / kTR;
   TaskRec r{0u, 0u, make_uint2(kFlJunk << kFlagShift, 0u), 0ull};
   if (i < b.n) {
@@ -447,82 +458,145 @@ __device__ __forceinline__ TaskRec stage3_load(const PipeArgs& A, u32 task) {
   return r;
 }
 
-__device__ void stage3_task(const PipeArgs& A, const Stage3Smem& S, u32 task, const TaskRec& R, uint4& stat_out) {
-  const PipeBatch& b = A.b3;
+__device__ __forceinline__ bool stage3_cand(const PipeArgs& A, u32 task, const TaskRec& R, u32 rej) {
+  const u32 i = task * kTaskRecs + ((threadIdx.x & 63) >> 1);
+  return i < A.b3.n && (R.cr.x >> kFlagShift) == 0u && rej == 0u;
+}
+
+// Aligned payload blocks of round c held by lane j: block 8c + j + 2q, q < kBL, loaded only if
+// it holds a byte of the record (never touches a page without one).
+__device__ __forceinline__ void round_blocks(const PipeArgs& A, const TaskRec& R, u32 c, bool live, uint4 (&blk)[kBL]) {
+  const u32 j = threadIdx.x & 1u;
+  const u64 ua = reinterpret_cast<u64>(A.b3.payload + R.src);
+  const u64 a0 = ua & ~15ull;
+  const u64 lim = ua + R.L;  // one past the last byte
+#pragma unroll
+  for (u32 q = 0; q < kBL; ++q) {
+    const u64 blk_addr = a0 + 16ull * (kPR * c + j + 2u * q);
+    blk[q] = make_uint4(0, 0, 0, 0);
+    if (live && blk_addr < lim && !(A.debug & 4u)) blk[q] = *reinterpret_cast<const uint4*>(blk_addr);
+  }
+}
+
+__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, u32 task, const TaskRec& R, bool cand) {
   const PipeScratch& x = A.s3;
   const DevState& st = A.st;
-  const u32 lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
-  const u32 P = st.P, RF = st.RF;
-  const u32 i = task * kTaskRecs + g;
-  const bool in = i < b.n;
   const u32 t = (task * kTaskRecs) / kTR;
-  PIPE_STAMP(0);
-  const u32 rej = (u32)x.binfo[0];
-  const u32 p = R.p, L = R.L;
-  const uint2 cr = R.cr;
-  const u64 src = R.src;
-  const u32 fl = cr.x >> kFlagShift;
-  const bool cand = in && fl == 0u && rej == 0u;
-  // ---- round 2: partition state and payload, issued together
-  u64 ex = 0, tot = 0, leo = 0, used = 0, spos = 0;
-  u32 lm = 0, lead = 0;
+  TaskState S;
+  S.ex = S.tot = S.leo = S.used = S.spos = 0ull;
+  S.lm = S.lead = 0u;
   if (cand) {
-    lead = st.is_leader[p];
-    ex = x.excl[(u64)t * P + p];
-    tot = x.totals[p];
-    leo = A.cur.leo[p];
-    used = A.cur.used[p];
-    spos = A.cur.start_pos[p];
-    lm = st.local_mask[p];
+    const u32 p = R.p;
+    S.lead = st.is_leader[p];
+    S.ex = x.excl[(u64)t * st.P + p];
+    S.tot = x.totals[p];
+    S.leo = A.cur.leo[p];
+    S.used = A.cur.used[p];
+    S.spos = A.cur.start_pos[p];
+    S.lm = st.local_mask[p];
   }
-  const bool ok = cand && lead != 0u;
+  // first round of payload blocks, speculatively (leadership is checked before any store)
+  round_blocks(A, R, 0u, cand, S.blk);
+  return S;
+}
+
+// CRC register of one 16-byte piece followed by d more 16-byte pieces of the record.
+__device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S, uint4 v, u32 jp, u32 d) {
+  if (jp == 0) v.x ^= 0xFFFFFFFFu;  // CRC init folded into the first payload dword
+  u32 c = (A.debug & 2u) ? v.x : crc_piece16(S.t8, v);
+  if (d & 1u) c = crc_zshift(S.z[0], c);
+  if (d & 2u) c = crc_zshift(S.z[1], c);
+  if (d & 4u) c = crc_zshift(S.z[2], c);
+  for (u32 bb = 3; bb < 28u && (d >> bb) != 0u; ++bb)
+    if ((d >> bb) & 1u) c = gf2_mulmod(A.crc->shift_pow2[bb + 4], c);
+  return c;
+}
+
+__device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, const TaskRec& R,
+                              const TaskState& Z, bool cand, u32 rej, uint4& stat_out) {
+  const PipeBatch& b = A.b3;
+  const DevState& st = A.st;
+  const u32 lane = threadIdx.x & 63, j = lane & 1u;
+  const u32 P = st.P, RF = st.RF;
+  const u32 i = task * kTaskRecs + (lane >> 1);
+  const bool in = i < b.n;
+  const u32 p = R.p, L = R.L;
+  const u32 fl = R.cr.x >> kFlagShift;
+  const bool ok = cand && Z.lead != 0u;
   const u32 m = (L + 15u) >> 4;  // payload pieces
-  const u32 nck = ok ? (m + 7u) >> 3 : 0u;
-  PIPE_STAMP(1);
   const u64 segmask = st.seg - 1ull;
   const u64 rstride = (u64)P * st.seg;
-  const u64 off = leo + (ex >> 40) + (cr.x & kRankMask);
-  const u64 pos = used + 16ull * ((ex & kLow40) + cr.y);
+  const u64 off = Z.leo + (Z.ex >> 40) + (R.cr.x & kRankMask);
+  const u64 pos = Z.used + 16ull * ((Z.ex & kLow40) + R.cr.y);
   uint8_t* const ring = st.logs + (u64)p * st.seg;
+  const u32 lmw = (A.debug & 1u) ? 0u : Z.lm;
+  const u32 sa = (u32)(reinterpret_cast<u64>(b.payload + R.src) & 15u);
   u32 acc = 0;
-  for (u32 c = 0; __any(c < nck); ++c) {
-    const u32 jp = 8u * c + j;
-    const bool act = c < nck && jp < m;
-    if (act) {
-      const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
-      const u64 addr = src + 16ull * jp;
-      uint4 b0, b1;
-      load_blocks(b.payload, addr, nb, b0, b1);
-      const uint4 v = extract_piece(b0, b1, (u32)(reinterpret_cast<u64>(b.payload + addr) & 15u), nb);
-      uint4 vc = v;
-      if (jp == 0) vc.x ^= 0xFFFFFFFFu;  // CRC init folded into the first payload dword
-      u32 cc = crc_piece16(S.t8, vc);
-      const u32 d = m - 1u - jp;  // 16-byte pieces after this one (< 2^28)
-      if (d & 1u) cc = crc_zshift(S.z[0], cc);
-      if (d & 2u) cc = crc_zshift(S.z[1], cc);
-      if (d & 4u) cc = crc_zshift(S.z[2], cc);
-      for (u32 bb = 3; bb < 28u && (d >> bb) != 0u; ++bb)
-        if ((d >> bb) & 1u) cc = gf2_mulmod(A.crc->shift_pow2[bb + 4], cc);
-      acc ^= cc;
-      uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
-      for (u32 r = 0; r < RF; ++r)
-        if ((lm >> r) & 1u) *reinterpret_cast<uint4*>(dst + r * rstride) = v;
+  const u32 nr = ok ? (m + kPR - 1u) / kPR : 0u;
+  // records of at most 7 pieces (112 payload bytes) go through an LDS image of the log so that
+  // 8 consecutive lanes store each record's 128 bytes; longer ones are stored piecewise
+  const bool img = __all(!ok || m <= 7u);
+  const u32 w = threadIdx.x >> 6, r32 = lane >> 1;
+  uint4 blk[kBL];
+#pragma unroll
+  for (u32 q = 0; q < kBL; ++q) blk[q] = Z.blk[q];
+  for (u32 c = 0; __any(c < nr); ++c) {
+    if (c) round_blocks(A, R, c, c < nr, blk);
+#pragma unroll
+    for (u32 q = 0; q < 4; ++q) {
+      // piece jp = blocks jp (own q-th) and jp + 1 (partner's q-th for lane 0, (q+1)-th for
+      // lane 1): each lane offers what its partner needs, then one DPP swap
+      const uint4 pb = pair_swap4(j ? blk[q] : blk[q + 1]);
+      const u32 jp = kPR * c + j + 2u * q;
+      if (c < nr && jp < m) {
+        const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
+        const uint4 v = extract_piece(blk[q], pb, sa, nb);
+        acc ^= piece_crc(A, S, v, jp, m - 1u - jp);
+        if (img) {
+          const_cast<Stage3Smem&>(S).img[w][r32][jp + 1] = v;
+        } else {
+          uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
+          for (u32 r = 0; r < RF; ++r)
+            if ((lmw >> r) & 1u) store_log16(dst + r * rstride, v);
+        }
+      }
     }
   }
-  PIPE_STAMP(2);
-  acc = group8_xor_to_top(acc);
+  acc ^= pair_swap(acc);
 
-  // ---- header (lane 7), out offset (lane 0), sparse index (lane 1), retention crossing (lane 2)
-  if (ok && j == 7) {
+  // ---- header (lane 1), out offset + retention crossing (lane 0), sparse index (lane 1)
+  uint4 h = make_uint4(0, 0, 0, 0);
+  if (ok && j == 1) {
     u32 crc = 0;
     if (L) {  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad))
       const u32 pad = 16u * m - L;
       crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
     }
-    const uint4 h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
+    h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
+  }
+  if (img) {
+    Stage3Smem& W = const_cast<Stage3Smem&>(S);
+    if (j == 1) W.img[w][r32][0] = h;
+    if (j == 0) W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), p, Z.lm | (m << 8) | ((ok ? 1u : 0u) << 16));
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (u32 s4 = 0; s4 < kTaskRecs * 8u / 64u; ++s4) {
+      const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
+      const uint4 inf = W.info[w][rr];
+      const u32 mr = (inf.w >> 8) & 0xFFu;
+      if (((inf.w >> 16) & 1u) && k <= mr) {
+        const uint4 v = W.img[w][rr][k];
+        const u64 rpos = ((u64)inf.y << 32) | inf.x;
+        uint8_t* dst = st.logs + (u64)inf.z * st.seg + ((rpos + 16ull * k) & segmask);
+        const u32 lmr = (A.debug & 1u) ? 0u : (inf.w & 0xFFu);
+        for (u32 r = 0; r < RF; ++r)
+          if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
+      }
+    }
+  } else if (ok && j == 1) {
     uint8_t* dst = ring + (pos & segmask);
     for (u32 r = 0; r < RF; ++r)
-      if ((lm >> r) & 1u) *reinterpret_cast<uint4*>(dst + r * rstride) = h;
+      if ((Z.lm >> r) & 1u) store_log16(dst + r * rstride, h);
   }
   if (in && j == 0) b.out_offsets[i] = ok ? off : ~0ull;
   const u32 ilog = st.interval_log2;
@@ -534,9 +608,9 @@ __device__ void stage3_task(const PipeArgs& A, const Stage3Smem& S, u32 task, co
       e[1] = end;
     }
   }
-  if (ok && j == 2) {  // retention (FORMAT.md §4): the record whose range holds m* * I names E[m*]
-    const u64 fin = used + 16ull * (tot & kLow40);
-    if (fin - spos > st.seg) {
+  if (ok && j == 0) {  // retention (FORMAT.md §4): the record whose range holds m* * I names E[m*]
+    const u64 fin = Z.used + 16ull * (Z.tot & kLow40);
+    if (fin - Z.spos > st.seg) {
       const u64 ms = (fin - st.seg + (1ull << ilog) - 1) >> ilog;
       const u64 X = ms << ilog;
       if (pos < X && X <= end) {
@@ -549,14 +623,12 @@ __device__ void stage3_task(const PipeArgs& A, const Stage3Smem& S, u32 task, co
     const bool h = j == 0;
     const u32 n_in = (u32)__popcll(__ballot(h && in));
     const u32 n_app = (u32)__popcll(__ballot(h && ok));
-    const u32 n_nl = (u32)__popcll(__ballot(h && cand && !lead));
+    const u32 n_nl = (u32)__popcll(__ballot(h && cand && !Z.lead));
     const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h && in && fl == kFlNoPart));
     const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
     const u32 n_ns = (rej & kRejInvalid) ? 0u : (rej & kRejNoSpace) ? n_in : 0u;
     stat_out = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
   }
-  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(3);
 }
 
 // Thread per partition: the batch's new log end, matchIndex, quorum commit, high watermark and
@@ -604,13 +676,14 @@ __device__ void stage3_partition(const PipeArgs& A, u32 p) {
 }
 
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
-#define RMQ_PIPE_WAVES_PER_SIMD 6  // 75 VGPRs, no spills: 3 resident workgroups per CU
+#define RMQ_PIPE_WAVES_PER_SIMD 4  // 106 VGPRs, no spills: 2 resident workgroups per CU
 #endif
 __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(PipeArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
     __hip_atomic_store(A.done_word, A.launch_seq - 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   u32 wg = blockIdx.x;
+  if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
   if (wg < A.wg1) {
     stage1_tile(A, wg, *reinterpret_cast<Stage1Smem*>(smem_raw));
     return;
@@ -623,22 +696,36 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   wg -= A.wg2;
   Stage3Smem& S = *reinterpret_cast<Stage3Smem*>(smem_raw);
   const u32 tasks = (A.b3.n + kTaskRecs - 1) / kTaskRecs;
-  u32 task = wg * kPW + (threadIdx.x >> 6);
-  TaskRec R = stage3_load(A, task < tasks ? task : 0u);  // in flight during the table fill
-  for (u32 k = threadIdx.x; k < 8 * 256; k += kPT) (&S.t8[0][0])[k] = (&A.crc->table[0][0])[k];
-  for (u32 k = threadIdx.x; k < 3 * 4 * 256; k += kPT) (&S.z[0][0][0])[k] = (&A.crc->zshift[0][0][0])[k];
-  __syncthreads();
   const u32 lane = threadIdx.x & 63;
-  for (; task < tasks; task += A.wg3 * kPW) {
+  const u32 rej = (u32)A.s3.binfo[0];
+  u32 task = wg * kPW + (threadIdx.x >> 6);
+  PIPE_STAMP(0);
+  // first task: its record and state/payload loads are in flight while the CRC tables fill LDS
+  TaskRec R = stage3_r1(A, task < tasks ? task : 0u);
+  if (!(A.debug & 8u)) {
+    for (u32 k = threadIdx.x; k < 8 * 256; k += kPT) (&S.t8[0][0])[k] = (&A.crc->table[0][0])[k];
+    for (u32 k = threadIdx.x; k < 3 * 4 * 256; k += kPT) (&S.z[0][0][0])[k] = (&A.crc->zshift[0][0][0])[k];
+  }
+  bool cand = task < tasks && stage3_cand(A, task, R, rej);
+  TaskState Z = stage3_r2(A, task, R, cand);
+  __syncthreads();
+  PIPE_STAMP(1);
+  while (task < tasks) {
     uint4 so;
-    stage3_task(A, S, task, R, so);
+    PIPE_STAMP(2);
+    stage3_finish(A, S, task, R, Z, cand, rej, so);
     if (lane == 0) A.stats3[task] = so;
-    const u32 nt = task + A.wg3 * kPW;
-    if (nt < tasks) R = stage3_load(A, nt);
+    PIPE_STAMP(3);
+    task += A.wg3 * kPW;
+    if (task < tasks) {
+      R = stage3_r1(A, task);
+      cand = stage3_cand(A, task, R, rej);
+      Z = stage3_r2(A, task, R, cand);
+    }
   }
   for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wg3 * kPT) stage3_partition(A, p);
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(4);
+  PIPE_STAMP(6);
 }
 
 uint32_t pipeline_lds_bytes() { return (uint32_t)kSmemBytes; }

@@ -12,8 +12,8 @@ import numpy as np
 PHASES = {
     1: ["loads+input scans", "radix passes", "seg scan+writes"],
     2: ["column scans+tile scan"],
-    3: ["records+state issue", "payload, crc, ring stores", "headers/index/offsets",
-        "partition threads (+later tasks)"],
+    3: ["first task r1+tables+r2 issue", "(earlier tasks)", "last task finish", "(unused)",
+        "(unused)", "partition threads"],
 }
 
 
@@ -27,15 +27,19 @@ def main(path):
             r = r[r[:, 1] == 0]
         if not len(r):
             continue
-        t = (r[:, 3:3 + len(names) + 1] - t0).astype(np.float64) * 0.01
-        valid = (r[:, 3:3 + len(names) + 1] > 0).all(axis=1)
-        t = t[valid]
+        raw = r[:, 3:3 + len(names) + 1]
+        valid = (raw[:, 0] > 0) & (raw[:, -1] > 0)
+        t = (raw[valid] - t0).astype(np.float64) * 0.01
+        t[raw[valid] == 0] = np.nan
         if not len(t):
             continue
         print(f" stage {stage}: {len(t)} rows, start p0 {t[:, 0].min():.2f} p50 {np.median(t[:, 0]):.2f} "
               f"max {t[:, 0].max():.2f} | end p50 {np.median(t[:, -1]):.2f} max {t[:, -1].max():.2f} us")
         for k, n in enumerate(names):
             d = t[:, k + 1] - t[:, k]
+            d = d[~np.isnan(d)]
+            if not len(d):
+                continue
             print(f"   {n:>26s}: p10 {np.percentile(d, 10):7.2f} p50 {np.percentile(d, 50):7.2f} "
                   f"p90 {np.percentile(d, 90):7.2f} max {d.max():7.2f} us")
 
