@@ -76,8 +76,6 @@ def main() -> None:
                     help="ring bytes per (replica, partition); a 64k x 128 B batch needs > 8 MiB")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-every", type=int, default=8,
-                    help="bracket every N-th pipeline launch with HIP events (kernel duration)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,17 +122,18 @@ def main() -> None:
     for k in range(args.warmup):
         step(k)
     barrier()
-    eng.profile(args.profile_every)
+    eng.profile(True)  # HIP events bracket the timed region's launches on the engine's stream
     t0 = time.perf_counter()
     last = 0
     for k in range(args.steps):
         last = step(args.warmup + k)
     barrier()
     elapsed = time.perf_counter() - t0
+    n_launch, region_ms = eng.profile_query(0)
+    n_applied, _ = eng.profile_query(1)
     st = eng.wait(last) if last else {}
     if st and st.get("appended") != spec.records:
         raise SystemExit(f"bench: last batch not fully appended ({st}); the measurement would be void")
-    n_app, app_ms = eng.profile_query(0)
     eng.profile(False)
 
     t_max = max_over_ranks(elapsed, dist)
@@ -145,8 +144,8 @@ def main() -> None:
     out = None
     if rank == 0:
         alg = algorithmic_bytes(n, L or 0, rf, spec.partitions)
-        mean_app_s = app_ms / 1e3 / max(n_app, 1)
-        achieved = alg / mean_app_s / 1e9 if n_app else 0.0
+        # algorithmic bytes per launch / mean launch duration = bytes of the applied batches / region
+        achieved = alg * n_applied / (region_ms / 1e3) / 1e9 if n_launch and region_ms > 0 else 0.0
         out = {
             "metric": "committed msgs/sec (node) + HBM GB/s, 100B msgs, 4096 partitions RF=3",
             "value": msgs_per_s,
@@ -169,8 +168,10 @@ def main() -> None:
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "rmq::pipeline_kernel", "algorithmic_bytes_per_launch": alg,
-                         "mean_kernel_us": mean_app_s * 1e6, "timed_launches": n_app},
+                         "kernel": "rmq::pipeline_kernel",
+                         "algorithmic_bytes_per_launch": alg * n_applied / max(n_launch, 1),
+                         "mean_kernel_us": region_ms * 1e3 / max(n_launch, 1), "timed_launches": n_launch,
+                         "batches_per_launch": n_applied / max(n_launch, 1)},
             "append_stats_last": st,
             "device": dev_name,
             "cu_count": cus,

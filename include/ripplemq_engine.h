@@ -205,9 +205,11 @@ int rmq_read_consumer_offsets(rmq_engine* e, uint32_t pidx, uint64_t* out /* max
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out);
 int rmq_device_free(rmq_engine* e, void* p);
 int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int kind /*0 h2d,1 d2h,2 d2d*/);
-/* Kernel timing with HIP events on the engine's stream. enable = N > 0 brackets every N-th
-   pipeline launch with an event pair (0 = off). kernel: 0 pipeline launch, 1 unused,
-   2 commit, 3 fetch-resolve, 4 fetch-gather. */
+/* Kernel timing with HIP events on the engine's stream (enable != 0 turns it on and resets it).
+   kernels 0 and 1: the pipeline launches from the first one after enable up to the next drain
+   (sync, control call, read-back) timed as ONE region (no events between launches): total_ms =
+   region time; launches = pipeline launches in it (kernel 0) or batches they applied (kernel 1).
+   kernels 3 / 4: fetch-resolve / fetch-gather, one event pair per launch. 2: unused. */
 int rmq_profile_enable(rmq_engine* e, int enable);
 int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* total_ms);
 /* Device name / CU count for reports. */

@@ -102,9 +102,13 @@ struct rmq_engine {
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;
   uint32_t ctl_cap = 0;
-  // profiling: HIP event pairs around every `profile`-th pipeline launch (0 = off)
+  // profiling: pipeline launches are timed as one region (event before the first launch after
+  // enable, event at the next drain) so no per-launch events sit between kernels; fetch kernels
+  // keep per-launch event pairs (prof[3], prof[4])
   uint32_t profile = 0;
-  uint64_t prof_count = 0;
+  uint64_t prof_launches = 0, prof_batches = 0;
+  hipEvent_t prof_t0 = nullptr, prof_t1 = nullptr;
+  bool prof_started = false, prof_ended = false;
   std::vector<EvPair> prof[5];
   std::vector<hipEvent_t> ev_pool;
   // diagnostics: RMQ_STAMPS=<csv> records per-wave phase stamps of launch RMQ_STAMPS_AT (default 100)
@@ -280,19 +284,16 @@ int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const I
     e->stamps_wg[1] = a.wg2;
     e->stamps_wg[2] = a.wg3;
   }
-  const bool prof = e->profile && (e->prof_count++ % e->profile) == 0;
-  EvPair ev;
-  if (prof) {
-    ev.a = pool_event(e);
-    ev.b = pool_event(e);
-    HIP_TRY(hipEventRecord(ev.a, e->main_s));
+  if (e->profile && !e->prof_ended) {
+    if (!e->prof_started) {
+      HIP_TRY(hipEventRecord(e->prof_t0, e->main_s));
+      e->prof_started = true;
+    }
+    e->prof_launches++;
+    if (s3) e->prof_batches++;
   }
   launch_pipeline(a, e->main_s);
   HIP_TRY(hipGetLastError());
-  if (prof) {
-    HIP_TRY(hipEventRecord(ev.b, e->main_s));
-    e->prof[0].push_back(ev);
-  }
   if (s3) {
     e->applied++;
     e->st.leo = nxt.leo;
@@ -321,6 +322,10 @@ int flush(rmq_engine* e) {
 int drain(rmq_engine* e) {
   int rc = flush(e);
   if (rc) return rc;
+  if (e->profile && e->prof_started && !e->prof_ended) {
+    HIP_TRY(hipEventRecord(e->prof_t1, e->main_s));
+    e->prof_ended = true;
+  }
   HIP_TRY(hipStreamSynchronize(e->main_s));
   return check_err(e);
 }
@@ -417,6 +422,8 @@ void free_engine(rmq_engine* e) {
       if (p.b) hipEventDestroy(p.b);
     }
   for (hipEvent_t ev : e->ev_pool) hipEventDestroy(ev);
+  if (e->prof_t0) hipEventDestroy(e->prof_t0);
+  if (e->prof_t1) hipEventDestroy(e->prof_t1);
   if (e->main_s) hipStreamDestroy(e->main_s);
   delete e;
 }
@@ -1044,8 +1051,13 @@ int rmq_profile_enable(rmq_engine* e, int enable) {
     }
     v.clear();
   }
-  e->profile = enable > 0 ? (uint32_t)enable : 0u;
-  e->prof_count = 0;
+  e->profile = enable > 0 ? 1u : 0u;
+  e->prof_launches = e->prof_batches = 0;
+  e->prof_started = e->prof_ended = false;
+  if (e->profile && !e->prof_t0) {
+    HIP_TRY(hipEventCreate(&e->prof_t0));
+    HIP_TRY(hipEventCreate(&e->prof_t1));
+  }
   return RMQ_OK;
 }
 
@@ -1055,6 +1067,13 @@ int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* tot
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
   if (rc) return rc;
+  if (kernel <= 1) {  // 0: pipeline launches in the region, 1: batches applied in it
+    float ms = 0;
+    if (e->prof_ended) HIP_TRY(hipEventElapsedTime(&ms, e->prof_t0, e->prof_t1));
+    if (launches) *launches = e->prof_ended ? (kernel ? e->prof_batches : e->prof_launches) : 0;
+    if (total_ms) *total_ms = ms;
+    return RMQ_OK;
+  }
   double tot = 0;
   for (const EvPair& p : e->prof[kernel]) {
     float ms = 0;

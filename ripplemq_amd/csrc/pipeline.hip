@@ -636,7 +636,8 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, 
 __device__ void stage3_partition(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
   const u32 rej = (u32)A.s3.binfo[0];
-  const u64 tot = rej ? 0ull : A.s3.totals[p];
+  // a follower's records are counted by stages 1/2 (ranks are per partition) but never applied
+  const u64 tot = (rej || !st.is_leader[p]) ? 0ull : A.s3.totals[p];
   const u64 tc = tot >> 40, tb = 16ull * (tot & kLow40);
   const u64 leo = A.cur.leo[p], used = A.cur.used[p];
   const u64 so = A.cur.start_off[p], sp = A.cur.start_pos[p];

@@ -19,7 +19,7 @@ def pair(oracle_mod, **kw):
 
 
 def test_small_mixed_sizes(oracle_mod):
-    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=3, segment_bytes=1 << 16,
+    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=3, segment_bytes=1 << 20,
                          index_interval=256, max_batch_records=4096)
     with dev, ora:
         spec = StreamSpec(8, 300, "uniform", size=(0, 700), config_index=11)
@@ -61,7 +61,7 @@ def test_large_records_direct_path(oracle_mod):
 
 
 def test_rejections_and_leadership(oracle_mod):
-    cfg, dev, ora = pair(oracle_mod, num_partitions=16, replication_factor=3, segment_bytes=1 << 16,
+    cfg, dev, ora = pair(oracle_mod, num_partitions=16, replication_factor=3, segment_bytes=1 << 20,
                          index_interval=256, max_batch_records=4096)
     with dev, ora:
         spec = StreamSpec(16, 1500, "uniform", size=(1, 200), config_index=15, invalid_frac=0.05)
@@ -95,7 +95,7 @@ def test_no_space_and_edge_batches(oracle_mod):
 
 def test_explicit_payload_offsets(oracle_mod):
     # caller-provided payload_off with gaps and unaligned starts
-    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=2, segment_bytes=1 << 16,
+    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=2, segment_bytes=1 << 20,
                          index_interval=256, max_batch_records=4096)
     with dev, ora:
         g = np.random.default_rng(7)
@@ -112,7 +112,8 @@ def test_consumer_fetch_paths(oracle_mod):
     cfg, dev, ora = pair(oracle_mod, num_partitions=32, replication_factor=3, segment_bytes=1 << 16,
                          index_interval=256, max_consumers=4, max_batch_records=8192)
     with dev, ora:
-        spec = StreamSpec(32, 3000, "zipf", size=(1, 180), config_index=17)
+        # 450 records (~50 KB) per batch fit the 64 KB rings; hot partitions wrap them (eviction)
+        spec = StreamSpec(32, 450, "zipf", size=(1, 180), config_index=17)
         g = np.random.default_rng(3)
         ops = []
         for b in range(8):
