@@ -3,19 +3,22 @@
 
 Workload (BASELINE.json configs[2], the metric's configuration): per GPU, 4096 partitions,
 RF = 3 replicas co-located, Zipf(s = 1.1) partition load over a random permutation of ranks,
-100-byte records in 65536-record batches. One step = one rmq_append of one batch: stable
-partition sort, offsets, CRC32C, three replica copies, sparse index, quorum commit, high
-watermark. Inputs are resident in HBM before timing (a pool of distinct batches larger than the
-256 MiB Infinity Cache, so payload reads come from HBM).
+100-byte records in 65536-record batches. One step = one rmq_append of one batch: partition
+ranking, offsets, CRC32C, three replica copies, sparse index, quorum commit, high watermark,
+retention. Inputs are resident in HBM before timing (a pool of distinct batches larger than the
+256 MiB Infinity Cache, so payload reads come from HBM). The engine applies the batches in launch
+groups of --group (cfg.pipeline_depth); every batch keeps its own semantics.
 
 Multi-GPU: one process per GPU (torch.distributed.run); partitions shard by GPU (4096 per GPU,
 config C's layout) with no data-path collective -> weak scaling. The barrier and the max-over-
 ranks of the timed region use torch.distributed over gloo (host side); the engine itself never
 touches torch.
 
-roofline: achieved = algorithmic bytes per append launch / mean append-kernel duration, timed
-with HIP events on the engine's own stream inside the timed region; algorithmic bytes per record
-= (8 + L) read + RF * (16 + L) written, plus RF*8 + 16 per partition per batch.
+roofline: achieved = algorithmic bytes per launch / mean launch duration = algorithmic bytes of
+the batches applied in the timed region / the region's time between HIP events recorded on the
+engine's own stream before its first and after its last launch (rmq_profile_*); algorithmic bytes
+per record = (8 + L) read + RF * (16 + L) written, plus RF*8 + 16 per partition
+per batch.
 """
 from __future__ import annotations
 
@@ -76,6 +79,8 @@ def main() -> None:
                     help="ring bytes per (replica, partition); a 64k x 128 B batch needs > 8 MiB")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--group", type=int, default=4,
+                    help="batches per pipeline launch group (cfg.pipeline_depth, 1..4)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,7 +98,7 @@ def main() -> None:
     cfg = EngineConfig(num_partitions=spec.partitions, replication_factor=rf,
                        segment_bytes=args.segment_mb << 20, index_interval=1024,
                        max_batch_records=spec.records, max_batch_bytes=64 << 20,
-                       pipeline_depth=3, device=local_rank, rank=0)
+                       pipeline_depth=args.group, device=local_rank, rank=0)
     eng = Engine(cfg)
     dev_name, cus = eng.device_info()
 
@@ -164,7 +169,7 @@ def main() -> None:
                                    f"{L} B records, {n} records/batch",
                        "partitions_per_gpu": spec.partitions, "replication_factor": rf,
                        "records_per_batch": n, "record_payload_bytes": L,
-                       "parallelism": f"partition-sharded x{world}"},
+                       "parallelism": f"partition-sharded x{world}", "batches_per_launch_group": args.group},
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,

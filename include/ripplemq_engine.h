@@ -77,7 +77,7 @@ typedef struct rmq_config {
   uint32_t index_interval;     /* sparse offset-index interval in bytes; power of two in [64, 1<<20] */
   uint32_t max_consumers;      /* consumer-offset table width per partition (dense consumer ids) */
   uint32_t max_batch_records;  /* capacity of one rmq_append call */
-  uint32_t pipeline_depth;     /* append batches allowed in flight (>= 1); 0 -> default 3 */
+  uint32_t pipeline_depth;     /* batches applied per pipeline launch group, 1..4; 0 -> default 2 */
   uint64_t max_batch_bytes;    /* payload bytes of one rmq_append call */
   int32_t device;              /* HIP device ordinal */
   uint32_t rank;               /* replica rank of this engine (placement in rmq_set_replicas) */
@@ -162,9 +162,11 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
    offset of each record, or RMQ_OFFSET_NONE if it was rejected (not leader / unknown pidx).
    If the batch's total record bytes (sum of 16 + align16(len)) exceed segment_bytes -
    index_interval, no record is appended (rmq_ticket_stats reports rejected_no_space).
-   Each call issues one kernel launch that also advances the two batches submitted before it;
-   a batch is applied by the second launch after its own, or when rmq_poll_commit /
-   rmq_ticket_stats / rmq_sync / any control call flushes the pipeline. */
+   Batches are collected into launch groups of up to cfg.pipeline_depth: the call that fills a
+   group issues one kernel launch that ranks it and advances the three groups submitted before
+   it (scan, apply, retention); every batch keeps its own semantics. A batch is applied by the
+   second launch after its group's own, or when rmq_poll_commit / rmq_ticket_stats / rmq_sync /
+   any control call closes the forming group and flushes the pipeline. */
 int rmq_append(rmq_engine* e, const rmq_batch* batch, uint64_t* out_offsets, uint64_t* ticket);
 
 /* External replica acks (followers on other ranks): match[slot] = max(match[slot],

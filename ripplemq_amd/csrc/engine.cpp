@@ -1,11 +1,13 @@
 // engine.cpp — host side of the C-ABI (include/ripplemq_engine.h).
 //
 // Owns all device memory of one engine (one HIP device): per-(replica, partition) ring segments,
-// the sparse offset index, per-partition Raft state and consumer offsets. Each rmq_append issues
-// exactly ONE kernel launch (pipeline.hip): it ranks the new batch (stage 1), scans the previous
-// batch (stage 2) and applies the one before (stage 3). A batch is therefore complete two launches
-// after its own; rmq_poll_commit / rmq_sync / any control call flush the pipeline with up to two
-// launches that carry only stages 2-3. No host synchronisation and no HIP events sit on the
+// the sparse offset index, per-partition Raft state and consumer offsets. Appended batches are
+// collected into groups of up to cfg.pipeline_depth; each full group issues exactly ONE kernel
+// launch (pipeline.hip) that ranks it (stage 1), scans the group before (stage 2), applies the one
+// before that (stage 3) and evaluates the retention of the one before that (stage 4). A batch is
+// therefore applied two launches after its group's own; rmq_poll_commit / rmq_sync / any control
+// call close the forming group and flush the pipeline with up to three more launches that carry
+// only the later stages. No host synchronisation and no HIP events sit on the
 // append path: launch k reports launch k-1 complete through a host-visible word, and the tail is
 // read with hipStreamQuery. Control-plane calls (leadership, replicas, acks, consumer offsets,
 // fetch) flush and drain first and run synchronously: they are rare next to the append stream.
@@ -30,7 +32,7 @@ namespace {
 
 constexpr uint32_t kStatsRing = 64;                                // tickets whose stats stay readable
 constexpr uint32_t kMaxBatchRecords = kMaxTiles * kTileRecs;       // 262144
-constexpr uint32_t kSets = 3;                                      // pipeline scratch sets
+constexpr uint32_t kSets = 4;                                      // pipeline scratch sets
 
 struct EvPair {
   hipEvent_t a = nullptr, b = nullptr;
@@ -50,8 +52,14 @@ struct Staging {
 struct InFlight {
   uint64_t ticket = 0;
   PipeBatch b{};
-  uint32_t set = 0;             // scratch set = ticket % kSets
   uint64_t* host_out = nullptr;  // host batches: caller's out_offsets
+};
+
+// A group of consecutive batches moving through the pipeline together (one launch per stage).
+struct GroupFlight {
+  uint32_t nb = 0, tiles = 0, tasks = 0;
+  uint32_t set = 0;              // scratch set = group number % kSets
+  InFlight b[kMaxGroup];
 };
 
 }  // namespace
@@ -63,7 +71,7 @@ struct rmq_engine {
   uint32_t cu_count = 0;
   char dev_name[256] = {0};
   hipStream_t main_s = nullptr;
-  DevState st{};            // leo/used/start_off/start_pos point at sets[applied & 1]
+  DevState st{};            // leo/used point at sets[applied & 1]
   StateSet sets[2]{};
   uint64_t applied = 0;     // stage-3 launches issued
   CrcConsts* d_crc = nullptr;
@@ -76,9 +84,13 @@ struct rmq_engine {
   uint32_t epoch = 0;
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
-  // pipeline
-  bool has1 = false, has2 = false;  // batch ranked (needs stage 2) / scanned (needs stage 3)
-  InFlight st1, st2;
+  // pipeline: the group being formed, then groups ranked (need stage 2), scanned (need stage 3)
+  // and applied (need stage 4)
+  GroupFlight forming, g1, g2, g3;
+  bool has1 = false, has2 = false, has3 = false;
+  uint32_t group_max = 2;       // batches per group (cfg.pipeline_depth)
+  uint32_t max_group_tiles = 0;
+  uint64_t groups = 0;          // groups formed
   uint64_t launch_seq = 0;
   uint64_t* done_host = nullptr;     // pinned: launch k-1 complete, written by launch k
   uint64_t* done_dev = nullptr;
@@ -115,7 +127,7 @@ struct rmq_engine {
   const char* stamps_path = nullptr;
   uint64_t stamps_at = 100;
   uint64_t* d_stamps = nullptr;
-  uint32_t stamps_wg[3] = {0, 0, 0};
+  uint32_t stamps_wg[4] = {0, 0, 0, 0};
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
 };
 
@@ -241,8 +253,30 @@ hipEvent_t pool_event(rmq_engine* e) {
   return ev;
 }
 
-// One pipeline launch: stage 1 on `s1`, stage 2 on `s2`, stage 3 on `s3` (each may be null).
-int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const InFlight* s3) {
+PipeGroup make_group(const rmq_engine* e, const GroupFlight& g) {
+  PipeGroup G{};
+  uint32_t tile = 0, task = 0;
+  for (uint32_t j = 0; j < kMaxGroup; ++j) {
+    G.tile0[j] = tile;
+    G.task0[j] = task;
+    if (j < g.nb) {
+      const InFlight& f = g.b[j];
+      G.b[j] = f.b;
+      G.stats[j] = e->d_stats + (size_t)(f.ticket % kStatsRing) * e->max_tasks;
+      tile += f.b.tiles;
+      task += (f.b.n + kTaskRecs - 1) / kTaskRecs;
+    }
+  }
+  G.tile0[kMaxGroup] = tile;
+  G.task0[kMaxGroup] = task;
+  G.nb = g.nb;
+  G.tiles = tile;
+  return G;
+}
+
+// One pipeline launch: stage 1 on group s1, 2 on s2, 3 on s3, 4 on s4 (each may be null).
+int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, const GroupFlight* s3,
+                  const GroupFlight* s4) {
   PipeArgs a{};
   const uint32_t P = e->cfg.num_partitions;
   const StateSet cur = e->sets[e->applied & 1u], nxt = e->sets[(e->applied + 1) & 1u];
@@ -255,34 +289,38 @@ int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const I
   a.done_word = e->done_dev;
   a.debug = e->debug;
   if (s1) {
-    a.b1 = s1->b;
+    a.g1 = make_group(e, *s1);
     a.s1 = e->scratch[s1->set];
-    a.wg1 = s1->b.tiles;
+    a.wg1 = s1->tiles;
   }
   if (s2) {
-    a.b2 = s2->b;
+    a.g2 = make_group(e, *s2);
     a.s2 = e->scratch[s2->set];
     a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + kPipeThreads - 1) / kPipeThreads, 2u * e->cu_count));
   }
+  if (s3 || s4) a.wgp = (P + kPipeThreads - 1) / kPipeThreads;
+  if (s4) {
+    a.g4 = make_group(e, *s4);
+    a.s4 = e->scratch[s4->set];
+  }
   if (s3) {
-    a.b3 = s3->b;
+    a.g3 = make_group(e, *s3);
     a.s3 = e->scratch[s3->set];
-    const uint32_t tasks = (s3->b.n + kTaskRecs - 1) / kTaskRecs;
     const uint32_t wpb = kPipeThreads / 64;
-    const uint32_t want = std::max((tasks + wpb - 1) / wpb, (P + kPipeThreads - 1) / kPipeThreads);
-    // fill the chip next to the stage-1/2 workgroups of this launch (resident workgroups per CU
-    // from the kernel's launch bounds)
-    const uint32_t slots = pipeline_wgs_per_cu() * e->cu_count;
-    const uint32_t room = slots > a.wg1 + a.wg2 + e->cu_count ? slots - a.wg1 - a.wg2 : e->cu_count;
-    a.wg3 = std::max<uint32_t>(1u, std::min<uint32_t>(want, room));
-    a.stats3 = e->d_stats + (size_t)(s3->ticket % kStatsRing) * e->max_tasks;
+    const uint32_t want = std::max<uint32_t>(1u, (s3->tasks + wpb - 1) / wpb);
+    // fill the chip next to the other roles of this launch (resident workgroups per CU from the
+    // kernel's launch bounds); the task waves loop over the rest
+    const uint32_t slots = pipeline_wgs_per_cu() * e->cu_count, busy = a.wg1 + a.wg2 + a.wgp;
+    const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
+    a.wg3 = std::min<uint32_t>(want, room);
   }
   a.launch_seq = ++e->launch_seq;
   if (e->d_stamps && a.launch_seq == e->stamps_at) {
     a.stamps = e->d_stamps;
     e->stamps_wg[0] = a.wg1;
     e->stamps_wg[1] = a.wg2;
-    e->stamps_wg[2] = a.wg3;
+    e->stamps_wg[2] = a.wgp;
+    e->stamps_wg[3] = a.wg3;
   }
   if (e->profile && !e->prof_ended) {
     if (!e->prof_started) {
@@ -290,7 +328,7 @@ int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const I
       e->prof_started = true;
     }
     e->prof_launches++;
-    if (s3) e->prof_batches++;
+    if (s3) e->prof_batches += s3->nb;
   }
   launch_pipeline(a, e->main_s);
   HIP_TRY(hipGetLastError());
@@ -298,23 +336,37 @@ int launch_stages(rmq_engine* e, const InFlight* s1, const InFlight* s2, const I
     e->applied++;
     e->st.leo = nxt.leo;
     e->st.used = nxt.used;
-    e->st.start_off = nxt.start_off;
-    e->st.start_pos = nxt.start_pos;
-    e->ticket_launch[s3->ticket % kStatsRing] = e->launch_seq;
-    if (s3->host_out && s3->b.n)
-      HIP_TRY(hipMemcpyAsync(s3->host_out, s3->b.out_offsets, s3->b.n * 8ull, hipMemcpyDeviceToHost, e->main_s));
+    for (uint32_t j = 0; j < s3->nb; ++j) {
+      const InFlight& f = s3->b[j];
+      e->ticket_launch[f.ticket % kStatsRing] = e->launch_seq;
+      if (f.host_out && f.b.n)
+        HIP_TRY(hipMemcpyAsync(f.host_out, f.b.out_offsets, f.b.n * 8ull, hipMemcpyDeviceToHost, e->main_s));
+    }
   }
   return RMQ_OK;
 }
 
-// Push everything in the pipeline through stage 3 (at most two launches).
+// One launch: ranks the group being formed (if any) and advances the groups ahead of it.
+int close_group(rmq_engine* e) {
+  const GroupFlight* s1 = e->forming.nb ? &e->forming : nullptr;
+  int rc = launch_stages(e, s1, e->has1 ? &e->g1 : nullptr, e->has2 ? &e->g2 : nullptr,
+                         e->has3 ? &e->g3 : nullptr);
+  if (rc) return rc;
+  e->has3 = e->has2;
+  e->g3 = e->g2;
+  e->has2 = e->has1;
+  e->g2 = e->g1;
+  e->has1 = s1 != nullptr;
+  if (s1) e->g1 = e->forming;
+  e->forming = GroupFlight{};
+  return RMQ_OK;
+}
+
+// Push everything through stage 4 (at most four launches).
 int flush(rmq_engine* e) {
-  while (e->has1 || e->has2) {
-    int rc = launch_stages(e, nullptr, e->has1 ? &e->st1 : nullptr, e->has2 ? &e->st2 : nullptr);
+  while (e->forming.nb || e->has1 || e->has2 || e->has3) {
+    int rc = close_group(e);
     if (rc) return rc;
-    e->has2 = e->has1;
-    e->st2 = e->st1;
-    e->has1 = false;
   }
   return RMQ_OK;
 }
@@ -368,7 +420,7 @@ int ensure_ctl(rmq_engine* e, uint32_t n) {
 }
 
 void dump_stamps(rmq_engine* e) {
-  const uint32_t nwg = e->stamps_wg[0] + e->stamps_wg[1] + e->stamps_wg[2];
+  const uint32_t nwg = e->stamps_wg[0] + e->stamps_wg[1] + e->stamps_wg[2] + e->stamps_wg[3];
   if (!e->stamps_path || !e->d_stamps || !nwg) return;
   std::vector<uint64_t> h((size_t)nwg * 64);
   if (hipMemcpy(h.data(), e->d_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
@@ -376,7 +428,8 @@ void dump_stamps(rmq_engine* e) {
   if (!f) return;
   std::fprintf(f, "wg,wave,stage,t0,t1,t2,t3,t4,t5,t6,t7\n");
   for (uint32_t g = 0; g < nwg; ++g) {
-    const int stage = g < e->stamps_wg[0] ? 1 : g < e->stamps_wg[0] + e->stamps_wg[1] ? 2 : 3;
+    const uint32_t a1 = e->stamps_wg[0], a2 = a1 + e->stamps_wg[1], a3 = a2 + e->stamps_wg[2];
+    const int stage = g < a1 ? 1 : g < a2 ? 2 : g < a3 ? 4 : 3;  // 4: partition threads
     for (uint32_t w = 0; w < 8; ++w) {
       std::fprintf(f, "%u,%u,%d", g, w, stage);
       for (int k = 0; k < 8; ++k) std::fprintf(f, ",%llu", (unsigned long long)h[((size_t)g * 8 + w) * 8 + k]);
@@ -395,18 +448,16 @@ void free_engine(rmq_engine* e) {
     dump_stamps(e);
   }
   DevState& s = e->st;
-  std::vector<void*> bufs = {s.commit, s.hw, s.term_start, s.match, s.is_leader, s.local_mask, s.index,
-                             s.logs, s.cons, e->d_crc, e->d_winner, e->d_err, e->d_stats, e->d_req,
-                             e->d_res, e->d_aux, e->d_total, e->d_fetch_out, e->d_ctl32, e->d_ctl64,
-                             e->d_stamps};
+  std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match, s.is_leader,
+                             s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner, e->d_err,
+                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_total, e->d_fetch_out,
+                             e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
     bufs.push_back(z.used);
-    bufs.push_back(z.start_off);
-    bufs.push_back(z.start_pos);
   }
   for (const PipeScratch& x : e->scratch) {
-    void* xs[] = {x.hist, x.excl, x.totals, x.crank, x.pre, x.tsum, x.tile_base, x.binfo};
+    void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo};
     for (void* p : xs) bufs.push_back(p);
   }
   for (const Staging& sg : e->staging) {
@@ -438,6 +489,9 @@ int validate_cfg(const rmq_config* c) {
   if (c->max_consumers == 0) return RMQ_EINVAL;
   if (c->max_batch_records == 0 || c->max_batch_records > kMaxBatchRecords) return RMQ_EINVAL;
   if (c->max_batch_bytes >= (1ull << 32)) return RMQ_EINVAL;
+  if (c->pipeline_depth > kMaxGroup) return RMQ_EINVAL;
+  const uint64_t g = c->pipeline_depth ? c->pipeline_depth : 2u;
+  if ((2 * g + 1) * (c->segment_bytes / c->index_interval) + 2 >= (1ull << 32)) return RMQ_EINVAL;
   return RMQ_OK;
 }
 
@@ -471,7 +525,7 @@ void rmq_config_default(rmq_config* c, uint32_t P, uint32_t RF) {
   c->index_interval = 1024;
   c->max_consumers = 8;
   c->max_batch_records = 65536;
-  c->pipeline_depth = 3;
+  c->pipeline_depth = 2;
   c->max_batch_bytes = 64ull << 20;
   c->device = 0;
   c->rank = 0;
@@ -488,7 +542,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   rmq_engine* e = new (std::nothrow) rmq_engine();
   if (!e) return RMQ_ENOMEM;
   e->cfg = *cfg;
-  if (!e->cfg.pipeline_depth) e->cfg.pipeline_depth = 3;
+  if (!e->cfg.pipeline_depth) e->cfg.pipeline_depth = 2;
   e->device = cfg->device;
   e->stamps_path = std::getenv("RMQ_STAMPS");
   if (const char* v = std::getenv("RMQ_DEBUG")) e->debug = (uint32_t)std::atoi(v);
@@ -516,17 +570,19 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   s.C = C;
   s.seg = cfg->segment_bytes;
   s.interval_log2 = ilog2(cfg->index_interval);
-  s.icap = (uint32_t)(cfg->segment_bytes / cfg->index_interval + 2);
+  e->group_max = std::min<uint32_t>(kMaxGroup, e->cfg.pipeline_depth);
+  // stage 4 reads a group's index entries while stage 3 of the group two later writes new ones
+  // (each batch adds at most segment - interval bytes to a partition): 2G + 1 segments of entries
+  // keep every entry stage 4 may read from being overwritten in time
+  s.icap = (uint32_t)((2ull * e->group_max + 1ull) * (cfg->segment_bytes / cfg->index_interval) + 2ull);
   for (StateSet& z : e->sets) {
     CREATE_TRY(dalloc(&z.leo, P));
     CREATE_TRY(dalloc(&z.used, P));
-    CREATE_TRY(dalloc(&z.start_off, P));
-    CREATE_TRY(dalloc(&z.start_pos, P));
   }
   s.leo = e->sets[0].leo;
   s.used = e->sets[0].used;
-  s.start_off = e->sets[0].start_off;
-  s.start_pos = e->sets[0].start_pos;
+  CREATE_TRY(dalloc(&s.start_off, P));
+  CREATE_TRY(dalloc(&s.start_pos, P));
   CREATE_TRY(dalloc(&s.commit, P));
   CREATE_TRY(dalloc(&s.hw, P));
   CREATE_TRY(dalloc(&s.term_start, P));
@@ -541,16 +597,18 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
   CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));
+  e->max_group_tiles = std::min<uint32_t>(kMaxTiles, e->group_max * e->max_tiles);
   for (PipeScratch& x : e->scratch) {
-    const size_t TP = (size_t)e->max_tiles * P;
+    const size_t GT = e->max_group_tiles, TP = GT * P;
     CREATE_TRY(dalloc(&x.hist, TP));
     CREATE_TRY(dalloc(&x.excl, TP));
     CREATE_TRY(dalloc(&x.totals, P));
-    CREATE_TRY(dalloc(&x.crank, cfg->max_batch_records));
-    CREATE_TRY(dalloc(&x.pre, cfg->max_batch_records));
-    CREATE_TRY(dalloc(&x.tsum, (size_t)e->max_tiles * 4));
-    CREATE_TRY(dalloc(&x.tile_base, e->max_tiles));
-    CREATE_TRY(dalloc(&x.binfo, 4));
+    CREATE_TRY(dalloc(&x.bcum, (size_t)kMaxGroup * P));
+    CREATE_TRY(dalloc(&x.crank, GT * kTileRecs));
+    CREATE_TRY(dalloc(&x.pre, GT * kTileRecs));
+    CREATE_TRY(dalloc(&x.tsum, GT * 4));
+    CREATE_TRY(dalloc(&x.tile_base, GT));
+    CREATE_TRY(dalloc(&x.binfo, (size_t)kMaxGroup * 4));
   }
   if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(4u * e->cu_count + 2u * kMaxTiles) * 64));
   CREATE_HIP(hipHostMalloc((void**)&e->done_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
@@ -579,7 +637,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     while ((1u << bits) < P) ++bits;  // keys in [0, P)
     e->key_passes = bits == 0 ? 0u : bits <= 8 ? 1u : 2u;
   }
-  e->staging.resize(std::max<uint32_t>(e->cfg.pipeline_depth, kSets) + 1);
+  e->staging.resize(4u * e->group_max + 1u);  // batches of the forming group and of three in flight
   CREATE_HIP(hipDeviceSynchronize());
   *out = e;
   return RMQ_OK;
@@ -668,7 +726,6 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
 
   InFlight f;
   f.ticket = t;
-  f.set = (uint32_t)(t % kSets);
   f.b.pidx = b->pidx;
   f.b.len = b->len;
   f.b.poff = b->payload_off;
@@ -706,13 +763,16 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     f.b.out_offsets = sg.d_out;
     f.host_out = out_offsets;
   }
-  int rc = launch_stages(e, &f, e->has1 ? &e->st1 : nullptr, e->has2 ? &e->st2 : nullptr);
-  if (rc) return rc;
-  e->has2 = e->has1;
-  e->st2 = e->st1;
-  e->has1 = true;
-  e->st1 = f;
-  return RMQ_OK;
+  if (e->forming.nb && e->forming.tiles + f.b.tiles > e->max_group_tiles) {
+    int rc = close_group(e);
+    if (rc) return rc;
+  }
+  GroupFlight& fg = e->forming;
+  if (!fg.nb) fg.set = (uint32_t)(e->groups++ % kSets);
+  fg.b[fg.nb++] = f;
+  fg.tiles += f.b.tiles;
+  fg.tasks += (n + kTaskRecs - 1) / kTaskRecs;
+  return fg.nb >= e->group_max ? close_group(e) : RMQ_OK;
 }
 
 int rmq_ack(rmq_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n) {
@@ -928,8 +988,19 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     if (x.status == RMQ_ENOSPC) rc_all = RMQ_ENOSPC;
   }
   if (mem == RMQ_MEM_HOST && out_cap) {
-    const uint64_t nb = std::min(total, out_cap);
-    if (nb) HIP_TRY(hipMemcpy(out, d_out, nb, hipMemcpyDeviceToHost));
+    // copy back the byte runs of the served requests only: the regions of requests that did not
+    // fit stay untouched in the caller's buffer, as with a device buffer the gather writes itself
+    uint64_t lo = 0, hi = 0;
+    for (uint32_t r = 0; r <= n; ++r) {
+      const bool served = r < n && res[r].status == RMQ_OK && res[r].bytes;
+      if (served && res[r].out_pos == hi && hi > lo) {
+        hi += res[r].bytes;
+        continue;
+      }
+      if (hi > lo) HIP_TRY(hipMemcpy(out + lo, d_out + lo, hi - lo, hipMemcpyDeviceToHost));
+      lo = hi = served ? res[r].out_pos : 0;
+      if (served) hi += res[r].bytes;
+    }
   }
   if (bytes_used) *bytes_used = total;
   return rc_all;

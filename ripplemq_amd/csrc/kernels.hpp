@@ -9,9 +9,10 @@ namespace rmq {
 constexpr uint32_t kPipeThreads = 512;   // 8 waves per workgroup, every role of the pipeline launch
 constexpr uint32_t kTileRecs = 1024;     // records per ranking tile (stage 1)
 constexpr uint32_t kTileIdxBits = 10;    // log2(kTileRecs)
-constexpr uint32_t kMaxTiles = 256;      // max_batch_records <= kMaxTiles * kTileRecs
+constexpr uint32_t kMaxTiles = 256;      // tiles per group; max_batch_records <= kMaxTiles * kTileRecs
 constexpr uint32_t kScanLanes = 8;       // stage 2: threads per partition column
 constexpr uint32_t kTaskRecs = 32;       // records per apply task (one wave, 2 lanes per record)
+constexpr uint32_t kMaxGroup = 4;        // batches per pipeline group (cfg.pipeline_depth)
 constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-bit LDS radix passes)
 constexpr uint32_t kMaxRF = 8;
 
@@ -19,10 +20,10 @@ struct CrcConsts;
 
 // Per-partition device state (SoA, [P] unless noted). Owned by the engine.
 struct DevState {
-  // leo / used / start_off / start_pos point at the CURRENT state set (see StateSet)
+  // leo / used point at the CURRENT state set (see StateSet)
   uint64_t* leo;         // log end offset (next offset)
   uint64_t* used;        // log end byte position (logical)
-  uint64_t* start_off;   // retained log start
+  uint64_t* start_off;   // retained log start (pipeline stage 4 updates it in place)
   uint64_t* start_pos;
   uint64_t* commit;
   uint64_t* hw;
@@ -40,13 +41,11 @@ struct DevState {
   uint32_t pad;
 };
 
-// Double-buffered per-partition log-position state: apply #a reads set a&1 and writes set (a+1)&1,
-// so records can read their partition's batch-start state while its new state is being written.
+// Double-buffered per-partition log end: the apply of group #a reads set a&1 and writes set
+// (a+1)&1, so records can read their partition's group-start state while its new one is written.
 struct StateSet {
   uint64_t* leo;
   uint64_t* used;
-  uint64_t* start_off;
-  uint64_t* start_pos;
 };
 
 // One append batch as the pipeline sees it (device pointers).
@@ -61,36 +60,48 @@ struct PipeBatch {
   uint32_t tiles;              // ceil(n / kTileRecs)
 };
 
-// Batch-local scratch of one pipeline set (three sets rotate: a batch is ranked in launch k,
-// scanned in launch k+1 and applied in launch k+2).
-struct PipeScratch {
-  uint64_t* hist;       // [tiles][P] tile aggregate {count << 40 | bytes/16}; 0 = absent (stage 2 clears)
-  uint64_t* excl;       // [tiles][P] exclusive prefix of the aggregates over tiles (present entries only)
-  uint64_t* totals;     // [P] batch aggregate per partition
-  uint2* crank;         // [n] {rank in tile run | flags << 29, bytes/16 before it in the tile run}
-  uint32_t* pre;        // [n] payload bytes before the record inside its tile (packed payloads)
-  uint64_t* tsum;       // [tiles][4] {payload bytes, record bytes, invalid records, 0}
-  uint64_t* tile_base;  // [tiles] payload offset of the tile's first record (packed payloads)
-  uint64_t* binfo;      // [4] {reject flags (1 no space, 2 invalid), record bytes, payload bytes, 0}
+// A group of up to kMaxGroup consecutive batches moving through the pipeline together. Batch j
+// owns the group tiles [tile0[j], tile0[j+1]) and the stage-3 tasks [task0[j], task0[j+1]).
+struct PipeGroup {
+  PipeBatch b[kMaxGroup];
+  uint4* stats[kMaxGroup];        // per batch: [tasks] {appended, not leader, unknown partition,
+                                  //   no space | invalid << 16}
+  uint32_t tile0[kMaxGroup + 1];
+  uint32_t task0[kMaxGroup + 1];
+  uint32_t nb;                    // batches (0: the stage is absent from the launch)
+  uint32_t tiles;                 // tile0[nb]
 };
 
-// The single per-batch launch: stage 1 (rank tiles of batch k), stage 2 (column scans of batch
-// k-1), stage 3 (apply batch k-2). Any stage may be absent (count 0).
+// Group-local scratch of one pipeline set (four sets rotate: a group is ranked in launch k,
+// scanned in k+1, applied in k+2 and its retention evaluated in k+3).
+struct PipeScratch {
+  uint64_t* hist;       // [tiles][P] tile aggregate {count << 40 | bytes/16}; 0 = absent (stage 2 clears)
+  uint64_t* excl;       // [tiles][P] exclusive prefix over the group's tiles of applied batches
+  uint64_t* totals;     // [P] group aggregate over applied batches
+  uint64_t* bcum;       // [kMaxGroup][P] aggregate through batch j (applied batches)
+  uint2* crank;         // [tiles * kTileRecs] {rank in tile run | flags << 29, bytes/16 before it in the run}
+  uint32_t* pre;        // [tiles * kTileRecs] payload bytes before the record inside its tile
+  uint64_t* tsum;       // [tiles][4] {payload bytes, record bytes, invalid records, 0}
+  uint64_t* tile_base;  // [tiles] payload offset of the tile's first record inside its batch
+  uint64_t* binfo;      // [kMaxGroup][4] per batch {reject flags (1 no space, 2 invalid), record bytes, payload bytes, 0}
+};
+
+// The single per-group launch: stage 1 (rank the tiles of group k), stage 2 (column scans of
+// group k-1), stage 3 (apply group k-2) and stage 4 (retention of group k-3). Any may be absent.
 struct PipeArgs {
   DevState st;
-  StateSet cur, nxt;    // stage 3: read cur, write nxt
-  PipeBatch b1, b2, b3;
-  PipeScratch s1, s2, s3;
-  uint32_t wg1, wg2, wg3;  // workgroups per stage, in this order along blockIdx.x
+  StateSet cur, nxt;       // stage 3: read cur, write nxt; stage 4: cur = log end after its group
+  PipeGroup g1, g2, g3, g4;
+  PipeScratch s1, s2, s3, s4;
+  uint32_t wg1, wg2, wgp, wg3;  // workgroups per role, in this order along blockIdx.x
   uint32_t key_passes;     // 1 (P <= 256) or 2
+  uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
+                           // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
+                           // 16 skip stages 1-2
   uint64_t nospace_limit;  // segment - interval
   const CrcConsts* crc;
-  uint4* stats3;           // [tasks] {appended, not leader, unknown partition, no space | invalid << 16}
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
   uint64_t launch_seq;
-  uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
-                           // stores, 2 no CRC lookups, 4 no payload loads
-  uint32_t pad0;
   uint64_t* stamps;        // diagnostic only (RMQ_STAMPS): [workgroup][wave][8] s_memrealtime, or null
 };
 

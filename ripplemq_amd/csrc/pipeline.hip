@@ -1,5 +1,6 @@
-// pipeline.hip — the append path as ONE launch per batch: a three-stage software pipeline whose
-// stages work on three different batches at once, so no stage waits on another inside a launch.
+// pipeline.hip — the append path as a four-stage software pipeline over GROUPS of batches: one
+// launch ranks group g, scans group g-1, applies group g-2 and evaluates retention of group g-3,
+// so no stage waits on another inside a launch.
 //
 // Reference semantics restated (file:line relative to the reference root):
 //   PartitionStateMachine.onApply / handleMessageAppendRequest — messages.addAll(batch): record j of
@@ -9,20 +10,26 @@
 //   jraft BallotBox quorum commit: commit = k-th largest matchIndex, k = RF/2 + 1,
 //   when that entry is from the current term. Log bytes, index and retention: FORMAT.md.
 //
-// Stage 1 (batch k, workgroup per 1024-record tile, no inter-workgroup traffic): stable LDS radix
-//   sort of the tile by partition id (two 8-bit passes, ballot-match ranks), a segmented scan of
-//   {1, record bytes/16} over the sorted tile, which gives every record its count / byte rank
-//   inside its partition's run in the tile, and the tile aggregate of each present partition,
-//   written sparsely into hist[tile][p]. Also the tile's payload prefix (packed payloads) and sums.
-// Stage 2 (batch k-1, 8 threads per partition): exclusive scan of hist[.][p] over the tiles ->
-//   excl[tile][p] and totals[p]; clears hist for reuse. Workgroup 0 scans the tile sums
-//   (payload bases, batch record bytes -> the no-space rule).
-// Stage 3 (batch k-2, wave per 32-record task): offset = log end + excl + rank, position likewise,
-//   out offsets, sparse index, then the records' 16-byte pieces are spread over the 64 lanes:
-//   coalesced-per-record payload loads, CRC32C of each piece from LDS tables (shifted into place
-//   by zero-byte tables, XOR-reduced per record), 16-byte stores into every local replica ring;
-//   headers last. Thread per partition: new log end, matchIndex, quorum commit, high watermark,
-//   retention — into the other state set, so no record ever reads a half-updated partition.
+// A group is up to kMaxGroup consecutive batches (engine.cpp forms them). Every batch keeps its own
+// semantics: offsets in batch order, the no-space rule, its stats, retention after the batch.
+// Stage 1 (group g, workgroup per 1024-record tile of one batch, no inter-workgroup traffic):
+//   stable LDS radix sort of the tile by partition id (8-bit passes, ballot-match ranks), a
+//   segmented scan of {1, record bytes/16} over the sorted tile, which gives every record its
+//   count / byte rank inside its partition's run in the tile, and the tile aggregate of each
+//   present partition, written sparsely into hist[tile][p]. Also the tile's payload prefix and sums.
+// Stage 2 (group g-1, 8 threads per partition): the batch rules (no space, invalid payload ranges)
+//   from the tile sums, then an exclusive scan of hist[.][p] over the group's tiles that skips
+//   rejected batches -> excl[tile][p], the aggregate through each batch bcum[j][p] and totals[p];
+//   clears hist for reuse. Workgroup 0 also writes the payload base of every tile in its batch.
+// Stage 3 (group g-2, wave per 32-record task): offset = log end + excl + rank, position likewise,
+//   out offsets, sparse index, then the records' 16-byte pieces are spread over the lanes: payload
+//   loads as aligned 16-byte blocks, CRC32C of each piece from LDS tables (shifted into place by
+//   zero-byte tables, XOR-reduced per record), 16-byte stores into every local replica ring
+//   through an LDS image of the log. Partition threads (workgroups of their own, from the start of
+//   the launch): the group's new log end, matchIndex, quorum commit and high watermark, into the
+//   other state set, so no record ever reads a half-updated partition.
+// Stage 4 (group g-3, the same partition threads): retention after each batch of the group, from
+//   the sparse-index entries that stage 3 wrote one launch earlier (FORMAT.md §4).
 //
 // Launch k starts only after launch k-1 has finished (one stream), so every hand-off between
 // stages crosses a kernel boundary. Launch k's first lane reports launch k-1 complete to the host.
@@ -34,7 +41,7 @@ namespace rmq {
 
 constexpr u32 kPT = kPipeThreads;   // 512
 constexpr u32 kPW = kPT / 64;       // 8 waves
-constexpr u32 kTR = kTileRecs;      // 2048
+constexpr u32 kTR = kTileRecs;      // 1024
 constexpr u32 kTI = kTR / kPT;      // 2 records per thread in stage 1
 constexpr u32 kWR = kTR / kPW;      // 128 records per wave in stage 1
 constexpr u32 kIB = kTileIdxBits;   // 10
@@ -53,12 +60,13 @@ constexpr u32 kRejNoSpace = 1u, kRejInvalid = 2u;
   do {                                                                                        \
     if (A.stamps) {                                                                           \
       const u64 t_ = __builtin_amdgcn_s_memrealtime();                                        \
-      if ((threadIdx.x & 63) == 0) A.stamps[((u64)blockIdx.x * 8 + (threadIdx.x >> 6)) * 8 + (k)] = t_; \
+      if ((threadIdx.x & 63) == 0)                                                            \
+        A.stamps[((u64)blockIdx.x * kPW + (threadIdx.x >> 6)) * 8 + (k)] = t_;               \
     }                                                                                         \
   } while (0)
 
 struct Stage1Smem {
-  u32 items[2][kTR];   // key << 11 | position in tile (ping-pong between radix passes)
+  u32 items[2][kTR];   // key << 10 | position in tile (ping-pong between radix passes)
   u32 cnt[kPW][256];   // per-wave digit counters, then per-wave digit bases
   u32 dbase[256];      // digit totals, then digit bases
   u32 info[kTR];       // record bytes/16 | flags << 29, by input position in the tile
@@ -91,20 +99,45 @@ __device__ __forceinline__ u32 record_rs16(u32 L) {  // (16 + align16(L)) / 16 w
   return (L >> 4) + ((L & 15u) ? 1u : 0u) + 1u;
 }
 
+// Batch of a group tile / stage-3 task, and the tile after the last one of a tile's batch
+// (kernel-argument lookups over <= kMaxGroup entries).
+__device__ __forceinline__ u32 batch_of_tile(const PipeGroup& G, u32 t) {
+  u32 j = 0;
+#pragma unroll
+  for (u32 k = 1; k < kMaxGroup; ++k) j += (k < G.nb && t >= G.tile0[k]) ? 1u : 0u;
+  return j;
+}
+__device__ __forceinline__ u32 batch_of_task(const PipeGroup& G, u32 task) {
+  u32 j = 0;
+#pragma unroll
+  for (u32 k = 1; k < kMaxGroup; ++k) j += (k < G.nb && task >= G.task0[k]) ? 1u : 0u;
+  return j;
+}
+__device__ __forceinline__ u32 batch_end_tile(const PipeGroup& G, u32 t) {
+  u32 e = G.tiles;
+#pragma unroll
+  for (int k = (int)kMaxGroup - 1; k >= 1; --k)
+    if ((u32)k < G.nb && t < G.tile0[k]) e = G.tile0[k];
+  return e;
+}
+
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
 __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
-  const PipeBatch& b = A.b1;
+  const PipeGroup& G = A.g1;
+  const u32 jb = batch_of_tile(G, t);
+  const PipeBatch& b = G.b[jb];
   const PipeScratch& x = A.s1;
   const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const u32 base = t * kTR;
+  const u32 base = (t - G.tile0[jb]) * kTR;  // first record of the tile inside its batch
+  const u64 gbase = (u64)t * kTR;            // its slot in the group's per-record scratch
   const u32 P = A.st.P;
   const u64 lt = (1ull << lane) - 1ull;
   const u32 nin = b.n - base < kTR ? b.n - base : kTR;
   PIPE_STAMP(0);
 
-  // ---- loads (input position q = 256w + 64r + lane)
+  // ---- loads (input position q = 128w + 64r + lane)
   u32 item[kTI], lenv[kTI], fl[kTI];
   u32 pc[kTI];
 #pragma unroll
@@ -162,7 +195,7 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
 #pragma unroll
     for (u32 r = 0; r < kTI; ++r) {
       const u32 q = w * kWR + r * 64u + lane;
-      if (q < nin) x.pre[base + q] = (u32)wpre + pre_r[r];
+      if (q < nin) x.pre[gbase + q] = (u32)wpre + pre_r[r];
     }
     if (tid == 0) {
       u64 ps = 0, rs = 0, ic = 0;
@@ -283,7 +316,7 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
     const u32 f = S.info[q] >> kFlagShift;
     if (q < nin) {
       const u64 ex = v - val[r];
-      x.crank[base + q] = make_uint2((u32)(ex >> 40) | (f << kFlagShift), (u32)(ex & kLow40));
+      x.crank[gbase + q] = make_uint2((u32)(ex >> 40) | (f << kFlagShift), (u32)(ex & kLow40));
     }
     const u32 nkey = s + 1 < kTR ? (sorted[s + 1] >> kIB) : 0xFFFFFFFFu;
     if (nkey != key && (v >> 40)) x.hist[(u64)t * P + key] = v;
@@ -293,24 +326,76 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Stage 2: column scans over the tiles, tile payload bases, batch rules
+// Stage 2: batch rules, column scans over the group's tiles, tile payload bases
 // ------------------------------------------------------------------------------------------
 __device__ void stage2(const PipeArgs& A, u32 wg) {
-  const PipeBatch& b = A.b2;
+  const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
-  const u32 P = A.st.P, T = b.tiles;
+  const u32 P = A.st.P, T = G.tiles;
+  const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  __shared__ u64 s_acc[kMaxGroup][3];
+  __shared__ u64 s_ex[kMaxTiles];
+  __shared__ u64 s_w[kPW];
+  __shared__ u32 s_tinfo[kMaxTiles];  // per tile: batch | last tile of its batch << 8
+  __shared__ u32 s_rej;
   PIPE_STAMP(0);
-  // kScanLanes consecutive threads share a partition column; per block of 8 * kScanLanes tiles,
-  // thread s holds tiles [8s, 8s + 8) of the block in registers (one load round per block)
-  const u32 s = threadIdx.x % kScanLanes;
-  for (u32 g = wg * kPT + threadIdx.x; g < P * kScanLanes; g += A.wg2 * kPT) {  // whole columns per group
+  // ---- batch rules from the tile sums: every workgroup, since the scans skip rejected batches
+  if (tid < kMaxGroup * 3) (&s_acc[0][0])[tid] = 0ull;
+  __syncthreads();
+  const bool in = tid < T;
+  const u32 jt = in ? batch_of_tile(G, tid) : 0u;
+  const u64 pay = in ? x.tsum[(u64)tid * 4 + 0] : 0ull;
+  if (in) {
+    s_tinfo[tid] = jt | (tid + 1u == batch_end_tile(G, tid) ? 0x100u : 0u);
+    atomicAdd(&s_acc[jt][0], pay);
+    atomicAdd(&s_acc[jt][1], x.tsum[(u64)tid * 4 + 1]);
+    atomicAdd(&s_acc[jt][2], x.tsum[(u64)tid * 4 + 2]);
+  }
+  if (wg == 0) {  // payload offset of every tile's first record inside its batch (packed payloads)
+    const u64 inc = wave_incl_scan_u64(pay);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    u64 wpre = 0;
+    for (u32 ww = 0; ww < w; ++ww) wpre += s_w[ww];
+    if (in) s_ex[tid] = wpre + inc - pay;
+    __syncthreads();
+    if (in) x.tile_base[tid] = s_ex[tid] - s_ex[G.tile0[jt]];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    u32 rm = 0;
+    for (u32 j = 0; j < G.nb; ++j) {
+      const u64 ptot = s_acc[j][0], rtot = s_acc[j][1], itot = s_acc[j][2];
+      u32 rej = 0;
+      if (itot || (!G.b[j].poff && ptot > G.b[j].payload_bytes)) rej |= kRejInvalid;
+      if (rtot > A.nospace_limit) rej |= kRejNoSpace;
+      rm |= (rej ? 1u : 0u) << j;
+      if (wg == 0) {
+        x.binfo[j * 4 + 0] = rej;
+        x.binfo[j * 4 + 1] = rtot;
+        x.binfo[j * 4 + 2] = ptot;
+        x.binfo[j * 4 + 3] = 0;
+      }
+    }
+    s_rej = rm;
+  }
+  __syncthreads();
+  const u32 rm = s_rej;
+
+  // ---- column scans: kScanLanes consecutive threads share a partition column; per block of
+  // 8 * kScanLanes tiles, thread s holds tiles [8s, 8s + 8) of the block in registers
+  const u32 s = tid % kScanLanes;
+  for (u32 g = wg * kPT + tid; g < P * kScanLanes; g += A.wg2 * kPT) {  // whole columns per group
     const u32 p = g / kScanLanes;
     u64 carry = 0;
     for (u32 B = 0; B < T; B += 8u * kScanLanes) {
       const u32 ta = B + 8u * s;
-      u64 h[8];
+      u64 h[8];  // tiles of rejected batches read as absent (their entries are cleared below)
 #pragma unroll
-      for (u32 k = 0; k < 8; ++k) h[k] = ta + k < T ? x.hist[(u64)(ta + k) * P + p] : 0ull;
+      for (u32 k = 0; k < 8; ++k) {
+        const u32 tk = ta + k;
+        h[k] = (tk < T && !((rm >> (s_tinfo[tk] & 0xFFu)) & 1u)) ? x.hist[(u64)tk * P + p] : 0ull;
+      }
       u64 loc = 0;
 #pragma unroll
       for (u32 k = 0; k < 8; ++k) loc += h[k];
@@ -324,52 +409,20 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
       carry += __shfl(inc, kScanLanes - 1, kScanLanes);
 #pragma unroll
       for (u32 k = 0; k < 8; ++k) {
+        const u32 tk = ta + k;
         if (h[k]) {
-          x.excl[(u64)(ta + k) * P + p] = run;
-          x.hist[(u64)(ta + k) * P + p] = 0ull;  // clear for the set's next batch
-          run += h[k];
+          x.excl[(u64)tk * P + p] = run;
+          x.hist[(u64)tk * P + p] = 0ull;  // clear for the set's next group
         }
+        run += h[k];
+        if (tk < T && (s_tinfo[tk] & 0x100u))  // last tile of its batch
+          x.bcum[(u64)(s_tinfo[tk] & 0xFFu) * P + p] = run;
       }
     }
+    if (rm)  // rejected batches (rare): clear their tiles' entries of this column
+      for (u32 tk = s; tk < T; tk += kScanLanes)
+        if ((rm >> (s_tinfo[tk] & 0xFFu)) & 1u) x.hist[(u64)tk * P + p] = 0ull;
     if (s == 0) x.totals[p] = carry;
-  }
-  if (wg == 0) {
-    __shared__ u64 s_w[kPW][3];
-    const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const bool in = tid < T;
-    const u64 pay = in ? x.tsum[(u64)tid * 4 + 0] : 0ull;
-    const u64 rb = in ? x.tsum[(u64)tid * 4 + 1] : 0ull;
-    const u64 ic = in ? x.tsum[(u64)tid * 4 + 2] : 0ull;
-    const u64 pinc = wave_incl_scan_u64(pay);
-    u64 rsum = rb, isum = ic;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      rsum += __shfl_xor(rsum, d, 64);
-      isum += __shfl_xor(isum, d, 64);
-    }
-    if (lane == 63) s_w[w][0] = pinc;
-    if (lane == 0) {
-      s_w[w][1] = rsum;
-      s_w[w][2] = isum;
-    }
-    __syncthreads();
-    u64 wpre = 0, ptot = 0, rtot = 0, itot = 0;
-    for (u32 ww = 0; ww < kPW; ++ww) {
-      wpre += ww < w ? s_w[ww][0] : 0ull;
-      ptot += s_w[ww][0];
-      rtot += s_w[ww][1];
-      itot += s_w[ww][2];
-    }
-    if (in) x.tile_base[tid] = wpre + pinc - pay;
-    if (tid == 0) {
-      u32 rej = 0;
-      if (itot || (!b.poff && ptot > b.payload_bytes)) rej |= kRejInvalid;
-      if (rtot > A.nospace_limit) rej |= kRejNoSpace;
-      x.binfo[0] = rej;
-      x.binfo[1] = rtot;
-      x.binfo[2] = ptot;
-      x.binfo[3] = 0;
-    }
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(1);
@@ -378,17 +431,6 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
 // ------------------------------------------------------------------------------------------
 // Stage 3: apply
 // ------------------------------------------------------------------------------------------
-
-// The aligned 16-byte blocks holding payload bytes [addr, addr + nb), nb in [1, 16]: the block of
-// addr and, if the range crosses into it, the next one (never touches a block without a
-// requested byte, so never a page without one).
-__device__ __forceinline__ void load_blocks(const uint8_t* payload, u64 addr, u32 nb, uint4& b0, uint4& b1) {
-  const u64 ua = reinterpret_cast<u64>(payload + addr);
-  const u32 s = (u32)(ua & 15u);
-  b0 = *reinterpret_cast<const uint4*>(ua - s);
-  b1 = make_uint4(0, 0, 0, 0);
-  if (s + nb > 16u) b1 = *reinterpret_cast<const uint4*>(ua - s + 16u);
-}
 
 // Bytes [s, s + nb) of b0 || b1 as 4 little-endian dwords, zero-padded past nb. 64-bit funnel
 // shifts with two-way selects (no dynamically indexed array, which would go to scratch).
@@ -415,12 +457,11 @@ __device__ __forceinline__ u32 crc_piece16(const u32 (*t)[256], uint4 v) {
   return crc_step8(t, crc_step8(t, 0u, v.x, v.y), v.z, v.w);
 }
 
-// Stage 3 works on tasks of kTaskRecs = 32 records, one per lane pair. The pair loads the
-// record's payload as aligned 16-byte blocks (lane j takes blocks j, j + 2, ...; 8 pieces = up
-// to 9 blocks per round) and each lane builds its pieces (j, j + 2, j + 4, j + 6 of the round)
-// from its own block and its partner's (DPP swap); lane 1 writes the header once the pair's
-// CRC registers are XOR-reduced.
-constexpr u32 kPL = 2;          // lanes per record
+// Stage 3 works on tasks of kTaskRecs = 32 records of one batch, one per lane pair. The pair loads
+// the record's payload as aligned 16-byte blocks (lane j takes blocks j, j + 2, ...; 8 pieces =
+// up to 9 blocks per round) and each lane builds its pieces (j, j + 2, j + 4, j + 6 of the round)
+// from its own block and its partner's (DPP swap); lane 1 writes the header once the pair's CRC
+// registers are XOR-reduced.
 constexpr u32 kPR = 8;          // pieces per record per round
 constexpr u32 kBL = 5;          // blocks per lane per round (9 blocks cover 8 misaligned pieces)
 
@@ -434,42 +475,58 @@ __device__ __forceinline__ uint4 pair_swap4(uint4 v) {
 struct TaskRec {  // round 1: the record (the same words in both lanes of its pair)
   u32 p, L;
   uint2 cr;
-  u64 src;
+  u64 src;        // payload address
 };
 
+// Where a task's records live: its batch in the group and the first record's index in the batch
+// (the task index is wave-uniform, so all of this stays in scalar registers).
+struct TaskPos {
+  u32 jb, i0;
+};
+__device__ __forceinline__ TaskPos task_pos(const PipeGroup& G, u32 task) {
+  const u32 jb = batch_of_task(G, task);
+  return TaskPos{jb, (task - G.task0[jb]) * kTaskRecs};
+}
+__device__ __forceinline__ u32 task_rec(const TaskPos& T) { return T.i0 + ((threadIdx.x & 63) >> 1); }
+
 struct TaskState {  // round 2: partition state of the record and its first round of payload blocks
-  u64 ex, tot, leo, used, spos;
+  u64 ex, leo, used;
   u32 lm, lead;
   uint4 blk[kBL];
 };
 
-__device__ __forceinline__ TaskRec stage3_r1(const PipeArgs& A, u32 task) {
-  const PipeBatch& b = A.b3;
+__device__ __forceinline__ TaskRec stage3_r1(const PipeArgs& A, const TaskPos& T) {
+  const PipeGroup& G = A.g3;
   const PipeScratch& x = A.s3;
-  const u32 i = task * kTaskRecs + ((threadIdx.x & 63) >> 1);
-  const u32 t = (task * kTaskRecs) / kTR;
-  TaskRec r{0u, 0u, make_uint2(kFlJunk << kFlagShift, 0u), 0ull};
+  const PipeBatch& b = G.b[T.jb];
+  const u32 i = task_rec(T);
+  TaskRec r;
+  r.p = 0u;
+  r.L = 0u;
+  r.cr = make_uint2(kFlJunk << kFlagShift, 0u);
+  r.src = reinterpret_cast<u64>(b.payload);
   if (i < b.n) {
+    const u64 gi = (u64)G.tile0[T.jb] * kTR + i;  // group record slot
     r.p = b.pidx[i];
     r.L = b.len[i];
-    r.cr = x.crank[i];
-    r.src = b.poff ? b.poff[i] : x.tile_base[t] + x.pre[i];
+    r.cr = x.crank[gi];
+    r.src += b.poff ? b.poff[i] : x.tile_base[gi / kTR] + x.pre[gi];
   }
   return r;
 }
 
-__device__ __forceinline__ bool stage3_cand(const PipeArgs& A, u32 task, const TaskRec& R, u32 rej) {
-  const u32 i = task * kTaskRecs + ((threadIdx.x & 63) >> 1);
-  return i < A.b3.n && (R.cr.x >> kFlagShift) == 0u && rej == 0u;
+__device__ __forceinline__ u32 batch_rej(const PipeArgs& A, const TaskPos& T) { return (u32)A.s3.binfo[T.jb * 4]; }
+
+__device__ __forceinline__ bool stage3_cand(const PipeArgs& A, const TaskPos& T, const TaskRec& R) {
+  return task_rec(T) < A.g3.b[T.jb].n && (R.cr.x >> kFlagShift) == 0u && batch_rej(A, T) == 0u;
 }
 
 // Aligned payload blocks of round c held by lane j: block 8c + j + 2q, q < kBL, loaded only if
 // it holds a byte of the record (never touches a page without one).
 __device__ __forceinline__ void round_blocks(const PipeArgs& A, const TaskRec& R, u32 c, bool live, uint4 (&blk)[kBL]) {
   const u32 j = threadIdx.x & 1u;
-  const u64 ua = reinterpret_cast<u64>(A.b3.payload + R.src);
-  const u64 a0 = ua & ~15ull;
-  const u64 lim = ua + R.L;  // one past the last byte
+  const u64 a0 = R.src & ~15ull;
+  const u64 lim = R.src + R.L;  // one past the last byte
 #pragma unroll
   for (u32 q = 0; q < kBL; ++q) {
     const u64 blk_addr = a0 + 16ull * (kPR * c + j + 2u * q);
@@ -478,21 +535,19 @@ __device__ __forceinline__ void round_blocks(const PipeArgs& A, const TaskRec& R
   }
 }
 
-__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, u32 task, const TaskRec& R, bool cand) {
-  const PipeScratch& x = A.s3;
+__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos& T, const TaskRec& R, bool cand) {
+  const PipeGroup& G = A.g3;
   const DevState& st = A.st;
-  const u32 t = (task * kTaskRecs) / kTR;
   TaskState S;
-  S.ex = S.tot = S.leo = S.used = S.spos = 0ull;
+  S.ex = S.leo = S.used = 0ull;
   S.lm = S.lead = 0u;
   if (cand) {
     const u32 p = R.p;
+    const u32 t = G.tile0[T.jb] + task_rec(T) / kTR;
     S.lead = st.is_leader[p];
-    S.ex = x.excl[(u64)t * st.P + p];
-    S.tot = x.totals[p];
+    S.ex = A.s3.excl[(u64)t * st.P + p];
     S.leo = A.cur.leo[p];
     S.used = A.cur.used[p];
-    S.spos = A.cur.start_pos[p];
     S.lm = st.local_mask[p];
   }
   // first round of payload blocks, speculatively (leadership is checked before any store)
@@ -512,16 +567,17 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
   return c;
 }
 
-__device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, const TaskRec& R,
-                              const TaskState& Z, bool cand, u32 rej, uint4& stat_out) {
-  const PipeBatch& b = A.b3;
+__device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
+                              const TaskState& Z, bool cand, uint4& stat_out) {
+  const PipeBatch& b = A.g3.b[T.jb];
   const DevState& st = A.st;
   const u32 lane = threadIdx.x & 63, j = lane & 1u;
   const u32 P = st.P, RF = st.RF;
-  const u32 i = task * kTaskRecs + (lane >> 1);
+  const u32 i = task_rec(T);
   const bool in = i < b.n;
   const u32 p = R.p, L = R.L;
   const u32 fl = R.cr.x >> kFlagShift;
+  const u32 rej = batch_rej(A, T);
   const bool ok = cand && Z.lead != 0u;
   const u32 m = (L + 15u) >> 4;  // payload pieces
   const u64 segmask = st.seg - 1ull;
@@ -530,7 +586,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, 
   const u64 pos = Z.used + 16ull * ((Z.ex & kLow40) + R.cr.y);
   uint8_t* const ring = st.logs + (u64)p * st.seg;
   const u32 lmw = (A.debug & 1u) ? 0u : Z.lm;
-  const u32 sa = (u32)(reinterpret_cast<u64>(b.payload + R.src) & 15u);
+  const u32 sa = (u32)(R.src & 15u);
   u32 acc = 0;
   const u32 nr = ok ? (m + kPR - 1u) / kPR : 0u;
   // records of at most 7 pieces (112 payload bytes) go through an LDS image of the log so that
@@ -564,7 +620,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, 
   }
   acc ^= pair_swap(acc);
 
-  // ---- header (lane 1), out offset + retention crossing (lane 0), sparse index (lane 1)
+  // ---- header (lane 1), out offset (lane 0), sparse index (lane 1)
   uint4 h = make_uint4(0, 0, 0, 0);
   if (ok && j == 1) {
     u32 crc = 0;
@@ -593,6 +649,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, 
           if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
       }
     }
+    __builtin_amdgcn_wave_barrier();  // the image is rewritten by the wave's next task
   } else if (ok && j == 1) {
     uint8_t* dst = ring + (pos & segmask);
     for (u32 r = 0; r < RF; ++r)
@@ -608,43 +665,30 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, u32 task, 
       e[1] = end;
     }
   }
-  if (ok && j == 0) {  // retention (FORMAT.md §4): the record whose range holds m* * I names E[m*]
-    const u64 fin = Z.used + 16ull * (Z.tot & kLow40);
-    if (fin - Z.spos > st.seg) {
-      const u64 ms = (fin - st.seg + (1ull << ilog) - 1) >> ilog;
-      const u64 X = ms << ilog;
-      if (pos < X && X <= end) {
-        A.nxt.start_off[p] = off + 1;
-        A.nxt.start_pos[p] = end;
-      }
-    }
-  }
   {
-    const bool h = j == 0;
-    const u32 n_in = (u32)__popcll(__ballot(h && in));
-    const u32 n_app = (u32)__popcll(__ballot(h && ok));
-    const u32 n_nl = (u32)__popcll(__ballot(h && cand && !Z.lead));
-    const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h && in && fl == kFlNoPart));
+    const bool h0 = j == 0;
+    const u32 n_in = (u32)__popcll(__ballot(h0 && in));
+    const u32 n_app = (u32)__popcll(__ballot(h0 && ok));
+    const u32 n_nl = (u32)__popcll(__ballot(h0 && cand && !Z.lead));
+    const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h0 && in && fl == kFlNoPart));
     const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
     const u32 n_ns = (rej & kRejInvalid) ? 0u : (rej & kRejNoSpace) ? n_in : 0u;
     stat_out = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
   }
 }
 
-// Thread per partition: the batch's new log end, matchIndex, quorum commit, high watermark and
-// retention, into the next state set.
-__device__ void stage3_partition(const PipeArgs& A, u32 p) {
+// Thread per partition, stage 3: the group's new log end, matchIndex, quorum commit and high
+// watermark, into the next state set. The commit rule is monotone in the log end, so evaluating
+// it once after the group equals evaluating it after each batch.
+__device__ void partition_apply(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
-  const u32 rej = (u32)A.s3.binfo[0];
-  // a follower's records are counted by stages 1/2 (ranks are per partition) but never applied
-  const u64 tot = (rej || !st.is_leader[p]) ? 0ull : A.s3.totals[p];
+  // a follower's records are counted by stages 1/2 (ranks are per partition) but never applied;
+  // stage 2 leaves rejected batches out of totals
+  const u64 tot = st.is_leader[p] ? A.s3.totals[p] : 0ull;
   const u64 tc = tot >> 40, tb = 16ull * (tot & kLow40);
-  const u64 leo = A.cur.leo[p], used = A.cur.used[p];
-  const u64 so = A.cur.start_off[p], sp = A.cur.start_pos[p];
-  const u64 nleo = leo + tc, nused = used + tb;
+  const u64 nleo = A.cur.leo[p] + tc;
   A.nxt.leo[p] = nleo;
-  A.nxt.used[p] = nused;
-  bool copy_start = true;
+  A.nxt.used[p] = A.cur.used[p] + tb;
   if (tc) {
     const u32 RF = st.RF, lm = st.local_mask[p];
     u64 row[kMaxRF];
@@ -659,25 +703,43 @@ __device__ void stage3_partition(const PipeArgs& A, u32 p) {
     const u64 c = quorum_commit(row, RF, st.commit[p], st.term_start[p]);
     st.commit[p] = c;
     st.hw[p] = c;
-    if (nused - sp > st.seg) {
-      const u32 ilog = st.interval_log2;
-      const u64 ms = (nused - st.seg + (1ull << ilog) - 1) >> ilog;
-      if ((ms << ilog) <= used) {  // crossing record from an earlier batch: E[m*] is in the index
-        const u64* e = st.index + ((u64)p * st.icap + ms % st.icap) * 2;
-        A.nxt.start_off[p] = e[0];
-        A.nxt.start_pos[p] = e[1];
-      }
-      copy_start = false;  // otherwise the crossing record of this batch writes the new start
-    }
   }
-  if (copy_start) {
-    A.nxt.start_off[p] = so;
-    A.nxt.start_pos[p] = sp;
+}
+
+// Thread per partition, stage 4: retention after each batch of the group applied one launch
+// earlier (FORMAT.md §4), batch by batch, from the index entries that launch wrote. The state set
+// this launch reads (cur) holds that group's final log end.
+__device__ void partition_retention(const PipeArgs& A, u32 p) {
+  const DevState& st = A.st;
+  const PipeScratch& x = A.s4;
+  if (!st.is_leader[p]) return;
+  const u64 gtot = x.totals[p];
+  if (!(gtot >> 40)) return;  // the partition took no record in the group
+  const u64 fin_g = A.cur.used[p];
+  const u32 ilog = st.interval_log2;
+  const u64 soff0 = st.start_off[p], spos0 = st.start_pos[p];
+  u64 soff = soff0, spos = spos0, prev = 0;
+  for (u32 j = 0; j < A.g4.nb; ++j) {
+    const u64 c = x.bcum[(u64)j * st.P + p];
+    if ((c >> 40) != (prev >> 40)) {  // batch j appended records of p
+      const u64 fin = fin_g - 16ull * ((gtot - c) & kLow40);
+      if (fin - spos > st.seg) {
+        const u64 ms = (fin - st.seg + (1ull << ilog) - 1) >> ilog;
+        const u64* e = st.index + ((u64)p * st.icap + ms % st.icap) * 2;
+        soff = e[0];
+        spos = e[1];
+      }
+    }
+    prev = c;
+  }
+  if (soff != soff0 || spos != spos0) {
+    st.start_off[p] = soff;
+    st.start_pos[p] = spos;
   }
 }
 
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
-#define RMQ_PIPE_WAVES_PER_SIMD 4  // 106 VGPRs, no spills: 2 resident workgroups per CU
+#define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
 __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(PipeArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -695,36 +757,49 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     return;
   }
   wg -= A.wg2;
+  if (wg < A.wgp) {  // partition threads: stage 3's state advance and stage 4's retention
+    PIPE_STAMP(0);
+    for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) {
+      if (A.g3.nb) partition_apply(A, p);
+      if (A.g4.nb) partition_retention(A, p);
+    }
+    if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PIPE_STAMP(6);
+    return;
+  }
+  wg -= A.wgp;
   Stage3Smem& S = *reinterpret_cast<Stage3Smem*>(smem_raw);
-  const u32 tasks = (A.b3.n + kTaskRecs - 1) / kTaskRecs;
+  const PipeGroup& G = A.g3;
+  const u32 tasks = G.task0[G.nb];
   const u32 lane = threadIdx.x & 63;
-  const u32 rej = (u32)A.s3.binfo[0];
-  u32 task = wg * kPW + (threadIdx.x >> 6);
+  // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
+  u32 task = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);
   // first task: its record and state/payload loads are in flight while the CRC tables fill LDS
-  TaskRec R = stage3_r1(A, task < tasks ? task : 0u);
+  TaskPos T = task_pos(G, task < tasks ? task : 0u);
+  TaskRec R = stage3_r1(A, T);
   if (!(A.debug & 8u)) {
     for (u32 k = threadIdx.x; k < 8 * 256; k += kPT) (&S.t8[0][0])[k] = (&A.crc->table[0][0])[k];
     for (u32 k = threadIdx.x; k < 3 * 4 * 256; k += kPT) (&S.z[0][0][0])[k] = (&A.crc->zshift[0][0][0])[k];
   }
-  bool cand = task < tasks && stage3_cand(A, task, R, rej);
-  TaskState Z = stage3_r2(A, task, R, cand);
+  bool cand = task < tasks && stage3_cand(A, T, R);
+  TaskState Z = stage3_r2(A, T, R, cand);
   __syncthreads();
   PIPE_STAMP(1);
   while (task < tasks) {
     uint4 so;
     PIPE_STAMP(2);
-    stage3_finish(A, S, task, R, Z, cand, rej, so);
-    if (lane == 0) A.stats3[task] = so;
+    stage3_finish(A, S, T, R, Z, cand, so);
+    if (lane == 0) G.stats[T.jb][task - G.task0[T.jb]] = so;
     PIPE_STAMP(3);
     task += A.wg3 * kPW;
     if (task < tasks) {
-      R = stage3_r1(A, task);
-      cand = stage3_cand(A, task, R, rej);
-      Z = stage3_r2(A, task, R, cand);
+      T = task_pos(G, task);
+      R = stage3_r1(A, T);
+      cand = stage3_cand(A, T, R);
+      Z = stage3_r2(A, T, R, cand);
     }
   }
-  for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wg3 * kPT) stage3_partition(A, p);
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(6);
 }
@@ -733,7 +808,7 @@ uint32_t pipeline_lds_bytes() { return (uint32_t)kSmemBytes; }
 uint32_t pipeline_wgs_per_cu() { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (kPT / 64u); }
 
 void launch_pipeline(const PipeArgs& a, hipStream_t s) {
-  const u32 grid = a.wg1 + a.wg2 + a.wg3;
+  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3;
   if (!grid) return;
   hipLaunchKernelGGL(pipeline_kernel, dim3(grid), dim3(kPT), kSmemBytes, s, a);
 }

@@ -145,6 +145,50 @@ def test_read_then_commit_consume_loop(oracle_mod):
         assert [int(dev.consumer_offsets(p)[0]) for p in range(3)] == [32, 32, 31]
 
 
+def _pipelined(dev, ora, batches):
+    """Submit every batch before waiting for any (the engine coalesces them into launch groups of
+    cfg.pipeline_depth), then check each batch's offsets and stats against the oracle applying the
+    batches one at a time."""
+    subs = [dev.append_async(b.pidx, b.lens, b.payload) for b in batches]
+    for (t, out), b in zip(subs, batches):
+        sd = dev.wait(t)
+        oo, so = ora.append(b.pidx, b.lens, b.payload)
+        assert sd == so, f"append stats gpu={sd} cpu={so}"
+        if not np.array_equal(out, oo):
+            bad = np.flatnonzero(out != oo)
+            raise AssertionError(f"out_offsets differ at {bad[:8]}: gpu={out[bad[:8]]} cpu={oo[bad[:8]]}")
+
+
+@pytest.mark.parametrize("group", [1, 2, 3, 4])
+def test_pipelined_groups(oracle_mod, group):
+    # back-to-back submissions: launch groups of `group` batches with retention after every batch,
+    # a no-space batch inside a group, a partition this rank does not lead, unknown partitions
+    cfg, dev, ora = pair(oracle_mod, num_partitions=64, replication_factor=3, segment_bytes=1 << 17,
+                         index_interval=256, max_batch_records=4096, pipeline_depth=group)
+    with dev, ora:
+        spec = StreamSpec(64, 1400, "zipf", size=(0, 120), config_index=22, invalid_frac=0.01)
+        big = make_batch(StreamSpec(64, 1100, "uniform", size=100, config_index=23), 0)  # > ring - I
+        for e in (dev, ora):
+            e.set_replicas(5, [1, 0, 2], 0)
+        batches = [make_batch(spec, b) for b in range(11)]
+        batches.insert(5, big)
+        _pipelined(dev, ora, batches)
+        compare_state(dev, ora, cfg, full_rings=True)
+        assert max(ora.state(p)["log_start_offset"] for p in range(64)) > 0, "scenario must exercise retention"
+        assert dev.state(5)["log_end_offset"] == 0
+
+
+def test_config_B_pipelined(oracle_mod):
+    # BASELINE configs[2] batches submitted back to back in groups of 4
+    cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,
+                         index_interval=1024, max_batch_records=65536, pipeline_depth=4)
+    with dev, ora:
+        spec = StreamSpec(4096, 65536, "zipf", size=100, config_index=2)
+        _pipelined(dev, ora, [make_batch(spec, b) for b in range(6)])
+        hot = np.argsort([-ora.state(p)["log_end_offset"] for p in range(4096)])
+        compare_state(dev, ora, cfg, parts=list(hot[:32]) + list(range(0, 4096, 131)))
+
+
 def test_config_B_full_batches(oracle_mod):
     # BASELINE configs[2] at full size: 4096 partitions, Zipf s=1.1, 64k x 100 B, RF=3
     # (16 MiB rings: a 64k x 128 B batch is exactly 8 MiB, over the 8 MiB - interval batch limit)
