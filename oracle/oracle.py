@@ -50,6 +50,8 @@ def load() -> C.CDLL:
         "ro_read_index": (C.c_int, [vp, u32, u64, u64, vp]),
         "ro_read_consumer_offsets": (C.c_int, [vp, u32, vp]),
         "ro_record_pos": (C.c_int, [vp, u32, u64, C.POINTER(u64)]),
+        "ro_append_sharded": (C.c_int, [vp, u32, vp, vp, vp, u32, C.c_int, C.POINTER(u32)]),
+        "ro_reserve": (C.c_int, [vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -116,6 +118,34 @@ class OracleEngine:
         if rc:
             raise EngineError(rc, "oracle")
         return out, {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_}
+
+    def append_sharded(self, batches, threads, pin=True):
+        """ro_append_sharded over a list of workload Batches (bench.py's multi-core CPU baseline).
+        Returns [(out_offsets, stats)] per batch, like append()."""
+        nb = len(batches)
+        keep, outs = [], []
+        arr = (A.RmqBatch * max(nb, 1))()
+        for k, b in enumerate(batches):
+            pidx = np.ascontiguousarray(b.pidx, np.uint32)
+            lens = np.ascontiguousarray(b.lens, np.uint32)
+            pay = np.ascontiguousarray(b.payload, np.uint8)
+            keep += [pidx, lens, pay]
+            arr[k] = A.RmqBatch(len(pidx), A.RMQ_MEM_HOST, _p(pidx), _p(lens), None,
+                                _p(pay) if pay.size else None, pay.size)
+            outs.append(np.empty(len(pidx), np.uint64))
+        optr = (C.c_void_p * max(nb, 1))(*[o.ctypes.data for o in outs])
+        st = (A.RmqAppendStats * max(nb, 1))()
+        done = C.c_uint32()
+        rc = self.lib.ro_append_sharded(self.h, nb, arr, optr, st, threads, int(pin), C.byref(done))
+        if rc:
+            raise EngineError(rc, "oracle")
+        return [(outs[k], {f: int(getattr(st[k], f)) for f, _ in A.RmqAppendStats._fields_}) for k in range(nb)]
+
+    def reserve(self, bytes_per_partition):
+        b = np.ascontiguousarray(bytes_per_partition, np.uint64)
+        rc = self.lib.ro_reserve(self.h, _p(b))
+        if rc:
+            raise EngineError(rc, "oracle")
 
     def ack(self, pidx, slot, match):
         pidx = np.ascontiguousarray(pidx, np.uint32)

@@ -4,8 +4,11 @@
  * how it is pinned). Plain C99, one record at a time in apply order; no attempt to mirror how the
  * GPU engine computes anything (no sort, no scans, no sparse-index walk for lookups).
  */
+#define _GNU_SOURCE /* pthread_setaffinity_np, CPU_SET: the sharded baseline pins its threads */
 #include "ripple_oracle.h"
 
+#include <pthread.h>
+#include <sched.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -283,18 +286,9 @@ int ro_become_leader(ro_engine* e, uint32_t p, uint64_t term) {
 /* Append: PartitionStateMachine.onApply -> handleMessageAppendRequest (messages.addAll)       */
 /* ------------------------------------------------------------------------------------------ */
 
-int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* len,
-              const uint64_t* payload_off, const uint8_t* payload, uint64_t payload_bytes,
-              uint64_t* out_offsets, rmq_append_stats* stats) {
-  const rmq_config* c = &e->cfg;
-  uint32_t P = c->num_partitions, RF = c->replication_factor;
-  uint64_t I = c->index_interval;
-  rmq_append_stats st;
-  memset(&st, 0, sizeof st);
-  st.records = n;
-  if (n && (!pidx || !len || !out_offsets)) return RMQ_EINVAL;
-
-  /* validate payload ranges; compute the batch's record bytes (all records, FORMAT.md §3) */
+/* The payload-range check (RMQ_EINVAL) and the FORMAT.md §3 batch rule, over every record. */
+static int batch_scan(const ro_engine* e, uint32_t n, const uint32_t* len, const uint64_t* payload_off,
+                      const uint8_t* payload, uint64_t payload_bytes, int* no_space) {
   uint64_t run = 0, out_bytes = 0;
   for (uint32_t i = 0; i < n; ++i) {
     uint64_t off = payload_off ? payload_off[i] : run;
@@ -302,21 +296,80 @@ int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* le
     run += len[i];
     out_bytes += RMQ_RECORD_HEADER_BYTES + ((len[i] + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
   }
-  if (out_bytes > c->segment_bytes - I) {
+  *no_space = out_bytes > e->cfg.segment_bytes - e->cfg.index_interval;
+  return RMQ_OK;
+}
+
+typedef struct {
+  uint8_t* v;
+  uint64_t cap;
+} ro_buf;
+
+/* One record of a partition this rank leads: header + payload + zero pad into every local replica
+   ring at the log end, sparse-index entries, new log end. */
+static int append_record(ro_engine* e, ro_part* s, uint32_t p, const uint8_t* src, uint32_t L, ro_buf* rec,
+                         uint64_t* out_offset) {
+  const rmq_config* c = &e->cfg;
+  const uint64_t I = c->index_interval;
+  const uint64_t rs = RMQ_RECORD_HEADER_BYTES + ((L + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
+  if (rs > rec->cap) {
+    uint8_t* nr = (uint8_t*)realloc(rec->v, rs);
+    if (!nr) return RMQ_ENOMEM;
+    rec->v = nr;
+    rec->cap = rs;
+  }
+  uint8_t* r8 = rec->v;
+  const uint64_t o = s->leo, pos = s->used;
+  const uint32_t crc = ro_crc32c(src, L);
+  memcpy(r8, &o, 8); /* little-endian host */
+  memcpy(r8 + 8, &L, 4);
+  memcpy(r8 + 12, &crc, 4);
+  if (L) memcpy(r8 + 16, src, L);
+  memset(r8 + 16 + L, 0, rs - 16 - L);
+  for (uint32_t r = 0; r < c->replication_factor; ++r)
+    if (s->ranks[r] == c->rank) ring_write(e, ring_of(e, r, p), pos, r8, rs);
+  /* sparse index: every multiple m*I in (pos, pos + rs] now names the next record */
+  for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
+    if (vec_push(&s->idx_off, o + 1) || vec_push(&s->idx_pos, pos + rs)) return RMQ_ENOMEM;
+  if (vec_push(&s->rec_pos, pos)) return RMQ_ENOMEM;
+  s->leo = o + 1;
+  s->used = pos + rs;
+  *out_offset = o;
+  return RMQ_OK;
+}
+
+/* End of a batch for a partition that took records: co-located matchIndex, commit, retention. */
+static void finish_partition(ro_engine* e, ro_part* s) {
+  for (uint32_t r = 0; r < e->cfg.replication_factor; ++r)
+    if (s->ranks[r] == e->cfg.rank) s->match[r] = s->leo; /* co-located replicas persisted */
+  commit_eval(e, s);
+  retention_eval(e, s);
+}
+
+int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* len,
+              const uint64_t* payload_off, const uint8_t* payload, uint64_t payload_bytes,
+              uint64_t* out_offsets, rmq_append_stats* stats) {
+  const uint32_t P = e->cfg.num_partitions;
+  rmq_append_stats st;
+  memset(&st, 0, sizeof st);
+  st.records = n;
+  if (n && (!pidx || !len || !out_offsets)) return RMQ_EINVAL;
+  int no_space = 0;
+  int rc = batch_scan(e, n, len, payload_off, payload, payload_bytes, &no_space);
+  if (rc) return rc;
+  if (no_space) {
     for (uint32_t i = 0; i < n; ++i) out_offsets[i] = RMQ_OFFSET_NONE;
     st.rejected_no_space = n;
     if (stats) *stats = st;
     return RMQ_OK;
   }
-
   memset(e->touched, 0, P);
-  uint8_t* rec = NULL;
-  uint64_t rec_cap = 0;
-  run = 0;
+  ro_buf rec = {NULL, 0};
+  uint64_t run = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    uint64_t off = payload_off ? payload_off[i] : run;
+    const uint64_t off = payload_off ? payload_off[i] : run;
     run += len[i];
-    uint32_t p = pidx[i];
+    const uint32_t p = pidx[i];
     if (p >= P) {
       out_offsets[i] = RMQ_OFFSET_NONE;
       st.rejected_no_partition++;
@@ -328,53 +381,189 @@ int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* le
       st.rejected_not_leader++;
       continue;
     }
-    uint32_t L = len[i];
-    uint64_t rs = RMQ_RECORD_HEADER_BYTES + ((L + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
-    if (rs > rec_cap) {
-      uint8_t* nr = (uint8_t*)realloc(rec, rs);
-      if (!nr) {
-        free(rec);
-        return RMQ_ENOMEM;
-      }
-      rec = nr;
-      rec_cap = rs;
+    rc = append_record(e, s, p, payload + off, len[i], &rec, &out_offsets[i]);
+    if (rc) {
+      free(rec.v);
+      return rc;
     }
-    uint64_t o = s->leo, pos = s->used;
-    uint32_t crc = ro_crc32c(payload + off, L);
-    memcpy(rec, &o, 8); /* little-endian host */
-    memcpy(rec + 8, &L, 4);
-    memcpy(rec + 12, &crc, 4);
-    if (L) memcpy(rec + 16, payload + off, L);
-    memset(rec + 16 + L, 0, rs - 16 - L);
-    for (uint32_t r = 0; r < RF; ++r)
-      if (s->ranks[r] == c->rank) ring_write(e, ring_of(e, r, p), pos, rec, rs);
-    /* sparse index: every multiple m*I in (pos, pos + rs] now names the next record */
-    for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m) {
-      if (vec_push(&s->idx_off, o + 1) || vec_push(&s->idx_pos, pos + rs)) {
-        free(rec);
-        return RMQ_ENOMEM;
-      }
-    }
-    if (vec_push(&s->rec_pos, pos)) {
-      free(rec);
-      return RMQ_ENOMEM;
-    }
-    s->leo = o + 1;
-    s->used = pos + rs;
-    out_offsets[i] = o;
     st.appended++;
     e->touched[p] = 1;
   }
-  free(rec);
-  for (uint32_t p = 0; p < P; ++p) {
-    if (!e->touched[p]) continue;
-    ro_part* s = &e->parts[p];
-    for (uint32_t r = 0; r < RF; ++r)
-      if (s->ranks[r] == c->rank) s->match[r] = s->leo; /* co-located replicas persisted */
-    commit_eval(e, s);
-    retention_eval(e, s);
-  }
+  free(rec.v);
+  for (uint32_t p = 0; p < P; ++p)
+    if (e->touched[p]) finish_partition(e, &e->parts[p]);
   if (stats) *stats = st;
+  return RMQ_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Partition-sharded append: the multi-core CPU baseline                        */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Thread t of T applies, batch after batch, the records of the partitions it owns (p % T == t;
+   unknown partitions go to thread 0). Partitions are independent Raft groups
+   (mq-broker/src/main/java/metadata/PartitionManager.java:111-176), so this is ro_append batch by
+   batch; every thread evaluates the batch rules itself and so stops at the same invalid batch. */
+typedef struct {
+  ro_engine* e;
+  const rmq_batch* b;
+  uint64_t* const* out;
+  rmq_append_stats* st; /* [nb]: this thread's share */
+  uint32_t nb, t, T, done;
+  int cpu, rc;
+} ro_shard;
+
+static void* shard_main(void* arg) {
+  ro_shard* j = (ro_shard*)arg;
+  ro_engine* e = j->e;
+  const uint32_t P = e->cfg.num_partitions;
+  if (j->cpu >= 0) {
+    cpu_set_t cs;
+    CPU_ZERO(&cs);
+    CPU_SET(j->cpu, &cs);
+    pthread_setaffinity_np(pthread_self(), sizeof cs, &cs);
+  }
+  ro_buf rec = {NULL, 0};
+  uint32_t* mine = (uint32_t*)malloc(((size_t)P / j->T + 1) * sizeof(uint32_t));
+  if (!mine) {
+    j->rc = RMQ_ENOMEM;
+    return NULL;
+  }
+  for (uint32_t k = 0; k < j->nb; ++k) {
+    const rmq_batch* b = &j->b[k];
+    uint64_t* out = j->out[k];
+    rmq_append_stats* st = &j->st[k];
+    int no_space = 0;
+    int rc = batch_scan(e, b->n, b->len, b->payload_off, b->payload, b->payload_bytes, &no_space);
+    uint32_t nm = 0;
+    uint64_t run = 0;
+    for (uint32_t i = 0; i < b->n && !rc; ++i) {
+      const uint32_t p = b->pidx[i];
+      const uint64_t off = b->payload_off ? b->payload_off[i] : run;
+      run += b->len[i];
+      if ((p < P ? p % j->T : 0u) != j->t) continue;
+      st->records++;
+      if (no_space) {
+        out[i] = RMQ_OFFSET_NONE;
+        st->rejected_no_space++;
+      } else if (p >= P) {
+        out[i] = RMQ_OFFSET_NONE;
+        st->rejected_no_partition++;
+      } else if (!e->parts[p].is_leader) {
+        out[i] = RMQ_OFFSET_NONE;
+        st->rejected_not_leader++;
+      } else {
+        rc = append_record(e, &e->parts[p], p, b->payload + off, b->len[i], &rec, &out[i]);
+        if (rc) break;
+        st->appended++;
+        if (!e->touched[p]) {
+          e->touched[p] = 1;
+          mine[nm++] = p;
+        }
+      }
+    }
+    if (rc) {
+      j->rc = rc;
+      break;
+    }
+    for (uint32_t q = 0; q < nm; ++q) {
+      finish_partition(e, &e->parts[mine[q]]);
+      e->touched[mine[q]] = 0;
+    }
+    j->done = k + 1;
+  }
+  free(rec.v);
+  free(mine);
+  return NULL;
+}
+
+int ro_append_sharded(ro_engine* e, uint32_t nb, const rmq_batch* batches, uint64_t* const* out_offsets,
+                      rmq_append_stats* stats, uint32_t threads, int pin, uint32_t* batches_done) {
+  if (!e || (nb && (!batches || !out_offsets || !stats))) return RMQ_EINVAL;
+  for (uint32_t k = 0; k < nb; ++k)
+    if (batches[k].n && (!batches[k].pidx || !batches[k].len || !out_offsets[k])) return RMQ_EINVAL;
+  const uint32_t P = e->cfg.num_partitions;
+  uint32_t T = threads ? threads : 1u;
+  if (T > P) T = P;
+  int cpus[CPU_SETSIZE];
+  int ncpu = 0;
+  if (pin) {
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0)
+      for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &cs)) cpus[ncpu++] = c;
+  }
+  ro_shard* J = (ro_shard*)calloc(T, sizeof *J);
+  rmq_append_stats* S = (rmq_append_stats*)calloc((size_t)T * (nb ? nb : 1u), sizeof *S);
+  pthread_t* th = (pthread_t*)calloc(T, sizeof *th);
+  uint8_t* started = (uint8_t*)calloc(T, 1);
+  if (!J || !S || !th || !started) {
+    free(J);
+    free(S);
+    free(th);
+    free(started);
+    return RMQ_ENOMEM;
+  }
+  memset(e->touched, 0, P);
+  for (uint32_t t = 0; t < T; ++t) {
+    J[t].e = e;
+    J[t].b = batches;
+    J[t].out = out_offsets;
+    J[t].st = S + (size_t)t * nb;
+    J[t].nb = nb;
+    J[t].t = t;
+    J[t].T = T;
+    J[t].cpu = ncpu ? cpus[t % (uint32_t)ncpu] : -1;
+  }
+  for (uint32_t t = 0; t < T; ++t) started[t] = pthread_create(&th[t], NULL, shard_main, &J[t]) == 0;
+  for (uint32_t t = 0; t < T; ++t) {
+    if (started[t]) {
+      pthread_join(th[t], NULL);
+    } else {
+      J[t].cpu = -1; /* runs on the calling thread: leave its affinity alone */
+      shard_main(&J[t]);
+    }
+  }
+  int rc = RMQ_OK;
+  uint32_t done = nb;
+  for (uint32_t t = 0; t < T; ++t) {
+    if (J[t].rc && rc == RMQ_OK) rc = J[t].rc;
+    if (J[t].done < done) done = J[t].done;
+  }
+  for (uint32_t k = 0; k < nb; ++k) {
+    rmq_append_stats a;
+    memset(&a, 0, sizeof a);
+    for (uint32_t t = 0; t < T; ++t) {
+      const rmq_append_stats* x = &S[(size_t)t * nb + k];
+      a.records += x->records;
+      a.appended += x->appended;
+      a.rejected_not_leader += x->rejected_not_leader;
+      a.rejected_no_partition += x->rejected_no_partition;
+      a.rejected_no_space += x->rejected_no_space;
+      a.rejected_invalid += x->rejected_invalid;
+    }
+    stats[k] = a;
+  }
+  if (batches_done) *batches_done = done;
+  free(J);
+  free(S);
+  free(th);
+  free(started);
+  return rc;
+}
+
+int ro_reserve(ro_engine* e, const uint64_t* bytes) {
+  if (!e || !bytes) return RMQ_EINVAL;
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  const uint64_t S = e->cfg.segment_bytes;
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint64_t n = bytes[p] < S ? bytes[p] : S;
+    for (uint32_t r = 0; r < RF; ++r) {
+      if (e->parts[p].ranks[r] != e->cfg.rank) continue;
+      volatile uint8_t* ring = ring_of(e, r, p);
+      for (uint64_t o = 0; o < n; o += 4096) ring[o] = ring[o]; /* first touch, content unchanged */
+    }
+  }
   return RMQ_OK;
 }
 

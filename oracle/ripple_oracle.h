@@ -49,6 +49,15 @@ int ro_become_leader(ro_engine* e, uint32_t pidx, uint64_t term);
 int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* len,
               const uint64_t* payload_off, const uint8_t* payload, uint64_t payload_bytes,
               uint64_t* out_offsets, rmq_append_stats* stats);
+/* Partition-sharded ro_append over nb batches (the CPU baseline's multi-core leg):
+   thread t of `threads` applies, batch after batch, the records of the partitions p with
+   p % threads == t. Same results as ro_append per batch; *batches_done = batches applied before
+   the first error. pin != 0 pins thread t to the t-th CPU this process may run on. */
+int ro_append_sharded(ro_engine* e, uint32_t nb, const rmq_batch* batches, uint64_t* const* out_offsets,
+                      rmq_append_stats* stats, uint32_t threads, int pin, uint32_t* batches_done);
+/* First touch of ring bytes [0, min(segment, bytes[p])) of every local replica of every partition
+   (untimed setup, so a timed run does not pay page faults the device rings never see). */
+int ro_reserve(ro_engine* e, const uint64_t* bytes);
 int ro_ack(ro_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n);
 int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                               const uint64_t* offset, uint32_t n, int32_t* status);
