@@ -23,6 +23,7 @@ per batch.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -43,6 +44,22 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 def algorithmic_bytes(n: int, L: int, rf: int, P: int) -> int:
     return n * ((8 + L) + rf * (16 + L)) + P * (rf * 8 + 16)
+
+
+def pmc_traffic(group: int, config: str):
+    """HBM bytes per launch of the pipeline kernel from the newest committed PMC summary taken at
+    this group size and config (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from
+    the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or (None, None)."""
+    found = (None, None)
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json"))):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("group") == group and d.get("config") == config:
+            found = (d["traffic_bytes_per_launch"], os.path.relpath(path, REPO))
+    return found
 
 
 def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float, name: str = "B") -> dict:
@@ -171,6 +188,7 @@ def main() -> None:
         alg = algorithmic_bytes(n, L or 0, rf, spec.partitions)
         # algorithmic bytes per launch / mean launch duration = bytes of the applied batches / region
         achieved = alg * n_applied / (region_ms / 1e3) / 1e9 if n_launch and region_ms > 0 else 0.0
+        traffic, traffic_src = pmc_traffic(args.group, args.config)
         out = {
             "metric": "committed msgs/sec (node) + HBM GB/s, 100B msgs, 4096 partitions RF=3",
             "value": msgs_per_s,
@@ -192,7 +210,7 @@ def main() -> None:
                        "parallelism": f"partition-sharded x{world}", "batches_per_launch_group": args.group},
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "rmq::pipeline_kernel",
                          "algorithmic_bytes_per_launch": alg * n_applied / max(n_launch, 1),
                          "mean_kernel_us": region_ms * 1e3 / max(n_launch, 1), "timed_launches": n_launch,

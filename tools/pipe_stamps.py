@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Summarise pipeline-launch phase stamps (RMQ_STAMPS=<csv>, one launch: RMQ_STAMPS_AT).
 
-Rows: workgroup, wave, stage (1 rank tiles, 2 column scans, 3 apply), t0..t7 s_memrealtime
-(100 MHz -> 10 ns). Stage 1/2 stamps are per workgroup (wave 0); stage 3 per wave (one task).
+Rows: workgroup, wave, role (1 rank tiles, 2 column scans, 3 apply tasks, 4 partition threads),
+t0..t7 s_memrealtime (100 MHz -> 10 ns). Stage 1/2 stamps are per workgroup (wave 0); stage 3 per
+wave (stamps 2/3 bracket the wave's last task); partition threads per wave.
 Prints, per stage, start/end spread relative to the first stamp of the launch and per-phase
 percentiles."""
 import sys
@@ -13,7 +14,8 @@ PHASES = {
     1: ["loads+input scans", "radix passes", "seg scan+writes"],
     2: ["column scans+tile scan"],
     3: ["first task r1+tables+r2 issue", "(earlier tasks)", "last task finish", "(unused)",
-        "(unused)", "partition threads"],
+        "(unused)", "(unused)"],
+    4: ["(unused)", "(unused)", "(unused)", "(unused)", "(unused)", "partition apply + retention"],
 }
 
 
