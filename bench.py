@@ -116,7 +116,7 @@ def main() -> None:
                     help="ring bytes per (replica, partition); a 64k x 128 B batch needs > 8 MiB")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--group", type=int, default=2,
+    ap.add_argument("--group", type=int, default=4,
                     help="batches per pipeline launch group (cfg.pipeline_depth, 1..4)")
     args = ap.parse_args()
 

@@ -128,6 +128,9 @@ struct rmq_engine {
   uint64_t stamps_at = 100;
   uint64_t* d_stamps = nullptr;
   uint32_t stamps_wg[4] = {0, 0, 0, 0};
+  // one stage-3 wave per task: the workgroups beyond the resident slots dispatch as stage-1/2
+  // workgroups retire (RMQ_WG3_ALL=0: only as many as fit next to them, looping over tasks)
+  uint32_t wg3_all = 1;
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
 };
 
@@ -308,11 +311,12 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.s3 = e->scratch[s3->set];
     const uint32_t wpb = kPipeThreads / 64;
     const uint32_t want = std::max<uint32_t>(1u, (s3->tasks + wpb - 1) / wpb);
-    // fill the chip next to the other roles of this launch (resident workgroups per CU from the
-    // kernel's launch bounds); the task waves loop over the rest
+    // default: one wave per task (the workgroups past the resident slots start as stage-1/2
+    // workgroups retire); RMQ_WG3_ALL=0 fills only the slots next to the other roles (resident
+    // workgroups per CU from the kernel's launch bounds) and the task waves loop over the rest
     const uint32_t slots = pipeline_wgs_per_cu() * e->cu_count, busy = a.wg1 + a.wg2 + a.wgp;
     const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
-    a.wg3 = std::min<uint32_t>(want, room);
+    a.wg3 = e->wg3_all ? want : std::min<uint32_t>(want, room);
   }
   a.launch_seq = ++e->launch_seq;
   if (e->d_stamps && a.launch_seq == e->stamps_at) {
@@ -546,6 +550,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->device = cfg->device;
   e->stamps_path = std::getenv("RMQ_STAMPS");
   if (const char* v = std::getenv("RMQ_DEBUG")) e->debug = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_WG3_ALL")) e->wg3_all = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
