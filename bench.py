@@ -117,7 +117,7 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--group", type=int, default=4,
-                    help="batches per pipeline launch group (cfg.pipeline_depth, 1..4)")
+                    help="batches per pipeline launch group (cfg.pipeline_depth, 1..8)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

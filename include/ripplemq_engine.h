@@ -77,7 +77,7 @@ typedef struct rmq_config {
   uint32_t index_interval;     /* sparse offset-index interval in bytes; power of two in [64, 1<<20] */
   uint32_t max_consumers;      /* consumer-offset table width per partition (dense consumer ids) */
   uint32_t max_batch_records;  /* capacity of one rmq_append call */
-  uint32_t pipeline_depth;     /* batches applied per pipeline launch group, 1..4; 0 -> default 2 */
+  uint32_t pipeline_depth;     /* batches applied per pipeline launch group, 1..8; 0 -> default 2 */
   uint64_t max_batch_bytes;    /* payload bytes of one rmq_append call */
   int32_t device;              /* HIP device ordinal */
   uint32_t rank;               /* replica rank of this engine (placement in rmq_set_replicas) */

@@ -31,7 +31,7 @@ using namespace rmq;
 namespace {
 
 constexpr uint32_t kStatsRing = 64;                                // tickets whose stats stay readable
-constexpr uint32_t kMaxBatchRecords = kMaxTiles * kTileRecs;       // 262144
+constexpr uint32_t kMaxBatchRecords = kMaxTiles * kTileRecs;       // 524288
 constexpr uint32_t kSets = 4;                                      // pipeline scratch sets
 
 struct EvPair {
@@ -615,7 +615,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_TRY(dalloc(&x.tile_base, GT));
     CREATE_TRY(dalloc(&x.binfo, (size_t)kMaxGroup * 4));
   }
-  if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(4u * e->cu_count + 2u * kMaxTiles) * 64));
+  if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(2u * e->cu_count + kMaxTiles + (P + kPipeThreads - 1) / kPipeThreads +
+                                                       kMaxTiles * kTileRecs / (kTaskRecs * kPipeThreads / 64)) * 64));
   CREATE_HIP(hipHostMalloc((void**)&e->done_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
   *e->done_host = 0;
   CREATE_HIP(hipHostGetDevicePointer((void**)&e->done_dev, e->done_host, 0));

@@ -9,10 +9,13 @@ namespace rmq {
 constexpr uint32_t kPipeThreads = 512;   // 8 waves per workgroup, every role of the pipeline launch
 constexpr uint32_t kTileRecs = 1024;     // records per ranking tile (stage 1)
 constexpr uint32_t kTileIdxBits = 10;    // log2(kTileRecs)
-constexpr uint32_t kMaxTiles = 256;      // tiles per group; max_batch_records <= kMaxTiles * kTileRecs
-constexpr uint32_t kScanLanes = 8;       // stage 2: threads per partition column
+constexpr uint32_t kMaxTiles = 512;      // tiles per group (<= kPipeThreads: stage 2 holds one per thread)
+#ifndef RMQ_SCAN_LANES
+#define RMQ_SCAN_LANES 16
+#endif
+constexpr uint32_t kScanLanes = RMQ_SCAN_LANES;  // stage 2: threads per partition column
 constexpr uint32_t kTaskRecs = 32;       // records per apply task (one wave, 2 lanes per record)
-constexpr uint32_t kMaxGroup = 4;        // batches per pipeline group (cfg.pipeline_depth)
+constexpr uint32_t kMaxGroup = 8;        // batches per pipeline group (cfg.pipeline_depth)
 constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-bit LDS radix passes)
 constexpr uint32_t kMaxRF = 8;
 

@@ -17,7 +17,7 @@
 //   segmented scan of {1, record bytes/16} over the sorted tile, which gives every record its
 //   count / byte rank inside its partition's run in the tile, and the tile aggregate of each
 //   present partition, written sparsely into hist[tile][p]. Also the tile's payload prefix and sums.
-// Stage 2 (group g-1, 8 threads per partition): the batch rules (no space, invalid payload ranges)
+// Stage 2 (group g-1, 16 threads per partition): the batch rules (no space, invalid payload ranges)
 //   from the tile sums, then an exclusive scan of hist[.][p] over the group's tiles that skips
 //   rejected batches -> excl[tile][p], the aggregate through each batch bcum[j][p] and totals[p];
 //   clears hist for reuse. Workgroup 0 also writes the payload base of every tile in its batch.

@@ -45,7 +45,7 @@ class EngineConfig:
     index_interval: int = 1024
     max_consumers: int = 8
     max_batch_records: int = 65536
-    pipeline_depth: int = 2          # batches per pipeline launch group (1..4)
+    pipeline_depth: int = 2          # batches per pipeline launch group (1..8)
     max_batch_bytes: int = 64 << 20
     device: int = 0
     rank: int = 0

@@ -159,7 +159,7 @@ def _pipelined(dev, ora, batches):
             raise AssertionError(f"out_offsets differ at {bad[:8]}: gpu={out[bad[:8]]} cpu={oo[bad[:8]]}")
 
 
-@pytest.mark.parametrize("group", [1, 2, 3, 4])
+@pytest.mark.parametrize("group", [1, 2, 3, 4, 8])
 def test_pipelined_groups(oracle_mod, group):
     # back-to-back submissions: launch groups of `group` batches with retention after every batch,
     # a no-space batch inside a group, a partition this rank does not lead, unknown partitions
