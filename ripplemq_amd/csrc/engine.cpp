@@ -131,6 +131,7 @@ struct rmq_engine {
   // one stage-3 wave per task: the workgroups beyond the resident slots dispatch as stage-1/2
   // workgroups retire (RMQ_WG3_ALL=0: only as many as fit next to them, looping over tasks)
   uint32_t wg3_all = 1;
+  uint32_t s3_first = 0;  // RMQ_S3_FIRST=1: stage-3 workgroups first in dispatch order
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
 };
 
@@ -287,6 +288,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.cur = cur;
   a.nxt = nxt;
   a.key_passes = e->key_passes;
+  a.s3_first = e->s3_first;
   a.nospace_limit = e->cfg.segment_bytes - e->cfg.index_interval;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
@@ -551,6 +553,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->stamps_path = std::getenv("RMQ_STAMPS");
   if (const char* v = std::getenv("RMQ_DEBUG")) e->debug = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_WG3_ALL")) e->wg3_all = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \

@@ -7,8 +7,11 @@
 namespace rmq {
 
 constexpr uint32_t kPipeThreads = 512;   // 8 waves per workgroup, every role of the pipeline launch
-constexpr uint32_t kTileRecs = 1024;     // records per ranking tile (stage 1)
-constexpr uint32_t kTileIdxBits = 10;    // log2(kTileRecs)
+#ifndef RMQ_TILE_BITS
+#define RMQ_TILE_BITS 10
+#endif
+constexpr uint32_t kTileIdxBits = RMQ_TILE_BITS;       // log2(kTileRecs)
+constexpr uint32_t kTileRecs = 1u << kTileIdxBits;     // records per ranking tile (stage 1)
 constexpr uint32_t kMaxTiles = 512;      // tiles per group (<= kPipeThreads: stage 2 holds one per thread)
 #ifndef RMQ_SCAN_LANES
 #define RMQ_SCAN_LANES 16
@@ -98,6 +101,7 @@ struct PipeArgs {
   PipeScratch s1, s2, s3, s4;
   uint32_t wg1, wg2, wgp, wg3;  // workgroups per role, in this order along blockIdx.x
   uint32_t key_passes;     // 1 (P <= 256) or 2
+  uint32_t s3_first;       // 1: stage-3 workgroups first along blockIdx.x (dispatched first)
   uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2

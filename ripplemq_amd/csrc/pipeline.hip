@@ -746,18 +746,29 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
     __hip_atomic_store(A.done_word, A.launch_seq - 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   u32 wg = blockIdx.x;
-  if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
-  if (wg < A.wg1) {
-    stage1_tile(A, wg, *reinterpret_cast<Stage1Smem*>(smem_raw));
-    return;
+  // roles along blockIdx.x: [stage 1 | stage 2 | partition threads | stage 3], or with s3_first
+  // [stage 3 | stage 1 | stage 2 | partition threads]
+  bool s3 = false;
+  if (A.s3_first) {
+    s3 = wg < A.wg3;
+    if (!s3) wg -= A.wg3;
+  } else {
+    s3 = wg >= A.wg1 + A.wg2 + A.wgp;
+    if (s3) wg -= A.wg1 + A.wg2 + A.wgp;
   }
-  wg -= A.wg1;
-  if (wg < A.wg2) {
-    stage2(A, wg);
-    return;
-  }
-  wg -= A.wg2;
-  if (wg < A.wgp) {  // partition threads: stage 3's state advance and stage 4's retention
+  if (!s3) {
+    if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
+    if (wg < A.wg1) {
+      stage1_tile(A, wg, *reinterpret_cast<Stage1Smem*>(smem_raw));
+      return;
+    }
+    wg -= A.wg1;
+    if (wg < A.wg2) {
+      stage2(A, wg);
+      return;
+    }
+    wg -= A.wg2;
+    // partition threads: stage 3's state advance and stage 4's retention
     PIPE_STAMP(0);
     for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) {
       if (A.g3.nb) partition_apply(A, p);
@@ -767,7 +778,6 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     PIPE_STAMP(6);
     return;
   }
-  wg -= A.wgp;
   Stage3Smem& S = *reinterpret_cast<Stage3Smem*>(smem_raw);
   const PipeGroup& G = A.g3;
   const u32 tasks = G.task0[G.nb];
@@ -779,8 +789,12 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   TaskPos T = task_pos(G, task < tasks ? task : 0u);
   TaskRec R = stage3_r1(A, T);
   if (!(A.debug & 8u)) {
-    for (u32 k = threadIdx.x; k < 8 * 256; k += kPT) (&S.t8[0][0])[k] = (&A.crc->table[0][0])[k];
-    for (u32 k = threadIdx.x; k < 3 * 4 * 256; k += kPT) (&S.z[0][0][0])[k] = (&A.crc->zshift[0][0][0])[k];
+    // slicing and zero-shift tables are contiguous in CrcConsts and in Stage3Smem: 16-byte copies
+    static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
+    static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
+    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
   }
   bool cand = task < tasks && stage3_cand(A, T, R);
   TaskState Z = stage3_r2(A, T, R, cand);
