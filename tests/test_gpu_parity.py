@@ -178,6 +178,21 @@ def test_pipelined_groups(oracle_mod, group):
         assert dev.state(5)["log_end_offset"] == 0
 
 
+@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "1"}])
+def test_pipelined_dispatch_modes(oracle_mod, monkeypatch, env):
+    # the non-default stage-3 dispatch modes (read at rmq_create): resident task waves looping over
+    # the group's tasks, and stage-3 workgroups dispatched before the other roles
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,
+                         index_interval=1024, max_batch_records=65536, pipeline_depth=4)
+    with dev, ora:
+        spec = StreamSpec(4096, 65536, "zipf", size=100, config_index=2)
+        _pipelined(dev, ora, [make_batch(spec, b) for b in range(6)])
+        hot = np.argsort([-ora.state(p)["log_end_offset"] for p in range(4096)])
+        compare_state(dev, ora, cfg, parts=list(hot[:16]) + list(range(0, 4096, 257)))
+
+
 def test_config_B_pipelined(oracle_mod):
     # BASELINE configs[2] batches submitted back to back in groups of 4
     cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,
