@@ -1,5 +1,6 @@
 # Stage-1 tile of 1024 (default build) vs 2048 records (variant build via RMQ_LIB), then the
 # parity tests on the 2048 build.
+# Variant build: make -C ripplemq_amd/csrc BUILD=../../build/t11 OUT=../../variants/libt11.so CXXFLAGS="... -DRMQ_TILE_BITS=11"
 set -e
 R=$GRAFT_REPO_ROOT
 cd $R
