@@ -78,7 +78,7 @@ struct Stage1Smem {
 
 struct Stage3Smem {
   u32 t8[8][256];       // slicing-by-8 CRC32C tables
-  u32 z[3][4][256];     // register shift past 16, 32, 64 zero bytes
+  u32 z[2][4][256];     // register shift past 16 and 32 zero bytes
   uint4 img[kPW][kTaskRecs][8];  // per wave: the task's records as laid out in the log (<= 128 B each)
   uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16}
 };
@@ -555,16 +555,10 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   return S;
 }
 
-// CRC register of one 16-byte piece followed by d more 16-byte pieces of the record.
-__device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S, uint4 v, u32 jp, u32 d) {
+// CRC register of one 16-byte piece of the record (piece 0 carries the CRC init).
+__device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S, uint4 v, u32 jp) {
   if (jp == 0) v.x ^= 0xFFFFFFFFu;  // CRC init folded into the first payload dword
-  u32 c = (A.debug & 2u) ? v.x : crc_piece16(S.t8, v);
-  if (d & 1u) c = crc_zshift(S.z[0], c);
-  if (d & 2u) c = crc_zshift(S.z[1], c);
-  if (d & 4u) c = crc_zshift(S.z[2], c);
-  for (u32 bb = 3; bb < 28u && (d >> bb) != 0u; ++bb)
-    if ((d >> bb) & 1u) c = gf2_mulmod(A.crc->shift_pow2[bb + 4], c);
-  return c;
+  return (A.debug & 2u) ? v.x : crc_piece16(S.t8, v);
 }
 
 __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
@@ -607,7 +601,8 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
       if (c < nr && jp < m) {
         const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
         const uint4 v = extract_piece(blk[q], pb, sa, nb);
-        acc ^= piece_crc(A, S, v, jp, m - 1u - jp);
+        // Horner over the lane's pieces (jp rises by 2 = 32 bytes): reg(.. || p) = reg(..) * x^256 ^ reg(p)
+        acc = crc_zshift(S.z[1], acc) ^ piece_crc(A, S, v, jp);
         if (img) {
           const_cast<Stage3Smem&>(S).img[w][r32][jp + 1] = v;
         } else {
@@ -618,6 +613,8 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
       }
     }
   }
+  // align the lane's register to the record end: its last piece is m-1 or m-2 (then 16 bytes short)
+  if (ok && m > j && ((m - 1u - j) & 1u)) acc = crc_zshift(S.z[0], acc);
   acc ^= pair_swap(acc);
 
   // ---- header (lane 1), out offset (lane 0), sparse index (lane 1)
