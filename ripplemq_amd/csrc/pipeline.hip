@@ -23,8 +23,8 @@
 //   clears hist for reuse. Workgroup 0 also writes the payload base of every tile in its batch.
 // Stage 3 (group g-2, wave per 32-record task): offset = log end + excl + rank, position likewise,
 //   out offsets, sparse index, then the records' 16-byte pieces are spread over the lanes: payload
-//   loads as aligned 16-byte blocks, CRC32C of each piece from LDS tables (shifted into place by
-//   zero-byte tables, XOR-reduced per record), 16-byte stores into every local replica ring
+//   loads as aligned 16-byte blocks, CRC32C of each piece from LDS tables (folded per lane by
+//   Horner with a zero-byte shift table, XOR-reduced per record), 16-byte stores into every local replica ring
 //   through an LDS image of the log. Partition threads (workgroups of their own, from the start of
 //   the launch): the group's new log end, matchIndex, quorum commit and high watermark, into the
 //   other state set, so no record ever reads a half-updated partition.
@@ -555,7 +555,8 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   return S;
 }
 
-// CRC register of one 16-byte piece of the record (piece 0 carries the CRC init).
+// CRC register of one 16-byte piece of the record (piece 0 carries the CRC init); the caller
+// folds a lane's pieces by Horner's rule with the 32-byte zero-shift table.
 __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S, uint4 v, u32 jp) {
   if (jp == 0) v.x ^= 0xFFFFFFFFu;  // CRC init folded into the first payload dword
   return (A.debug & 2u) ? v.x : crc_piece16(S.t8, v);
