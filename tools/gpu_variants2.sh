@@ -1,4 +1,4 @@
-# Stage-2 lanes per partition column: 8 (default build), 16, 32 (variant builds via RMQ_LIB).
+# Stage-2 lanes per partition column: default build (16), 16, 32 (variant builds via RMQ_LIB).
 # Variant builds: make -C ripplemq_amd/csrc BUILD=../../build/vN OUT=../../variants/libN.so CXXFLAGS="... -DRMQ_SCAN_LANES=N"
 set -e
 R=$GRAFT_REPO_ROOT
