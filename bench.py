@@ -26,6 +26,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -105,6 +107,56 @@ def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float, name: str
                       f"1 thread (ro_append): {nb1} batches, {rate1 / 1e6:.2f} M msgs/s"}
 
 
+def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
+    """Consumer fetch over the bench engine's committed logs (SURVEY §8(d) B_fetch): per round every
+    (partition, consumer) commits an offset lagging the high watermark by U[0, retained records]
+    (config D's lagging consumers, bounded by what retention keeps), then one rmq_fetch of all
+    P x consumers requests into a device buffer, at max = 10 (ConsumerClientImpl.java:21) and
+    max = 1024. Timed with HIP events around the fetch kernels on the engine's fetch stream.
+    B_fetch = 2 (16 + L) per returned record (read log, write output) + 8 ceil(log2(index entries))
+    per request."""
+    P = spec.partitions
+    st = [eng.state(p) for p in range(P)]
+    hw = np.array([s["high_watermark"] for s in st], np.int64)
+    lo = np.array([s["log_start_offset"] for s in st], np.int64)
+    idx_entries = np.maximum(1, np.array([(s["log_end_pos"] - s["log_start_pos"]) // 1024 + 1 for s in st]))
+    search_bytes = int((8 * np.ceil(np.log2(idx_entries + 1))).sum()) * consumers
+    g = np.random.default_rng(0x52495050)
+    pp = np.repeat(np.arange(P, dtype=np.uint32), consumers)
+    cc = np.tile(np.arange(consumers, dtype=np.uint32), P)
+    out = {}
+    for mx in (10, 1024):
+        cap = P * consumers * mx * 128 + 4096
+        d_out = eng.device_alloc(cap)
+        recs = nbytes = 0
+        t_kern = t_wall = 0.0
+        for k in range(rounds):
+            lag = (g.random(P * consumers) * (np.repeat(hw - lo, consumers) + 1)).astype(np.int64)
+            eng.commit_consumer_offset(pp, cc, (np.repeat(hw, consumers) - lag).astype(np.uint64))
+            eng.profile(True)
+            t0 = time.perf_counter()
+            rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+            t_wall += time.perf_counter() - t0
+            _, ms_r = eng.profile_query(3)
+            _, ms_g = eng.profile_query(4)
+            eng.profile(False)
+            if rc or np.any(res["status"] != 0):
+                raise SystemExit(f"bench: fetch leg failed rc={rc} statuses={np.unique(res['status'])}")
+            t_kern += (ms_r + ms_g) / 1e3
+            recs += int(res["count"].sum())
+            nbytes += int(res["bytes"].sum())
+        eng.device_free(d_out)
+        alg = 2 * nbytes + search_bytes * rounds
+        out[f"max{mx}"] = {"records_per_s_kernels": recs / t_kern, "records_per_s_call": recs / t_wall,
+                           "records_per_request": recs / (rounds * P * consumers),
+                           "requests": P * consumers, "rounds": rounds,
+                           "roofline": {"bound": "hbm", "achieved": alg / t_kern / 1e9, "peak": HBM_PEAK_GBS,
+                                        "unit": "GB/s", "frac": alg / t_kern / 1e9 / HBM_PEAK_GBS,
+                                        "kernels": "rmq::fetch_resolve + fetch_place + fetch_gather",
+                                        "mean_us_per_fetch": t_kern / rounds * 1e6}}
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,11 +168,27 @@ def main() -> None:
                     help="ring bytes per (replica, partition); a 64k x 128 B batch needs > 8 MiB")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
     ap.add_argument("--group", type=int, default=4,
                     help="batches per pipeline launch group (cfg.pipeline_depth, 1..8)")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one rank process per GPU ourselves, before this process touches HIP
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        procs = []
+        for r in range(args.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                       LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        rcs = [p.wait() for p in procs]
+        sys.exit(next((rc for rc in rcs if rc), 0))
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the line would misreport n_gpus")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -219,6 +287,8 @@ def main() -> None:
             "device": dev_name,
             "cu_count": cus,
         }
+    if rank == 0 and args.fetch_rounds > 0:
+        out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
     for _, dp, dl, dpay, _, _ in pool:
         eng.device_free(dp)
         eng.device_free(dl)

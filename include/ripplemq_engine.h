@@ -131,7 +131,8 @@ typedef struct rmq_append_stats {
   uint32_t appended;           /* records given offsets */
   uint32_t rejected_not_leader;
   uint32_t rejected_no_partition;
-  uint32_t rejected_no_space;  /* whole batch rejected: sum of record sizes > segment - interval */
+  uint32_t rejected_no_space;  /* records of partitions whose record bytes in this batch exceed
+                                  segment - interval (FORMAT.md §3: the partition takes none) */
   uint32_t rejected_invalid;   /* device batches only: whole batch rejected, a payload range lies
                                   outside payload_bytes (host batches get RMQ_EINVAL instead) */
 } rmq_append_stats;
@@ -159,9 +160,10 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
    with CRC32C into every local replica log, advances the offset index, the quorum commit and
    the high watermark. Asynchronous: returns a ticket; caller buffers must stay valid until
    rmq_poll_commit(ticket) returns RMQ_OK. out_offsets (same memory kind as the batch) gets the
-   offset of each record, or RMQ_OFFSET_NONE if it was rejected (not leader / unknown pidx).
-   If the batch's total record bytes (sum of 16 + align16(len)) exceed segment_bytes -
-   index_interval, no record is appended (rmq_ticket_stats reports rejected_no_space).
+   offset of each record, or RMQ_OFFSET_NONE if it was rejected (unknown pidx / not leader / no
+   space). A partition whose record bytes in this batch (sum of 16 + align16(len)) exceed
+   segment_bytes - index_interval takes none of the batch's records (rmq_ticket_stats reports them
+   as rejected_no_space); the batch's other partitions are unaffected.
    Batches are collected into launch groups of up to cfg.pipeline_depth: the call that fills a
    group issues one kernel launch that ranks it and advances the three groups submitted before
    it (scan, apply, retention); every batch keeps its own semantics. A batch is applied by the

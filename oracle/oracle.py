@@ -183,6 +183,9 @@ class OracleEngine:
             raise EngineError(rc, "oracle")
         return state_to_dict(s, self.cfg.replication_factor)
 
+    def commit_snapshot(self):
+        return np.array([self.state(p)["commit"] for p in range(self.cfg.num_partitions)], np.uint64)
+
     def read_segment(self, replica, pidx, ring_off=0, n=None):
         n = self.cfg.segment_bytes - ring_off if n is None else n
         out = np.empty(n, np.uint8)

@@ -119,6 +119,8 @@ struct ro_engine {
   ro_part* parts;
   uint8_t** rings; /* [replica][partition] -> segment_bytes */
   uint8_t* touched;
+  uint64_t* pbytes; /* [P] record bytes of the current batch per partition */
+  uint8_t* full;    /* [P] 1: the partition takes no record of the current batch (FORMAT.md §3) */
 };
 
 static int cfg_ok(const rmq_config* c) {
@@ -140,8 +142,10 @@ ro_engine* ro_create(const rmq_config* cfg) {
   uint32_t P = cfg->num_partitions, RF = cfg->replication_factor;
   e->parts = (ro_part*)calloc(P, sizeof(ro_part));
   e->touched = (uint8_t*)calloc(P, 1);
+  e->pbytes = (uint64_t*)calloc(P, sizeof(uint64_t));
+  e->full = (uint8_t*)calloc(P, 1);
   e->rings = (uint8_t**)calloc((size_t)P * RF, sizeof(uint8_t*));
-  if (!e->parts || !e->touched || !e->rings) {
+  if (!e->parts || !e->touched || !e->pbytes || !e->full || !e->rings) {
     ro_destroy(e);
     return NULL;
   }
@@ -183,6 +187,8 @@ void ro_destroy(ro_engine* e) {
   free(e->rings);
   free(e->parts);
   free(e->touched);
+  free(e->pbytes);
+  free(e->full);
   free(e);
 }
 
@@ -286,18 +292,34 @@ int ro_become_leader(ro_engine* e, uint32_t p, uint64_t term) {
 /* Append: PartitionStateMachine.onApply -> handleMessageAppendRequest (messages.addAll)       */
 /* ------------------------------------------------------------------------------------------ */
 
-/* The payload-range check (RMQ_EINVAL) and the FORMAT.md §3 batch rule, over every record. */
-static int batch_scan(const ro_engine* e, uint32_t n, const uint32_t* len, const uint64_t* payload_off,
-                      const uint8_t* payload, uint64_t payload_bytes, int* no_space) {
-  uint64_t run = 0, out_bytes = 0;
+static uint64_t rec_size(uint32_t L) {
+  return RMQ_RECORD_HEADER_BYTES + ((L + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
+}
+
+/* The payload-range check (RMQ_EINVAL) over every record. */
+static int range_check(uint32_t n, const uint32_t* len, const uint64_t* payload_off, const uint8_t* payload,
+                       uint64_t payload_bytes) {
+  uint64_t run = 0;
   for (uint32_t i = 0; i < n; ++i) {
     uint64_t off = payload_off ? payload_off[i] : run;
     if (len[i] && (!payload || off > payload_bytes || len[i] > payload_bytes - off)) return RMQ_EINVAL;
     run += len[i];
-    out_bytes += RMQ_RECORD_HEADER_BYTES + ((len[i] + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
   }
-  *no_space = out_bytes > e->cfg.segment_bytes - e->cfg.index_interval;
   return RMQ_OK;
+}
+
+/* The FORMAT.md §3 space rule for the partitions p with p % T == t: bytes[p] = record bytes the
+   batch holds for p; full[p] = 1 if they exceed segment - interval (p then takes no record of the
+   batch). */
+static void space_scan(const ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* len, uint64_t* bytes,
+                       uint8_t* full, uint32_t t, uint32_t T) {
+  const uint32_t P = e->cfg.num_partitions;
+  for (uint32_t i = 0; i < n; ++i)
+    if (pidx[i] < P && pidx[i] % T == t) bytes[pidx[i]] = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (pidx[i] < P && pidx[i] % T == t) bytes[pidx[i]] += rec_size(len[i]);
+  for (uint32_t i = 0; i < n; ++i)
+    if (pidx[i] < P && pidx[i] % T == t) full[pidx[i]] = bytes[pidx[i]] > e->cfg.segment_bytes - e->cfg.index_interval;
 }
 
 typedef struct {
@@ -311,7 +333,7 @@ static int append_record(ro_engine* e, ro_part* s, uint32_t p, const uint8_t* sr
                          uint64_t* out_offset) {
   const rmq_config* c = &e->cfg;
   const uint64_t I = c->index_interval;
-  const uint64_t rs = RMQ_RECORD_HEADER_BYTES + ((L + RMQ_RECORD_ALIGN - 1u) & ~(uint64_t)(RMQ_RECORD_ALIGN - 1u));
+  const uint64_t rs = rec_size(L);
   if (rs > rec->cap) {
     uint8_t* nr = (uint8_t*)realloc(rec->v, rs);
     if (!nr) return RMQ_ENOMEM;
@@ -354,15 +376,9 @@ int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* le
   memset(&st, 0, sizeof st);
   st.records = n;
   if (n && (!pidx || !len || !out_offsets)) return RMQ_EINVAL;
-  int no_space = 0;
-  int rc = batch_scan(e, n, len, payload_off, payload, payload_bytes, &no_space);
+  int rc = range_check(n, len, payload_off, payload, payload_bytes);
   if (rc) return rc;
-  if (no_space) {
-    for (uint32_t i = 0; i < n; ++i) out_offsets[i] = RMQ_OFFSET_NONE;
-    st.rejected_no_space = n;
-    if (stats) *stats = st;
-    return RMQ_OK;
-  }
+  space_scan(e, n, pidx, len, e->pbytes, e->full, 0, 1);
   memset(e->touched, 0, P);
   ro_buf rec = {NULL, 0};
   uint64_t run = 0;
@@ -379,6 +395,11 @@ int ro_append(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint32_t* le
     if (!s->is_leader) {
       out_offsets[i] = RMQ_OFFSET_NONE;
       st.rejected_not_leader++;
+      continue;
+    }
+    if (e->full[p]) {
+      out_offsets[i] = RMQ_OFFSET_NONE;
+      st.rejected_no_space++;
       continue;
     }
     rc = append_record(e, s, p, payload + off, len[i], &rec, &out_offsets[i]);
@@ -433,8 +454,8 @@ static void* shard_main(void* arg) {
     const rmq_batch* b = &j->b[k];
     uint64_t* out = j->out[k];
     rmq_append_stats* st = &j->st[k];
-    int no_space = 0;
-    int rc = batch_scan(e, b->n, b->len, b->payload_off, b->payload, b->payload_bytes, &no_space);
+    int rc = range_check(b->n, b->len, b->payload_off, b->payload, b->payload_bytes);
+    if (!rc) space_scan(e, b->n, b->pidx, b->len, e->pbytes, e->full, j->t, j->T); /* own partitions only */
     uint32_t nm = 0;
     uint64_t run = 0;
     for (uint32_t i = 0; i < b->n && !rc; ++i) {
@@ -443,15 +464,15 @@ static void* shard_main(void* arg) {
       run += b->len[i];
       if ((p < P ? p % j->T : 0u) != j->t) continue;
       st->records++;
-      if (no_space) {
-        out[i] = RMQ_OFFSET_NONE;
-        st->rejected_no_space++;
-      } else if (p >= P) {
+      if (p >= P) {
         out[i] = RMQ_OFFSET_NONE;
         st->rejected_no_partition++;
       } else if (!e->parts[p].is_leader) {
         out[i] = RMQ_OFFSET_NONE;
         st->rejected_not_leader++;
+      } else if (e->full[p]) {
+        out[i] = RMQ_OFFSET_NONE;
+        st->rejected_no_space++;
       } else {
         rc = append_record(e, &e->parts[p], p, b->payload + off, b->len[i], &rec, &out[i]);
         if (rc) break;

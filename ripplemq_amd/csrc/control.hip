@@ -3,8 +3,8 @@
 //   * external replica acks (matchIndex = max(matchIndex, ack)),
 //   * leader start (term_start = log end; Raft matchIndex reset for remote replicas),
 //   * consumer-offset commits (PartitionStateMachine.handleConsumerOffsetUpdateRequest,
-//     mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:71-77): last writer wins
-//     inside one call, resolved deterministically by an {epoch | item+1} atomicMax ticket.
+//     mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:71-77): last writer wins;
+//     the host keeps the last item per (partition, consumer), so this is a plain scatter.
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "partition_ops.hpp"
@@ -34,18 +34,9 @@ __global__ void become_leader_kernel(DevState st, u32 only) {
   for (u32 r = 0; r < st.RF; ++r) st.match[(u64)p * st.RF + r] = (lm >> r & 1u) ? leo : 0ull;
 }
 
-__global__ void consumer_ticket_kernel(ConsumerCommitArgs a) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  const u64 slot = (u64)a.pidx[i] * a.st.C + a.consumer[i];
-  atomicMax((unsigned long long*)&a.winner[slot], ((u64)a.epoch << 32) | (i + 1u));
-}
-
 __global__ void consumer_apply_kernel(ConsumerCommitArgs a) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
-  const u64 slot = (u64)a.pidx[i] * a.st.C + a.consumer[i];
-  if (a.winner[slot] == (((u64)a.epoch << 32) | (i + 1u))) a.st.cons[slot] = a.offset[i];
+  if (i < a.n) a.st.cons[(u64)a.pidx[i] * a.st.C + a.consumer[i]] = a.offset[i];
 }
 
 static inline dim3 grid_for(u32 n, u32 b) { return dim3((n + b - 1) / b ? (n + b - 1) / b : 1); }
@@ -66,7 +57,6 @@ void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s) {
 }
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s) {
   if (!a.n) return;
-  hipLaunchKernelGGL(consumer_ticket_kernel, grid_for(a.n, 256), dim3(256), 0, s, a);
   hipLaunchKernelGGL(consumer_apply_kernel, grid_for(a.n, 256), dim3(256), 0, s, a);
 }
 

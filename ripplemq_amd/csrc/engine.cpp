@@ -17,9 +17,11 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <new>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/ripplemq_engine.h"
@@ -75,13 +77,11 @@ struct rmq_engine {
   StateSet sets[2]{};
   uint64_t applied = 0;     // stage-3 launches issued
   CrcConsts* d_crc = nullptr;
-  uint64_t* d_winner = nullptr;
   uint32_t* d_err = nullptr;
   uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
   uint32_t max_tasks = 0;
   uint32_t max_tiles = 0;
   uint32_t key_passes = 0;
-  uint32_t epoch = 0;
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
   // pipeline: the group being formed, then groups ranked (need stage 2), scanned (need stage 3)
@@ -95,18 +95,27 @@ struct rmq_engine {
   uint64_t* done_host = nullptr;     // pinned: launch k-1 complete, written by launch k
   uint64_t* done_dev = nullptr;
   uint64_t last_ticket = 0;
-  uint64_t last_nonempty = 0;
-  std::vector<uint32_t> ticket_n;        // [kStatsRing]
-  std::vector<uint64_t> ticket_launch;   // [kStatsRing] launch applying the ticket (0: not yet)
-  std::vector<uint64_t> ticket_dep;      // [kStatsRing] empty batches: the ticket they wait for
+  std::vector<uint32_t> ticket_n;        // [kStatsRing] records of each recent ticket (stats)
+  // completion: tickets are applied in order, launch after launch. marks = {hi, L}: every ticket
+  // <= hi not covered by an earlier mark is applied by launch L (empty tickets count with the
+  // non-empty one before them); every ticket <= done_ticket is complete.
+  std::deque<std::pair<uint64_t, uint64_t>> marks;
+  uint64_t done_ticket = 0;
   // host mirrors of control state
   std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
   std::vector<uint64_t> term;
-  // fetch scratch
+  // fetch: its own stream and scratch, serialised by fetch_mu (engine state under mu only while
+  // the fetch is ordered against the pipeline stream)
+  std::mutex fetch_mu;
+  hipStream_t fetch_s = nullptr;
+  hipEvent_t ev_main = nullptr, ev_fetch = nullptr;
   uint32_t* d_req = nullptr;
   uint64_t* d_res = nullptr;
   uint64_t* d_aux = nullptr;
+  uint32_t* d_cpre = nullptr;
   uint64_t* d_total = nullptr;
+  uint32_t* h_req = nullptr;   // pinned
+  uint64_t* h_res = nullptr;   // pinned [cap][4] + 2 totals
   uint32_t fetch_cap = 0;
   uint8_t* d_fetch_out = nullptr;
   uint64_t fetch_out_cap = 0;
@@ -219,13 +228,14 @@ void build_crc_consts(CrcConsts* c) {
   uint32_t x2n[40];
   x2n[0] = 0x40000000u;  // x^1 in the reflected representation
   for (int k = 1; k < 40; ++k) x2n[k] = host_mulmod(x2n[k - 1], x2n[k - 1]);
-  for (int j = 0; j < 32; ++j) c->shift_pow2[j] = x2n[j + 3];  // x^(8 * 2^j)
-  c->pow8[0] = 0x80000000u;                                     // x^0
-  for (uint32_t n = 1; n < kCrcPow8; ++n) c->pow8[n] = host_mulmod(c->pow8[n - 1], x2n[3]);
-  for (uint32_t k = 0; k < 3; ++k)  // shift past 16 << k zero bytes = multiply by x^(2^(7+k))
+  for (uint32_t k = 0; k < 2; ++k)  // shift past 16 << k zero bytes = multiply by x^(2^(7+k))
     for (uint32_t i = 0; i < 4; ++i)
       for (uint32_t b = 0; b < 256; ++b) c->zshift[k][i][b] = host_mulmod(b << (8 * i), x2n[7 + k]);
-  for (uint32_t n = 0; n < 16; ++n) c->inv_pad[n] = n ? host_inverse(c->pow8[n]) : 0x80000000u;
+  uint32_t x8n = 0x80000000u;  // x^(8n), n = 0..15
+  for (uint32_t n = 0; n < 16; ++n) {
+    c->inv_pad[n] = n ? host_inverse(x8n) : 0x80000000u;
+    x8n = host_mulmod(x8n, x2n[3]);
+  }
 }
 
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
@@ -288,6 +298,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.cur = cur;
   a.nxt = nxt;
   a.key_passes = e->key_passes;
+  a.gt = e->max_group_tiles;
   a.s3_first = e->s3_first;
   a.nospace_limit = e->cfg.segment_bytes - e->cfg.index_interval;
   a.crc = e->d_crc;
@@ -344,10 +355,13 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     e->st.used = nxt.used;
     for (uint32_t j = 0; j < s3->nb; ++j) {
       const InFlight& f = s3->b[j];
-      e->ticket_launch[f.ticket % kStatsRing] = e->launch_seq;
       if (f.host_out && f.b.n)
         HIP_TRY(hipMemcpyAsync(f.host_out, f.b.out_offsets, f.b.n * 8ull, hipMemcpyDeviceToHost, e->main_s));
     }
+    // this launch also completes the empty tickets up to the next group's first one
+    const GroupFlight* next = s2 ? s2 : s1;
+    const uint64_t hi = next ? next->b[0].ticket - 1 : e->last_ticket;
+    e->marks.emplace_back(hi, e->launch_seq);
   }
   return RMQ_OK;
 }
@@ -388,26 +402,52 @@ int drain(rmq_engine* e) {
   return check_err(e);
 }
 
+// Wait for everything issued on the pipeline stream, without flushing batches that are still
+// forming or in the pipeline's earlier stages (reads of committed state, consumer commits).
+int quiesce(rmq_engine* e) {
+  HIP_TRY(hipStreamSynchronize(e->main_s));
+  return check_err(e);
+}
+
 // Has the launch with sequence number L completed?
 bool launch_done(rmq_engine* e, uint64_t L) {
   if (L <= __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE)) return true;
   return hipStreamQuery(e->main_s) == hipSuccess;
 }
 
-// The ticket whose completion `t` stands for (empty batches wait for the last non-empty one).
-uint64_t resolve_ticket(rmq_engine* e, uint64_t t) {
-  return e->ticket_n[t % kStatsRing] ? t : e->ticket_dep[t % kStatsRing];
+// Ticket completion: 1 complete, 0 applied by a launch still running, -1 not applied yet.
+int ticket_state(rmq_engine* e, uint64_t t) {
+  while (!e->marks.empty() && launch_done(e, e->marks.front().second)) {
+    e->done_ticket = std::max(e->done_ticket, e->marks.front().first);
+    e->marks.pop_front();
+  }
+  if (t <= e->done_ticket) return 1;
+  if (!e->marks.empty() && t <= e->marks.back().first) return 0;
+  return -1;
 }
 
-// Block until ticket t (non-empty, issued) is applied and complete.
+// Block until ticket t (issued) is applied and complete.
 int wait_ticket(rmq_engine* e, uint64_t t) {
-  if (!t) return RMQ_OK;
-  if (!e->ticket_launch[t % kStatsRing]) {
+  int s = ticket_state(e, t);
+  if (s < 0) {
     int rc = flush(e);
     if (rc) return rc;
+    s = ticket_state(e, t);
   }
-  const uint64_t L = e->ticket_launch[t % kStatsRing];
-  if (!launch_done(e, L)) HIP_TRY(hipStreamSynchronize(e->main_s));
+  if (s == 0) {
+    HIP_TRY(hipStreamSynchronize(e->main_s));
+    ticket_state(e, t);
+  }
+  return RMQ_OK;
+}
+
+// The pipeline advances the double-buffered log end only for partitions this engine leads; before
+// a partition changes role, both state sets must hold its current log end (engine drained).
+int equalize_state_sets(rmq_engine* e) {
+  const StateSet other = e->sets[(e->applied + 1) & 1u];
+  const size_t bytes = (size_t)e->cfg.num_partitions * 8;
+  HIP_TRY(hipMemcpy(other.leo, e->st.leo, bytes, hipMemcpyDeviceToDevice));
+  HIP_TRY(hipMemcpy(other.used, e->st.used, bytes, hipMemcpyDeviceToDevice));
   return RMQ_OK;
 }
 
@@ -455,8 +495,8 @@ void free_engine(rmq_engine* e) {
   }
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_winner, e->d_err,
-                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_total, e->d_fetch_out,
+                             s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_err,
+                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_total, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -473,6 +513,11 @@ void free_engine(rmq_engine* e) {
   for (void* p : bufs)
     if (p) hipFree(p);
   if (e->done_host) hipHostFree(e->done_host);
+  if (e->h_req) hipHostFree(e->h_req);
+  if (e->h_res) hipHostFree(e->h_res);
+  if (e->ev_main) hipEventDestroy(e->ev_main);
+  if (e->ev_fetch) hipEventDestroy(e->ev_fetch);
+  if (e->fetch_s) hipStreamDestroy(e->fetch_s);
   for (auto& v : e->prof)
     for (EvPair& p : v) {
       if (p.a) hipEventDestroy(p.a);
@@ -570,6 +615,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->cu_count = (uint32_t)prop.multiProcessorCount;
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
+  CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
+  CREATE_HIP(hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming));
+  CREATE_HIP(hipEventCreateWithFlags(&e->ev_fetch, hipEventDisableTiming));
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
   DevState& s = e->st;
@@ -600,7 +648,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.index, (size_t)P * s.icap * 2));
   CREATE_TRY(dalloc(&s.logs, (size_t)RF * P * s.seg));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
-  CREATE_TRY(dalloc(&e->d_winner, (size_t)P * C));
   CREATE_TRY(dalloc(&e->d_err, 1));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
@@ -639,8 +686,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->ranks.assign((size_t)P * RF, cfg->rank);
   e->term.assign(P, 1ull);
   e->ticket_n.assign(kStatsRing, 0u);
-  e->ticket_launch.assign(kStatsRing, 0ull);
-  e->ticket_dep.assign(kStatsRing, 0ull);
   {
     uint32_t bits = 0;
     while ((1u << bits) < P) ++bits;  // keys in [0, P)
@@ -664,6 +709,7 @@ int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* ranks, uint32
   if (!ranks || rf != RF || leader_slot >= rf) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
+  if (!rc) rc = equalize_state_sets(e);
   if (rc) return rc;
   uint32_t mask = 0;
   for (uint32_t r = 0; r < RF; ++r) {
@@ -691,6 +737,7 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   }
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
+  if (!rc) rc = equalize_state_sets(e);
   if (rc) return rc;
   for (uint32_t p = lo; p < hi; ++p) {
     uint32_t slot = 0;
@@ -728,10 +775,15 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   const uint64_t t = ++e->last_ticket;
   *ticket = t;
   e->ticket_n[t % kStatsRing] = n;
-  e->ticket_launch[t % kStatsRing] = 0;
-  e->ticket_dep[t % kStatsRing] = e->last_nonempty;
-  if (n == 0) return RMQ_OK;  // completes with the last non-empty batch before it
-  e->last_nonempty = t;
+  if (n == 0) {  // completes with the last non-empty batch before it
+    if (!e->forming.nb && !e->has1 && !e->has2) {
+      if (!e->marks.empty())
+        e->marks.back().first = t;
+      else
+        e->done_ticket = t;
+    }
+    return RMQ_OK;
+  }
 
   InFlight f;
   f.ticket = t;
@@ -815,15 +867,16 @@ int rmq_ack(rmq_engine* e, const uint32_t* pidx, const uint32_t* slot, const uin
 int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64_t* hw_out) {
   if (!e) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
-  if (ticket > e->last_ticket || (ticket && e->last_ticket - ticket >= kStatsRing)) return RMQ_EINVAL;
+  if (ticket > e->last_ticket) return RMQ_EINVAL;  // never issued
   HIP_TRY(hipSetDevice(e->device));
-  const uint64_t t = ticket ? resolve_ticket(e, ticket) : 0;
-  if (t) {
-    if (!e->ticket_launch[t % kStatsRing]) {
+  if (ticket) {
+    int s = ticket_state(e, ticket);
+    if (s < 0) {
       int rc = flush(e);  // a poll pushes the batch through the remaining stages
       if (rc) return rc;
+      s = ticket_state(e, ticket);
     }
-    if (!launch_done(e, e->ticket_launch[t % kStatsRing])) return RMQ_PENDING;
+    if (s == 0) return RMQ_PENDING;
   }
   int rc = check_err(e);
   if (rc) return rc;
@@ -842,7 +895,7 @@ int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out) {
   std::lock_guard<std::mutex> g(e->mu);
   if (!ticket || ticket > e->last_ticket || e->last_ticket - ticket >= kStatsRing) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = wait_ticket(e, resolve_ticket(e, ticket));
+  int rc = wait_ticket(e, ticket);
   if (rc) return rc;
   const uint32_t n = e->ticket_n[ticket % kStatsRing];
   const uint32_t tasks = (n + kTaskRecs - 1) / kTaskRecs;
@@ -896,8 +949,24 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
     vo.push_back(offset[i]);
   }
   if (vp.empty()) return rc_all;
+  // last writer wins (PartitionStateMachine.java:71-77): keep only the last item per
+  // (partition, consumer), so the device scatter has no two writers to one slot
+  {
+    std::unordered_set<uint64_t> seen;
+    size_t k = vp.size();
+    for (size_t i = vp.size(); i-- > 0;) {
+      if (!seen.insert((uint64_t)vp[i] * e->cfg.max_consumers + vc[i]).second) continue;
+      --k;
+      vp[k] = vp[i];
+      vc[k] = vc[i];
+      vo[k] = vo[i];
+    }
+    vp.erase(vp.begin(), vp.begin() + k);
+    vc.erase(vc.begin(), vc.begin() + k);
+    vo.erase(vo.begin(), vo.begin() + k);
+  }
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = quiesce(e);  // the ctl buffers are free; no flush: the pipeline never reads the table
   if (rc) return rc;
   const uint32_t m = (uint32_t)vp.size();
   rc = ensure_ctl(e, m);
@@ -910,38 +979,45 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   a.pidx = e->d_ctl32;
   a.consumer = e->d_ctl32 + e->ctl_cap;
   a.offset = e->d_ctl64;
-  a.winner = e->d_winner;
   a.n = m;
-  a.epoch = ++e->epoch;
   launch_consumer_commit(a, e->main_s);
   HIP_TRY(hipGetLastError());
-  rc = drain(e);
+  rc = quiesce(e);
   return rc ? rc : rc_all;
 }
 
 int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
               uint64_t out_cap, rmq_fetch_res* res, uint64_t* bytes_used) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  std::lock_guard<std::mutex> fg(e->fetch_mu);
   if (bytes_used) *bytes_used = 0;
   if (!n) return RMQ_OK;
   if (!reqs || !res || (mem != RMQ_MEM_HOST && mem != RMQ_MEM_DEVICE)) return RMQ_EINVAL;
   if (out_cap && !out) return RMQ_EINVAL;
-  if (mem == RMQ_MEM_DEVICE && (reinterpret_cast<uintptr_t>(out) & 3u)) return RMQ_EINVAL;
+  if (mem == RMQ_MEM_DEVICE && (reinterpret_cast<uintptr_t>(out) & 15u)) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
-  if (rc) return rc;
+  int rc = RMQ_OK;
   if (n > e->fetch_cap) {
     hipFree(e->d_req);
     hipFree(e->d_res);
     hipFree(e->d_aux);
+    hipFree(e->d_cpre);
+    if (e->h_req) hipHostFree(e->h_req);
+    if (e->h_res) hipHostFree(e->h_res);
+    e->d_req = nullptr;
+    e->d_res = e->d_aux = nullptr;
+    e->d_cpre = e->h_req = nullptr;
+    e->h_res = nullptr;
     e->fetch_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     rc = dalloc(&e->d_req, (size_t)cap * 4);
     if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4);
     if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
-    if (!rc && !e->d_total) rc = dalloc(&e->d_total, 1);
+    if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 1);
+    if (!rc && !e->d_total) rc = dalloc(&e->d_total, 2);
     if (rc) return rc;
+    HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
+    HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));
     e->fetch_cap = cap;
   }
   uint8_t* d_out = out;
@@ -956,44 +1032,54 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     }
     d_out = e->d_fetch_out;
   }
-  HIP_TRY(hipMemcpy(e->d_req, reqs, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice));
-  FetchArgs a{};
-  a.st = e->st;
-  a.req = e->d_req;
-  a.res = e->d_res;
-  a.aux = e->d_aux;
-  a.out = d_out;
-  a.out_cap = out_cap;
-  a.n = n;
-  a.total = e->d_total;
-  hipEvent_t r0 = nullptr, r1 = nullptr, g0 = nullptr, g1 = nullptr;
-  if (e->profile) {
-    r0 = pool_event(e);
-    r1 = pool_event(e);
-    g0 = pool_event(e);
-    g1 = pool_event(e);
+  std::memcpy(e->h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
+  uint64_t* const h_total = e->h_res + (size_t)n * 4;
+  {
+    // Order against the append pipeline without flushing it: the fetch reads the committed state
+    // after the last launch issued so far, and the next launch waits for the fetch, so no ring
+    // bytes or log starts it reads change under it.
+    std::lock_guard<std::mutex> g(e->mu);
+    FetchArgs a{};
+    a.st = e->st;
+    a.req = e->d_req;
+    a.res = e->d_res;
+    a.aux = e->d_aux;
+    a.cpre = e->d_cpre;
+    a.out = d_out;
+    a.out_cap = out_cap;
+    a.n = n;
+    a.gather_wgs = std::max<uint32_t>(1u, 4u * e->cu_count);
+    a.total = e->d_total;
+    HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
+    HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
+    HIP_TRY(hipMemcpyAsync(e->d_req, e->h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
+    hipEvent_t r0 = nullptr, r1 = nullptr, g0 = nullptr, g1 = nullptr;
+    if (e->profile) {
+      r0 = pool_event(e);
+      r1 = pool_event(e);
+      g0 = pool_event(e);
+      g1 = pool_event(e);
+      e->prof[3].push_back({r0, r1});
+      e->prof[4].push_back({g0, g1});
+    }
+    launch_fetch(a, e->fetch_s, r0, r1, g0, g1);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, (size_t)n * 32, hipMemcpyDeviceToHost, e->fetch_s));
+    HIP_TRY(hipMemcpyAsync(h_total, e->d_total, 16, hipMemcpyDeviceToHost, e->fetch_s));
+    HIP_TRY(hipEventRecord(e->ev_fetch, e->fetch_s));
+    HIP_TRY(hipStreamWaitEvent(e->main_s, e->ev_fetch, 0));
   }
-  launch_fetch(a, e->main_s, r0, r1, g0, g1);
-  HIP_TRY(hipGetLastError());
-  if (e->profile) {
-    e->prof[3].push_back({r0, r1});
-    e->prof[4].push_back({g0, g1});
-  }
-  rc = drain(e);
-  if (rc) return rc;
-  std::vector<uint64_t> hres((size_t)n * 4);
-  uint64_t total = 0;
-  HIP_TRY(hipMemcpy(hres.data(), e->d_res, hres.size() * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(&total, e->d_total, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipEventSynchronize(e->ev_fetch));
   int rc_all = RMQ_OK;
   for (uint32_t r = 0; r < n; ++r) {
+    const uint64_t* h = e->h_res + 4ull * r;
     rmq_fetch_res& x = res[r];
     std::memset(&x, 0, sizeof x);
-    x.start_offset = hres[4 * r + 0];
-    x.out_pos = hres[4 * r + 1];
-    x.count = (uint32_t)hres[4 * r + 2];
-    x.bytes = (uint32_t)(hres[4 * r + 2] >> 32);
-    x.status = (int32_t)(uint32_t)hres[4 * r + 3];
+    x.start_offset = h[0];
+    x.out_pos = h[1];
+    x.count = (uint32_t)h[2];
+    x.bytes = (uint32_t)(h[2] >> 32);
+    x.status = (int32_t)(uint32_t)h[3];
     if (x.status == RMQ_ENOSPC) rc_all = RMQ_ENOSPC;
   }
   if (mem == RMQ_MEM_HOST && out_cap) {
@@ -1006,12 +1092,13 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
         hi += res[r].bytes;
         continue;
       }
-      if (hi > lo) HIP_TRY(hipMemcpy(out + lo, d_out + lo, hi - lo, hipMemcpyDeviceToHost));
+      if (hi > lo) HIP_TRY(hipMemcpyAsync(out + lo, d_out + lo, hi - lo, hipMemcpyDeviceToHost, e->fetch_s));
       lo = hi = served ? res[r].out_pos : 0;
       if (served) hi += res[r].bytes;
     }
+    HIP_TRY(hipStreamSynchronize(e->fetch_s));
   }
-  if (bytes_used) *bytes_used = total;
+  if (bytes_used) *bytes_used = h_total[0];
   return rc_all;
 }
 
@@ -1020,7 +1107,7 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   std::lock_guard<std::mutex> g(e->mu);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = quiesce(e);
   if (rc) return rc;
   const DevState& s = e->st;
   const uint32_t RF = e->cfg.replication_factor;
@@ -1047,7 +1134,7 @@ int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t p, uint64_t ring_
   const uint64_t S = e->cfg.segment_bytes;
   if (replica >= e->cfg.replication_factor || ring_off > S || len > S - ring_off) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = quiesce(e);
   if (rc) return rc;
   if (len)
     HIP_TRY(hipMemcpy(out, e->st.logs + ((uint64_t)replica * e->cfg.num_partitions + p) * S + ring_off,
@@ -1062,7 +1149,7 @@ int rmq_read_index(rmq_engine* e, uint32_t p, uint64_t m_first, uint64_t count, 
   const uint32_t icap = e->st.icap;
   if (count > icap) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = quiesce(e);
   if (rc) return rc;
   std::vector<uint64_t> ring((size_t)icap * 2);
   HIP_TRY(hipMemcpy(ring.data(), e->st.index + (size_t)p * icap * 2, ring.size() * 8, hipMemcpyDeviceToHost));
@@ -1079,7 +1166,7 @@ int rmq_read_consumer_offsets(rmq_engine* e, uint32_t p, uint64_t* out) {
   std::lock_guard<std::mutex> g(e->mu);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = quiesce(e);
   if (rc) return rc;
   HIP_TRY(hipMemcpy(out, e->st.cons + (size_t)p * e->cfg.max_consumers, e->cfg.max_consumers * 8ull,
                     hipMemcpyDeviceToHost));

@@ -81,15 +81,16 @@ struct PipeGroup {
 // Group-local scratch of one pipeline set (four sets rotate: a group is ranked in launch k,
 // scanned in k+1, applied in k+2 and its retention evaluated in k+3).
 struct PipeScratch {
-  uint64_t* hist;       // [tiles][P] tile aggregate {count << 40 | bytes/16}; 0 = absent (stage 2 clears)
-  uint64_t* excl;       // [tiles][P] exclusive prefix over the group's tiles of applied batches
-  uint64_t* totals;     // [P] group aggregate over applied batches
-  uint64_t* bcum;       // [kMaxGroup][P] aggregate through batch j (applied batches)
+  uint64_t* hist;       // [P][gt] tile aggregate {count << 40 | bytes/16}; 0 = absent (stage 2 clears)
+  uint64_t* excl;       // [P][gt] exclusive prefix over the group's accepted cells (bit 63: the
+                        //   cell's (batch, partition) is rejected for space, FORMAT.md §3)
+  uint64_t* totals;     // [P] group aggregate over accepted cells
+  uint64_t* bcum;       // [kMaxGroup][P] aggregate through batch j (accepted cells)
   uint2* crank;         // [tiles * kTileRecs] {rank in tile run | flags << 29, bytes/16 before it in the run}
   uint32_t* pre;        // [tiles * kTileRecs] payload bytes before the record inside its tile
   uint64_t* tsum;       // [tiles][4] {payload bytes, record bytes, invalid records, 0}
   uint64_t* tile_base;  // [tiles] payload offset of the tile's first record inside its batch
-  uint64_t* binfo;      // [kMaxGroup][4] per batch {reject flags (1 no space, 2 invalid), record bytes, payload bytes, 0}
+  uint64_t* binfo;      // [kMaxGroup][4] per batch {reject flags (2 invalid payload ranges), 0, payload bytes, 0}
 };
 
 // The single per-group launch: stage 1 (rank the tiles of group k), stage 2 (column scans of
@@ -101,11 +102,12 @@ struct PipeArgs {
   PipeScratch s1, s2, s3, s4;
   uint32_t wg1, wg2, wgp, wg3;  // workgroups per role, in this order along blockIdx.x
   uint32_t key_passes;     // 1 (P <= 256) or 2
+  uint32_t gt;             // tiles per hist / excl column (group tile capacity)
   uint32_t s3_first;       // 1: stage-3 workgroups first along blockIdx.x (dispatched first)
   uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2
-  uint64_t nospace_limit;  // segment - interval
+  uint64_t nospace_limit;  // segment - interval: record bytes one batch may add to one partition
   const CrcConsts* crc;
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
   uint64_t launch_seq;
@@ -116,22 +118,22 @@ struct FetchArgs {
   DevState st;
   const uint32_t* req;       // [n][4] {pidx, consumer, max, reserved}
   uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}
-  uint64_t* aux;             // [n][2] {source byte position, pidx}
-  uint8_t* out;
+  uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
+  uint32_t* cpre;            // [n + 1] exclusive prefix of the served requests' 1 KiB chunks
+  uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
   uint32_t n;
-  uint32_t pad;
-  uint64_t* total;           // [1] bytes needed
+  uint32_t gather_wgs;       // gather grid (waves loop over the chunks)
+  uint64_t* total;           // [2] {bytes needed, chunks}
 };
 
-struct ConsumerCommitArgs {
+struct ConsumerCommitArgs {  // one item per (partition, consumer): the host resolved last-writer-wins
   DevState st;
   const uint32_t* pidx;
   const uint32_t* consumer;
   const uint64_t* offset;
-  uint64_t* winner;          // [P*C] {epoch:32 | item+1:32}, monotone across calls
   uint32_t n;
-  uint32_t epoch;
+  uint32_t pad;
 };
 
 struct AckArgs {

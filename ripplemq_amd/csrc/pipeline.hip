@@ -16,13 +16,18 @@
 //   stable LDS radix sort of the tile by partition id (8-bit passes, ballot-match ranks), a
 //   segmented scan of {1, record bytes/16} over the sorted tile, which gives every record its
 //   count / byte rank inside its partition's run in the tile, and the tile aggregate of each
-//   present partition, written sparsely into hist[tile][p]. Also the tile's payload prefix and sums.
-// Stage 2 (group g-1, 16 threads per partition): the batch rules (no space, invalid payload ranges)
-//   from the tile sums, then an exclusive scan of hist[.][p] over the group's tiles that skips
-//   rejected batches -> excl[tile][p], the aggregate through each batch bcum[j][p] and totals[p];
-//   clears hist for reuse. Workgroup 0 also writes the payload base of every tile in its batch.
+//   present partition, written sparsely into the column-major hist[p][tile]. Also the tile's
+//   payload prefix and sums.
+// Stage 2 (group g-1, 16 threads per partition column, contiguous column reads): the batch rule
+//   for invalid payload ranges from the tile sums, then per batch an exclusive scan of hist[p][.]
+//   over the batch's tiles -> excl[p][tile]; a (batch, partition) whose record bytes exceed
+//   segment - interval takes no record (FORMAT.md §3: its cells are flagged kExclNoSpace and it
+//   adds nothing to the prefix); the aggregate through each batch bcum[j][p] and totals[p]; clears
+//   hist for reuse. Workgroup 0 also writes the payload base of every tile in its batch.
 // Stage 3 (group g-2, wave per 32-record task): offset = log end + excl + rank, position likewise,
-//   out offsets, sparse index, then the records' 16-byte pieces are spread over the lanes: payload
+//   out offsets, sparse index, then the records' 16-byte pieces are spread over the lanes (a piece
+//   whose ring slot a later piece of the same group overwrites is not stored, so no two stores of
+//   one launch ever hit the same ring bytes): payload
 //   loads as aligned 16-byte blocks, CRC32C of each piece from LDS tables (folded per lane by
 //   Horner with a zero-byte shift table, XOR-reduced per record), 16-byte stores into every local replica ring
 //   through an LDS image of the log. Partition threads (workgroups of their own, from the start of
@@ -52,7 +57,9 @@ constexpr u32 kRankMask = (1u << kFlagShift) - 1u;
 constexpr u32 kFlNoPart = 1u, kFlInvalid = 4u, kFlJunk = 7u;
 constexpr u64 kLow40 = (1ull << 40) - 1ull;
 constexpr u64 kOne40 = 1ull << 40;
-constexpr u32 kRejNoSpace = 1u, kRejInvalid = 2u;
+constexpr u64 kCnt23 = (1ull << 23) - 1ull;  // count field of an excl value (bits 40..62)
+constexpr u64 kExclNoSpace = 1ull << 63;     // excl flag: the cell's (batch, partition) is rejected
+constexpr u32 kRejInvalid = 2u;
 
 // Diagnostic phase stamps (RMQ_STAMPS): stamps[(workgroup * 8 + wave) * 8 + k], s_memrealtime
 // (100 MHz). Never read by the kernel.
@@ -167,9 +174,9 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
     item[r] = (pc[r] << kIB) | q;
   }
 
-  // ---- input-order scans: payload prefix per record, tile sums {payload, record bytes}
+  // ---- input-order scans: payload prefix per record, tile sums {payload, invalid ranges}
   {
-    u64 carry = 0, rb = 0;
+    u64 carry = 0;
     u32 pre_r[kTI];
 #pragma unroll
     for (u32 r = 0; r < kTI; ++r) {
@@ -177,16 +184,12 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
       const u64 inc = wave_incl_scan_u64(v);
       pre_r[r] = (u32)(carry + inc - v);
       carry += __shfl(inc, 63, 64);
-      rb += fl[r] == kFlJunk ? 0ull : 16ull * record_rs16(lenv[r]);
     }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      rb += __shfl_xor(rb, d, 64);
-      inv_cnt += __shfl_xor(inv_cnt, d, 64);
-    }
+    for (int d = 32; d >= 1; d >>= 1) inv_cnt += __shfl_xor(inv_cnt, d, 64);
     if (lane == 0) {
       S.wsum[w][0] = carry;
-      S.wsum[w][1] = rb | (inv_cnt << 48);
+      S.wsum[w][1] = inv_cnt;
     }
     __syncthreads();
     u64 wpre = 0;
@@ -198,14 +201,13 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
       if (q < nin) x.pre[gbase + q] = (u32)wpre + pre_r[r];
     }
     if (tid == 0) {
-      u64 ps = 0, rs = 0, ic = 0;
+      u64 ps = 0, ic = 0;
       for (u32 ww = 0; ww < kPW; ++ww) {
         ps += S.wsum[ww][0];
-        rs += S.wsum[ww][1] & ((1ull << 48) - 1ull);
-        ic += S.wsum[ww][1] >> 48;
+        ic += S.wsum[ww][1];
       }
       x.tsum[(u64)t * 4 + 0] = ps;
-      x.tsum[(u64)t * 4 + 1] = rs;
+      x.tsum[(u64)t * 4 + 1] = 0;
       x.tsum[(u64)t * 4 + 2] = ic;
       x.tsum[(u64)t * 4 + 3] = 0;
     }
@@ -319,7 +321,7 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
       x.crank[gbase + q] = make_uint2((u32)(ex >> 40) | (f << kFlagShift), (u32)(ex & kLow40));
     }
     const u32 nkey = s + 1 < kTR ? (sorted[s + 1] >> kIB) : 0xFFFFFFFFu;
-    if (nkey != key && (v >> 40)) x.hist[(u64)t * P + key] = v;
+    if (nkey != key && (v >> 40)) x.hist[(u64)key * A.gt + t] = v;
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(3);
@@ -331,25 +333,22 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
 __device__ void stage2(const PipeArgs& A, u32 wg) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
-  const u32 P = A.st.P, T = G.tiles;
+  const u32 P = A.st.P, T = G.tiles, GT = A.gt;
   const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  __shared__ u64 s_acc[kMaxGroup][3];
+  __shared__ u64 s_acc[kMaxGroup][2];
   __shared__ u64 s_ex[kMaxTiles];
   __shared__ u64 s_w[kPW];
-  __shared__ u32 s_tinfo[kMaxTiles];  // per tile: batch | last tile of its batch << 8
   __shared__ u32 s_rej;
   PIPE_STAMP(0);
-  // ---- batch rules from the tile sums: every workgroup, since the scans skip rejected batches
-  if (tid < kMaxGroup * 3) (&s_acc[0][0])[tid] = 0ull;
+  // ---- batch rule from the tile sums (every workgroup, since the scans skip invalid batches)
+  if (tid < kMaxGroup * 2) (&s_acc[0][0])[tid] = 0ull;
   __syncthreads();
   const bool in = tid < T;
   const u32 jt = in ? batch_of_tile(G, tid) : 0u;
   const u64 pay = in ? x.tsum[(u64)tid * 4 + 0] : 0ull;
   if (in) {
-    s_tinfo[tid] = jt | (tid + 1u == batch_end_tile(G, tid) ? 0x100u : 0u);
     atomicAdd(&s_acc[jt][0], pay);
-    atomicAdd(&s_acc[jt][1], x.tsum[(u64)tid * 4 + 1]);
-    atomicAdd(&s_acc[jt][2], x.tsum[(u64)tid * 4 + 2]);
+    atomicAdd(&s_acc[jt][1], x.tsum[(u64)tid * 4 + 2]);
   }
   if (wg == 0) {  // payload offset of every tile's first record inside its batch (packed payloads)
     const u64 inc = wave_incl_scan_u64(pay);
@@ -365,14 +364,12 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
   if (tid == 0) {
     u32 rm = 0;
     for (u32 j = 0; j < G.nb; ++j) {
-      const u64 ptot = s_acc[j][0], rtot = s_acc[j][1], itot = s_acc[j][2];
-      u32 rej = 0;
-      if (itot || (!G.b[j].poff && ptot > G.b[j].payload_bytes)) rej |= kRejInvalid;
-      if (rtot > A.nospace_limit) rej |= kRejNoSpace;
+      const u64 ptot = s_acc[j][0], itot = s_acc[j][1];
+      const u32 rej = (itot || (!G.b[j].poff && ptot > G.b[j].payload_bytes)) ? kRejInvalid : 0u;
       rm |= (rej ? 1u : 0u) << j;
       if (wg == 0) {
         x.binfo[j * 4 + 0] = rej;
-        x.binfo[j * 4 + 1] = rtot;
+        x.binfo[j * 4 + 1] = 0;
         x.binfo[j * 4 + 2] = ptot;
         x.binfo[j * 4 + 3] = 0;
       }
@@ -382,46 +379,59 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
   __syncthreads();
   const u32 rm = s_rej;
 
-  // ---- column scans: kScanLanes consecutive threads share a partition column; per block of
-  // 8 * kScanLanes tiles, thread s holds tiles [8s, 8s + 8) of the block in registers
+  // ---- column scans: kScanLanes consecutive threads share a partition column (contiguous in
+  // hist / excl); per batch, blocks of 8 * kScanLanes tiles, thread s holding tiles [8s, 8s + 8)
   const u32 s = tid % kScanLanes;
+  const u64 lim16 = A.nospace_limit >> 4;  // record bytes / 16 a (batch, partition) may add
   for (u32 g = wg * kPT + tid; g < P * kScanLanes; g += A.wg2 * kPT) {  // whole columns per group
     const u32 p = g / kScanLanes;
+    u64* const col = x.hist + (u64)p * GT;
+    u64* const ecol = x.excl + (u64)p * GT;
     u64 carry = 0;
-    for (u32 B = 0; B < T; B += 8u * kScanLanes) {
-      const u32 ta = B + 8u * s;
-      u64 h[8];  // tiles of rejected batches read as absent (their entries are cleared below)
+    for (u32 j = 0; j < G.nb; ++j) {
+      const u32 t0 = G.tile0[j], t1 = G.tile0[j + 1];
+      const bool binv = (rm >> j) & 1u;  // invalid batch: its cells are cleared and count nothing
+      u64 bsum = 0;
+      for (u32 B = t0; B < t1; B += 8u * kScanLanes) {
+        const u32 ta = B + 8u * s;
+        u64 h[8];
 #pragma unroll
-      for (u32 k = 0; k < 8; ++k) {
-        const u32 tk = ta + k;
-        h[k] = (tk < T && !((rm >> (s_tinfo[tk] & 0xFFu)) & 1u)) ? x.hist[(u64)tk * P + p] : 0ull;
-      }
-      u64 loc = 0;
+        for (u32 k = 0; k < 8; ++k) h[k] = ta + k < t1 ? col[ta + k] : 0ull;
+        u64 loc = 0;
 #pragma unroll
-      for (u32 k = 0; k < 8; ++k) loc += h[k];
-      u64 inc = loc;
+        for (u32 k = 0; k < 8; ++k) loc += h[k];
+        if (binv) loc = 0;
+        u64 inc = loc;
 #pragma unroll
-      for (u32 d = 1; d < kScanLanes; d <<= 1) {
-        const u64 o = __shfl_up(inc, d, kScanLanes);
-        if (s >= d) inc += o;
-      }
-      u64 run = carry + inc - loc;
-      carry += __shfl(inc, kScanLanes - 1, kScanLanes);
-#pragma unroll
-      for (u32 k = 0; k < 8; ++k) {
-        const u32 tk = ta + k;
-        if (h[k]) {
-          x.excl[(u64)tk * P + p] = run;
-          x.hist[(u64)tk * P + p] = 0ull;  // clear for the set's next group
+        for (u32 d = 1; d < kScanLanes; d <<= 1) {
+          const u64 o = __shfl_up(inc, d, kScanLanes);
+          if (s >= d) inc += o;
         }
-        run += h[k];
-        if (tk < T && (s_tinfo[tk] & 0x100u))  // last tile of its batch
-          x.bcum[(u64)(s_tinfo[tk] & 0xFFu) * P + p] = run;
+        u64 run = carry + bsum + inc - loc;
+#pragma unroll
+        for (u32 k = 0; k < 8; ++k) {
+          if (h[k]) {
+            if (!binv) ecol[ta + k] = run;
+            col[ta + k] = 0ull;  // clear for the set's next group
+          }
+          if (!binv) run += h[k];
+        }
+        bsum += __shfl(inc, kScanLanes - 1, kScanLanes);
       }
+      if (!binv) {
+        if ((bsum & kLow40) > lim16) {
+          // FORMAT.md §3: partition p takes no record of batch j. The same threads that wrote the
+          // cells flag them (program order), absent cells included (stage 3 never reads those).
+          for (u32 B = t0; B < t1; B += 8u * kScanLanes)
+#pragma unroll
+            for (u32 k = 0; k < 8; ++k)
+              if (B + 8u * s + k < t1) ecol[B + 8u * s + k] = kExclNoSpace;
+        } else {
+          carry += bsum;
+        }
+      }
+      if (s == 0) x.bcum[(u64)j * P + p] = carry;
     }
-    if (rm)  // rejected batches (rare): clear their tiles' entries of this column
-      for (u32 tk = s; tk < T; tk += kScanLanes)
-        if ((rm >> (s_tinfo[tk] & 0xFFu)) & 1u) x.hist[(u64)tk * P + p] = 0ull;
     if (s == 0) x.totals[p] = carry;
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -491,6 +501,7 @@ __device__ __forceinline__ u32 task_rec(const TaskPos& T) { return T.i0 + ((thre
 
 struct TaskState {  // round 2: partition state of the record and its first round of payload blocks
   u64 ex, leo, used;
+  u64 gend;        // the partition's log end position after the whole group
   u32 lm, lead;
   uint4 blk[kBL];
 };
@@ -539,15 +550,17 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   const PipeGroup& G = A.g3;
   const DevState& st = A.st;
   TaskState S;
-  S.ex = S.leo = S.used = 0ull;
+  S.ex = S.leo = S.used = S.gend = 0ull;
   S.lm = S.lead = 0u;
   if (cand) {
     const u32 p = R.p;
     const u32 t = G.tile0[T.jb] + task_rec(T) / kTR;
     S.lead = st.is_leader[p];
-    S.ex = A.s3.excl[(u64)t * st.P + p];
+    S.ex = A.s3.excl[(u64)p * A.gt + t];
+    const u64 tot = A.s3.totals[p];
     S.leo = A.cur.leo[p];
     S.used = A.cur.used[p];
+    S.gend = S.used + 16ull * (tot & kLow40);
     S.lm = st.local_mask[p];
   }
   // first round of payload blocks, speculatively (leadership is checked before any store)
@@ -573,12 +586,16 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   const u32 p = R.p, L = R.L;
   const u32 fl = R.cr.x >> kFlagShift;
   const u32 rej = batch_rej(A, T);
-  const bool ok = cand && Z.lead != 0u;
+  const bool ns = (Z.ex & kExclNoSpace) != 0ull;  // the record's (batch, partition) is over its limit
+  const bool ok = cand && Z.lead != 0u && !ns;
   const u32 m = (L + 15u) >> 4;  // payload pieces
   const u64 segmask = st.seg - 1ull;
   const u64 rstride = (u64)P * st.seg;
-  const u64 off = Z.leo + (Z.ex >> 40) + (R.cr.x & kRankMask);
+  const u64 off = Z.leo + ((Z.ex >> 40) & kCnt23) + (R.cr.x & kRankMask);
   const u64 pos = Z.used + 16ull * ((Z.ex & kLow40) + R.cr.y);
+  // pieces (0 = header, k = payload piece k - 1 at pos + 16k) whose ring slot a later piece of the
+  // same group overwrites (pos + 16k + seg < group end) are dead: not stored
+  const u32 dead = Z.gend > pos + st.seg ? (u32)min((Z.gend - st.seg - pos) >> 4, (u64)m + 1ull) : 0u;
   uint8_t* const ring = st.logs + (u64)p * st.seg;
   const u32 lmw = (A.debug & 1u) ? 0u : Z.lm;
   const u32 sa = (u32)(R.src & 15u);
@@ -608,8 +625,9 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
           const_cast<Stage3Smem&>(S).img[w][r32][jp + 1] = v;
         } else {
           uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
-          for (u32 r = 0; r < RF; ++r)
-            if ((lmw >> r) & 1u) store_log16(dst + r * rstride, v);
+          if (jp + 1u >= dead)
+            for (u32 r = 0; r < RF; ++r)
+              if ((lmw >> r) & 1u) store_log16(dst + r * rstride, v);
         }
       }
     }
@@ -631,14 +649,15 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   if (img) {
     Stage3Smem& W = const_cast<Stage3Smem&>(S);
     if (j == 1) W.img[w][r32][0] = h;
-    if (j == 0) W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), p, Z.lm | (m << 8) | ((ok ? 1u : 0u) << 16));
+    if (j == 0)
+      W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), p, Z.lm | (m << 8) | ((ok ? 1u : 0u) << 16) | (dead << 24));
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (u32 s4 = 0; s4 < kTaskRecs * 8u / 64u; ++s4) {
       const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
       const uint4 inf = W.info[w][rr];
       const u32 mr = (inf.w >> 8) & 0xFFu;
-      if (((inf.w >> 16) & 1u) && k <= mr) {
+      if (((inf.w >> 16) & 1u) && k <= mr && k >= (inf.w >> 24)) {
         const uint4 v = W.img[w][rr][k];
         const u64 rpos = ((u64)inf.y << 32) | inf.x;
         uint8_t* dst = st.logs + (u64)inf.z * st.seg + ((rpos + 16ull * k) & segmask);
@@ -648,7 +667,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
       }
     }
     __builtin_amdgcn_wave_barrier();  // the image is rewritten by the wave's next task
-  } else if (ok && j == 1) {
+  } else if (ok && j == 1 && dead == 0u) {
     uint8_t* dst = ring + (pos & segmask);
     for (u32 r = 0; r < RF; ++r)
       if ((Z.lm >> r) & 1u) store_log16(dst + r * rstride, h);
@@ -670,7 +689,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     const u32 n_nl = (u32)__popcll(__ballot(h0 && cand && !Z.lead));
     const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h0 && in && fl == kFlNoPart));
     const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
-    const u32 n_ns = (rej & kRejInvalid) ? 0u : (rej & kRejNoSpace) ? n_in : 0u;
+    const u32 n_ns = (u32)__popcll(__ballot(h0 && cand && Z.lead && ns));
     stat_out = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
   }
 }
@@ -680,9 +699,11 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
 // it once after the group equals evaluating it after each batch.
 __device__ void partition_apply(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
-  // a follower's records are counted by stages 1/2 (ranks are per partition) but never applied;
-  // stage 2 leaves rejected batches out of totals
-  const u64 tot = st.is_leader[p] ? A.s3.totals[p] : 0ull;
+  // a partition this engine does not lead keeps its state outside the pipeline (its records are
+  // counted by stages 1/2, ranks being per partition, but never applied; the host keeps both state
+  // sets equal for it); stage 2 leaves rejected (batch, partition) cells out of totals
+  if (!st.is_leader[p]) return;
+  const u64 tot = A.s3.totals[p];
   const u64 tc = tot >> 40, tb = 16ull * (tot & kLow40);
   const u64 nleo = A.cur.leo[p] + tc;
   A.nxt.leo[p] = nleo;

@@ -142,6 +142,13 @@ class Engine:
         stats = self.wait(t)
         return out, stats
 
+    def commit_snapshot(self) -> np.ndarray:
+        """Commit index of every partition after everything submitted so far."""
+        P = self.cfg.num_partitions
+        commit = np.empty(P, np.uint64)
+        _check(self.lib.rmq_poll_commit(self.h, 0, _ptr(commit), None), "rmq_poll_commit")
+        return commit
+
     def sync(self) -> None:
         _check(self.lib.rmq_sync(self.h), "rmq_sync")
 
@@ -179,6 +186,18 @@ class Engine:
         if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
             raise EngineError(rc, "rmq_fetch")
         return rc, res, out[:out_cap], int(used.value)
+
+    def fetch_device(self, pidx, consumer, max_records, d_out: int, out_cap: int):
+        """rmq_fetch into a device buffer (16-byte aligned); returns (rc, res, bytes_used)."""
+        n = len(pidx)
+        req = np.zeros((n, 4), np.uint32)
+        req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
+        res = np.zeros(n, FETCH_RES_DTYPE)
+        used = C.c_uint64()
+        rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_DEVICE, d_out, out_cap, _ptr(res), C.byref(used))
+        if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
+            raise EngineError(rc, "rmq_fetch")
+        return rc, res, int(used.value)
 
     # ---- read-back
     def state(self, pidx: int) -> dict:

@@ -37,6 +37,7 @@ from . import _abi as A
 from .engine import Engine, EngineConfig, EngineError, parse_records
 
 NOT_LEADER = "Not leader"
+COMMIT_PENDING = "Commit pending"
 
 
 # ---- request / response records (mq-common/src/main/java/request/partition/)
@@ -188,9 +189,14 @@ class PartitionBroker:
     def process_append(self, requests: list[MessageAppendRequest]) -> list[MessageAppendResponse]:
         """Apply every request's messages in request order as ONE engine batch.
 
-        A request succeeds when all of its messages got offsets and are committed; a request for
-        a partition this broker does not lead answers "Not leader"; an unknown groupId answers
-        "Unknown partition" (the reference dereferences null there)."""
+        As in the reference, a request succeeds only once its entries are committed and applied
+        (the PartitionClosure runs after BallotBox commit, MessageAppendRequestProcessor.java:39-48):
+        a request whose records all got offsets below the partition's commit index answers success;
+        one whose records are appended but not yet committed (followers on other ranks have not
+        acknowledged) answers "Commit pending". A request for a partition this broker does not
+        lead answers "Not leader"; one whose partition had no room for this batch (FORMAT.md §3)
+        answers RMQ_ENOSPC; an unknown groupId answers "Unknown partition" (the reference
+        dereferences null there)."""
         pidx, msgs, owner = [], [], []
         out = [MessageAppendResponse() for _ in requests]
         for r, req in enumerate(requests):
@@ -209,24 +215,28 @@ class PartitionBroker:
             return out
         lens = np.fromiter((len(m) for m in msgs), np.uint32, len(msgs))
         payload = np.frombuffer(b"".join(msgs), np.uint8) if lens.sum() else np.zeros(0, np.uint8)
+        pidx = np.asarray(pidx, np.uint32)
         try:
-            offs, stats = self.engine.append(np.asarray(pidx, np.uint32), lens, payload)
-        except EngineError as e:  # whole-batch rejections: no space, invalid ranges
+            offs, _ = self.engine.append(pidx, lens, payload)
+        except EngineError as e:  # whole-batch rejections (invalid payload ranges)
             for r in set(owner):
                 out[r].errorMsg = A.STATUS_NAMES.get(e.status, str(e.status))
             return out
-        if stats.get("rejected_no_space"):  # FORMAT.md §3: the whole batch is refused
-            for r in set(owner):
-                out[r].errorMsg = A.STATUS_NAMES[A.RMQ_ENOSPC]
-            return out
         owner = np.asarray(owner)
         rejected = offs == np.uint64(A.RMQ_OFFSET_NONE)
-        bad = set(owner[rejected].tolist())
+        commit = self.engine.commit_snapshot()
+        pending = ~rejected & (offs >= commit[pidx])
+        leads = {p: bool(self.engine.state(p)["is_leader"]) for p in set(pidx[rejected].tolist())}
+        bad, wait = {}, set(owner[pending].tolist())
+        for k in np.flatnonzero(rejected).tolist():
+            bad.setdefault(int(owner[k]), NOT_LEADER if not leads[int(pidx[k])] else A.STATUS_NAMES[A.RMQ_ENOSPC])
         for r in range(len(requests)):
             if out[r].errorMsg is not None:
                 continue
             if r in bad:
-                out[r].errorMsg = NOT_LEADER
+                out[r].errorMsg = bad[r]
+            elif r in wait:
+                out[r].errorMsg = COMMIT_PENDING
             else:
                 out[r].success = True
         return out

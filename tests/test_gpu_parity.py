@@ -50,8 +50,8 @@ def test_retention_wraps_ring(oracle_mod):
 
 
 def test_large_records_direct_path(oracle_mod):
-    # log-uniform 64 B..16 KB (config D sizes): tiles overflow the LDS image -> direct path,
-    # long payloads -> whole-wave CRC with GF(2) shift-combine
+    # log-uniform 64 B..16 KB (config D sizes): records longer than 112 B skip the LDS log image
+    # and are stored piece by piece; long payloads take many Horner rounds per lane
     cfg, dev, ora = pair(oracle_mod, num_partitions=16, replication_factor=5, segment_bytes=1 << 23,
                          index_interval=1024, max_batch_records=4096, max_batch_bytes=32 << 20)
     with dev, ora:
@@ -167,7 +167,8 @@ def test_pipelined_groups(oracle_mod, group):
                          index_interval=256, max_batch_records=4096, pipeline_depth=group)
     with dev, ora:
         spec = StreamSpec(64, 1400, "zipf", size=(0, 120), config_index=22, invalid_frac=0.01)
-        big = make_batch(StreamSpec(64, 1100, "uniform", size=100, config_index=23), 0)  # > ring - I
+        big = make_batch(StreamSpec(64, 1100, "uniform", size=100, config_index=23), 0)
+        big.pidx[:1050] = 7  # 1050 x 128 B > ring - I: partition 7 takes none of this batch's records
         for e in (dev, ora):
             e.set_replicas(5, [1, 0, 2], 0)
         batches = [make_batch(spec, b) for b in range(11)]
@@ -214,8 +215,7 @@ def test_config_B_full_batches(oracle_mod):
         ops = [("append", make_batch(spec, b)) for b in range(3)]
         log = run_ops(dev, ora, cfg, ops, check=False)
         assert all(st["appended"] == 65536 for _, st in log), log
-        hot = np.argsort([-ora.state(p)["log_end_offset"] for p in range(4096)])
-        compare_state(dev, ora, cfg, parts=list(hot[:64]) + list(range(0, 4096, 97)))
+        compare_state(dev, ora, cfg)  # all 4096 partitions: state, every replica's ring window, index
 
 
 def test_config_A_full_batches(oracle_mod):
@@ -230,7 +230,7 @@ def test_config_A_full_batches(oracle_mod):
 
 @pytest.mark.parametrize("P", [4097, 20000])
 def test_multi_pass_sort(oracle_mod, P):
-    # P > 4096: two 12-bit radix passes before the slot records
+    # P > 256: two 8-bit radix passes over the partition keys
     cfg, dev, ora = pair(oracle_mod, num_partitions=P, replication_factor=2, segment_bytes=1 << 18,
                          index_interval=1024, max_batch_records=8192)
     with dev, ora:

@@ -13,7 +13,8 @@ def test_sharded_equals_sequential(oracle_mod, threads, mode, P):
     cfg = EngineConfig(num_partitions=P, replication_factor=3, segment_bytes=1 << 17, index_interval=I,
                        max_batch_records=4096)
     spec = StreamSpec(P, 1000, mode, size=(0, 150), config_index=21, invalid_frac=0.01)
-    big = make_batch(StreamSpec(P, 2500, "uniform", size=100, config_index=24), 0)  # > ring - I
+    big = make_batch(StreamSpec(P, 2500, "uniform", size=100, config_index=24), 0)
+    big.pidx[::2] = 0  # 1250 x 128 B for partition 0 > ring - I: partition 0 takes none of them
     batches = [make_batch(spec, b) for b in range(12)]
     batches.insert(3, big)
     with oracle_mod.OracleEngine(cfg) as seq, oracle_mod.OracleEngine(cfg) as par:
@@ -21,7 +22,8 @@ def test_sharded_equals_sequential(oracle_mod, threads, mode, P):
             e.set_replicas(1 % P, [1, 0, 2], 0)  # a partition this rank does not lead
         exp = [seq.append(b.pidx, b.lens, b.payload) for b in batches]
         got = par.append_sharded(batches, threads)
-        assert exp[3][1]["rejected_no_space"] == len(big.pidx)
+        assert exp[3][1]["rejected_no_space"] == int(np.sum(big.pidx == 0))
+        assert exp[3][1]["appended"] == len(big.pidx) - int(np.sum(big.pidx == 0)) - int(np.sum(big.pidx == 1 % P))
         for (oe, se), (og, sg) in zip(exp, got):
             assert se == sg
             assert np.array_equal(oe, og)
