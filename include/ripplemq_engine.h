@@ -26,6 +26,13 @@
  *                                  (mq-broker/src/main/java/metadata/raft/PartitionRaftServer.java:82-86)
  *   rmq_create / rmq_destroy    <- PartitionManager.startPartition / PartitionRaftServer.shutdown
  *                                  (PartitionManager.java:166-176, PartitionRaftServer.java:100-108)
+ *   rmq_set_placement           <- PartitionManager.handleTopicListChange starting the groups this broker
+ *                                  hosts with their peers (PartitionManager.java:111-176), as placed by
+ *                                  PartitionAssigner.assignPartitions (PartitionAssigner.java:25-94)
+ *   rmq_attach_rccl /           <- the shared RpcServer/BoltRpcClient pair jraft replicates over
+ *   rmq_attach_local               (PartitionRaftServer.java:93): AppendEntries to the followers and
+ *                                  their acks, here grouped RCCL send/recv of replica-log rounds
+ *                                  (FORMAT.md §9) between the engines of one node
  *
  * Only dense partition indices (pidx) cross this boundary; the Java side keeps the
  * "topic-partitionId" -> pidx map (PartitionManager.java:121,196-198).
@@ -34,6 +41,14 @@
  * rmq_commit_consumer_offset / rmq_become_leader / rmq_set_replicas. rmq_fetch, rmq_poll_commit
  * and the read-back calls may be called from any thread (they serialize on an internal lock).
  * Completion is by polling tickets; the library never calls back into the host.
+ *
+ * Replication transport (multi-GPU): after rmq_attach_rccl / rmq_attach_local the
+ * engines of the world replicate every launch group of appends to the followers named by the
+ * placement and commit on quorum. Rounds are collective, like the launches that drive them: every
+ * rank must make the same sequence of rmq_append calls (empty batches count) and of the calls that
+ * flush the pipeline (rmq_sync, rmq_set_placement, rmq_set_replicas, rmq_become_leader, rmq_ack);
+ * rmq_poll_commit / rmq_ticket_stats never flush then (they answer RMQ_PENDING until an rmq_sync on
+ * every rank applied the ticket), and rmq_sync before rmq_destroy.
  *
  * Log byte format, offset index and retention are defined in FORMAT.md.
  */
@@ -137,7 +152,21 @@ typedef struct rmq_append_stats {
                                   outside payload_bytes (host batches get RMQ_EINVAL instead) */
 } rmq_append_stats;
 
+typedef struct rmq_repl_stats {
+  uint32_t world, rank;
+  uint32_t out_entries;        /* (led partition, remote slot) pairs this engine sends rounds for */
+  uint32_t in_entries;         /* (followed partition, local slot) pairs it receives rounds for */
+  uint64_t rounds;             /* replication rounds posted (one per launch group) */
+  uint64_t bytes_sent;         /* round regions sent (FORMAT.md §9), all peers */
+  uint64_t bytes_received;
+  uint64_t records_ingested;   /* follower records whose CRC32C and log position checked out */
+  uint64_t refused_crc;        /* follower entries refused: CRC32C differs from the record header */
+  uint64_t refused_log;        /* follower entries refused: do not continue the follower's log */
+  uint64_t bytes_ingested;
+} rmq_repl_stats;
+
 typedef struct rmq_engine rmq_engine;
+typedef struct rmq_local_hub rmq_local_hub;
 
 uint32_t rmq_abi_version(void);
 const char* rmq_strerror(int status);
@@ -152,6 +181,14 @@ void rmq_destroy(rmq_engine* e);
    The engine leads pidx iff replica_ranks[leader_slot] == cfg.rank. rf must equal cfg RF. */
 int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* replica_ranks, uint32_t rf,
                      uint32_t leader_slot);
+/* Placement of n partitions at once (one drain): for partition pidx[i], replica_ranks[i * RF + slot]
+   and leader_slot[i] as in rmq_set_replicas, and key[i] (nullable: keys unchanged, default pidx) a
+   cluster-wide id of the partition (its groupId) that orders replication lists identically on
+   every rank (FORMAT.md §9). With a transport attached this is collective and checks every pair of
+   ranks agrees on what they replicate to each other (RMQ_EINVAL on every rank if not). */
+int rmq_set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* key,
+                      const uint32_t* replica_ranks, const uint32_t* leader_slot);
+
 /* New leader term for pidx (or RMQ_ALL_PARTITIONS): term_start = log_end_offset, so only
    entries appended in this term can advance the commit (Raft current-term rule). */
 int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
@@ -195,6 +232,21 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
    fit in out_cap (those get count 0, status RMQ_ENOSPC). */
 int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
               uint64_t out_cap, rmq_fetch_res* res, uint64_t* bytes_used);
+
+/* ---- replication transport (FORMAT.md §9) ---- */
+/* 128-byte communicator id: one rank creates it, the application hands it to every rank. */
+int rmq_rccl_unique_id(uint8_t* out /* 128 bytes */);
+/* RCCL over xGMI between the world's engines, one per GPU and process; rank = cfg.rank. Collective. */
+int rmq_attach_rccl(rmq_engine* e, const uint8_t* comm_id, uint32_t world);
+/* In-process transport: engines of one process exchange by device copies; each rank's engine must
+   be driven by its own host thread (the hub's barriers stand in for the collective). */
+int rmq_local_hub_create(uint32_t world, rmq_local_hub** out);
+void rmq_local_hub_destroy(rmq_local_hub* hub);
+int rmq_attach_local(rmq_engine* e, rmq_local_hub* hub);
+int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out);
+/* Region bytes of the last posted round for destination rank dst (FORMAT.md §9): *size gets its
+   length; copied to out if out != NULL and cap suffices (tests, tools). */
+int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size);
 
 /* ---- read-back (tests, tools) ---- */
 int rmq_get_partition_state(rmq_engine* e, uint32_t pidx, rmq_partition_state* out);

@@ -52,6 +52,14 @@ def load() -> C.CDLL:
         "ro_record_pos": (C.c_int, [vp, u32, u64, C.POINTER(u64)]),
         "ro_append_sharded": (C.c_int, [vp, u32, vp, vp, vp, u32, C.c_int, C.POINTER(u32)]),
         "ro_reserve": (C.c_int, [vp, vp]),
+        "ro_set_world": (C.c_int, [vp, u32]),
+        "ro_set_key": (C.c_int, [vp, u32, u64]),
+        "ro_round_region": (C.c_int, [vp, u32, vp, u64, C.POINTER(u64)]),
+        "ro_end_round": (None, [vp]),
+        "ro_ingest": (C.c_int, [vp, u32, vp, u64, vp]),
+        "ro_apply_acks": (C.c_int, [vp, u32, vp, u32]),
+        "ro_pair_entries": (u32, [vp, u32, u32]),
+        "ro_counters": (None, [vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -99,6 +107,52 @@ class OracleEngine:
         rc = self.lib.ro_set_replicas(self.h, pidx, r, len(ranks), leader_slot)
         if rc:
             raise EngineError(rc, "oracle")
+
+    def set_placement(self, pidx, keys, ranks, leader_slot):
+        ranks = np.asarray(ranks).reshape(len(pidx), self.cfg.replication_factor)
+        for i, p in enumerate(pidx):
+            self.set_replicas(int(p), [int(x) for x in ranks[i]], int(leader_slot[i]))
+            if keys is not None:
+                self.lib.ro_set_key(self.h, int(p), int(keys[i]))
+
+    # ---- replication rounds (FORMAT.md §9)
+    def set_world(self, world):
+        if self.lib.ro_set_world(self.h, world):
+            raise EngineError(A.RMQ_EINVAL, "oracle")
+
+    def round_region(self, dst) -> np.ndarray:
+        n = C.c_uint64()
+        self.lib.ro_round_region(self.h, dst, None, 0, C.byref(n))
+        out = np.zeros(max(int(n.value), 1), np.uint8)
+        rc = self.lib.ro_round_region(self.h, dst, _p(out), out.size, C.byref(n))
+        if rc:
+            raise EngineError(rc, "oracle")
+        return out[:int(n.value)]
+
+    def end_round(self):
+        self.lib.ro_end_round(self.h)
+
+    def pair_entries(self, src, dst) -> int:
+        return int(self.lib.ro_pair_entries(self.h, src, dst))
+
+    def ingest(self, src, region) -> np.ndarray:
+        region = np.ascontiguousarray(region, np.uint8)
+        acks = np.zeros(max(self.pair_entries(src, self.cfg.rank), 1), np.uint64)
+        rc = self.lib.ro_ingest(self.h, src, _p(region) if region.size else None, region.size, _p(acks))
+        if rc:
+            raise EngineError(rc, "oracle ingest")
+        return acks[:self.pair_entries(src, self.cfg.rank)]
+
+    def apply_acks(self, dst, acks):
+        acks = np.ascontiguousarray(acks, np.uint64)
+        rc = self.lib.ro_apply_acks(self.h, dst, _p(acks) if acks.size else None, len(acks))
+        if rc:
+            raise EngineError(rc, "oracle apply_acks")
+
+    def counters(self) -> np.ndarray:
+        out = np.zeros(4, np.uint64)
+        self.lib.ro_counters(self.h, _p(out))
+        return out
 
     def become_leader(self, pidx, term):
         rc = self.lib.ro_become_leader(self.h, pidx, term)

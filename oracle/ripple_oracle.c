@@ -112,6 +112,9 @@ typedef struct {
   u64vec idx_off, idx_pos; /* sparse index entries E[m], m = 0.. (unbounded, logical) */
   u64vec rec_pos;          /* dense logical position of every record (oracle-only lookup) */
   uint64_t* cons;          /* consumer offsets (reference: HashMap<String,Long>, default 0) */
+  uint64_t key;            /* placement key (FORMAT.md §9 list order), default pidx */
+  uint8_t* round;          /* records appended in the current replication round, log layout */
+  uint64_t round_bytes, round_cap, round_count, round_first;
 } ro_part;
 
 struct ro_engine {
@@ -121,6 +124,8 @@ struct ro_engine {
   uint8_t* touched;
   uint64_t* pbytes; /* [P] record bytes of the current batch per partition */
   uint8_t* full;    /* [P] 1: the partition takes no record of the current batch (FORMAT.md §3) */
+  uint32_t world;   /* replication ranks (1: none; FORMAT.md §9 rounds when > 1) */
+  uint64_t counters[4]; /* follower: records ingested, refused (CRC), refused (log), bytes */
 };
 
 static int cfg_ok(const rmq_config* c) {
@@ -139,6 +144,7 @@ ro_engine* ro_create(const rmq_config* cfg) {
   ro_engine* e = (ro_engine*)calloc(1, sizeof(ro_engine));
   if (!e) return NULL;
   e->cfg = *cfg;
+  e->world = 1;
   uint32_t P = cfg->num_partitions, RF = cfg->replication_factor;
   e->parts = (ro_part*)calloc(P, sizeof(ro_part));
   e->touched = (uint8_t*)calloc(P, 1);
@@ -156,6 +162,7 @@ ro_engine* ro_create(const rmq_config* cfg) {
     s->is_leader = 1; /* this engine leads every partition it hosts, term 1 */
     s->term = 1;
     s->term_start = 0;
+    s->key = p;
     s->cons = (uint64_t*)calloc(cfg->max_consumers, sizeof(uint64_t));
     if (!s->cons || vec_push(&s->idx_off, 0) || vec_push(&s->idx_pos, 0)) { /* E[0] = (0, 0) */
       ro_destroy(e);
@@ -181,6 +188,7 @@ void ro_destroy(ro_engine* e) {
       free(e->parts[p].idx_pos.v);
       free(e->parts[p].rec_pos.v);
       free(e->parts[p].cons);
+      free(e->parts[p].round);
     }
   if (e->rings)
     for (size_t k = 0; k < (size_t)P * RF; ++k) free(e->rings[k]);
@@ -354,6 +362,20 @@ static int append_record(ro_engine* e, ro_part* s, uint32_t p, const uint8_t* sr
   for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
     if (vec_push(&s->idx_off, o + 1) || vec_push(&s->idx_pos, pos + rs)) return RMQ_ENOMEM;
   if (vec_push(&s->rec_pos, pos)) return RMQ_ENOMEM;
+  if (e->world > 1) { /* kept for the replication round (the ring may wrap inside a round) */
+    if (s->round_bytes + rs > s->round_cap) {
+      uint64_t nc = s->round_cap ? s->round_cap * 2 : 4096;
+      while (nc < s->round_bytes + rs) nc *= 2;
+      uint8_t* nr = (uint8_t*)realloc(s->round, nc);
+      if (!nr) return RMQ_ENOMEM;
+      s->round = nr;
+      s->round_cap = nc;
+    }
+    memcpy(s->round + s->round_bytes, r8, rs);
+    if (!s->round_count) s->round_first = o;
+    s->round_bytes += rs;
+    s->round_count++;
+  }
   s->leo = o + 1;
   s->used = pos + rs;
   *out_offset = o;
@@ -733,3 +755,237 @@ int ro_record_pos(ro_engine* e, uint32_t p, uint64_t offset, uint64_t* pos) {
   *pos = offset == s->leo ? s->used : s->rec_pos.v[offset];
   return RMQ_OK;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* Replication rounds (FORMAT.md §9): the leader's region per destination, the follower's      */
+/* ingest, the leader's ack application. Restated from the format, record by record.          */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct {
+  uint64_t key;
+  uint32_t slot, p;
+} ro_entry;
+
+static int entry_cmp(const void* a, const void* b) {
+  const ro_entry *x = (const ro_entry*)a, *y = (const ro_entry*)b;
+  if (x->key != y->key) return x->key < y->key ? -1 : 1;
+  return x->slot < y->slot ? -1 : x->slot > y->slot;
+}
+
+/* Entries exchanged between leader `src` and follower `dst`, ascending (key, slot): the
+   (partition, slot) pairs whose leader is src and whose replica slot lives on dst. */
+static uint32_t pair_entries(const ro_engine* e, uint32_t src, uint32_t dst, ro_entry** out) {
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  ro_entry* v = (ro_entry*)malloc(((size_t)P * RF + 1) * sizeof(ro_entry));
+  uint32_t n = 0;
+  for (uint32_t p = 0; p < P && v; ++p) {
+    const ro_part* s = &e->parts[p];
+    if (s->ranks[s->leader_slot] != src) continue;
+    for (uint32_t r = 0; r < RF; ++r)
+      if (s->ranks[r] == dst && dst != src) v[n++] = (ro_entry){s->key, r, p};
+  }
+  if (v) qsort(v, n, sizeof *v, entry_cmp);
+  *out = v;
+  return v ? n : 0;
+}
+
+int ro_set_world(ro_engine* e, uint32_t world) {
+  if (!e || world == 0 || world <= e->cfg.rank) return RMQ_EINVAL;
+  e->world = world;
+  return RMQ_OK;
+}
+
+int ro_set_key(ro_engine* e, uint32_t p, uint64_t key) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  e->parts[p].key = key;
+  return RMQ_OK;
+}
+
+/* The region this engine (leader) sends to rank dst for the current round; *size = its bytes
+   (0 when the two ranks share no partition). out may be NULL to ask for the size. */
+int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size) {
+  const uint32_t me = e->cfg.rank;
+  ro_entry* v = NULL;
+  const uint32_t n = pair_entries(e, me, dst, &v);
+  if (!v) return RMQ_ENOMEM;
+  uint64_t N = 0, B = 0, keysum = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const ro_part* s = &e->parts[v[k].p];
+    N += s->round_count;
+    B += s->round_bytes;
+    keysum += v[k].key * RMQ_MAX_RF + v[k].slot;
+  }
+  const uint64_t tab = 32 + 32ull * n, data = tab + ((8 * N + 15) & ~15ull);
+  *size = n ? data + B : 0;
+  if (!out || !n) {
+    free(v);
+    return RMQ_OK;
+  }
+  if (*size > cap) {
+    free(v);
+    return RMQ_ENOSPC;
+  }
+  memset(out, 0, data);
+  const uint32_t h[4] = {0x58514D52u, n, (uint32_t)N, me};
+  memcpy(out, h, 16);
+  memcpy(out + 16, &keysum, 8);
+  memcpy(out + 24, &data, 8);
+  uint64_t t = 0, b16 = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const ro_part* s = &e->parts[v[k].p];
+    uint8_t* d = out + 32 + 32ull * k;
+    const uint32_t cnt = (uint32_t)s->round_count, by16 = (uint32_t)(s->round_bytes / 16);
+    const uint64_t first = cnt ? s->round_first : 0;
+    const uint32_t ts = (uint32_t)t, ds = (uint32_t)b16;
+    memcpy(d, &cnt, 4);
+    memcpy(d + 4, &by16, 4);
+    memcpy(d + 8, &first, 8);
+    memcpy(d + 16, &ts, 4);
+    memcpy(d + 20, &ds, 4);
+    uint64_t rel = 0;
+    for (uint64_t r = 0; r < s->round_count; ++r) { /* record table: {entry, record position / 16} */
+      uint32_t len;
+      memcpy(&len, s->round + rel + 8, 4);
+      const uint64_t slot = (uint64_t)k | ((uint64_t)(ds + rel / 16) << 32);
+      memcpy(out + tab + 8 * (t + r), &slot, 8);
+      rel += rec_size(len);
+    }
+    memcpy(out + data + 16 * b16, s->round, s->round_bytes);
+    t += cnt;
+    b16 += by16;
+  }
+  free(v);
+  return RMQ_OK;
+}
+
+/* Closes the round: the leader forgets the records it kept for it. */
+void ro_end_round(ro_engine* e) {
+  for (uint32_t p = 0; p < e->cfg.num_partitions; ++p) e->parts[p].round_bytes = e->parts[p].round_count = 0;
+}
+
+/* Follower: ingest the region leader `src` sent (FORMAT.md §9); acks[k] = this engine's log end of
+   entry k afterwards (0 for a refused entry). */
+int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks) {
+  const uint32_t me = e->cfg.rank;
+  const uint64_t S = e->cfg.segment_bytes, I = e->cfg.index_interval;
+  ro_entry* v = NULL;
+  const uint32_t n = pair_entries(e, src, me, &v);
+  if (!v) return RMQ_ENOMEM;
+  if (!n) {
+    free(v);
+    return size ? RMQ_EINVAL : RMQ_OK;
+  }
+  uint32_t h[4];
+  uint64_t keysum, data, want = 0;
+  memcpy(h, region, 16);
+  memcpy(&keysum, region + 16, 8);
+  memcpy(&data, region + 24, 8);
+  for (uint32_t k = 0; k < n; ++k) want += v[k].key * RMQ_MAX_RF + v[k].slot;
+  if (size < 32 || h[0] != 0x58514D52u || h[1] != n || h[3] != src || keysum != want) {
+    free(v);
+    return RMQ_EINVAL;
+  }
+  const uint64_t tab = 32 + 32ull * n;
+  uint64_t leo = 0, used = 0; /* the partition's log end before this round */
+  for (uint32_t k = 0; k < n; ++k) {
+    ro_part* s = &e->parts[v[k].p];
+    const int owner = k == 0 || v[k - 1].p != v[k].p; /* two local slots: the first keeps the state */
+    if (owner) {
+      leo = s->leo;
+      used = s->used;
+    }
+    const uint8_t* d = region + 32 + 32ull * k;
+    uint32_t cnt, by16, ts, ds;
+    uint64_t first;
+    memcpy(&cnt, d, 4);
+    memcpy(&by16, d + 4, 4);
+    memcpy(&first, d + 8, 8);
+    memcpy(&ts, d + 16, 4);
+    memcpy(&ds, d + 20, 4);
+    if (!cnt) {
+      acks[k] = s->leo;
+      continue;
+    }
+    int ok = first == leo;
+    uint64_t rel = 0;
+    for (uint32_t r = 0; r < cnt && ok; ++r) {
+      uint64_t slot, off;
+      uint32_t len, crc;
+      memcpy(&slot, region + tab + 8ull * (ts + r), 8);
+      const uint8_t* rec = region + data + 16ull * (ds + rel / 16);
+      memcpy(&off, rec, 8);
+      memcpy(&len, rec + 8, 4);
+      memcpy(&crc, rec + 12, 4);
+      ok = (uint32_t)slot == k && (slot >> 32) == ds + rel / 16 && off == first + r &&
+           rel + rec_size(len) <= 16ull * by16 && ro_crc32c(rec + 16, len) == crc;
+      for (uint64_t z = 16 + len; ok && z < rec_size(len); ++z) ok = rec[z] == 0; /* zero padding (§1) */
+      rel += rec_size(len);
+    }
+    if (!ok) {
+      acks[k] = 0;
+      e->counters[first == leo ? 1 : 2]++;
+      continue;
+    }
+    const uint8_t* bytes = region + data + 16ull * ds;
+    ring_write(e, ring_of(e, v[k].slot, v[k].p), used, bytes, 16ull * by16);
+    if (owner) {
+      rel = 0;
+      for (uint32_t r = 0; r < cnt; ++r) {
+        uint32_t len;
+        memcpy(&len, bytes + rel + 8, 4);
+        const uint64_t pos = used + rel, rs = rec_size(len);
+        for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
+          if (vec_push(&s->idx_off, first + r + 1) || vec_push(&s->idx_pos, pos + rs)) {
+            free(v);
+            return RMQ_ENOMEM;
+          }
+        if (vec_push(&s->rec_pos, pos)) {
+          free(v);
+          return RMQ_ENOMEM;
+        }
+        rel += rs;
+      }
+      s->leo = first + cnt;
+      s->used = used + 16ull * by16;
+      if (s->used - s->start_pos > S) { /* retention once per round (FORMAT.md §4 rule) */
+        const uint64_t m = (s->used - S + I - 1) / I;
+        s->start_off = s->idx_off.v[m];
+        s->start_pos = s->idx_pos.v[m];
+      }
+      e->counters[3] += 16ull * by16;
+    }
+    e->counters[0] += cnt;
+    acks[k] = first + cnt;
+  }
+  free(v);
+  return RMQ_OK;
+}
+
+/* Leader: the acks follower `dst` returned for this engine's entries (match = max(match,
+   min(ack, log end))), then the quorum commit rule of every partition they name. */
+int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks) {
+  ro_entry* v = NULL;
+  const uint32_t n = pair_entries(e, e->cfg.rank, dst, &v);
+  if (!v) return RMQ_ENOMEM;
+  if (n != n_acks) {
+    free(v);
+    return RMQ_EINVAL;
+  }
+  for (uint32_t k = 0; k < n; ++k) {
+    ro_part* s = &e->parts[v[k].p];
+    const uint64_t a = acks[k] < s->leo ? acks[k] : s->leo;
+    if (a > s->match[v[k].slot]) s->match[v[k].slot] = a;
+  }
+  for (uint32_t k = 0; k < n; ++k) commit_eval(e, &e->parts[v[k].p]);
+  free(v);
+  return RMQ_OK;
+}
+
+uint32_t ro_pair_entries(ro_engine* e, uint32_t src, uint32_t dst) {
+  ro_entry* v = NULL;
+  const uint32_t n = pair_entries(e, src, dst, &v);
+  free(v);
+  return n;
+}
+
+void ro_counters(ro_engine* e, uint64_t* out) { memcpy(out, e->counters, sizeof e->counters); }

@@ -72,6 +72,17 @@ int ro_read_consumer_offsets(ro_engine* e, uint32_t pidx, uint64_t* out);
 /* Logical position of record `offset` (dense, for cross-checking the sparse index). */
 int ro_record_pos(ro_engine* e, uint32_t pidx, uint64_t offset, uint64_t* pos);
 
+/* Replication rounds (FORMAT.md §9): world > 1 makes the leader keep each round's
+   records; the caller closes a round after the batches the engine groups into one launch group. */
+int ro_set_world(ro_engine* e, uint32_t world);
+int ro_set_key(ro_engine* e, uint32_t pidx, uint64_t key);
+int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size);
+void ro_end_round(ro_engine* e);
+int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks);
+int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks);
+uint32_t ro_pair_entries(ro_engine* e, uint32_t src, uint32_t dst);
+void ro_counters(ro_engine* e, uint64_t* out /* [4] */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -81,6 +81,14 @@ class RmqPartitionState(C.Structure):
     ]
 
 
+class RmqReplStats(C.Structure):
+    _fields_ = [
+        ("world", u32), ("rank", u32), ("out_entries", u32), ("in_entries", u32), ("rounds", u64),
+        ("bytes_sent", u64), ("bytes_received", u64), ("records_ingested", u64), ("refused_crc", u64),
+        ("refused_log", u64), ("bytes_ingested", u64),
+    ]
+
+
 class RmqAppendStats(C.Structure):
     _fields_ = [
         ("records", u32), ("appended", u32), ("rejected_not_leader", u32),
@@ -119,6 +127,14 @@ _SIGS = {
     "rmq_profile_enable": (C.c_int, [vp, C.c_int]),
     "rmq_profile_query": (C.c_int, [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]),
     "rmq_device_info": (C.c_int, [vp, C.c_char_p, u32, C.POINTER(u32)]),
+    "rmq_set_placement": (C.c_int, [vp, u32, vp, vp, vp, vp]),
+    "rmq_rccl_unique_id": (C.c_int, [vp]),
+    "rmq_attach_rccl": (C.c_int, [vp, vp, u32]),
+    "rmq_local_hub_create": (C.c_int, [u32, C.POINTER(vp)]),
+    "rmq_local_hub_destroy": (None, [vp]),
+    "rmq_attach_local": (C.c_int, [vp, vp]),
+    "rmq_replication_stats": (C.c_int, [vp, C.POINTER(RmqReplStats)]),
+    "rmq_read_outbox": (C.c_int, [vp, u32, vp, u64, C.POINTER(u64)]),
 }
 
 _lib = None

@@ -12,6 +12,17 @@ namespace rmq {
 
 typedef uint32_t u32;
 typedef uint64_t u64;
+typedef __attribute__((address_space(1))) u64 gu64;
+typedef __attribute__((address_space(1))) u32 gu32;
+
+// Relaxed agent-scope (`sc1`) global accesses: an L2-coherent hand-off between workgroups of one
+// launch without fences (MI355X_MICROARCH.md, inter-workgroup visibility, first table row).
+__device__ __forceinline__ void store_sc1(u64* p, u64 v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 load_sc1(const u64* p) {
+  return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 constexpr u32 kCrcPoly = 0x82F63B78u;
 constexpr u32 kRecAlign = 16;         // FORMAT.md §1: records padded to 16 bytes
@@ -72,6 +83,16 @@ __device__ __forceinline__ u32 crc_step8(const u32 (*t)[256], u32 c, u32 lo, u32
 // Register shift past 16 << k zero bytes (k = 0, 1) by a 4 x 256 table (linearity in the register).
 __device__ __forceinline__ u32 crc_zshift(const u32 (*z)[256], u32 c) {
   return z[0][c & 0xFF] ^ z[1][(c >> 8) & 0xFF] ^ z[2][(c >> 16) & 0xFF] ^ z[3][c >> 24];
+}
+
+// CRC register of one 16-byte piece (two slicing-by-8 steps from a zero register).
+__device__ __forceinline__ u32 crc_piece16(const u32 (*t)[256], uint4 v) {
+  return crc_step8(t, crc_step8(t, 0u, v.x, v.y), v.z, v.w);
+}
+
+// Value of the partner lane of a lane pair (lanes 2i, 2i + 1), one DPP move.
+__device__ __forceinline__ u32 pair_swap(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -11,165 +11,11 @@
 // append path: launch k reports launch k-1 complete through a host-visible word, and the tail is
 // read with hipStreamQuery. Control-plane calls (leadership, replicas, acks, consumer offsets,
 // fetch) flush and drain first and run synchronously: they are rare next to the append stream.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <deque>
-#include <mutex>
-#include <new>
-#include <string>
-#include <unordered_set>
-#include <vector>
-
-#include "../../include/ripplemq_engine.h"
-#include "device_common.hpp"
-#include "kernels.hpp"
+#include "engine_internal.hpp"
 
 using namespace rmq;
 
-namespace {
-
-constexpr uint32_t kStatsRing = 64;                                // tickets whose stats stay readable
-constexpr uint32_t kMaxBatchRecords = kMaxTiles * kTileRecs;       // 524288
-constexpr uint32_t kSets = 4;                                      // pipeline scratch sets
-
-struct EvPair {
-  hipEvent_t a = nullptr, b = nullptr;
-};
-
-// Device staging of host-memory batches.
-struct Staging {
-  uint32_t* d_pidx = nullptr;
-  uint32_t* d_len = nullptr;
-  uint64_t* d_poff = nullptr;
-  uint8_t* d_payload = nullptr;
-  uint64_t* d_out = nullptr;
-  uint64_t ticket = 0;  // last ticket that used it
-};
-
-// A batch inside the launch pipeline.
-struct InFlight {
-  uint64_t ticket = 0;
-  PipeBatch b{};
-  uint64_t* host_out = nullptr;  // host batches: caller's out_offsets
-};
-
-// A group of consecutive batches moving through the pipeline together (one launch per stage).
-struct GroupFlight {
-  uint32_t nb = 0, tiles = 0, tasks = 0;
-  uint32_t set = 0;              // scratch set = group number % kSets
-  InFlight b[kMaxGroup];
-};
-
-}  // namespace
-
-struct rmq_engine {
-  rmq_config cfg{};
-  std::mutex mu;
-  int device = 0;
-  uint32_t cu_count = 0;
-  char dev_name[256] = {0};
-  hipStream_t main_s = nullptr;
-  DevState st{};            // leo/used point at sets[applied & 1]
-  StateSet sets[2]{};
-  uint64_t applied = 0;     // stage-3 launches issued
-  CrcConsts* d_crc = nullptr;
-  uint32_t* d_err = nullptr;
-  uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
-  uint32_t max_tasks = 0;
-  uint32_t max_tiles = 0;
-  uint32_t key_passes = 0;
-  PipeScratch scratch[kSets]{};
-  std::vector<Staging> staging;
-  // pipeline: the group being formed, then groups ranked (need stage 2), scanned (need stage 3)
-  // and applied (need stage 4)
-  GroupFlight forming, g1, g2, g3;
-  bool has1 = false, has2 = false, has3 = false;
-  uint32_t group_max = 2;       // batches per group (cfg.pipeline_depth)
-  uint32_t max_group_tiles = 0;
-  uint64_t groups = 0;          // groups formed
-  uint64_t launch_seq = 0;
-  uint64_t* done_host = nullptr;     // pinned: launch k-1 complete, written by launch k
-  uint64_t* done_dev = nullptr;
-  uint64_t last_ticket = 0;
-  std::vector<uint32_t> ticket_n;        // [kStatsRing] records of each recent ticket (stats)
-  // completion: tickets are applied in order, launch after launch. marks = {hi, L}: every ticket
-  // <= hi not covered by an earlier mark is applied by launch L (empty tickets count with the
-  // non-empty one before them); every ticket <= done_ticket is complete.
-  std::deque<std::pair<uint64_t, uint64_t>> marks;
-  uint64_t done_ticket = 0;
-  // host mirrors of control state
-  std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
-  std::vector<uint64_t> term;
-  // fetch: its own stream and scratch, serialised by fetch_mu (engine state under mu only while
-  // the fetch is ordered against the pipeline stream)
-  std::mutex fetch_mu;
-  hipStream_t fetch_s = nullptr;
-  hipEvent_t ev_main = nullptr, ev_fetch = nullptr;
-  uint32_t* d_req = nullptr;
-  uint64_t* d_res = nullptr;
-  uint64_t* d_aux = nullptr;
-  uint32_t* d_cpre = nullptr;
-  uint64_t* d_total = nullptr;
-  uint32_t* h_req = nullptr;   // pinned
-  uint64_t* h_res = nullptr;   // pinned [cap][4] + 2 totals
-  uint32_t fetch_cap = 0;
-  uint8_t* d_fetch_out = nullptr;
-  uint64_t fetch_out_cap = 0;
-  // consumer-commit / ack scratch
-  uint32_t* d_ctl32 = nullptr;
-  uint64_t* d_ctl64 = nullptr;
-  uint32_t ctl_cap = 0;
-  // profiling: pipeline launches are timed as one region (event before the first launch after
-  // enable, event at the next drain) so no per-launch events sit between kernels; fetch kernels
-  // keep per-launch event pairs (prof[3], prof[4])
-  uint32_t profile = 0;
-  uint64_t prof_launches = 0, prof_batches = 0;
-  hipEvent_t prof_t0 = nullptr, prof_t1 = nullptr;
-  bool prof_started = false, prof_ended = false;
-  std::vector<EvPair> prof[5];
-  std::vector<hipEvent_t> ev_pool;
-  // diagnostics: RMQ_STAMPS=<csv> records per-wave phase stamps of launch RMQ_STAMPS_AT (default 100)
-  const char* stamps_path = nullptr;
-  uint64_t stamps_at = 100;
-  uint64_t* d_stamps = nullptr;
-  uint32_t stamps_wg[4] = {0, 0, 0, 0};
-  // one stage-3 wave per task: the workgroups beyond the resident slots dispatch as stage-1/2
-  // workgroups retire (RMQ_WG3_ALL=0: only as many as fit next to them, looping over tasks)
-  uint32_t wg3_all = 1;
-  uint32_t s3_first = 0;  // RMQ_S3_FIRST=1: stage-3 workgroups first in dispatch order
-  uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
-};
-
-namespace {
-
-int hip_fail(hipError_t e) {
-  if (e == hipSuccess) return RMQ_OK;
-  std::fprintf(stderr, "ripplemq: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
-  return e == hipErrorOutOfMemory ? RMQ_ENOMEM : RMQ_EDEVICE;
-}
-
-#define HIP_TRY(x)                      \
-  do {                                  \
-    hipError_t _e = (x);                \
-    if (_e != hipSuccess) return hip_fail(_e); \
-  } while (0)
-
-template <typename T>
-int dalloc(T** p, size_t count) {
-  *p = nullptr;
-  if (!count) count = 1;
-  HIP_TRY(hipMalloc((void**)p, count * sizeof(T)));
-  // The null stream does not order with the engine's non-blocking streams: finish the zeroing
-  // before any engine stream can touch the buffer (a lazily allocated staging buffer would
-  // otherwise be zeroed after its first H2D copy).
-  HIP_TRY(hipMemset(*p, 0, count * sizeof(T)));
-  HIP_TRY(hipDeviceSynchronize());
-  return RMQ_OK;
-}
+namespace rmq {
 
 uint32_t host_mulmod(uint32_t a, uint32_t b) {
   uint32_t p = 0;
@@ -314,7 +160,12 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.s2 = e->scratch[s2->set];
     a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + kPipeThreads - 1) / kPipeThreads, 2u * e->cu_count));
   }
-  if (s3 || s4) a.wgp = (P + kPipeThreads - 1) / kPipeThreads;
+  repl_pipe_args(e, a, s2, s3);
+  {
+    int rc = repl_before_launch(e, a);  // followers' acks of the group applied three launches ago
+    if (rc) return rc;
+  }
+  if (s3 || s4 || a.ackin) a.wgp = (P + kPipeThreads - 1) / kPipeThreads;
   if (s4) {
     a.g4 = make_group(e, *s4);
     a.s4 = e->scratch[s4->set];
@@ -363,7 +214,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     const uint64_t hi = next ? next->b[0].ticket - 1 : e->last_ticket;
     e->marks.emplace_back(hi, e->launch_seq);
   }
-  return RMQ_OK;
+  return repl_after_launch(e, s2, s3);
 }
 
 // One launch: ranks the group being formed (if any) and advances the groups ahead of it.
@@ -393,6 +244,7 @@ int flush(rmq_engine* e) {
 
 int drain(rmq_engine* e) {
   int rc = flush(e);
+  if (!rc) rc = repl_drain(e);  // the remaining replication rounds and their acks
   if (rc) return rc;
   if (e->profile && e->prof_started && !e->prof_ended) {
     HIP_TRY(hipEventRecord(e->prof_t1, e->main_s));
@@ -430,6 +282,7 @@ int ticket_state(rmq_engine* e, uint64_t t) {
 int wait_ticket(rmq_engine* e, uint64_t t) {
   int s = ticket_state(e, t);
   if (s < 0) {
+    if (e->repl) return RMQ_PENDING;  // a flush is collective with a transport: rmq_sync on every rank
     int rc = flush(e);
     if (rc) return rc;
     s = ticket_state(e, t);
@@ -489,10 +342,13 @@ void free_engine(rmq_engine* e) {
   if (!e) return;
   hipSetDevice(e->device);
   if (e->main_s) {
-    flush(e);  // every submitted batch is applied before the memory goes away
+    // every submitted batch is applied before the memory goes away; with a replication transport
+    // a flush is collective, so the application must have called rmq_sync on every rank
+    if (!e->repl) flush(e);
     hipStreamSynchronize(e->main_s);
     dump_stamps(e);
   }
+  repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_err,
@@ -546,7 +402,7 @@ int validate_cfg(const rmq_config* c) {
   return RMQ_OK;
 }
 
-}  // namespace
+}  // namespace rmq
 
 extern "C" {
 
@@ -685,6 +541,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->leader_slot.assign(P, 0u);
   e->ranks.assign((size_t)P * RF, cfg->rank);
   e->term.assign(P, 1ull);
+  e->key.resize(P);
+  for (uint32_t p = 0; p < P; ++p) e->key[p] = p;
   e->ticket_n.assign(kStatsRing, 0u);
   {
     uint32_t bits = 0;
@@ -701,26 +559,54 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
 
 void rmq_destroy(rmq_engine* e) { free_engine(e); }
 
-int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* ranks, uint32_t rf, uint32_t leader_slot) {
-  if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
-  if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
-  const uint32_t RF = e->cfg.replication_factor;
-  if (!ranks || rf != RF || leader_slot >= rf) return RMQ_EINVAL;
+namespace {
+
+// Placement of n partitions (engine locked). With a replication transport this is collective:
+// every rank recomputes its out / in lists and checks them against its peers'.
+int set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* key, const uint32_t* ranks,
+                  const uint32_t* leader_slot) {
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  if (n && (!pidx || !ranks || !leader_slot)) return RMQ_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (pidx[i] >= P) return RMQ_ENOPART;
+    if (leader_slot[i] >= RF) return RMQ_EINVAL;
+  }
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
   if (!rc) rc = equalize_state_sets(e);
   if (rc) return rc;
-  uint32_t mask = 0;
-  for (uint32_t r = 0; r < RF; ++r) {
-    e->ranks[(size_t)pidx * RF + r] = ranks[r];
-    if (ranks[r] == e->cfg.rank) mask |= 1u << r;
+  std::vector<uint32_t> mask(P);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = pidx[i];
+    for (uint32_t r = 0; r < RF; ++r) e->ranks[(size_t)p * RF + r] = ranks[(size_t)i * RF + r];
+    e->leader_slot[p] = leader_slot[i];
+    e->is_leader[p] = ranks[(size_t)i * RF + leader_slot[i]] == e->cfg.rank;
+    if (key) e->key[p] = key[i];
   }
-  e->leader_slot[pidx] = leader_slot;
-  e->is_leader[pidx] = ranks[leader_slot] == e->cfg.rank;
-  HIP_TRY(hipMemcpy(e->st.is_leader + pidx, &e->is_leader[pidx], 4, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->st.local_mask + pidx, &mask, 4, hipMemcpyHostToDevice));
-  return RMQ_OK;
+  for (uint32_t p = 0; p < P; ++p) {
+    mask[p] = 0;
+    for (uint32_t r = 0; r < RF; ++r) mask[p] |= (e->ranks[(size_t)p * RF + r] == e->cfg.rank ? 1u : 0u) << r;
+  }
+  HIP_TRY(hipMemcpy(e->st.is_leader, e->is_leader.data(), P * 4ull, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->st.local_mask, mask.data(), P * 4ull, hipMemcpyHostToDevice));
+  return e->repl ? repl_set_lists(e) : RMQ_OK;
+}
+
+}  // namespace
+
+int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* ranks, uint32_t rf, uint32_t leader_slot) {
+  if (!e) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
+  if (!ranks || rf != e->cfg.replication_factor || leader_slot >= rf) return RMQ_EINVAL;
+  return set_placement(e, 1, &pidx, nullptr, ranks, &leader_slot);
+}
+
+int rmq_set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* key, const uint32_t* ranks,
+                      const uint32_t* leader_slot) {
+  if (!e) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  return set_placement(e, n, pidx, key, ranks, leader_slot);
 }
 
 int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
@@ -734,14 +620,19 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
     bool local = false;
     for (uint32_t r = 0; r < RF; ++r) local |= e->ranks[(size_t)p * RF + r] == e->cfg.rank;
     if (!local) return RMQ_EINVAL;
+    // with a transport the placement (collective) names the leader; this starts its term
+    if (e->repl && e->ranks[(size_t)p * RF + e->leader_slot[p]] != e->cfg.rank) return RMQ_EINVAL;
   }
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
   if (!rc) rc = equalize_state_sets(e);
   if (rc) return rc;
   for (uint32_t p = lo; p < hi; ++p) {
-    uint32_t slot = 0;
-    while (e->ranks[(size_t)p * RF + slot] != e->cfg.rank) ++slot;
+    uint32_t slot = e->leader_slot[p];
+    if (!e->repl) {
+      slot = 0;
+      while (e->ranks[(size_t)p * RF + slot] != e->cfg.rank) ++slot;
+    }
     e->leader_slot[p] = slot;
     e->is_leader[p] = 1;
     e->term[p] = term;
@@ -775,16 +666,8 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   const uint64_t t = ++e->last_ticket;
   *ticket = t;
   e->ticket_n[t % kStatsRing] = n;
-  if (n == 0) {  // completes with the last non-empty batch before it
-    if (!e->forming.nb && !e->has1 && !e->has2) {
-      if (!e->marks.empty())
-        e->marks.back().first = t;
-      else
-        e->done_ticket = t;
-    }
-    return RMQ_OK;
-  }
-
+  // an empty batch still takes its place in a launch group (0 tiles, 0 tasks): every rank of a
+  // replication transport forms the same groups from the same number of calls
   InFlight f;
   f.ticket = t;
   f.b.pidx = b->pidx;
@@ -795,7 +678,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   f.b.out_offsets = out_offsets;
   f.b.n = n;
   f.b.tiles = (n + kTileRecs - 1) / kTileRecs;
-  if (b->mem == RMQ_MEM_HOST) {
+  if (b->mem == RMQ_MEM_HOST && n) {
     Staging& sg = e->staging[t % e->staging.size()];
     if (sg.ticket) {  // the batch that used this staging slot must be complete
       int rc = wait_ticket(e, sg.ticket);
@@ -824,7 +707,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     f.b.out_offsets = sg.d_out;
     f.host_out = out_offsets;
   }
-  if (e->forming.nb && e->forming.tiles + f.b.tiles > e->max_group_tiles) {
+  if (e->forming.nb && e->forming.tiles + f.b.tiles > e->max_group_tiles) {  // (never with a transport)
     int rc = close_group(e);
     if (rc) return rc;
   }
@@ -871,18 +754,18 @@ int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64
   HIP_TRY(hipSetDevice(e->device));
   if (ticket) {
     int s = ticket_state(e, ticket);
-    if (s < 0) {
+    if (s < 0 && !e->repl) {
       int rc = flush(e);  // a poll pushes the batch through the remaining stages
       if (rc) return rc;
       s = ticket_state(e, ticket);
     }
-    if (s == 0) return RMQ_PENDING;
+    if (s <= 0) return RMQ_PENDING;
   }
   int rc = check_err(e);
   if (rc) return rc;
   const size_t P = e->cfg.num_partitions;
   if (commit_out || hw_out) {
-    rc = drain(e);  // snapshot after everything submitted so far
+    rc = e->repl ? quiesce(e) : drain(e);  // snapshot after everything submitted (applied, with a transport)
     if (rc) return rc;
     if (commit_out) HIP_TRY(hipMemcpy(commit_out, e->st.commit, P * 8, hipMemcpyDeviceToHost));
     if (hw_out) HIP_TRY(hipMemcpy(hw_out, e->st.hw, P * 8, hipMemcpyDeviceToHost));
@@ -896,7 +779,7 @@ int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out) {
   if (!ticket || ticket > e->last_ticket || e->last_ticket - ticket >= kStatsRing) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = wait_ticket(e, ticket);
-  if (rc) return rc;
+  if (rc) return rc;  // RMQ_PENDING with a transport until an rmq_sync applied the ticket
   const uint32_t n = e->ticket_n[ticket % kStatsRing];
   const uint32_t tasks = (n + kTaskRecs - 1) / kTaskRecs;
   std::vector<uint4> ts(tasks ? tasks : 1);
@@ -1256,6 +1139,95 @@ int rmq_device_info(rmq_engine* e, char* name, uint32_t name_cap, uint32_t* cu_c
   if (!e) return RMQ_EINVAL;
   if (name && name_cap) std::snprintf(name, name_cap, "%s", e->dev_name);
   if (cu_count) *cu_count = e->cu_count;
+  return RMQ_OK;
+}
+
+int rmq_rccl_unique_id(uint8_t* out) {
+  if (!out) return RMQ_EINVAL;
+  return rccl_unique_id(out);
+}
+
+int rmq_attach_rccl(rmq_engine* e, const uint8_t* comm_id, uint32_t world) {
+  if (!e || !comm_id || world < 2 || world > kMaxWorld) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (e->repl) return RMQ_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = drain(e);
+  if (rc) return rc;
+  Transport* t = make_rccl_transport(comm_id, world, e->cfg.rank);
+  if (!t) return RMQ_EDEVICE;
+  rc = repl_attach(e, t);
+  if (rc && !e->repl) delete t;
+  return rc;
+}
+
+struct rmq_local_hub {
+  rmq::LocalHub hub;
+  explicit rmq_local_hub(uint32_t w) : hub(w) {}
+};
+
+int rmq_local_hub_create(uint32_t world, rmq_local_hub** out) {
+  if (!out || world < 2 || world > kMaxWorld) return RMQ_EINVAL;
+  *out = new (std::nothrow) rmq_local_hub(world);
+  return *out ? RMQ_OK : RMQ_ENOMEM;
+}
+
+void rmq_local_hub_destroy(rmq_local_hub* h) { delete h; }
+
+int rmq_attach_local(rmq_engine* e, rmq_local_hub* h) {
+  if (!e || !h) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (e->repl) return RMQ_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = drain(e);
+  if (rc) return rc;
+  Transport* t = make_local_transport(&h->hub, e->cfg.rank, e->device);
+  rc = repl_attach(e, t);
+  if (rc && !e->repl) delete t;
+  return rc;
+}
+
+int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
+  if (!e || !out) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  std::memset(out, 0, sizeof *out);
+  if (!e->repl) return RMQ_OK;
+  const Replication* r = e->repl;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(r->xchg_s));
+  uint64_t c[4];
+  HIP_TRY(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost));
+  out->world = r->world;
+  out->rank = r->rank;
+  out->out_entries = (uint32_t)r->xo_p.size();
+  out->in_entries = (uint32_t)r->xi_p.size();
+  out->rounds = r->rounds;
+  out->bytes_sent = r->bytes_sent;
+  out->bytes_received = r->bytes_recv;
+  out->records_ingested = c[0];
+  out->refused_crc = c[1];
+  out->refused_log = c[2];
+  out->bytes_ingested = c[3];
+  return RMQ_OK;
+}
+
+int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size) {
+  if (!e || !size) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  *size = 0;
+  Replication* r = e->repl;
+  if (!r || dst >= r->world) return RMQ_EINVAL;
+  if (r->last_set == ~0u) return RMQ_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipStreamSynchronize(r->xchg_s));
+  const XchgSet& x = r->sets[r->last_set];
+  uint64_t off = 0;
+  for (uint32_t q = 0; q < dst; ++q) off += q == r->rank ? 0 : x.h_sizes[2 * q];
+  const uint64_t n = dst == r->rank ? 0 : x.h_sizes[2 * dst];
+  *size = n;
+  if (!out) return RMQ_OK;
+  if (n > cap) return RMQ_ENOSPC;
+  if (n) HIP_TRY(hipMemcpy(out, x.outbox + off, n, hipMemcpyDeviceToHost));
   return RMQ_OK;
 }
 

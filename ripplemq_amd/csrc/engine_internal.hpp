@@ -1,0 +1,223 @@
+// engine_internal.hpp — the engine object shared by the host-side translation units
+// (engine.cpp: C-ABI, append pipeline, fetch, control; replication.cpp: replica-log rounds).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <new>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/ripplemq_engine.h"
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "transport.hpp"
+
+using namespace rmq;
+
+namespace rmq {
+
+constexpr uint32_t kStatsRing = 64;                                // tickets whose stats stay readable
+constexpr uint32_t kMaxBatchRecords = kMaxTiles * kTileRecs;       // 524288
+// pipeline scratch sets: a group's set lives from its stage 1 (launch k) to the application of its
+// followers' acks (launch k + 5 with a replication transport), so six sets rotate
+constexpr uint32_t kSets = 6;
+
+struct EvPair {
+  hipEvent_t a = nullptr, b = nullptr;
+};
+
+// Device staging of host-memory batches.
+struct Staging {
+  uint32_t* d_pidx = nullptr;
+  uint32_t* d_len = nullptr;
+  uint64_t* d_poff = nullptr;
+  uint8_t* d_payload = nullptr;
+  uint64_t* d_out = nullptr;
+  uint64_t ticket = 0;  // last ticket that used it
+};
+
+// A batch inside the launch pipeline.
+struct InFlight {
+  uint64_t ticket = 0;
+  PipeBatch b{};
+  uint64_t* host_out = nullptr;  // host batches: caller's out_offsets
+};
+
+// A group of consecutive batches moving through the pipeline together (one launch per stage).
+struct GroupFlight {
+  uint32_t nb = 0, tiles = 0, tasks = 0;
+  uint32_t set = 0;              // scratch set = group number % kSets
+  InFlight b[kMaxGroup];
+};
+
+// Replica-log rounds over a transport (replication.cpp, FORMAT.md §9): per scratch set, the
+// group's outbox and inbox and the exchange's events.
+struct XchgSet {
+  uint8_t* outbox = nullptr;
+  uint8_t* inbox = nullptr;
+  XEntry* xe = nullptr;        // [n_out]
+  uint64_t* sizes = nullptr;   // device [2 * world]: send sizes (plan), receive sizes (exchange)
+  uint64_t* h_sizes = nullptr; // pinned copy
+  uint64_t* ackout = nullptr;  // [n_in]
+  uint64_t* ackin = nullptr;   // [n_out]
+  uint32_t* count = nullptr;   // stage-2 arrival counter
+  hipEvent_t ev_s2 = nullptr, ev_s3 = nullptr, ev_sz = nullptr, ev_x = nullptr;
+  uint64_t applied_launch = 0; // launch that ran the group's stage 3
+};
+
+struct Replication {
+  Transport* xport = nullptr;
+  uint32_t world = 1, rank = 0;
+  hipStream_t xchg_s = nullptr;
+  // out list: (led partition, remote slot) grouped by destination, ascending (key, slot);
+  // in list: (followed partition, local slot) grouped by source, same order on both sides
+  std::vector<uint32_t> xo_p, xo_slot, xo_start, xi_p, xi_slot, xi_start;
+  std::vector<uint64_t> keysum;  // [world] of the out lists
+  uint32_t* d_xo_p = nullptr;
+  uint32_t* d_xo_start = nullptr;
+  uint64_t* d_keysum = nullptr;
+  uint32_t* d_outidx = nullptr;  // [P][RF]
+  uint32_t* d_xi_p = nullptr;
+  uint32_t* d_xi_slot = nullptr;
+  uint32_t* d_xi_start = nullptr;
+  uint32_t* d_bad = nullptr;     // [n_in]
+  uint64_t* d_counters = nullptr;  // [4] (IngestArgs)
+  uint64_t out_cap = 0, in_cap = 0;
+  XchgSet sets[kSets];
+  std::deque<uint32_t> sized;    // sets whose size exchange is posted, data exchange not yet
+  std::deque<uint32_t> acking;   // sets whose data exchange is posted, acks not yet applied
+  uint64_t rounds = 0, bytes_sent = 0, bytes_recv = 0;
+  uint32_t last_set = ~0u;       // set of the last posted round (rmq_read_outbox)
+};
+
+}  // namespace rmq
+
+struct rmq_engine {
+  rmq_config cfg{};
+  std::mutex mu;
+  int device = 0;
+  uint32_t cu_count = 0;
+  char dev_name[256] = {0};
+  hipStream_t main_s = nullptr;
+  DevState st{};            // leo/used point at sets[applied & 1]
+  StateSet sets[2]{};
+  uint64_t applied = 0;     // stage-3 launches issued
+  CrcConsts* d_crc = nullptr;
+  uint32_t* d_err = nullptr;
+  uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
+  uint32_t max_tasks = 0;
+  uint32_t max_tiles = 0;
+  uint32_t key_passes = 0;
+  PipeScratch scratch[kSets]{};
+  std::vector<Staging> staging;
+  // pipeline: the group being formed, then groups ranked (need stage 2), scanned (need stage 3)
+  // and applied (need stage 4)
+  GroupFlight forming, g1, g2, g3;
+  bool has1 = false, has2 = false, has3 = false;
+  uint32_t group_max = 2;       // batches per group (cfg.pipeline_depth)
+  uint32_t max_group_tiles = 0;
+  uint64_t groups = 0;          // groups formed
+  uint64_t launch_seq = 0;
+  uint64_t* done_host = nullptr;     // pinned: launch k-1 complete, written by launch k
+  uint64_t* done_dev = nullptr;
+  uint64_t last_ticket = 0;
+  std::vector<uint32_t> ticket_n;        // [kStatsRing] records of each recent ticket (stats)
+  // completion: tickets are applied in order, launch after launch. marks = {hi, L}: every ticket
+  // <= hi not covered by an earlier mark is applied by launch L (empty tickets count with the
+  // non-empty one before them); every ticket <= done_ticket is complete.
+  std::deque<std::pair<uint64_t, uint64_t>> marks;
+  uint64_t done_ticket = 0;
+  // host mirrors of control state
+  std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
+  std::vector<uint64_t> term;
+  // fetch: its own stream and scratch, serialised by fetch_mu (engine state under mu only while
+  // the fetch is ordered against the pipeline stream)
+  std::mutex fetch_mu;
+  hipStream_t fetch_s = nullptr;
+  hipEvent_t ev_main = nullptr, ev_fetch = nullptr;
+  uint32_t* d_req = nullptr;
+  uint64_t* d_res = nullptr;
+  uint64_t* d_aux = nullptr;
+  uint32_t* d_cpre = nullptr;
+  uint64_t* d_total = nullptr;
+  uint32_t* h_req = nullptr;   // pinned
+  uint64_t* h_res = nullptr;   // pinned [cap][4] + 2 totals
+  uint32_t fetch_cap = 0;
+  uint8_t* d_fetch_out = nullptr;
+  uint64_t fetch_out_cap = 0;
+  // consumer-commit / ack scratch
+  uint32_t* d_ctl32 = nullptr;
+  uint64_t* d_ctl64 = nullptr;
+  uint32_t ctl_cap = 0;
+  // profiling: pipeline launches are timed as one region (event before the first launch after
+  // enable, event at the next drain) so no per-launch events sit between kernels; fetch kernels
+  // keep per-launch event pairs (prof[3], prof[4])
+  uint32_t profile = 0;
+  uint64_t prof_launches = 0, prof_batches = 0;
+  hipEvent_t prof_t0 = nullptr, prof_t1 = nullptr;
+  bool prof_started = false, prof_ended = false;
+  std::vector<EvPair> prof[5];
+  std::vector<hipEvent_t> ev_pool;
+  // diagnostics: RMQ_STAMPS=<csv> records per-wave phase stamps of launch RMQ_STAMPS_AT (default 100)
+  const char* stamps_path = nullptr;
+  uint64_t stamps_at = 100;
+  uint64_t* d_stamps = nullptr;
+  uint32_t stamps_wg[4] = {0, 0, 0, 0};
+  // one stage-3 wave per task: the workgroups beyond the resident slots dispatch as stage-1/2
+  // workgroups retire (RMQ_WG3_ALL=0: only as many as fit next to them, looping over tasks)
+  uint32_t wg3_all = 1;
+  uint32_t s3_first = 0;  // RMQ_S3_FIRST=1: stage-3 workgroups first in dispatch order
+  uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
+  std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)
+  rmq::Replication* repl = nullptr;  // replication transport attached (collective mode)
+};
+
+namespace rmq {
+
+inline int hip_fail(hipError_t e) {
+  if (e == hipSuccess) return RMQ_OK;
+  std::fprintf(stderr, "ripplemq: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
+  return e == hipErrorOutOfMemory ? RMQ_ENOMEM : RMQ_EDEVICE;
+}
+
+#define HIP_TRY(x)                      \
+  do {                                  \
+    hipError_t _e = (x);                \
+    if (_e != hipSuccess) return hip_fail(_e); \
+  } while (0)
+
+template <typename T>
+int dalloc(T** p, size_t count) {
+  *p = nullptr;
+  if (!count) count = 1;
+  HIP_TRY(hipMalloc((void**)p, count * sizeof(T)));
+  // The null stream does not order with the engine's non-blocking streams: finish the zeroing
+  // before any engine stream can touch the buffer (a lazily allocated staging buffer would
+  // otherwise be zeroed after its first H2D copy).
+  HIP_TRY(hipMemset(*p, 0, count * sizeof(T)));
+  HIP_TRY(hipDeviceSynchronize());
+  return RMQ_OK;
+}
+
+// engine.cpp
+int flush(rmq_engine* e);
+int drain(rmq_engine* e);
+int quiesce(rmq_engine* e);
+int check_err(rmq_engine* e);
+// replication.cpp
+int repl_attach(rmq_engine* e, Transport* t);
+void repl_free(rmq_engine* e);
+int repl_set_lists(rmq_engine* e);
+void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const GroupFlight* s3);
+int repl_before_launch(rmq_engine* e, PipeArgs& a);
+int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s3);
+int repl_drain(rmq_engine* e);
+
+}  // namespace rmq

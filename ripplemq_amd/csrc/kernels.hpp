@@ -21,8 +21,36 @@ constexpr uint32_t kTaskRecs = 32;       // records per apply task (one wave, 2 
 constexpr uint32_t kMaxGroup = 8;        // batches per pipeline group (cfg.pipeline_depth)
 constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-bit LDS radix passes)
 constexpr uint32_t kMaxRF = 8;
+constexpr uint32_t kMaxWorld = 16;       // ranks of a replication transport
+constexpr uint32_t kMaxRemote = 4;       // remote replica slots per partition with a transport (RF <= 5)
+constexpr uint32_t kXMagic = 0x58514D52u;  // "RMQX": replica-log round region (FORMAT.md §9)
+constexpr uint32_t kRegionHdr = 32;      // region header bytes
+constexpr uint32_t kDirEntry = 32;       // directory entry bytes
 
 struct CrcConsts;
+
+// Where one out entry (a led partition's remote replica slot) of a group lands in the group's
+// outbox (FORMAT.md §9), written by stage 2's plan, read by stage 3. 32 bytes.
+struct XEntry {
+  uint64_t data_abs;      // outbox byte offset of the entry's first record
+  uint64_t tab_abs;       // outbox byte offset of the entry's first record-table slot
+  uint64_t dir_abs;       // outbox byte offset of the entry's directory entry
+  uint32_t k;             // entry index inside its destination's list
+  uint32_t data_start16;  // entry's first record inside the region's data section, / 16
+};
+
+// Leader side of a replication round: the layout plan of one group's outbox (stage 2 of the group,
+// computed by the last stage-2 workgroup of the launch).
+struct XPlanArgs {
+  const uint32_t* xo_p;      // [n_out] led partition of each out entry, grouped by destination
+  const uint32_t* xo_start;  // [world + 1]
+  const uint64_t* keysum;    // [world] FORMAT.md §9 key sum of each destination's entry list
+  uint32_t world, rank, n_out, pad;
+  uint32_t* count;           // arrival counter of the launch's stage-2 workgroups (reset by the plan)
+  XEntry* xe;                // [n_out]
+  uint8_t* outbox;
+  uint64_t* sizes;           // [world][2] {region bytes, records} per destination (0: nothing to send)
+};
 
 // Per-partition device state (SoA, [P] unless noted). Owned by the engine.
 struct DevState {
@@ -108,6 +136,12 @@ struct PipeArgs {
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2
   uint64_t nospace_limit;  // segment - interval: record bytes one batch may add to one partition
+  // replication transport attached (else all null / n_out = 0)
+  XPlanArgs xp2;           // stage 2's group: outbox plan
+  const uint32_t* outidx;  // [P][RF] out entry of (partition, slot), ~0: local or no entry
+  const XEntry* xe3;       // stage 3's group: entry placement
+  uint8_t* outbox3;        // stage 3's group: its outbox
+  const uint64_t* ackin;   // acks of an earlier group, by out entry (partition threads), or null
   const CrcConsts* crc;
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
   uint64_t launch_seq;
@@ -144,6 +178,31 @@ struct AckArgs {
   uint32_t n;
 };
 
+// Follower side of a replication round: ingest every source's region of one inbox.
+struct IngestArgs {
+  DevState st;
+  StateSet sets[2];          // follower partitions keep both sets equal
+  const uint8_t* inbox;
+  uint64_t region[kMaxWorld];     // inbox byte offset of each source's region
+  uint64_t rbytes[kMaxWorld];     // its size (0: nothing from that source)
+  uint32_t task0[kMaxWorld + 1];  // prefix of the per-source task bounds (32 records per task)
+  const uint32_t* xi_p;      // [n_in] local partition of each in entry, grouped by source
+  const uint32_t* xi_slot;   // [n_in] local replica slot
+  const uint32_t* xi_start;  // [world + 1]
+  uint32_t world, rank, n_in, pad;
+  uint32_t* bad;             // [n_in] entry refused this round (cleared by the finish kernel)
+  uint64_t* ackout;          // [n_in] follower log end after the round
+  const CrcConsts* crc;
+  uint64_t* counters;        // [4] records ingested, entries refused (CRC), refused (log mismatch), bytes
+};
+
+// Acks of one round applied outside the pipeline (drain): thread per partition.
+struct AckApplyArgs {
+  DevState st;
+  const uint32_t* outidx;
+  const uint64_t* ackin;
+};
+
 // launchers (defined in the .hip files)
 void launch_pipeline(const PipeArgs& a, hipStream_t s);
 uint32_t pipeline_lds_bytes();
@@ -154,5 +213,7 @@ void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev_resolve0, hipEvent_t ev_resolve1,
                   hipEvent_t ev_gather0, hipEvent_t ev_gather1);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
+void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s);
+void launch_ack_apply(const AckApplyArgs& a, hipStream_t s);
 
 }  // namespace rmq

@@ -29,6 +29,26 @@ __device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u
   return (N > commit && N > term_start) ? N : commit;
 }
 
+// Remote replica acks of one replication round (FORMAT.md §9) into the partition's matchIndex row:
+// match = max(match, min(ack, log end)) for every slot with an out entry. True if a slot moved.
+__device__ __forceinline__ bool apply_acks(const DevState& st, u32 p, const u32* outidx, const u64* ackin, u64 leo,
+                                           u64 (&row)[kMaxRF]) {
+  bool moved = false;
+#pragma unroll
+  for (u32 r = 0; r < kMaxRF; ++r) {
+    if (r >= st.RF) continue;
+    const u32 e = outidx[(u64)p * st.RF + r];
+    if (e == ~0u) continue;
+    const u64 a = ackin[e] < leo ? ackin[e] : leo;
+    if (a > row[r]) {
+      row[r] = a;
+      st.match[(u64)p * st.RF + r] = a;
+      moved = true;
+    }
+  }
+  return moved;
+}
+
 __device__ __forceinline__ void commit_rule(const DevState& st, u32 p) {
   u64 row[kMaxRF];
 #pragma unroll

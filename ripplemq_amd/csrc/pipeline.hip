@@ -87,7 +87,9 @@ struct Stage3Smem {
   u32 t8[8][256];       // slicing-by-8 CRC32C tables
   u32 z[2][4][256];     // register shift past 16 and 32 zero bytes
   uint4 img[kPW][kTaskRecs][8];  // per wave: the task's records as laid out in the log (<= 128 B each)
-  uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16}
+  uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16 | dead << 24}
+  u64 xdst[kPW][kTaskRecs][kMaxRemote];  // replication: each record's outbox address per remote slot
+  u32 xn[kPW][kTaskRecs];                // and how many
 };
 
 constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
@@ -330,6 +332,94 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
 // ------------------------------------------------------------------------------------------
 // Stage 2: batch rules, column scans over the group's tiles, tile payload bases
 // ------------------------------------------------------------------------------------------
+
+// Block-wide inclusive scan of one u64 per thread (kPT threads); *total gets the block sum.
+__device__ __forceinline__ u64 block_incl_scan_u64(u64 v, u64* s_w, u64* total) {
+  const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const u64 inc = wave_incl_scan_u64(v);
+  if (lane == 63) s_w[w] = inc;
+  __syncthreads();
+  u64 pre = 0, tot = 0;
+#pragma unroll
+  for (u32 k = 0; k < kPW; ++k) {
+    pre += k < w ? s_w[k] : 0ull;
+    tot += s_w[k];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc;
+}
+
+// The group's outbox layout (FORMAT.md §9), one workgroup: per destination d a region
+//   [header 32 B][directory n_d x 32 B][record table N_d x 8 B, padded to 16][records]
+// with the entries (led partition, remote slot) in the destination's list order; per entry its
+// record count / bytes and where stage 3 puts its records, table slots and first offset.
+__device__ void stage2_plan(const PipeArgs& A) {
+  const XPlanArgs& X = A.xp2;
+  const u64* const totals = A.s2.totals;
+  const u32 tid = threadIdx.x;
+  __shared__ u64 s_tot[kMaxWorld];   // {records << 40 | bytes / 16} per destination
+  __shared__ u64 s_base[kMaxWorld];  // region start
+  __shared__ u64 s_w[kPW];
+  if (tid < kMaxWorld) s_tot[tid] = 0ull;
+  __syncthreads();
+  for (u32 d = 0; d < X.world; ++d)
+    for (u32 e = X.xo_start[d] + tid; e < X.xo_start[d + 1]; e += kPT) atomicAdd(&s_tot[d], load_sc1(&totals[X.xo_p[e]]));
+  __syncthreads();
+  if (tid == 0) {
+    u64 start = 0;
+    for (u32 d = 0; d < X.world; ++d) {
+      const u64 n = X.xo_start[d + 1] - X.xo_start[d], N = s_tot[d] >> 40, b16 = s_tot[d] & kLow40;
+      const u64 size = n ? kRegionHdr + kDirEntry * n + ((8ull * N + 15ull) & ~15ull) + 16ull * b16 : 0ull;
+      s_base[d] = start;
+      X.sizes[2 * d] = size;    // the exchange swaps {region bytes, records} per peer
+      X.sizes[2 * d + 1] = n ? N : 0ull;
+      start += size;
+    }
+  }
+  __syncthreads();
+  for (u32 d = 0; d < X.world; ++d) {
+    const u32 e0 = X.xo_start[d], e1 = X.xo_start[d + 1];
+    if (e0 == e1) continue;
+    const u64 n = e1 - e0, N = s_tot[d] >> 40;
+    const u64 base = s_base[d], tab = base + kRegionHdr + kDirEntry * n, data = tab + ((8ull * N + 15ull) & ~15ull);
+    if (tid == 0) {
+      u32* h = reinterpret_cast<u32*>(X.outbox + base);
+      h[0] = kXMagic;
+      h[1] = (u32)n;
+      h[2] = (u32)N;
+      h[3] = X.rank;
+      *reinterpret_cast<u64*>(h + 4) = X.keysum[d];
+      *reinterpret_cast<u64*>(h + 6) = data - base;
+      if (N & 1ull) *reinterpret_cast<u64*>(X.outbox + tab + 8ull * N) = 0ull;  // table padding
+    }
+    u64 run = 0;
+    for (u32 c0 = e0; c0 < e1; c0 += kPT) {
+      const u32 e = c0 + tid;
+      const u64 v = e < e1 ? load_sc1(&totals[X.xo_p[e]]) : 0ull;
+      u64 tot;
+      const u64 ex = run + block_incl_scan_u64(v, s_w, &tot) - v;
+      run += tot;
+      if (e < e1) {
+        const u32 k = e - e0;
+        const u64 cnt_ex = ex >> 40, b16_ex = ex & kLow40;
+        const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
+        uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
+        de[0] = make_uint4((u32)(v >> 40), (u32)(v & kLow40), 0u, 0u);  // count, bytes / 16, first offset (stage 3)
+        de[1] = make_uint4((u32)cnt_ex, (u32)b16_ex, 0u, 0u);           // table start, data start / 16, reserved
+        XEntry xe;
+        xe.data_abs = data + 16ull * b16_ex;
+        xe.tab_abs = tab + 8ull * cnt_ex;
+        xe.dir_abs = dir;
+        xe.k = k;
+        xe.data_start16 = (u32)b16_ex;
+        X.xe[e] = xe;
+      }
+    }
+  }
+  if (tid == 0) __hip_atomic_store(X.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next used six launches later
+}
+
 __device__ void stage2(const PipeArgs& A, u32 wg) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
@@ -432,7 +522,19 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
       }
       if (s == 0) x.bcum[(u64)j * P + p] = carry;
     }
-    if (s == 0) x.totals[p] = carry;
+    if (s == 0) store_sc1(&x.totals[p], carry);  // sc1: the plan below reads it in this launch
+  }
+  if (A.xp2.n_out) {
+    // replication transport: the last stage-2 workgroup to finish lays out the group's outbox
+    // (every storing wave drained, then one counter add per workgroup; the last adder reads the
+    // sc1-stored totals with sc1 loads: MI355X_MICROARCH.md inter-workgroup visibility, row 1)
+    __shared__ u32 s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0)
+      s_last = __hip_atomic_fetch_add(A.xp2.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.wg2 - 1u;
+    __syncthreads();
+    if (s_last) stage2_plan(A);
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(1);
@@ -463,9 +565,6 @@ __device__ __forceinline__ uint4 extract_piece(uint4 b0, uint4 b1, u32 s, u32 nb
   return make_uint4((u32)lo, (u32)(lo >> 32), (u32)hi, (u32)(hi >> 32));
 }
 
-__device__ __forceinline__ u32 crc_piece16(const u32 (*t)[256], uint4 v) {
-  return crc_step8(t, crc_step8(t, 0u, v.x, v.y), v.z, v.w);
-}
 
 // Stage 3 works on tasks of kTaskRecs = 32 records of one batch, one per lane pair. The pair loads
 // the record's payload as aligned 16-byte blocks (lane j takes blocks j, j + 2, ...; 8 pieces =
@@ -475,9 +574,6 @@ __device__ __forceinline__ u32 crc_piece16(const u32 (*t)[256], uint4 v) {
 constexpr u32 kPR = 8;          // pieces per record per round
 constexpr u32 kBL = 5;          // blocks per lane per round (9 blocks cover 8 misaligned pieces)
 
-__device__ __forceinline__ u32 pair_swap(u32 v) {
-  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
-}
 __device__ __forceinline__ uint4 pair_swap4(uint4 v) {
   return make_uint4(pair_swap(v.x), pair_swap(v.y), pair_swap(v.z), pair_swap(v.w));
 }
@@ -575,6 +671,7 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
   return (A.debug & 2u) ? v.x : crc_piece16(S.t8, v);
 }
 
+template <bool XR>
 __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
                               const TaskState& Z, bool cand, uint4& stat_out) {
   const PipeBatch& b = A.g3.b[T.jb];
@@ -605,6 +702,32 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   // 8 consecutive lanes store each record's 128 bytes; longer ones are stored piecewise
   const bool img = __all(!ok || m <= 7u);
   const u32 w = threadIdx.x >> 6, r32 = lane >> 1;
+  Stage3Smem& W = const_cast<Stage3Smem&>(S);
+  // replication transport: every record also goes, whole, to the group's outbox once per remote
+  // replica slot (FORMAT.md §9), with its record-table slot and, for the partition's first record
+  // of the group, the directory's first offset
+  constexpr bool xr = XR;
+  if (xr) {
+    if (j == 0) {
+      u32 nx = 0;
+      if (ok) {
+        const u64 rel = pos - Z.used;                                            // bytes into the group
+        const u64 rk = ((Z.ex >> 40) & kCnt23) + (R.cr.x & kRankMask);           // records into the group
+        for (u32 r = 0; r < RF; ++r) {
+          if ((Z.lm >> r) & 1u) continue;
+          const u32 e = A.outidx[(u64)p * RF + r];
+          if (e == ~0u) continue;
+          const XEntry x = A.xe3[e];
+          W.xdst[w][r32][nx++] = reinterpret_cast<u64>(A.outbox3 + x.data_abs + rel);
+          *reinterpret_cast<u64*>(A.outbox3 + x.tab_abs + 8ull * rk) =
+              (u64)x.k | ((u64)(x.data_start16 + (u32)(rel >> 4)) << 32);
+          if (rk == 0) *reinterpret_cast<u64*>(A.outbox3 + x.dir_abs + 8) = off;
+        }
+      }
+      W.xn[w][r32] = nx;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
   uint4 blk[kBL];
 #pragma unroll
   for (u32 q = 0; q < kBL; ++q) blk[q] = Z.blk[q];
@@ -628,6 +751,9 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
           if (jp + 1u >= dead)
             for (u32 r = 0; r < RF; ++r)
               if ((lmw >> r) & 1u) store_log16(dst + r * rstride, v);
+          if (xr)
+            for (u32 q = 0; q < S.xn[w][r32]; ++q)
+              store_log16(reinterpret_cast<uint8_t*>(S.xdst[w][r32][q]) + 16ull + 16ull * jp, v);
         }
       }
     }
@@ -647,7 +773,6 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
   }
   if (img) {
-    Stage3Smem& W = const_cast<Stage3Smem&>(S);
     if (j == 1) W.img[w][r32][0] = h;
     if (j == 0)
       W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), p, Z.lm | (m << 8) | ((ok ? 1u : 0u) << 16) | (dead << 24));
@@ -657,20 +782,27 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
       const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
       const uint4 inf = W.info[w][rr];
       const u32 mr = (inf.w >> 8) & 0xFFu;
-      if (((inf.w >> 16) & 1u) && k <= mr && k >= (inf.w >> 24)) {
+      if (((inf.w >> 16) & 1u) && k <= mr) {
         const uint4 v = W.img[w][rr][k];
-        const u64 rpos = ((u64)inf.y << 32) | inf.x;
-        uint8_t* dst = st.logs + (u64)inf.z * st.seg + ((rpos + 16ull * k) & segmask);
-        const u32 lmr = (A.debug & 1u) ? 0u : (inf.w & 0xFFu);
-        for (u32 r = 0; r < RF; ++r)
-          if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
+        if (k >= (inf.w >> 24)) {
+          const u64 rpos = ((u64)inf.y << 32) | inf.x;
+          uint8_t* dst = st.logs + (u64)inf.z * st.seg + ((rpos + 16ull * k) & segmask);
+          const u32 lmr = (A.debug & 1u) ? 0u : (inf.w & 0xFFu);
+          for (u32 r = 0; r < RF; ++r)
+            if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
+        }
+        if (xr)
+          for (u32 q = 0; q < W.xn[w][rr]; ++q) store_log16(reinterpret_cast<uint8_t*>(W.xdst[w][rr][q]) + 16ull * k, v);
       }
     }
     __builtin_amdgcn_wave_barrier();  // the image is rewritten by the wave's next task
-  } else if (ok && j == 1 && dead == 0u) {
+  } else if (ok && j == 1) {
     uint8_t* dst = ring + (pos & segmask);
-    for (u32 r = 0; r < RF; ++r)
-      if ((Z.lm >> r) & 1u) store_log16(dst + r * rstride, h);
+    if (dead == 0u)
+      for (u32 r = 0; r < RF; ++r)
+        if ((Z.lm >> r) & 1u) store_log16(dst + r * rstride, h);
+    if (xr)
+      for (u32 q = 0; q < S.xn[w][r32]; ++q) store_log16(reinterpret_cast<uint8_t*>(S.xdst[w][r32][q]), h);
   }
   if (in && j == 0) b.out_offsets[i] = ok ? off : ~0ull;
   const u32 ilog = st.interval_log2;
@@ -703,22 +835,33 @@ __device__ void partition_apply(const PipeArgs& A, u32 p) {
   // counted by stages 1/2, ranks being per partition, but never applied; the host keeps both state
   // sets equal for it); stage 2 leaves rejected (batch, partition) cells out of totals
   if (!st.is_leader[p]) return;
-  const u64 tot = A.s3.totals[p];
-  const u64 tc = tot >> 40, tb = 16ull * (tot & kLow40);
-  const u64 nleo = A.cur.leo[p] + tc;
-  A.nxt.leo[p] = nleo;
-  A.nxt.used[p] = A.cur.used[p] + tb;
-  if (tc) {
-    const u32 RF = st.RF, lm = st.local_mask[p];
-    u64 row[kMaxRF];
+  u64 tc = 0, leo;
+  if (A.g3.nb) {
+    const u64 tot = A.s3.totals[p];
+    tc = tot >> 40;
+    leo = A.cur.leo[p] + tc;
+    A.nxt.leo[p] = leo;
+    A.nxt.used[p] = A.cur.used[p] + 16ull * (tot & kLow40);
+  } else {
+    leo = A.cur.leo[p];
+  }
+  if (!tc && !A.ackin) return;
+  const u32 RF = st.RF, lm = st.local_mask[p];
+  u64 row[kMaxRF];
 #pragma unroll
-    for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
+  for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
+  bool moved = tc != 0;
+  if (tc) {
 #pragma unroll
     for (u32 r = 0; r < kMaxRF; ++r)
       if (r < RF && ((lm >> r) & 1u)) {
-        row[r] = nleo;
-        st.match[(u64)p * RF + r] = nleo;
+        row[r] = leo;
+        st.match[(u64)p * RF + r] = leo;
       }
+  }
+  // followers' acks of an earlier group (replication transport, FORMAT.md §9)
+  if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row);
+  if (moved) {
     const u64 c = quorum_commit(row, RF, st.commit[p], st.term_start[p]);
     st.commit[p] = c;
     st.hw[p] = c;
@@ -760,6 +903,9 @@ __device__ void partition_retention(const PipeArgs& A, u32 p) {
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
 #define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
+// XR: a replication transport is attached (stage 3 also fills the group's outbox); a separate
+// instantiation so the single-GPU kernel keeps its register budget.
+template <bool XR>
 __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(PipeArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
@@ -790,7 +936,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     // partition threads: stage 3's state advance and stage 4's retention
     PIPE_STAMP(0);
     for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) {
-      if (A.g3.nb) partition_apply(A, p);
+      if (A.g3.nb || A.ackin) partition_apply(A, p);
       if (A.g4.nb) partition_retention(A, p);
     }
     if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -822,7 +968,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   while (task < tasks) {
     uint4 so;
     PIPE_STAMP(2);
-    stage3_finish(A, S, T, R, Z, cand, so);
+    stage3_finish<XR>(A, S, T, R, Z, cand, so);
     if (lane == 0) G.stats[T.jb][task - G.task0[T.jb]] = so;
     PIPE_STAMP(3);
     task += A.wg3 * kPW;
@@ -843,7 +989,10 @@ uint32_t pipeline_wgs_per_cu() { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (kPT / 64
 void launch_pipeline(const PipeArgs& a, hipStream_t s) {
   const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3;
   if (!grid) return;
-  hipLaunchKernelGGL(pipeline_kernel, dim3(grid), dim3(kPT), kSmemBytes, s, a);
+  if (a.outidx)
+    hipLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, a);
+  else
+    hipLaunchKernelGGL(pipeline_kernel<false>, dim3(grid), dim3(kPT), kSmemBytes, s, a);
 }
 
 }  // namespace rmq

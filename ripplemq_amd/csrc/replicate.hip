@@ -1,0 +1,217 @@
+// replicate.hip — the follower side of a replica-log round (FORMAT.md §9).
+//
+// Reference: jraft replicates every partition log to its RF-1 followers with AppendEntries; a
+// follower appends the entries after checking that they continue its log (Raft log matching) and
+// acknowledges the index it now holds, which the leader's BallotBox turns into the commit index
+// (PartitionRaftServer.java:82-93 configures the group; MessageAppendRequestProcessor.java:59 is
+// the Node.apply that starts it). Here a round carries one launch group of the leader's appends
+// for every partition the two ranks share, as one region of the exchange:
+//   ingest_records (wave per 32 records, a lane pair per record, like the append's stage 3):
+//     checks the record continues the follower's log (first offset == follower log end, header
+//     offset == first offset + rank), recomputes its CRC32C from the payload pieces (slicing-by-8
+//     and zero-shift tables in LDS, Horner fold per lane, the pad removed by x^(-8 pad)) against
+//     the header's, and stores the record into the follower's replica ring at the same logical
+//     position the leader used (pieces a later piece of the round overwrites are not stored), plus
+//     the sparse-index entries;
+//   ingest_finish (thread per entry): advances the follower partition's log end (both state sets:
+//     the append pipeline never touches a partition it does not lead), evaluates retention once per
+//     round (FORMAT.md §4 rule) and writes the ack (the follower's log end) for the leader.
+// A refused entry (CRC or log mismatch) leaves the follower's log end where it was.
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "partition_ops.hpp"
+
+namespace rmq {
+
+constexpr u32 kIT = 512;           // threads per ingest workgroup
+constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
+constexpr u32 kIR = 32;            // records per task
+
+struct RegionView {
+  const uint8_t* base;
+  u32 n_entries, n_records;
+  u64 data_off;
+};
+
+__device__ __forceinline__ RegionView region_of(const IngestArgs& A, u32 src) {
+  RegionView v;
+  v.base = A.inbox + A.region[src];
+  const u32* h = reinterpret_cast<const u32*>(v.base);
+  v.n_entries = h[1];
+  v.n_records = h[2];
+  v.data_off = *reinterpret_cast<const u64*>(h + 6);
+  return v;
+}
+
+__device__ __forceinline__ u32 source_of_task(const IngestArgs& A, u32 task) {
+  u32 q = 0;
+  for (u32 k = 1; k < A.world; ++k) q += task >= A.task0[k] ? 1u : 0u;
+  return q;
+}
+
+__global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
+  __shared__ __attribute__((aligned(16))) u32 t8[8][256];
+  __shared__ __attribute__((aligned(16))) u32 z[2][4][256];
+  {
+    static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
+    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+    uint4* d0 = reinterpret_cast<uint4*>(&t8[0][0]);
+    uint4* d1 = reinterpret_cast<uint4*>(&z[0][0][0]);
+    for (u32 k = threadIdx.x; k < sizeof(t8) / 16; k += kIT) d0[k] = src[k];
+    for (u32 k = threadIdx.x; k < sizeof(z) / 16; k += kIT) d1[k] = src[sizeof(t8) / 16 + k];
+  }
+  __syncthreads();
+  const u32 task = __builtin_amdgcn_readfirstlane(blockIdx.x * kIW + (threadIdx.x >> 6));
+  if (task >= A.task0[A.world]) return;
+  const u32 src = source_of_task(A, task);
+  if (!A.rbytes[src]) return;
+  const RegionView R = region_of(A, src);
+  if (R.n_entries != A.xi_start[src + 1] - A.xi_start[src]) return;  // malformed (finish counts it)
+  const u32 lane = threadIdx.x & 63, j = lane & 1u;
+  const u32 i = (task - A.task0[src]) * kIR + (lane >> 1);
+  const bool in = i < R.n_records;
+  const DevState& st = A.st;
+  u32 p = 0, L = 0, m = 0, e = 0;
+  u64 pos = 0, gend = 0, off = 0;
+  bool ok = false, owner = false;
+  const uint8_t* rec = R.base;
+  uint4 hdr = make_uint4(0, 0, 0, 0);
+  if (in) {
+    const u64 tab = *reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries + 8ull * i);
+    const u32 k = min((u32)tab, R.n_entries - 1u), d16 = (u32)(tab >> 32);  // ok below requires k == tab
+    const uint4* de = reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
+    const uint4 d0 = de[0], d1 = de[1];
+    const u32 bytes16 = d0.y, tstart = d1.x, dstart16 = d1.y;
+    const u64 first = ((u64)d0.w << 32) | d0.z;
+    e = A.xi_start[src] + k;
+    p = A.xi_p[e];
+    owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
+    const u64 leo = st.leo[p], used = st.used[p];
+    rec = R.base + R.data_off + 16ull * d16;
+    hdr = *reinterpret_cast<const uint4*>(rec);
+    off = ((u64)hdr.y << 32) | hdr.x;
+    L = hdr.z;
+    m = (L + 15u) >> 4;
+    const u64 rel = 16ull * (d16 - dstart16);
+    pos = used + rel;
+    gend = used + 16ull * bytes16;
+    ok = k == (u32)tab && first == leo && off == first + (i - tstart) && d16 >= dstart16 &&
+         rel + 16ull * (1ull + m) <= 16ull * bytes16;
+    if (!ok && j == 1) atomicOr(&A.bad[e], 2u);  // does not continue the follower's log
+  }
+  // CRC32C of the payload from its 16-byte pieces (zero-padded in the log): lane j folds pieces
+  // j, j + 2, ... by Horner's rule with the 32-byte zero-shift table
+  const u32 mm = ok ? m : 0u;
+  u32 acc = 0;
+  uint8_t* const ring = st.logs + ((u64)(in ? A.xi_slot[e] : 0u) * st.P + p) * st.seg;
+  const u64 segmask = st.seg - 1ull;
+  for (u32 c = 0; __any(c < (mm + 1u) / 2u); ++c) {
+    const u32 jp = 2u * c + j;
+    if (jp < mm) {
+      uint4 v = *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * jp);
+      const u64 x = pos + 16ull + 16ull * jp;
+      if (x + st.seg >= gend) store_log16(ring + (x & segmask), v);
+      if (jp == 0) v.x ^= 0xFFFFFFFFu;
+      acc = crc_zshift(z[1], acc) ^ crc_piece16(t8, v);
+    }
+  }
+  if (ok && mm > j && ((mm - 1u - j) & 1u)) acc = crc_zshift(z[0], acc);
+  acc ^= pair_swap(acc);
+  if (ok && j == 1) {
+    u32 crc = 0;
+    if (L) {
+      const u32 pad = 16u * m - L;
+      crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
+    }
+    ok = crc == hdr.w;
+    if (ok) {
+      if (pos + st.seg >= gend) store_log16(ring + (pos & segmask), hdr);
+      if (owner) {  // sparse index: every multiple of the interval the record crosses names the next record
+        const u32 ilog = st.interval_log2;
+        const u64 end = pos + 16ull * (1ull + m);
+        for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end; ++q) {
+          u64* ie = st.index + ((u64)p * st.icap + q % st.icap) * 2;
+          ie[0] = off + 1;
+          ie[1] = end;
+        }
+      }
+    } else {
+      atomicOr(&A.bad[e], 1u);  // CRC32C differs from the header's
+    }
+  }
+  const u32 n_ok = (u32)__popcll(__ballot(in && ok && j == 1));
+  if (lane == 0 && n_ok) atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)n_ok);
+}
+
+__global__ void ingest_finish_kernel(IngestArgs A) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= A.n_in) return;
+  u32 src = 0;
+  for (u32 q = 1; q < A.world; ++q) src += e >= A.xi_start[q] ? 1u : 0u;
+  const DevState& st = A.st;
+  const u32 p = A.xi_p[e], k = e - A.xi_start[src];
+  const bool owner = k == 0 || A.xi_p[e - 1] != p;
+  u64 ack = st.leo[p];
+  const bool whole = A.rbytes[src] && region_of(A, src).n_entries == A.xi_start[src + 1] - A.xi_start[src];
+  if (A.rbytes[src] && !whole) {
+    ack = 0;
+    if (k == 0) atomicAdd((unsigned long long*)&A.counters[2], 1ull);
+  } else if (A.rbytes[src]) {
+    const RegionView R = region_of(A, src);
+    const uint4 d0 = *reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
+    const u32 count = d0.x, bytes16 = d0.y;
+    const u64 first = ((u64)d0.w << 32) | d0.z;
+    if (count) {
+      const u32 bad = A.bad[e];
+      if (bad) {
+        ack = 0;  // no new information (match only moves up)
+        atomicAdd((unsigned long long*)&A.counters[(bad & 2u) ? 2 : 1], 1ull);
+        A.bad[e] = 0u;
+      } else {
+        ack = first + count;
+        if (owner) {
+          const u64 used = st.used[p] + 16ull * bytes16;
+          for (u32 s = 0; s < 2; ++s) {
+            A.sets[s].leo[p] = ack;
+            A.sets[s].used[p] = used;
+          }
+          // retention once per round (FORMAT.md §4 rule on the follower's log)
+          if (used - st.start_pos[p] > st.seg) {
+            const u64 ms = (used - st.seg + (1ull << st.interval_log2) - 1) >> st.interval_log2;
+            const u64* ie = st.index + ((u64)p * st.icap + ms % st.icap) * 2;
+            st.start_off[p] = ie[0];
+            st.start_pos[p] = ie[1];
+          }
+          atomicAdd((unsigned long long*)&A.counters[3], 16ull * bytes16);
+        }
+      }
+    }
+  }
+  A.ackout[e] = ack;
+}
+
+// Acks of one round applied after the pipeline has drained (thread per partition).
+__global__ void ack_apply_kernel(AckApplyArgs a) {
+  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  const DevState& st = a.st;
+  if (p >= st.P || !st.is_leader[p]) return;
+  u64 row[kMaxRF];
+#pragma unroll
+  for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < st.RF ? st.match[(u64)p * st.RF + r] : 0ull;
+  if (apply_acks(st, p, a.outidx, a.ackin, st.leo[p], row)) {
+    const u64 c = quorum_commit(row, st.RF, st.commit[p], st.term_start[p]);
+    st.commit[p] = c;
+    st.hw[p] = c;
+  }
+}
+
+void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s) {
+  if (tasks) hipLaunchKernelGGL(ingest_records_kernel, dim3((tasks + kIW - 1) / kIW), dim3(kIT), 0, s, a);
+  if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
+}
+
+void launch_ack_apply(const AckApplyArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(ack_apply_kernel, dim3((a.st.P + 255) / 256), dim3(256), 0, s, a);
+}
+
+}  // namespace rmq

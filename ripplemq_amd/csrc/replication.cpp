@@ -1,0 +1,415 @@
+// replication.cpp — replica-log rounds between engines over a Transport (FORMAT.md §9).
+//
+// Reference: each partition is a jraft group whose leader replicates its log to RF-1 followers
+// with AppendEntries and commits on a quorum of acks (BallotBox) — configured in
+// PartitionRaftServer.java:82-93 (peers of the group), started by node.apply at
+// MessageAppendRequestProcessor.java:59; replicas are spread over brokers by
+// PartitionAssigner.java:25-94. Here one engine per GPU leads some partitions and follows others
+// (rmq_set_placement); every launch group of appends is one round:
+//
+//   launch k+1 (stage 2 of group g): the last stage-2 workgroup plans g's outbox (pipeline.hip);
+//       after it, the exchange stream swaps {region bytes, records} with every peer;
+//   launch k+2 (stage 3 of g): records also go, once per remote slot, into g's outbox;
+//   after launch k+3 is issued: the host reads g's sizes (exchanged one launch earlier) and posts
+//       on the exchange stream, behind launch k+2: the grouped send/recv of the regions, the
+//       follower ingest (CRC32C check, ring + index writes, log end, retention; replicate.hip) and
+//       the grouped send/recv of the acks (follower log ends);
+//   launch k+5 (three launches after g's stage 3): waits for g's exchange and applies the acks to
+//       the matchIndex rows in its partition threads, then the quorum commit rule.
+//
+// Every rank makes the same calls in the same order (rounds are collective, like the launches
+// that drive them): with a transport attached, launch groups close only when full, and control
+// calls that flush (rmq_sync, placement, leadership) are collective. At a drain the remaining
+// rounds are exchanged and their acks applied by a separate kernel.
+#include <numeric>
+
+#include "engine_internal.hpp"
+
+namespace rmq {
+
+namespace {
+
+template <typename T>
+int upload(T** d, const std::vector<T>& h) {
+  if (*d) hipFree(*d);
+  *d = nullptr;
+  int rc = dalloc(d, h.size());
+  if (rc || h.empty()) return rc;
+  HIP_TRY(hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return RMQ_OK;
+}
+
+struct Entry {
+  uint64_t key;
+  uint32_t slot, p;
+  bool operator<(const Entry& o) const { return key != o.key ? key < o.key : slot < o.slot; }
+};
+
+uint64_t entry_hash(uint64_t key, uint32_t slot) { return key * RMQ_MAX_RF + slot; }
+
+void free_set_buffers(Replication* r) {
+  for (XchgSet& x : r->sets) {
+    void* bufs[] = {x.outbox, x.inbox, x.xe, x.sizes, x.ackout, x.ackin};
+    for (void* p : bufs)
+      if (p) hipFree(p);
+    x.outbox = x.inbox = nullptr;
+    x.xe = nullptr;
+    x.sizes = x.ackout = x.ackin = nullptr;
+  }
+}
+
+// Post the {region bytes, records} swap of the group in set s (after its stage-2 launch).
+int post_sizes(rmq_engine* e, uint32_t s) {
+  Replication* r = e->repl;
+  XchgSet& x = r->sets[s];
+  const uint32_t W = r->world;
+  void* sb[kMaxWorld];
+  void* rb[kMaxWorld];
+  uint64_t n16[kMaxWorld];
+  for (uint32_t q = 0; q < W; ++q) {
+    sb[q] = x.sizes + 2 * q;
+    rb[q] = x.sizes + 2 * W + 2 * q;
+    n16[q] = q == r->rank ? 0 : 16;
+  }
+  HIP_TRY(hipStreamWaitEvent(r->xchg_s, x.ev_s2, 0));
+  int rc = r->xport->exchange(sb, n16, rb, n16, r->xchg_s);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(x.h_sizes, x.sizes, 4ull * W * 8, hipMemcpyDeviceToHost, r->xchg_s));
+  HIP_TRY(hipEventRecord(x.ev_sz, r->xchg_s));
+  return RMQ_OK;
+}
+
+// Post the round of the group in set s (applied already): regions, follower ingest, acks.
+int post_round(rmq_engine* e, uint32_t s) {
+  Replication* r = e->repl;
+  XchgSet& x = r->sets[s];
+  const uint32_t W = r->world, me = r->rank;
+  HIP_TRY(hipEventSynchronize(x.ev_sz));
+  const uint64_t* hs = x.h_sizes;  // [q]: {send bytes, send records}, then [W + q]: {recv bytes, recv records}
+  void* sb[kMaxWorld];
+  void* rb[kMaxWorld];
+  uint64_t sn[kMaxWorld], rn[kMaxWorld];
+  IngestArgs a{};
+  uint64_t so = 0, ro = 0;
+  uint32_t tasks = 0;
+  for (uint32_t q = 0; q < W; ++q) {
+    sn[q] = q == me ? 0 : hs[2 * q];
+    rn[q] = q == me ? 0 : hs[2 * W + 2 * q];
+    sb[q] = x.outbox + so;
+    rb[q] = x.inbox + ro;
+    a.region[q] = ro;
+    a.rbytes[q] = rn[q];
+    a.task0[q] = tasks;
+    tasks += (uint32_t)((rn[q] ? hs[2 * W + 2 * q + 1] : 0) + 31) / 32;
+    so += sn[q];
+    ro += rn[q];
+  }
+  a.task0[W] = tasks;
+  if (so > r->out_cap || ro > r->in_cap) {
+    std::fprintf(stderr, "ripplemq: replication round exceeds its buffers (%llu/%llu out, %llu/%llu in)\n",
+                 (unsigned long long)so, (unsigned long long)r->out_cap, (unsigned long long)ro,
+                 (unsigned long long)r->in_cap);
+    return RMQ_EDEVICE;
+  }
+  HIP_TRY(hipStreamWaitEvent(r->xchg_s, x.ev_s3, 0));
+  int rc = r->xport->exchange(sb, sn, rb, rn, r->xchg_s);
+  if (rc) return rc;
+  a.st = e->st;
+  a.sets[0] = e->sets[0];
+  a.sets[1] = e->sets[1];
+  a.inbox = x.inbox;
+  a.xi_p = r->d_xi_p;
+  a.xi_slot = r->d_xi_slot;
+  a.xi_start = r->d_xi_start;
+  a.world = W;
+  a.rank = me;
+  a.n_in = (uint32_t)r->xi_p.size();
+  a.bad = r->d_bad;
+  a.ackout = x.ackout;
+  a.crc = e->d_crc;
+  a.counters = r->d_counters;
+  launch_ingest(a, tasks, r->xchg_s);
+  HIP_TRY(hipGetLastError());
+  // acks: the follower log end of every in entry back to its leader, fixed sizes both ways
+  for (uint32_t q = 0; q < W; ++q) {
+    sn[q] = q == me ? 0 : 8ull * (r->xi_start[q + 1] - r->xi_start[q]);
+    rn[q] = q == me ? 0 : 8ull * (r->xo_start[q + 1] - r->xo_start[q]);
+    sb[q] = x.ackout + r->xi_start[q];
+    rb[q] = x.ackin + r->xo_start[q];
+  }
+  rc = r->xport->exchange(sb, sn, rb, rn, r->xchg_s);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(x.ev_x, r->xchg_s));
+  r->rounds++;
+  r->bytes_sent += so;
+  r->bytes_recv += ro;
+  r->last_set = s;
+  r->acking.push_back(s);
+  return RMQ_OK;
+}
+
+}  // namespace
+
+int repl_attach(rmq_engine* e, Transport* t) {
+  if (e->repl) return RMQ_EINVAL;
+  if (t->world() > kMaxWorld || t->rank() != e->cfg.rank || t->world() <= e->cfg.rank) return RMQ_EINVAL;
+  // groups must close by count alone so every rank forms the same rounds
+  if (e->group_max * e->max_tiles > kMaxTiles) return RMQ_EINVAL;
+  Replication* r = new (std::nothrow) Replication();
+  if (!r) return RMQ_ENOMEM;
+  r->xport = t;
+  r->world = t->world();
+  r->rank = t->rank();
+  e->repl = r;
+  HIP_TRY(hipStreamCreateWithFlags(&r->xchg_s, hipStreamNonBlocking));
+  for (XchgSet& x : r->sets) {
+    HIP_TRY(hipEventCreateWithFlags(&x.ev_s2, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&x.ev_s3, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&x.ev_sz, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&x.ev_x, hipEventDisableTiming));
+    int rc = dalloc(&x.count, 1);
+    if (rc) return rc;
+    HIP_TRY(hipHostMalloc((void**)&x.h_sizes, 4ull * kMaxWorld * 8, 0));
+  }
+  int rc = dalloc(&r->d_counters, 4);
+  if (rc) return rc;
+  return repl_set_lists(e);
+}
+
+void repl_free(rmq_engine* e) {
+  Replication* r = e->repl;
+  if (!r) return;
+  if (r->xchg_s) hipStreamSynchronize(r->xchg_s);
+  free_set_buffers(r);
+  for (XchgSet& x : r->sets) {
+    hipEvent_t evs[] = {x.ev_s2, x.ev_s3, x.ev_sz, x.ev_x};
+    for (hipEvent_t v : evs)
+      if (v) hipEventDestroy(v);
+    if (x.count) hipFree(x.count);
+    if (x.h_sizes) hipHostFree(x.h_sizes);
+  }
+  void* bufs[] = {r->d_xo_p, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot, r->d_xi_start,
+                  r->d_bad, r->d_counters};
+  for (void* p : bufs)
+    if (p) hipFree(p);
+  if (r->xchg_s) hipStreamDestroy(r->xchg_s);
+  delete r->xport;
+  delete r;
+  e->repl = nullptr;
+}
+
+// Out / in lists from the placement, the collective consistency check, and the round buffers.
+// Called with the engine drained, by every rank.
+int repl_set_lists(rmq_engine* e) {
+  Replication* r = e->repl;
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor, W = r->world, me = r->rank;
+  std::vector<std::vector<Entry>> out(W), in(W);
+  int bad = RMQ_OK;
+  for (uint32_t p = 0; p < P; ++p) {
+    const uint32_t* rk = &e->ranks[(size_t)p * RF];
+    const uint32_t lead = rk[e->leader_slot[p]];
+    uint32_t remote = 0;
+    for (uint32_t s = 0; s < RF; ++s) {
+      if (rk[s] >= W) bad = RMQ_EINVAL;
+      else if (lead == me && rk[s] != me) {
+        out[rk[s]].push_back({e->key[p], s, p});
+        ++remote;
+      } else if (lead != me && rk[s] == me && lead < W) {
+        in[lead].push_back({e->key[p], s, p});
+      }
+    }
+    if (remote > kMaxRemote) bad = RMQ_EINVAL;
+  }
+  r->xo_p.clear();
+  r->xo_slot.clear();
+  r->xi_p.clear();
+  r->xi_slot.clear();
+  r->xo_start.assign(W + 1, 0);
+  r->xi_start.assign(W + 1, 0);
+  r->keysum.assign(W, 0);
+  std::vector<uint64_t> keysum_in(W, 0);
+  std::vector<uint32_t> outidx((size_t)P * RF, ~0u);
+  for (uint32_t q = 0; q < W; ++q) {
+    std::sort(out[q].begin(), out[q].end());
+    std::sort(in[q].begin(), in[q].end());
+    r->xo_start[q] = (uint32_t)r->xo_p.size();
+    for (const Entry& x : out[q]) {
+      outidx[(size_t)x.p * RF + x.slot] = (uint32_t)r->xo_p.size();
+      r->xo_p.push_back(x.p);
+      r->xo_slot.push_back(x.slot);
+      r->keysum[q] += entry_hash(x.key, x.slot);
+    }
+    r->xi_start[q] = (uint32_t)r->xi_p.size();
+    for (const Entry& x : in[q]) {
+      r->xi_p.push_back(x.p);
+      r->xi_slot.push_back(x.slot);
+      keysum_in[q] += entry_hash(x.key, x.slot);
+    }
+  }
+  r->xo_start[W] = (uint32_t)r->xo_p.size();
+  r->xi_start[W] = (uint32_t)r->xi_p.size();
+  // handshake: what I send to q must be what q expects from me, and every rank learns whether all
+  // pairs agree (two exchanges, so no rank starts rounds that another refuses)
+  {
+    std::vector<uint64_t> h(8ull * W, 0);  // [q]: send {entries, keysum}; [W + q]: recv; [2W..] verdicts
+    for (uint32_t q = 0; q < W; ++q) {
+      h[2 * q] = r->xo_start[q + 1] - r->xo_start[q];
+      h[2 * q + 1] = r->keysum[q];
+    }
+    uint64_t* d = nullptr;
+    int rc = dalloc(&d, h.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+    void* sb[kMaxWorld];
+    void* rb[kMaxWorld];
+    uint64_t n[kMaxWorld];
+    for (uint32_t q = 0; q < W; ++q) {
+      sb[q] = d + 2 * q;
+      rb[q] = d + 2 * W + 2 * q;
+      n[q] = q == me ? 0 : 16;
+    }
+    rc = r->xport->exchange(sb, n, rb, n, r->xchg_s);
+    if (!rc) rc = hip_fail(hipStreamSynchronize(r->xchg_s));
+    if (!rc) rc = hip_fail(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t verdict = bad ? 1 : 0;
+    for (uint32_t q = 0; q < W && !rc; ++q)
+      if (q != me && (h[2 * W + 2 * q] != r->xi_start[q + 1] - r->xi_start[q] || h[2 * W + 2 * q + 1] != keysum_in[q]))
+        verdict = 1;
+    for (uint32_t q = 0; q < W; ++q) h[4 * W + q] = verdict;
+    if (!rc) rc = hip_fail(hipMemcpy(d + 4 * W, h.data() + 4 * W, 8ull * W, hipMemcpyHostToDevice));
+    for (uint32_t q = 0; q < W; ++q) {
+      sb[q] = d + 4 * W + q;
+      rb[q] = d + 5 * W + q;
+      n[q] = q == me ? 0 : 8;
+    }
+    if (!rc) rc = r->xport->exchange(sb, n, rb, n, r->xchg_s);
+    if (!rc) rc = hip_fail(hipStreamSynchronize(r->xchg_s));
+    if (!rc) rc = hip_fail(hipMemcpy(h.data() + 5 * W, d + 5 * W, 8ull * W, hipMemcpyDeviceToHost));
+    hipFree(d);
+    if (rc) return rc;
+    for (uint32_t q = 0; q < W; ++q) verdict |= q != me ? h[5 * W + q] : 0;
+    if (verdict) {
+      std::fprintf(stderr, "ripplemq: replica placement differs between ranks (rank %u)\n", me);
+      return RMQ_EINVAL;
+    }
+  }
+  int rc = upload(&r->d_xo_p, r->xo_p);
+  if (!rc) rc = upload(&r->d_xo_start, r->xo_start);
+  if (!rc) rc = upload(&r->d_keysum, r->keysum);
+  if (!rc) rc = upload(&r->d_outidx, outidx);
+  if (!rc) rc = upload(&r->d_xi_p, r->xi_p);
+  if (!rc) rc = upload(&r->d_xi_slot, r->xi_slot);
+  if (!rc) rc = upload(&r->d_xi_start, r->xi_start);
+  if (!rc) rc = upload(&r->d_bad, std::vector<uint32_t>(r->xi_p.size(), 0u));
+  if (rc) return rc;
+  // round buffers (FORMAT.md §9 bounds): a record is at most 31 + L bytes in the log, sent once per
+  // remote slot, plus an 8-byte table slot; per region a header, a directory and table padding
+  const uint64_t G = e->group_max, NR = e->cfg.max_batch_records, MB = e->cfg.max_batch_bytes;
+  const uint64_t rec = G * (39ull * NR + MB);
+  uint32_t max_remote = 0;
+  for (uint32_t p = 0; p < P; ++p) {
+    uint32_t k = 0;
+    for (uint32_t s = 0; s < RF; ++s) k += outidx[(size_t)p * RF + s] != ~0u;
+    max_remote = std::max(max_remote, k);
+  }
+  r->out_cap = (uint64_t)max_remote * rec + 48ull * W + 32ull * r->xo_p.size();
+  r->in_cap = (uint64_t)(W - 1) * (RF - 1) * rec + 48ull * W + 32ull * r->xi_p.size();
+  free_set_buffers(r);
+  for (XchgSet& x : r->sets) {
+    rc = dalloc(&x.outbox, r->out_cap);
+    if (!rc) rc = dalloc(&x.inbox, r->in_cap);
+    if (!rc) rc = dalloc(&x.xe, std::max<size_t>(1, r->xo_p.size()));
+    if (!rc) rc = dalloc(&x.sizes, 4ull * W);
+    if (!rc) rc = dalloc(&x.ackout, std::max<size_t>(1, r->xi_p.size()));
+    if (!rc) rc = dalloc(&x.ackin, std::max<size_t>(1, r->xo_p.size()));
+    if (rc) return rc;
+  }
+  return RMQ_OK;
+}
+
+void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const GroupFlight* s3) {
+  Replication* r = e->repl;
+  if (!r || r->xo_p.empty()) return;  // nothing led here has a remote replica
+  a.outidx = r->d_outidx;
+  if (s2) {
+    XchgSet& x = r->sets[s2->set];
+    a.xp2.xo_p = r->d_xo_p;
+    a.xp2.xo_start = r->d_xo_start;
+    a.xp2.keysum = r->d_keysum;
+    a.xp2.world = r->world;
+    a.xp2.rank = r->rank;
+    a.xp2.n_out = (uint32_t)r->xo_p.size();
+    a.xp2.count = x.count;
+    a.xp2.xe = x.xe;
+    a.xp2.outbox = x.outbox;
+    a.xp2.sizes = x.sizes;
+  }
+  if (s3) {
+    a.xe3 = r->sets[s3->set].xe;
+    a.outbox3 = r->sets[s3->set].outbox;
+  }
+}
+
+// Before issuing launch launch_seq + 1: the acks of the group applied three launches earlier.
+int repl_before_launch(rmq_engine* e, PipeArgs& a) {
+  Replication* r = e->repl;
+  if (!r || r->acking.empty()) return RMQ_OK;
+  const uint32_t s = r->acking.front();
+  if (r->sets[s].applied_launch + 3 > e->launch_seq + 1) return RMQ_OK;
+  HIP_TRY(hipStreamWaitEvent(e->main_s, r->sets[s].ev_x, 0));
+  if (!r->xo_p.empty()) a.ackin = r->sets[s].ackin;
+  r->acking.pop_front();
+  return RMQ_OK;
+}
+
+// After launch launch_seq: post the size swap of its stage-2 group and the rounds of the groups
+// applied by earlier launches.
+int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s3) {
+  Replication* r = e->repl;
+  if (!r) return RMQ_OK;
+  if (s2) {
+    HIP_TRY(hipEventRecord(r->sets[s2->set].ev_s2, e->main_s));
+    int rc = post_sizes(e, s2->set);
+    if (rc) return rc;
+  }
+  while (!r->sized.empty() && r->sets[r->sized.front()].applied_launch < e->launch_seq) {
+    int rc = post_round(e, r->sized.front());
+    if (rc) return rc;
+    r->sized.pop_front();
+  }
+  if (s3) {
+    XchgSet& x = r->sets[s3->set];
+    HIP_TRY(hipEventRecord(x.ev_s3, e->main_s));
+    x.applied_launch = e->launch_seq;
+    r->sized.push_back(s3->set);
+  }
+  return RMQ_OK;
+}
+
+// After the pipeline is flushed: post the remaining rounds and apply their acks.
+int repl_drain(rmq_engine* e) {
+  Replication* r = e->repl;
+  if (!r) return RMQ_OK;
+  while (!r->sized.empty()) {
+    int rc = post_round(e, r->sized.front());
+    if (rc) return rc;
+    r->sized.pop_front();
+  }
+  while (!r->acking.empty()) {
+    XchgSet& x = r->sets[r->acking.front()];
+    HIP_TRY(hipStreamWaitEvent(e->main_s, x.ev_x, 0));
+    if (!r->xo_p.empty()) {
+      AckApplyArgs a{};
+      a.st = e->st;
+      a.outidx = r->d_outidx;
+      a.ackin = x.ackin;
+      launch_ack_apply(a, e->main_s);
+      HIP_TRY(hipGetLastError());
+    }
+    r->acking.pop_front();
+  }
+  HIP_TRY(hipStreamSynchronize(r->xchg_s));
+  return RMQ_OK;
+}
+
+}  // namespace rmq

@@ -95,6 +95,34 @@ class Engine:
         r = (C.c_uint32 * len(ranks))(*ranks)
         _check(self.lib.rmq_set_replicas(self.h, pidx, r, len(ranks), leader_slot), "rmq_set_replicas")
 
+    def set_placement(self, pidx, keys, ranks, leader_slot) -> None:
+        """rmq_set_placement: ranks is [n][RF]; keys may be None (unchanged)."""
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        ranks = np.ascontiguousarray(ranks, np.uint32).reshape(len(pidx), self.cfg.replication_factor)
+        leader_slot = np.ascontiguousarray(leader_slot, np.uint32)
+        keys = None if keys is None else np.ascontiguousarray(keys, np.uint64)
+        _check(self.lib.rmq_set_placement(self.h, len(pidx), _ptr(pidx), _ptr(keys), _ptr(ranks), _ptr(leader_slot)),
+               "rmq_set_placement")
+
+    def attach_local(self, hub: "LocalHub") -> None:
+        _check(self.lib.rmq_attach_local(self.h, hub.h), "rmq_attach_local")
+
+    def attach_rccl(self, comm_id: bytes, world: int) -> None:
+        buf = (C.c_uint8 * 128).from_buffer_copy(comm_id)
+        _check(self.lib.rmq_attach_rccl(self.h, buf, world), "rmq_attach_rccl")
+
+    def replication_stats(self) -> dict:
+        st = A.RmqReplStats()
+        _check(self.lib.rmq_replication_stats(self.h, C.byref(st)), "rmq_replication_stats")
+        return {f: int(getattr(st, f)) for f, _ in A.RmqReplStats._fields_}
+
+    def read_outbox(self, dst: int) -> np.ndarray:
+        n = C.c_uint64()
+        _check(self.lib.rmq_read_outbox(self.h, dst, None, 0, C.byref(n)), "rmq_read_outbox")
+        out = np.zeros(max(int(n.value), 1), np.uint8)
+        _check(self.lib.rmq_read_outbox(self.h, dst, _ptr(out), out.size, C.byref(n)), "rmq_read_outbox")
+        return out[:int(n.value)]
+
     def become_leader(self, pidx: int, term: int) -> None:
         _check(self.lib.rmq_become_leader(self.h, pidx, term), "rmq_become_leader")
 
@@ -250,6 +278,27 @@ class Engine:
         cu = C.c_uint32()
         _check(self.lib.rmq_device_info(self.h, buf, 256, C.byref(cu)), "rmq_device_info")
         return buf.value.decode(), int(cu.value)
+
+
+class LocalHub:
+    """rmq_local_hub: in-process transport for `world` engines, each driven by its own thread."""
+
+    def __init__(self, world: int, lib_path: str | None = None):
+        self.lib = A.load(lib_path) if lib_path else A.load()
+        h = C.c_void_p()
+        _check(self.lib.rmq_local_hub_create(world, C.byref(h)), "rmq_local_hub_create")
+        self.h = h
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            self.lib.rmq_local_hub_destroy(self.h)
+            self.h = None
+
+
+def rccl_unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    _check(A.load().rmq_rccl_unique_id(buf), "rmq_rccl_unique_id")
+    return bytes(buf)
 
 
 def parse_records(buf: np.ndarray) -> list[tuple[int, int, bytes]]:

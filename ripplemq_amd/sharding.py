@@ -59,6 +59,44 @@ def merge_offsets(n: int, shards: list[Shard], shard_offsets: list[np.ndarray]) 
     return out
 
 
+def replica_ranks(leader: int, gp: int, world: int, rf: int) -> list[int]:
+    """Replica ranks of global partition gp led by `leader` (slot 0 = the leader): follower j on
+    (leader + 1 + ((gp + j * s) mod (world - 1))) mod world, s = max(1, (world - 1) // (rf - 1)), so
+    every GPU's follower traffic spreads over all its xGMI peers; the intent of the
+    reference's least-loaded replica spread (PartitionAssigner.java:81-89). With world = 2 both
+    followers of an RF-3 partition sit on the other GPU (two replica slots there)."""
+    if world == 1:
+        return [leader] * rf
+    s = max(1, (world - 1) // max(1, rf - 1))
+    return [leader] + [(leader + 1 + ((gp + j * s) % (world - 1))) % world for j in range(1, rf)]
+
+
+@dataclass
+class RankView:
+    """One rank's engine partitions: local pidx -> global partition (its placement key)."""
+    rank: int
+    gp: np.ndarray           # u64 [P_local] global partition of each local pidx
+    ranks: np.ndarray        # u32 [P_local][rf]
+    leader_slot: np.ndarray  # u32 [P_local]
+    led: int                 # local pidx [0, led) are the partitions this rank leads
+
+
+def rank_view(rank: int, world: int, parts_per_rank: int, rf: int) -> RankView:
+    """Rank g leads global partitions [g * parts_per_rank, (g + 1) * parts_per_rank) as local pidx
+    [0, parts_per_rank); the partitions it follows come after, ascending by global id."""
+    led = list(range(rank * parts_per_rank, (rank + 1) * parts_per_rank))
+    followed = []
+    for g in range(world):
+        if g == rank:
+            continue
+        for gp in range(g * parts_per_rank, (g + 1) * parts_per_rank):
+            if rank in replica_ranks(g, gp, world, rf)[1:]:
+                followed.append(gp)
+    gps = np.array(led + sorted(followed), np.uint64)
+    rk = np.array([replica_ranks(int(gp) // parts_per_rank, int(gp), world, rf) for gp in gps], np.uint32)
+    return RankView(rank, gps, rk.reshape(len(gps), rf), np.zeros(len(gps), np.uint32), len(led))
+
+
 def max_over_ranks(value: float, dist=None) -> float:
     """Max of a host-side scalar over the process group (the bench's timed-region rule); identity
     without a group. Uses the group's own backend (gloo on CPU)."""

@@ -76,3 +76,47 @@ def test_gloo_two_ranks_match_single_engine(oracle_mod, tmp_path):
                 for rep in range(3):
                     ring = one.read_segment(rep, r * p_local + p).tobytes()
                     assert ranks[r]["rings"][rep][p] == oracle_mod.crc32c(ring)
+
+
+def test_gloo_two_ranks_replication_rounds(oracle_mod, tmp_path):
+    # the replica-log round protocol (FORMAT.md §9) between two rank processes over gloo equals the
+    # in-process simulation of the same rounds (tests/repl_sim.py), rank by rank
+    from repl_sim import exchange_round, place, rank_batches, rank_cfg
+    from ripplemq_amd.sharding import rank_view
+
+    world, ppr, rounds, group = 2, 6, 3, 2
+    out = tmp_path / "repl.json"
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_repl_worker.py"), str(out),
+                                       str(ppr), str(rounds), str(group)], env=env))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    got = json.loads(out.read_text())
+    base = EngineConfig(num_partitions=1, replication_factor=3, segment_bytes=1 << 16, index_interval=256)
+    views = [rank_view(r, world, ppr, 3) for r in range(world)]
+    spec = StreamSpec(ppr, 500, "zipf", size=(0, 120), config_index=71)
+    oras = [oracle_mod.OracleEngine(rank_cfg(base, views[r], r)) for r in range(world)]
+    try:
+        for r in range(world):
+            place(oras[r], views[r], world)
+        batches = [rank_batches(spec, r, rounds, group) for r in range(world)]
+        for k in range(rounds):
+            for r in range(world):
+                for b in batches[r][k * group:(k + 1) * group]:
+                    oras[r].append(b.pidx, b.lens, b.payload)
+            exchange_round(oras)
+        for r in range(world):
+            assert got[r]["rank"] == r
+            for p in range(len(views[r].gp)):
+                assert got[r]["states"][p] == oras[r].state(p)
+                assert got[r]["rings"][p] == [oracle_mod.crc32c(oras[r].read_segment(s, p).tobytes())
+                                              for s in range(3)]
+        leaders = [oras[r].state(p) for r in range(world) for p in range(views[r].led)]
+        assert all(s["commit"] == s["log_end_offset"] > 0 for s in leaders if s["log_end_offset"])
+    finally:
+        for o in oras:
+            o.close()
