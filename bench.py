@@ -9,10 +9,14 @@ retention. Inputs are resident in HBM before timing (a pool of distinct batches 
 256 MiB Infinity Cache, so payload reads come from HBM). The engine applies the batches in launch
 groups of --group (cfg.pipeline_depth); every batch keeps its own semantics.
 
-Multi-GPU: one process per GPU (torch.distributed.run); partitions shard by GPU (4096 per GPU,
-config C's layout) with no data-path collective -> weak scaling. The barrier and the max-over-
-ranks of the timed region use torch.distributed over gloo (host side); the engine itself never
-touches torch.
+Multi-GPU (config C's layout, configs[3]): one process per GPU (torch.distributed.run, or this
+script spawning its ranks); GPU g leads 4096 partitions (global ids [4096 g, 4096 (g + 1))) and holds
+the RF - 1 = 2 follower replicas of other GPUs' partitions, spread over all its peers
+(ripplemq_amd.sharding.replica_ranks). Each launch group of appends is one replication round over
+RCCL (xGMI): grouped send/recv of the round's records to the followers, CRC-checking follower
+ingest, acks back into the leaders' matchIndex rows (FORMAT.md §9) -> weak scaling, records counted
+once they are committed on a quorum. torch.distributed (gloo) is used only for the host barrier, the
+max-over-ranks of the timed region and handing rank 0's RCCL id to the others.
 
 roofline: achieved = algorithmic bytes per launch / mean launch duration = algorithmic bytes of
 the batches applied in the timed region / the region's time between HIP events recorded on the
@@ -29,6 +33,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import numpy as np
@@ -37,11 +42,12 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
-from ripplemq_amd.engine import Engine, EngineConfig  # noqa: E402
-from ripplemq_amd.sharding import max_over_ranks  # noqa: E402
+from ripplemq_amd.engine import Engine, EngineConfig, rccl_unique_id  # noqa: E402
+from ripplemq_amd.sharding import max_over_ranks, rank_view  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0  # one xGMI link, one direction; 7 per GPU in an 8-GPU node
 
 
 def algorithmic_bytes(n: int, L: int, rf: int, P: int) -> int:
@@ -157,54 +163,94 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     return out
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
-    ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
-    ap.add_argument("--segment-mb", type=int, default=16,
-                    help="ring bytes per (replica, partition); a 64k x 128 B batch needs > 8 MiB")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
-    ap.add_argument("--group", type=int, default=4,
-                    help="batches per pipeline launch group (cfg.pipeline_depth, 1..8)")
-    args = ap.parse_args()
+class SoloGroup:
+    """One rank: the identity group."""
+    world = 1
+    rank = 0
 
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # no launcher: start one rank process per GPU ourselves, before this process touches HIP
-        with socket.socket() as so:
-            so.bind(("127.0.0.1", 0))
-            port = so.getsockname()[1]
-        procs = []
-        for r in range(args.gpus):
-            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                       LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-        rcs = [p.wait() for p in procs]
-        sys.exit(next((rc for rc in rcs if rc), 0))
+    def barrier(self):
+        pass
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the line would misreport n_gpus")
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # host-side barrier / max only (gloo)
+    def max(self, x: float) -> float:
+        return float(x)
 
-        dist.init_process_group("gloo")
+    def bcast(self, obj):
+        return obj
 
+
+class DistGroup:
+    """One process per GPU: host barrier / max / broadcast over torch.distributed (gloo)."""
+
+    def __init__(self, dist):
+        self.dist = dist
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+
+    def barrier(self):
+        self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        return max_over_ranks(x, self.dist)
+
+    def bcast(self, obj):
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=0)
+        return box[0]
+
+
+class ThreadGroup:
+    """Ranks as threads of one process (--transport local: engines on one GPU, in-process hub)."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.bar = threading.Barrier(world)
+        self.slots = [None] * world
+
+    def view(self, rank: int):
+        g = self
+
+        class _Rank:
+            world = g.world
+
+            def __init__(self):
+                self.rank = rank
+
+            def barrier(self):
+                g.bar.wait()
+
+            def max(self, x: float) -> float:
+                g.slots[rank] = float(x)
+                g.bar.wait()
+                m = max(g.slots)
+                g.bar.wait()
+                return m
+
+            def bcast(self, obj):
+                if rank == 0:
+                    g.slots[0] = obj
+                g.bar.wait()
+                v = g.slots[0]
+                g.bar.wait()
+                return v
+
+        return _Rank()
+
+
+def run_rank(args, grp, device: int, attach) -> dict | None:
+    """One rank's engine, resident input pool, timed region and (rank 0) the JSON line."""
+    rank, world = grp.rank, grp.world
     spec = CONFIGS[args.config]
     rf = 3
     L = spec.size if isinstance(spec.size, int) else None
-    cfg = EngineConfig(num_partitions=spec.partitions, replication_factor=rf,
-                       segment_bytes=args.segment_mb << 20, index_interval=1024,
-                       max_batch_records=spec.records, max_batch_bytes=64 << 20,
-                       pipeline_depth=args.group, device=local_rank, rank=0)
+    seg_mb = args.segment_mb or (16 if world == 1 else 4)
+    view = rank_view(rank, world, spec.partitions, rf)  # world 1: every replica on this GPU
+    cfg = EngineConfig(num_partitions=len(view.gp), replication_factor=rf,
+                       segment_bytes=seg_mb << 20, index_interval=1024,
+                       max_batch_records=spec.records, max_batch_bytes=8 << 20,
+                       pipeline_depth=args.group, device=device, rank=rank)
     eng = Engine(cfg)
+    if world > 1:
+        attach(eng, grp)
+        eng.set_placement(np.arange(len(view.gp), dtype=np.uint32), view.gp, view.ranks, view.leader_slot)
     dev_name, cus = eng.device_info()
 
     # resident input pool: distinct batches per rank (rank-salted stream keys)
@@ -225,28 +271,36 @@ def main() -> None:
         return eng.append_device(n, dp, dl, dpay, pb, d_out[k % len(d_out)])
 
     def barrier():
-        eng.sync()
-        if dist is not None:
-            dist.barrier()
+        eng.sync()  # collective with a transport: every rank flushes the same rounds
+        grp.barrier()
 
     for k in range(args.warmup):
         step(k)
     barrier()
     eng.profile(True)  # HIP events bracket the timed region's launches on the engine's stream
+    x0 = eng.replication_stats()
     t0 = time.perf_counter()
     last = 0
     for k in range(args.steps):
         last = step(args.warmup + k)
     barrier()
     elapsed = time.perf_counter() - t0
+    x1 = eng.replication_stats()
     n_launch, region_ms = eng.profile_query(0)
     n_applied, _ = eng.profile_query(1)
     st = eng.wait(last) if last else {}
     if st and st.get("appended") != spec.records:
         raise SystemExit(f"bench: last batch not fully appended ({st}); the measurement would be void")
     eng.profile(False)
+    committed = int(eng.commit_snapshot()[:view.led].sum(dtype=np.uint64))
+    if committed != spec.records * (args.warmup + args.steps):
+        raise SystemExit(f"bench: {committed} records committed of {spec.records * (args.warmup + args.steps)} "
+                         "appended; the measurement would be void")
 
-    t_max = max_over_ranks(elapsed, dist)
+    t_max = grp.max(elapsed)
+    sent_max = grp.max(float(x1["bytes_sent"] - x0["bytes_sent"]))
+    if grp.max(float(x1["refused_crc"] + x1["refused_log"])):
+        raise SystemExit("bench: a follower refused replication rounds; the measurement would be void")
 
     n = spec.records
     total_records = n * args.steps * world
@@ -261,7 +315,7 @@ def main() -> None:
             "metric": "committed msgs/sec (node) + HBM GB/s, 100B msgs, 4096 partitions RF=3",
             "value": msgs_per_s,
             "unit": "msgs/s",
-            "n_gpus": world,
+            "n_gpus": world if args.transport != "local" else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": t_max * 1e3 / args.steps,
@@ -275,7 +329,11 @@ def main() -> None:
                                    f"{L} B records, {n} records/batch",
                        "partitions_per_gpu": spec.partitions, "replication_factor": rf,
                        "records_per_batch": n, "record_payload_bytes": L,
-                       "parallelism": f"partition-sharded x{world}", "batches_per_launch_group": args.group},
+                       "parallelism": (f"partition-sharded x{world}, RF={rf} replicas over "
+                                       + ("xGMI (RCCL)" if args.transport == "rccl" else
+                                          "the in-process transport on ONE GPU (functional rehearsal)")
+                                       if world > 1 else "1 GPU, RF=3 replicas co-located"),
+                       "batches_per_launch_group": args.group, "segment_mb": seg_mb},
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
@@ -283,12 +341,18 @@ def main() -> None:
                          "algorithmic_bytes_per_launch": alg * n_applied / max(n_launch, 1),
                          "mean_kernel_us": region_ms * 1e3 / max(n_launch, 1), "timed_launches": n_launch,
                          "batches_per_launch": n_applied / max(n_launch, 1)},
+            "xgmi": None if world == 1 else {
+                "bytes_sent_per_gpu_max": sent_max, "achieved": sent_max / t_max / 1e9,
+                "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
+                "frac": sent_max / t_max / 1e9 / (XGMI_LINK_GBS * (world - 1)),
+                "note": "round regions sent per GPU (records + record table + directories) over the timed "
+                        "region / the links to the job's other GPUs (one direction)"},
             "append_stats_last": st,
             "device": dev_name,
             "cu_count": cus,
         }
-    if rank == 0 and args.fetch_rounds > 0:
-        out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
+        if args.fetch_rounds > 0:
+            out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
     for _, dp, dl, dpay, _, _ in pool:
         eng.device_free(dp)
         eng.device_free(dl)
@@ -298,11 +362,96 @@ def main() -> None:
     eng.close()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(spec, rf, args.segment_mb << 20, args.cpu_budget, args.config)
+            out["cpu_baseline"] = cpu_baseline(spec, rf, seg_mb << 20, args.cpu_budget, args.config)
         else:
             out["cpu_baseline"] = None
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
+    ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
+    ap.add_argument("--segment-mb", type=int, default=None,
+                    help="ring bytes per (replica, partition) [MiB]; default 16 on one GPU, 4 with replication "
+                         "(the hot Zipf partition takes ~1.3 MB of a 64k x 128 B batch)")
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
+    ap.add_argument("--watchdog", type=float, default=900.0, help="multi-GPU: exit a rank stuck this long [s]")
+    ap.add_argument("--group", type=int, default=4,
+                    help="batches per pipeline launch group (cfg.pipeline_depth, 1..8)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "local"],
+                    help="local: --gpus ranks as threads on ONE GPU over the in-process transport "
+                         "(functional rehearsal of the multi-GPU path; never a scaling number)")
+    args = ap.parse_args()
+
+    if args.transport == "local":
+        from ripplemq_amd.engine import LocalHub
+
+        world = args.gpus
+        hub = LocalHub(world)
+        tg = ThreadGroup(world)
+        outs, errs = [None] * world, [None] * world
+
+        def body(r):
+            try:
+                outs[r] = run_rank(args, tg.view(r), 0, lambda eng, grp: eng.attach_local(hub))
+            except BaseException as ex:  # noqa: BLE001 - reported below
+                errs[r] = ex
+
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for ex in errs:
+            if ex is not None:
+                raise ex
+        print(json.dumps(outs[0]), flush=True)
+        return
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start one rank process per GPU ourselves, before this process touches HIP
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        procs = []
+        for r in range(args.gpus):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                       LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        rcs = [p.wait() for p in procs]
+        sys.exit(next((rc for rc in rcs if rc), 0))
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the line would misreport n_gpus")
+    grp = SoloGroup()
+    dist = None
+    if world > 1:
+        # a rank that waits on a peer forever (a collective out of step) must not hold the node
+        wd = threading.Timer(args.watchdog, lambda: (print(f"bench: rank {os.environ.get('RANK')} watchdog "
+                                                           f"after {args.watchdog} s", file=sys.stderr, flush=True),
+                                                     os._exit(3)))
+        wd.daemon = True
+        wd.start()
+        import torch.distributed as dist  # host-side barrier / max / id broadcast only (gloo)
+
+        dist.init_process_group("gloo")
+        grp = DistGroup(dist)
+
+    def attach_rccl(eng, g):
+        eng.attach_rccl(g.bcast(rccl_unique_id() if g.rank == 0 else None), g.world)
+
+    out = run_rank(args, grp, int(os.environ.get("LOCAL_RANK", "0")), attach_rccl)
+    if out is not None:
         print(json.dumps(out), flush=True)
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -261,6 +261,10 @@ int quiesce(rmq_engine* e) {
   return check_err(e);
 }
 
+// Drain, or with a replication transport (where a flush is collective: rmq_sync) just wait for
+// what is issued: device memory management and profiling calls.
+int settle(rmq_engine* e) { return e->repl ? quiesce(e) : drain(e); }
+
 // Has the launch with sequence number L completed?
 bool launch_done(rmq_engine* e, uint64_t L) {
   if (L <= __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE)) return true;
@@ -1069,7 +1073,7 @@ int rmq_device_free(rmq_engine* e, void* p) {
   if (!e) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = settle(e);
   if (rc) return rc;
   if (p) HIP_TRY(hipFree(p));
   return RMQ_OK;
@@ -1082,7 +1086,7 @@ int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int ki
   const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
                         : kind == 1 ? hipMemcpyDeviceToHost
                                     : hipMemcpyDeviceToDevice;
-  int rc = drain(e);
+  int rc = settle(e);
   if (rc) return rc;
   if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, k));
   return RMQ_OK;
@@ -1092,7 +1096,7 @@ int rmq_profile_enable(rmq_engine* e, int enable) {
   if (!e) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = settle(e);
   if (rc) return rc;
   for (auto& v : e->prof) {
     for (EvPair& p : v) {
@@ -1115,7 +1119,7 @@ int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* tot
   if (!e || kernel < 0 || kernel > 4) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = settle(e);
   if (rc) return rc;
   if (kernel <= 1) {  // 0: pipeline launches in the region, 1: batches applied in it
     float ms = 0;
