@@ -143,12 +143,11 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             t0 = time.perf_counter()
             rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
             t_wall += time.perf_counter() - t0
-            _, ms_r = eng.profile_query(3)
-            _, ms_g = eng.profile_query(4)
+            _, ms_f = eng.profile_query(3)  # resolve + place + gather, one event pair per call
             eng.profile(False)
             if rc or np.any(res["status"] != 0):
                 raise SystemExit(f"bench: fetch leg failed rc={rc} statuses={np.unique(res['status'])}")
-            t_kern += (ms_r + ms_g) / 1e3
+            t_kern += ms_f / 1e3
             recs += int(res["count"].sum())
             nbytes += int(res["bytes"].sum())
         eng.device_free(d_out)
@@ -241,7 +240,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     spec = CONFIGS[args.config]
     rf = 3
     L = spec.size if isinstance(spec.size, int) else None
-    seg_mb = args.segment_mb or (16 if world == 1 else 4)
+    seg_mb = args.segment_mb or 4
     view = rank_view(rank, world, spec.partitions, rf)  # world 1: every replica on this GPU
     cfg = EngineConfig(num_partitions=len(view.gp), replication_factor=rf,
                        segment_bytes=seg_mb << 20, index_interval=1024,
@@ -376,8 +375,9 @@ def main() -> None:
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
     ap.add_argument("--segment-mb", type=int, default=None,
-                    help="ring bytes per (replica, partition) [MiB]; default 16 on one GPU, 4 with replication "
-                         "(the hot Zipf partition takes ~1.3 MB of a 64k x 128 B batch)")
+                    help="ring bytes per (replica, partition) [MiB]; default 4 (the hot Zipf partition takes "
+                         "~1.3 MB of a 64k x 128 B batch; 16 MiB rings span 192 GiB and the first launches of "
+                         "a process run up to 1.5x slower until the translation caches warm)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")

@@ -153,12 +153,13 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   if (s1) {
     a.g1 = make_group(e, *s1);
     a.s1 = e->scratch[s1->set];
-    a.wg1 = s1->tiles;
+    a.wg1 = e->s1_wgs ? std::min<uint32_t>(s1->tiles, e->s1_wgs) : s1->tiles;
   }
   if (s2) {
     a.g2 = make_group(e, *s2);
     a.s2 = e->scratch[s2->set];
     a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + kPipeThreads - 1) / kPipeThreads, 2u * e->cu_count));
+    if (e->s2_wgs) a.wg2 = std::min(a.wg2, e->s2_wgs);
   }
   repl_pipe_args(e, a, s2, s3);
   {
@@ -356,7 +357,7 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_err,
-                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_total, e->d_fetch_out,
+                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_opos, e->d_total, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -458,6 +459,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->stamps_path = std::getenv("RMQ_STAMPS");
   if (const char* v = std::getenv("RMQ_DEBUG")) e->debug = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_WG3_ALL")) e->wg3_all = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S1_WGS")) e->s1_wgs = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S2_WGS")) e->s2_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
@@ -889,22 +892,25 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     hipFree(e->d_res);
     hipFree(e->d_aux);
     hipFree(e->d_cpre);
+    hipFree(e->d_opos);
     if (e->h_req) hipHostFree(e->h_req);
     if (e->h_res) hipHostFree(e->h_res);
     e->d_req = nullptr;
     e->d_res = e->d_aux = nullptr;
     e->d_cpre = e->h_req = nullptr;
+    e->d_opos = nullptr;
     e->h_res = nullptr;
     e->fetch_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     rc = dalloc(&e->d_req, (size_t)cap * 4);
     if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4);
     if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
-    if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 1);
+    if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 4);
+    if (!rc) rc = dalloc(&e->d_opos, (size_t)cap);
     if (!rc && !e->d_total) rc = dalloc(&e->d_total, 2);
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
-    HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));
+    HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 5 + 2) * 8, 0));  // res, total, positions
     e->fetch_cap = cap;
   }
   uint8_t* d_out = out;
@@ -932,27 +938,26 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     a.res = e->d_res;
     a.aux = e->d_aux;
     a.cpre = e->d_cpre;
+    a.opos = e->d_opos;
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
-    a.gather_wgs = std::max<uint32_t>(1u, 4u * e->cu_count);
+    a.gather_wgs = std::max<uint32_t>(1u, 32u * e->cu_count);
     a.total = e->d_total;
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
     HIP_TRY(hipMemcpyAsync(e->d_req, e->h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
-    hipEvent_t r0 = nullptr, r1 = nullptr, g0 = nullptr, g1 = nullptr;
-    if (e->profile) {
+    hipEvent_t r0 = nullptr, g1 = nullptr;
+    if (e->profile) {  // one timed region around the three fetch kernels (profile_query(3))
       r0 = pool_event(e);
-      r1 = pool_event(e);
-      g0 = pool_event(e);
       g1 = pool_event(e);
-      e->prof[3].push_back({r0, r1});
-      e->prof[4].push_back({g0, g1});
+      e->prof[3].push_back({r0, g1});
     }
-    launch_fetch(a, e->fetch_s, r0, r1, g0, g1);
+    launch_fetch(a, e->fetch_s, r0, nullptr, nullptr, g1);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, (size_t)n * 32, hipMemcpyDeviceToHost, e->fetch_s));
     HIP_TRY(hipMemcpyAsync(h_total, e->d_total, 16, hipMemcpyDeviceToHost, e->fetch_s));
+    HIP_TRY(hipMemcpyAsync(h_total + 2, e->d_opos, (size_t)n * 8, hipMemcpyDeviceToHost, e->fetch_s));
     HIP_TRY(hipEventRecord(e->ev_fetch, e->fetch_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, e->ev_fetch, 0));
   }
@@ -963,7 +968,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     rmq_fetch_res& x = res[r];
     std::memset(&x, 0, sizeof x);
     x.start_offset = h[0];
-    x.out_pos = h[1];
+    x.out_pos = h_total[2 + r];
     x.count = (uint32_t)h[2];
     x.bytes = (uint32_t)(h[2] >> 32);
     x.status = (int32_t)(uint32_t)h[3];

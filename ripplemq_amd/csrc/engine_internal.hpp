@@ -146,6 +146,7 @@ struct rmq_engine {
   uint64_t* d_res = nullptr;
   uint64_t* d_aux = nullptr;
   uint32_t* d_cpre = nullptr;
+  uint64_t* d_opos = nullptr;
   uint64_t* d_total = nullptr;
   uint32_t* h_req = nullptr;   // pinned
   uint64_t* h_res = nullptr;   // pinned [cap][4] + 2 totals
@@ -173,6 +174,8 @@ struct rmq_engine {
   // one stage-3 wave per task: the workgroups beyond the resident slots dispatch as stage-1/2
   // workgroups retire (RMQ_WG3_ALL=0: only as many as fit next to them, looping over tasks)
   uint32_t wg3_all = 1;
+  uint32_t s1_wgs = 0;    // RMQ_S1_WGS: stage-1 workgroups per launch (0: one per tile; fewer loop over tiles)
+  uint32_t s2_wgs = 0;    // RMQ_S2_WGS: cap on stage-2 workgroups (0: one thread group per column)
   uint32_t s3_first = 0;  // RMQ_S3_FIRST=1: stage-3 workgroups first in dispatch order
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
   std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)

@@ -2,13 +2,15 @@
 // (mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:85-110), served directly from
 // committed state like MessageBatchReadRequestProcessor.java:39 (no read-index).
 //
-//  resolve (lane per request): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
-//          byte range of records [off, end) by binary search of the sparse offset index
-//          (FORMAT.md §5: E[m] = first record starting at or after m*I) plus a short header walk;
-//  place   (one workgroup): exclusive scans of request bytes -> output positions (ENOSPC marking)
-//          and of request 1 KiB chunks -> the gather's work list;
-//  gather  (wave per 1 KiB chunk of one request, grid-stride): 16-byte loads from the leader ring
-//          and 16-byte stores to the output. Records and output positions are 16-byte aligned
+//  resolve (wave per request): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
+//          byte range of records [off, end): a 64-ary search of the sparse offset index (FORMAT.md
+//          §5: E[m] = first record starting at or after m*I; 64 probes per round, one round per
+//          factor 64 of index entries), then the record headers of the 1 KiB after the entry found
+//          are loaded at once (a lane per 16 bytes) and walked in registers;
+//  place   (one workgroup): exclusive scan of the requests' bytes -> compact output positions,
+//          ENOSPC marking (every request's bytes count, served or not: FORMAT.md §7);
+//  gather  (wave per request): 16-byte loads from the lowest local replica ring, four in flight per
+//          lane, 16-byte stores to the output. Records and output positions are 16-byte aligned
 //          (FORMAT.md §1), so no piece straddles a record, the ring end or an output boundary.
 //
 // The three kernels run on the engine's fetch stream, after the last pipeline launch the host had
@@ -20,44 +22,78 @@
 namespace rmq {
 
 constexpr int kOk = 0, kNotLeader = -1, kNoPart = -2, kInval = -3, kNoSpc = -4, kOffset = -6;
-constexpr u32 kChunkLog2 = 10;  // gather chunk: 1 KiB = 64 lanes x 16 B
+constexpr u32 kFW = 4;  // waves per workgroup (resolve, gather)
 
 struct PartView {
   u64 leo, used, start_off, start_pos;
   const uint8_t* ring;  // lowest local replica ring of the partition
 };
 
-// Logical byte position of record t, start_off <= t <= leo.
-__device__ u64 record_pos(const DevState& st, u32 p, const PartView& v, u64 t) {
-  if (t == v.leo) return v.used;
+// Logical byte positions of records t0 (lanes 0..31) and t1 (lanes 32..63), start_off <= t <= leo,
+// found together (wave-uniform arguments; the half-wave of each record returns its position).
+__device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0, u64 t1) {
+  const u32 lane = lane_id(), h = lane >> 5, hl = lane & 31u;
+  const u64 t = h ? t1 : t0;
   const u32 ilog = st.interval_log2;
   const u64 I = 1ull << ilog;
+  const u64* E = st.index + (u64)p * st.icap * 2;
+  // per half: largest m in [lo, hi] with E[m].offset <= t (E rises with m), 32 probes per round;
+  // none: the log start
   u64 c_off = v.start_off, c_pos = v.start_pos;
   long lo = (long)((v.start_pos + I - 1) >> ilog), hi = (long)(v.used >> ilog);
-  const u64* E = st.index + (u64)p * st.icap * 2;
-  while (lo <= hi) {  // largest m with E[m].offset <= t
-    const long mid = lo + ((hi - lo) >> 1);
-    const u64* e = E + ((u64)mid % st.icap) * 2;
-    const u64 eo = e[0];
-    if (eo <= t) {
-      c_off = eo;
-      c_pos = e[1];
-      lo = mid + 1;
-    } else {
-      hi = mid - 1;
+  bool open = t < v.leo && lo <= hi;
+  while (__any(open)) {
+    const long span = hi - lo + 1;
+    const long step = (span + 31) / 32;
+    const long m = lo + (long)hl * step;
+    bool le = false;
+    u64 eo = 0, ep = 0;
+    if (open && m <= hi) {
+      const u64* e = E + ((u64)m % st.icap) * 2;
+      eo = e[0];
+      ep = e[1];
+      le = eo <= t;
+    }
+    const u32 bal = (u32)(__ballot(le) >> (32u * h));  // this half's probes
+    const u32 last = bal ? 31u - (u32)__builtin_clz(bal) : 0u;
+    const u64 so = __shfl(eo, (int)(32u * h + last), 64), sp = __shfl(ep, (int)(32u * h + last), 64);
+    if (open) {
+      if (!bal) {
+        open = false;  // every probe past t: the answer precedes this round's range
+      } else {
+        c_off = so;
+        c_pos = sp;
+        if (step == 1) {
+          open = false;
+        } else {
+          lo = lo + (long)last * step + 1;  // the answer is that probe or one of the next step - 1
+          hi = min(hi, lo + step - 2);
+          open = lo <= hi;
+        }
+      }
     }
   }
+  if (t >= v.leo) return v.used;
+  // walk the headers of the records in [c_off, t): they start in the interval after c_pos, so one
+  // 1 KiB window of 16-byte pieces holds them all (two pieces per lane of the half)
   const u64 mask = st.seg - 1;
-  for (u32 guard = 0; c_off < t && guard < (1u << 20); ++guard) {  // at most ~I / 16 records
-    const u32 L = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 8) & mask));
-    c_pos += record_bytes(L);
-    ++c_off;
+  const u32 Lw0 = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 32ull * hl + 8ull) & mask));
+  const u32 Lw1 = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 32ull * hl + 24ull) & mask));
+  u64 k = t - c_off;
+  u32 cur = 0;  // window piece of the current record
+  while (__any(k > 0)) {
+    const u32 src = 32u * h + (cur >> 1);
+    const u32 a0 = (u32)__shfl((int)Lw0, (int)src, 64), a1 = (u32)__shfl((int)Lw1, (int)src, 64);
+    if (k > 0) {
+      cur += record_bytes((cur & 1u) ? a1 : a0) >> 4;
+      --k;
+    }
   }
-  return c_pos;
+  return c_pos + 16ull * cur;
 }
 
-__global__ void fetch_resolve_kernel(FetchArgs a) {
-  const u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
+  const u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6));
   if (r >= a.n) return;
   const DevState& st = a.st;
   const u32 p = a.req[4 * r], c = a.req[4 * r + 1], mx = a.req[4 * r + 2];
@@ -89,94 +125,108 @@ __global__ void fetch_resolve_kernel(FetchArgs a) {
         const u32 r0 = lm ? (u32)__ffs(lm) - 1u : 0u;
         ring_off = ((u64)r0 * st.P + p) * st.seg;
         v.ring = st.logs + ring_off;
-        pos0 = record_pos(st, p, v, off);
-        bytes = record_pos(st, p, v, end) - pos0;
+        const u64 pp = record_pos2(st, p, v, off, end);
+        pos0 = __shfl(pp, 0, 64);
+        bytes = __shfl(pp, 32, 64) - pos0;
         count = end - off;
       }
     }
   }
-  a.res[4 * r + 0] = start;
-  a.res[4 * r + 2] = count | (bytes << 32);
-  a.res[4 * r + 3] = (u64)(uint32_t)status;
-  a.aux[2 * r + 0] = pos0;
-  a.aux[2 * r + 1] = ring_off;
+  if (lane_id() == 0) {
+    a.res[4 * r + 0] = start;
+    a.res[4 * r + 2] = count | (bytes << 32);
+    a.res[4 * r + 3] = (u64)(uint32_t)status;
+    a.aux[2 * r + 0] = pos0;
+    a.aux[2 * r + 1] = ring_off;
+    a.cpre[r] = (u32)bytes;
+  }
 }
 
+// One workgroup: output positions = exclusive scan of the requests' bytes in request order; each
+// thread scans 16 consecutive requests per pass (16-byte loads of the byte counts, 16-byte stores of
+// the compact positions: one load round per 16384 requests).
 __global__ __launch_bounds__(1024) void fetch_place_kernel(FetchArgs a) {
   __shared__ u64 sh[16];
-  __shared__ u64 shc[16];
-  const u32 tid = threadIdx.x, T = blockDim.x, l = tid & 63, w = tid >> 6;
-  const u32 per = (a.n + T - 1) / T;
-  const u32 b = tid * per, e = b + per < a.n ? b + per : a.n;
-  u64 local = 0;
-  for (u32 r = b; r < e; ++r) local += a.res[4 * r + 2] >> 32;
-  // output positions: every request's bytes count, served or not (FORMAT.md §7)
-  const u64 inc = wave_incl_scan(local);
-  if (l == 63) sh[w] = inc;
-  __syncthreads();
-  u64 cur = inc - local, tot = 0;
-  for (u32 k = 0; k < 16; ++k) {
-    cur += k < w ? sh[k] : 0ull;
-    tot += sh[k];
-  }
-  u64 lch = 0;
-  for (u32 r = b; r < e; ++r) {
-    const u64 cb = a.res[4 * r + 2];
-    const u64 nb = cb >> 32;
-    a.res[4 * r + 1] = cur;
-    if (nb && cur + nb > a.out_cap) {
-      a.res[4 * r + 2] = 0;
-      a.res[4 * r + 3] = (u64)(uint32_t)kNoSpc;
+  constexpr u32 kPer = 16;
+  const u32 tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  u64 carry = 0;
+  for (u32 b = 0; b < a.n; b += 1024 * kPer) {
+    const u32 r0 = b + tid * kPer;
+    u32 nb[kPer];
+    if (r0 + kPer <= a.n) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.cpre + r0);
+#pragma unroll
+      for (u32 k = 0; k < kPer / 4; ++k) {
+        const uint4 v = src[k];
+        nb[4 * k] = v.x;
+        nb[4 * k + 1] = v.y;
+        nb[4 * k + 2] = v.z;
+        nb[4 * k + 3] = v.w;
+      }
     } else {
-      lch += (nb + (1ull << kChunkLog2) - 1) >> kChunkLog2;
+#pragma unroll
+      for (u32 k = 0; k < kPer; ++k) nb[k] = r0 + k < a.n ? a.cpre[r0 + k] : 0u;
     }
-    cur += nb;
+    u64 loc = 0;
+#pragma unroll
+    for (u32 k = 0; k < kPer; ++k) loc += nb[k];
+    const u64 inc = wave_incl_scan(loc);
+    if (l == 63) sh[w] = inc;
+    __syncthreads();
+    u64 cur = carry + inc - loc, tot = 0;
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k) {
+      cur += k < w ? sh[k] : 0ull;
+      tot += sh[k];
+    }
+    u64 pos[kPer];
+#pragma unroll
+    for (u32 k = 0; k < kPer; ++k) {
+      pos[k] = cur;
+      if (nb[k] && cur + nb[k] > a.out_cap && r0 + k < a.n) {  // does not fit: not served (rare)
+        a.res[4 * (r0 + k) + 2] = 0;
+        a.res[4 * (r0 + k) + 3] = (u64)(uint32_t)kNoSpc;
+      }
+      cur += nb[k];
+    }
+    if (r0 + kPer <= a.n) {
+      uint4* dst = reinterpret_cast<uint4*>(a.opos + r0);
+#pragma unroll
+      for (u32 k = 0; k < kPer / 2; ++k)
+        dst[k] = make_uint4((u32)pos[2 * k], (u32)(pos[2 * k] >> 32), (u32)pos[2 * k + 1], (u32)(pos[2 * k + 1] >> 32));
+    } else {
+#pragma unroll
+      for (u32 k = 0; k < kPer; ++k)
+        if (r0 + k < a.n) a.opos[r0 + k] = pos[k];
+    }
+    carry += tot;
+    __syncthreads();
   }
-  // gather work list: chunks of the requests that are served
-  const u64 cinc = wave_incl_scan(lch);
-  if (l == 63) shc[w] = cinc;
-  __syncthreads();
-  u64 ccur = cinc - lch, ctot = 0;
-  for (u32 k = 0; k < 16; ++k) {
-    ccur += k < w ? shc[k] : 0ull;
-    ctot += shc[k];
-  }
-  for (u32 r = b; r < e; ++r) {
-    a.cpre[r] = (u32)ccur;
-    const u64 nb = a.res[4 * r + 2] >> 32;
-    ccur += (nb + (1ull << kChunkLog2) - 1) >> kChunkLog2;
-  }
-  if (tid == 0) {
-    a.cpre[a.n] = (u32)ctot;
-    a.total[0] = tot;
-    a.total[1] = ctot;
-  }
+  if (tid == 0) a.total[0] = carry;
 }
 
-__global__ __launch_bounds__(256) void fetch_gather_kernel(FetchArgs a) {
+__global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   const DevState& st = a.st;
   const u64 mask = st.seg - 1;
-  const u32 lane = threadIdx.x & 63;
-  const u32 nw = gridDim.x * (blockDim.x >> 6);
-  const u32 chunks = (u32)a.total[1];
-  for (u32 c = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); c < chunks;
-       c += nw) {
-    // request of chunk c: the last r with cpre[r] <= c (requests without chunks are skipped)
-    u32 lo = 0, hi = a.n;  // cpre[lo] <= c < cpre[hi]
-    while (hi - lo > 1) {
-      const u32 mid = (lo + hi) >> 1;
-      if (a.cpre[mid] <= c) lo = mid; else hi = mid;
-    }
-    const u32 r = lo;
-    const u64 nb = a.res[4 * r + 2] >> 32;
+  const u32 lane = lane_id();
+  const u32 nw = gridDim.x * kFW;
+  for (u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6)); r < a.n; r += nw) {
+    const u64 nb = a.res[4 * r + 2] >> 32;  // 0 for requests not served
+    if (!nb) continue;
     const u64 pos0 = a.aux[2 * r + 0];
     const uint8_t* ring = st.logs + a.aux[2 * r + 1];
-    uint8_t* out = a.out + a.res[4 * r + 1];
-    const u64 piece = ((u64)(c - a.cpre[r]) << (kChunkLog2 - 4)) + lane;
-    if (16ull * piece < nb) {
-      const uint4 v = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * piece) & mask));
-      *reinterpret_cast<uint4*>(out + 16ull * piece) = v;
+    uint8_t* out = a.out + a.opos[r];
+    const u64 pieces = nb >> 4;
+    u64 q = lane;
+    for (; q + 192 < pieces; q += 256) {  // four 16-byte pieces in flight per lane
+      uint4 v[4];
+#pragma unroll
+      for (u32 u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (q + 64 * u)) & mask));
+#pragma unroll
+      for (u32 u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(out + 16ull * (q + 64 * u)) = v[u];
     }
+    for (; q < pieces; q += 64)
+      *reinterpret_cast<uint4*>(out + 16ull * q) = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * q) & mask));
   }
 }
 
@@ -184,11 +234,12 @@ void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e
                   hipEvent_t g1) {
   if (!a.n) return;
   if (e0) hipEventRecord(e0, s);
-  hipLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW - 1) / kFW), dim3(64 * kFW), 0, s, a);
   hipLaunchKernelGGL(fetch_place_kernel, dim3(1), dim3(1024), 0, s, a);
-  if (e1) hipEventRecord(e1, s);
+  if (e1) hipEventRecord(e1, s);  // optional split of the timed region (null: one region)
   if (g0) hipEventRecord(g0, s);
-  hipLaunchKernelGGL(fetch_gather_kernel, dim3(a.gather_wgs), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(fetch_gather_kernel, dim3(std::min<u32>((a.n + kFW - 1) / kFW, a.gather_wgs)), dim3(64 * kFW), 0,
+                     s, a);
   if (g1) hipEventRecord(g1, s);
 }
 

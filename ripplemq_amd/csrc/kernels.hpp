@@ -153,12 +153,13 @@ struct FetchArgs {
   const uint32_t* req;       // [n][4] {pidx, consumer, max, reserved}
   uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}
   uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
-  uint32_t* cpre;            // [n + 1] exclusive prefix of the served requests' 1 KiB chunks
+  uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> place), 16-byte aligned
+  uint64_t* opos;            // [n] output position of each request (place -> gather, host)
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
   uint32_t n;
-  uint32_t gather_wgs;       // gather grid (waves loop over the chunks)
-  uint64_t* total;           // [2] {bytes needed, chunks}
+  uint32_t gather_wgs;       // gather grid cap (a wave per request, looping)
+  uint64_t* total;           // [2] {bytes needed, 0}
 };
 
 struct ConsumerCommitArgs {  // one item per (partition, consumer): the host resolved last-writer-wins

@@ -923,8 +923,11 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   }
   if (!s3) {
     if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
-    if (wg < A.wg1) {
-      stage1_tile(A, wg, *reinterpret_cast<Stage1Smem*>(smem_raw));
+    if (wg < A.wg1) {  // a workgroup ranks tiles wg, wg + wg1, ... (RMQ_S1_WGS < tiles: fewer slots held)
+      for (u32 t = wg; t < A.g1.tiles; t += A.wg1) {
+        stage1_tile(A, t, *reinterpret_cast<Stage1Smem*>(smem_raw));
+        __syncthreads();  // the tile's LDS is reused by the next one
+      }
       return;
     }
     wg -= A.wg1;
