@@ -55,9 +55,10 @@ def algorithmic_bytes(n: int, L: int, rf: int, P: int) -> int:
 
 
 def pmc_traffic(group: int, config: str):
-    """HBM bytes per launch of the pipeline kernel from the newest committed PMC summary taken at
-    this group size and config (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from
-    the rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench), or (None, None)."""
+    """HBM bytes per BATCH of the pipeline kernel from the newest committed PMC summary taken at this
+    group size and config (profiles/*_pmc_traffic.json, written by tools/pmc_summary.py from the
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this bench; `measured_at` names the commit of the
+    code it measured), or (None, None)."""
     found = (None, None)
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc_traffic.json"))):
         try:
@@ -65,8 +66,9 @@ def pmc_traffic(group: int, config: str):
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get("group") == group and d.get("config") == config:
-            found = (d["traffic_bytes_per_launch"], os.path.relpath(path, REPO))
+        if d.get("group") == group and d.get("config") == config and "traffic_bytes_per_batch" in d:
+            src = os.path.relpath(path, REPO) + (f" (measured at {d['measured_at']})" if d.get("measured_at") else "")
+            found = (d["traffic_bytes_per_batch"], src)
     return found
 
 
@@ -309,7 +311,10 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
         alg = algorithmic_bytes(n, L or 0, rf, spec.partitions)
         # algorithmic bytes per launch / mean launch duration = bytes of the applied batches / region
         achieved = alg * n_applied / (region_ms / 1e3) / 1e9 if n_launch and region_ms > 0 else 0.0
-        traffic, traffic_src = pmc_traffic(args.group, args.config)
+        traffic_b, traffic_src = pmc_traffic(args.group, args.config)
+        bpl = n_applied / max(n_launch, 1)
+        # per launch of THIS run (its launches average bpl batches), from the per-batch PMC figure
+        traffic = traffic_b * bpl if traffic_b else None
         out = {
             "metric": "committed msgs/sec (node) + HBM GB/s, 100B msgs, 4096 partitions RF=3",
             "value": msgs_per_s,
@@ -335,7 +340,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
                        "batches_per_launch_group": args.group, "segment_mb": seg_mb},
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_per_batch": traffic_b,
+                         "traffic_source": traffic_src,
                          "kernel": "rmq::pipeline_kernel",
                          "algorithmic_bytes_per_launch": alg * n_applied / max(n_launch, 1),
                          "mean_kernel_us": region_ms * 1e3 / max(n_launch, 1), "timed_launches": n_launch,
