@@ -26,6 +26,8 @@
  *                                  (mq-broker/src/main/java/metadata/raft/PartitionRaftServer.java:82-86)
  *   rmq_create / rmq_destroy    <- PartitionManager.startPartition / PartitionRaftServer.shutdown
  *                                  (PartitionManager.java:166-176, PartitionRaftServer.java:100-108)
+ *   rmq_set_segments            <- no reference counterpart (its logs never evict, PartitionStateMachine.java
+ *                                  :26,66): per-partition retention size inside a shared HBM pool
  *   rmq_set_placement           <- PartitionManager.handleTopicListChange starting the groups this broker
  *                                  hosts with their peers (PartitionManager.java:111-176), as placed by
  *                                  PartitionAssigner.assignPartitions (PartitionAssigner.java:25-94)
@@ -62,7 +64,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 1u
+#define RMQ_ABI_VERSION 2u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -96,6 +98,9 @@ typedef struct rmq_config {
   uint64_t max_batch_bytes;    /* payload bytes of one rmq_append call */
   int32_t device;              /* HIP device ordinal */
   uint32_t rank;               /* replica rank of this engine (placement in rmq_set_replicas) */
+  uint64_t pool_bytes;         /* ring bytes per replica shared by all partitions (FORMAT.md §2);
+                                  0 -> num_partitions * segment_bytes. Every partition starts with a
+                                  segment_bytes ring; rmq_set_segments resizes them inside the pool */
 } rmq_config;
 
 /* One append batch: records of many partitions, interleaved, in apply order (SoA). */
@@ -139,6 +144,7 @@ typedef struct rmq_partition_state {
   uint32_t replica_rank[RMQ_MAX_RF];
   uint32_t leader_slot;
   uint32_t is_leader;
+  uint64_t segment_bytes;      /* ring bytes of this partition (retention keeps at most this much) */
 } rmq_partition_state;
 
 typedef struct rmq_append_stats {
@@ -188,6 +194,15 @@ int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* replica_ranks
    ranks agrees on what they replicate to each other (RMQ_EINVAL on every rank if not). */
 int rmq_set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* key,
                       const uint32_t* replica_ranks, const uint32_t* leader_slot);
+
+/* Ring sizes of n partitions (reference: per-topic log retention; the reference keeps every
+   message in memory, PartitionStateMachine.java:26,66): segment_bytes[i] (power of two, at least
+   4 * index_interval) for partition pidx[i], allocated from the engine's pool. A shrinking ring
+   first applies retention at the new size (FORMAT.md §4 rule); the retained records, their bytes in
+   every local replica and their index entries keep their offsets and logical positions. All or
+   nothing: RMQ_ENOMEM (nothing changed) if the pool cannot hold the new rings. Drains first (with a
+   transport attached: collective, like rmq_sync). */
+int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* segment_bytes);
 
 /* New leader term for pidx (or RMQ_ALL_PARTITIONS): term_start = log_end_offset, so only
    entries appended in this term can advance the commit (Raft current-term rule). */

@@ -60,6 +60,7 @@ def load() -> C.CDLL:
         "ro_apply_acks": (C.c_int, [vp, u32, vp, u32]),
         "ro_pair_entries": (u32, [vp, u32, u32]),
         "ro_counters": (None, [vp, vp]),
+        "ro_set_segments": (C.c_int, [vp, u32, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -240,8 +241,15 @@ class OracleEngine:
     def commit_snapshot(self):
         return np.array([self.state(p)["commit"] for p in range(self.cfg.num_partitions)], np.uint64)
 
+    def set_segments(self, pidx, segment_bytes):
+        p = np.ascontiguousarray(pidx, np.uint32)
+        sb = np.ascontiguousarray(segment_bytes, np.uint64)
+        rc = self.lib.ro_set_segments(self.h, len(p), _p(p), _p(sb))
+        if rc:
+            raise EngineError(rc, "oracle")
+
     def read_segment(self, replica, pidx, ring_off=0, n=None):
-        n = self.cfg.segment_bytes - ring_off if n is None else n
+        n = self.state(pidx)["segment_bytes"] - ring_off if n is None else n
         out = np.empty(n, np.uint8)
         rc = self.lib.ro_read_segment(self.h, replica, pidx, ring_off, n, _p(out))
         if rc:

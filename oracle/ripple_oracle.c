@@ -113,6 +113,7 @@ typedef struct {
   u64vec rec_pos;          /* dense logical position of every record (oracle-only lookup) */
   uint64_t* cons;          /* consumer offsets (reference: HashMap<String,Long>, default 0) */
   uint64_t key;            /* placement key (FORMAT.md §9 list order), default pidx */
+  uint64_t seg;            /* ring bytes of this partition (rmq_set_segments) */
   uint8_t* round;          /* records appended in the current replication round, log layout */
   uint64_t round_bytes, round_cap, round_count, round_first;
 } ro_part;
@@ -120,7 +121,7 @@ typedef struct {
 struct ro_engine {
   rmq_config cfg;
   ro_part* parts;
-  uint8_t** rings; /* [replica][partition] -> segment_bytes */
+  uint8_t** rings; /* [replica][partition] -> that partition's ring bytes */
   uint8_t* touched;
   uint64_t* pbytes; /* [P] record bytes of the current batch per partition */
   uint8_t* full;    /* [P] 1: the partition takes no record of the current batch (FORMAT.md §3) */
@@ -163,6 +164,7 @@ ro_engine* ro_create(const rmq_config* cfg) {
     s->term = 1;
     s->term_start = 0;
     s->key = p;
+    s->seg = cfg->segment_bytes;
     s->cons = (uint64_t*)calloc(cfg->max_consumers, sizeof(uint64_t));
     if (!s->cons || vec_push(&s->idx_off, 0) || vec_push(&s->idx_pos, 0)) { /* E[0] = (0, 0) */
       ro_destroy(e);
@@ -204,8 +206,7 @@ static uint8_t* ring_of(ro_engine* e, uint32_t replica, uint32_t p) {
   return e->rings[(size_t)replica * e->cfg.num_partitions + p];
 }
 
-static void ring_write(ro_engine* e, uint8_t* ring, uint64_t pos, const uint8_t* src, uint64_t n) {
-  uint64_t S = e->cfg.segment_bytes;
+static void ring_write(uint64_t S, uint8_t* ring, uint64_t pos, const uint8_t* src, uint64_t n) {
   while (n) {
     uint64_t o = pos % S, k = S - o < n ? S - o : n;
     memcpy(ring + o, src, k);
@@ -215,8 +216,7 @@ static void ring_write(ro_engine* e, uint8_t* ring, uint64_t pos, const uint8_t*
   }
 }
 
-static void ring_read(ro_engine* e, const uint8_t* ring, uint64_t pos, uint8_t* dst, uint64_t n) {
-  uint64_t S = e->cfg.segment_bytes;
+static void ring_read(uint64_t S, const uint8_t* ring, uint64_t pos, uint8_t* dst, uint64_t n) {
   while (n) {
     uint64_t o = pos % S, k = S - o < n ? S - o : n;
     memcpy(dst, ring + o, k);
@@ -245,7 +245,7 @@ static void commit_eval(ro_engine* e, ro_part* s) {
 
 /* Size retention (FORMAT.md §4): evaluated once per append batch. */
 static void retention_eval(ro_engine* e, ro_part* s) {
-  uint64_t S = e->cfg.segment_bytes, I = e->cfg.index_interval;
+  uint64_t S = s->seg, I = e->cfg.index_interval;
   if (s->used - s->start_pos <= S) return;
   uint64_t m = (s->used - S + I - 1) / I;
   s->start_off = s->idx_off.v[m];
@@ -327,7 +327,7 @@ static void space_scan(const ro_engine* e, uint32_t n, const uint32_t* pidx, con
   for (uint32_t i = 0; i < n; ++i)
     if (pidx[i] < P && pidx[i] % T == t) bytes[pidx[i]] += rec_size(len[i]);
   for (uint32_t i = 0; i < n; ++i)
-    if (pidx[i] < P && pidx[i] % T == t) full[pidx[i]] = bytes[pidx[i]] > e->cfg.segment_bytes - e->cfg.index_interval;
+    if (pidx[i] < P && pidx[i] % T == t) full[pidx[i]] = bytes[pidx[i]] > e->parts[pidx[i]].seg - e->cfg.index_interval;
 }
 
 typedef struct {
@@ -357,7 +357,7 @@ static int append_record(ro_engine* e, ro_part* s, uint32_t p, const uint8_t* sr
   if (L) memcpy(r8 + 16, src, L);
   memset(r8 + 16 + L, 0, rs - 16 - L);
   for (uint32_t r = 0; r < c->replication_factor; ++r)
-    if (s->ranks[r] == c->rank) ring_write(e, ring_of(e, r, p), pos, r8, rs);
+    if (s->ranks[r] == c->rank) ring_write(s->seg, ring_of(e, r, p), pos, r8, rs);
   /* sparse index: every multiple m*I in (pos, pos + rs] now names the next record */
   for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
     if (vec_push(&s->idx_off, o + 1) || vec_push(&s->idx_pos, pos + rs)) return RMQ_ENOMEM;
@@ -598,14 +598,57 @@ int ro_append_sharded(ro_engine* e, uint32_t nb, const rmq_batch* batches, uint6
 int ro_reserve(ro_engine* e, const uint64_t* bytes) {
   if (!e || !bytes) return RMQ_EINVAL;
   const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
-  const uint64_t S = e->cfg.segment_bytes;
   for (uint32_t p = 0; p < P; ++p) {
+    const uint64_t S = e->parts[p].seg;
     const uint64_t n = bytes[p] < S ? bytes[p] : S;
     for (uint32_t r = 0; r < RF; ++r) {
       if (e->parts[p].ranks[r] != e->cfg.rank) continue;
       volatile uint8_t* ring = ring_of(e, r, p);
       for (uint64_t o = 0; o < n; o += 4096) ring[o] = ring[o]; /* first touch, content unchanged */
     }
+  }
+  return RMQ_OK;
+}
+
+/* rmq_set_segments: ring sizes of n partitions. A smaller ring first applies retention at its size
+   (FORMAT.md §4 rule); the retained records keep their offsets and logical positions in every
+   replica ring; the rest of a new ring is zero. No pool limit here (the engine's RMQ_ENOMEM is
+   engine-only). */
+int ro_set_segments(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* seg) {
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  const uint64_t I = e->cfg.index_interval;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (pidx[i] >= P) return RMQ_ENOPART;
+    if (!seg[i] || (seg[i] & (seg[i] - 1)) || seg[i] < 4 * I) return RMQ_EINVAL;
+    for (uint32_t k = 0; k < i; ++k)
+      if (pidx[k] == pidx[i]) return RMQ_EINVAL;
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    ro_part* s = &e->parts[pidx[i]];
+    const uint64_t S0 = s->seg, S1 = seg[i];
+    if (S1 == S0) continue;
+    if (s->used - s->start_pos > S1) {
+      const uint64_t m = (s->used - S1 + I - 1) / I;
+      s->start_off = s->idx_off.v[m];
+      s->start_pos = s->idx_pos.v[m];
+    }
+    const uint64_t keep = s->used - s->start_pos;
+    uint8_t* tmp = (uint8_t*)malloc(keep ? keep : 1);
+    if (!tmp) return RMQ_ENOMEM;
+    for (uint32_t r = 0; r < RF; ++r) {
+      uint8_t** slot = &e->rings[(size_t)r * P + pidx[i]];
+      uint8_t* nr = (uint8_t*)calloc(S1, 1);
+      if (!nr) {
+        free(tmp);
+        return RMQ_ENOMEM;
+      }
+      ring_read(S0, *slot, s->start_pos, tmp, keep);
+      ring_write(S1, nr, s->start_pos, tmp, keep);
+      free(*slot);
+      *slot = nr;
+    }
+    free(tmp);
+    s->seg = S1;
   }
   return RMQ_OK;
 }
@@ -688,7 +731,7 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
       rc = RMQ_ENOSPC;
       continue;
     }
-    if (out) ring_read(e, ring_of(e, s->leader_slot, p), p0, out + cursor, nb);
+    if (out) ring_read(s->seg, ring_of(e, s->leader_slot, p), p0, out + cursor, nb);
     x->count = (uint32_t)(end - off);
     x->bytes = (uint32_t)nb;
     cursor += nb;
@@ -719,13 +762,13 @@ int ro_get_partition_state(ro_engine* e, uint32_t p, rmq_partition_state* o) {
   }
   o->leader_slot = s->leader_slot;
   o->is_leader = s->is_leader;
+  o->segment_bytes = s->seg;
   return RMQ_OK;
 }
 
 int ro_read_segment(ro_engine* e, uint32_t replica, uint32_t p, uint64_t ring_off, uint64_t len, uint8_t* out) {
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
-  if (replica >= e->cfg.replication_factor || ring_off > e->cfg.segment_bytes ||
-      len > e->cfg.segment_bytes - ring_off)
+  if (replica >= e->cfg.replication_factor || ring_off > e->parts[p].seg || len > e->parts[p].seg - ring_off)
     return RMQ_EINVAL;
   memcpy(out, ring_of(e, replica, p) + ring_off, len);
   return RMQ_OK;
@@ -867,7 +910,7 @@ void ro_end_round(ro_engine* e) {
    entry k afterwards (0 for a refused entry). */
 int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks) {
   const uint32_t me = e->cfg.rank;
-  const uint64_t S = e->cfg.segment_bytes, I = e->cfg.index_interval;
+  const uint64_t I = e->cfg.index_interval;
   ro_entry* v = NULL;
   const uint32_t n = pair_entries(e, src, me, &v);
   if (!v) return RMQ_ENOMEM;
@@ -927,7 +970,7 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
       continue;
     }
     const uint8_t* bytes = region + data + 16ull * ds;
-    ring_write(e, ring_of(e, v[k].slot, v[k].p), used, bytes, 16ull * by16);
+    ring_write(e->parts[v[k].p].seg, ring_of(e, v[k].slot, v[k].p), used, bytes, 16ull * by16);
     if (owner) {
       rel = 0;
       for (uint32_t r = 0; r < cnt; ++r) {
@@ -947,8 +990,8 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
       }
       s->leo = first + cnt;
       s->used = used + 16ull * by16;
-      if (s->used - s->start_pos > S) { /* retention once per round (FORMAT.md §4 rule) */
-        const uint64_t m = (s->used - S + I - 1) / I;
+      if (s->used - s->start_pos > s->seg) { /* retention once per round (FORMAT.md §4 rule) */
+        const uint64_t m = (s->used - s->seg + I - 1) / I;
         s->start_off = s->idx_off.v[m];
         s->start_pos = s->idx_pos.v[m];
       }

@@ -58,6 +58,7 @@ int ro_append_sharded(ro_engine* e, uint32_t nb, const rmq_batch* batches, uint6
 /* First touch of ring bytes [0, min(segment, bytes[p])) of every local replica of every partition
    (untimed setup, so a timed run does not pay page faults the device rings never see). */
 int ro_reserve(ro_engine* e, const uint64_t* bytes);
+int ro_set_segments(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* seg);
 int ro_ack(ro_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n);
 int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                               const uint64_t* offset, uint32_t n, int32_t* status);

@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 1
+RMQ_ABI_VERSION = 2
 RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
@@ -51,6 +51,7 @@ class RmqConfig(C.Structure):
         ("num_partitions", u32), ("replication_factor", u32), ("segment_bytes", u64),
         ("index_interval", u32), ("max_consumers", u32), ("max_batch_records", u32),
         ("pipeline_depth", u32), ("max_batch_bytes", u64), ("device", i32), ("rank", u32),
+        ("pool_bytes", u64),
     ]
 
 
@@ -77,7 +78,7 @@ class RmqPartitionState(C.Structure):
         ("log_end_offset", u64), ("log_end_pos", u64), ("log_start_offset", u64),
         ("log_start_pos", u64), ("commit", u64), ("high_watermark", u64), ("term", u64),
         ("term_start", u64), ("match", u64 * RMQ_MAX_RF), ("replica_rank", u32 * RMQ_MAX_RF),
-        ("leader_slot", u32), ("is_leader", u32),
+        ("leader_slot", u32), ("is_leader", u32), ("segment_bytes", u64),
     ]
 
 
@@ -110,6 +111,7 @@ _SIGS = {
     "rmq_destroy": (None, [vp]),
     "rmq_set_replicas": (C.c_int, [vp, u32, C.POINTER(u32), u32, u32]),
     "rmq_become_leader": (C.c_int, [vp, u32, u64]),
+    "rmq_set_segments": (C.c_int, [vp, u32, C.POINTER(u32), C.POINTER(u64)]),
     "rmq_append": (C.c_int, [vp, C.POINTER(RmqBatch), vp, C.POINTER(u64)]),
     "rmq_ack": (C.c_int, [vp, vp, vp, vp, u32]),
     "rmq_poll_commit": (C.c_int, [vp, u64, vp, vp]),

@@ -4,7 +4,8 @@
 //   * leader start (term_start = log end; Raft matchIndex reset for remote replicas),
 //   * consumer-offset commits (PartitionStateMachine.handleConsumerOffsetUpdateRequest,
 //     mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:71-77): last writer wins;
-//     the host keeps the last item per (partition, consumer), so this is a plain scatter.
+//     the host keeps the last item per (partition, consumer), so this is a plain scatter;
+//   * ring moves (rmq_set_segments): a partition's retained log and index entries into a new ring.
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "partition_ops.hpp"
@@ -58,6 +59,53 @@ void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s) {
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s) {
   if (!a.n) return;
   hipLaunchKernelGGL(consumer_apply_kernel, grid_for(a.n, 256), dim3(256), 0, s, a);
+}
+
+// Workgroup per moved partition. Every 16-byte piece of the new ring of every replica slot gets its
+// logical position's bytes if that position is retained ([spos, used) is at most one new ring
+// long), zero otherwise; every slot of the new index ring gets entry m (m = the retained m with
+// m mod icap = slot) or zero. Old and new blocks are disjoint (both allocated while moving).
+__global__ __launch_bounds__(256) void migrate_kernel(DevState st, const MigrateItem* items) {
+  const MigrateItem it = items[blockIdx.x];
+  // the partition's new ring and log start, written by the device (a host copy into these arrays
+  // could leave other XCDs' L2 holding the old lines for the next launch)
+  if (threadIdx.x == 0) {
+    st.ring[it.p] = it.new_desc;
+    st.start_pos[it.p] = it.spos;
+    st.start_off[it.p] = it.soff;
+  }
+  const RingRef o = ring_ref(it.old_desc, st.interval_log2, st.icap_mul);
+  const RingRef nw = ring_ref(it.new_desc, st.interval_log2, st.icap_mul);
+  const u64 keep = it.used - it.spos, nmask = nw.seg - 1ull, omask = o.seg - 1ull;
+  const u64 s0 = it.spos & nmask;
+  for (u32 r = 0; r < st.RF; ++r) {
+    const uint8_t* src = st.logs + (u64)r * st.rstride + o.base;
+    uint8_t* dst = st.logs + (u64)r * st.rstride + nw.base;
+    for (u64 q = threadIdx.x; q < (nw.seg >> 4); q += blockDim.x) {
+      const u64 d = ((16ull * q - s0) & nmask);  // bytes after spos, if retained
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (d < keep) v = *reinterpret_cast<const uint4*>(src + ((it.spos + d) & omask));
+      store_log16(dst + 16ull * q, v);  // the pipeline's ring-store flavour (non-temporal)
+    }
+  }
+  const u32 ilog = st.interval_log2;
+  const u64 m0 = (it.spos + (1ull << ilog) - 1) >> ilog, m1 = it.used >> ilog;
+  for (u64 q = threadIdx.x; q < nw.icap; q += blockDim.x) {
+    const u64 m = m0 + ((q + nw.icap - m0 % nw.icap) % nw.icap);
+    u64 e0 = 0, e1 = 0;
+    if (m <= m1) {
+      const u64* oe = st.index + (o.ibase + m % o.icap) * 2;
+      e0 = oe[0];
+      e1 = oe[1];
+    }
+    u64* ne = st.index + (nw.ibase + q) * 2;
+    ne[0] = e0;
+    ne[1] = e1;
+  }
+}
+
+void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(migrate_kernel, dim3(n), dim3(256), 0, s, st, items);
 }
 
 }  // namespace rmq

@@ -146,7 +146,6 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.key_passes = e->key_passes;
   a.gt = e->max_group_tiles;
   a.s3_first = e->s3_first;
-  a.nospace_limit = e->cfg.segment_bytes - e->cfg.index_interval;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
   a.debug = e->debug;
@@ -356,7 +355,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.cons, e->d_crc, e->d_err,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc, e->d_err,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_opos, e->d_total, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
@@ -403,7 +402,9 @@ int validate_cfg(const rmq_config* c) {
   if (c->max_batch_bytes >= (1ull << 32)) return RMQ_EINVAL;
   if (c->pipeline_depth > kMaxGroup) return RMQ_EINVAL;
   const uint64_t g = c->pipeline_depth ? c->pipeline_depth : 2u;
-  if ((2 * g + 1) * (c->segment_bytes / c->index_interval) + 2 >= (1ull << 32)) return RMQ_EINVAL;
+  const uint64_t pool = c->pool_bytes ? c->pool_bytes : (uint64_t)c->num_partitions * c->segment_bytes;
+  if (pool < (uint64_t)c->num_partitions * c->segment_bytes || pool % c->index_interval) return RMQ_EINVAL;
+  if ((2 * g + 2) * (pool / c->index_interval) >= (1ull << 40)) return RMQ_EINVAL;
   return RMQ_OK;
 }
 
@@ -487,13 +488,25 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   s.P = P;
   s.RF = RF;
   s.C = C;
-  s.seg = cfg->segment_bytes;
   s.interval_log2 = ilog2(cfg->index_interval);
   e->group_max = std::min<uint32_t>(kMaxGroup, e->cfg.pipeline_depth);
   // stage 4 reads a group's index entries while stage 3 of the group two later writes new ones
-  // (each batch adds at most segment - interval bytes to a partition): 2G + 1 segments of entries
-  // keep every entry stage 4 may read from being overwritten in time
-  s.icap = (uint32_t)((2ull * e->group_max + 1ull) * (cfg->segment_bytes / cfg->index_interval) + 2ull);
+  // (each batch adds at most ring - interval bytes to a partition): 2G + 1 rings' worth of entries
+  // (+2) keep every entry stage 4 may read from being overwritten in time; (2G + 2) per interval
+  // of ring covers that for every ring of at least 4 intervals
+  s.icap_mul = 2u * e->group_max + 2u;
+  s.rstride = cfg->pool_bytes ? cfg->pool_bytes : (uint64_t)P * cfg->segment_bytes;
+  e->pool.size = s.rstride;
+  e->ring.assign(P, 0);
+  for (uint32_t p = 0; p < P; ++p) {  // every partition starts with a segment_bytes ring
+    uint64_t off = 0;
+    const uint32_t lg = ilog2(cfg->segment_bytes);
+    if (!e->pool.alloc(lg, &off)) {
+      free_engine(e);
+      return RMQ_EINVAL;
+    }
+    e->ring[p] = off | lg;
+  }
   for (StateSet& z : e->sets) {
     CREATE_TRY(dalloc(&z.leo, P));
     CREATE_TRY(dalloc(&z.used, P));
@@ -508,8 +521,10 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.match, (size_t)P * RF));
   CREATE_TRY(dalloc(&s.is_leader, P));
   CREATE_TRY(dalloc(&s.local_mask, P));
-  CREATE_TRY(dalloc(&s.index, (size_t)P * s.icap * 2));
-  CREATE_TRY(dalloc(&s.logs, (size_t)RF * P * s.seg));
+  CREATE_TRY(dalloc(&s.index, (size_t)(s.rstride >> s.interval_log2) * s.icap_mul * 2));
+  CREATE_TRY(dalloc(&s.logs, (size_t)RF * s.rstride));
+  CREATE_TRY(dalloc(&s.ring, P));
+  CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&e->d_err, 1));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
@@ -648,6 +663,82 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   launch_become_leader(e->st, pidx, e->main_s);
   HIP_TRY(hipGetLastError());
   return drain(e);
+}
+
+int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* seg) {
+  if (!e) return RMQ_EINVAL;
+  if (!n) return RMQ_OK;
+  if (!pidx || !seg) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> fg(e->fetch_mu);  // no fetch reads a ring while it moves
+  std::lock_guard<std::mutex> g(e->mu);
+  const uint32_t P = e->cfg.num_partitions, ilog = e->st.interval_log2;
+  std::vector<uint8_t> seen(P, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (pidx[i] >= P) return RMQ_ENOPART;
+    if (seen[pidx[i]]++ || !is_pow2(seg[i]) || seg[i] < 4ull * e->cfg.index_interval || seg[i] > e->st.rstride)
+      return RMQ_EINVAL;
+  }
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = drain(e);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->fetch_s));
+  // new rings first, all or nothing
+  std::vector<MigrateItem> items;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = pidx[i], lg = ilog2(seg[i]);
+    if ((e->ring[p] & 63ull) == lg) continue;
+    uint64_t off = 0;
+    if (!e->pool.alloc(lg, &off)) {
+      for (const MigrateItem& it : items) e->pool.release((uint32_t)(it.new_desc & 63ull), it.new_desc & ~63ull);
+      return RMQ_ENOMEM;
+    }
+    MigrateItem it{};
+    it.p = p;
+    it.old_desc = e->ring[p];
+    it.new_desc = off | lg;
+    items.push_back(it);
+  }
+  if (items.empty()) return RMQ_OK;
+  // retained range of every moved partition; a shrinking ring first applies retention at its new
+  // size (FORMAT.md §4: start = the first record at or after used - S', from the index)
+  std::vector<uint64_t> spos(P), soff(P), used(P);
+  HIP_TRY(hipMemcpy(spos.data(), e->st.start_pos, (size_t)P * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(soff.data(), e->st.start_off, (size_t)P * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(used.data(), e->st.used, (size_t)P * 8, hipMemcpyDeviceToHost));
+  for (MigrateItem& it : items) {
+    const uint64_t S1 = 1ull << (it.new_desc & 63ull);
+    const uint32_t p = it.p;
+    if (used[p] - spos[p] > S1) {
+      const uint64_t m = (used[p] - S1 + (1ull << ilog) - 1) >> ilog;
+      const RingRef o = ring_ref(it.old_desc, ilog, e->st.icap_mul);
+      uint64_t ent[2];
+      HIP_TRY(hipMemcpy(ent, e->st.index + (o.ibase + m % o.icap) * 2, 16, hipMemcpyDeviceToHost));
+      soff[p] = ent[0];
+      spos[p] = ent[1];
+    }
+    it.spos = spos[p];
+    it.soff = soff[p];
+    it.used = used[p];
+  }
+  MigrateItem* d_items = nullptr;
+  rc = dalloc(&d_items, items.size());
+  if (!rc) {
+    HIP_TRY(hipMemcpy(d_items, items.data(), items.size() * sizeof(MigrateItem), hipMemcpyHostToDevice));
+    launch_migrate(e->st, d_items, (uint32_t)items.size(), e->main_s);
+    if (hipGetLastError() != hipSuccess) rc = RMQ_EDEVICE;
+  }
+  if (!rc) {
+    for (const MigrateItem& it : items) {
+      e->ring[it.p] = it.new_desc;
+      e->pool.release((uint32_t)(it.old_desc & 63ull), it.old_desc & ~63ull);
+    }
+    HIP_TRY(hipStreamSynchronize(e->main_s));
+    rc = check_err(e);
+  } else {
+    for (const MigrateItem& it : items) e->pool.release((uint32_t)(it.new_desc & 63ull), it.new_desc & ~63ull);
+  }
+  if (d_items) hipFree(d_items);
+  return rc;
 }
 
 int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_t* ticket) {
@@ -1016,6 +1107,7 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   for (uint32_t r = 0; r < RF; ++r) o->replica_rank[r] = e->ranks[(size_t)p * RF + r];
   o->leader_slot = e->leader_slot[p];
   o->is_leader = e->is_leader[p];
+  o->segment_bytes = 1ull << (e->ring[p] & 63ull);
   return RMQ_OK;
 }
 
@@ -1023,14 +1115,14 @@ int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t p, uint64_t ring_
   if (!e || (len && !out)) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
-  const uint64_t S = e->cfg.segment_bytes;
-  if (replica >= e->cfg.replication_factor || ring_off > S || len > S - ring_off) return RMQ_EINVAL;
+  const RingRef rg = ring_ref(e->ring[p], e->st.interval_log2, e->st.icap_mul);
+  if (replica >= e->cfg.replication_factor || ring_off > rg.seg || len > rg.seg - ring_off) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = quiesce(e);
   if (rc) return rc;
   if (len)
-    HIP_TRY(hipMemcpy(out, e->st.logs + ((uint64_t)replica * e->cfg.num_partitions + p) * S + ring_off,
-                      len, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out, e->st.logs + (uint64_t)replica * e->st.rstride + rg.base + ring_off, len,
+                      hipMemcpyDeviceToHost));
   return RMQ_OK;
 }
 
@@ -1038,13 +1130,14 @@ int rmq_read_index(rmq_engine* e, uint32_t p, uint64_t m_first, uint64_t count, 
   if (!e || (count && !out)) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
-  const uint32_t icap = e->st.icap;
+  const RingRef rg = ring_ref(e->ring[p], e->st.interval_log2, e->st.icap_mul);
+  const uint32_t icap = rg.icap;
   if (count > icap) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = quiesce(e);
   if (rc) return rc;
   std::vector<uint64_t> ring((size_t)icap * 2);
-  HIP_TRY(hipMemcpy(ring.data(), e->st.index + (size_t)p * icap * 2, ring.size() * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(ring.data(), e->st.index + rg.ibase * 2, ring.size() * 8, hipMemcpyDeviceToHost));
   for (uint64_t k = 0; k < count; ++k) {
     const uint64_t sl = (m_first + k) % icap;
     out[2 * k] = ring[2 * sl];

@@ -99,6 +99,40 @@ struct Replication {
 
 }  // namespace rmq
 
+namespace rmq {
+// Ring space of the pool (FORMAT.md §2): power-of-two blocks aligned to their size, free lists per
+// size class, blocks split from larger free ones or cut from the unused tail; no coalescing.
+struct SegPool {
+  uint64_t size = 0, bump = 0;
+  std::vector<uint64_t> free[64];
+  void give(uint64_t off, uint64_t end) {  // [off, end) into the free lists as aligned blocks
+    while (off < end) {
+      uint32_t lg = off ? (uint32_t)__builtin_ctzll(off) : 63u;
+      while ((1ull << lg) > end - off) --lg;
+      free[lg].push_back(off);
+      off += 1ull << lg;
+    }
+  }
+  bool alloc(uint32_t lg, uint64_t* off) {
+    for (uint32_t k = lg; k < 64; ++k) {
+      if (free[k].empty()) continue;
+      const uint64_t o = free[k].back();
+      free[k].pop_back();
+      for (uint32_t q = k; q > lg; --q) free[q - 1].push_back(o + (1ull << (q - 1)));  // split
+      *off = o;
+      return true;
+    }
+    const uint64_t a = (bump + (1ull << lg) - 1) & ~((1ull << lg) - 1);
+    if (a + (1ull << lg) > size) return false;
+    give(bump, a);
+    bump = a + (1ull << lg);
+    *off = a;
+    return true;
+  }
+  void release(uint32_t lg, uint64_t off) { free[lg].push_back(off); }
+};
+}  // namespace rmq
+
 struct rmq_engine {
   rmq_config cfg{};
   std::mutex mu;
@@ -112,6 +146,8 @@ struct rmq_engine {
   CrcConsts* d_crc = nullptr;
   uint32_t* d_err = nullptr;
   uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
+  rmq::SegPool pool;         // ring space of each replica region
+  std::vector<uint64_t> ring;  // [P] host copy of DevState::ring
   uint32_t max_tasks = 0;
   uint32_t max_tiles = 0;
   uint32_t key_passes = 0;

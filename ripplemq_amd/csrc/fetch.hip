@@ -26,6 +26,7 @@ constexpr u32 kFW = 4;  // waves per workgroup (resolve, gather)
 
 struct PartView {
   u64 leo, used, start_off, start_pos;
+  RingRef rg;           // the partition's ring and index ring
   const uint8_t* ring;  // lowest local replica ring of the partition
 };
 
@@ -36,7 +37,7 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   const u64 t = h ? t1 : t0;
   const u32 ilog = st.interval_log2;
   const u64 I = 1ull << ilog;
-  const u64* E = st.index + (u64)p * st.icap * 2;
+  const u64* E = st.index + v.rg.ibase * 2;
   // per half: largest m in [lo, hi] with E[m].offset <= t (E rises with m), 32 probes per round;
   // none: the log start
   u64 c_off = v.start_off, c_pos = v.start_pos;
@@ -49,7 +50,7 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
     bool le = false;
     u64 eo = 0, ep = 0;
     if (open && m <= hi) {
-      const u64* e = E + ((u64)m % st.icap) * 2;
+      const u64* e = E + ((u64)m % v.rg.icap) * 2;
       eo = e[0];
       ep = e[1];
       le = eo <= t;
@@ -76,7 +77,7 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   if (t >= v.leo) return v.used;
   // walk the headers of the records in [c_off, t): they start in the interval after c_pos, so one
   // 1 KiB window of 16-byte pieces holds them all (two pieces per lane of the half)
-  const u64 mask = st.seg - 1;
+  const u64 mask = v.rg.seg - 1;
   const u32 Lw0 = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 32ull * hl + 8ull) & mask));
   const u32 Lw1 = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 32ull * hl + 24ull) & mask));
   u64 k = t - c_off;
@@ -123,7 +124,8 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
       } else {
         const u32 lm = st.local_mask[p];
         const u32 r0 = lm ? (u32)__ffs(lm) - 1u : 0u;
-        ring_off = ((u64)r0 * st.P + p) * st.seg;
+        v.rg = ring_ref(st, p);
+        ring_off = (u64)r0 * st.rstride + v.rg.base;
         v.ring = st.logs + ring_off;
         const u64 pp = record_pos2(st, p, v, off, end);
         pos0 = __shfl(pp, 0, 64);
@@ -137,7 +139,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
     a.res[4 * r + 2] = count | (bytes << 32);
     a.res[4 * r + 3] = (u64)(uint32_t)status;
     a.aux[2 * r + 0] = pos0;
-    a.aux[2 * r + 1] = ring_off;
+    a.aux[2 * r + 1] = (ring_off << 6) | (st.ring[p < st.P ? p : 0] & 63ull);  // ring | log2(ring bytes)
     a.cpre[r] = (u32)bytes;
   }
 }
@@ -207,14 +209,14 @@ __global__ __launch_bounds__(1024) void fetch_place_kernel(FetchArgs a) {
 
 __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   const DevState& st = a.st;
-  const u64 mask = st.seg - 1;
   const u32 lane = lane_id();
   const u32 nw = gridDim.x * kFW;
   for (u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6)); r < a.n; r += nw) {
     const u64 nb = a.res[4 * r + 2] >> 32;  // 0 for requests not served
     if (!nb) continue;
     const u64 pos0 = a.aux[2 * r + 0];
-    const uint8_t* ring = st.logs + a.aux[2 * r + 1];
+    const uint8_t* ring = st.logs + (a.aux[2 * r + 1] >> 6);
+    const u64 mask = (1ull << (a.aux[2 * r + 1] & 63ull)) - 1ull;
     uint8_t* out = a.out + a.opos[r];
     const u64 pieces = nb >> 4;
     u64 q = lane;

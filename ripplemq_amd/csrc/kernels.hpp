@@ -65,15 +65,38 @@ struct DevState {
   uint64_t* match;       // [P][RF]
   uint32_t* is_leader;   // 0/1
   uint32_t* local_mask;  // bit r set: replica slot r is stored on this device
-  uint64_t* index;       // [P][icap][2] sparse offset index {offset, pos}
-  uint8_t* logs;         // [RF][P][seg] ring segments
+  uint64_t* index;       // sparse offset index {offset, pos}: partition p's ring of entries at RingRef.ibase
+  uint8_t* logs;         // [RF][pool] replica regions; partition p's ring at RingRef.base in each
+  uint64_t* ring;        // [P] ring descriptor: byte offset in the pool | log2(ring bytes) (bits 0..5)
   uint64_t* cons;        // [P][C] consumer offsets
+  uint64_t rstride;      // bytes per replica region (the pool)
   uint32_t P, RF, C;
-  uint32_t icap;         // index ring entries per partition
-  uint64_t seg;          // ring bytes (power of two)
+  uint32_t icap_mul;     // index entries per interval of ring (2 * group + 2)
   uint32_t interval_log2;
   uint32_t pad;
 };
+
+// Where partition p's ring and index live (FORMAT.md §2, §5). A ring of S bytes sits at a multiple
+// of S inside each replica region; its index ring holds icap_mul * S / I entries at a proportional
+// offset of the index pool, so rings and index rings never overlap.
+struct RingRef {
+  uint64_t base;   // byte offset of the ring inside a replica region
+  uint64_t seg;    // ring bytes (power of two)
+  uint64_t ibase;  // first index entry of the partition
+  uint32_t icap;   // index ring entries
+};
+
+__host__ __device__ __forceinline__ RingRef ring_ref(uint64_t desc, uint32_t interval_log2, uint32_t icap_mul) {
+  RingRef r;
+  r.seg = 1ull << (desc & 63ull);
+  r.base = desc & ~63ull;
+  r.ibase = (r.base >> interval_log2) * icap_mul;
+  r.icap = icap_mul * (uint32_t)(r.seg >> interval_log2);
+  return r;
+}
+__host__ __device__ __forceinline__ RingRef ring_ref(const DevState& st, uint32_t p) {
+  return ring_ref(st.ring[p], st.interval_log2, st.icap_mul);
+}
 
 // Double-buffered per-partition log end: the apply of group #a reads set a&1 and writes set
 // (a+1)&1, so records can read their partition's group-start state while its new one is written.
@@ -135,7 +158,6 @@ struct PipeArgs {
   uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2
-  uint64_t nospace_limit;  // segment - interval: record bytes one batch may add to one partition
   // replication transport attached (else all null / n_out = 0)
   XPlanArgs xp2;           // stage 2's group: outbox plan
   const uint32_t* outidx;  // [P][RF] out entry of (partition, slot), ~0: local or no entry
@@ -204,6 +226,15 @@ struct AckApplyArgs {
   const uint64_t* ackin;
 };
 
+// One partition's ring moving to a new block of the pool (rmq_set_segments): the retained log
+// [spos, used) of every replica slot and its index entries are copied; the new block is zeroed first.
+struct MigrateItem {
+  uint32_t p, pad;
+  uint64_t old_desc, new_desc;  // DevState::ring descriptors
+  uint64_t spos, used;          // retained log [spos, used) after the move
+  uint64_t soff;                // offset of the record at spos
+};
+
 // launchers (defined in the .hip files)
 void launch_pipeline(const PipeArgs& a, hipStream_t s);
 uint32_t pipeline_lds_bytes();
@@ -215,6 +246,7 @@ void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev_resolve0, hip
                   hipEvent_t ev_gather0, hipEvent_t ev_gather1);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s);
+void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, hipStream_t s);
 void launch_ack_apply(const AckApplyArgs& a, hipStream_t s);
 
 }  // namespace rmq

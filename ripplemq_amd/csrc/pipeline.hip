@@ -472,9 +472,10 @@ __device__ void stage2(const PipeArgs& A, u32 wg) {
   // ---- column scans: kScanLanes consecutive threads share a partition column (contiguous in
   // hist / excl); per batch, blocks of 8 * kScanLanes tiles, thread s holding tiles [8s, 8s + 8)
   const u32 s = tid % kScanLanes;
-  const u64 lim16 = A.nospace_limit >> 4;  // record bytes / 16 a (batch, partition) may add
   for (u32 g = wg * kPT + tid; g < P * kScanLanes; g += A.wg2 * kPT) {  // whole columns per group
     const u32 p = g / kScanLanes;
+    // record bytes / 16 one batch may add to p: its ring less one index interval (FORMAT.md §3)
+    const u64 lim16 = ((1ull << (A.st.ring[p] & 63ull)) - (1ull << A.st.interval_log2)) >> 4;
     u64* const col = x.hist + (u64)p * GT;
     u64* const ecol = x.excl + (u64)p * GT;
     u64 carry = 0;
@@ -598,6 +599,7 @@ __device__ __forceinline__ u32 task_rec(const TaskPos& T) { return T.i0 + ((thre
 struct TaskState {  // round 2: partition state of the record and its first round of payload blocks
   u64 ex, leo, used;
   u64 gend;        // the partition's log end position after the whole group
+  u64 rdesc;       // the partition's ring descriptor (DevState::ring)
   u32 lm, lead;
   uint4 blk[kBL];
 };
@@ -647,6 +649,7 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   const DevState& st = A.st;
   TaskState S;
   S.ex = S.leo = S.used = S.gend = 0ull;
+  S.rdesc = 8ull;  // any valid descriptor (a 256-byte ring at 0) for lanes that store nothing
   S.lm = S.lead = 0u;
   if (cand) {
     const u32 p = R.p;
@@ -658,6 +661,7 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
     S.used = A.cur.used[p];
     S.gend = S.used + 16ull * (tot & kLow40);
     S.lm = st.local_mask[p];
+    S.rdesc = st.ring[p];
   }
   // first round of payload blocks, speculatively (leadership is checked before any store)
   round_blocks(A, R, 0u, cand, S.blk);
@@ -677,7 +681,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   const PipeBatch& b = A.g3.b[T.jb];
   const DevState& st = A.st;
   const u32 lane = threadIdx.x & 63, j = lane & 1u;
-  const u32 P = st.P, RF = st.RF;
+  const u32 RF = st.RF;
   const u32 i = task_rec(T);
   const bool in = i < b.n;
   const u32 p = R.p, L = R.L;
@@ -686,14 +690,15 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   const bool ns = (Z.ex & kExclNoSpace) != 0ull;  // the record's (batch, partition) is over its limit
   const bool ok = cand && Z.lead != 0u && !ns;
   const u32 m = (L + 15u) >> 4;  // payload pieces
-  const u64 segmask = st.seg - 1ull;
-  const u64 rstride = (u64)P * st.seg;
+  const RingRef rg = ring_ref(Z.rdesc, st.interval_log2, st.icap_mul);
+  const u64 segmask = rg.seg - 1ull;
+  const u64 rstride = st.rstride;
   const u64 off = Z.leo + ((Z.ex >> 40) & kCnt23) + (R.cr.x & kRankMask);
   const u64 pos = Z.used + 16ull * ((Z.ex & kLow40) + R.cr.y);
   // pieces (0 = header, k = payload piece k - 1 at pos + 16k) whose ring slot a later piece of the
   // same group overwrites (pos + 16k + seg < group end) are dead: not stored
-  const u32 dead = Z.gend > pos + st.seg ? (u32)min((Z.gend - st.seg - pos) >> 4, (u64)m + 1ull) : 0u;
-  uint8_t* const ring = st.logs + (u64)p * st.seg;
+  const u32 dead = Z.gend > pos + rg.seg ? (u32)min((Z.gend - rg.seg - pos) >> 4, (u64)m + 1ull) : 0u;
+  uint8_t* const ring = st.logs + rg.base;
   const u32 lmw = (A.debug & 1u) ? 0u : Z.lm;
   const u32 sa = (u32)(R.src & 15u);
   u32 acc = 0;
@@ -774,19 +779,23 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   }
   if (img) {
     if (j == 1) W.img[w][r32][0] = h;
+    // the 4-bit piece count is only meaningful for a stored record (ok implies m <= 7 here); a
+    // rejected record may be long, and its count must not spill into the flag bits
     if (j == 0)
-      W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), p, Z.lm | (m << 8) | ((ok ? 1u : 0u) << 16) | (dead << 24));
+      W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), (u32)(rg.base >> 8),
+                                  ok ? Z.lm | (m << 8) | (1u << 12) | (dead << 13) | ((u32)(Z.rdesc & 63ull) << 24) : 0u);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (u32 s4 = 0; s4 < kTaskRecs * 8u / 64u; ++s4) {
       const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
       const uint4 inf = W.info[w][rr];
-      const u32 mr = (inf.w >> 8) & 0xFFu;
-      if (((inf.w >> 16) & 1u) && k <= mr) {
+      const u32 mr = (inf.w >> 8) & 0xFu;
+      if (((inf.w >> 12) & 1u) && k <= mr) {
         const uint4 v = W.img[w][rr][k];
-        if (k >= (inf.w >> 24)) {
+        if (k >= ((inf.w >> 13) & 0x1Fu)) {
           const u64 rpos = ((u64)inf.y << 32) | inf.x;
-          uint8_t* dst = st.logs + (u64)inf.z * st.seg + ((rpos + 16ull * k) & segmask);
+          const u64 rmask = (1ull << (inf.w >> 24)) - 1ull;
+          uint8_t* dst = st.logs + ((u64)inf.z << 8) + ((rpos + 16ull * k) & rmask);
           const u32 lmr = (A.debug & 1u) ? 0u : (inf.w & 0xFFu);
           for (u32 r = 0; r < RF; ++r)
             if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
@@ -809,7 +818,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   const u64 end = pos + 16ull * (1ull + m);
   if (ok && j == 1) {
     for (u64 mm = (pos >> ilog) + 1; (mm << ilog) <= end; ++mm) {
-      u64* e = st.index + ((u64)p * st.icap + mm % st.icap) * 2;
+      u64* e = st.index + (rg.ibase + mm % rg.icap) * 2;
       e[0] = off + 1;
       e[1] = end;
     }
@@ -881,13 +890,14 @@ __device__ void partition_retention(const PipeArgs& A, u32 p) {
   const u32 ilog = st.interval_log2;
   const u64 soff0 = st.start_off[p], spos0 = st.start_pos[p];
   u64 soff = soff0, spos = spos0, prev = 0;
+  const RingRef rg = ring_ref(st, p);
   for (u32 j = 0; j < A.g4.nb; ++j) {
     const u64 c = x.bcum[(u64)j * st.P + p];
     if ((c >> 40) != (prev >> 40)) {  // batch j appended records of p
       const u64 fin = fin_g - 16ull * ((gtot - c) & kLow40);
-      if (fin - spos > st.seg) {
-        const u64 ms = (fin - st.seg + (1ull << ilog) - 1) >> ilog;
-        const u64* e = st.index + ((u64)p * st.icap + ms % st.icap) * 2;
+      if (fin - spos > rg.seg) {
+        const u64 ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
+        const u64* e = st.index + (rg.ibase + ms % rg.icap) * 2;
         soff = e[0];
         spos = e[1];
       }

@@ -103,14 +103,15 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   // j, j + 2, ... by Horner's rule with the 32-byte zero-shift table
   const u32 mm = ok ? m : 0u;
   u32 acc = 0;
-  uint8_t* const ring = st.logs + ((u64)(in ? A.xi_slot[e] : 0u) * st.P + p) * st.seg;
-  const u64 segmask = st.seg - 1ull;
+  const RingRef rg = ring_ref(st, p);  // p = 0 for lanes without a record (nothing is stored)
+  uint8_t* const ring = st.logs + (u64)(in ? A.xi_slot[e] : 0u) * st.rstride + rg.base;
+  const u64 segmask = rg.seg - 1ull;
   for (u32 c = 0; __any(c < (mm + 1u) / 2u); ++c) {
     const u32 jp = 2u * c + j;
     if (jp < mm) {
       uint4 v = *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * jp);
       const u64 x = pos + 16ull + 16ull * jp;
-      if (x + st.seg >= gend) store_log16(ring + (x & segmask), v);
+      if (x + rg.seg >= gend) store_log16(ring + (x & segmask), v);
       if (jp == 0) v.x ^= 0xFFFFFFFFu;
       acc = crc_zshift(z[1], acc) ^ crc_piece16(t8, v);
     }
@@ -125,12 +126,12 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
     }
     ok = crc == hdr.w;
     if (ok) {
-      if (pos + st.seg >= gend) store_log16(ring + (pos & segmask), hdr);
+      if (pos + rg.seg >= gend) store_log16(ring + (pos & segmask), hdr);
       if (owner) {  // sparse index: every multiple of the interval the record crosses names the next record
         const u32 ilog = st.interval_log2;
         const u64 end = pos + 16ull * (1ull + m);
         for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end; ++q) {
-          u64* ie = st.index + ((u64)p * st.icap + q % st.icap) * 2;
+          u64* ie = st.index + (rg.ibase + q % rg.icap) * 2;
           ie[0] = off + 1;
           ie[1] = end;
         }
@@ -176,9 +177,10 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
             A.sets[s].used[p] = used;
           }
           // retention once per round (FORMAT.md §4 rule on the follower's log)
-          if (used - st.start_pos[p] > st.seg) {
-            const u64 ms = (used - st.seg + (1ull << st.interval_log2) - 1) >> st.interval_log2;
-            const u64* ie = st.index + ((u64)p * st.icap + ms % st.icap) * 2;
+          const RingRef rg = ring_ref(st, p);
+          if (used - st.start_pos[p] > rg.seg) {
+            const u64 ms = (used - rg.seg + (1ull << st.interval_log2) - 1) >> st.interval_log2;
+            const u64* ie = st.index + (rg.ibase + ms % rg.icap) * 2;
             st.start_off[p] = ie[0];
             st.start_pos[p] = ie[1];
           }

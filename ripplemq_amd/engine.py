@@ -49,6 +49,7 @@ class EngineConfig:
     max_batch_bytes: int = 64 << 20
     device: int = 0
     rank: int = 0
+    pool_bytes: int = 0              # ring bytes per replica shared by all partitions (0: P * segment)
 
     def to_c(self) -> A.RmqConfig:
         c = A.RmqConfig()
@@ -63,6 +64,7 @@ def state_to_dict(s: A.RmqPartitionState, rf: int) -> dict:
     d["replica_rank"] = [int(s.replica_rank[r]) for r in range(rf)]
     d["leader_slot"] = int(s.leader_slot)
     d["is_leader"] = int(s.is_leader)
+    d["segment_bytes"] = int(s.segment_bytes)
     return d
 
 
@@ -227,6 +229,14 @@ class Engine:
             raise EngineError(rc, "rmq_fetch")
         return rc, res, int(used.value)
 
+    def set_segments(self, pidx, segment_bytes) -> None:
+        """Ring sizes of partitions pidx[i] (rmq_set_segments: retention at a smaller size first, the
+        retained log keeps its offsets and positions)."""
+        p = np.ascontiguousarray(pidx, np.uint32)
+        sb = np.ascontiguousarray(segment_bytes, np.uint64)
+        _check(self.lib.rmq_set_segments(self.h, len(p), p.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                         sb.ctypes.data_as(C.POINTER(C.c_uint64))), "rmq_set_segments")
+
     # ---- read-back
     def state(self, pidx: int) -> dict:
         s = A.RmqPartitionState()
@@ -234,7 +244,7 @@ class Engine:
         return state_to_dict(s, self.cfg.replication_factor)
 
     def read_segment(self, replica: int, pidx: int, ring_off: int = 0, n: int | None = None) -> np.ndarray:
-        n = self.cfg.segment_bytes - ring_off if n is None else n
+        n = self.state(pidx)["segment_bytes"] - ring_off if n is None else n
         out = np.empty(n, np.uint8)
         _check(self.lib.rmq_read_segment(self.h, replica, pidx, ring_off, n, _ptr(out)), "rmq_read_segment")
         return out

@@ -11,6 +11,7 @@ int main(void) {
   printf("rmq_partition_state %zu\n", sizeof(rmq_partition_state));
   printf("rmq_append_stats %zu\n", sizeof(rmq_append_stats));
   F(rmq_config, segment_bytes); F(rmq_config, max_batch_bytes); F(rmq_config, device); F(rmq_config, rank);
+  F(rmq_config, pool_bytes); F(rmq_partition_state, segment_bytes);
   F(rmq_batch, pidx); F(rmq_batch, payload_bytes);
   F(rmq_fetch_res, count); F(rmq_fetch_res, status);
   F(rmq_partition_state, match); F(rmq_partition_state, replica_rank); F(rmq_partition_state, is_leader);

@@ -49,6 +49,56 @@ def test_retention_wraps_ring(oracle_mod):
         assert max(starts) > 0, "scenario must exercise retention"
 
 
+def test_set_segments_grow_shrink_in_pool(oracle_mod):
+    # rmq_set_segments (FORMAT.md §2): the hot Zipf partitions grow 4x inside the shared pool, cold
+    # ones shrink (retention at the new size first); appends, retention, fetch and consumer commits
+    # then continue bit-exact with the oracle, and every ring is compared whole (zeros outside the
+    # retained log)
+    P, S = 32, 1 << 16
+    cfg, dev, ora = pair(oracle_mod, num_partitions=P, replication_factor=3, segment_bytes=S,
+                         index_interval=1024, max_batch_records=4096, pool_bytes=3 * P * S)
+    with dev, ora:
+        spec = StreamSpec(P, 3000, "zipf", size=(1, 300), config_index=56)
+        first = [make_batch(spec, b) for b in range(5)]
+        load = np.bincount(np.concatenate([b.pidx for b in first]), minlength=P)
+        order = np.argsort(-load, kind="stable")
+        hot, cold = order[:4], order[-6:]
+        grow = ("set_segments", hot, np.full(4, 4 * S, np.uint64))
+        shrink = ("set_segments", np.concatenate([cold, order[4:6]]), np.full(8, 4096, np.uint64))
+        pp = np.arange(P, dtype=np.uint32)
+        ops = [("append", b) for b in first] + [grow, shrink]
+        ops += [("append", make_batch(spec, b)) for b in range(5, 12)]
+        ops += [("consumer_commit", pp, np.zeros(P, np.uint32), pp * 7),
+                ("fetch", pp, np.zeros(P, np.uint32), np.full(P, 64, np.uint32))]
+        ops += [("set_segments", hot[:2], np.full(2, S, np.uint64))]  # shrink two grown rings back
+        ops += [("append", make_batch(spec, b)) for b in range(12, 14)]
+        run_ops(dev, ora, cfg, ops, full_rings=True)
+        segs = [ora.state(p)["segment_bytes"] for p in range(P)]
+        assert sorted(set(segs)) == [4096, S, 4 * S], segs
+        assert ora.state(int(order[4]))["log_start_offset"] > 0, "a shrink must apply retention"
+
+
+def test_set_segments_pool_exhausted_changes_nothing():
+    # all or nothing: a pool without room for the new rings answers RMQ_ENOMEM and leaves every ring
+    P, S = 16, 1 << 14
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=S, index_interval=1024,
+                       max_batch_records=2048, pool_bytes=P * S + 4 * S)
+    spec = StreamSpec(P, 1000, "uniform", size=(1, 100), config_index=57)
+    from ripplemq_amd.engine import EngineError
+    with Engine(cfg) as dev:
+        b = make_batch(spec, 0)
+        dev.append(b.pidx, b.lens, b.payload)
+        before = [dev.state(p) for p in range(P)]
+        rings = [dev.read_segment(0, p) for p in range(P)]
+        with pytest.raises(EngineError) as ex:
+            dev.set_segments(np.arange(3, dtype=np.uint32), np.full(3, 4 * S, np.uint64))
+        assert "ENOMEM" in str(ex.value)
+        assert [dev.state(p) for p in range(P)] == before
+        assert all(np.array_equal(dev.read_segment(0, p), r) for p, r in enumerate(rings))
+        dev.set_segments(np.arange(1, dtype=np.uint32), np.full(1, 4 * S, np.uint64))  # one fits
+        assert dev.state(0)["segment_bytes"] == 4 * S
+
+
 def test_large_records_direct_path(oracle_mod):
     # log-uniform 64 B..16 KB (config D sizes): records longer than 112 B skip the LDS log image
     # and are stored piece by piece; long payloads take many Horner rounds per lane
@@ -91,6 +141,22 @@ def test_no_space_and_edge_batches(oracle_mod):
         ok = make_batch(StreamSpec(4, 100, "uniform", size=(0, 20), config_index=16), 1)
         run_ops(dev, ora, cfg, [("append", empty), ("append", one), ("append", big), ("append", ok),
                                 ("append", ok), ("append", big)], full_rings=True)
+
+
+def test_rejected_long_records_next_to_short_ones(oracle_mod):
+    # a wave whose stored records are all short (the LDS-image store path) but which also holds
+    # rejected long records (no space): their piece counts must not turn into store flags
+    cfg, dev, ora = pair(oracle_mod, num_partitions=2, replication_factor=2, segment_bytes=1 << 12,
+                         index_interval=64, max_batch_records=4096)
+    with dev, ora:
+        g = np.random.default_rng(11)
+        n = 192
+        pidx = (np.arange(n) & 1).astype(np.uint32)                   # 0, 1, 0, 1, ...
+        lens = np.where(pidx == 0, g.integers(241, 600, n), g.integers(0, 20, n)).astype(np.uint32)
+        b = Batch(pidx, lens, g.integers(0, 256, int(lens.sum()), dtype=np.uint8))
+        small = make_batch(StreamSpec(2, 60, "uniform", size=(0, 40), config_index=18), 0)
+        run_ops(dev, ora, cfg, [("append", small), ("append", b), ("append", small), ("append", b)],
+                full_rings=True)
 
 
 def test_explicit_payload_offsets(oracle_mod):
