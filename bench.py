@@ -44,14 +44,52 @@ sys.path.insert(0, REPO)
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
 from ripplemq_amd.engine import Engine, EngineConfig, rccl_unique_id  # noqa: E402
 from ripplemq_amd.sharding import max_over_ranks, rank_view  # noqa: E402
+from ripplemq_amd.rings import partition_traffic, pool_layout, ring_sizes  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+INDEX_INTERVAL = 1024
+RING_FLOOR = 64 << 10  # smallest ring of the load policy
 XGMI_LINK_GBS = 153.0  # one xGMI link, one direction; 7 per GPU in an 8-GPU node
 
 
-def algorithmic_bytes(n: int, L: int, rf: int, P: int) -> int:
-    return n * ((8 + L) + rf * (16 + L)) + P * (rf * 8 + 16)
+def algorithmic_bytes(n: int, payload: float, rf: int, P: int) -> float:
+    """Per batch of n records carrying `payload` bytes: (8 + L) read and RF (16 + L) written per
+    record, RF * 8 + 16 per partition."""
+    return n * (8 + rf * 16) + (1 + rf) * payload + P * (rf * 8 + 16)
+
+
+def ring_plan(args, spec: StreamSpec, batches, view) -> dict:
+    """Ring bytes of every local partition (ripplemq_amd.rings): --rings load sizes each ring from
+    the traffic of the rank's input batches (retain --retain-batches batches of the partition's
+    mean traffic, a 64 KiB floor); --rings equal gives every partition --segment-mb. A follower
+    replica is sized like its leader (the Zipf ranking is the same on every rank)."""
+    P = len(view.gp)
+    if args.rings == "equal":
+        seg = (args.segment_mb or 4) << 20
+        return {"policy": "equal", "segment_bytes": seg, "pool_bytes": 0, "sizes": np.full(P, seg, np.uint64),
+                "grown": np.zeros(0, np.uint32), "grown_bytes": np.zeros(0, np.uint64)}
+    mean, peak = partition_traffic(batches, spec.partitions)
+    by_local = ring_sizes(mean, peak, args.retain_batches, RING_FLOOR, INDEX_INTERVAL,
+                          max_bytes=(args.segment_mb << 20) if args.segment_mb else 1 << 40)
+    lay = pool_layout(by_local[np.asarray(view.gp, np.int64) % spec.partitions])
+    sizes = np.maximum(by_local[np.asarray(view.gp, np.int64) % spec.partitions], np.uint64(lay.segment_bytes))
+    return {"policy": "load", "segment_bytes": lay.segment_bytes, "pool_bytes": lay.pool_bytes, "sizes": sizes,
+            "grown": lay.grown, "grown_bytes": lay.grown_bytes, "free_bytes": lay.free_bytes}
+
+
+def ring_report(rings: dict, rf: int, group: int, P: int) -> dict:
+    """HBM held by the logs and what the hottest partition retains, next to equal rings."""
+    sizes = rings["sizes"]
+    pool = rings["pool_bytes"] or int(sizes.sum())
+    equal_same = 1 << int(np.floor(np.log2(pool / P)))  # equal power-of-two rings in the same pool
+    index_bytes = (pool // INDEX_INTERVAL) * (2 * group + 2) * 16
+    return {"policy": rings["policy"], "pool_bytes_per_replica": pool, "ring_bytes_total": rf * pool,
+            "index_bytes": index_bytes, "hbm_total_bytes": rf * pool + index_bytes,
+            "ring_bytes_min": int(sizes.min()), "ring_bytes_hot": int(sizes.max()),
+            "partitions_grown": int((sizes > sizes.min()).sum()),
+            "equal_ring_same_pool": equal_same, "hot_retention_vs_equal_same_pool": int(sizes.max()) / equal_same,
+            "equal_16mib_total_bytes": rf * P * (16 << 20)}
 
 
 def pmc_traffic(group: int, config: str):
@@ -134,7 +172,9 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     cc = np.tile(np.arange(consumers, dtype=np.uint32), P)
     out = {}
     for mx in (10, 1024):
-        cap = P * consumers * mx * 128 + 4096
+        hi = spec.size if isinstance(spec.size, int) else spec.size[1]
+        retained = int(sum(s["log_end_pos"] - s["log_start_pos"] for s in st))
+        cap = min(P * consumers * mx * (16 + (hi + 15) // 16 * 16), consumers * retained) + 4096
         d_out = eng.device_alloc(cap)
         recs = nbytes = 0
         t_kern = t_wall = 0.0
@@ -240,24 +280,30 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     """One rank's engine, resident input pool, timed region and (rank 0) the JSON line."""
     rank, world = grp.rank, grp.world
     spec = CONFIGS[args.config]
-    rf = 3
+    rf = 5 if args.config == "D" else 3  # configs[4]: RF = 5
     L = spec.size if isinstance(spec.size, int) else None
-    seg_mb = args.segment_mb or 4
     view = rank_view(rank, world, spec.partitions, rf)  # world 1: every replica on this GPU
+    # the rank's distinct input batches (rank-salted stream keys), made before the engine so that
+    # the rings can be sized from their traffic
+    batches = [make_batch(spec, 1_000_000 * rank + q) for q in range(args.pool)]
+    max_payload = max(int(b.payload.nbytes) for b in batches)
+    rings = ring_plan(args, spec, batches, view)
     cfg = EngineConfig(num_partitions=len(view.gp), replication_factor=rf,
-                       segment_bytes=seg_mb << 20, index_interval=1024,
-                       max_batch_records=spec.records, max_batch_bytes=8 << 20,
+                       segment_bytes=rings["segment_bytes"], pool_bytes=rings["pool_bytes"],
+                       index_interval=INDEX_INTERVAL, max_batch_records=spec.records,
+                       max_batch_bytes=max(8 << 20, (max_payload + (1 << 20) - 1) >> 20 << 20),
                        pipeline_depth=args.group, device=device, rank=rank)
     eng = Engine(cfg)
     if world > 1:
         attach(eng, grp)
         eng.set_placement(np.arange(len(view.gp), dtype=np.uint32), view.gp, view.ranks, view.leader_slot)
+    if rings["grown"].size:  # collective with a transport: every rank grows its rings here
+        eng.set_segments(rings["grown"], rings["grown_bytes"])
     dev_name, cus = eng.device_info()
 
-    # resident input pool: distinct batches per rank (rank-salted stream keys)
+    # resident input pool
     pool = []
-    for q in range(args.pool):
-        b = make_batch(spec, 1_000_000 * rank + q)
+    for b in batches:
         d_pidx = eng.device_alloc(b.n * 4)
         d_len = eng.device_alloc(b.n * 4)
         d_pay = eng.device_alloc(max(b.payload.nbytes, 4))
@@ -265,6 +311,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
         eng.h2d(d_len, b.lens)
         eng.h2d(d_pay, b.payload)
         pool.append((b.n, d_pidx, d_len, d_pay, int(b.payload.nbytes), record_bytes(b.lens)))
+    mean_payload = float(np.mean([b.payload.nbytes for b in batches]))
+    del batches
     d_out = [eng.device_alloc(spec.records * 8) for _ in range(4)]
 
     def step(k: int) -> int:
@@ -308,7 +356,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     msgs_per_s = total_records / t_max
     out = None
     if rank == 0:
-        alg = algorithmic_bytes(n, L or 0, rf, spec.partitions)
+        alg = algorithmic_bytes(n, mean_payload, rf, spec.partitions)
         # algorithmic bytes per launch / mean launch duration = bytes of the applied batches / region
         achieved = alg * n_applied / (region_ms / 1e3) / 1e9 if n_launch and region_ms > 0 else 0.0
         traffic_b, traffic_src = pmc_traffic(args.group, args.config)
@@ -330,14 +378,15 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
             "data": "synthetic",
             "config": {"workload": f"config {args.config}: {spec.partitions} partitions/GPU, RF={rf}, "
                                    f"{spec.mode}{'(s=%.1f)' % spec.zipf_s if spec.mode == 'zipf' else ''}, "
-                                   f"{L} B records, {n} records/batch",
+                                   f"{L if L else '%d-%d' % spec.size} B records, {n} records/batch",
                        "partitions_per_gpu": spec.partitions, "replication_factor": rf,
                        "records_per_batch": n, "record_payload_bytes": L,
                        "parallelism": (f"partition-sharded x{world}, RF={rf} replicas over "
                                        + ("xGMI (RCCL)" if args.transport == "rccl" else
                                           "the in-process transport on ONE GPU (functional rehearsal)")
                                        if world > 1 else "1 GPU, RF=3 replicas co-located"),
-                       "batches_per_launch_group": args.group, "segment_mb": seg_mb},
+                       "batches_per_launch_group": args.group,
+                       "rings": ring_report(rings, rf, args.group, len(view.gp))},
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_per_batch": traffic_b,
@@ -367,7 +416,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     eng.close()
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(spec, rf, seg_mb << 20, args.cpu_budget, args.config)
+            out["cpu_baseline"] = cpu_baseline(spec, rf, 4 << 20, args.cpu_budget, args.config)
         else:
             out["cpu_baseline"] = None
     return out
@@ -380,10 +429,15 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
+    ap.add_argument("--rings", default="load", choices=["load", "equal"],
+                    help="load: ring per partition from its traffic in one shared pool (rmq_set_segments); "
+                         "equal: every ring --segment-mb (default 4)")
+    ap.add_argument("--retain-batches", type=float, default=64.0,
+                    help="load policy: batches of a partition's mean traffic its ring retains")
     ap.add_argument("--segment-mb", type=int, default=None,
-                    help="ring bytes per (replica, partition) [MiB]; default 4 (the hot Zipf partition takes "
-                         "~1.3 MB of a 64k x 128 B batch; 16 MiB rings span 192 GiB and the first launches of "
-                         "a process run up to 1.5x slower until the translation caches warm)")
+                    help="equal policy: ring bytes per (replica, partition) [MiB], default 4 (16 MiB rings span "
+                         "192 GiB and the first launches of a process run up to 1.5x slower until the "
+                         "translation caches warm); load policy: the largest ring [MiB]")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")

@@ -78,6 +78,28 @@ def test_set_segments_grow_shrink_in_pool(oracle_mod):
         assert ora.state(int(order[4]))["log_start_offset"] > 0, "a shrink must apply retention"
 
 
+def test_config_d_shape_in_load_sized_pool(oracle_mod):
+    # config D's shape on one GPU (RF 5, 4096 partitions, log-uniform 64 B..16 KB): rings sized from
+    # the traffic (ripplemq_amd.rings) in one pool of a few GiB, where equal 16 MiB rings need 320 GiB
+    from ripplemq_amd.rings import partition_traffic, pool_layout, ring_sizes
+    from ripplemq_amd.workload import CONFIGS
+    spec = CONFIGS["D"]
+    batches = [make_batch(spec, q) for q in range(4)]
+    mean, peak = partition_traffic(batches, spec.partitions)
+    lay = pool_layout(ring_sizes(mean, peak, 64, 64 << 10, 1024))
+    assert 5 * lay.pool_bytes < 16 << 30
+    cfg, dev, ora = pair(oracle_mod, num_partitions=spec.partitions, replication_factor=5,
+                         segment_bytes=lay.segment_bytes, pool_bytes=lay.pool_bytes, index_interval=1024,
+                         max_batch_records=spec.records, max_batch_bytes=64 << 20)
+    with dev, ora:
+        P = spec.partitions
+        g = np.random.default_rng(21)
+        pp = g.integers(0, P, 512).astype(np.uint32)
+        ops = [("set_segments", lay.grown, lay.grown_bytes)] + [("append", b) for b in batches]
+        ops += [("fetch", pp, np.zeros(512, np.uint32), g.integers(1, 6, 512).astype(np.uint32))]
+        run_ops(dev, ora, cfg, ops)
+
+
 def test_set_segments_pool_exhausted_changes_nothing():
     # all or nothing: a pool without room for the new rings answers RMQ_ENOMEM and leaves every ring
     P, S = 16, 1 << 14
