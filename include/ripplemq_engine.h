@@ -262,6 +262,10 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out);
 /* Region bytes of the last posted round for destination rank dst (FORMAT.md §9): *size gets its
    length; copied to out if out != NULL and cap suffices (tests, tools). */
 int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size);
+/* Fault injection (tests): the rounds of the next n launch groups this engine forms from batches
+   appended after the call send empty regions, as if the leader failed before replicating them
+   (its own log keeps the records; followers neither see nor ack them). Not collective. */
+int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n);
 
 /* ---- read-back (tests, tools) ---- */
 int rmq_get_partition_state(rmq_engine* e, uint32_t pidx, rmq_partition_state* out);

@@ -878,13 +878,14 @@ int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint
     const ro_part* s = &e->parts[v[k].p];
     uint8_t* d = out + 32 + 32ull * k;
     const uint32_t cnt = (uint32_t)s->round_count, by16 = (uint32_t)(s->round_bytes / 16);
-    const uint64_t first = cnt ? s->round_first : 0;
+    const uint64_t first = s->leo - s->round_count; /* the leader's log end before the round */
     const uint32_t ts = (uint32_t)t, ds = (uint32_t)b16;
     memcpy(d, &cnt, 4);
     memcpy(d + 4, &by16, 4);
     memcpy(d + 8, &first, 8);
     memcpy(d + 16, &ts, 4);
     memcpy(d + 20, &ds, 4);
+    memcpy(d + 24, &s->term, 8);
     uint64_t rel = 0;
     for (uint64_t r = 0; r < s->round_count; ++r) { /* record table: {entry, record position / 16} */
       uint32_t len;
@@ -906,15 +907,27 @@ void ro_end_round(ro_engine* e) {
   for (uint32_t p = 0; p < e->cfg.num_partitions; ++p) e->parts[p].round_bytes = e->parts[p].round_count = 0;
 }
 
+/* Follower: truncate partition p's log to offset t (start_off <= t < leo): the records from t on
+   are dropped (their ring bytes stay, outside the log), index entries past the new end too. */
+static void truncate_log(ro_engine* e, ro_part* s, uint64_t t) {
+  const uint64_t I = e->cfg.index_interval;
+  s->used = s->rec_pos.v[t];
+  s->leo = t;
+  s->rec_pos.n = t;
+  s->idx_off.n = s->idx_pos.n = s->used / I + 1;
+}
+
 /* Follower: ingest the region leader `src` sent (FORMAT.md §9); acks[k] = this engine's log end of
-   entry k afterwards (0 for a refused entry). */
+   entry k afterwards when the entry continues it (0 otherwise, and for a refused entry). size 0:
+   the leader sent nothing this round (acks = log ends, nothing changes). */
 int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks) {
   const uint32_t me = e->cfg.rank;
   const uint64_t I = e->cfg.index_interval;
   ro_entry* v = NULL;
   const uint32_t n = pair_entries(e, src, me, &v);
   if (!v) return RMQ_ENOMEM;
-  if (!n) {
+  if (!n || !size) {
+    for (uint32_t k = 0; k < n; ++k) acks[k] = e->parts[v[k].p].leo;
     free(v);
     return size ? RMQ_EINVAL : RMQ_OK;
   }
@@ -929,27 +942,32 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     return RMQ_EINVAL;
   }
   const uint64_t tab = 32 + 32ull * n;
-  uint64_t leo = 0, used = 0; /* the partition's log end before this round */
+  /* the state every entry of a partition sees: the log end it continues, decided once (owner) */
+  uint64_t leo = 0, used = 0, term0 = 0;
+  int stale = 0;
   for (uint32_t k = 0; k < n; ++k) {
     ro_part* s = &e->parts[v[k].p];
     const int owner = k == 0 || v[k - 1].p != v[k].p; /* two local slots: the first keeps the state */
-    if (owner) {
-      leo = s->leo;
-      used = s->used;
-    }
     const uint8_t* d = region + 32 + 32ull * k;
     uint32_t cnt, by16, ts, ds;
-    uint64_t first;
+    uint64_t first, term;
     memcpy(&cnt, d, 4);
     memcpy(&by16, d + 4, 4);
     memcpy(&first, d + 8, 8);
     memcpy(&ts, d + 16, 4);
     memcpy(&ds, d + 20, 4);
-    if (!cnt) {
-      acks[k] = s->leo;
-      continue;
+    memcpy(&term, d + 24, 8);
+    if (owner) {
+      term0 = s->term;
+      stale = term < term0; /* a leader of an older term */
+      leo = s->leo;
+      used = s->used;
+      if (!stale && first < leo && first >= s->start_off) { /* the leader's log wins: truncate */
+        used = s->rec_pos.v[first];
+        leo = first;
+      }
     }
-    int ok = first == leo;
+    int ok = !stale && (!cnt || first == leo);
     uint64_t rel = 0;
     for (uint32_t r = 0; r < cnt && ok; ++r) {
       uint64_t slot, off;
@@ -966,7 +984,15 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     }
     if (!ok) {
       acks[k] = 0;
-      e->counters[first == leo ? 1 : 2]++;
+      e->counters[!stale && first == leo ? 1 : 2]++;
+      continue;
+    }
+    if (owner) {
+      if (term > s->term) s->term = term;
+      if (leo < s->leo) truncate_log(e, s, leo);
+    }
+    if (!cnt) {
+      acks[k] = first == leo ? leo : 0;
       continue;
     }
     const uint8_t* bytes = region + data + 16ull * ds;

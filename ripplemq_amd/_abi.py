@@ -137,6 +137,7 @@ _SIGS = {
     "rmq_attach_local": (C.c_int, [vp, vp]),
     "rmq_replication_stats": (C.c_int, [vp, C.POINTER(RmqReplStats)]),
     "rmq_read_outbox": (C.c_int, [vp, u32, vp, u64, C.POINTER(u64)]),
+    "rmq_fault_drop_rounds": (C.c_int, [vp, u32]),
 }
 
 _lib = None

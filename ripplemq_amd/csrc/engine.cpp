@@ -354,7 +354,7 @@ void free_engine(rmq_engine* e) {
   }
   repl_free(e);
   DevState& s = e->st;
-  std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.match, s.is_leader,
+  std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc, e->d_err,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_opos, e->d_total, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
@@ -518,6 +518,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.commit, P));
   CREATE_TRY(dalloc(&s.hw, P));
   CREATE_TRY(dalloc(&s.term_start, P));
+  CREATE_TRY(dalloc(&s.term, P));
   CREATE_TRY(dalloc(&s.match, (size_t)P * RF));
   CREATE_TRY(dalloc(&s.is_leader, P));
   CREATE_TRY(dalloc(&s.local_mask, P));
@@ -563,6 +564,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->leader_slot.assign(P, 0u);
   e->ranks.assign((size_t)P * RF, cfg->rank);
   e->term.assign(P, 1ull);
+  CREATE_HIP(hipMemcpy(s.term, e->term.data(), P * 8ull, hipMemcpyHostToDevice));
   e->key.resize(P);
   for (uint32_t p = 0; p < P; ++p) e->key[p] = p;
   e->ticket_n.assign(kStatsRing, 0u);
@@ -638,7 +640,6 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   if (pidx != RMQ_ALL_PARTITIONS && pidx >= P) return RMQ_ENOPART;
   const uint32_t lo = pidx == RMQ_ALL_PARTITIONS ? 0 : pidx, hi = pidx == RMQ_ALL_PARTITIONS ? P : pidx + 1;
   for (uint32_t p = lo; p < hi; ++p) {  // validate everything before changing anything
-    if (term < e->term[p]) return RMQ_EINVAL;
     bool local = false;
     for (uint32_t r = 0; r < RF; ++r) local |= e->ranks[(size_t)p * RF + r] == e->cfg.rank;
     if (!local) return RMQ_EINVAL;
@@ -649,6 +650,11 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   int rc = drain(e);
   if (!rc) rc = equalize_state_sets(e);
   if (rc) return rc;
+  // a follower adopts newer leader terms from replication rounds (FORMAT.md §9): the device holds
+  // the current terms
+  HIP_TRY(hipMemcpy(&e->term[lo], e->st.term + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
+  for (uint32_t p = lo; p < hi; ++p)
+    if (term < e->term[p]) return RMQ_EINVAL;
   for (uint32_t p = lo; p < hi; ++p) {
     uint32_t slot = e->leader_slot[p];
     if (!e->repl) {
@@ -660,6 +666,7 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
     e->term[p] = term;
   }
   HIP_TRY(hipMemcpy(e->st.is_leader + lo, &e->is_leader[lo], (size_t)(hi - lo) * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(e->st.term + lo, &e->term[lo], (size_t)(hi - lo) * 8, hipMemcpyHostToDevice));
   launch_become_leader(e->st, pidx, e->main_s);
   HIP_TRY(hipGetLastError());
   return drain(e);
@@ -1103,7 +1110,7 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   HIP_TRY(hipMemcpy(&o->high_watermark, s.hw + p, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&o->term_start, s.term_start + p, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(o->match, s.match + (size_t)p * RF, RF * 8ull, hipMemcpyDeviceToHost));
-  o->term = e->term[p];
+  HIP_TRY(hipMemcpy(&o->term, s.term + p, 8, hipMemcpyDeviceToHost));
   for (uint32_t r = 0; r < RF; ++r) o->replica_rank[r] = e->ranks[(size_t)p * RF + r];
   o->leader_slot = e->leader_slot[p];
   o->is_leader = e->is_leader[p];
@@ -1310,6 +1317,15 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   out->refused_crc = c[1];
   out->refused_log = c[2];
   out->bytes_ingested = c[3];
+  return RMQ_OK;
+}
+
+int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n) {
+  if (!e) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (!e->repl) return RMQ_EINVAL;
+  e->repl->drop_from = e->last_ticket + 1;
+  e->repl->drop_n = n;
   return RMQ_OK;
 }
 

@@ -88,6 +88,7 @@ struct Replication {
   uint32_t* d_xi_slot = nullptr;
   uint32_t* d_xi_start = nullptr;
   uint32_t* d_bad = nullptr;     // [n_in]
+  uint64_t* d_base = nullptr;    // [n_in][2] IngestArgs::base
   uint64_t* d_counters = nullptr;  // [4] (IngestArgs)
   uint64_t out_cap = 0, in_cap = 0;
   XchgSet sets[kSets];
@@ -95,6 +96,10 @@ struct Replication {
   std::deque<uint32_t> acking;   // sets whose data exchange is posted, acks not yet applied
   uint64_t rounds = 0, bytes_sent = 0, bytes_recv = 0;
   uint32_t last_set = ~0u;       // set of the last posted round (rmq_read_outbox)
+  // fault injection (rmq_fault_drop_rounds): the rounds of the next `drop_n` groups whose first
+  // ticket is at least `drop_from` send empty regions
+  uint64_t drop_from = 0;
+  uint32_t drop_n = 0;
 };
 
 }  // namespace rmq

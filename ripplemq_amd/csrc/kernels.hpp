@@ -62,6 +62,8 @@ struct DevState {
   uint64_t* commit;
   uint64_t* hw;
   uint64_t* term_start;
+  uint64_t* term;        // current term of the partition known here (leader: its own; follower: the
+                         // newest leader term a round carried, FORMAT.md §9)
   uint64_t* match;       // [P][RF]
   uint32_t* is_leader;   // 0/1
   uint32_t* local_mask;  // bit r set: replica slot r is stored on this device
@@ -214,6 +216,8 @@ struct IngestArgs {
   const uint32_t* xi_start;  // [world + 1]
   uint32_t world, rank, n_in, pad;
   uint32_t* bad;             // [n_in] entry refused this round (cleared by the finish kernel)
+  uint64_t* base;            // [n_in][2] {log end offset, log end position} the entry continues:
+                             // the follower's, or the leader's first offset after a truncation
   uint64_t* ackout;          // [n_in] follower log end after the round
   const CrcConsts* crc;
   uint64_t* counters;        // [4] records ingested, entries refused (CRC), refused (log mismatch), bytes

@@ -726,7 +726,6 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
           W.xdst[w][r32][nx++] = reinterpret_cast<u64>(A.outbox3 + x.data_abs + rel);
           *reinterpret_cast<u64*>(A.outbox3 + x.tab_abs + 8ull * rk) =
               (u64)x.k | ((u64)(x.data_start16 + (u32)(rel >> 4)) << 32);
-          if (rk == 0) *reinterpret_cast<u64*>(A.outbox3 + x.dir_abs + 8) = off;
         }
       }
       W.xn[w][r32] = nx;
@@ -844,6 +843,18 @@ __device__ void partition_apply(const PipeArgs& A, u32 p) {
   // counted by stages 1/2, ranks being per partition, but never applied; the host keeps both state
   // sets equal for it); stage 2 leaves rejected (batch, partition) cells out of totals
   if (!st.is_leader[p]) return;
+  // replication transport: every directory entry of the partition in the group's outbox names the
+  // log end the round continues (this leader's, before the group) and the leader's term (FORMAT §9)
+  if (A.outbox3 && A.g3.nb) {
+    const u32 lmx = st.local_mask[p];
+    for (u32 r = 0; r < st.RF; ++r) {
+      const u32 e = (lmx >> r) & 1u ? ~0u : A.outidx[(u64)p * st.RF + r];
+      if (e == ~0u) continue;
+      u64* d = reinterpret_cast<u64*>(A.outbox3 + A.xe3[e].dir_abs);
+      d[1] = A.cur.leo[p];
+      d[3] = st.term[p];
+    }
+  }
   u64 tc = 0, leo;
   if (A.g3.nb) {
     const u64 tot = A.s3.totals[p];

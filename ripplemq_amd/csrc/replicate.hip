@@ -6,6 +6,12 @@
 // (PartitionRaftServer.java:82-93 configures the group; MessageAppendRequestProcessor.java:59 is
 // the Node.apply that starts it). Here a round carries one launch group of the leader's appends
 // for every partition the two ranks share, as one region of the exchange:
+//   ingest_prepare (thread per entry): the log end the entry continues — the follower's own, or,
+//     when the round's first offset lies inside the follower's retained log below its end, that
+//     offset and its position (the follower truncates its log to the leader's: Raft's follower
+//     deletes the entries that conflict with the leader's; the position comes from the sparse
+//     index and a walk over the follower's record headers). An entry whose leader term is older
+//     than the follower's is refused (a stale leader);
 //   ingest_records (wave per 32 records, a lane pair per record, like the append's stage 3):
 //     checks the record continues the follower's log (first offset == follower log end, header
 //     offset == first offset + rank), recomputes its CRC32C from the payload pieces (slicing-by-8
@@ -13,10 +19,11 @@
 //     the header's, and stores the record into the follower's replica ring at the same logical
 //     position the leader used (pieces a later piece of the round overwrites are not stored), plus
 //     the sparse-index entries;
-//   ingest_finish (thread per entry): advances the follower partition's log end (both state sets:
-//     the append pipeline never touches a partition it does not lead), evaluates retention once per
-//     round (FORMAT.md §4 rule) and writes the ack (the follower's log end) for the leader.
-// A refused entry (CRC or log mismatch) leaves the follower's log end where it was.
+//   ingest_finish (thread per entry): moves the follower partition's log end (both state sets:
+//     the append pipeline never touches a partition it does not lead), adopts a newer leader term,
+//     evaluates retention once per round (FORMAT.md §4 rule) and writes the ack (the follower's
+//     log end, 0 when the entry does not continue it) for the leader.
+// A refused entry (CRC, log mismatch or stale term) leaves the follower's log end where it was.
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "partition_ops.hpp"
@@ -49,6 +56,82 @@ __device__ __forceinline__ u32 source_of_task(const IngestArgs& A, u32 task) {
   return q;
 }
 
+// Directory entry k of a region: {count, bytes / 16, first offset} and the leader's term.
+struct DirView {
+  u32 count, bytes16, tstart, dstart16;
+  u64 first, term;
+};
+__device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
+  const uint4* de = reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
+  const uint4 d0 = de[0], d1 = de[1];
+  DirView d;
+  d.count = d0.x;
+  d.bytes16 = d0.y;
+  d.first = ((u64)d0.w << 32) | d0.z;
+  d.tstart = d1.x;
+  d.dstart16 = d1.y;
+  d.term = ((u64)d1.w << 32) | d1.z;
+  return d;
+}
+
+__device__ __forceinline__ u32 source_of_entry(const IngestArgs& A, u32 e) {
+  u32 src = 0;
+  for (u32 q = 1; q < A.world; ++q) src += e >= A.xi_start[q] ? 1u : 0u;
+  return src;
+}
+
+// Logical position of offset t (start_off <= t <= leo) in the follower's log of partition p, read
+// from replica slot `slot`: the largest live index entry at or below t, then the record headers
+// (FORMAT.md §5 lookup).
+__device__ u64 follower_pos(const DevState& st, u32 p, u32 slot, u64 t) {
+  const RingRef rg = ring_ref(st, p);
+  const u32 ilog = st.interval_log2;
+  u64 off = st.start_off[p], pos = st.start_pos[p];
+  u64 lo = (pos + (1ull << ilog) - 1) >> ilog, hi = (st.used[p] >> ilog) + 1;  // live m in [lo, hi)
+  while (lo < hi) {
+    const u64 mid = lo + (hi - lo) / 2;
+    const u64* ie = st.index + (rg.ibase + mid % rg.icap) * 2;
+    if (ie[0] <= t) {
+      if (ie[0] >= off) {
+        off = ie[0];
+        pos = ie[1];
+      }
+      lo = mid + 1;
+    } else {
+      hi = mid;
+    }
+  }
+  const uint8_t* ring = st.logs + (u64)slot * st.rstride + rg.base;
+  for (; off < t; ++off) {
+    const u32 L = *reinterpret_cast<const u32*>(ring + ((pos + 8ull) & (rg.seg - 1ull)));
+    pos += 16ull + ((L + 15ull) & ~15ull);
+  }
+  return pos;
+}
+
+__global__ void ingest_prepare_kernel(IngestArgs A) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= A.n_in) return;
+  const u32 src = source_of_entry(A, e), k = e - A.xi_start[src];
+  const DevState& st = A.st;
+  const u32 p = A.xi_p[e];
+  u64 leo = st.leo[p], used = st.used[p];
+  if (A.rbytes[src]) {
+    const RegionView R = region_of(A, src);
+    if (R.n_entries == A.xi_start[src + 1] - A.xi_start[src]) {
+      const DirView d = dir_of(R, k);
+      if (d.term < st.term[p]) {
+        A.bad[e] |= 4u;  // a stale leader
+      } else if (d.first < leo && d.first >= st.start_off[p]) {
+        used = follower_pos(st, p, A.xi_slot[e], d.first);  // the leader's log wins: truncate
+        leo = d.first;
+      }
+    }
+  }
+  A.base[2 * e] = leo;
+  A.base[2 * e + 1] = used;
+}
+
 __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   __shared__ __attribute__((aligned(16))) u32 t8[8][256];
   __shared__ __attribute__((aligned(16))) u32 z[2][4][256];
@@ -79,14 +162,13 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   if (in) {
     const u64 tab = *reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries + 8ull * i);
     const u32 k = min((u32)tab, R.n_entries - 1u), d16 = (u32)(tab >> 32);  // ok below requires k == tab
-    const uint4* de = reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
-    const uint4 d0 = de[0], d1 = de[1];
-    const u32 bytes16 = d0.y, tstart = d1.x, dstart16 = d1.y;
-    const u64 first = ((u64)d0.w << 32) | d0.z;
+    const DirView d = dir_of(R, k);
+    const u32 bytes16 = d.bytes16, tstart = d.tstart, dstart16 = d.dstart16;
+    const u64 first = d.first;
     e = A.xi_start[src] + k;
     p = A.xi_p[e];
     owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
-    const u64 leo = st.leo[p], used = st.used[p];
+    const u64 leo = A.base[2 * e], used = A.base[2 * e + 1];  // after a truncation: the leader's first offset
     rec = R.base + R.data_off + 16ull * d16;
     hdr = *reinterpret_cast<const uint4*>(rec);
     off = ((u64)hdr.y << 32) | hdr.x;
@@ -96,7 +178,7 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
     pos = used + rel;
     gend = used + 16ull * bytes16;
     ok = k == (u32)tab && first == leo && off == first + (i - tstart) && d16 >= dstart16 &&
-         rel + 16ull * (1ull + m) <= 16ull * bytes16;
+         rel + 16ull * (1ull + m) <= 16ull * bytes16 && !(A.bad[e] & 4u);
     if (!ok && j == 1) atomicOr(&A.bad[e], 2u);  // does not continue the follower's log
   }
   // CRC32C of the payload from its 16-byte pieces (zero-padded in the log): lane j folds pieces
@@ -147,44 +229,44 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
 __global__ void ingest_finish_kernel(IngestArgs A) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= A.n_in) return;
-  u32 src = 0;
-  for (u32 q = 1; q < A.world; ++q) src += e >= A.xi_start[q] ? 1u : 0u;
+  const u32 src = source_of_entry(A, e);
   const DevState& st = A.st;
   const u32 p = A.xi_p[e], k = e - A.xi_start[src];
   const bool owner = k == 0 || A.xi_p[e - 1] != p;
-  u64 ack = st.leo[p];
+  u64 ack = st.leo[p];  // no region from this leader: nothing new
   const bool whole = A.rbytes[src] && region_of(A, src).n_entries == A.xi_start[src + 1] - A.xi_start[src];
   if (A.rbytes[src] && !whole) {
     ack = 0;
     if (k == 0) atomicAdd((unsigned long long*)&A.counters[2], 1ull);
   } else if (A.rbytes[src]) {
-    const RegionView R = region_of(A, src);
-    const uint4 d0 = *reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
-    const u32 count = d0.x, bytes16 = d0.y;
-    const u64 first = ((u64)d0.w << 32) | d0.z;
-    if (count) {
-      const u32 bad = A.bad[e];
-      if (bad) {
-        ack = 0;  // no new information (match only moves up)
-        atomicAdd((unsigned long long*)&A.counters[(bad & 2u) ? 2 : 1], 1ull);
-        A.bad[e] = 0u;
-      } else {
-        ack = first + count;
-        if (owner) {
-          const u64 used = st.used[p] + 16ull * bytes16;
-          for (u32 s = 0; s < 2; ++s) {
-            A.sets[s].leo[p] = ack;
-            A.sets[s].used[p] = used;
-          }
+    const DirView d = dir_of(region_of(A, src), k);
+    const u32 bad = A.bad[e];
+    const u64 bleo = A.base[2 * e], bused = A.base[2 * e + 1];
+    if (bad) {
+      ack = 0;  // no new information (match only moves up)
+      atomicAdd((unsigned long long*)&A.counters[(bad & 6u) ? 2 : 1], 1ull);
+      A.bad[e] = 0u;
+    } else {
+      // the entry continues the log at bleo (or does not: a follower behind the leader acks 0)
+      const bool cont = d.first == bleo;
+      ack = d.count ? d.first + d.count : (cont ? bleo : 0ull);
+      if (owner) {
+        if (d.term > st.term[p]) st.term[p] = d.term;
+        const u64 nleo = d.count ? ack : bleo, nused = bused + 16ull * d.bytes16;
+        for (u32 s = 0; s < 2; ++s) {
+          A.sets[s].leo[p] = nleo;
+          A.sets[s].used[p] = nused;
+        }
+        if (d.count) {
           // retention once per round (FORMAT.md §4 rule on the follower's log)
           const RingRef rg = ring_ref(st, p);
-          if (used - st.start_pos[p] > rg.seg) {
-            const u64 ms = (used - rg.seg + (1ull << st.interval_log2) - 1) >> st.interval_log2;
+          if (nused - st.start_pos[p] > rg.seg) {
+            const u64 ms = (nused - rg.seg + (1ull << st.interval_log2) - 1) >> st.interval_log2;
             const u64* ie = st.index + (rg.ibase + ms % rg.icap) * 2;
             st.start_off[p] = ie[0];
             st.start_pos[p] = ie[1];
           }
-          atomicAdd((unsigned long long*)&A.counters[3], 16ull * bytes16);
+          atomicAdd((unsigned long long*)&A.counters[3], 16ull * d.bytes16);
         }
       }
     }
@@ -208,6 +290,7 @@ __global__ void ack_apply_kernel(AckApplyArgs a) {
 }
 
 void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s) {
+  if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
   if (tasks) hipLaunchKernelGGL(ingest_records_kernel, dim3((tasks + kIW - 1) / kIW), dim3(kIT), 0, s, a);
   if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
 }

@@ -59,7 +59,7 @@ void free_set_buffers(Replication* r) {
 }
 
 // Post the {region bytes, records} swap of the group in set s (after its stage-2 launch).
-int post_sizes(rmq_engine* e, uint32_t s) {
+int post_sizes(rmq_engine* e, uint32_t s, bool drop) {
   Replication* r = e->repl;
   XchgSet& x = r->sets[s];
   const uint32_t W = r->world;
@@ -72,6 +72,7 @@ int post_sizes(rmq_engine* e, uint32_t s) {
     n16[q] = q == r->rank ? 0 : 16;
   }
   HIP_TRY(hipStreamWaitEvent(r->xchg_s, x.ev_s2, 0));
+  if (drop) HIP_TRY(hipMemsetAsync(x.sizes, 0, 2ull * W * 8, r->xchg_s));  // no region to anyone
   int rc = r->xport->exchange(sb, n16, rb, n16, r->xchg_s);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(x.h_sizes, x.sizes, 4ull * W * 8, hipMemcpyDeviceToHost, r->xchg_s));
@@ -125,6 +126,7 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.rank = me;
   a.n_in = (uint32_t)r->xi_p.size();
   a.bad = r->d_bad;
+  a.base = r->d_base;
   a.ackout = x.ackout;
   a.crc = e->d_crc;
   a.counters = r->d_counters;
@@ -189,7 +191,7 @@ void repl_free(rmq_engine* e) {
     if (x.h_sizes) hipHostFree(x.h_sizes);
   }
   void* bufs[] = {r->d_xo_p, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot, r->d_xi_start,
-                  r->d_bad, r->d_counters};
+                  r->d_bad, r->d_base, r->d_counters};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (r->xchg_s) hipStreamDestroy(r->xchg_s);
@@ -301,6 +303,7 @@ int repl_set_lists(rmq_engine* e) {
   if (!rc) rc = upload(&r->d_xi_slot, r->xi_slot);
   if (!rc) rc = upload(&r->d_xi_start, r->xi_start);
   if (!rc) rc = upload(&r->d_bad, std::vector<uint32_t>(r->xi_p.size(), 0u));
+  if (!rc) rc = upload(&r->d_base, std::vector<uint64_t>(2 * std::max<size_t>(1, r->xi_p.size()), 0ull));
   if (rc) return rc;
   // round buffers (FORMAT.md §9 bounds): a record is at most 31 + L bytes in the log, sent once per
   // remote slot, plus an 8-byte table slot; per region a header, a directory and table padding
@@ -369,7 +372,9 @@ int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s
   if (!r) return RMQ_OK;
   if (s2) {
     HIP_TRY(hipEventRecord(r->sets[s2->set].ev_s2, e->main_s));
-    int rc = post_sizes(e, s2->set);
+    const bool drop = r->drop_n && s2->b[0].ticket >= r->drop_from;
+    if (drop) r->drop_n--;
+    int rc = post_sizes(e, s2->set, drop);
     if (rc) return rc;
   }
   while (!r->sized.empty() && r->sets[r->sized.front()].applied_launch < e->launch_seq) {

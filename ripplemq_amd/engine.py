@@ -125,6 +125,10 @@ class Engine:
         _check(self.lib.rmq_read_outbox(self.h, dst, _ptr(out), out.size, C.byref(n)), "rmq_read_outbox")
         return out[:int(n.value)]
 
+    def fault_drop_rounds(self, n: int = 1) -> None:
+        """Tests: the next n rounds this engine leads carry no records (rmq_fault_drop_rounds)."""
+        _check(self.lib.rmq_fault_drop_rounds(self.h, n), "rmq_fault_drop_rounds")
+
     def become_leader(self, pidx: int, term: int) -> None:
         _check(self.lib.rmq_become_leader(self.h, pidx, term), "rmq_become_leader")
 

@@ -10,8 +10,8 @@ from __future__ import annotations
 import numpy as np
 
 from ripplemq_amd.engine import EngineConfig
-from ripplemq_amd.sharding import rank_view
-from ripplemq_amd.workload import StreamSpec, make_batch
+from ripplemq_amd.sharding import RankView, rank_view
+from ripplemq_amd.workload import Batch, StreamSpec, make_batch
 
 
 def rank_cfg(base: EngineConfig, view, rank: int) -> EngineConfig:
@@ -32,16 +32,22 @@ def rank_batches(spec: StreamSpec, rank: int, rounds: int, group: int):
     return [make_batch(spec, 1000 * rank + k) for k in range(rounds * group)]
 
 
-def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None):
+def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None, drop=()):
     """Regions of every leader to every follower, ingested there; acks back to the leaders.
     corrupt=(src, dst, byte): flip one byte of that region; skip=(src, dst): drop that region and
-    its acks (the follower misses the round)."""
+    its acks (the follower misses the round); drop: leaders whose round sends empty regions
+    (rmq_fault_drop_rounds: followers ingest nothing and ack their log ends)."""
     W = len(oras)
     regions = [[oras[s].round_region(d) if d != s else None for d in range(W)] for s in range(W)]
+    for s in drop:
+        regions[s] = [None if d == s else np.zeros(0, np.uint8) for d in range(W)]
     for o in oras:
         o.end_round()
     for s in range(W):
         for d in range(W):
+            if s in drop and d != s:
+                oras[s].apply_acks(d, oras[d].ingest(s, regions[s][d]))
+                continue
             if d == s or regions[s][d].size == 0 or (skip and (s, d) == tuple(skip)):
                 continue
             reg = regions[s][d]
@@ -51,3 +57,71 @@ def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None):
             acks = oras[d].ingest(s, reg)
             oras[s].apply_acks(d, acks)
     return regions if keep_regions else None
+
+
+def moved_leadership(views, old_leader: int = 0, new_slot: int = 1):
+    """Placement after a leader change: every partition `old_leader` leads moves its leadership to
+    replica slot `new_slot` (a follower that holds the same committed log)."""
+    out = []
+    for v in views:
+        ls = v.leader_slot.copy()
+        moved = v.ranks[np.arange(len(v.gp)), ls] == old_leader
+        ls[moved] = new_slot
+        out.append(RankView(v.rank, v.gp, v.ranks, ls.astype(np.uint32), v.led))
+    return out
+
+
+def led_batches(spec: StreamSpec, view, rank: int, count: int, salt: int):
+    """Batches over the partitions `view` names this rank the leader of (all local pidx if none:
+    every record is then rejected as not leader)."""
+    mine = np.flatnonzero(view.ranks[np.arange(len(view.gp)), view.leader_slot] == rank).astype(np.uint32)
+    out = []
+    for k in range(count):
+        b = make_batch(StreamSpec(max(len(mine), 1), spec.records, spec.mode, size=spec.size,
+                                  config_index=spec.config_index), salt + 1000 * rank + k)
+        pidx = mine[b.pidx] if len(mine) else b.pidx
+        out.append(Batch(pidx.astype(np.uint32), b.lens, b.payload))
+    return out
+
+
+def leader_change_script(spec: StreamSpec, world: int, rf: int, ppr: int, group: int):
+    """Raft's follower-truncation case: rank 0 leads, two rounds reach every follower, the third
+    round of rank 0 is lost (rank 0 keeps those records, uncommitted), leadership of rank 0's
+    partitions moves to replica slot 1 at term 2 while batches are still in flight, and the new
+    leaders append: rank 0, now a follower, must truncate its log to the new leaders' and accept.
+    Returns (views, new views, phases): each phase is (batches per rank, drop set, placement or
+    None, become_leader list per rank [(local pidx, term)])."""
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    new = moved_leadership(views)
+    phases = []
+    for k in range(2):
+        phases.append(([[make_batch(spec, 1000 * r + k * group + j) for j in range(group)] for r in range(world)],
+                       (), None, [[] for _ in range(world)]))
+    phases.append(([[make_batch(spec, 1000 * r + 2 * group + j) for j in range(group)] for r in range(world)],
+                   (0,), None, [[] for _ in range(world)]))
+    bl = []
+    for r in range(world):
+        v = new[r]
+        moved = np.flatnonzero((v.ranks[np.arange(len(v.gp)), v.leader_slot] == r) &
+                               (views[r].ranks[np.arange(len(v.gp)), views[r].leader_slot] != r))
+        bl.append([(int(p), 2) for p in moved])
+    phases.append(([led_batches(spec, new[r], r, group, 77) for r in range(world)], (), new, bl))
+    phases.append(([led_batches(spec, new[r], r, group, 99) for r in range(world)], (), None, [[] for _ in range(world)]))
+    return views, new, phases
+
+
+def run_script_oracle(oras, views, phases, world):
+    """The script on per-rank oracles: a phase's batches form one round (one launch group)."""
+    regions = None
+    for batches, drop, placement, bl in phases:
+        if placement is not None:
+            for r in range(world):
+                place(oras[r], placement[r])
+            for r in range(world):
+                for p, t in bl[r]:
+                    oras[r].become_leader(p, t)
+        for r in range(world):
+            for b in batches[r]:
+                oras[r].append(b.pidx, b.lens, b.payload)
+        regions = exchange_round(oras, keep_regions=True, drop=drop)
+    return regions

@@ -109,3 +109,46 @@ def test_refused_rounds_do_not_commit_on_their_own(oracle_mod):
     finally:
         for o in oras:
             o.close()
+
+
+def test_leader_change_truncates_follower(oracle_mod):
+    # Raft's follower truncation (FORMAT.md §9): rank 0's third round is lost, leadership of its
+    # partitions moves to slot 1 at term 2; rank 0 drops its uncommitted tail and follows
+    from repl_sim import leader_change_script, run_script_oracle
+    world, rf, ppr, group = 3, 3, 6, 2
+    spec = StreamSpec(ppr, 300, "uniform", size=(0, 120), config_index=71)
+    base = EngineConfig(num_partitions=1, replication_factor=rf, segment_bytes=1 << 16, index_interval=256,
+                        max_batch_records=4096, pipeline_depth=group)
+    views, new, phases = leader_change_script(spec, world, rf, ppr, group)
+    cfgs = [rank_cfg(base, views[r], r) for r in range(world)]
+    oras = [oracle_mod.OracleEngine(c) for c in cfgs]
+    try:
+        for r in range(world):
+            place(oras[r], views[r], world)
+        # before the change: rank 0 holds a tail nobody else has
+        run_script_oracle(oras, views, phases[:3], world)
+        s0 = [oras[0].state(p) for p in range(ppr)]
+        assert all(s["log_end_offset"] > s["commit"] for s in s0)
+        f1 = {int(views[1].gp[i]): oras[1].state(i) for i in range(len(views[1].gp))}
+        assert all(f1[int(views[0].gp[p])]["log_end_offset"] == s0[p]["commit"] for p in range(ppr)
+                   if int(views[0].gp[p]) in f1)
+        run_script_oracle(oras, views, phases[3:], world)
+        c = oras[0].counters()
+        assert c[1] == 0 and c[2] == 0, c  # nothing refused: rank 0 truncated and accepted
+        for p in range(ppr):  # rank 0 now follows: same log end and term as the new leader
+            g = int(views[0].gp[p])
+            r1 = int(views[0].ranks[p][1])
+            q = int(np.flatnonzero(views[r1].gp == g)[0])
+            lead, fol = oras[r1].state(q), oras[0].state(p)
+            assert fol["log_end_offset"] == lead["log_end_offset"] and fol["term"] == 2 == lead["term"]
+            assert lead["commit"] == lead["log_end_offset"] > s0[p]["commit"]
+            assert fol["log_end_pos"] == lead["log_end_pos"]
+            a = oras[0].read_segment(int(np.flatnonzero(views[0].ranks[p] == 0)[0]), p)
+            b = oras[r1].read_segment(int(np.flatnonzero(views[r1].ranks[q] == r1)[0]), q)
+            lo, hi = fol["log_start_pos"], fol["log_end_pos"]
+            S = fol["segment_bytes"]
+            idx = (np.arange(lo, hi) % S)
+            assert np.array_equal(a[idx], b[idx])
+    finally:
+        for o in oras:
+            o.close()
