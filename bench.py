@@ -153,6 +153,31 @@ def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float, name: str
                       f"1 thread (ro_append): {nb1} batches, {rate1 / 1e6:.2f} M msgs/s"}
 
 
+def host_leg(eng, batches, steps: int) -> dict:
+    """The workload's batches handed over from HOST memory (rmq_append, RMQ_MEM_HOST): the engine
+    packs each into a pinned staging slot and moves it with one DMA on its copy stream, overlapped
+    with the pipeline; out offsets return through pinned memory. A PCIe-inclusive rate, reported
+    beside `value` (which is HBM-resident input), never instead of it."""
+    for k in range(2 * len(batches)):  # untimed: the engine sets up its staging slots
+        b = batches[k % len(batches)]
+        eng.append_async(b.pidx, b.lens, b.payload)
+    eng.sync()
+    n = batches[0].n
+    h2d = 0
+    t0 = time.perf_counter()
+    for k in range(steps):
+        b = batches[k % len(batches)]
+        eng.append_async(b.pidx, b.lens, b.payload)
+        h2d += 8 * b.n + b.payload.nbytes
+    eng.sync()
+    dt = time.perf_counter() - t0
+    return {"value": steps * n / dt, "unit": "msgs/s", "steps": steps, "h2d_gbs": h2d / dt / 1e9,
+            "ms_per_step": dt * 1e3 / steps,
+            "note": "host numpy batches through rmq_append: memcpy into a pinned staging slot, one "
+                    "H2D DMA per batch on the copy stream, pipeline waits on its event; h2d_gbs = "
+                    "pidx + len + payload bytes over the wall time"}
+
+
 def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     """Consumer fetch over the bench engine's committed logs (SURVEY §8(d) B_fetch): per round every
     (partition, consumer) commits an offset lagging the high watermark by U[0, retained records]
@@ -312,6 +337,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
         eng.h2d(d_pay, b.payload)
         pool.append((b.n, d_pidx, d_len, d_pay, int(b.payload.nbytes), record_bytes(b.lens)))
     mean_payload = float(np.mean([b.payload.nbytes for b in batches]))
+    host_batches = batches[:8]
     del batches
     d_out = [eng.device_alloc(spec.records * 8) for _ in range(4)]
 
@@ -405,6 +431,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
             "device": dev_name,
             "cu_count": cus,
         }
+        if args.host_steps > 0 and world == 1:
+            out["host_path"] = host_leg(eng, host_batches, args.host_steps)
         if args.fetch_rounds > 0:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
     for _, dp, dl, dpay, _, _ in pool:
@@ -441,6 +469,8 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
+    ap.add_argument("--host-steps", type=int, default=100,
+                    help="batches of the host-memory leg (PCIe-inclusive rate, 1 GPU; 0: skip)")
     ap.add_argument("--watchdog", type=float, default=900.0, help="multi-GPU: exit a rank stuck this long [s]")
     ap.add_argument("--group", type=int, default=4,
                     help="batches per pipeline launch group (cfg.pipeline_depth, 1..8)")

@@ -242,6 +242,8 @@ int flush(rmq_engine* e) {
   return RMQ_OK;
 }
 
+void collect_done(rmq_engine* e);
+
 int drain(rmq_engine* e) {
   int rc = flush(e);
   if (!rc) rc = repl_drain(e);  // the remaining replication rounds and their acks
@@ -251,6 +253,7 @@ int drain(rmq_engine* e) {
     e->prof_ended = true;
   }
   HIP_TRY(hipStreamSynchronize(e->main_s));
+  collect_done(e);
   return check_err(e);
 }
 
@@ -258,6 +261,7 @@ int drain(rmq_engine* e) {
 // forming or in the pipeline's earlier stages (reads of committed state, consumer commits).
 int quiesce(rmq_engine* e) {
   HIP_TRY(hipStreamSynchronize(e->main_s));
+  collect_done(e);
   return check_err(e);
 }
 
@@ -271,12 +275,23 @@ bool launch_done(rmq_engine* e, uint64_t L) {
   return hipStreamQuery(e->main_s) == hipSuccess;
 }
 
-// Ticket completion: 1 complete, 0 applied by a launch still running, -1 not applied yet.
-int ticket_state(rmq_engine* e, uint64_t t) {
+// Completed launches: the tickets they complete, and those host batches' out offsets from their
+// pinned slots into the callers' buffers.
+void collect_done(rmq_engine* e) {
   while (!e->marks.empty() && launch_done(e, e->marks.front().second)) {
     e->done_ticket = std::max(e->done_ticket, e->marks.front().first);
     e->marks.pop_front();
   }
+  for (Staging& sg : e->staging)
+    if (sg.user_out && sg.ticket <= e->done_ticket) {
+      std::memcpy(sg.user_out, sg.h_out, (size_t)sg.out_n * 8);
+      sg.user_out = nullptr;
+    }
+}
+
+// Ticket completion: 1 complete, 0 applied by a launch still running, -1 not applied yet.
+int ticket_state(rmq_engine* e, uint64_t t) {
+  collect_done(e);
   if (t <= e->done_ticket) return 1;
   if (!e->marks.empty() && t <= e->marks.back().first) return 0;
   return -1;
@@ -291,8 +306,14 @@ int wait_ticket(rmq_engine* e, uint64_t t) {
     if (rc) return rc;
     s = ticket_state(e, t);
   }
-  if (s == 0) {
-    HIP_TRY(hipStreamSynchronize(e->main_s));
+  if (s == 0) {  // wait for the launch that completes t, not for everything queued behind it
+    uint64_t L = e->launch_seq;
+    for (const auto& m : e->marks)
+      if (m.first >= t) {
+        L = m.second;
+        break;
+      }
+    while (!launch_done(e, L)) std::this_thread::yield();
     ticket_state(e, t);
   }
   return RMQ_OK;
@@ -366,9 +387,13 @@ void free_engine(rmq_engine* e) {
     void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo};
     for (void* p : xs) bufs.push_back(p);
   }
+  delete e->copy_pool;
   for (const Staging& sg : e->staging) {
-    void* xs[] = {sg.d_pidx, sg.d_len, sg.d_poff, sg.d_payload, sg.d_out};
-    for (void* p : xs) bufs.push_back(p);
+    bufs.push_back(sg.d_blk);
+    bufs.push_back(sg.d_out);
+    if (sg.h_blk) hipHostFree(sg.h_blk);
+    if (sg.h_out) hipHostFree(sg.h_out);
+    if (sg.ev_in) hipEventDestroy(sg.ev_in);
   }
   for (void* p : bufs)
     if (p) hipFree(p);
@@ -378,6 +403,7 @@ void free_engine(rmq_engine* e) {
   if (e->ev_main) hipEventDestroy(e->ev_main);
   if (e->ev_fetch) hipEventDestroy(e->ev_fetch);
   if (e->fetch_s) hipStreamDestroy(e->fetch_s);
+  if (e->copy_s) hipStreamDestroy(e->copy_s);
   for (auto& v : e->prof)
     for (EvPair& p : v) {
       if (p.a) hipEventDestroy(p.a);
@@ -480,6 +506,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
+  CREATE_HIP(hipStreamCreateWithFlags(&e->copy_s, hipStreamNonBlocking));
   CREATE_HIP(hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming));
   CREATE_HIP(hipEventCreateWithFlags(&e->ev_fetch, hipEventDisableTiming));
 
@@ -788,29 +815,45 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     if (sg.ticket) {  // the batch that used this staging slot must be complete
       int rc = wait_ticket(e, sg.ticket);
       if (rc) return rc;
+      collect_done(e);
     }
-    const uint32_t NB = e->cfg.max_batch_records;
-    if (!sg.d_pidx) {
-      int rc = dalloc(&sg.d_pidx, NB);
-      if (!rc) rc = dalloc(&sg.d_len, NB);
-      if (!rc) rc = dalloc(&sg.d_poff, NB);
-      if (!rc) rc = dalloc(&sg.d_out, NB);
-      if (!rc) rc = dalloc(&sg.d_payload, e->cfg.max_batch_bytes + 32);
-      if (rc) return rc;
-    }
+    const uint64_t NB = e->cfg.max_batch_records, cap = 32ull * NB + e->cfg.max_batch_bytes + 64;
+    if (!sg.d_blk)  // the first host batch sets up every slot (allocation synchronizes the device)
+      for (Staging& z : e->staging) {
+        int rc = dalloc(&z.d_blk, cap);
+        if (!rc) rc = dalloc(&z.d_out, NB);
+        if (rc) return rc;
+        HIP_TRY(hipHostMalloc((void**)&z.h_blk, cap, 0));
+        HIP_TRY(hipHostMalloc((void**)&z.h_out, NB * 8, 0));
+        HIP_TRY(hipEventCreateWithFlags(&z.ev_in, hipEventDisableTiming));
+      }
     sg.ticket = t;
-    HIP_TRY(hipMemcpyAsync(sg.d_pidx, b->pidx, n * 4ull, hipMemcpyHostToDevice, e->main_s));
-    HIP_TRY(hipMemcpyAsync(sg.d_len, b->len, n * 4ull, hipMemcpyHostToDevice, e->main_s));
-    if (b->payload_off)
-      HIP_TRY(hipMemcpyAsync(sg.d_poff, b->payload_off, n * 8ull, hipMemcpyHostToDevice, e->main_s));
-    if (b->payload_bytes)
-      HIP_TRY(hipMemcpyAsync(sg.d_payload, b->payload, b->payload_bytes, hipMemcpyHostToDevice, e->main_s));
-    f.b.pidx = sg.d_pidx;
-    f.b.len = sg.d_len;
-    f.b.poff = b->payload_off ? sg.d_poff : nullptr;
-    f.b.payload = sg.d_payload;
+    const uint64_t o_len = (4ull * n + 15) & ~15ull, o_poff = o_len + ((4ull * n + 15) & ~15ull);
+    const uint64_t o_pay = o_poff + (b->payload_off ? (8ull * n + 15) & ~15ull : 0ull);
+    if (!e->copy_pool) {
+      // RMQ_COPY_THREADS: packing threads besides the caller's (default min(7, cores / 2))
+      const char* env = std::getenv("RMQ_COPY_THREADS");
+      const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+      unsigned k = env ? (unsigned)std::atoi(env) : std::min(7u, hc / 2u);
+      e->copy_pool = new (std::nothrow) CopyPool(std::min(k, 64u));
+      if (!e->copy_pool) return RMQ_ENOMEM;
+    }
+    std::vector<CopyPool::Seg> segs = {{sg.h_blk, reinterpret_cast<const uint8_t*>(b->pidx), 4ull * n},
+                                       {sg.h_blk + o_len, reinterpret_cast<const uint8_t*>(b->len), 4ull * n}};
+    if (b->payload_off) segs.push_back({sg.h_blk + o_poff, reinterpret_cast<const uint8_t*>(b->payload_off), 8ull * n});
+    if (b->payload_bytes) segs.push_back({sg.h_blk + o_pay, b->payload, b->payload_bytes});
+    e->copy_pool->run(segs, 512u << 10);
+    HIP_TRY(hipMemcpyAsync(sg.d_blk, sg.h_blk, o_pay + b->payload_bytes, hipMemcpyHostToDevice, e->copy_s));
+    HIP_TRY(hipEventRecord(sg.ev_in, e->copy_s));
+    HIP_TRY(hipStreamWaitEvent(e->main_s, sg.ev_in, 0));  // before the group's first launch
+    f.b.pidx = reinterpret_cast<const uint32_t*>(sg.d_blk);
+    f.b.len = reinterpret_cast<const uint32_t*>(sg.d_blk + o_len);
+    f.b.poff = b->payload_off ? reinterpret_cast<const uint64_t*>(sg.d_blk + o_poff) : nullptr;
+    f.b.payload = sg.d_blk + o_pay;
     f.b.out_offsets = sg.d_out;
-    f.host_out = out_offsets;
+    f.host_out = sg.h_out;
+    sg.user_out = out_offsets;
+    sg.out_n = n;
   }
   if (e->forming.nb && e->forming.tiles + f.b.tiles > e->max_group_tiles) {  // (never with a transport)
     int rc = close_group(e);

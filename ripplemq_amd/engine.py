@@ -185,6 +185,7 @@ class Engine:
 
     def sync(self) -> None:
         _check(self.lib.rmq_sync(self.h), "rmq_sync")
+        self._keep.clear()  # every ticket is complete: its out offsets are in the caller's arrays
 
     def ack(self, pidx, slot, match) -> None:
         pidx = np.ascontiguousarray(pidx, np.uint32)
