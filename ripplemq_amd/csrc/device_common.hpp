@@ -32,7 +32,9 @@ constexpr u32 kRecAlign = 16;         // FORMAT.md §1: records padded to 16 byt
 struct CrcConsts {
   u32 table[8][256];      // slicing-by-8: table[k][b] = CRC register after byte b then k zero bytes
   u32 zshift[2][4][256];  // zshift[k][i][b] = (b << 8i) * x^(8 * 16 * 2^k): register shift past 16 << k zero bytes
+  u32 zshift1k[4][256];   // register shift past 1024 zero bytes (a wave's round of 64 pieces)
   u32 inv_pad[16];        // inv_pad[n] = x^(-8n) mod P: "remove n trailing zero bytes"
+  u32 sh16[64];           // sh16[e] = x^(8 * 16 * e) mod P: shift past e 16-byte pieces
 };
 
 // FORMAT.md §1 record size: 16-byte header + payload padded to kRecAlign.

@@ -77,6 +77,13 @@ void build_crc_consts(CrcConsts* c) {
   for (uint32_t k = 0; k < 2; ++k)  // shift past 16 << k zero bytes = multiply by x^(2^(7+k))
     for (uint32_t i = 0; i < 4; ++i)
       for (uint32_t b = 0; b < 256; ++b) c->zshift[k][i][b] = host_mulmod(b << (8 * i), x2n[7 + k]);
+  for (uint32_t i = 0; i < 4; ++i)  // 1024 bytes = 2^13 bits
+    for (uint32_t b = 0; b < 256; ++b) c->zshift1k[i][b] = host_mulmod(b << (8 * i), x2n[13]);
+  uint32_t x128e = 0x80000000u;  // x^(128 e), e = 0..63
+  for (uint32_t e = 0; e < 64; ++e) {
+    c->sh16[e] = x128e;
+    x128e = host_mulmod(x128e, x2n[7]);
+  }
   uint32_t x8n = 0x80000000u;  // x^(8n), n = 0..15
   for (uint32_t n = 0; n < 16; ++n) {
     c->inv_pad[n] = n ? host_inverse(x8n) : 0x80000000u;

@@ -86,6 +86,7 @@ struct Stage1Smem {
 struct Stage3Smem {
   u32 t8[8][256];       // slicing-by-8 CRC32C tables
   u32 z[2][4][256];     // register shift past 16 and 32 zero bytes
+  u32 zk[4][256];       // register shift past 1024 zero bytes (wave-wide records)
   uint4 img[kPW][kTaskRecs][8];  // per wave: the task's records as laid out in the log (<= 128 B each)
   uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16 | dead << 24}
   u64 xdst[kPW][kTaskRecs][kMaxRemote];  // replication: each record's outbox address per remote slot
@@ -575,6 +576,18 @@ __device__ __forceinline__ uint4 extract_piece(uint4 b0, uint4 b1, u32 s, u32 nb
 constexpr u32 kPR = 8;          // pieces per record per round
 constexpr u32 kBL = 5;          // blocks per lane per round (9 blocks cover 8 misaligned pieces)
 
+// Records longer than kBigPieces payload pieces are stored by the whole wave, one after another
+// (lane l takes pieces l, l + 64, ...; kBU pieces per lane in flight): the lane-pair path would
+// keep its wave for m / 8 rounds while the other 31 pairs idle.
+constexpr u32 kBigPieces = 64;
+constexpr u32 kBU = 2;
+
+__device__ __forceinline__ u64 readlane64(u64 v, u32 l) {
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+         (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
+}
+__device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
+
 __device__ __forceinline__ uint4 pair_swap4(uint4 v) {
   return make_uint4(pair_swap(v.x), pair_swap(v.y), pair_swap(v.z), pair_swap(v.w));
 }
@@ -596,11 +609,16 @@ __device__ __forceinline__ TaskPos task_pos(const PipeGroup& G, u32 task) {
 }
 __device__ __forceinline__ u32 task_rec(const TaskPos& T) { return T.i0 + ((threadIdx.x & 63) >> 1); }
 
-struct TaskState {  // round 2: partition state of the record and its first round of payload blocks
-  u64 ex, leo, used;
-  u64 gend;        // the partition's log end position after the whole group
+// Round 2: where the record goes and its first round of payload blocks (derived from the
+// partition's state as soon as it arrives, so that only these words stay live).
+constexpr u32 kLead = 1u << 31;     // TaskState::lm: this engine leads the partition
+constexpr u32 kNoSpace = 1u << 30;  // TaskState::lm: the (batch, partition) cell is over its limit
+struct TaskState {
+  u64 pos, off;    // logical position and offset of the record
   u64 rdesc;       // the partition's ring descriptor (DevState::ring)
-  u32 lm, lead;
+  u32 lm;          // local replica mask | kLead | kNoSpace
+  u32 dead;        // leading pieces (0 = header) a later piece of the group overwrites
+  u32 rel16, rk;   // replication: 16-byte units and records into the partition's group run
   uint4 blk[kBL];
 };
 
@@ -648,23 +666,35 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   const PipeGroup& G = A.g3;
   const DevState& st = A.st;
   TaskState S;
-  S.ex = S.leo = S.used = S.gend = 0ull;
+  S.pos = S.off = 0ull;
   S.rdesc = 8ull;  // any valid descriptor (a 256-byte ring at 0) for lanes that store nothing
-  S.lm = S.lead = 0u;
+  S.lm = S.dead = S.rel16 = S.rk = 0u;
+  u64 ex = 0, tot = 0, leo = 0, used = 0;
+  u32 lead = 0, lm = 0;
   if (cand) {
     const u32 p = R.p;
     const u32 t = G.tile0[T.jb] + task_rec(T) / kTR;
-    S.lead = st.is_leader[p];
-    S.ex = A.s3.excl[(u64)p * A.gt + t];
-    const u64 tot = A.s3.totals[p];
-    S.leo = A.cur.leo[p];
-    S.used = A.cur.used[p];
-    S.gend = S.used + 16ull * (tot & kLow40);
-    S.lm = st.local_mask[p];
+    lead = st.is_leader[p];
+    ex = A.s3.excl[(u64)p * A.gt + t];
+    tot = A.s3.totals[p];
+    leo = A.cur.leo[p];
+    used = A.cur.used[p];
+    lm = st.local_mask[p];
     S.rdesc = st.ring[p];
   }
   // first round of payload blocks, speculatively (leadership is checked before any store)
   round_blocks(A, R, 0u, cand, S.blk);
+  if (cand) {
+    S.rk = (u32)((ex >> 40) & kCnt23) + (R.cr.x & kRankMask);
+    S.rel16 = (u32)(ex & kLow40) + R.cr.y;
+    S.off = leo + S.rk;
+    S.pos = used + 16ull * S.rel16;
+    // pieces (0 = header, k = payload piece k - 1 at pos + 16k) whose ring slot a later piece of
+    // the same group overwrites (pos + 16k + seg < group end) are dead: not stored
+    const u64 seg = 1ull << (S.rdesc & 63ull), gend = used + 16ull * (tot & kLow40);
+    S.dead = gend > S.pos + seg ? (u32)min((gend - seg - S.pos) >> 4, (u64)((R.L + 15u) >> 4) + 1ull) : 0u;
+    S.lm = lm | (lead ? kLead : 0u) | ((ex & kExclNoSpace) ? kNoSpace : 0u);
+  }
   return S;
 }
 
@@ -687,25 +717,26 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   const u32 p = R.p, L = R.L;
   const u32 fl = R.cr.x >> kFlagShift;
   const u32 rej = batch_rej(A, T);
-  const bool ns = (Z.ex & kExclNoSpace) != 0ull;  // the record's (batch, partition) is over its limit
-  const bool ok = cand && Z.lead != 0u && !ns;
+  const bool ns = (Z.lm & kNoSpace) != 0u;  // the record's (batch, partition) is over its limit
+  const bool lead = (Z.lm & kLead) != 0u;
+  const u32 lm8 = Z.lm & 0xFFu;
+  const bool ok = cand && lead && !ns;
   const u32 m = (L + 15u) >> 4;  // payload pieces
+  const bool big = ok && m > kBigPieces;  // stored by the whole wave below
+  const bool okp = ok && !big;           // stored by its lane pair
   const RingRef rg = ring_ref(Z.rdesc, st.interval_log2, st.icap_mul);
   const u64 segmask = rg.seg - 1ull;
   const u64 rstride = st.rstride;
-  const u64 off = Z.leo + ((Z.ex >> 40) & kCnt23) + (R.cr.x & kRankMask);
-  const u64 pos = Z.used + 16ull * ((Z.ex & kLow40) + R.cr.y);
-  // pieces (0 = header, k = payload piece k - 1 at pos + 16k) whose ring slot a later piece of the
-  // same group overwrites (pos + 16k + seg < group end) are dead: not stored
-  const u32 dead = Z.gend > pos + rg.seg ? (u32)min((Z.gend - rg.seg - pos) >> 4, (u64)m + 1ull) : 0u;
+  const u64 off = Z.off, pos = Z.pos;
+  const u32 dead = Z.dead;
   uint8_t* const ring = st.logs + rg.base;
-  const u32 lmw = (A.debug & 1u) ? 0u : Z.lm;
+  const u32 lmw = (A.debug & 1u) ? 0u : lm8;
   const u32 sa = (u32)(R.src & 15u);
   u32 acc = 0;
-  const u32 nr = ok ? (m + kPR - 1u) / kPR : 0u;
+  const u32 nr = okp ? (m + kPR - 1u) / kPR : 0u;
   // records of at most 7 pieces (112 payload bytes) go through an LDS image of the log so that
   // 8 consecutive lanes store each record's 128 bytes; longer ones are stored piecewise
-  const bool img = __all(!ok || m <= 7u);
+  const bool img = __all(!okp || m <= 7u);
   const u32 w = threadIdx.x >> 6, r32 = lane >> 1;
   Stage3Smem& W = const_cast<Stage3Smem&>(S);
   // replication transport: every record also goes, whole, to the group's outbox once per remote
@@ -716,10 +747,10 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     if (j == 0) {
       u32 nx = 0;
       if (ok) {
-        const u64 rel = pos - Z.used;                                            // bytes into the group
-        const u64 rk = ((Z.ex >> 40) & kCnt23) + (R.cr.x & kRankMask);           // records into the group
+        const u64 rel = 16ull * Z.rel16;  // bytes into the group
+        const u64 rk = Z.rk;              // records into the group
         for (u32 r = 0; r < RF; ++r) {
-          if ((Z.lm >> r) & 1u) continue;
+          if ((lm8 >> r) & 1u) continue;
           const u32 e = A.outidx[(u64)p * RF + r];
           if (e == ~0u) continue;
           const XEntry x = A.xe3[e];
@@ -763,12 +794,66 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     }
   }
   // align the lane's register to the record end: its last piece is m-1 or m-2 (then 16 bytes short)
-  if (ok && m > j && ((m - 1u - j) & 1u)) acc = crc_zshift(S.z[0], acc);
+  if (okp && m > j && ((m - 1u - j) & 1u)) acc = crc_zshift(S.z[0], acc);
   acc ^= pair_swap(acc);
+
+  // ---- records longer than kBigPieces pieces: the whole wave, one record at a time
+  for (u64 bm = __ballot(j == 0 && big); bm; bm &= bm - 1ull) {
+    const u32 sl = (u32)__builtin_ctzll(bm), rb = sl >> 1;
+    const u64 bsrc = readlane64(R.src, sl), bpos = readlane64(pos, sl), boff = readlane64(off, sl);
+    const u64 bring = readlane64(reinterpret_cast<u64>(ring), sl), bmask = readlane64(segmask, sl);
+    const u32 bL = readlane32(L, sl), bdead = readlane32(dead, sl), blm = readlane32(lmw, sl);
+    const u32 bm16 = (bL + 15u) >> 4, sa_b = (u32)(bsrc & 15u);
+    const u64 a0 = bsrc & ~15ull, lim = bsrc + bL;
+    const u32 nx = xr ? W.xn[w][rb] : 0u;
+    u32 bacc = 0;
+    for (u32 k0 = 0; 64u * k0 < bm16; k0 += kBU) {
+      uint4 b0[kBU], b1[kBU];
+#pragma unroll
+      for (u32 u = 0; u < kBU; ++u) {
+        const u64 ad = a0 + 16ull * (64u * (k0 + u) + lane);
+        b0[u] = ad < lim ? *reinterpret_cast<const uint4*>(ad) : make_uint4(0, 0, 0, 0);
+        b1[u] = (sa_b && ad + 16ull < lim) ? *reinterpret_cast<const uint4*>(ad + 16ull) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (u32 u = 0; u < kBU; ++u) {
+        const u32 jp = 64u * (k0 + u) + lane;
+        if (jp < bm16) {
+          const u32 nb = bL - 16u * jp < 16u ? bL - 16u * jp : 16u;
+          const uint4 v = extract_piece(b0[u], b1[u], sa_b, nb);
+          bacc = crc_zshift(S.zk, bacc) ^ piece_crc(A, S, v, jp);
+          uint8_t* dst = reinterpret_cast<uint8_t*>(bring) + ((bpos + 16ull + 16ull * jp) & bmask);
+          if (jp + 1u >= bdead)
+            for (u32 r = 0; r < RF; ++r)
+              if ((blm >> r) & 1u) store_log16(dst + r * rstride, v);
+          if (xr)
+            for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(W.xdst[w][rb][q]) + 16ull + 16ull * jp, v);
+        }
+      }
+    }
+    // lane l's last piece is l + 64 (K - 1); e pieces follow it in the record
+    if (lane < bm16) {
+      const u32 e = (bm16 - 1u - lane) & 63u;
+      if (e) bacc = gf2_mulmod(bacc, A.crc->sh16[e]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) bacc ^= (u32)__shfl_xor((int)bacc, d, 64);
+    if (lane == 0) {
+      const u32 pad = 16u * bm16 - bL;
+      const u32 crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], bacc) : bacc);
+      const uint4 hb = make_uint4((u32)boff, (u32)(boff >> 32), bL, crc);
+      uint8_t* dst = reinterpret_cast<uint8_t*>(bring) + (bpos & bmask);
+      if (bdead == 0u)
+        for (u32 r = 0; r < RF; ++r)
+          if ((blm >> r) & 1u) store_log16(dst + r * rstride, hb);
+      if (xr)
+        for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(W.xdst[w][rb][q]), hb);
+    }
+  }
 
   // ---- header (lane 1), out offset (lane 0), sparse index (lane 1)
   uint4 h = make_uint4(0, 0, 0, 0);
-  if (ok && j == 1) {
+  if (okp && j == 1) {
     u32 crc = 0;
     if (L) {  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad))
       const u32 pad = 16u * m - L;
@@ -782,7 +867,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     // rejected record may be long, and its count must not spill into the flag bits
     if (j == 0)
       W.info[w][r32] = make_uint4((u32)pos, (u32)(pos >> 32), (u32)(rg.base >> 8),
-                                  ok ? Z.lm | (m << 8) | (1u << 12) | (dead << 13) | ((u32)(Z.rdesc & 63ull) << 24) : 0u);
+                                  okp ? lm8 | (m << 8) | (1u << 12) | (dead << 13) | ((u32)(Z.rdesc & 63ull) << 24) : 0u);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (u32 s4 = 0; s4 < kTaskRecs * 8u / 64u; ++s4) {
@@ -804,11 +889,11 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
       }
     }
     __builtin_amdgcn_wave_barrier();  // the image is rewritten by the wave's next task
-  } else if (ok && j == 1) {
+  } else if (okp && j == 1) {
     uint8_t* dst = ring + (pos & segmask);
     if (dead == 0u)
       for (u32 r = 0; r < RF; ++r)
-        if ((Z.lm >> r) & 1u) store_log16(dst + r * rstride, h);
+        if ((lm8 >> r) & 1u) store_log16(dst + r * rstride, h);
     if (xr)
       for (u32 q = 0; q < S.xn[w][r32]; ++q) store_log16(reinterpret_cast<uint8_t*>(S.xdst[w][r32][q]), h);
   }
@@ -826,10 +911,10 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     const bool h0 = j == 0;
     const u32 n_in = (u32)__popcll(__ballot(h0 && in));
     const u32 n_app = (u32)__popcll(__ballot(h0 && ok));
-    const u32 n_nl = (u32)__popcll(__ballot(h0 && cand && !Z.lead));
+    const u32 n_nl = (u32)__popcll(__ballot(h0 && cand && !lead));
     const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h0 && in && fl == kFlNoPart));
     const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
-    const u32 n_ns = (u32)__popcll(__ballot(h0 && cand && Z.lead && ns));
+    const u32 n_ns = (u32)__popcll(__ballot(h0 && cand && lead && ns));
     stat_out = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
   }
 }
@@ -980,10 +1065,12 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (!(A.debug & 8u)) {
     // slicing and zero-shift tables are contiguous in CrcConsts and in Stage3Smem: 16-byte copies
     static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
+    static_assert(offsetof(Stage3Smem, zk) == sizeof(S.t8) + sizeof(S.z), "z and zk adjacent in LDS");
     static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
+    static_assert(offsetof(CrcConsts, zshift1k) == offsetof(CrcConsts, zshift) + sizeof(A.crc->zshift), "zshift1k next");
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z) + sizeof(S.zk)) / 16u; k += kPT) dst[k] = src[k];
   }
   bool cand = task < tasks && stage3_cand(A, T, R);
   TaskState Z = stage3_r2(A, T, R, cand);
