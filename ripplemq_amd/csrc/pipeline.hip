@@ -580,7 +580,7 @@ constexpr u32 kBL = 5;          // blocks per lane per round (9 blocks cover 8 m
 // (lane l takes pieces l, l + 64, ...; kBU pieces per lane in flight): the lane-pair path would
 // keep its wave for m / 8 rounds while the other 31 pairs idle.
 constexpr u32 kBigPieces = 64;
-constexpr u32 kBU = 2;
+constexpr u32 kBU = 4;
 
 __device__ __forceinline__ u64 readlane64(u64 v, u32 l) {
   return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
@@ -808,19 +808,37 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
     const u32 nx = xr ? W.xn[w][rb] : 0u;
     u32 bacc = 0;
     for (u32 k0 = 0; 64u * k0 < bm16; k0 += kBU) {
-      uint4 b0[kBU], b1[kBU];
+      // aligned blocks 64 (k0 + u) + lane; a piece also needs the next block: the next lane's
+      // (lane 63: lane 0's of the next u, or one more load after the last u)
+      uint4 b0[kBU];
 #pragma unroll
       for (u32 u = 0; u < kBU; ++u) {
         const u64 ad = a0 + 16ull * (64u * (k0 + u) + lane);
         b0[u] = ad < lim ? *reinterpret_cast<const uint4*>(ad) : make_uint4(0, 0, 0, 0);
-        b1[u] = (sa_b && ad + 16ull < lim) ? *reinterpret_cast<const uint4*>(ad + 16ull) : make_uint4(0, 0, 0, 0);
+      }
+      uint4 tail = make_uint4(0, 0, 0, 0);
+      {
+        const u64 ad = a0 + 16ull * (64u * (k0 + kBU));
+        if (sa_b && lane == 63u && ad < lim) tail = *reinterpret_cast<const uint4*>(ad);
       }
 #pragma unroll
       for (u32 u = 0; u < kBU; ++u) {
         const u32 jp = 64u * (k0 + u) + lane;
+        uint4 b1;
+        b1.x = (u32)__shfl_down((int)b0[u].x, 1, 64);
+        b1.y = (u32)__shfl_down((int)b0[u].y, 1, 64);
+        b1.z = (u32)__shfl_down((int)b0[u].z, 1, 64);
+        b1.w = (u32)__shfl_down((int)b0[u].w, 1, 64);
+        if (lane == 63u) {
+          if (u + 1 < kBU)
+            b1 = make_uint4(readlane32(b0[u + 1 < kBU ? u + 1 : u].x, 0), readlane32(b0[u + 1 < kBU ? u + 1 : u].y, 0),
+                            readlane32(b0[u + 1 < kBU ? u + 1 : u].z, 0), readlane32(b0[u + 1 < kBU ? u + 1 : u].w, 0));
+          else
+            b1 = tail;
+        }
         if (jp < bm16) {
           const u32 nb = bL - 16u * jp < 16u ? bL - 16u * jp : 16u;
-          const uint4 v = extract_piece(b0[u], b1[u], sa_b, nb);
+          const uint4 v = extract_piece(b0[u], b1, sa_b, nb);
           bacc = crc_zshift(S.zk, bacc) ^ piece_crc(A, S, v, jp);
           uint8_t* dst = reinterpret_cast<uint8_t*>(bring) + ((bpos + 16ull + 16ull * jp) & bmask);
           if (jp + 1u >= bdead)
