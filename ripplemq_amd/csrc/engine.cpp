@@ -188,6 +188,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     const uint32_t slots = pipeline_wgs_per_cu() * e->cu_count, busy = a.wg1 + a.wg2 + a.wgp;
     const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
     a.wg3 = e->wg3_all ? want : std::min<uint32_t>(want, room);
+    a.wgb = e->big_wgs;
   }
   a.launch_seq = ++e->launch_seq;
   if (e->d_stamps && a.launch_seq == e->stamps_at) {
@@ -391,7 +392,7 @@ void free_engine(rmq_engine* e) {
     bufs.push_back(z.used);
   }
   for (const PipeScratch& x : e->scratch) {
-    void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo};
+    void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.nbig, x.bigl};
     for (void* p : xs) bufs.push_back(p);
   }
   delete e->copy_pool;
@@ -510,6 +511,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   hipDeviceProp_t prop;
   CREATE_HIP(hipGetDeviceProperties(&prop, e->device));
   e->cu_count = (uint32_t)prop.multiProcessorCount;
+  e->big_wgs = e->cu_count;
+  if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
@@ -577,6 +580,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_TRY(dalloc(&x.tsum, GT * 4));
     CREATE_TRY(dalloc(&x.tile_base, GT));
     CREATE_TRY(dalloc(&x.binfo, (size_t)kMaxGroup * 4));
+    CREATE_TRY(dalloc(&x.nbig, 1));
+    CREATE_TRY(dalloc(&x.bigl, GT * kTileRecs));
   }
   if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(2u * e->cu_count + kMaxTiles + (P + kPipeThreads - 1) / kPipeThreads +
                                                        kMaxTiles * kTileRecs / (kTaskRecs * kPipeThreads / 64)) * 64));

@@ -144,6 +144,8 @@ struct PipeScratch {
   uint64_t* tsum;       // [tiles][4] {payload bytes, record bytes, invalid records, 0}
   uint64_t* tile_base;  // [tiles] payload offset of the tile's first record inside its batch
   uint64_t* binfo;      // [kMaxGroup][4] per batch {reject flags (2 invalid payload ranges), 0, payload bytes, 0}
+  uint32_t* nbig;       // [1] records over 1 KB in the group (stage 1 appends, stage 4 resets)
+  uint32_t* bigl;       // [tiles * kTileRecs] their group record slots, in no particular order
 };
 
 // The single per-group launch: stage 1 (rank the tiles of group k), stage 2 (column scans of
@@ -154,6 +156,7 @@ struct PipeArgs {
   PipeGroup g1, g2, g3, g4;
   PipeScratch s1, s2, s3, s4;
   uint32_t wg1, wg2, wgp, wg3;  // workgroups per role, in this order along blockIdx.x
+  uint32_t wgb;                 // stage 3's large-record workgroups (last along blockIdx.x)
   uint32_t key_passes;     // 1 (P <= 256) or 2
   uint32_t gt;             // tiles per hist / excl column (group tile capacity)
   uint32_t s3_first;       // 1: stage-3 workgroups first along blockIdx.x (dispatched first)

@@ -131,6 +131,18 @@ __device__ __forceinline__ u32 batch_end_tile(const PipeGroup& G, u32 t) {
   return e;
 }
 
+// Records longer than kBigPieces payload pieces are stored by the whole wave, one after another
+// (lane l takes pieces l, l + 64, ...; kBU pieces per lane in flight): the lane-pair path would
+// keep its wave for m / 8 rounds while the other 31 pairs idle.
+constexpr u32 kBigPieces = 64;
+constexpr u32 kBU = 4;
+
+__device__ __forceinline__ u64 readlane64(u64 v, u32 l) {
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+         (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
+}
+__device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
+
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
@@ -175,6 +187,15 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
     const u32 rs16 = fl[r] == kFlJunk ? 0u : record_rs16(lenv[r]);
     S.info[q] = rs16 | (fl[r] << kFlagShift);
     item[r] = (pc[r] << kIB) | q;
+    // records over 1 KB go to stage 3's large-record waves (kBigPieces)
+    const bool bigr = fl[r] == 0u && lenv[r] > 16u * kBigPieces;
+    const u64 bm = __ballot(bigr);
+    if (bm) {
+      u32 at = 0;
+      if (lane == 0) at = atomicAdd(x.nbig, (u32)__popcll(bm));
+      at = readlane32(at, 0) + (u32)__popcll(bm & lt);
+      if (bigr) x.bigl[at] = (u32)(gbase + q);
+    }
   }
 
   // ---- input-order scans: payload prefix per record, tile sums {payload, invalid ranges}
@@ -576,18 +597,6 @@ __device__ __forceinline__ uint4 extract_piece(uint4 b0, uint4 b1, u32 s, u32 nb
 constexpr u32 kPR = 8;          // pieces per record per round
 constexpr u32 kBL = 5;          // blocks per lane per round (9 blocks cover 8 misaligned pieces)
 
-// Records longer than kBigPieces payload pieces are stored by the whole wave, one after another
-// (lane l takes pieces l, l + 64, ...; kBU pieces per lane in flight): the lane-pair path would
-// keep its wave for m / 8 rounds while the other 31 pairs idle.
-constexpr u32 kBigPieces = 64;
-constexpr u32 kBU = 4;
-
-__device__ __forceinline__ u64 readlane64(u64 v, u32 l) {
-  return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
-         (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
-}
-__device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
-
 __device__ __forceinline__ uint4 pair_swap4(uint4 v) {
   return make_uint4(pair_swap(v.x), pair_swap(v.y), pair_swap(v.z), pair_swap(v.w));
 }
@@ -705,6 +714,125 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
   return (A.debug & 2u) ? v.x : crc_piece16(S.t8, v);
 }
 
+// One record over 1 KB, by the whole wave (wave-uniform arguments): lane l takes payload pieces
+// l, l + 64, ... (kBU per lane in flight, the block after each from the neighbour lane), folds
+// them by Horner's rule with the 1 KB shift table, shifts its register past the pieces that follow
+// its last one and the wave XOR-reduces; lane 0 writes the header. xdst: the record's outbox copies.
+__device__ void big_record(const PipeArgs& A, const Stage3Smem& S, u64 src, u32 L, u64 pos, u64 off, u32 dead,
+                           uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx) {
+  const u32 lane = threadIdx.x & 63, RF = A.st.RF;
+  const u64 rstride = A.st.rstride;
+  const u32 m = (L + 15u) >> 4, sa = (u32)(src & 15u);
+  const u64 a0 = src & ~15ull, lim = src + L;
+  u32 acc = 0;
+  for (u32 k0 = 0; 64u * k0 < m; k0 += kBU) {
+    uint4 b0[kBU];
+#pragma unroll
+    for (u32 u = 0; u < kBU; ++u) {
+      const u64 ad = a0 + 16ull * (64u * (k0 + u) + lane);
+      b0[u] = ad < lim ? *reinterpret_cast<const uint4*>(ad) : make_uint4(0, 0, 0, 0);
+    }
+    uint4 tail = make_uint4(0, 0, 0, 0);
+    {
+      const u64 ad = a0 + 16ull * (64u * (k0 + kBU));
+      if (sa && lane == 63u && ad < lim) tail = *reinterpret_cast<const uint4*>(ad);
+    }
+#pragma unroll
+    for (u32 u = 0; u < kBU; ++u) {
+      const u32 jp = 64u * (k0 + u) + lane;
+      uint4 b1;
+      b1.x = (u32)__shfl_down((int)b0[u].x, 1, 64);
+      b1.y = (u32)__shfl_down((int)b0[u].y, 1, 64);
+      b1.z = (u32)__shfl_down((int)b0[u].z, 1, 64);
+      b1.w = (u32)__shfl_down((int)b0[u].w, 1, 64);
+      if (lane == 63u) {
+        const u32 un = u + 1 < kBU ? u + 1 : u;  // unrolled: a constant
+        b1 = u + 1 < kBU ? make_uint4(readlane32(b0[un].x, 0), readlane32(b0[un].y, 0), readlane32(b0[un].z, 0),
+                                      readlane32(b0[un].w, 0))
+                         : tail;
+      }
+      if (jp < m) {
+        const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
+        const uint4 v = extract_piece(b0[u], b1, sa, nb);
+        acc = crc_zshift(S.zk, acc) ^ piece_crc(A, S, v, jp);
+        uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
+        if (jp + 1u >= dead)
+          for (u32 r = 0; r < RF; ++r)
+            if ((lm >> r) & 1u) store_log16(dst + r * rstride, v);
+        for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(xdst[q]) + 16ull + 16ull * jp, v);
+      }
+    }
+  }
+  // lane l's last piece is l + 64 (K - 1); e pieces follow it in the record
+  if (lane < m) {
+    const u32 e = (m - 1u - lane) & 63u;
+    if (e) acc = gf2_mulmod(acc, A.crc->sh16[e]);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) acc ^= (u32)__shfl_xor((int)acc, d, 64);
+  if (lane == 0) {
+    const u32 pad = 16u * m - L;
+    const u32 crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
+    const uint4 h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
+    if (dead == 0u)
+      for (u32 r = 0; r < RF; ++r)
+        if ((lm >> r) & 1u) store_log16(ring + (pos & segmask) + r * rstride, h);
+    for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(xdst[q]), h);
+  }
+}
+
+// Large-record waves of the stage-3 launch: wave g of G takes entries g, g + G, ... of the group's
+// list of records over 1 KB (stage 1), re-derives each record's place like stage3_r1/r2 and stores
+// it with big_record. Their task waves leave these records to them (header and payload; the task
+// wave still writes the out offset, index entries, record-table slots and statistics).
+template <bool XR>
+__device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
+  const PipeGroup& G = A.g3;
+  const PipeScratch& x = A.s3;
+  const DevState& st = A.st;
+  const u32 nbig = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(x.nbig));
+  if (!nbig) return;  // no table copy either
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z) + sizeof(S.zk)) / 16u; k += kPT) dst[k] = src[k];
+  }
+  __syncthreads();
+  const u32 nw = A.wgb * kPW;
+  for (u32 e = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6)); e < nbig; e += nw) {
+    const u32 gi = __builtin_amdgcn_readfirstlane(x.bigl[e]);
+    const u32 t = gi / kTR, jb = batch_of_tile(G, t);
+    const PipeBatch& b = G.b[jb];
+    const u32 i = (t - G.tile0[jb]) * kTR + gi % kTR;
+    if ((u32)A.s3.binfo[jb * 4]) continue;  // batch rejected as a whole
+    const uint2 cr = x.crank[gi];
+    if ((cr.x >> kFlagShift) != 0u) continue;
+    const u32 p = b.pidx[i], L = b.len[i];
+    const u64 src = reinterpret_cast<u64>(b.payload) + (b.poff ? b.poff[i] : x.tile_base[t] + x.pre[gi]);
+    const u64 ex = x.excl[(u64)p * A.gt + t];
+    if (!st.is_leader[p] || (ex & kExclNoSpace)) continue;
+    const u64 tot = x.totals[p], leo = A.cur.leo[p], used = A.cur.used[p];
+    const u32 rk = (u32)((ex >> 40) & kCnt23) + (cr.x & kRankMask);
+    const u32 rel16 = (u32)(ex & kLow40) + cr.y;
+    const u64 off = leo + rk, pos = used + 16ull * rel16;
+    const RingRef rg = ring_ref(st.ring[p], st.interval_log2, st.icap_mul);
+    const u64 gend = used + 16ull * (tot & kLow40);
+    const u32 dead = gend > pos + rg.seg ? (u32)min((gend - rg.seg - pos) >> 4, (u64)((L + 15u) >> 4) + 1ull) : 0u;
+    const u32 lm = st.local_mask[p];
+    u64 xdst[kMaxRemote];
+    u32 nx = 0;
+    if (XR) {
+      for (u32 r = 0; r < st.RF && nx < kMaxRemote; ++r) {
+        if ((lm >> r) & 1u) continue;
+        const u32 oe = A.outidx[(u64)p * st.RF + r];
+        if (oe == ~0u) continue;
+        xdst[nx++] = reinterpret_cast<u64>(A.outbox3 + A.xe3[oe].data_abs + 16ull * rel16);
+      }
+    }
+    big_record(A, S, src, L, pos, off, dead, st.logs + rg.base, rg.seg - 1ull, (A.debug & 1u) ? 0u : lm, xdst, nx);
+  }
+}
+
 template <bool XR>
 __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
                               const TaskState& Z, bool cand, uint4& stat_out) {
@@ -796,78 +924,6 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   // align the lane's register to the record end: its last piece is m-1 or m-2 (then 16 bytes short)
   if (okp && m > j && ((m - 1u - j) & 1u)) acc = crc_zshift(S.z[0], acc);
   acc ^= pair_swap(acc);
-
-  // ---- records longer than kBigPieces pieces: the whole wave, one record at a time
-  for (u64 bm = __ballot(j == 0 && big); bm; bm &= bm - 1ull) {
-    const u32 sl = (u32)__builtin_ctzll(bm), rb = sl >> 1;
-    const u64 bsrc = readlane64(R.src, sl), bpos = readlane64(pos, sl), boff = readlane64(off, sl);
-    const u64 bring = readlane64(reinterpret_cast<u64>(ring), sl), bmask = readlane64(segmask, sl);
-    const u32 bL = readlane32(L, sl), bdead = readlane32(dead, sl), blm = readlane32(lmw, sl);
-    const u32 bm16 = (bL + 15u) >> 4, sa_b = (u32)(bsrc & 15u);
-    const u64 a0 = bsrc & ~15ull, lim = bsrc + bL;
-    const u32 nx = xr ? W.xn[w][rb] : 0u;
-    u32 bacc = 0;
-    for (u32 k0 = 0; 64u * k0 < bm16; k0 += kBU) {
-      // aligned blocks 64 (k0 + u) + lane; a piece also needs the next block: the next lane's
-      // (lane 63: lane 0's of the next u, or one more load after the last u)
-      uint4 b0[kBU];
-#pragma unroll
-      for (u32 u = 0; u < kBU; ++u) {
-        const u64 ad = a0 + 16ull * (64u * (k0 + u) + lane);
-        b0[u] = ad < lim ? *reinterpret_cast<const uint4*>(ad) : make_uint4(0, 0, 0, 0);
-      }
-      uint4 tail = make_uint4(0, 0, 0, 0);
-      {
-        const u64 ad = a0 + 16ull * (64u * (k0 + kBU));
-        if (sa_b && lane == 63u && ad < lim) tail = *reinterpret_cast<const uint4*>(ad);
-      }
-#pragma unroll
-      for (u32 u = 0; u < kBU; ++u) {
-        const u32 jp = 64u * (k0 + u) + lane;
-        uint4 b1;
-        b1.x = (u32)__shfl_down((int)b0[u].x, 1, 64);
-        b1.y = (u32)__shfl_down((int)b0[u].y, 1, 64);
-        b1.z = (u32)__shfl_down((int)b0[u].z, 1, 64);
-        b1.w = (u32)__shfl_down((int)b0[u].w, 1, 64);
-        if (lane == 63u) {
-          if (u + 1 < kBU)
-            b1 = make_uint4(readlane32(b0[u + 1 < kBU ? u + 1 : u].x, 0), readlane32(b0[u + 1 < kBU ? u + 1 : u].y, 0),
-                            readlane32(b0[u + 1 < kBU ? u + 1 : u].z, 0), readlane32(b0[u + 1 < kBU ? u + 1 : u].w, 0));
-          else
-            b1 = tail;
-        }
-        if (jp < bm16) {
-          const u32 nb = bL - 16u * jp < 16u ? bL - 16u * jp : 16u;
-          const uint4 v = extract_piece(b0[u], b1, sa_b, nb);
-          bacc = crc_zshift(S.zk, bacc) ^ piece_crc(A, S, v, jp);
-          uint8_t* dst = reinterpret_cast<uint8_t*>(bring) + ((bpos + 16ull + 16ull * jp) & bmask);
-          if (jp + 1u >= bdead)
-            for (u32 r = 0; r < RF; ++r)
-              if ((blm >> r) & 1u) store_log16(dst + r * rstride, v);
-          if (xr)
-            for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(W.xdst[w][rb][q]) + 16ull + 16ull * jp, v);
-        }
-      }
-    }
-    // lane l's last piece is l + 64 (K - 1); e pieces follow it in the record
-    if (lane < bm16) {
-      const u32 e = (bm16 - 1u - lane) & 63u;
-      if (e) bacc = gf2_mulmod(bacc, A.crc->sh16[e]);
-    }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) bacc ^= (u32)__shfl_xor((int)bacc, d, 64);
-    if (lane == 0) {
-      const u32 pad = 16u * bm16 - bL;
-      const u32 crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], bacc) : bacc);
-      const uint4 hb = make_uint4((u32)boff, (u32)(boff >> 32), bL, crc);
-      uint8_t* dst = reinterpret_cast<uint8_t*>(bring) + (bpos & bmask);
-      if (bdead == 0u)
-        for (u32 r = 0; r < RF; ++r)
-          if ((blm >> r) & 1u) store_log16(dst + r * rstride, hb);
-      if (xr)
-        for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(W.xdst[w][rb][q]), hb);
-    }
-  }
 
   // ---- header (lane 1), out offset (lane 0), sparse index (lane 1)
   uint4 h = make_uint4(0, 0, 0, 0);
@@ -1035,8 +1091,12 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
     __hip_atomic_store(A.done_word, A.launch_seq - 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   u32 wg = blockIdx.x;
-  // roles along blockIdx.x: [stage 1 | stage 2 | partition threads | stage 3], or with s3_first
-  // [stage 3 | stage 1 | stage 2 | partition threads]
+  // roles along blockIdx.x: [stage 1 | stage 2 | partition threads | stage 3 | large records], or
+  // with s3_first [stage 3 | stage 1 | stage 2 | partition threads | large records]
+  if (wg >= A.wg1 + A.wg2 + A.wgp + A.wg3) {
+    stage3_big_waves<XR>(A, *reinterpret_cast<Stage3Smem*>(smem_raw), wg - (A.wg1 + A.wg2 + A.wgp + A.wg3));
+    return;
+  }
   bool s3 = false;
   if (A.s3_first) {
     s3 = wg < A.wg3;
@@ -1062,6 +1122,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     wg -= A.wg2;
     // partition threads: stage 3's state advance and stage 4's retention
     PIPE_STAMP(0);
+    if (wg == 0 && threadIdx.x == 0 && A.g4.nb) *A.s4.nbig = 0u;  // the set's next group starts its list
     for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) {
       if (A.g3.nb || A.ackin) partition_apply(A, p);
       if (A.g4.nb) partition_retention(A, p);
@@ -1088,7 +1149,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     static_assert(offsetof(CrcConsts, zshift1k) == offsetof(CrcConsts, zshift) + sizeof(A.crc->zshift), "zshift1k next");
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z) + sizeof(S.zk)) / 16u; k += kPT) dst[k] = src[k];
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];  // zk: large-record waves only
   }
   bool cand = task < tasks && stage3_cand(A, T, R);
   TaskState Z = stage3_r2(A, T, R, cand);
@@ -1116,7 +1177,7 @@ uint32_t pipeline_lds_bytes() { return (uint32_t)kSmemBytes; }
 uint32_t pipeline_wgs_per_cu() { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (kPT / 64u); }
 
 void launch_pipeline(const PipeArgs& a, hipStream_t s) {
-  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3;
+  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb;
   if (!grid) return;
   if (a.outidx)
     hipLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, a);
