@@ -511,7 +511,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   hipDeviceProp_t prop;
   CREATE_HIP(hipGetDeviceProperties(&prop, e->device));
   e->cu_count = (uint32_t)prop.multiProcessorCount;
-  e->big_wgs = e->cu_count;
+  e->big_wgs = 4u * e->cu_count;
   if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
