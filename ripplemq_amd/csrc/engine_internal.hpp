@@ -303,7 +303,7 @@ struct rmq_engine {
   uint32_t wg3_all = 1;
   uint32_t s1_wgs = 0;    // RMQ_S1_WGS: stage-1 workgroups per launch (0: one per tile; fewer loop over tiles)
   uint32_t s2_wgs = 0;    // RMQ_S2_WGS: cap on stage-2 workgroups (0: one thread group per column)
-  uint32_t s3_first = 0;  // RMQ_S3_FIRST=1: stage-3 workgroups first in dispatch order
+  uint32_t s3_first = 1;  // stage-3 workgroups first in dispatch order (RMQ_S3_FIRST=0: last)
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
   std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)
   rmq::Replication* repl = nullptr;  // replication transport attached (collective mode)

@@ -132,6 +132,29 @@ def test_large_records_direct_path(oracle_mod):
         run_ops(dev, ora, cfg, ops)
 
 
+@pytest.mark.parametrize("big_wgs", [None, "1"])
+def test_large_record_waves_in_groups(oracle_mod, monkeypatch, big_wgs):
+    # records over 1 KB go to stage 3's large-record waves: rings that wrap inside a launch group
+    # (dead pieces), a partition this engine does not lead, a no-space batch of large records, and
+    # one workgroup taking the whole list (RMQ_BIG_WGS=1)
+    if big_wgs:
+        monkeypatch.setenv("RMQ_BIG_WGS", big_wgs)
+    cfg, dev, ora = pair(oracle_mod, num_partitions=8, replication_factor=3, segment_bytes=1 << 18,
+                         index_interval=1024, max_batch_records=4096, max_batch_bytes=8 << 20, pipeline_depth=4)
+    with dev, ora:
+        for e in (dev, ora):
+            e.set_replicas(6, [1, 0, 2], 0)  # partition 6 led by rank 1
+        spec = StreamSpec(8, 200, "uniform", size=(64, 16384), config_index=19)
+        batches = [make_batch(spec, b) for b in range(9)]
+        g = np.random.default_rng(19)
+        hog_l = g.integers(4000, 16000, 90).astype(np.uint32)  # > 256 KiB for partition 0: no space
+        hog = Batch(np.zeros(90, np.uint32), hog_l, g.integers(0, 256, int(hog_l.sum()), dtype=np.uint8))
+        batches.insert(5, hog)
+        _pipelined(dev, ora, batches)
+        compare_state(dev, ora, cfg, full_rings=True)
+        assert max(ora.state(p)["log_start_offset"] for p in range(8)) > 0, "rings must wrap"
+
+
 def test_rejections_and_leadership(oracle_mod):
     cfg, dev, ora = pair(oracle_mod, num_partitions=16, replication_factor=3, segment_bytes=1 << 20,
                          index_interval=256, max_batch_records=4096)
@@ -267,10 +290,11 @@ def test_pipelined_groups(oracle_mod, group):
         assert dev.state(5)["log_end_offset"] == 0
 
 
-@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "1"}])
+@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"}])
 def test_pipelined_dispatch_modes(oracle_mod, monkeypatch, env):
-    # the non-default stage-3 dispatch modes (read at rmq_create): resident task waves looping over
-    # the group's tasks, and stage-3 workgroups dispatched before the other roles
+    # the non-default dispatch modes (read at rmq_create): resident task waves looping over the
+    # group's tasks, stage-3 workgroups dispatched after the other roles, and few large-record
+    # workgroups (each wave then takes many records of the list)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,

@@ -1,9 +1,11 @@
-set -e
+# Phase stamps of one steady-state launch (launch 100) of the default bench, plus a DEBUG timing
+# set: 1 no ring stores, 16 stage 3 alone. usage: bash tools/gpu_stamps.sh <tag>
+set -o pipefail
 cd $GRAFT_REPO_ROOT
-export HSA_ENABLE_IPC_MODE_LEGACY=0
+T=$1
 mkdir -p gpurun_out
-RMQ_DEBUG_SKIP=4 RMQ_STAMPS=gpurun_out/stamps_serial.csv timeout -k 10 240 python bench.py --steps 200 --warmup 50 --no-cpu-baseline > gpurun_out/b_serial.log 2>&1
-RMQ_STAMPS=gpurun_out/stamps_overlap.csv timeout -k 10 240 python bench.py --steps 200 --warmup 50 --no-cpu-baseline > gpurun_out/b_overlap.log 2>&1
-python tools/stamps.py gpurun_out/stamps_serial.csv gpurun_out/stamps_overlap.csv > gpurun_out/stamps.txt
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o r1 -- python3 $GRAFT_REPO_ROOT/bench.py --steps 500 --warmup 100 > $GRAFT_REPO_ROOT/gpurun_out/b_prof.log 2>&1
+RMQ_STAMPS=gpurun_out/${T}_st.csv RMQ_STAMPS_AT=100 timeout -k 10 200 python bench.py --steps 600 --warmup 60 --no-cpu-baseline --fetch-rounds 0 --host-steps 0 > gpurun_out/${T}_stamped_B_1.json 2>&1 || exit 1
+python tools/pipe_stamps.py gpurun_out/${T}_st.csv > gpurun_out/${T}_stamps.txt 2>&1
+for d in 1 2 4 16; do
+  RMQ_DEBUG=$d timeout -k 10 200 python bench.py --steps 400 --warmup 40 --no-cpu-baseline --fetch-rounds 0 --host-steps 0 > gpurun_out/${T}_dbg${d}_B_1.json 2>&1 || true
+done
