@@ -61,15 +61,22 @@ void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(consumer_apply_kernel, grid_for(a.n, 256), dim3(256), 0, s, a);
 }
 
-// Workgroup per moved partition. Every 16-byte piece of the new ring of every replica slot gets its
-// logical position's bytes if that position is retained ([spos, used) is at most one new ring
-// long), zero otherwise; every slot of the new index ring gets entry m (m = the retained m with
-// m mod icap = slot) or zero. Old and new blocks are disjoint (both allocated while moving).
-__global__ __launch_bounds__(256) void migrate_kernel(DevState st, const MigrateItem* items) {
-  const MigrateItem it = items[blockIdx.x];
-  // the partition's new ring and log start, written by the device (a host copy into these arrays
-  // could leave other XCDs' L2 holding the old lines for the next launch)
-  if (threadIdx.x == 0) {
+// A move in chunks: workgroup c of a moved partition owns bytes [c K, (c + 1) K) of the new ring
+// of every replica slot (K = kMigrateChunk, or the whole ring when smaller) and the same share of
+// its index ring. Each 16-byte piece gets its logical position's bytes if that position is
+// retained ([spos, used) is at most one new ring long), zero otherwise; each index slot gets entry
+// m (the retained m with m mod icap = slot) or zero. Old and new blocks are disjoint (both
+// allocated while moving). The first chunk writes the partition's new descriptor and log start on
+// the device (a host copy into these arrays could leave other XCDs' L2 holding the old lines).
+__global__ __launch_bounds__(256) void migrate_kernel(DevState st, const MigrateItem* items, u32 n) {
+  u32 lo = 0, hi = n;  // the item whose chunks hold blockIdx.x: largest chunk0 <= blockIdx.x
+  while (hi - lo > 1) {
+    const u32 mid = (lo + hi) / 2;
+    if (items[mid].chunk0 <= blockIdx.x) lo = mid; else hi = mid;
+  }
+  const MigrateItem it = items[lo];
+  const u32 c = blockIdx.x - it.chunk0;
+  if (c == 0 && threadIdx.x == 0) {
     st.ring[it.p] = it.new_desc;
     st.start_pos[it.p] = it.spos;
     st.start_off[it.p] = it.soff;
@@ -78,10 +85,12 @@ __global__ __launch_bounds__(256) void migrate_kernel(DevState st, const Migrate
   const RingRef nw = ring_ref(it.new_desc, st.interval_log2, st.icap_mul);
   const u64 keep = it.used - it.spos, nmask = nw.seg - 1ull, omask = o.seg - 1ull;
   const u64 s0 = it.spos & nmask;
+  const u64 K = nw.seg < kMigrateChunk ? nw.seg : kMigrateChunk;
+  const u64 q0 = (c * K) >> 4, q1 = ((c + 1ull) * K) >> 4;
   for (u32 r = 0; r < st.RF; ++r) {
     const uint8_t* src = st.logs + (u64)r * st.rstride + o.base;
     uint8_t* dst = st.logs + (u64)r * st.rstride + nw.base;
-    for (u64 q = threadIdx.x; q < (nw.seg >> 4); q += blockDim.x) {
+    for (u64 q = q0 + threadIdx.x; q < q1; q += blockDim.x) {
       const u64 d = ((16ull * q - s0) & nmask);  // bytes after spos, if retained
       uint4 v = make_uint4(0, 0, 0, 0);
       if (d < keep) v = *reinterpret_cast<const uint4*>(src + ((it.spos + d) & omask));
@@ -90,7 +99,8 @@ __global__ __launch_bounds__(256) void migrate_kernel(DevState st, const Migrate
   }
   const u32 ilog = st.interval_log2;
   const u64 m0 = (it.spos + (1ull << ilog) - 1) >> ilog, m1 = it.used >> ilog;
-  for (u64 q = threadIdx.x; q < nw.icap; q += blockDim.x) {
+  const u64 nch = nw.seg / K, i0 = nw.icap * c / nch, i1 = nw.icap * (c + 1ull) / nch;
+  for (u64 q = i0 + threadIdx.x; q < i1; q += blockDim.x) {
     const u64 m = m0 + ((q + nw.icap - m0 % nw.icap) % nw.icap);
     u64 e0 = 0, e1 = 0;
     if (m <= m1) {
@@ -104,8 +114,8 @@ __global__ __launch_bounds__(256) void migrate_kernel(DevState st, const Migrate
   }
 }
 
-void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, hipStream_t s) {
-  if (n) hipLaunchKernelGGL(migrate_kernel, dim3(n), dim3(256), 0, s, st, items);
+void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(migrate_kernel, dim3(chunks), dim3(256), 0, s, st, items, n);
 }
 
 }  // namespace rmq

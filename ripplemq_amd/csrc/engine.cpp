@@ -766,11 +766,17 @@ int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint
     it.soff = soff[p];
     it.used = used[p];
   }
+  uint32_t chunks = 0;  // workgroups of each move: its new ring in kMigrateChunk pieces
+  for (MigrateItem& it : items) {
+    it.chunk0 = chunks;
+    const uint64_t S1 = 1ull << (it.new_desc & 63ull);
+    chunks += (uint32_t)((S1 + kMigrateChunk - 1) / kMigrateChunk);
+  }
   MigrateItem* d_items = nullptr;
   rc = dalloc(&d_items, items.size());
   if (!rc) {
     HIP_TRY(hipMemcpy(d_items, items.data(), items.size() * sizeof(MigrateItem), hipMemcpyHostToDevice));
-    launch_migrate(e->st, d_items, (uint32_t)items.size(), e->main_s);
+    launch_migrate(e->st, d_items, (uint32_t)items.size(), chunks, e->main_s);
     if (hipGetLastError() != hipSuccess) rc = RMQ_EDEVICE;
   }
   if (!rc) {

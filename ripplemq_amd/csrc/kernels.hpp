@@ -236,7 +236,8 @@ struct AckApplyArgs {
 // One partition's ring moving to a new block of the pool (rmq_set_segments): the retained log
 // [spos, used) of every replica slot and its index entries are copied; the new block is zeroed first.
 struct MigrateItem {
-  uint32_t p, pad;
+  uint32_t p;
+  uint32_t chunk0;              // first workgroup of the move (prefix of kMigrateChunk pieces)
   uint64_t old_desc, new_desc;  // DevState::ring descriptors
   uint64_t spos, used;          // retained log [spos, used) after the move
   uint64_t soff;                // offset of the record at spos
@@ -253,7 +254,9 @@ void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev_resolve0, hip
                   hipEvent_t ev_gather0, hipEvent_t ev_gather1);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s);
-void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, hipStream_t s);
+constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
+// chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))
+void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s);
 void launch_ack_apply(const AckApplyArgs& a, hipStream_t s);
 
 }  // namespace rmq

@@ -33,6 +33,7 @@ namespace rmq {
 constexpr u32 kIT = 512;           // threads per ingest workgroup
 constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
 constexpr u32 kIR = 32;            // records per task
+constexpr u32 kBigIngest = 64;     // records over this many 16-byte pieces: the whole wave
 
 struct RegionView {
   const uint8_t* base;
@@ -135,13 +136,17 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
 __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   __shared__ __attribute__((aligned(16))) u32 t8[8][256];
   __shared__ __attribute__((aligned(16))) u32 z[2][4][256];
+  __shared__ __attribute__((aligned(16))) u32 zk[4][256];  // 1 KB shift: records over 1 KB, by the wave
   {
     static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
+    static_assert(offsetof(CrcConsts, zshift1k) == offsetof(CrcConsts, zshift) + sizeof(A.crc->zshift), "zshift1k next");
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
     uint4* d0 = reinterpret_cast<uint4*>(&t8[0][0]);
     uint4* d1 = reinterpret_cast<uint4*>(&z[0][0][0]);
+    uint4* d2 = reinterpret_cast<uint4*>(&zk[0][0]);
     for (u32 k = threadIdx.x; k < sizeof(t8) / 16; k += kIT) d0[k] = src[k];
     for (u32 k = threadIdx.x; k < sizeof(z) / 16; k += kIT) d1[k] = src[sizeof(t8) / 16 + k];
+    for (u32 k = threadIdx.x; k < sizeof(zk) / 16; k += kIT) d2[k] = src[(sizeof(t8) + sizeof(z)) / 16 + k];
   }
   __syncthreads();
   const u32 task = __builtin_amdgcn_readfirstlane(blockIdx.x * kIW + (threadIdx.x >> 6));
@@ -182,8 +187,10 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
     if (!ok && j == 1) atomicOr(&A.bad[e], 2u);  // does not continue the follower's log
   }
   // CRC32C of the payload from its 16-byte pieces (zero-padded in the log): lane j folds pieces
-  // j, j + 2, ... by Horner's rule with the 32-byte zero-shift table
-  const u32 mm = ok ? m : 0u;
+  // j, j + 2, ... by Horner's rule with the 32-byte zero-shift table; records over 1 KB are done
+  // by the whole wave below
+  const bool big = ok && m > kBigIngest;
+  const u32 mm = ok && !big ? m : 0u;
   u32 acc = 0;
   const RingRef rg = ring_ref(st, p);  // p = 0 for lanes without a record (nothing is stored)
   uint8_t* const ring = st.logs + (u64)(in ? A.xi_slot[e] : 0u) * st.rstride + rg.base;
@@ -200,6 +207,50 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   }
   if (ok && mm > j && ((mm - 1u - j) & 1u)) acc = crc_zshift(z[0], acc);
   acc ^= pair_swap(acc);
+  // records over 1 KB, one at a time by the wave: lane l takes pieces l, l + 64, ... (Horner with
+  // the 1 KB shift), shifts past the pieces after its last one, XOR-reduce; the record's lane 1
+  // gets the register
+  for (u64 bm = __ballot(j == 0 && big); bm; bm &= bm - 1ull) {
+    const u32 sl = (u32)__builtin_ctzll(bm);
+    const u64 brec = ((u64)(u32)__builtin_amdgcn_readlane((int)(reinterpret_cast<u64>(rec) >> 32), (int)sl) << 32) |
+                     (u32)__builtin_amdgcn_readlane((int)(u32)reinterpret_cast<u64>(rec), (int)sl);
+    const u64 bpos = ((u64)(u32)__builtin_amdgcn_readlane((int)(pos >> 32), (int)sl) << 32) |
+                     (u32)__builtin_amdgcn_readlane((int)(u32)pos, (int)sl);
+    const u64 bgend = ((u64)(u32)__builtin_amdgcn_readlane((int)(gend >> 32), (int)sl) << 32) |
+                      (u32)__builtin_amdgcn_readlane((int)(u32)gend, (int)sl);
+    const u64 bring = ((u64)(u32)__builtin_amdgcn_readlane((int)(reinterpret_cast<u64>(ring) >> 32), (int)sl) << 32) |
+                      (u32)__builtin_amdgcn_readlane((int)(u32)reinterpret_cast<u64>(ring), (int)sl);
+    const u32 bm16 = ((u32)__builtin_amdgcn_readlane((int)L, (int)sl) + 15u) >> 4;
+    const u64 bseg = ((u64)(u32)__builtin_amdgcn_readlane((int)(rg.seg >> 32), (int)sl) << 32) |
+                     (u32)__builtin_amdgcn_readlane((int)(u32)rg.seg, (int)sl);
+    u32 bacc = 0;
+    for (u32 k0 = 0; 64u * k0 < bm16; k0 += 4u) {
+      uint4 v[4];
+#pragma unroll
+      for (u32 u = 0; u < 4u; ++u) {
+        const u32 jp = 64u * (k0 + u) + lane;
+        v[u] = jp < bm16 ? *reinterpret_cast<const uint4*>(brec + 16ull + 16ull * jp) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (u32 u = 0; u < 4u; ++u) {
+        const u32 jp = 64u * (k0 + u) + lane;
+        if (jp < bm16) {
+          const u64 x = bpos + 16ull + 16ull * jp;
+          if (x + bseg >= bgend) store_log16(reinterpret_cast<uint8_t*>(bring) + (x & (bseg - 1ull)), v[u]);
+          uint4 w = v[u];
+          if (jp == 0) w.x ^= 0xFFFFFFFFu;
+          bacc = crc_zshift(zk, bacc) ^ crc_piece16(t8, w);
+        }
+      }
+    }
+    if (lane < bm16) {
+      const u32 eb = (bm16 - 1u - lane) & 63u;
+      if (eb) bacc = gf2_mulmod(bacc, A.crc->sh16[eb]);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) bacc ^= (u32)__shfl_xor((int)bacc, d, 64);
+    if (lane == sl + 1u) acc = bacc;
+  }
   if (ok && j == 1) {
     u32 crc = 0;
     if (L) {
