@@ -11,6 +11,8 @@
 // append path: launch k reports launch k-1 complete through a host-visible word, and the tail is
 // read with hipStreamQuery. Control-plane calls (leadership, replicas, acks, consumer offsets,
 // fetch) flush and drain first and run synchronously: they are rare next to the append stream.
+#include <chrono>
+
 #include "engine_internal.hpp"
 
 using namespace rmq;
@@ -99,13 +101,25 @@ uint32_t ilog2(uint64_t v) {
   return r;
 }
 
+// A fault of earlier work on the pipeline stream (kernels report nothing else: every rejection is
+// a per-record status). Asynchronous errors are sticky, so a query sees them without a copy.
 int check_err(rmq_engine* e) {
-  uint32_t err = 0;
-  HIP_TRY(hipMemcpy(&err, e->d_err, 4, hipMemcpyDeviceToHost));
-  if (err) {
-    std::fprintf(stderr, "ripplemq: device error word %u\n", err);
-    return RMQ_EDEVICE;
+  const hipError_t q = hipStreamQuery(e->main_s);
+  return q == hipSuccess || q == hipErrorNotReady ? RMQ_OK : hip_fail(q);
+}
+
+// Wait for everything issued on stream s. A blocking hipStreamSynchronize returns ~10 us after the
+// last kernel ends (interrupt wake-up); a sync sits on the producer's path (rmq_sync, a poll that
+// needs commit indices), so poll the stream for up to 20 ms first, then block.
+int stream_wait(hipStream_t s) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return RMQ_OK;
+    if (q != hipErrorNotReady) return hip_fail(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
   }
+  HIP_TRY(hipStreamSynchronize(s));
   return RMQ_OK;
 }
 
@@ -198,15 +212,16 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     e->stamps_wg[2] = a.wgp;
     e->stamps_wg[3] = a.wg3;
   }
+  hipEvent_t ev_start = nullptr;
   if (e->profile && !e->prof_ended) {
     if (!e->prof_started) {
-      HIP_TRY(hipEventRecord(e->prof_t0, e->main_s));
+      ev_start = e->prof_t0;  // recorded by the launch itself (no separate hipEventRecord call)
       e->prof_started = true;
     }
     e->prof_launches++;
     if (s3) e->prof_batches += s3->nb;
   }
-  launch_pipeline(a, e->main_s);
+  launch_pipeline(a, e->main_s, ev_start);
   HIP_TRY(hipGetLastError());
   if (s3) {
     e->applied++;
@@ -260,17 +275,19 @@ int drain(rmq_engine* e) {
     HIP_TRY(hipEventRecord(e->prof_t1, e->main_s));
     e->prof_ended = true;
   }
-  HIP_TRY(hipStreamSynchronize(e->main_s));
+  rc = stream_wait(e->main_s);
+  if (rc) return rc;
   collect_done(e);
-  return check_err(e);
+  return RMQ_OK;
 }
 
 // Wait for everything issued on the pipeline stream, without flushing batches that are still
 // forming or in the pipeline's earlier stages (reads of committed state, consumer commits).
 int quiesce(rmq_engine* e) {
-  HIP_TRY(hipStreamSynchronize(e->main_s));
+  int rc = stream_wait(e->main_s);
+  if (rc) return rc;
   collect_done(e);
-  return check_err(e);
+  return RMQ_OK;
 }
 
 // Drain, or with a replication transport (where a flush is collective: rmq_sync) just wait for
@@ -384,7 +401,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc, e->d_err,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_opos, e->d_total, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
@@ -564,7 +581,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.ring, P));
   CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
-  CREATE_TRY(dalloc(&e->d_err, 1));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
   CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));

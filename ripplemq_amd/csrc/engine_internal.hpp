@@ -232,7 +232,6 @@ struct rmq_engine {
   StateSet sets[2]{};
   uint64_t applied = 0;     // stage-3 launches issued
   CrcConsts* d_crc = nullptr;
-  uint32_t* d_err = nullptr;
   uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
   rmq::SegPool pool;         // ring space of each replica region
   std::vector<uint64_t> ring;  // [P] host copy of DevState::ring

@@ -244,7 +244,8 @@ struct MigrateItem {
 };
 
 // launchers (defined in the .hip files)
-void launch_pipeline(const PipeArgs& a, hipStream_t s);
+// start: an event the dispatch records as the kernel starts (profiling), or null
+void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start = nullptr);
 uint32_t pipeline_lds_bytes();
 uint32_t pipeline_wgs_per_cu();
 void launch_commit_all(const DevState& st, hipStream_t s);

@@ -38,6 +38,8 @@
 //
 // Launch k starts only after launch k-1 has finished (one stream), so every hand-off between
 // stages crosses a kernel boundary. Launch k's first lane reports launch k-1 complete to the host.
+#include <hip/hip_ext.h>
+
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "partition_ops.hpp"
@@ -1176,13 +1178,16 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
 uint32_t pipeline_lds_bytes() { return (uint32_t)kSmemBytes; }
 uint32_t pipeline_wgs_per_cu() { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (kPT / 64u); }
 
-void launch_pipeline(const PipeArgs& a, hipStream_t s) {
+void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start) {
   const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb;
-  if (!grid) return;
+  if (!grid) {
+    if (start) (void)hipEventRecord(start, s);
+    return;
+  }
   if (a.outidx)
-    hipLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, a);
+    hipExtLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, start, nullptr, 0, a);
   else
-    hipLaunchKernelGGL(pipeline_kernel<false>, dim3(grid), dim3(kPT), kSmemBytes, s, a);
+    hipExtLaunchKernelGGL(pipeline_kernel<false>, dim3(grid), dim3(kPT), kSmemBytes, s, start, nullptr, 0, a);
 }
 
 }  // namespace rmq

@@ -79,6 +79,10 @@ class Engine:
         _check(self.lib.rmq_create(C.byref(c), C.byref(h)), "rmq_create")
         self.h = h
         self._keep: dict[int, tuple] = {}
+        # append_device reuses one argument block: a producer loop calls it once per batch
+        self._dbatch = A.RmqBatch(0, A.RMQ_MEM_DEVICE)
+        self._dticket = C.c_uint64()
+        self._dargs = (C.byref(self._dbatch), C.byref(self._dticket))
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -150,10 +154,13 @@ class Engine:
 
     def append_device(self, n: int, d_pidx: int, d_len: int, d_payload: int, payload_bytes: int,
                       d_out: int, d_payload_off: int | None = None) -> int:
-        b = A.RmqBatch(n, A.RMQ_MEM_DEVICE, d_pidx, d_len, d_payload_off, d_payload, payload_bytes)
-        t = C.c_uint64()
-        _check(self.lib.rmq_append(self.h, C.byref(b), d_out, C.byref(t)), "rmq_append")
-        return t.value
+        b = self._dbatch
+        b.n, b.pidx, b.len, b.payload_off, b.payload, b.payload_bytes = (
+            n, d_pidx, d_len, d_payload_off, d_payload, payload_bytes)
+        rc = self.lib.rmq_append(self.h, self._dargs[0], d_out, self._dargs[1])
+        if rc < 0:
+            raise EngineError(rc, "rmq_append")
+        return self._dticket.value
 
     def poll(self, ticket: int, want_commit: bool = False):
         P = self.cfg.num_partitions
