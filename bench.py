@@ -328,10 +328,23 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
 
     # resident input pool
     pool = []
+    # one device region for the whole pool (a broker's receive ring), or an allocation per array
+    sizes = [(b.n * 4, b.n * 4, max(b.payload.nbytes, 4)) for b in batches]
+    rnd = lambda x: (x + 4095) // 4096 * 4096  # noqa: E731
+    region = eng.device_alloc(sum(rnd(x) for z in sizes for x in z)) if args.inputs == "region" else None
+    at = 0
+
+    def carve(nbytes: int) -> int:
+        nonlocal at
+        if region is None:
+            return eng.device_alloc(nbytes)
+        at += rnd(nbytes)
+        return region + at - rnd(nbytes)
+
     for b in batches:
-        d_pidx = eng.device_alloc(b.n * 4)
-        d_len = eng.device_alloc(b.n * 4)
-        d_pay = eng.device_alloc(max(b.payload.nbytes, 4))
+        d_pidx = carve(b.n * 4)
+        d_len = carve(b.n * 4)
+        d_pay = carve(max(b.payload.nbytes, 4))
         eng.h2d(d_pidx, b.pidx)
         eng.h2d(d_len, b.lens)
         eng.h2d(d_pay, b.payload)
@@ -435,10 +448,13 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
             out["host_path"] = host_leg(eng, host_batches, args.host_steps)
         if args.fetch_rounds > 0:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
-    for _, dp, dl, dpay, _, _ in pool:
-        eng.device_free(dp)
-        eng.device_free(dl)
-        eng.device_free(dpay)
+    if region is not None:
+        eng.device_free(region)
+    else:
+        for _, dp, dl, dpay, _, _ in pool:
+            eng.device_free(dp)
+            eng.device_free(dl)
+            eng.device_free(dpay)
     for d in d_out:
         eng.device_free(d)
     eng.close()
@@ -457,6 +473,8 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="B", choices=sorted(CONFIGS))
     ap.add_argument("--pool", type=int, default=48, help="distinct resident input batches")
+    ap.add_argument("--inputs", default="arrays", choices=["arrays", "region"],
+                    help="input pool: a device allocation per array, or one region carved into batches")
     ap.add_argument("--rings", default="load", choices=["load", "equal"],
                     help="load: ring per partition from its traffic in one shared pool (rmq_set_segments); "
                          "equal: every ring --segment-mb (default 4)")
@@ -537,7 +555,10 @@ def main() -> None:
     def attach_rccl(eng, g):
         eng.attach_rccl(g.bcast(rccl_unique_id() if g.rank == 0 else None), g.world)
 
-    out = run_rank(args, grp, int(os.environ.get("LOCAL_RANK", "0")), attach_rccl)
+    device = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("RMQ_BENCH_DEVICES"):  # rehearsal only: ranks share the box's few GPUs
+        device %= int(os.environ["RMQ_BENCH_DEVICES"])
+    out = run_rank(args, grp, device, attach_rccl)
     if out is not None:
         print(json.dumps(out), flush=True)
     if dist is not None:
