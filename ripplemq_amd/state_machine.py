@@ -171,8 +171,12 @@ class PartitionBroker:
 
     def __init__(self, directory: PartitionDirectory, engine=None, *, replication_factor: int = 1,
                  segment_bytes: int = 1 << 22, index_interval: int = 4096, device: int = 0,
-                 messages_as_str: bool = True):
+                 messages_as_str: bool = True, durable=None):
+        """durable: a ``ripplemq_amd.tier.DurableLog`` over this engine, or None. With it, a read
+        below a ring's retained start is served from the segment files (the reference never
+        evicts, PartitionStateMachine.java:26) instead of failing with RMQ_EOFFSET."""
         self.dir = directory
+        self.durable = durable
         if engine is None:
             cfg = EngineConfig(num_partitions=len(directory), replication_factor=replication_factor,
                                segment_bytes=segment_bytes, index_interval=index_interval,
@@ -283,10 +287,22 @@ class PartitionBroker:
         if idx:
             _, res, buf, _ = self.engine.fetch(np.asarray(p, np.uint32), np.asarray(c, np.uint32),
                                                np.asarray(mx, np.uint32))
+            spilled = False
             for k, r in enumerate(idx):
                 st = int(res["status"][k])
                 if st == A.RMQ_ENOTLEADER:
                     out[r] = NOT_LEADER
+                    continue
+                if st == A.RMQ_EOFFSET and self.durable is not None:
+                    # below the ring: [off, min(off + max, hw)) from the segment files, after a
+                    # spill has made everything committed durable
+                    if not spilled:
+                        self.durable.spill()
+                        spilled = True
+                    off = int(res["start_offset"][k])
+                    hw = int(self.engine.state(p[k])["high_watermark"])
+                    recs = self.durable.read(p[k], off, min(mx[k], hw - off))
+                    out[r] = MessageBatchReadResponse([_decode(b, self.as_str) for _, _, b in recs], off)
                     continue
                 if st != A.RMQ_OK:
                     raise EngineError(st, f"fetch {requests[r].getGroupId()}")

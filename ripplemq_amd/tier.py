@@ -1,0 +1,244 @@
+"""Durable segment files below the HBM rings, and replay.
+
+The reference never evicts a record: ``PartitionStateMachine`` keeps every message in its
+``messages`` list (``mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:26,64-69``)
+and jraft persists the log under the partition's data path (``PartitionRaftServer.java:53,88-90``).
+The engine's replica rings keep a retained window only (FORMAT.md §4): a fetch below it answers
+``RMQ_EOFFSET``. This module is the tier that restores the reference's semantics on the host side:
+
+* ``DurableLog.spill()`` moves every committed record not yet durable into per-partition segment
+  files with ONE ``rmq_fetch`` for all partitions: the durable end of each partition is a consumer
+  offset of its own (a reserved consumer slot, ``cursor``), so the fetch kernel returns exactly the
+  records ``[durable end, high watermark)`` and the cursor advances with one
+  ``rmq_commit_consumer_offset``. A segment file holds the records exactly as the rings do (FORMAT.md
+  §1: 16-byte header {offset, length, CRC32C} + payload padded to 16 bytes), named by its first
+  offset (``p<pidx>/<first offset>.seg``), rolled at ``segment_file_bytes``.
+* ``DurableLog.read(p, off, max)`` serves ``[off, min(off + max, durable end))`` from the files
+  (the broker's ``process_batch_read`` falls back to it on ``RMQ_EOFFSET`` after a spill, so a
+  consumer below the rings gets what the reference's list would give it).
+* ``replay(directory, engine)`` rebuilds a fresh engine's logs from the files: the records are
+  re-appended in offset order (the engine computes every CRC again) and the result is checked
+  bit for bit against the files: offsets, and the ring bytes of the retained window.
+
+Spill must run at least once per retained window of every partition (rings hold ``retain``
+batches of their traffic, ``ripplemq_amd/rings.py``); a cursor below a ring's start raises, since
+records were lost before they were durable.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from . import _abi as A
+from .engine import EngineError
+
+SEG_SUFFIX = ".seg"
+
+
+def record_positions(buf: np.ndarray, count: int | None = None) -> np.ndarray:
+    """Byte positions of the FORMAT.md §1 records laid back to back in ``buf`` (plus the end)."""
+    b = buf.tobytes() if not isinstance(buf, (bytes, bytearray)) else bytes(buf)
+    out, pos = [], 0
+    while pos + 16 <= len(b) and (count is None or len(out) < count):
+        out.append(pos)
+        ln = int.from_bytes(b[pos + 8:pos + 12], "little")
+        pos += 16 + ((ln + 15) & ~15)
+    out.append(pos)
+    return np.asarray(out, np.int64)
+
+
+class _PartitionFiles:
+    """One partition's segment files: record k (offset base + k) at logical byte pos[k] of the
+    concatenated files; segment s covers logical bytes [seg_pos[s], seg_pos[s + 1])."""
+
+    def __init__(self, root: str, p: int, segment_file_bytes: int):
+        self.dir = os.path.join(root, f"p{p:06d}")
+        os.makedirs(self.dir, exist_ok=True)
+        self.limit = segment_file_bytes
+        self.base = 0
+        self.pos = np.zeros(1, np.int64)
+        self.seg_first: list[int] = []   # first offset of every segment file
+        self.seg_pos: list[int] = []     # its first logical byte
+        names = sorted(int(f[:-len(SEG_SUFFIX)]) for f in os.listdir(self.dir) if f.endswith(SEG_SUFFIX))
+        cat, acc = [], 0
+        for first in names:  # reopen: walk the headers of every file, in offset order
+            rp = record_positions(np.fromfile(self._path(first), np.uint8))
+            if not self.seg_first:
+                self.base = first
+            elif first != self.base + sum(len(x) for x in cat):
+                raise EngineError(A.RMQ_EINVAL, f"{self.dir}: segment {first} does not continue the log")
+            self.seg_first.append(first)
+            self.seg_pos.append(acc)
+            cat.append(rp[:-1] + acc)
+            acc += int(rp[-1])
+        if cat:
+            self.pos = np.concatenate(cat + [np.asarray([acc], np.int64)])
+
+    def _path(self, first: int) -> str:
+        return os.path.join(self.dir, f"{first:020d}{SEG_SUFFIX}")
+
+    @property
+    def end(self) -> int:
+        """Offset after the last durable record."""
+        return self.base + len(self.pos) - 1
+
+    def append(self, first: int, data: np.ndarray, count: int, fsync: bool) -> None:
+        if not count:
+            return
+        if not self.seg_first:
+            self.base = first
+        elif first != self.end:
+            raise EngineError(A.RMQ_EINVAL, f"{self.dir}: spill of offset {first} does not continue {self.end}")
+        rp = record_positions(data, count)
+        if len(rp) != count + 1 or int(rp[-1]) != len(data):
+            raise EngineError(A.RMQ_EINVAL, f"{self.dir}: {count} records expected in {len(data)} bytes")
+        total = int(self.pos[-1])
+        if not self.seg_first or total - self.seg_pos[-1] >= self.limit:
+            self.seg_first.append(first)
+            self.seg_pos.append(total)
+        with open(self._path(self.seg_first[-1]), "ab") as f:
+            f.write(data.tobytes())
+            if fsync:
+                f.flush()
+                os.fsync(f.fileno())
+        self.pos = np.concatenate([self.pos[:-1], rp + total])
+
+    def read_bytes(self, a: int, b: int) -> bytes:
+        """Logical bytes [a, b) across the segment files."""
+        out = []
+        for s, first in enumerate(self.seg_first):
+            lo = self.seg_pos[s]
+            hi = self.seg_pos[s + 1] if s + 1 < len(self.seg_pos) else int(self.pos[-1])
+            x, y = max(a, lo), min(b, hi)
+            if x < y:
+                with open(self._path(first), "rb") as f:
+                    f.seek(x - lo)
+                    out.append(f.read(y - x))
+        return b"".join(out)
+
+    def read_records(self, off: int, end: int) -> bytes:
+        """The record images of offsets [off, end) (both within [base, self.end])."""
+        return self.read_bytes(int(self.pos[off - self.base]), int(self.pos[end - self.base]))
+
+
+def split_records(data: bytes) -> list[tuple[int, int, bytes]]:
+    """[(offset, crc, payload)] of back-to-back FORMAT.md §1 records."""
+    out, pos = [], 0
+    while pos + 16 <= len(data):
+        off = int.from_bytes(data[pos:pos + 8], "little")
+        ln = int.from_bytes(data[pos + 8:pos + 12], "little")
+        crc = int.from_bytes(data[pos + 12:pos + 16], "little")
+        out.append((off, crc, data[pos + 16:pos + 16 + ln]))
+        pos += 16 + ((ln + 15) & ~15)
+    return out
+
+
+class DurableLog:
+    """Segment files of the partitions ``partitions`` of one engine (their leader), fed by spill."""
+
+    def __init__(self, engine, directory: str, partitions, cursor: int, *,
+                 segment_file_bytes: int = 64 << 20, fsync: bool = False):
+        self.engine = engine
+        self.dir = directory
+        self.cursor = int(cursor)
+        self.fsync = fsync
+        self.parts = {int(p): _PartitionFiles(directory, int(p), segment_file_bytes) for p in partitions}
+        # a reopened tier continues where its files end: the cursor slot names that offset
+        pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
+        ends = np.fromiter((f.end for f in self.parts.values()), np.uint64, len(self.parts))
+        if len(pidx) and ends.any():
+            self.engine.commit_consumer_offset(pidx, np.full(len(pidx), self.cursor, np.uint32), ends)
+
+    def end(self, p: int) -> int:
+        return self.parts[p].end
+
+    def spill(self) -> int:
+        """Make every committed record durable; returns the number of records written."""
+        pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
+        if not len(pidx):
+            return 0
+        cons = np.full(len(pidx), self.cursor, np.uint32)
+        _, res, buf, _ = self.engine.fetch(pidx, cons, np.full(len(pidx), 0xFFFFFFFF, np.uint32))
+        moved = 0
+        adv_p, adv_o = [], []
+        for k, p in enumerate(pidx.tolist()):
+            st = int(res["status"][k])
+            if st == A.RMQ_ENOTLEADER:
+                continue  # a follower's tier is fed by its own leader term later
+            if st != A.RMQ_OK:
+                raise EngineError(st, f"spill of partition {p} (records lost before they were durable)"
+                                  if st == A.RMQ_EOFFSET else f"spill of partition {p}")
+            n = int(res["count"][k])
+            if not n:
+                continue
+            pos, nb = int(res["out_pos"][k]), int(res["bytes"][k])
+            first = int(res["start_offset"][k])
+            self.parts[p].append(first, buf[pos:pos + nb], n, self.fsync)
+            moved += n
+            adv_p.append(p)
+            adv_o.append(first + n)
+        if adv_p:
+            self.engine.commit_consumer_offset(np.asarray(adv_p, np.uint32),
+                                               np.full(len(adv_p), self.cursor, np.uint32),
+                                               np.asarray(adv_o, np.uint64))
+        return moved
+
+    def read(self, p: int, off: int, max_messages: int) -> list[tuple[int, int, bytes]]:
+        """Records [off, min(off + max, durable end)) of partition p from the files."""
+        f = self.parts[p]
+        end = min(off + max(int(max_messages), 0), f.end)
+        if off < f.base or off >= end:
+            return []
+        return split_records(f.read_records(off, end))
+
+
+def replay(directory: str, engine, partitions, *, batch_records: int = 65536) -> dict:
+    """Rebuild a fresh engine's logs from segment files: every record is appended again in offset
+    order (the engine recomputes its CRC32C) and must get the offset the file holds; afterwards
+    the retained window of every partition's lowest local ring must equal the files' bytes for it.
+    Returns {"records": n, "partitions": k}."""
+    files = {int(p): _PartitionFiles(directory, int(p), 1 << 62) for p in partitions}
+    recs = {}
+    for p, f in files.items():
+        if f.end == f.base:
+            continue
+        st = engine.state(p)
+        if st["log_end_offset"] != f.base:
+            raise EngineError(A.RMQ_EINVAL, f"replay of partition {p}: log ends at {st['log_end_offset']}, "
+                                            f"files start at {f.base}")
+        recs[p] = split_records(f.read_records(f.base, f.end))
+    # interleave the partitions into batches (any order across partitions keeps per-partition order)
+    queue = [(p, k) for p, r in recs.items() for k in range(len(r))]
+    queue.sort(key=lambda x: (x[1], x[0]))
+    total = 0
+    for s in range(0, len(queue), batch_records):
+        chunk = queue[s:s + batch_records]
+        pidx = np.fromiter((p for p, _ in chunk), np.uint32, len(chunk))
+        pays = [recs[p][k][2] for p, k in chunk]
+        lens = np.fromiter((len(x) for x in pays), np.uint32, len(chunk))
+        payload = np.frombuffer(b"".join(pays) + bytes(16), np.uint8)
+        offs, stats = engine.append(pidx, lens, payload)
+        want = np.fromiter((recs[p][k][0] for p, k in chunk), np.uint64, len(chunk))
+        if stats["appended"] != len(chunk) or not np.array_equal(offs, want):
+            raise EngineError(A.RMQ_EINVAL, f"replay: batch at {s} got other offsets than the files hold")
+        total += len(chunk)
+    if hasattr(engine, "sync"):
+        engine.sync()
+    for p, f in files.items():
+        if p not in recs:
+            continue
+        st = engine.state(p)
+        lo_off = st["log_start_offset"]
+        data = f.read_records(lo_off, f.end)
+        S = st["segment_bytes"]
+        a = st["log_start_pos"] % S
+        n = st["log_end_pos"] - st["log_start_pos"]
+        r0 = st["leader_slot"]  # the leader's own replica is local
+        ring = engine.read_segment(r0, p, a, min(n, S - a)).tobytes()
+        if n > S - a:
+            ring += engine.read_segment(r0, p, 0, n - (S - a)).tobytes()
+        if ring != data:
+            raise EngineError(A.RMQ_EINVAL, f"replay of partition {p}: ring bytes differ from the files "
+                                            f"(a CRC or payload changed)")
+    return {"records": total, "partitions": len(recs)}

@@ -1,0 +1,102 @@
+"""Durable segment files and replay (ripplemq_amd/tier.py).
+
+The reference never evicts (PartitionStateMachine.java:26: every message stays in `messages`), so
+a consumer reading from offset 0 long after its records left the engine's rings must still get
+them: the broker serves such reads from the segment files the tier spilled. Checked against
+tests/refmodel.py (the literal restatement of the reference state machine). Replay rebuilds a
+fresh engine from the files and the tier checks every offset and the ring bytes of the retained
+window against the files. The CPU test injects the oracle's handle (host logic only); the GPU test
+runs the same flow on the HIP engine.
+"""
+import numpy as np
+import pytest
+
+from refmodel import Broker
+from ripplemq_amd.engine import EngineConfig
+from ripplemq_amd.state_machine import (ConsumerOffsetUpdateRequest, MessageAppendRequest, MessageBatchReadRequest,
+                                        PartitionBroker, PartitionDirectory)
+from ripplemq_amd.tier import DurableLog, replay
+
+TOPIC = "topic1"
+P = 4
+
+
+def _flow(make_engine, tmp_path, seg_file_bytes):
+    d = PartitionDirectory({TOPIC: P}, max_consumers=4)
+    cursor = d.consumer("__durable_tier")
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 14, index_interval=256,
+                       max_consumers=4, max_batch_records=4096)
+    ref = Broker(TOPIC, P)
+    g = np.random.default_rng(31)
+    with make_engine(cfg) as eng:
+        tier = DurableLog(eng, str(tmp_path), range(P), cursor, segment_file_bytes=seg_file_bytes)
+        b = PartitionBroker(d, eng, messages_as_str=False, durable=tier)
+        for rnd in range(40):
+            reqs = []
+            for i in range(int(g.integers(20, 60))):
+                pid = int(g.integers(0, P))
+                reqs.append(MessageAppendRequest([bytes(g.integers(0, 256, int(g.integers(0, 300)), dtype=np.uint8))],
+                                                 TOPIC, pid))
+            assert all(r.isSuccess() for r in b.process_append(reqs))
+            for r in reqs:
+                ref.produce(r.partitionId, r.messages[0])
+            if rnd % 3 == 2:
+                tier.spill()
+        starts = [eng.state(p)["log_start_offset"] for p in range(P)]
+        assert min(starts) > 0, "rings never evicted: the tier is not exercised"
+        # a consumer from offset 0: read max 10 then commit, until drained (ConsumerClientImpl.java:61-117)
+        for p in range(P):
+            sm = b.state_machine(f"{TOPIC}-{p}")
+            while True:
+                got = sm.handleBatchRead(MessageBatchReadRequest("late-consumer", 10, TOPIC, p))
+                want, off = ref.sms[p].handle_batch_read("late-consumer", 10)
+                assert got.getOffset() == off and got.getMessages() == want, f"partition {p} offset {off}"
+                if not want:
+                    break
+                assert sm.handleConsumerOffsetUpdateRequest(
+                    ConsumerOffsetUpdateRequest("late-consumer", off + len(want), TOPIC, p)).isSuccess()
+                ref.sms[p].handle_consumer_offset_update_request("late-consumer", off + len(want))
+        tier.spill()
+        ends = [tier.end(p) for p in range(P)]
+        assert ends == [len(ref.sms[p].messages) for p in range(P)]
+        # reopen: the files alone give the same durable ends and records
+        again = DurableLog(eng, str(tmp_path), range(P), cursor, segment_file_bytes=seg_file_bytes)
+        assert [again.end(p) for p in range(P)] == ends
+        assert [m for _, _, m in again.read(1, 5, 7)] == ref.sms[1].messages[5:12]
+    # replay into a fresh engine: offsets and ring bytes checked against the files by replay()
+    big = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=4, max_batch_records=4096)
+    with make_engine(big) as fresh:
+        out = replay(str(tmp_path), fresh, range(P), batch_records=500)
+        assert out["records"] == sum(ends)
+        assert [fresh.state(p)["log_end_offset"] for p in range(P)] == ends
+    return ends
+
+
+@pytest.mark.parametrize("seg_file_bytes", [1 << 30, 4096])
+def test_durable_tier_oracle_handle(oracle_mod, tmp_path, seg_file_bytes):
+    _flow(oracle_mod.OracleEngine, tmp_path, seg_file_bytes)
+
+
+def test_durable_tier_detects_corruption(oracle_mod, tmp_path):
+    d = PartitionDirectory({TOPIC: 1}, max_consumers=2)
+    cfg = EngineConfig(num_partitions=1, replication_factor=1, segment_bytes=1 << 14, index_interval=256,
+                       max_consumers=2)
+    with oracle_mod.OracleEngine(cfg) as eng:
+        tier = DurableLog(eng, str(tmp_path), [0], d.consumer("__durable_tier"))
+        PartitionBroker(d, eng, messages_as_str=False, durable=tier).process_append(
+            [MessageAppendRequest([b"abc" * k], TOPIC, 0) for k in range(50)])
+        assert tier.spill() == 50
+    seg = next((tmp_path / "p000000").glob("*.seg"))
+    raw = bytearray(seg.read_bytes())
+    raw[33] ^= 0x55  # record 0 is empty (16-byte header); this is payload byte 1 of record 1
+    seg.write_bytes(bytes(raw))
+    with oracle_mod.OracleEngine(cfg) as fresh:
+        with pytest.raises(Exception):
+            replay(str(tmp_path), fresh, [0])
+
+
+@pytest.mark.gpu
+def test_durable_tier_gpu(tmp_path):
+    from ripplemq_amd.engine import Engine
+    _flow(Engine, tmp_path, 4096)
