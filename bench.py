@@ -210,7 +210,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             t0 = time.perf_counter()
             rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
             t_wall += time.perf_counter() - t0
-            _, ms_f = eng.profile_query(3)  # resolve + place + gather, one event pair per call
+            _, ms_f = eng.profile_query(3)  # the fetch kernel, one event pair per call
             eng.profile(False)
             if rc or np.any(res["status"] != 0):
                 raise SystemExit(f"bench: fetch leg failed rc={rc} statuses={np.unique(res['status'])}")
@@ -224,7 +224,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                            "requests": P * consumers, "rounds": rounds,
                            "roofline": {"bound": "hbm", "achieved": alg / t_kern / 1e9, "peak": HBM_PEAK_GBS,
                                         "unit": "GB/s", "frac": alg / t_kern / 1e9 / HBM_PEAK_GBS,
-                                        "kernels": "rmq::fetch_resolve + fetch_place + fetch_gather",
+                                        "kernels": "rmq::fetch_kernel (resolve + look-back placement + gather, one launch)",
                                         "mean_us_per_fetch": t_kern / rounds * 1e6}}
     return out
 

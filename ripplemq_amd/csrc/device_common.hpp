@@ -112,26 +112,6 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
   return v;
 }
 
-// Block-wide exclusive scan for a block of NW waves. `sh` needs NW entries. Returns the
-// exclusive prefix; *total gets the block sum. Contains two __syncthreads().
-template <u32 NW, typename T>
-__device__ __forceinline__ T block_excl_scan(T v, T* sh, T* total) {
-  const u32 l = lane_id(), w = threadIdx.x >> 6;
-  T inc = wave_incl_scan(v);
-  if (l == 63) sh[w] = inc;
-  __syncthreads();
-  T base = 0, tot = 0;
-#pragma unroll
-  for (u32 k = 0; k < NW; ++k) {
-    T s = sh[k];
-    if (k < w) base += s;
-    tot += s;
-  }
-  __syncthreads();
-  *total = tot;
-  return base + inc - v;
-}
-
 // Segmented inclusive scan step helpers: pairs (flag, value). A set flag starts a new segment.
 template <typename T>
 __device__ __forceinline__ void wave_seg_incl_scan(u32& flag, T& v) {

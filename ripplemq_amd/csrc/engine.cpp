@@ -221,6 +221,9 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     e->prof_launches++;
     if (s3) e->prof_batches += s3->nb;
   }
+  if (e->trace)  // RMQ_TRACE: the roles of every launch (diagnostics only)
+    std::fprintf(stderr, "rmq launch %llu: s1 %u batches %u wgs | s2 %u batches %u wgs | parts %u wgs | s3 %u batches %u wgs + %u big | s4 %u batches\n",
+                 (unsigned long long)a.launch_seq, a.g1.nb, a.wg1, a.g2.nb, a.wg2, a.wgp, a.g3.nb, a.wg3, a.wgb, a.g4.nb);
   launch_pipeline(a, e->main_s, ev_start);
   HIP_TRY(hipGetLastError());
   if (s3) {
@@ -402,7 +405,7 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc,
-                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_opos, e->d_total, e->d_fetch_out,
+                             e->d_stats, e->d_req, e->d_res, e->d_flags, e->d_ticket, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -509,6 +512,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (!e->cfg.pipeline_depth) e->cfg.pipeline_depth = 2;
   e->device = cfg->device;
   e->stamps_path = std::getenv("RMQ_STAMPS");
+  if (const char* v = std::getenv("RMQ_TRACE")) e->trace = std::atoi(v) != 0;
   if (const char* v = std::getenv("RMQ_DEBUG")) e->debug = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_WG3_ALL")) e->wg3_all = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S1_WGS")) e->s1_wgs = (uint32_t)std::atoi(v);
@@ -1065,27 +1069,22 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
   if (n > e->fetch_cap) {
     hipFree(e->d_req);
     hipFree(e->d_res);
-    hipFree(e->d_aux);
-    hipFree(e->d_cpre);
-    hipFree(e->d_opos);
+    hipFree(e->d_flags);
     if (e->h_req) hipHostFree(e->h_req);
     if (e->h_res) hipHostFree(e->h_res);
     e->d_req = nullptr;
-    e->d_res = e->d_aux = nullptr;
-    e->d_cpre = e->h_req = nullptr;
-    e->d_opos = nullptr;
+    e->d_res = e->d_flags = nullptr;
+    e->h_req = nullptr;
     e->h_res = nullptr;
     e->fetch_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     rc = dalloc(&e->d_req, (size_t)cap * 4);
-    if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4);
-    if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
-    if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 4);
-    if (!rc) rc = dalloc(&e->d_opos, (size_t)cap);
-    if (!rc && !e->d_total) rc = dalloc(&e->d_total, 2);
+    if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4 + 2);
+    if (!rc) rc = dalloc(&e->d_flags, (size_t)fetch_workgroups(cap));  // zeroed: no epoch matches
+    if (!rc && !e->d_ticket) rc = dalloc(&e->d_ticket, 2);
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
-    HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 5 + 2) * 8, 0));  // res, total, positions
+    HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
     e->fetch_cap = cap;
   }
   uint8_t* d_out = out;
@@ -1111,28 +1110,31 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     a.st = e->st;
     a.req = e->d_req;
     a.res = e->d_res;
-    a.aux = e->d_aux;
-    a.cpre = e->d_cpre;
-    a.opos = e->d_opos;
+    a.flags = e->d_flags;
+    a.ticket = e->d_ticket;
+    a.ticket_base = e->fetch_ticket;
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
-    a.gather_wgs = std::max<uint32_t>(1u, 32u * e->cu_count);
-    a.total = e->d_total;
+    a.nwg = fetch_workgroups(n);
+    if (++e->fetch_epoch >= (1u << 24)) {  // status words of 2^24 - 1 calls ago could match again
+      e->fetch_epoch = 1;
+      HIP_TRY(hipMemsetAsync(e->d_flags, 0, (size_t)fetch_workgroups(e->fetch_cap) * 8, e->fetch_s));
+    }
+    a.epoch = e->fetch_epoch;
+    e->fetch_ticket += a.nwg;
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
     HIP_TRY(hipMemcpyAsync(e->d_req, e->h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     hipEvent_t r0 = nullptr, g1 = nullptr;
-    if (e->profile) {  // one timed region around the three fetch kernels (profile_query(3))
+    if (e->profile) {  // one timed region around the fetch kernel (profile_query(3))
       r0 = pool_event(e);
       g1 = pool_event(e);
       e->prof[3].push_back({r0, g1});
     }
-    launch_fetch(a, e->fetch_s, r0, nullptr, nullptr, g1);
+    launch_fetch(a, e->fetch_s, r0, g1);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, (size_t)n * 32, hipMemcpyDeviceToHost, e->fetch_s));
-    HIP_TRY(hipMemcpyAsync(h_total, e->d_total, 16, hipMemcpyDeviceToHost, e->fetch_s));
-    HIP_TRY(hipMemcpyAsync(h_total + 2, e->d_opos, (size_t)n * 8, hipMemcpyDeviceToHost, e->fetch_s));
+    HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
     HIP_TRY(hipEventRecord(e->ev_fetch, e->fetch_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, e->ev_fetch, 0));
   }
@@ -1143,7 +1145,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     rmq_fetch_res& x = res[r];
     std::memset(&x, 0, sizeof x);
     x.start_offset = h[0];
-    x.out_pos = h_total[2 + r];
+    x.out_pos = h[1];
     x.count = (uint32_t)h[2];
     x.bytes = (uint32_t)(h[2] >> 32);
     x.status = (int32_t)(uint32_t)h[3];

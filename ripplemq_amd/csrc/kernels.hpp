@@ -6,13 +6,16 @@
 
 namespace rmq {
 
-constexpr uint32_t kPipeThreads = 512;   // 8 waves per workgroup, every role of the pipeline launch
+#ifndef RMQ_PIPE_THREADS
+#define RMQ_PIPE_THREADS 512
+#endif
+constexpr uint32_t kPipeThreads = RMQ_PIPE_THREADS;  // threads per workgroup, every role of the pipeline launch
 #ifndef RMQ_TILE_BITS
 #define RMQ_TILE_BITS 10
 #endif
 constexpr uint32_t kTileIdxBits = RMQ_TILE_BITS;       // log2(kTileRecs)
 constexpr uint32_t kTileRecs = 1u << kTileIdxBits;     // records per ranking tile (stage 1)
-constexpr uint32_t kMaxTiles = 512;      // tiles per group (<= kPipeThreads: stage 2 holds one per thread)
+constexpr uint32_t kMaxTiles = 512;      // tiles per group (stage 2 keeps their payload bases in LDS)
 #ifndef RMQ_SCAN_LANES
 #define RMQ_SCAN_LANES 16
 #endif
@@ -178,16 +181,16 @@ struct PipeArgs {
 struct FetchArgs {
   DevState st;
   const uint32_t* req;       // [n][4] {pidx, consumer, max, reserved}
-  uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}
-  uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
-  uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> place), 16-byte aligned
-  uint64_t* opos;            // [n] output position of each request (place -> gather, host)
+  uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}, then [2] {bytes needed, 0}
+  uint64_t* flags;           // [nwg] look-back status words {epoch, flag, bytes}
+  uint64_t* ticket;          // virtual workgroup ids: ticket - ticket_base (monotonic over calls)
+  uint64_t ticket_base;
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
-  uint32_t n;
-  uint32_t gather_wgs;       // gather grid cap (a wave per request, looping)
-  uint64_t* total;           // [2] {bytes needed, 0}
+  uint32_t n, nwg;
+  uint32_t epoch;            // 1 .. 2^24 - 1, names the call in the status words
 };
+
 
 struct ConsumerCommitArgs {  // one item per (partition, consumer): the host resolved last-writer-wins
   DevState st;
@@ -251,8 +254,8 @@ uint32_t pipeline_wgs_per_cu();
 void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
-void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev_resolve0, hipEvent_t ev_resolve1,
-                  hipEvent_t ev_gather0, hipEvent_t ev_gather1);
+uint32_t fetch_workgroups(uint32_t n);
+void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move

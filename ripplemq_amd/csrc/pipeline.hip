@@ -44,9 +44,13 @@
 #include "kernels.hpp"
 #include "partition_ops.hpp"
 
+#ifndef RMQ_ZK_LDS
+#define RMQ_ZK_LDS (RMQ_PIPE_THREADS >= 512)
+#endif
+
 namespace rmq {
 
-constexpr u32 kPT = kPipeThreads;   // 512
+constexpr u32 kPT = kPipeThreads;   // 512 (RMQ_PIPE_THREADS)
 constexpr u32 kPW = kPT / 64;       // 8 waves
 constexpr u32 kTR = kTileRecs;      // 1024
 constexpr u32 kTI = kTR / kPT;      // 2 records per thread in stage 1
@@ -88,14 +92,28 @@ struct Stage1Smem {
 struct Stage3Smem {
   u32 t8[8][256];       // slicing-by-8 CRC32C tables
   u32 z[2][4][256];     // register shift past 16 and 32 zero bytes
+#if RMQ_ZK_LDS
   u32 zk[4][256];       // register shift past 1024 zero bytes (wave-wide records)
+#endif
   uint4 img[kPW][kTaskRecs][8];  // per wave: the task's records as laid out in the log (<= 128 B each)
   uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16 | dead << 24}
   u64 xdst[kPW][kTaskRecs][kMaxRemote];  // replication: each record's outbox address per remote slot
   u32 xn[kPW][kTaskRecs];                // and how many
 };
 
+// The 1 KB shift table of the large-record waves lives in LDS with 512-thread workgroups; with
+// smaller ones (RMQ_PIPE_THREADS=256, four resident per CU) LDS has no room for it and those waves
+// read it from global memory (L1/L2-resident, 4 KB).
+#if RMQ_ZK_LDS
+#define RMQ_ZK_TABLE S.zk
+constexpr u32 kBigTableBytes = sizeof(Stage3Smem::t8) + sizeof(Stage3Smem::z) + sizeof(Stage3Smem::zk);
+#else
+#define RMQ_ZK_TABLE A.crc->zshift1k
+constexpr u32 kBigTableBytes = sizeof(Stage3Smem::t8) + sizeof(Stage3Smem::z);
+#endif
+
 constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
+static_assert(kSmemBytes >= kMaxTiles * sizeof(u64), "stage 2's tile bases fit the dynamic LDS");
 
 __device__ __forceinline__ u64 wave_incl_scan_u64(u64 v) {
   const u32 l = lane_id();
@@ -444,35 +462,40 @@ __device__ void stage2_plan(const PipeArgs& A) {
   if (tid == 0) __hip_atomic_store(X.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next used six launches later
 }
 
-__device__ void stage2(const PipeArgs& A, u32 wg) {
+// s_ex: kMaxTiles words of the launch's dynamic LDS (static arrays would add to every role's LDS)
+__device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
   const u32 P = A.st.P, T = G.tiles, GT = A.gt;
-  const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const u32 tid = threadIdx.x;
   __shared__ u64 s_acc[kMaxGroup][2];
-  __shared__ u64 s_ex[kMaxTiles];
   __shared__ u64 s_w[kPW];
   __shared__ u32 s_rej;
   PIPE_STAMP(0);
   // ---- batch rule from the tile sums (every workgroup, since the scans skip invalid batches)
   if (tid < kMaxGroup * 2) (&s_acc[0][0])[tid] = 0ull;
   __syncthreads();
-  const bool in = tid < T;
-  const u32 jt = in ? batch_of_tile(G, tid) : 0u;
-  const u64 pay = in ? x.tsum[(u64)tid * 4 + 0] : 0ull;
-  if (in) {
-    atomicAdd(&s_acc[jt][0], pay);
-    atomicAdd(&s_acc[jt][1], x.tsum[(u64)tid * 4 + 2]);
+  // tiles t = tid, tid + kPT, ... (a group has at most kMaxTiles)
+  u64 carry = 0;
+  for (u32 t0 = 0; t0 < T; t0 += kPT) {
+    const u32 t = t0 + tid;
+    const bool in = t < T;
+    const u32 jt = in ? batch_of_tile(G, t) : 0u;
+    const u64 pay = in ? x.tsum[(u64)t * 4 + 0] : 0ull;
+    if (in) {
+      atomicAdd(&s_acc[jt][0], pay);
+      atomicAdd(&s_acc[jt][1], x.tsum[(u64)t * 4 + 2]);
+    }
+    if (wg == 0) {  // payload offset of every tile's first record in the group (packed payloads)
+      u64 tot;
+      const u64 inc = block_incl_scan_u64(pay, s_w, &tot);
+      if (in) s_ex[t] = carry + inc - pay;
+      carry += tot;
+    }
   }
-  if (wg == 0) {  // payload offset of every tile's first record inside its batch (packed payloads)
-    const u64 inc = wave_incl_scan_u64(pay);
-    if (lane == 63) s_w[w] = inc;
+  if (wg == 0) {  // ... and inside its batch
     __syncthreads();
-    u64 wpre = 0;
-    for (u32 ww = 0; ww < w; ++ww) wpre += s_w[ww];
-    if (in) s_ex[tid] = wpre + inc - pay;
-    __syncthreads();
-    if (in) x.tile_base[tid] = s_ex[tid] - s_ex[G.tile0[jt]];
+    for (u32 t = tid; t < T; t += kPT) x.tile_base[t] = s_ex[t] - s_ex[G.tile0[batch_of_tile(G, t)]];
   }
   __syncthreads();
   if (tid == 0) {
@@ -756,7 +779,7 @@ __device__ void big_record(const PipeArgs& A, const Stage3Smem& S, u64 src, u32 
       if (jp < m) {
         const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
         const uint4 v = extract_piece(b0[u], b1, sa, nb);
-        acc = crc_zshift(S.zk, acc) ^ piece_crc(A, S, v, jp);
+        acc = crc_zshift(RMQ_ZK_TABLE, acc) ^ piece_crc(A, S, v, jp);
         uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
         if (jp + 1u >= dead)
           for (u32 r = 0; r < RF; ++r)
@@ -797,7 +820,7 @@ __device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
   {
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z) + sizeof(S.zk)) / 16u; k += kPT) dst[k] = src[k];
+    for (u32 k = threadIdx.x; k < kBigTableBytes / 16u; k += kPT) dst[k] = src[k];
   }
   __syncthreads();
   const u32 nw = A.wgb * kPW;
@@ -1118,7 +1141,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     }
     wg -= A.wg1;
     if (wg < A.wg2) {
-      stage2(A, wg);
+      stage2(A, wg, reinterpret_cast<u64*>(smem_raw));
       return;
     }
     wg -= A.wg2;
@@ -1146,7 +1169,9 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (!(A.debug & 8u)) {
     // slicing and zero-shift tables are contiguous in CrcConsts and in Stage3Smem: 16-byte copies
     static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
+#if RMQ_ZK_LDS
     static_assert(offsetof(Stage3Smem, zk) == sizeof(S.t8) + sizeof(S.z), "z and zk adjacent in LDS");
+#endif
     static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
     static_assert(offsetof(CrcConsts, zshift1k) == offsetof(CrcConsts, zshift) + sizeof(A.crc->zshift), "zshift1k next");
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);

@@ -127,3 +127,31 @@ def test_fetch_during_pipelined_appends(oracle_mod):
         assert int(res["count"].sum()) == sum(b.n for b in batches)
         assert applied_before_sync < sum(b.n for b in batches), "fetches flushed the pipeline"
         assert seen > 0, "no fetch saw committed records while appends were in flight"
+
+
+def test_fetch_lookback_many_requests(oracle_mod):
+    """One fetch launch places 20k requests (5k workgroups: look-back chains far past one 64-word
+    window) with unknown partitions, bad consumers and zero-record slices mixed in, then the same
+    requests into an output buffer that ends mid-way (ENOSPC after the cut), over several calls so
+    the status words of earlier calls are present."""
+    P, C = 1024, 4
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 20, index_interval=512,
+                       max_consumers=C, max_batch_records=65536)
+    spec = StreamSpec(P, 40000, "zipf", size=(1, 400), config_index=7)
+    g = np.random.default_rng(5)
+    n = 20000
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        ops = [("append", make_batch(spec, b)) for b in range(3)]
+        p = g.integers(0, P + 8, n)  # a few unknown partitions
+        c = g.integers(0, C + 1, n)  # and bad consumer indices
+        pc = np.repeat(np.arange(P), C)
+        cc = np.tile(np.arange(C), P)
+        ops.append(("consumer_commit", pc, cc, g.integers(0, 200, P * C)))
+        mx = g.integers(0, 40, n)
+        ops.append(("fetch", p, c, mx))
+        ops.append(("fetch", p, c, mx, 1 << 20))  # ends mid-way: later requests are ENOSPC
+        ops.append(("fetch", p[:300], c[:300], mx[:300]))
+        ops.append(("fetch", p, c, np.full(n, 1000)))
+        run_ops(dev, ora, cfg, ops, check=False)
+        log = run_ops(dev, ora, cfg, [("fetch", p, c, mx, 1 << 20)], check=False)
+        assert (log[0][1]["status"] == -4).any() and (log[0][1]["status"] == 0).any()
