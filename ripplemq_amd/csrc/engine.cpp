@@ -405,7 +405,7 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc,
-                             e->d_stats, e->d_req, e->d_res, e->d_flags, e->d_ticket, e->d_fetch_out,
+                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -532,7 +532,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   hipDeviceProp_t prop;
   CREATE_HIP(hipGetDeviceProperties(&prop, e->device));
   e->cu_count = (uint32_t)prop.multiProcessorCount;
-  e->big_wgs = 4u * e->cu_count;
+  e->big_wgs = 4u * e->cu_count * (512u / kPipeThreads);  // 32 large-record waves per CU
   if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
@@ -1069,19 +1069,20 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
   if (n > e->fetch_cap) {
     hipFree(e->d_req);
     hipFree(e->d_res);
-    hipFree(e->d_flags);
+    hipFree(e->d_aux);
+    hipFree(e->d_cpre);
     if (e->h_req) hipHostFree(e->h_req);
     if (e->h_res) hipHostFree(e->h_res);
     e->d_req = nullptr;
-    e->d_res = e->d_flags = nullptr;
-    e->h_req = nullptr;
+    e->d_res = e->d_aux = nullptr;
+    e->d_cpre = e->h_req = nullptr;
     e->h_res = nullptr;
     e->fetch_cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     rc = dalloc(&e->d_req, (size_t)cap * 4);
     if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4 + 2);
-    if (!rc) rc = dalloc(&e->d_flags, (size_t)fetch_workgroups(cap));  // zeroed: no epoch matches
-    if (!rc && !e->d_ticket) rc = dalloc(&e->d_ticket, 2);
+    if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
+    if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 4);
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
@@ -1110,29 +1111,22 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     a.st = e->st;
     a.req = e->d_req;
     a.res = e->d_res;
-    a.flags = e->d_flags;
-    a.ticket = e->d_ticket;
-    a.ticket_base = e->fetch_ticket;
+    a.aux = e->d_aux;
+    a.cpre = e->d_cpre;
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
-    a.nwg = fetch_workgroups(n);
-    if (++e->fetch_epoch >= (1u << 24)) {  // status words of 2^24 - 1 calls ago could match again
-      e->fetch_epoch = 1;
-      HIP_TRY(hipMemsetAsync(e->d_flags, 0, (size_t)fetch_workgroups(e->fetch_cap) * 8, e->fetch_s));
-    }
-    a.epoch = e->fetch_epoch;
-    e->fetch_ticket += a.nwg;
+    a.gather_wgs = std::max<uint32_t>(1u, 32u * e->cu_count);
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
     HIP_TRY(hipMemcpyAsync(e->d_req, e->h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
-    hipEvent_t r0 = nullptr, g1 = nullptr;
-    if (e->profile) {  // one timed region around the fetch kernel (profile_query(3))
-      r0 = pool_event(e);
-      g1 = pool_event(e);
-      e->prof[3].push_back({r0, g1});
+    hipEvent_t ev[6] = {};
+    if (e->profile) {  // kernel 3: the three kernels' own durations; 4: first start to last end
+      for (hipEvent_t& x : ev) x = pool_event(e);
+      for (int k = 0; k < 3; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
+      e->prof[4].push_back({ev[0], ev[5]});
     }
-    launch_fetch(a, e->fetch_s, r0, g1);
+    launch_fetch(a, e->fetch_s, e->profile ? ev : nullptr);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
     HIP_TRY(hipEventRecord(e->ev_fetch, e->fetch_s));

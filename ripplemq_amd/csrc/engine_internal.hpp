@@ -270,13 +270,11 @@ struct rmq_engine {
   hipEvent_t ev_main = nullptr, ev_fetch = nullptr;
   uint32_t* d_req = nullptr;
   uint64_t* d_res = nullptr;
-  uint64_t* d_flags = nullptr;  // look-back status words, one per fetch workgroup
-  uint64_t* d_ticket = nullptr;
+  uint64_t* d_aux = nullptr;
+  uint32_t* d_cpre = nullptr;
   bool trace = false;           // RMQ_TRACE: print every launch's roles to stderr
-  uint64_t fetch_ticket = 0;    // workgroups launched by earlier fetch calls
-  uint32_t fetch_epoch = 0;     // last call's epoch (1 .. 2^24 - 1)
   uint32_t* h_req = nullptr;   // pinned
-  uint64_t* h_res = nullptr;   // pinned [cap][4] + 2 totals
+  uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}
   uint32_t fetch_cap = 0;
   uint8_t* d_fetch_out = nullptr;
   uint64_t fetch_out_cap = 0;

@@ -7,9 +7,9 @@
 namespace rmq {
 
 #ifndef RMQ_PIPE_THREADS
-#define RMQ_PIPE_THREADS 512
+#define RMQ_PIPE_THREADS 256
 #endif
-constexpr uint32_t kPipeThreads = RMQ_PIPE_THREADS;  // threads per workgroup, every role of the pipeline launch
+constexpr uint32_t kPipeThreads = RMQ_PIPE_THREADS;  // threads per workgroup, every role of the pipeline launch (4 resident per CU)
 #ifndef RMQ_TILE_BITS
 #define RMQ_TILE_BITS 10
 #endif
@@ -181,15 +181,15 @@ struct PipeArgs {
 struct FetchArgs {
   DevState st;
   const uint32_t* req;       // [n][4] {pidx, consumer, max, reserved}
-  uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}, then [2] {bytes needed, 0}
-  uint64_t* flags;           // [nwg] look-back status words {epoch, flag, bytes}
-  uint64_t* ticket;          // virtual workgroup ids: ticket - ticket_base (monotonic over calls)
-  uint64_t ticket_base;
+  uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}, then {bytes needed}
+  uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
+  uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> place), 16-byte aligned
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
-  uint32_t n, nwg;
-  uint32_t epoch;            // 1 .. 2^24 - 1, names the call in the status words
+  uint32_t n;
+  uint32_t gather_wgs;       // gather grid cap (a wave per request, looping)
 };
+
 
 
 struct ConsumerCommitArgs {  // one item per (partition, consumer): the host resolved last-writer-wins
@@ -254,8 +254,7 @@ uint32_t pipeline_wgs_per_cu();
 void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
-uint32_t fetch_workgroups(uint32_t n);
-void launch_fetch(const FetchArgs& a, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
+void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev6);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move

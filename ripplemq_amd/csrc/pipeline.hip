@@ -44,9 +44,6 @@
 #include "kernels.hpp"
 #include "partition_ops.hpp"
 
-#ifndef RMQ_ZK_LDS
-#define RMQ_ZK_LDS (RMQ_PIPE_THREADS >= 512)
-#endif
 
 namespace rmq {
 
@@ -92,25 +89,19 @@ struct Stage1Smem {
 struct Stage3Smem {
   u32 t8[8][256];       // slicing-by-8 CRC32C tables
   u32 z[2][4][256];     // register shift past 16 and 32 zero bytes
-#if RMQ_ZK_LDS
-  u32 zk[4][256];       // register shift past 1024 zero bytes (wave-wide records)
-#endif
   uint4 img[kPW][kTaskRecs][8];  // per wave: the task's records as laid out in the log (<= 128 B each)
   uint4 info[kPW][kTaskRecs];    // per wave: {pos lo, pos hi, p, lm | m << 8 | ok << 16 | dead << 24}
-  u64 xdst[kPW][kTaskRecs][kMaxRemote];  // replication: each record's outbox address per remote slot
-  u32 xn[kPW][kTaskRecs];                // and how many
+  union {
+    // single-GPU kernel: the register shift past 1024 zero bytes of the large-record waves (the
+    // kernel with a transport reads it from global memory, L1/L2-resident: with 256-thread
+    // workgroups LDS has room for four per CU only without it)
+    u32 zk[4][256];
+    struct {
+      u64 xdst[kPW][kTaskRecs][kMaxRemote];  // replication: each record's outbox address per remote slot
+      u32 xn[kPW][kTaskRecs];                // and how many
+    };
+  };
 };
-
-// The 1 KB shift table of the large-record waves lives in LDS with 512-thread workgroups; with
-// smaller ones (RMQ_PIPE_THREADS=256, four resident per CU) LDS has no room for it and those waves
-// read it from global memory (L1/L2-resident, 4 KB).
-#if RMQ_ZK_LDS
-#define RMQ_ZK_TABLE S.zk
-constexpr u32 kBigTableBytes = sizeof(Stage3Smem::t8) + sizeof(Stage3Smem::z) + sizeof(Stage3Smem::zk);
-#else
-#define RMQ_ZK_TABLE A.crc->zshift1k
-constexpr u32 kBigTableBytes = sizeof(Stage3Smem::t8) + sizeof(Stage3Smem::z);
-#endif
 
 constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
 static_assert(kSmemBytes >= kMaxTiles * sizeof(u64), "stage 2's tile bases fit the dynamic LDS");
@@ -743,8 +734,8 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
 // l, l + 64, ... (kBU per lane in flight, the block after each from the neighbour lane), folds
 // them by Horner's rule with the 1 KB shift table, shifts its register past the pieces that follow
 // its last one and the wave XOR-reduces; lane 0 writes the header. xdst: the record's outbox copies.
-__device__ void big_record(const PipeArgs& A, const Stage3Smem& S, u64 src, u32 L, u64 pos, u64 off, u32 dead,
-                           uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx) {
+__device__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
+                           u64 off, u32 dead, uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx) {
   const u32 lane = threadIdx.x & 63, RF = A.st.RF;
   const u64 rstride = A.st.rstride;
   const u32 m = (L + 15u) >> 4, sa = (u32)(src & 15u);
@@ -779,7 +770,7 @@ __device__ void big_record(const PipeArgs& A, const Stage3Smem& S, u64 src, u32 
       if (jp < m) {
         const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
         const uint4 v = extract_piece(b0[u], b1, sa, nb);
-        acc = crc_zshift(RMQ_ZK_TABLE, acc) ^ piece_crc(A, S, v, jp);
+        acc = crc_zshift(zk, acc) ^ piece_crc(A, S, v, jp);
         uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
         if (jp + 1u >= dead)
           for (u32 r = 0; r < RF; ++r)
@@ -820,7 +811,12 @@ __device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
   {
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < kBigTableBytes / 16u; k += kPT) dst[k] = src[k];
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
+    if (!XR) {
+      const uint4* zs = reinterpret_cast<const uint4*>(&A.crc->zshift1k[0][0]);
+      uint4* zd = reinterpret_cast<uint4*>(&S.zk[0][0]);
+      for (u32 k = threadIdx.x; k < sizeof(S.zk) / 16u; k += kPT) zd[k] = zs[k];
+    }
   }
   __syncthreads();
   const u32 nw = A.wgb * kPW;
@@ -854,7 +850,7 @@ __device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
         xdst[nx++] = reinterpret_cast<u64>(A.outbox3 + A.xe3[oe].data_abs + 16ull * rel16);
       }
     }
-    big_record(A, S, src, L, pos, off, dead, st.logs + rg.base, rg.seg - 1ull, (A.debug & 1u) ? 0u : lm, xdst, nx);
+    big_record(A, S, XR ? A.crc->zshift1k : S.zk, src, L, pos, off, dead, st.logs + rg.base, rg.seg - 1ull, (A.debug & 1u) ? 0u : lm, xdst, nx);
   }
 }
 
@@ -1169,14 +1165,10 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (!(A.debug & 8u)) {
     // slicing and zero-shift tables are contiguous in CrcConsts and in Stage3Smem: 16-byte copies
     static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
-#if RMQ_ZK_LDS
-    static_assert(offsetof(Stage3Smem, zk) == sizeof(S.t8) + sizeof(S.z), "z and zk adjacent in LDS");
-#endif
     static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
-    static_assert(offsetof(CrcConsts, zshift1k) == offsetof(CrcConsts, zshift) + sizeof(A.crc->zshift), "zshift1k next");
     const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
     uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];  // zk: large-record waves only
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];  // zk: large-record waves
   }
   bool cand = task < tasks && stage3_cand(A, T, R);
   TaskState Z = stage3_r2(A, T, R, cand);

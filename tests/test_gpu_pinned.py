@@ -129,11 +129,10 @@ def test_fetch_during_pipelined_appends(oracle_mod):
         assert seen > 0, "no fetch saw committed records while appends were in flight"
 
 
-def test_fetch_lookback_many_requests(oracle_mod):
-    """One fetch launch places 20k requests (5k workgroups: look-back chains far past one 64-word
-    window) with unknown partitions, bad consumers and zero-record slices mixed in, then the same
-    requests into an output buffer that ends mid-way (ENOSPC after the cut), over several calls so
-    the status words of earlier calls are present."""
+def test_fetch_many_requests(oracle_mod):
+    """One fetch call places 20k requests (several passes of the placement scan) with unknown
+    partitions, bad consumers and zero-record slices mixed in, then the same requests into an
+    output buffer that ends mid-way (ENOSPC after the cut), over several calls."""
     P, C = 1024, 4
     cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 20, index_interval=512,
                        max_consumers=C, max_batch_records=65536)
