@@ -210,7 +210,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             t0 = time.perf_counter()
             rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
             t_wall += time.perf_counter() - t0
-            _, ms_f = eng.profile_query(3)  # the two kernels' own dispatch-recorded spans, summed
+            _, ms_f = eng.profile_query(3)  # the three kernels' own dispatch-recorded spans, summed
             _, ms_r = eng.profile_query(4)  # first kernel start to last kernel end: the fetch's GPU time
             eng.profile(False)
             if rc or np.any(res["status"] != 0):
@@ -230,7 +230,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                            "requests": P * consumers, "rounds": rounds,
                            "roofline": {"bound": "hbm", "achieved": alg / t_reg / 1e9, "peak": HBM_PEAK_GBS,
                                         "unit": "GB/s", "frac": alg / t_reg / 1e9 / HBM_PEAK_GBS,
-                                        "kernels": "rmq::fetch_resolve (its last workgroup places) + fetch_gather",
+                                        "kernels": "rmq::fetch_resolve + fetch_place + fetch_gather",
                                         "mean_us_per_fetch": t_reg / rounds * 1e6,
                                         "kernel_spans_us_summed": t_kern / rounds * 1e6}}
     return out

@@ -96,31 +96,9 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   return c_pos + 16ull * cur;
 }
 
-__device__ void resolve_one(const FetchArgs& a, u32 r);
-template <u32 NT>
-__device__ void fetch_place(const FetchArgs& a);
-
 __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
   const u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6));
-  if (r < a.n) resolve_one(a, r);
-  // the last workgroup to finish places every request (one launch less per fetch): every wave's
-  // stores drained, a workgroup barrier, one agent-scope acq_rel add per workgroup; the last adder's
-  // acquire then makes every workgroup's results visible to it (MI355X_MICROARCH.md, inter-workgroup
-  // visibility: release before the flag, acquire after it)
-  __shared__ u32 s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(a.arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
-  __syncthreads();
-  if (!s_last) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  fetch_place<64 * kFW>(a);
-  if (threadIdx.x == 0) __hip_atomic_store(a.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
-}
-
-__device__ void resolve_one(const FetchArgs& a, u32 r) {
+  if (r >= a.n) return;
   const DevState& st = a.st;
   const u32 p = a.req[4 * r], c = a.req[4 * r + 1], mx = a.req[4 * r + 2];
   int status = kOk;
@@ -172,14 +150,12 @@ __device__ void resolve_one(const FetchArgs& a, u32 r) {
 // One workgroup: output positions = exclusive scan of the requests' bytes in request order; each
 // thread scans 16 consecutive requests per pass (16-byte loads of the byte counts, 16-byte stores of
 // the compact positions: one load round per 16384 requests).
-template <u32 NT>
-__device__ void fetch_place(const FetchArgs& a) {
-  constexpr u32 NW = NT / 64;
-  __shared__ u64 sh[NW];
+__global__ __launch_bounds__(1024) void fetch_place_kernel(FetchArgs a) {
+  __shared__ u64 sh[16];
   constexpr u32 kPer = 16;
   const u32 tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   u64 carry = 0;
-  for (u32 b = 0; b < a.n; b += NT * kPer) {
+  for (u32 b = 0; b < a.n; b += 1024 * kPer) {
     const u32 r0 = b + tid * kPer;
     u32 nb[kPer];
     if (r0 + kPer <= a.n) {
@@ -204,7 +180,7 @@ __device__ void fetch_place(const FetchArgs& a) {
     __syncthreads();
     u64 cur = carry + inc - loc, tot = 0;
 #pragma unroll
-    for (u32 k = 0; k < NW; ++k) {
+    for (u32 k = 0; k < 16; ++k) {
       cur += k < w ? sh[k] : 0ull;
       tot += sh[k];
     }
@@ -252,15 +228,16 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   }
 }
 
-// ev[4]: start / end events of the two kernels, recorded by the dispatches themselves
+// ev[6]: start / end events of the three kernels, recorded by the dispatches themselves
 // (profiling: kernel time without the host's launch gaps), or null
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
   hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW - 1) / kFW), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);
+  hipExtLaunchKernelGGL(fetch_place_kernel, dim3(1), dim3(1024), 0, s, e ? e[2] : nullptr, e ? e[3] : nullptr, 0, a);
   hipExtLaunchKernelGGL(fetch_gather_kernel, dim3(std::min<u32>((a.n + kFW - 1) / kFW, a.gather_wgs)), dim3(64 * kFW), 0,
-                        s, e ? e[2] : nullptr, e ? e[3] : nullptr, 0, a);
+                        s, e ? e[4] : nullptr, e ? e[5] : nullptr, 0, a);
 }
 
 }  // namespace rmq
