@@ -178,15 +178,19 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   if (s2) {
     a.g2 = make_group(e, *s2);
     a.s2 = e->scratch[s2->set];
-    a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + kPipeThreads - 1) / kPipeThreads, 2u * e->cu_count));
-    if (e->s2_wgs) a.wg2 = std::min(a.wg2, e->s2_wgs);
   }
   repl_pipe_args(e, a, s2, s3);
+  // the kernel with a transport (outboxes) runs 512-thread workgroups, the single-GPU one 256
+  const uint32_t PT = a.outidx ? kPipeThreadsXR : kPipeThreads;
+  if (s2) {
+    a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + PT - 1) / PT, 2u * e->cu_count));
+    if (e->s2_wgs) a.wg2 = std::min(a.wg2, e->s2_wgs);
+  }
   {
     int rc = repl_before_launch(e, a);  // followers' acks of the group applied three launches ago
     if (rc) return rc;
   }
-  if (s3 || s4 || a.ackin) a.wgp = (P + kPipeThreads - 1) / kPipeThreads;
+  if (s3 || s4 || a.ackin) a.wgp = (P + PT - 1) / PT;
   if (s4) {
     a.g4 = make_group(e, *s4);
     a.s4 = e->scratch[s4->set];
@@ -194,15 +198,15 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   if (s3) {
     a.g3 = make_group(e, *s3);
     a.s3 = e->scratch[s3->set];
-    const uint32_t wpb = kPipeThreads / 64;
+    const uint32_t wpb = PT / 64;
     const uint32_t want = std::max<uint32_t>(1u, (s3->tasks + wpb - 1) / wpb);
     // default: one wave per task (the workgroups past the resident slots start as stage-1/2
     // workgroups retire); RMQ_WG3_ALL=0 fills only the slots next to the other roles (resident
     // workgroups per CU from the kernel's launch bounds) and the task waves loop over the rest
-    const uint32_t slots = pipeline_wgs_per_cu() * e->cu_count, busy = a.wg1 + a.wg2 + a.wgp;
+    const uint32_t slots = pipeline_wgs_per_cu(PT) * e->cu_count, busy = a.wg1 + a.wg2 + a.wgp;
     const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
     a.wg3 = e->wg3_all ? want : std::min<uint32_t>(want, room);
-    a.wgb = e->big_wgs;
+    a.wgb = e->big_wgs ? e->big_wgs : 32u * e->cu_count / (PT / 64u);  // 32 large-record waves per CU
   }
   a.launch_seq = ++e->launch_seq;
   if (e->d_stamps && a.launch_seq == e->stamps_at) {
@@ -532,7 +536,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   hipDeviceProp_t prop;
   CREATE_HIP(hipGetDeviceProperties(&prop, e->device));
   e->cu_count = (uint32_t)prop.multiProcessorCount;
-  e->big_wgs = 4u * e->cu_count * (512u / kPipeThreads);  // 32 large-record waves per CU
   if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));

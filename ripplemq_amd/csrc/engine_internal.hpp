@@ -241,7 +241,7 @@ struct rmq_engine {
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
   CopyPool* copy_pool = nullptr;  // host batches (created with the first one)
-  uint32_t big_wgs = 0;           // stage-3 workgroups for records over 1 KB (RMQ_BIG_WGS, default 4 x CUs)
+  uint32_t big_wgs = 0;           // stage-3 workgroups for records over 1 KB (RMQ_BIG_WGS; 0: 32 waves per CU)
   // pipeline: the group being formed, then groups ranked (need stage 2), scanned (need stage 3)
   // and applied (need stage 4)
   GroupFlight forming, g1, g2, g3;

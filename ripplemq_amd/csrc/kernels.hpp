@@ -9,6 +9,7 @@ namespace rmq {
 #ifndef RMQ_PIPE_THREADS
 #define RMQ_PIPE_THREADS 256
 #endif
+constexpr uint32_t kPipeThreadsXR = 512;  // threads per workgroup of the kernel with a transport
 constexpr uint32_t kPipeThreads = RMQ_PIPE_THREADS;  // threads per workgroup, every role of the pipeline launch (4 resident per CU)
 #ifndef RMQ_TILE_BITS
 #define RMQ_TILE_BITS 10
@@ -249,8 +250,7 @@ struct MigrateItem {
 // launchers (defined in the .hip files)
 // start: an event the dispatch records as the kernel starts (profiling), or null
 void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start = nullptr);
-uint32_t pipeline_lds_bytes();
-uint32_t pipeline_wgs_per_cu();
+uint32_t pipeline_wgs_per_cu(uint32_t threads);  // resident workgroups per CU of that size
 void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
@@ -263,3 +263,8 @@ void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, ui
 void launch_ack_apply(const AckApplyArgs& a, hipStream_t s);
 
 }  // namespace rmq
+
+namespace rmq_x {
+// pipeline.hip compiled for a replication transport (512-thread workgroups)
+void launch_pipeline_xr(const rmq::PipeArgs& a, hipStream_t s, hipEvent_t start);
+}  // namespace rmq_x

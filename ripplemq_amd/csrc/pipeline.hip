@@ -45,7 +45,16 @@
 #include "partition_ops.hpp"
 
 
-namespace rmq {
+// This file is compiled twice (Makefile): as namespace rmq with RMQ_PIPE_THREADS=256 for the
+// single-GPU kernel, and as namespace rmq_x with 512 threads and RMQ_PIPE_XR_TU for the kernel with
+// a replication transport (its stage 3 also fills outboxes). The transport kernel keeps the
+// 512-thread workgroups it was developed with: A/B runs over the in-process transport (2 ranks on
+// one GPU) were inconclusive (the same kernel varied by +-8 % between runs).
+#ifndef RMQ_PIPE_NS
+#define RMQ_PIPE_NS rmq
+#endif
+namespace RMQ_PIPE_NS {
+using namespace rmq;
 
 constexpr u32 kPT = kPipeThreads;   // 512 (RMQ_PIPE_THREADS)
 constexpr u32 kPW = kPT / 64;       // 8 waves
@@ -1192,8 +1201,14 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   PIPE_STAMP(6);
 }
 
-uint32_t pipeline_lds_bytes() { return (uint32_t)kSmemBytes; }
-uint32_t pipeline_wgs_per_cu() { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (kPT / 64u); }
+#ifdef RMQ_PIPE_XR_TU
+// the kernel with a replication transport (engine.cpp sizes its roles for kPipeThreadsXR)
+void launch_pipeline_xr(const PipeArgs& a, hipStream_t s, hipEvent_t start) {
+  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb;
+  hipExtLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, start, nullptr, 0, a);
+}
+#else
+uint32_t pipeline_wgs_per_cu(uint32_t threads) { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (threads / 64u); }
 
 void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start) {
   const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb;
@@ -1202,9 +1217,10 @@ void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start) {
     return;
   }
   if (a.outidx)
-    hipExtLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, start, nullptr, 0, a);
+    rmq_x::launch_pipeline_xr(a, s, start);
   else
     hipExtLaunchKernelGGL(pipeline_kernel<false>, dim3(grid), dim3(kPT), kSmemBytes, s, start, nullptr, 0, a);
 }
+#endif
 
-}  // namespace rmq
+}  // namespace RMQ_PIPE_NS
