@@ -166,7 +166,6 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.nxt = nxt;
   a.key_passes = e->key_passes;
   a.gt = e->max_group_tiles;
-  a.s3_first = e->s3_first;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
   a.debug = e->debug;
@@ -207,6 +206,10 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
     a.wg3 = e->wg3_all ? want : std::min<uint32_t>(want, room);
     a.wgb = e->big_wgs ? e->big_wgs : 32u * e->cu_count / (PT / 64u);  // 32 large-record waves per CU
+    // dispatch order: s3_lead stage-3 workgroups, then ranking, scans and partition threads, then
+    // the rest of stage 3, so the ranking/scan chains start before stage 3's last workgroups and
+    // end with them (RMQ_S3_LEAD=<n>; RMQ_S3_FIRST=0 puts all of stage 3 last)
+    a.s3_lead = e->s3_first ? std::min<uint32_t>(a.wg3, e->s3_lead ? e->s3_lead : a.wg3) : 0u;
   }
   a.launch_seq = ++e->launch_seq;
   if (e->d_stamps && a.launch_seq == e->stamps_at) {
@@ -215,6 +218,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     e->stamps_wg[1] = a.wg2;
     e->stamps_wg[2] = a.wgp;
     e->stamps_wg[3] = a.wg3;
+    e->stamps_wg[4] = a.s3_lead;
   }
   hipEvent_t ev_start = nullptr;
   if (e->profile && !e->prof_ended) {
@@ -378,17 +382,20 @@ int ensure_ctl(rmq_engine* e, uint32_t n) {
 void dump_stamps(rmq_engine* e) {
   const uint32_t nwg = e->stamps_wg[0] + e->stamps_wg[1] + e->stamps_wg[2] + e->stamps_wg[3];
   if (!e->stamps_path || !e->d_stamps || !nwg) return;
-  std::vector<uint64_t> h((size_t)nwg * 64);
+  // the launch's layout: waves per workgroup of its variant, roles in dispatch order
+  const uint32_t wpg = (e->repl ? kPipeThreadsXR : kPipeThreads) / 64u;
+  std::vector<uint64_t> h((size_t)nwg * wpg * 8);
   if (hipMemcpy(h.data(), e->d_stamps, h.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
   FILE* f = std::fopen(e->stamps_path, "w");
   if (!f) return;
   std::fprintf(f, "wg,wave,stage,t0,t1,t2,t3,t4,t5,t6,t7\n");
+  const uint32_t w1 = e->stamps_wg[0], w2 = e->stamps_wg[1], wp = e->stamps_wg[2];
   for (uint32_t g = 0; g < nwg; ++g) {
-    const uint32_t a1 = e->stamps_wg[0], a2 = a1 + e->stamps_wg[1], a3 = a2 + e->stamps_wg[2];
-    const int stage = g < a1 ? 1 : g < a2 ? 2 : g < a3 ? 4 : 3;  // 4: partition threads
-    for (uint32_t w = 0; w < 8; ++w) {
+    const uint32_t ld = e->stamps_wg[4];  // stage-3 workgroups before the other roles
+    const int stage = g < ld ? 3 : g < ld + w1 ? 1 : g < ld + w1 + w2 ? 2 : g < ld + w1 + w2 + wp ? 4 : 3;  // 4: partitions
+    for (uint32_t w = 0; w < wpg; ++w) {
       std::fprintf(f, "%u,%u,%d", g, w, stage);
-      for (int k = 0; k < 8; ++k) std::fprintf(f, ",%llu", (unsigned long long)h[((size_t)g * 8 + w) * 8 + k]);
+      for (int k = 0; k < 8; ++k) std::fprintf(f, ",%llu", (unsigned long long)h[((size_t)g * wpg + w) * 8 + k]);
       std::fprintf(f, "\n");
     }
   }
@@ -522,6 +529,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S1_WGS")) e->s1_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S2_WGS")) e->s2_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \

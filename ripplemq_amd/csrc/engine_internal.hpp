@@ -295,13 +295,14 @@ struct rmq_engine {
   const char* stamps_path = nullptr;
   uint64_t stamps_at = 100;
   uint64_t* d_stamps = nullptr;
-  uint32_t stamps_wg[4] = {0, 0, 0, 0};
+  uint32_t stamps_wg[5] = {0, 0, 0, 0, 0};  // roles of the stamped launch: s1, s2, parts, s3, s3 lead
   // one stage-3 wave per task: the workgroups beyond the resident slots dispatch as stage-1/2
   // workgroups retire (RMQ_WG3_ALL=0: only as many as fit next to them, looping over tasks)
   uint32_t wg3_all = 1;
   uint32_t s1_wgs = 0;    // RMQ_S1_WGS: stage-1 workgroups per launch (0: one per tile; fewer loop over tiles)
   uint32_t s2_wgs = 0;    // RMQ_S2_WGS: cap on stage-2 workgroups (0: one thread group per column)
   uint32_t s3_first = 1;  // stage-3 workgroups first in dispatch order (RMQ_S3_FIRST=0: last)
+  uint32_t s3_lead = 0;   // stage-3 workgroups before the other roles (RMQ_S3_LEAD; 0: all of them)
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
   std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)
   rmq::Replication* repl = nullptr;  // replication transport attached (collective mode)

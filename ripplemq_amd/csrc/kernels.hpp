@@ -163,7 +163,7 @@ struct PipeArgs {
   uint32_t wgb;                 // stage 3's large-record workgroups (last along blockIdx.x)
   uint32_t key_passes;     // 1 (P <= 256) or 2
   uint32_t gt;             // tiles per hist / excl column (group tile capacity)
-  uint32_t s3_first;       // 1: stage-3 workgroups first along blockIdx.x (dispatched first)
+  uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
   uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2

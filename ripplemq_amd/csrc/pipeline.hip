@@ -1121,19 +1121,23 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
     __hip_atomic_store(A.done_word, A.launch_seq - 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   u32 wg = blockIdx.x;
-  // roles along blockIdx.x: [stage 1 | stage 2 | partition threads | stage 3 | large records], or
-  // with s3_first [stage 3 | stage 1 | stage 2 | partition threads | large records]
+  // roles along blockIdx.x: [s3_lead stage-3 workgroups | stage 1 | stage 2 | partition threads |
+  // the other stage-3 workgroups | large records] (dispatch order)
   if (wg >= A.wg1 + A.wg2 + A.wgp + A.wg3) {
     stage3_big_waves<XR>(A, *reinterpret_cast<Stage3Smem*>(smem_raw), wg - (A.wg1 + A.wg2 + A.wgp + A.wg3));
     return;
   }
   bool s3 = false;
-  if (A.s3_first) {
-    s3 = wg < A.wg3;
-    if (!s3) wg -= A.wg3;
-  } else {
-    s3 = wg >= A.wg1 + A.wg2 + A.wgp;
-    if (s3) wg -= A.wg1 + A.wg2 + A.wgp;
+  {
+    const u32 other = A.wg1 + A.wg2 + A.wgp;
+    if (wg < A.s3_lead) {
+      s3 = true;
+    } else if (wg < A.s3_lead + other) {
+      wg -= A.s3_lead;
+    } else {
+      s3 = true;
+      wg -= other;
+    }
   }
   if (!s3) {
     if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
