@@ -496,6 +496,8 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
+    ap.add_argument("--concurrent-rounds", type=int, default=0,
+                    help="rounds of the append+fetch mixed leg (0: skip)")
     ap.add_argument("--host-steps", type=int, default=100,
                     help="batches of the host-memory leg (PCIe-inclusive rate, 1 GPU; 0: skip)")
     ap.add_argument("--watchdog", type=float, default=900.0, help="multi-GPU: exit a rank stuck this long [s]")

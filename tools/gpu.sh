@@ -1,0 +1,72 @@
+# The canonical GPU measurement procedure (run through gpurun from the repo root):
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# Steps, each under its own time limit; the script stops at the first failing step and writes
+# everything under gpurun_out/<tag>_*:
+#   tests      pytest -m gpu (all GPU parity tests), log in <tag>_pytest_gpu.log
+#   tests:K    the same restricted to `-k K`
+#   smoke      __graft_entry__.smoke()
+#   bench      default bench line (2000 steps, CPU baseline, fetch, concurrent and host legs)
+#   bench20    two driver-shaped lines (--steps 20 --warmup 5)
+#   steady     one 600-step line without the side legs
+#   benchD     config D (RF 5, 64 B..16 KB) line
+#   ab         A/B of the current library against variants/head/ (400- and 20-step lines, 2 pairs)
+#   local2     2-rank rehearsal on one GPU over the in-process transport (+ kernel trace)
+#   local4     4-rank rehearsal (config C shape)
+#   prof       rocprofv3 --kernel-trace --stats of the default line (kernel stats CSV)
+#   pmc        rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) of a 300-step line
+#   stamps     per-wave phase stamps of launch 100 (RMQ_STAMPS) + timing-only RMQ_DEBUG lines
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+R=$GRAFT_REPO_ROOT
+T=$1
+shift
+mkdir -p gpurun_out
+Q="--no-cpu-baseline --fetch-rounds 0 --concurrent-rounds 0 --host-steps 0"
+run() {  # run <seconds> <out file> <command...>: stdout to the file, stderr to <file>.err
+  local lim=$1 out=$2
+  shift 2
+  echo "[gpu.sh] $(date +%T) $out: $*"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$out" 2> "gpurun_out/$out.err" || { echo "[gpu.sh] FAILED rc=$? $out"; tail -20 "gpurun_out/$out.err"; exit 1; }
+}
+prof() {  # prof <seconds> <name> <rocprofv3 args...> -- <python args...>
+  local lim=$1 name=$2
+  shift 2
+  echo "[gpu.sh] $(date +%T) rocprofv3 $name"
+  (cd /tmp && export TMPDIR=/tmp && timeout -s KILL "$lim" rocprofv3 "$@") > "$R/gpurun_out/${T}_$name.log" 2>&1 || { echo "[gpu.sh] FAILED rocprofv3 $name"; tail -20 "$R/gpurun_out/${T}_$name.log"; exit 1; }
+}
+for step in "$@"; do
+  case $step in
+    tests) run 1000 "${T}_pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread ;;
+    tests:*) run 600 "${T}_pytest_gpu.log" python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "${step#tests:}" ;;
+    smoke) run 300 "${T}_smoke.txt" python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run 500 "${T}_bench.json" python bench.py ;;
+    bench20) for k in 1 2; do run 200 "${T}_bench20_$k.json" python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
+    steady) run 300 "${T}_steady.json" python bench.py --steps 600 --warmup 60 $Q ;;
+    benchD) run 300 "${T}_benchD.json" python bench.py --config D --pool 16 --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0 ;;
+    ab)
+      for k in 1 2; do
+        for v in cur head; do
+          if [ $v = cur ]; then L=$R/ripplemq_amd/libripplemq_engine.so; else L=$R/variants/head/libripplemq_engine.so; fi
+          RMQ_LIB=$L run 200 "${T}_${v}_400_$k.json" python bench.py --steps 400 --warmup 40 $Q
+          RMQ_LIB=$L run 200 "${T}_${v}_20_$k.json" python bench.py --steps 20 --warmup 5 $Q
+        done
+      done ;;
+    local2)
+      run 300 "${T}_local2.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
+      prof 300 local2_prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_local2_kt" -o kt -- python3 "$R/bench.py" --gpus 2 --transport local --steps 100 --warmup 10 --segment-mb 2 --pool 8 $Q ;;
+    local4) run 300 "${T}_local4.json" python bench.py --gpus 4 --transport local --steps 100 --warmup 10 --segment-mb 1 --pool 4 --config C $Q ;;
+    prof) prof 500 prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_prof" -o kt -- python3 "$R/bench.py" --no-cpu-baseline --host-steps 0 ;;
+    pmc)
+      prof 150 pmc_fetch --pmc FETCH_SIZE -f csv -d "$R/gpurun_out/${T}_pmc_fetch" -o pf -- python3 "$R/bench.py" --steps 300 --warmup 50 $Q
+      prof 150 pmc_write --pmc WRITE_SIZE -f csv -d "$R/gpurun_out/${T}_pmc_write" -o pw -- python3 "$R/bench.py" --steps 300 --warmup 50 $Q ;;
+    stamps)
+      RMQ_STAMPS=gpurun_out/${T}_st.csv RMQ_STAMPS_AT=100 run 200 "${T}_stamped.json" python bench.py --steps 600 --warmup 60 $Q
+      python tools/pipe_stamps.py "gpurun_out/${T}_st.csv" > "gpurun_out/${T}_stamps.txt" 2>&1
+      for d in 1 16; do RMQ_DEBUG=$d run 200 "${T}_dbg$d.json" python bench.py --steps 400 --warmup 40 $Q; done ;;
+    *) echo "[gpu.sh] unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu.sh] $(date +%T) done"
