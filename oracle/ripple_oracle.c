@@ -942,12 +942,23 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     return RMQ_EINVAL;
   }
   const uint64_t tab = 32 + 32ull * n;
-  /* the state every entry of a partition sees: the log end it continues, decided once (owner) */
-  uint64_t leo = 0, used = 0, term0 = 0;
+  /* pass 1: the verdict of every entry against the state every entry of a partition sees (the log
+     end it continues, decided once by the owner: two local slots, the first keeps the state) */
+  int* okv = (int*)malloc((size_t)n * sizeof(int));
+  uint64_t* base = (uint64_t*)malloc((size_t)n * 2 * sizeof(uint64_t));
+  int* stv = (int*)malloc((size_t)n * sizeof(int));
+  if (!okv || !base || !stv) {
+    free(okv);
+    free(base);
+    free(stv);
+    free(v);
+    return RMQ_ENOMEM;
+  }
+  uint64_t leo = 0, used = 0;
   int stale = 0;
   for (uint32_t k = 0; k < n; ++k) {
     ro_part* s = &e->parts[v[k].p];
-    const int owner = k == 0 || v[k - 1].p != v[k].p; /* two local slots: the first keeps the state */
+    const int owner = k == 0 || v[k - 1].p != v[k].p;
     const uint8_t* d = region + 32 + 32ull * k;
     uint32_t cnt, by16, ts, ds;
     uint64_t first, term;
@@ -958,8 +969,7 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     memcpy(&ds, d + 20, 4);
     memcpy(&term, d + 24, 8);
     if (owner) {
-      term0 = s->term;
-      stale = term < term0; /* a leader of an older term */
+      stale = term < s->term; /* a leader of an older term */
       leo = s->leo;
       used = s->used;
       if (!stale && first < leo && first >= s->start_off) { /* the leader's log wins: truncate */
@@ -967,6 +977,9 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
         leo = first;
       }
     }
+    base[2 * k] = leo;
+    base[2 * k + 1] = used;
+    stv[k] = stale;
     int ok = !stale && (!cnt || first == leo);
     uint64_t rel = 0;
     for (uint32_t r = 0; r < cnt && ok; ++r) {
@@ -982,9 +995,29 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
       for (uint64_t z = 16 + len; ok && z < rec_size(len); ++z) ok = rec[z] == 0; /* zero padding (§1) */
       rel += rec_size(len);
     }
-    if (!ok) {
+    okv[k] = ok;
+    if (!ok) e->counters[!stale && (!cnt || first == leo) ? 1 : 2]++;
+  }
+  /* a refusal of either slot of a partition is a refusal of both */
+  for (uint32_t k = 0; k < n; ++k)
+    for (uint32_t q = k + 1; q < n && v[q].p == v[k].p; ++q)
+      if (!okv[k] || !okv[q]) okv[k] = okv[q] = 0;
+  /* pass 2: apply the accepted entries */
+  for (uint32_t k = 0; k < n; ++k) {
+    ro_part* s = &e->parts[v[k].p];
+    const int owner = k == 0 || v[k - 1].p != v[k].p;
+    const uint8_t* d = region + 32 + 32ull * k;
+    uint32_t cnt, by16, ds;
+    uint64_t first, term;
+    memcpy(&cnt, d, 4);
+    memcpy(&by16, d + 4, 4);
+    memcpy(&first, d + 8, 8);
+    memcpy(&ds, d + 20, 4);
+    memcpy(&term, d + 24, 8);
+    leo = base[2 * k];
+    used = base[2 * k + 1];
+    if (!okv[k]) {
       acks[k] = 0;
-      e->counters[!stale && first == leo ? 1 : 2]++;
       continue;
     }
     if (owner) {
@@ -998,17 +1031,23 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     const uint8_t* bytes = region + data + 16ull * ds;
     ring_write(e->parts[v[k].p].seg, ring_of(e, v[k].slot, v[k].p), used, bytes, 16ull * by16);
     if (owner) {
-      rel = 0;
+      uint64_t rel = 0;
       for (uint32_t r = 0; r < cnt; ++r) {
         uint32_t len;
         memcpy(&len, bytes + rel + 8, 4);
         const uint64_t pos = used + rel, rs = rec_size(len);
         for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
           if (vec_push(&s->idx_off, first + r + 1) || vec_push(&s->idx_pos, pos + rs)) {
+            free(okv);
+            free(base);
+            free(stv);
             free(v);
             return RMQ_ENOMEM;
           }
         if (vec_push(&s->rec_pos, pos)) {
+          free(okv);
+          free(base);
+          free(stv);
           free(v);
           return RMQ_ENOMEM;
         }
@@ -1026,6 +1065,9 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     e->counters[0] += cnt;
     acks[k] = first + cnt;
   }
+  free(okv);
+  free(base);
+  free(stv);
   free(v);
   return RMQ_OK;
 }

@@ -349,7 +349,13 @@ int wait_ticket(rmq_engine* e, uint64_t t) {
         L = m.second;
         break;
       }
-    while (!launch_done(e, L)) std::this_thread::yield();
+    // the done word only moves while launches succeed: a faulted stream (sticky error) ends the wait
+    while (L > __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE)) {
+      const hipError_t q = hipStreamQuery(e->main_s);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return hip_fail(q);
+      std::this_thread::yield();
+    }
     ticket_state(e, t);
   }
   return RMQ_OK;
@@ -844,9 +850,10 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   }
   HIP_TRY(hipSetDevice(e->device));
 
-  const uint64_t t = ++e->last_ticket;
-  *ticket = t;
-  e->ticket_n[t % kStatsRing] = n;
+  // the ticket is taken only once nothing below can fail short of a device error: the staging
+  // slot's wait and the first host batch's allocations come first (with a transport a used-up
+  // ticket without a queued batch would leave this rank's groups out of step with its peers')
+  const uint64_t t = e->last_ticket + 1;
   // an empty batch still takes its place in a launch group (0 tiles, 0 tasks): every rank of a
   // replication transport forms the same groups from the same number of calls
   InFlight f;
@@ -876,7 +883,6 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
         HIP_TRY(hipHostMalloc((void**)&z.h_out, NB * 8, 0));
         HIP_TRY(hipEventCreateWithFlags(&z.ev_in, hipEventDisableTiming));
       }
-    sg.ticket = t;
     const uint64_t o_len = (4ull * n + 15) & ~15ull, o_poff = o_len + ((4ull * n + 15) & ~15ull);
     const uint64_t o_pay = o_poff + (b->payload_off ? (8ull * n + 15) & ~15ull : 0ull);
     if (!e->copy_pool) {
@@ -891,6 +897,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
                                        {sg.h_blk + o_len, reinterpret_cast<const uint8_t*>(b->len), 4ull * n}};
     if (b->payload_off) segs.push_back({sg.h_blk + o_poff, reinterpret_cast<const uint8_t*>(b->payload_off), 8ull * n});
     if (b->payload_bytes) segs.push_back({sg.h_blk + o_pay, b->payload, b->payload_bytes});
+    sg.ticket = t;
     e->copy_pool->run(segs, 512u << 10);
     HIP_TRY(hipMemcpyAsync(sg.d_blk, sg.h_blk, o_pay + b->payload_bytes, hipMemcpyHostToDevice, e->copy_s));
     HIP_TRY(hipEventRecord(sg.ev_in, e->copy_s));
@@ -904,6 +911,9 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     sg.user_out = out_offsets;
     sg.out_n = n;
   }
+  e->last_ticket = t;
+  *ticket = t;
+  e->ticket_n[t % kStatsRing] = n;
   if (e->forming.nb && e->forming.tiles + f.b.tiles > e->max_group_tiles) {  // (never with a transport)
     int rc = close_group(e);
     if (rc) return rc;

@@ -117,12 +117,13 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
   const DevState& st = A.st;
   const u32 p = A.xi_p[e];
   u64 leo = st.leo[p], used = st.used[p];
+  A.bad[e] = 0u;  // this round's verdict starts clean (the finish kernel only reads it)
   if (A.rbytes[src]) {
     const RegionView R = region_of(A, src);
     if (R.n_entries == A.xi_start[src + 1] - A.xi_start[src]) {
       const DirView d = dir_of(R, k);
       if (d.term < st.term[p]) {
-        A.bad[e] |= 4u;  // a stale leader
+        A.bad[e] = 4u;  // a stale leader
       } else if (d.first < leo && d.first >= st.start_off[p]) {
         used = follower_pos(st, p, A.xi_slot[e], d.first);  // the leader's log wins: truncate
         leo = d.first;
@@ -291,12 +292,16 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
     if (k == 0) atomicAdd((unsigned long long*)&A.counters[2], 1ull);
   } else if (A.rbytes[src]) {
     const DirView d = dir_of(region_of(A, src), k);
-    const u32 bad = A.bad[e];
+    // two local slots of one partition (adjacent entries of the same source): the owner keeps the
+    // partition's state, so a refusal of either is a refusal of both (no slot acks records the
+    // follower's log end does not hold)
+    u32 bad = A.bad[e];
+    for (u32 q = e; q > A.xi_start[src] && A.xi_p[q - 1] == p; --q) bad |= A.bad[q - 1] ? 8u : 0u;
+    for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) bad |= A.bad[q] ? 8u : 0u;
     const u64 bleo = A.base[2 * e], bused = A.base[2 * e + 1];
     if (bad) {
       ack = 0;  // no new information (match only moves up)
-      atomicAdd((unsigned long long*)&A.counters[(bad & 6u) ? 2 : 1], 1ull);
-      A.bad[e] = 0u;
+      if (bad & 7u) atomicAdd((unsigned long long*)&A.counters[(bad & 6u) ? 2 : 1], 1ull);
     } else {
       // the entry continues the log at bleo (or does not: a follower behind the leader acks 0)
       const bool cont = d.first == bleo;

@@ -172,15 +172,25 @@ class Engine:
         self._keep.pop(ticket, None)
         return (commit, hw) if want_commit else True
 
-    def wait(self, ticket: int) -> dict:
+    def wait(self, ticket: int) -> dict | None:
+        """Stats of a completed ticket, or None while it is pending: with a replication transport a
+        ticket is applied only by an rmq_sync on every rank (the caller's arrays stay referenced
+        until then; their out offsets are not written yet)."""
         st = A.RmqAppendStats()
-        _check(self.lib.rmq_ticket_stats(self.h, ticket, C.byref(st)), "rmq_ticket_stats")
+        rc = _check(self.lib.rmq_ticket_stats(self.h, ticket, C.byref(st)), "rmq_ticket_stats")
+        if rc == A.RMQ_PENDING:
+            return None
         self._keep.pop(ticket, None)
         return {f: int(getattr(st, f)) for f, _ in A.RmqAppendStats._fields_}
 
     def append(self, pidx, lens, payload, payload_off=None) -> tuple[np.ndarray, dict]:
+        """Synchronous append: offsets and stats of the batch. With a replication transport the
+        batch is applied only by a collective rmq_sync, so this raises RMQ_PENDING (keep the
+        ticket: append_async + sync + wait)."""
         t, out = self.append_async(pidx, lens, payload, payload_off)
         stats = self.wait(t)
+        if stats is None:
+            raise EngineError(A.RMQ_PENDING, "rmq_append (transport attached: rmq_sync on every rank applies it)")
         return out, stats
 
     def commit_snapshot(self) -> np.ndarray:

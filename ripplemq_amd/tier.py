@@ -48,6 +48,21 @@ def record_positions(buf: np.ndarray, count: int | None = None) -> np.ndarray:
     return np.asarray(out, np.int64)
 
 
+def whole_records(b: bytes, first: int) -> tuple[int, int]:
+    """(records, bytes) of the longest prefix of ``b`` made of whole FORMAT.md §1 records whose
+    header offsets run first, first + 1, ...: a crash in the middle of a segment write leaves a
+    torn last record (cut short, or zero-filled by the file system), which this excludes."""
+    pos = k = 0
+    while pos + 16 <= len(b):
+        off = int.from_bytes(b[pos:pos + 8], "little")
+        ln = int.from_bytes(b[pos + 8:pos + 12], "little")
+        end = pos + 16 + ((ln + 15) & ~15)
+        if off != first + k or end > len(b):
+            break
+        pos, k = end, k + 1
+    return k, pos
+
+
 class _PartitionFiles:
     """One partition's segment files: record k (offset base + k) at logical byte pos[k] of the
     concatenated files; segment s covers logical bytes [seg_pos[s], seg_pos[s + 1])."""
@@ -62,8 +77,20 @@ class _PartitionFiles:
         self.seg_pos: list[int] = []     # its first logical byte
         names = sorted(int(f[:-len(SEG_SUFFIX)]) for f in os.listdir(self.dir) if f.endswith(SEG_SUFFIX))
         cat, acc = [], 0
-        for first in names:  # reopen: walk the headers of every file, in offset order
-            rp = record_positions(np.fromfile(self._path(first), np.uint8))
+        for i, first in enumerate(names):  # reopen: walk the headers of every file, in offset order
+            data = np.fromfile(self._path(first), np.uint8)
+            n, whole = whole_records(data.tobytes(), first)
+            if whole != data.size:
+                # a torn tail (the spill that wrote it never advanced the durable cursor, so the next
+                # spill fetches those records again): cut the file back to its last whole record
+                if i != len(names) - 1:
+                    raise EngineError(A.RMQ_EINVAL, f"{self.dir}: segment {first} is torn and not the last one")
+                os.truncate(self._path(first), whole)
+                data = data[:whole]
+            if n == 0:
+                os.remove(self._path(first))
+                continue
+            rp = record_positions(data)
             if not self.seg_first:
                 self.base = first
             elif first != self.base + sum(len(x) for x in cat):

@@ -100,3 +100,33 @@ def test_durable_tier_detects_corruption(oracle_mod, tmp_path):
 def test_durable_tier_gpu(tmp_path):
     from ripplemq_amd.engine import Engine
     _flow(Engine, tmp_path, 4096)
+
+
+@pytest.mark.parametrize("cut", ["mid_payload", "zero_filled"])
+def test_durable_tier_reopen_torn_tail(oracle_mod, tmp_path, cut):
+    # a crash in the middle of a segment write (fsync off) leaves a torn last record: the reopened
+    # tier cuts the file back to its last whole record, and the next spill writes the rest again
+    d = PartitionDirectory({TOPIC: 1}, max_consumers=2)
+    cfg = EngineConfig(num_partitions=1, replication_factor=1, segment_bytes=1 << 14, index_interval=256,
+                       max_consumers=2)
+    msgs = [bytes([k]) * (3 * k) for k in range(40)]
+    with oracle_mod.OracleEngine(cfg) as eng:
+        tier = DurableLog(eng, str(tmp_path), [0], d.consumer("__durable_tier"))
+        b = PartitionBroker(d, eng, messages_as_str=False, durable=tier)
+        b.process_append([MessageAppendRequest([m], TOPIC, 0) for m in msgs])
+        assert tier.spill() == 40
+        seg = next((tmp_path / "p000000").glob("*.seg"))
+        raw = seg.read_bytes()
+        whole = len(raw)
+        # the last record (offset 39, 117 B payload: 16 + 128 bytes) torn
+        last = whole - (16 + 128)
+        torn = raw[:last + 40] if cut == "mid_payload" else raw[:last] + bytes(16 + 128)
+        seg.write_bytes(torn)
+        # the engine's durable cursor still says 40: as after a crash, it restarts from the files
+        eng.commit_consumer_offset(np.zeros(1, np.uint32), np.full(1, d.consumer("__durable_tier"), np.uint32),
+                                   np.zeros(1, np.uint64))
+        again = DurableLog(eng, str(tmp_path), [0], d.consumer("__durable_tier"))
+        assert again.end(0) == 39 and seg.stat().st_size == last
+        assert again.spill() == 1 and again.end(0) == 40
+        assert seg.read_bytes() == raw
+        assert [m for _, _, m in again.read(0, 0, 100)] == msgs

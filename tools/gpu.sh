@@ -66,6 +66,12 @@ for step in "$@"; do
       RMQ_STAMPS=gpurun_out/${T}_st.csv RMQ_STAMPS_AT=100 run 200 "${T}_stamped.json" python bench.py --steps 600 --warmup 60 $Q
       python tools/pipe_stamps.py "gpurun_out/${T}_st.csv" > "gpurun_out/${T}_stamps.txt" 2>&1
       for d in 1 16; do RMQ_DEBUG=$d run 200 "${T}_dbg$d.json" python bench.py --steps 400 --warmup 40 $Q; done ;;
+    knob:*)  # knob:VAR=v1,v2,...: steady and 20-step lines per value of one environment knob
+      kv=${step#knob:}; var=${kv%%=*}
+      for val in $(echo "${kv#*=}" | tr , ' '); do
+        env "$var=$val" timeout -k 10 200 python bench.py --steps 600 --warmup 60 $Q > "gpurun_out/${T}_${var}_${val}_600.json" 2>&1 || exit 1
+        env "$var=$val" timeout -k 10 200 python bench.py --steps 20 --warmup 5 $Q > "gpurun_out/${T}_${var}_${val}_20.json" 2>&1 || exit 1
+      done ;;
     *) echo "[gpu.sh] unknown step $step"; exit 2 ;;
   esac
 done
