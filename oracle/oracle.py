@@ -57,7 +57,9 @@ def load() -> C.CDLL:
         "ro_round_region": (C.c_int, [vp, u32, vp, u64, C.POINTER(u64)]),
         "ro_end_round": (None, [vp]),
         "ro_ingest": (C.c_int, [vp, u32, vp, u64, vp]),
-        "ro_apply_acks": (C.c_int, [vp, u32, vp, u32]),
+        "ro_apply_acks": (C.c_int, [vp, u32, vp, u32, u64]),
+        "ro_round_no": (u64, [vp]),
+        "ro_catchup_reserve": (u64, [C.POINTER(A.RmqConfig)]),
         "ro_pair_entries": (u32, [vp, u32, u32]),
         "ro_counters": (None, [vp, vp]),
         "ro_set_segments": (C.c_int, [vp, u32, vp, vp]),
@@ -137,21 +139,32 @@ class OracleEngine:
         return int(self.lib.ro_pair_entries(self.h, src, dst))
 
     def ingest(self, src, region) -> np.ndarray:
+        """FORMAT.md §9 acks, [n][2] {log end offset | status << 62, log end position}."""
         region = np.ascontiguousarray(region, np.uint8)
-        acks = np.zeros(max(self.pair_entries(src, self.cfg.rank), 1), np.uint64)
+        n = self.pair_entries(src, self.cfg.rank)
+        acks = np.zeros((max(n, 1), 2), np.uint64)
         rc = self.lib.ro_ingest(self.h, src, _p(region) if region.size else None, region.size, _p(acks))
         if rc:
             raise EngineError(rc, "oracle ingest")
-        return acks[:self.pair_entries(src, self.cfg.rank)]
+        return acks[:n]
 
-    def apply_acks(self, dst, acks):
-        acks = np.ascontiguousarray(acks, np.uint64)
-        rc = self.lib.ro_apply_acks(self.h, dst, _p(acks) if acks.size else None, len(acks))
+    def apply_acks(self, dst, acks, round_no):
+        acks = np.ascontiguousarray(acks, np.uint64).reshape(-1, 2)
+        rc = self.lib.ro_apply_acks(self.h, dst, _p(acks) if acks.size else None, len(acks), round_no)
         if rc:
             raise EngineError(rc, "oracle apply_acks")
 
+    def round_no(self) -> int:
+        return int(self.lib.ro_round_no(self.h))
+
+    def catchup_reserve(self) -> int:
+        c = self.cfg.to_c()
+        return int(self.lib.ro_catchup_reserve(C.byref(c)))
+
     def counters(self) -> np.ndarray:
-        out = np.zeros(4, np.uint64)
+        """[0] records ingested, [1] entries refused (CRC), [2] refused (log / term / missed),
+        [3] bytes ingested, [4] catch-up entries sent, [5] detached entry plans."""
+        out = np.zeros(6, np.uint64)
         self.lib.ro_counters(self.h, _p(out))
         return out
 

@@ -116,6 +116,11 @@ typedef struct {
   uint64_t seg;            /* ring bytes of this partition (rmq_set_segments) */
   uint8_t* round;          /* records appended in the current replication round, log layout */
   uint64_t round_bytes, round_cap, round_count, round_first;
+  /* leader, per replica slot (FORMAT.md §9 catch-up): expected follower log end before the next
+     round, pending catch-up request {offset, position, round + 1 (0: none)}, last catch-up round */
+  uint64_t nx_off[RMQ_MAX_RF], nx_pos[RMQ_MAX_RF];
+  uint64_t rq_off[RMQ_MAX_RF], rq_pos[RMQ_MAX_RF], rq_r1[RMQ_MAX_RF], cu[RMQ_MAX_RF];
+  uint8_t dirty; /* consumer offsets changed since the last round (the row travels with it) */
 } ro_part;
 
 struct ro_engine {
@@ -126,8 +131,21 @@ struct ro_engine {
   uint64_t* pbytes; /* [P] record bytes of the current batch per partition */
   uint8_t* full;    /* [P] 1: the partition takes no record of the current batch (FORMAT.md §3) */
   uint32_t world;   /* replication ranks (1: none; FORMAT.md §9 rounds when > 1) */
-  uint64_t counters[4]; /* follower: records ingested, refused (CRC), refused (log), bytes */
+  uint64_t counters[6]; /* follower: records ingested, refused (CRC), refused (log), bytes;
+                           leader: catch-up entries, detached entry plans */
+  uint64_t round_no;    /* replication round being formed (FORMAT.md §9 round number) */
 };
+
+/* leader: a partition's catch-up state starts over (placement, leader start: Raft's nextIndex =
+   the leader's last index + 1) */
+static void reset_catchup(ro_part* s) {
+  for (uint32_t r = 0; r < RMQ_MAX_RF; ++r) {
+    s->nx_off[r] = s->leo;
+    s->nx_pos[r] = s->used;
+    s->rq_r1[r] = s->rq_off[r] = s->rq_pos[r] = 0;
+    s->cu[r] = 0;
+  }
+}
 
 static int cfg_ok(const rmq_config* c) {
   if (!c || c->num_partitions == 0 || c->replication_factor == 0 || c->replication_factor > RMQ_MAX_RF)
@@ -263,6 +281,7 @@ int ro_set_replicas(ro_engine* e, uint32_t p, const uint32_t* ranks, uint32_t rf
   for (uint32_t r = 0; r < rf; ++r) s->ranks[r] = ranks[r];
   s->leader_slot = leader_slot;
   s->is_leader = ranks[leader_slot] == e->cfg.rank;
+  reset_catchup(s);
   return RMQ_OK;
 }
 
@@ -281,6 +300,7 @@ static int become_leader_one(ro_engine* e, uint32_t p, uint64_t term) {
   s->term = term;
   s->term_start = s->leo; /* jraft: pendingIndex = lastLogIndex + 1 at leader start */
   for (uint32_t r = 0; r < RF; ++r) s->match[r] = s->ranks[r] == e->cfg.rank ? s->leo : 0;
+  reset_catchup(s);
   return RMQ_OK;
 }
 
@@ -680,8 +700,10 @@ int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t
       st = RMQ_ENOTLEADER;
     else if (consumer[i] >= e->cfg.max_consumers)
       st = RMQ_EINVAL;
-    else
+    else {
       e->parts[pidx[i]].cons[consumer[i]] = offset[i];
+      e->parts[pidx[i]].dirty = 1; /* the row travels with the next replication round (§9) */
+    }
     if (status) status[i] = st;
     if (st && !rc) rc = st;
   }
@@ -804,6 +826,13 @@ int ro_record_pos(ro_engine* e, uint32_t p, uint64_t offset, uint64_t* pos) {
 /* ingest, the leader's ack application. Restated from the format, record by record.          */
 /* ------------------------------------------------------------------------------------------ */
 
+
+#define RO_XMAGIC 0x33514D52u /* "RMQ3" */
+#define RO_HDR 64u
+#define RO_DIR 32u
+#define RO_ACK_REFUSED (1ull << 62)
+#define RO_ACK_LEO_MASK ((1ull << 62) - 1ull)
+
 typedef struct {
   uint64_t key;
   uint32_t slot, p;
@@ -844,67 +873,213 @@ int ro_set_key(ro_engine* e, uint32_t p, uint64_t key) {
   return RMQ_OK;
 }
 
+uint64_t ro_round_no(ro_engine* e) { return e->round_no; }
+
+uint64_t ro_catchup_reserve(const rmq_config* c) {
+  const uint64_t G = c->pipeline_depth ? c->pipeline_depth : 2u;
+  return G * (39ull * c->max_batch_records + c->max_batch_bytes);
+}
+
+/* The leader's plan of one entry for the current round (FORMAT.md §9 catch-up). */
+typedef struct {
+  uint64_t first, pos0;       /* where the entry starts in the leader's log (offset, position) */
+  uint64_t count, bytes;      /* records / record bytes it carries */
+  uint64_t gap_count, gap_bytes; /* of which the catch-up part [first, B) read from the ring */
+  uint64_t nx_off, nx_pos;    /* next after the round */
+  int set_cu, row, detached, catchup;
+} ro_plan;
+
+/* Largest sparse-index entry E[m] (m I <= lim, E[m].pos <= lim, E[m].pos > pos0, m <= mmax):
+   the end of a partial catch-up. Returns 0 if none. */
+static int partial_end(const ro_engine* e, const ro_part* s, uint64_t pos0, uint64_t lim, uint64_t mmax,
+                       uint64_t* off, uint64_t* pos) {
+  const uint64_t I = e->cfg.index_interval;
+  uint64_t m = lim / I;
+  if (m > mmax) m = mmax;
+  for (;; --m) {
+    if (m < s->idx_pos.n && s->idx_pos.v[m] <= lim && s->idx_pos.v[m] > pos0) {
+      *off = s->idx_off.v[m];
+      *pos = s->idx_pos.v[m];
+      return 1;
+    }
+    if (m == 0 || (m - 1) * I < pos0) return 0;
+  }
+}
+
+/* Plans every entry of the pair (me -> dst) for the current round, without changing state. */
+static void plan_pair(const ro_engine* e, const ro_entry* v, uint32_t n, ro_plan* pl) {
+  const uint64_t I = e->cfg.index_interval;
+  uint64_t left = ro_catchup_reserve(&e->cfg);
+  int stop = 0;
+  for (uint32_t k = 0; k < n; ++k) {
+    const ro_part* s = &e->parts[v[k].p];
+    const uint32_t sl = v[k].slot;
+    ro_plan* x = &pl[k];
+    memset(x, 0, sizeof *x);
+    const uint64_t Boff = s->leo - s->round_count, Bpos = s->used - s->round_bytes;
+    uint64_t Foff = s->nx_off[sl], Fpos = s->nx_pos[sl];
+    int req = 0;
+    if (s->rq_r1[sl] && s->rq_r1[sl] - 1 >= s->cu[sl]) {
+      Foff = s->rq_off[sl];
+      Fpos = s->rq_pos[sl];
+      req = 1;
+    }
+    if (Foff >= Boff) {
+      Foff = Boff;
+      Fpos = Bpos;
+    }
+    x->row = s->dirty || req;
+    /* default: the round's records from B (refused by a follower behind B) */
+    x->first = Boff;
+    x->pos0 = Bpos;
+    x->count = s->round_count;
+    x->bytes = s->round_bytes;
+    x->nx_off = s->leo;
+    x->nx_pos = s->used;
+    if (Foff == Boff) {
+      x->set_cu = req;
+      continue;
+    }
+    if (Fpos + s->seg < s->used) { /* the ring no longer holds [F, E) after the round */
+      x->detached = 1;
+      continue;
+    }
+    const uint64_t g = Bpos - Fpos;
+    if (!stop && g <= left) {
+      x->first = Foff;
+      x->pos0 = Fpos;
+      x->gap_count = Boff - Foff;
+      x->gap_bytes = g;
+      x->count += x->gap_count;
+      x->bytes += g;
+      x->set_cu = x->row = x->catchup = 1;
+      left -= g;
+      continue;
+    }
+    uint64_t Xoff = 0, Xpos = 0;
+    if (!stop && partial_end(e, s, Fpos, Fpos + left, Bpos / I, &Xoff, &Xpos)) {
+      x->first = Foff;
+      x->pos0 = Fpos;
+      x->gap_count = x->count = Xoff - Foff;
+      x->gap_bytes = x->bytes = Xpos - Fpos;
+      x->nx_off = Xoff;
+      x->nx_pos = Xpos;
+      x->set_cu = x->row = x->catchup = 1;
+    }
+    stop = 1;
+    left = 0;
+  }
+}
+
 /* The region this engine (leader) sends to rank dst for the current round; *size = its bytes
    (0 when the two ranks share no partition). out may be NULL to ask for the size. */
 int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size) {
-  const uint32_t me = e->cfg.rank;
+  const uint32_t me = e->cfg.rank, C = e->cfg.max_consumers;
   ro_entry* v = NULL;
   const uint32_t n = pair_entries(e, me, dst, &v);
   if (!v) return RMQ_ENOMEM;
-  uint64_t N = 0, B = 0, keysum = 0;
+  ro_plan* pl = (ro_plan*)calloc(n ? n : 1, sizeof(ro_plan));
+  if (!pl) {
+    free(v);
+    return RMQ_ENOMEM;
+  }
+  plan_pair(e, v, n, pl);
+  uint64_t N = 0, B = 0, keysum = 0, M = 0;
   for (uint32_t k = 0; k < n; ++k) {
-    const ro_part* s = &e->parts[v[k].p];
-    N += s->round_count;
-    B += s->round_bytes;
+    N += pl[k].count;
+    B += pl[k].bytes;
+    M += pl[k].row ? 1 : 0;
     keysum += v[k].key * RMQ_MAX_RF + v[k].slot;
   }
-  const uint64_t tab = 32 + 32ull * n, data = tab + ((8 * N + 15) & ~15ull);
-  *size = n ? data + B : 0;
+  const uint64_t tab = RO_HDR + (uint64_t)RO_DIR * n, data = tab + ((8 * N + 15) & ~15ull), rows = data + B;
+  const uint64_t rowb = 16 + 8ull * C;
+  *size = n ? rows + M * rowb : 0;
   if (!out || !n) {
+    free(pl);
     free(v);
     return RMQ_OK;
   }
   if (*size > cap) {
+    free(pl);
     free(v);
     return RMQ_ENOSPC;
   }
-  memset(out, 0, data);
-  const uint32_t h[4] = {0x58514D52u, n, (uint32_t)N, me};
+  memset(out, 0, *size);
+  const uint32_t h[4] = {RO_XMAGIC, n, (uint32_t)N, me};
   memcpy(out, h, 16);
   memcpy(out + 16, &keysum, 8);
   memcpy(out + 24, &data, 8);
-  uint64_t t = 0, b16 = 0;
+  memcpy(out + 32, &rows, 8);
+  const uint32_t mc[2] = {(uint32_t)M, C};
+  memcpy(out + 40, mc, 8);
+  memcpy(out + 48, &e->round_no, 8);
+  uint64_t t = 0, b16 = 0, mrow = 0;
   for (uint32_t k = 0; k < n; ++k) {
     const ro_part* s = &e->parts[v[k].p];
-    uint8_t* d = out + 32 + 32ull * k;
-    const uint32_t cnt = (uint32_t)s->round_count, by16 = (uint32_t)(s->round_bytes / 16);
-    const uint64_t first = s->leo - s->round_count; /* the leader's log end before the round */
+    const ro_plan* x = &pl[k];
+    uint8_t* d = out + RO_HDR + (uint64_t)RO_DIR * k;
+    const uint32_t cnt = (uint32_t)x->count, by16 = (uint32_t)(x->bytes / 16);
     const uint32_t ts = (uint32_t)t, ds = (uint32_t)b16;
     memcpy(d, &cnt, 4);
     memcpy(d + 4, &by16, 4);
-    memcpy(d + 8, &first, 8);
+    memcpy(d + 8, &x->first, 8);
     memcpy(d + 16, &ts, 4);
     memcpy(d + 20, &ds, 4);
     memcpy(d + 24, &s->term, 8);
+    uint8_t* dd = out + data + 16 * b16;
+    /* the catch-up part from the leader's ring, then the round's records (if carried) */
+    if (x->gap_bytes) ring_read(s->seg, ring_of(e, s->leader_slot, v[k].p), x->pos0, dd, x->gap_bytes);
+    if (x->bytes > x->gap_bytes) memcpy(dd + x->gap_bytes, s->round, s->round_bytes);
     uint64_t rel = 0;
-    for (uint64_t r = 0; r < s->round_count; ++r) { /* record table: {entry, record position / 16} */
+    for (uint64_t r = 0; r < x->count; ++r) { /* record table: {entry, record position / 16} */
       uint32_t len;
-      memcpy(&len, s->round + rel + 8, 4);
+      memcpy(&len, dd + rel + 8, 4);
       const uint64_t slot = (uint64_t)k | ((uint64_t)(ds + rel / 16) << 32);
       memcpy(out + tab + 8 * (t + r), &slot, 8);
       rel += rec_size(len);
     }
-    memcpy(out + data + 16 * b16, s->round, s->round_bytes);
+    if (x->row) {
+      uint8_t* rw = out + rows + rowb * mrow++;
+      memcpy(rw, &k, 4);
+      memcpy(rw + 16, s->cons, 8ull * C);
+    }
     t += cnt;
     b16 += by16;
   }
+  free(pl);
   free(v);
   return RMQ_OK;
 }
 
-/* Closes the round: the leader forgets the records it kept for it. */
+/* Closes the round: the leader applies its plan's per-entry state to every destination, forgets
+   the records it kept for the round and marks the consumer-offset rows sent. */
 void ro_end_round(ro_engine* e) {
-  for (uint32_t p = 0; p < e->cfg.num_partitions; ++p) e->parts[p].round_bytes = e->parts[p].round_count = 0;
+  const uint32_t me = e->cfg.rank;
+  for (uint32_t d = 0; d < e->world; ++d) {
+    if (d == me) continue;
+    ro_entry* v = NULL;
+    const uint32_t n = pair_entries(e, me, d, &v);
+    ro_plan* pl = v ? (ro_plan*)calloc(n ? n : 1, sizeof(ro_plan)) : NULL;
+    if (pl) {
+      plan_pair(e, v, n, pl);
+      for (uint32_t k = 0; k < n; ++k) {
+        ro_part* s = &e->parts[v[k].p];
+        const uint32_t sl = v[k].slot;
+        s->nx_off[sl] = pl[k].nx_off;
+        s->nx_pos[sl] = pl[k].nx_pos;
+        if (pl[k].set_cu) s->cu[sl] = e->round_no;
+        e->counters[4] += pl[k].catchup ? 1u : 0u;
+        e->counters[5] += pl[k].detached ? 1u : 0u;
+      }
+    }
+    free(pl);
+    free(v);
+  }
+  for (uint32_t p = 0; p < e->cfg.num_partitions; ++p) {
+    e->parts[p].round_bytes = e->parts[p].round_count = 0;
+    e->parts[p].dirty = 0;
+  }
+  e->round_no++;
 }
 
 /* Follower: truncate partition p's log to offset t (start_off <= t < leo): the records from t on
@@ -917,40 +1092,48 @@ static void truncate_log(ro_engine* e, ro_part* s, uint64_t t) {
   s->idx_off.n = s->idx_pos.n = s->used / I + 1;
 }
 
-/* Follower: ingest the region leader `src` sent (FORMAT.md §9); acks[k] = this engine's log end of
-   entry k afterwards when the entry continues it (0 otherwise, and for a refused entry). size 0:
-   the leader sent nothing this round (acks = log ends, nothing changes). */
+static void ack_of(const ro_part* s, int refused, uint64_t* ack) {
+  ack[0] = s->leo | (refused ? RO_ACK_REFUSED : 0ull);
+  ack[1] = s->used;
+}
+
+/* Follower: ingest the region leader `src` sent (FORMAT.md §9); acks[2k..2k+1] = this engine's
+   log end after the round for entry k with its status. size 0: the round from src is missed (every
+   entry refused). */
 int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks) {
-  const uint32_t me = e->cfg.rank;
+  const uint32_t me = e->cfg.rank, C = e->cfg.max_consumers;
   const uint64_t I = e->cfg.index_interval;
   ro_entry* v = NULL;
   const uint32_t n = pair_entries(e, src, me, &v);
   if (!v) return RMQ_ENOMEM;
   if (!n || !size) {
-    for (uint32_t k = 0; k < n; ++k) acks[k] = e->parts[v[k].p].leo;
+    for (uint32_t k = 0; k < n; ++k) {
+      ack_of(&e->parts[v[k].p], 1, acks + 2 * k);
+      e->counters[2]++;
+    }
     free(v);
-    return size ? RMQ_EINVAL : RMQ_OK;
+    return n && size ? RMQ_EINVAL : RMQ_OK;
   }
-  uint32_t h[4];
-  uint64_t keysum, data, want = 0;
+  uint32_t h[4], mc[2];
+  uint64_t keysum, data, rows, want = 0;
   memcpy(h, region, 16);
   memcpy(&keysum, region + 16, 8);
   memcpy(&data, region + 24, 8);
+  memcpy(&rows, region + 32, 8);
+  memcpy(mc, region + 40, 8);
   for (uint32_t k = 0; k < n; ++k) want += v[k].key * RMQ_MAX_RF + v[k].slot;
-  if (size < 32 || h[0] != 0x58514D52u || h[1] != n || h[3] != src || keysum != want) {
+  if (size < RO_HDR || h[0] != RO_XMAGIC || h[1] != n || h[3] != src || keysum != want || mc[1] != C) {
     free(v);
     return RMQ_EINVAL;
   }
-  const uint64_t tab = 32 + 32ull * n;
+  const uint64_t tab = RO_HDR + (uint64_t)RO_DIR * n, rowb = 16 + 8ull * C;
   /* pass 1: the verdict of every entry against the state every entry of a partition sees (the log
      end it continues, decided once by the owner: two local slots, the first keeps the state) */
   int* okv = (int*)malloc((size_t)n * sizeof(int));
   uint64_t* base = (uint64_t*)malloc((size_t)n * 2 * sizeof(uint64_t));
-  int* stv = (int*)malloc((size_t)n * sizeof(int));
-  if (!okv || !base || !stv) {
+  if (!okv || !base) {
     free(okv);
     free(base);
-    free(stv);
     free(v);
     return RMQ_ENOMEM;
   }
@@ -959,7 +1142,7 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
   for (uint32_t k = 0; k < n; ++k) {
     ro_part* s = &e->parts[v[k].p];
     const int owner = k == 0 || v[k - 1].p != v[k].p;
-    const uint8_t* d = region + 32 + 32ull * k;
+    const uint8_t* d = region + RO_HDR + (uint64_t)RO_DIR * k;
     uint32_t cnt, by16, ts, ds;
     uint64_t first, term;
     memcpy(&cnt, d, 4);
@@ -979,8 +1162,7 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     }
     base[2 * k] = leo;
     base[2 * k + 1] = used;
-    stv[k] = stale;
-    int ok = !stale && (!cnt || first == leo);
+    int ok = !stale && first == leo;
     uint64_t rel = 0;
     for (uint32_t r = 0; r < cnt && ok; ++r) {
       uint64_t slot, off;
@@ -996,17 +1178,18 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
       rel += rec_size(len);
     }
     okv[k] = ok;
-    if (!ok) e->counters[!stale && (!cnt || first == leo) ? 1 : 2]++;
+    if (!ok) e->counters[!stale && first == leo ? 1 : 2]++;
   }
   /* a refusal of either slot of a partition is a refusal of both */
   for (uint32_t k = 0; k < n; ++k)
     for (uint32_t q = k + 1; q < n && v[q].p == v[k].p; ++q)
       if (!okv[k] || !okv[q]) okv[k] = okv[q] = 0;
   /* pass 2: apply the accepted entries */
+  uint64_t mrow = 0;
   for (uint32_t k = 0; k < n; ++k) {
     ro_part* s = &e->parts[v[k].p];
     const int owner = k == 0 || v[k - 1].p != v[k].p;
-    const uint8_t* d = region + 32 + 32ull * k;
+    const uint8_t* d = region + RO_HDR + (uint64_t)RO_DIR * k;
     uint32_t cnt, by16, ds;
     uint64_t first, term;
     memcpy(&cnt, d, 4);
@@ -1016,65 +1199,73 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     memcpy(&term, d + 24, 8);
     leo = base[2 * k];
     used = base[2 * k + 1];
+    /* this entry's consumer-offset row, if any (rows ascend by entry) */
+    const uint8_t* row = NULL;
+    while (mrow < mc[0]) {
+      uint32_t rk;
+      memcpy(&rk, region + rows + rowb * mrow, 4);
+      if (rk > k) break;
+      if (rk == k) row = region + rows + rowb * mrow + 16;
+      ++mrow;
+    }
     if (!okv[k]) {
-      acks[k] = 0;
+      ack_of(s, 1, acks + 2 * k);
       continue;
     }
     if (owner) {
       if (term > s->term) s->term = term;
       if (leo < s->leo) truncate_log(e, s, leo);
+      if (row) memcpy(s->cons, row, 8ull * C);
     }
-    if (!cnt) {
-      acks[k] = first == leo ? leo : 0;
-      continue;
-    }
-    const uint8_t* bytes = region + data + 16ull * ds;
-    ring_write(e->parts[v[k].p].seg, ring_of(e, v[k].slot, v[k].p), used, bytes, 16ull * by16);
-    if (owner) {
-      uint64_t rel = 0;
-      for (uint32_t r = 0; r < cnt; ++r) {
-        uint32_t len;
-        memcpy(&len, bytes + rel + 8, 4);
-        const uint64_t pos = used + rel, rs = rec_size(len);
-        for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
-          if (vec_push(&s->idx_off, first + r + 1) || vec_push(&s->idx_pos, pos + rs)) {
+    if (cnt) {
+      const uint8_t* bytes = region + data + 16ull * ds;
+      ring_write(s->seg, ring_of(e, v[k].slot, v[k].p), used, bytes, 16ull * by16);
+      if (owner) {
+        uint64_t rel = 0;
+        for (uint32_t r = 0; r < cnt; ++r) {
+          uint32_t len;
+          memcpy(&len, bytes + rel + 8, 4);
+          const uint64_t pos = used + rel, rs = rec_size(len);
+          for (uint64_t m = pos / I + 1; m * I <= pos + rs; ++m)
+            if (vec_push(&s->idx_off, first + r + 1) || vec_push(&s->idx_pos, pos + rs)) {
+              free(okv);
+              free(base);
+              free(v);
+              return RMQ_ENOMEM;
+            }
+          if (vec_push(&s->rec_pos, pos)) {
             free(okv);
             free(base);
-            free(stv);
             free(v);
             return RMQ_ENOMEM;
           }
-        if (vec_push(&s->rec_pos, pos)) {
-          free(okv);
-          free(base);
-          free(stv);
-          free(v);
-          return RMQ_ENOMEM;
+          rel += rs;
         }
-        rel += rs;
+        s->leo = first + cnt;
+        s->used = used + 16ull * by16;
+        if (s->used - s->start_pos > s->seg) { /* retention once per round (FORMAT.md §4 rule) */
+          const uint64_t m = (s->used - s->seg + I - 1) / I;
+          s->start_off = s->idx_off.v[m];
+          s->start_pos = s->idx_pos.v[m];
+        }
+        e->counters[3] += 16ull * by16;
       }
-      s->leo = first + cnt;
-      s->used = used + 16ull * by16;
-      if (s->used - s->start_pos > s->seg) { /* retention once per round (FORMAT.md §4 rule) */
-        const uint64_t m = (s->used - s->seg + I - 1) / I;
-        s->start_off = s->idx_off.v[m];
-        s->start_pos = s->idx_pos.v[m];
-      }
-      e->counters[3] += 16ull * by16;
+      e->counters[0] += cnt; /* records written into this replica slot */
     }
-    e->counters[0] += cnt;
-    acks[k] = first + cnt;
+    /* the owner's state after the round: both slots ack it */
+    acks[2 * k] = first + cnt;
+    acks[2 * k + 1] = used + 16ull * by16;
   }
   free(okv);
   free(base);
-  free(stv);
   free(v);
   return RMQ_OK;
 }
 
-/* Leader: the acks follower `dst` returned for this engine's entries (match = max(match,
-   min(ack, log end))), then the quorum commit rule of every partition they name. */
-int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks) {
+/* Leader: the acks follower `dst` returned for round `round` (FORMAT.md §9): an accepted entry
+   moves match = max(match, min(ack, log end)), a refused one leaves a catch-up request; then the
+   quorum commit rule of every partition they name. */
+int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks, uint64_t round) {
   ro_entry* v = NULL;
   const uint32_t n = pair_entries(e, e->cfg.rank, dst, &v);
   if (!v) return RMQ_ENOMEM;
@@ -1084,8 +1275,16 @@ int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_a
   }
   for (uint32_t k = 0; k < n; ++k) {
     ro_part* s = &e->parts[v[k].p];
-    const uint64_t a = acks[k] < s->leo ? acks[k] : s->leo;
-    if (a > s->match[v[k].slot]) s->match[v[k].slot] = a;
+    const uint32_t sl = v[k].slot;
+    const uint64_t a = acks[2 * k] & RO_ACK_LEO_MASK;
+    if (acks[2 * k] & RO_ACK_REFUSED) {
+      s->rq_off[sl] = a;
+      s->rq_pos[sl] = acks[2 * k + 1];
+      s->rq_r1[sl] = round + 1;
+      continue;
+    }
+    const uint64_t m = a < s->leo ? a : s->leo;
+    if (m > s->match[sl]) s->match[sl] = m;
   }
   for (uint32_t k = 0; k < n; ++k) commit_eval(e, &e->parts[v[k].p]);
   free(v);

@@ -73,16 +73,27 @@ int ro_read_consumer_offsets(ro_engine* e, uint32_t pidx, uint64_t* out);
 /* Logical position of record `offset` (dense, for cross-checking the sparse index). */
 int ro_record_pos(ro_engine* e, uint32_t pidx, uint64_t offset, uint64_t* pos);
 
-/* Replication rounds (FORMAT.md §9): world > 1 makes the leader keep each round's
-   records; the caller closes a round after the batches the engine groups into one launch group. */
+/* Replication rounds (FORMAT.md §9 v3): world > 1 makes the leader keep each round's
+   records; the caller closes a round after the batches the engine groups into one launch group.
+   ro_round_region plans without changing state (it may be called twice per destination: size, then
+   bytes); ro_end_round applies the plan's per-entry state (catch-up next / round, consumer-offset
+   rows sent) and starts the next round. Acks are 2 words per entry: {log end offset | status << 62,
+   log end position}; ro_apply_acks takes the round number they answer (ro_round_no before the
+   round's ro_end_round). */
 int ro_set_world(ro_engine* e, uint32_t world);
 int ro_set_key(ro_engine* e, uint32_t pidx, uint64_t key);
 int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size);
 void ro_end_round(ro_engine* e);
+uint64_t ro_round_no(ro_engine* e);
 int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks);
-int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks);
+int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks, uint64_t round);
 uint32_t ro_pair_entries(ro_engine* e, uint32_t src, uint32_t dst);
-void ro_counters(ro_engine* e, uint64_t* out /* [4] */);
+/* [0] records ingested, [1] entries refused (CRC), [2] refused (log / term / missed round),
+   [3] bytes ingested, [4] catch-up entries sent, [5] detached entry plans (gap beyond the ring) */
+void ro_counters(ro_engine* e, uint64_t* out /* [6] */);
+/* Catch-up reserve per destination (FORMAT.md §9): pipeline_depth x (39 max_batch_records +
+   max_batch_bytes) bytes. */
+uint64_t ro_catchup_reserve(const rmq_config* cfg);
 
 #ifdef __cplusplus
 }

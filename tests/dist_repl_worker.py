@@ -4,7 +4,7 @@ Launched by tests/test_distributed.py as a plain subprocess per rank (RANK/WORLD
 the env, MASTER_ADDR=127.0.0.1). Each rank runs the oracle engine of the partitions it hosts
 (CPU stand-in for its GPU engine) and does what the engine's exchange stream does per round, over
 gloo instead of RCCL: swap {region bytes} with every peer, send/recv the regions, ingest what it
-received, send/recv the acks (follower log ends) and apply them. Rank 0 writes every rank's final
+received, send/recv the acks (FORMAT.md §9 v3: follower log end and status) and apply them. Rank 0 writes every rank's final
 partition states and ring digests as JSON for the parent test.
 """
 import json
@@ -65,17 +65,18 @@ def main():
         for k in range(rounds):
             for b in batches[k * group:(k + 1) * group]:
                 eng.append(b.pidx, b.lens, b.payload)
+            rnd = eng.round_no()
             regions = [eng.round_region(q) if q != rank else np.zeros(0, np.uint8) for q in range(world)]
             eng.end_round()
             got = exchange(rank, world, regions)
             acks = [np.zeros(0, np.uint8)] * world
             for q in range(world):
                 if q != rank and got[q].size:
-                    acks[q] = eng.ingest(q, got[q]).view(np.uint8)
+                    acks[q] = np.ascontiguousarray(eng.ingest(q, got[q])).reshape(-1).view(np.uint8)
             back = exchange(rank, world, acks)
             for q in range(world):
                 if q != rank and back[q].size:
-                    eng.apply_acks(q, back[q].view(np.uint64))
+                    eng.apply_acks(q, back[q].view(np.uint64).reshape(-1, 2), rnd)
         n = len(view.gp)
         states = [eng.state(p) for p in range(n)]
         rings = [[crc32c(eng.read_segment(s, p).tobytes()) for s in range(3)] for p in range(n)]

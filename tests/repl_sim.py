@@ -33,11 +33,14 @@ def rank_batches(spec: StreamSpec, rank: int, rounds: int, group: int):
 
 
 def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None, drop=()):
-    """Regions of every leader to every follower, ingested there; acks back to the leaders.
-    corrupt=(src, dst, byte): flip one byte of that region; skip=(src, dst): drop that region and
-    its acks (the follower misses the round); drop: leaders whose round sends empty regions
-    (rmq_fault_drop_rounds: followers ingest nothing and ack their log ends)."""
+    """Regions of every leader to every follower, ingested there; acks back to the leaders (FORMAT.md
+    §9 v3: a refused ack leaves a catch-up request for the next round's plan).
+    corrupt=(src, dst, byte): flip one byte of that region (byte < 0: from the end of its data
+    section, i.e. a payload byte of its last record); skip=(src, dst): drop that region and its
+    acks; drop: leaders whose round sends no region (rmq_fault_drop_rounds: their followers miss
+    the round and refuse every entry of it)."""
     W = len(oras)
+    rnd = [o.round_no() for o in oras]
     regions = [[oras[s].round_region(d) if d != s else None for d in range(W)] for s in range(W)]
     for s in drop:
         regions[s] = [None if d == s else np.zeros(0, np.uint8) for d in range(W)]
@@ -45,17 +48,19 @@ def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None, dr
         o.end_round()
     for s in range(W):
         for d in range(W):
-            if s in drop and d != s:
-                oras[s].apply_acks(d, oras[d].ingest(s, regions[s][d]))
+            if d == s or (skip and (s, d) == tuple(skip)):
                 continue
-            if d == s or regions[s][d].size == 0 or (skip and (s, d) == tuple(skip)):
+            if regions[s][d].size == 0 and s not in drop:
                 continue
             reg = regions[s][d]
             if corrupt and (s, d) == tuple(corrupt[:2]):
                 reg = reg.copy()
-                reg[corrupt[2]] ^= 0x5A
+                at = corrupt[2]
+                if at < 0:
+                    at += int(reg[32:40].view(np.uint64)[0])  # rows_off: end of the data section
+                reg[at] ^= 0x5A
             acks = oras[d].ingest(s, reg)
-            oras[s].apply_acks(d, acks)
+            oras[s].apply_acks(d, acks, rnd[s])
     return regions if keep_regions else None
 
 

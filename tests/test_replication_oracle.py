@@ -152,3 +152,172 @@ def test_leader_change_truncates_follower(oracle_mod):
     finally:
         for o in oras:
             o.close()
+
+
+def _follower_views(views, oras, g, gp):
+    """[(rank, local pidx, slot)] of the followers of global partition gp led by rank g."""
+    W = len(oras)
+    rf = views[0].ranks.shape[1]
+    out = []
+    for slot, r in enumerate(replica_ranks(g, gp, W, rf)):
+        if r != g:
+            out.append((r, local_of(views, r, gp), slot))
+    return out
+
+
+def test_crc_refusal_then_catch_up(oracle_mod):
+    # FORMAT.md §9 v3: a corrupted record makes the follower refuse that entry (its log does not
+    # move), the refused ack becomes a catch-up request, and the next round's entry for that
+    # follower starts at its log end and re-sends the gap from the leader's ring
+    world, ppr = 3, 4
+    views, oras = build(oracle_mod, world, ppr)
+    spec = StreamSpec(ppr, 200, "uniform", size=(1, 100), config_index=54)
+    try:
+        def rnd(k, **kw):
+            for r in range(world):
+                b = rank_batches(spec, r, 4, 1)[k]
+                oras[r].append(b.pidx, b.lens, b.payload)
+            return exchange_round(oras, keep_regions=True, **kw)
+
+        rnd(0)
+        before = [oras[1].state(p) for p in range(len(views[1].gp))]
+        regions = rnd(1, corrupt=(0, 1, -5))
+        assert oras[1].counters()[1] == 1  # one entry refused for its CRC
+        after = [oras[1].state(p) for p in range(len(views[1].gp))]
+        moved = [p for p in range(len(views[1].gp)) if after[p] != before[p]]
+        unmoved = [p for p in range(len(views[1].gp)) if after[p] == before[p]]
+        assert unmoved and moved  # the refused entry's partition stayed, the others advanced
+        c0 = oras[0].counters()
+        rnd(2)  # the plan of round 2 sends the gap first
+        assert oras[0].counters()[4] == c0[4] + 1  # one catch-up entry
+        check_followers(views, oras, ppr, 3)
+        assert regions[0][1].size > 0
+    finally:
+        for o in oras:
+            o.close()
+
+
+def test_missed_round_then_catch_up(oracle_mod):
+    world, ppr = 3, 4
+    views, oras = build(oracle_mod, world, ppr)
+    spec = StreamSpec(ppr, 300, "zipf", size=(0, 150), config_index=55)
+    try:
+        for k in range(4):
+            for r in range(world):
+                b = rank_batches(spec, r, 4, 1)[k]
+                oras[r].append(b.pidx, b.lens, b.payload)
+            exchange_round(oras, drop=(0,) if k == 1 else ())
+            if k == 1:
+                # every follower of rank 0 missed the round; rank 0's partitions have not committed it
+                assert oras[1].counters()[2] > 0 and oras[2].counters()[2] > 0
+                assert all(oras[0].state(p)["commit"] < oras[0].state(p)["log_end_offset"]
+                           for p in range(ppr))
+        check_followers(views, oras, ppr, 3)
+        assert oras[0].counters()[4] >= 2  # catch-up entries to both followers
+    finally:
+        for o in oras:
+            o.close()
+
+
+def test_partial_catch_up_within_the_reserve(oracle_mod):
+    # a gap larger than the destination's catch-up reserve is re-sent in pieces that end on sparse
+    # index entries, one per round, until the follower holds the leader's log again
+    world, ppr = 3, 2
+    base = EngineConfig(num_partitions=1, replication_factor=3, segment_bytes=1 << 17, index_interval=256,
+                        max_batch_records=64, max_batch_bytes=2048, pipeline_depth=1)
+    views, oras = build(oracle_mod, world, ppr, base=base)
+    assert oras[0].catchup_reserve() == 39 * 64 + 2048
+    big = StreamSpec(ppr, 400, "uniform", size=(80, 120), config_index=56)
+    small = StreamSpec(ppr, 4, "uniform", size=(10, 20), config_index=57)
+    try:
+        for r in range(world):
+            b = rank_batches(big, r, 1, 1)[0]
+            oras[r].append(b.pidx, b.lens, b.payload)
+        exchange_round(oras, drop=(0,))
+        rounds = 0
+        while rounds < 40:
+            for r in range(world):
+                b = rank_batches(small, r, 40, 1)[rounds]
+                oras[r].append(b.pidx, b.lens, b.payload)
+            exchange_round(oras)
+            rounds += 1
+            lead = [oras[0].state(p) for p in range(ppr)]
+            if all(s["commit"] == s["log_end_offset"] for s in lead):
+                break
+        assert 4 <= rounds < 40, rounds  # ~50 KB of gap per follower at < 4.5 KB per round
+        check_followers(views, oras, ppr, 3)
+    finally:
+        for o in oras:
+            o.close()
+
+
+def test_gap_beyond_the_ring_detaches(oracle_mod):
+    # a follower whose log end the leader's ring no longer holds cannot be caught up from the ring
+    world, ppr = 3, 1
+    base = EngineConfig(num_partitions=1, replication_factor=3, segment_bytes=1 << 13, index_interval=256)
+    views, oras = build(oracle_mod, world, ppr, base=base)
+    spec = StreamSpec(ppr, 10, "uniform", size=(100, 100), config_index=58)  # 1.3 KB per round
+    try:
+        for k in range(12):
+            for r in range(world):
+                b = rank_batches(spec, r, 12, 1)[k]
+                oras[r].append(b.pidx, b.lens, b.payload)
+            # round 0 is missed by both followers; rank 1 loses rounds 1..8 as well (no region, no
+            # ack): by then its log end lies more than the 8 KB ring behind
+            exchange_round(oras, drop=(0,) if k == 0 else (), skip=(0, 1) if 1 <= k <= 8 else None)
+        assert oras[0].counters()[5] > 0  # the plan toward rank 1 found its gap beyond the ring
+        gp = int(views[0].gp[0])
+        (r1, p1, _), (r2, p2, _) = _follower_views(views, oras, 0, gp)
+        lead = oras[0].state(0)
+        # the other follower caught up and keeps the quorum; the detached one stays behind
+        assert lead["commit"] == lead["log_end_offset"]
+        far = oras[1].state(p1) if r1 == 1 else oras[1].state(p2)
+        assert far["log_end_offset"] < lead["log_end_offset"]
+    finally:
+        for o in oras:
+            o.close()
+
+
+def test_consumer_offsets_replicate_and_survive_leader_change(oracle_mod):
+    # ConsumerOffsetUpdateRequestProcessor.java:59-60 applies an offset commit through Raft on every
+    # replica; after leadership moves, the new leader serves the same offsets
+    from repl_sim import moved_leadership
+    world, ppr = 3, 4
+    views, oras = build(oracle_mod, world, ppr)
+    spec = StreamSpec(ppr, 300, "uniform", size=(1, 60), config_index=59)
+    C = oras[0].cfg.max_consumers
+    try:
+        for k in range(2):
+            for r in range(world):
+                b = rank_batches(spec, r, 3, 1)[k]
+                oras[r].append(b.pidx, b.lens, b.payload)
+            if k == 1:
+                for r in range(world):  # every leader commits offsets of its partitions
+                    led = np.arange(views[r].led, dtype=np.uint32)
+                    rc, st = oras[r].commit_consumer_offset(np.repeat(led, 2), np.tile([0, 3], len(led)),
+                                                            np.arange(2 * len(led), dtype=np.uint64) * 7 + r)
+                    assert rc == 0 and not st.any()
+            exchange_round(oras)
+        for g in range(world):
+            for gp in range(g * ppr, (g + 1) * ppr):
+                want = oras[g].consumer_offsets(local_of(views, g, gp))
+                assert want.any()
+                for r, p, _ in _follower_views(views, oras, g, gp):
+                    assert np.array_equal(oras[r].consumer_offsets(p), want), (g, gp, r)
+        # leadership of rank 0's partitions moves to replica slot 1, term 2
+        new = moved_leadership(views)
+        for r in range(world):
+            place(oras[r], new[r])
+        for p in range(ppr):
+            gp = int(views[0].gp[p])
+            r1 = int(views[0].ranks[p][1])
+            q = local_of(views, r1, gp)
+            oras[r1].become_leader(q, 2)
+            want = oras[0].consumer_offsets(p)
+            assert np.array_equal(oras[r1].consumer_offsets(q), want)
+            _, res, _, _ = oras[r1].fetch([q], [3], [5])
+            assert int(res["start_offset"][0]) == int(want[3]) and res["status"][0] == 0
+        assert C >= 4
+    finally:
+        for o in oras:
+            o.close()
