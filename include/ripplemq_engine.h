@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 2u
+#define RMQ_ABI_VERSION 3u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -166,9 +166,12 @@ typedef struct rmq_repl_stats {
   uint64_t bytes_sent;         /* round regions sent (FORMAT.md §9), all peers */
   uint64_t bytes_received;
   uint64_t records_ingested;   /* follower records whose CRC32C and log position checked out */
-  uint64_t refused_crc;        /* follower entries refused: CRC32C differs from the record header */
-  uint64_t refused_log;        /* follower entries refused: do not continue the follower's log */
+  uint64_t refused_crc;        /* follower entries refused: a record's CRC32C / header / bounds is wrong */
+  uint64_t refused_log;        /* follower entries refused: do not continue the follower's log, stale
+                                  leader term, or the round missed (no region from the leader) */
   uint64_t bytes_ingested;
+  uint64_t catchup_entries;    /* leader: entries that re-sent a follower's gap (FORMAT.md §9 catch-up) */
+  uint64_t detached_plans;     /* leader: entry plans whose follower lies beyond the ring (needs a re-sync) */
 } rmq_repl_stats;
 
 typedef struct rmq_engine rmq_engine;
@@ -266,6 +269,11 @@ int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uin
    appended after the call send empty regions, as if the leader failed before replicating them
    (its own log keeps the records; followers neither see nor ack them). Not collective. */
 int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n);
+/* Fault injection (tests): the next round this engine sends to rank dst has the byte at `at` of its
+   region XORed with 0x5A (at < 0: counted back from the end of the region's data section, i.e. a
+   payload byte of its last record), as a link or memory corruption would; the follower refuses the
+   entry it hits and the leader's catch-up re-sends it (FORMAT.md §9). Not collective. */
+int rmq_fault_corrupt(rmq_engine* e, uint32_t dst, int64_t at);
 
 /* ---- read-back (tests, tools) ---- */
 int rmq_get_partition_state(rmq_engine* e, uint32_t pidx, rmq_partition_state* out);

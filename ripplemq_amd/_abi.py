@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 2
+RMQ_ABI_VERSION = 3
 RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
@@ -86,7 +86,7 @@ class RmqReplStats(C.Structure):
     _fields_ = [
         ("world", u32), ("rank", u32), ("out_entries", u32), ("in_entries", u32), ("rounds", u64),
         ("bytes_sent", u64), ("bytes_received", u64), ("records_ingested", u64), ("refused_crc", u64),
-        ("refused_log", u64), ("bytes_ingested", u64),
+        ("refused_log", u64), ("bytes_ingested", u64), ("catchup_entries", u64), ("detached_plans", u64),
     ]
 
 
@@ -138,6 +138,7 @@ _SIGS = {
     "rmq_replication_stats": (C.c_int, [vp, C.POINTER(RmqReplStats)]),
     "rmq_read_outbox": (C.c_int, [vp, u32, vp, u64, C.POINTER(u64)]),
     "rmq_fault_drop_rounds": (C.c_int, [vp, u32]),
+    "rmq_fault_corrupt": (C.c_int, [vp, u32, C.c_int64]),
 }
 
 _lib = None

@@ -37,7 +37,9 @@ __global__ void become_leader_kernel(DevState st, u32 only) {
 
 __global__ void consumer_apply_kernel(ConsumerCommitArgs a) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < a.n) a.st.cons[(u64)a.pidx[i] * a.st.C + a.consumer[i]] = a.offset[i];
+  if (i >= a.n) return;
+  a.st.cons[(u64)a.pidx[i] * a.st.C + a.consumer[i]] = a.offset[i];
+  a.st.cdirty[a.pidx[i]] = 1u;  // the row travels with the next replication round (FORMAT.md §9)
 }
 
 static inline dim3 grid_for(u32 n, u32 b) { return dim3((n + b - 1) / b ? (n + b - 1) / b : 1); }

@@ -421,7 +421,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, e->d_crc,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, e->d_crc,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
@@ -602,6 +602,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.ring, P));
   CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
+  CREATE_TRY(dalloc(&s.cdirty, P));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
   CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));
@@ -745,7 +746,10 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   HIP_TRY(hipMemcpy(e->st.term + lo, &e->term[lo], (size_t)(hi - lo) * 8, hipMemcpyHostToDevice));
   launch_become_leader(e->st, pidx, e->main_s);
   HIP_TRY(hipGetLastError());
-  return drain(e);
+  rc = drain(e);
+  // Raft's leader start: nextIndex of every follower = the leader's last index + 1
+  if (!rc && e->repl) rc = reset_catchup(e);
+  return rc;
 }
 
 int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* seg) {
@@ -1398,7 +1402,7 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   const Replication* r = e->repl;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(r->xchg_s));
-  uint64_t c[4];
+  uint64_t c[6];
   HIP_TRY(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost));
   out->world = r->world;
   out->rank = r->rank;
@@ -1411,6 +1415,8 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   out->refused_crc = c[1];
   out->refused_log = c[2];
   out->bytes_ingested = c[3];
+  out->catchup_entries = c[4];
+  out->detached_plans = c[5];
   return RMQ_OK;
 }
 
@@ -1420,6 +1426,15 @@ int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n) {
   if (!e->repl) return RMQ_EINVAL;
   e->repl->drop_from = e->last_ticket + 1;
   e->repl->drop_n = n;
+  return RMQ_OK;
+}
+
+int rmq_fault_corrupt(rmq_engine* e, uint32_t dst, int64_t at) {
+  if (!e) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (!e->repl || dst >= e->repl->world || dst == e->repl->rank) return RMQ_EINVAL;
+  e->repl->flip[dst] = true;
+  e->repl->flip_at[dst] = at;
   return RMQ_OK;
 }
 
@@ -1433,8 +1448,7 @@ int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uin
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(r->xchg_s));
   const XchgSet& x = r->sets[r->last_set];
-  uint64_t off = 0;
-  for (uint32_t q = 0; q < dst; ++q) off += q == r->rank ? 0 : x.h_sizes[2 * q];
+  const uint64_t off = (uint64_t)dst * r->dcap;  // region d at d * dcap of the outbox
   const uint64_t n = dst == r->rank ? 0 : x.h_sizes[2 * dst];
   *size = n;
   if (!out) return RMQ_OK;

@@ -143,16 +143,19 @@ struct GroupFlight {
 // Replica-log rounds over a transport (replication.cpp, FORMAT.md §9): per scratch set, the
 // group's outbox and inbox and the exchange's events.
 struct XchgSet {
-  uint8_t* outbox = nullptr;
-  uint8_t* inbox = nullptr;
+  uint8_t* outbox = nullptr;   // region for destination d at d * dcap
+  uint8_t* inbox = nullptr;    // received regions packed in source order
   XEntry* xe = nullptr;        // [n_out]
-  uint64_t* sizes = nullptr;   // device [2 * world]: send sizes (plan), receive sizes (exchange)
+  XCatch* xc = nullptr;        // [n_out] catch-up list (plan -> stage-3 catch-up waves)
+  uint32_t* xc_n = nullptr;    // [2]
+  uint64_t* sizes = nullptr;   // device [4 * world]: send sizes (plan), receive sizes (exchange)
   uint64_t* h_sizes = nullptr; // pinned copy
-  uint64_t* ackout = nullptr;  // [n_in]
-  uint64_t* ackin = nullptr;   // [n_out]
+  uint64_t* ackout = nullptr;  // [n_in][2]
+  uint64_t* ackin = nullptr;   // [n_out][2]
   uint32_t* count = nullptr;   // stage-2 arrival counter
   hipEvent_t ev_s2 = nullptr, ev_s3 = nullptr, ev_sz = nullptr, ev_x = nullptr;
   uint64_t applied_launch = 0; // launch that ran the group's stage 3
+  uint64_t round = 0;          // the group's round number (FORMAT.md §9)
 };
 
 struct Replication {
@@ -170,9 +173,23 @@ struct Replication {
   uint32_t* d_xi_p = nullptr;
   uint32_t* d_xi_slot = nullptr;
   uint32_t* d_xi_start = nullptr;
+  uint32_t* d_xo_slot = nullptr;  // [n_out]
   uint32_t* d_bad = nullptr;     // [n_in]
+  uint32_t* d_acc = nullptr;     // [n_in]
   uint64_t* d_base = nullptr;    // [n_in][2] IngestArgs::base
-  uint64_t* d_counters = nullptr;  // [4] (IngestArgs)
+  uint32_t* d_items = nullptr;   // [items_cap][2] follower copy work items
+  uint32_t* d_nitems = nullptr;  // [1]
+  uint64_t* d_counters = nullptr;  // [6]: follower [0..4) (IngestArgs), leader [4..6) (XPlanArgs)
+  // leader catch-up state per out entry (FORMAT.md §9 v3)
+  uint64_t* d_xnext = nullptr;   // [n_out][2]
+  uint64_t* d_xreq = nullptr;    // [n_out][4]
+  uint64_t* d_xcu = nullptr;     // [n_out]
+  XDecision* d_xdec = nullptr;   // [n_out]
+  uint32_t* d_dflag = nullptr;   // [world]
+  uint64_t dcap = 0;             // outbox bytes per destination
+  uint64_t reserve = 0;          // catch-up bytes per destination
+  uint64_t items_cap = 0;
+  uint64_t planned = 0;          // rounds planned (the next plan's round number)
   uint64_t out_cap = 0, in_cap = 0;
   XchgSet sets[kSets];
   std::deque<uint32_t> sized;    // sets whose size exchange is posted, data exchange not yet
@@ -183,6 +200,9 @@ struct Replication {
   // ticket is at least `drop_from` send empty regions
   uint64_t drop_from = 0;
   uint32_t drop_n = 0;
+  // rmq_fault_corrupt: the next round to destination q flips the byte at flip_at[q]
+  bool flip[kMaxWorld] = {};
+  int64_t flip_at[kMaxWorld] = {};
 };
 
 }  // namespace rmq
@@ -348,5 +368,6 @@ void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const Gro
 int repl_before_launch(rmq_engine* e, PipeArgs& a);
 int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s3);
 int repl_drain(rmq_engine* e);
+int reset_catchup(rmq_engine* e);
 
 }  // namespace rmq

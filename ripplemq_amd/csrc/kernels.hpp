@@ -27,33 +27,80 @@ constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-b
 constexpr uint32_t kMaxRF = 8;
 constexpr uint32_t kMaxWorld = 16;       // ranks of a replication transport
 constexpr uint32_t kMaxRemote = 4;       // remote replica slots per partition with a transport (RF <= 5)
-constexpr uint32_t kXMagic = 0x58514D52u;  // "RMQX": replica-log round region (FORMAT.md §9)
-constexpr uint32_t kRegionHdr = 32;      // region header bytes
+constexpr uint32_t kXMagic = 0x33514D52u;  // "RMQ3": replica-log round region v3 (FORMAT.md §9)
+constexpr uint32_t kRegionHdr = 64;      // region header bytes
 constexpr uint32_t kDirEntry = 32;       // directory entry bytes
+constexpr uint64_t kAckRefused = 1ull << 62;  // ack status bit (FORMAT.md §9 acks)
+constexpr uint64_t kAckLeoMask = kAckRefused - 1ull;
+constexpr uint64_t kNoRound = ~0ull;     // XEntry::data_abs: the entry carries no round records
 
 struct CrcConsts;
 
 // Where one out entry (a led partition's remote replica slot) of a group lands in the group's
 // outbox (FORMAT.md §9), written by stage 2's plan, read by stage 3. 32 bytes.
 struct XEntry {
-  uint64_t data_abs;      // outbox byte offset of the entry's first record
-  uint64_t tab_abs;       // outbox byte offset of the entry's first record-table slot
+  uint64_t data_abs;      // outbox byte offset of the entry's first ROUND record (after a catch-up
+                          //   gap), or kNoRound: the entry carries none (partial catch-up)
+  uint64_t tab_abs;       // outbox byte offset of that record's record-table slot
   uint64_t dir_abs;       // outbox byte offset of the entry's directory entry
   uint32_t k;             // entry index inside its destination's list
-  uint32_t data_start16;  // entry's first record inside the region's data section, / 16
+  uint32_t data_start16;  // that record's position inside the region's data section, / 16
 };
 
+// A catch-up entry of a round (FORMAT.md §9): the gap [first, first + count) of the leader's log,
+// bytes [pos, pos + bytes), copied from the leader's ring into the outbox by the stage-3 launch's
+// catch-up waves, one item per sparse-index interval the gap touches. 64 bytes.
+struct XCatch {
+  uint64_t pos;           // leader log position of the gap's first record (the follower's log end)
+  uint64_t first;         // its offset
+  uint64_t bytes;         // gap bytes
+  uint64_t data_abs;      // outbox byte offset of the entry's first record
+  uint64_t tab_abs;       // outbox byte offset of its record-table slot
+  uint32_t k;             // entry index inside its destination's list
+  uint32_t data_start16;  // the entry's first record inside the region's data section, / 16
+  uint32_t p;             // led partition
+  uint32_t items0;        // first copy item of the entry (prefix over the list)
+  uint64_t pad;
+};
+
+// Per out entry, what the stage-2 workers of a group decide before the plan lays out the outbox:
+// the follower log end F the entry would start at, the gap bytes before the round's records, kind.
+struct XDecision {
+  uint64_t f_off, f_pos;  // F (the leader's log end B before the round when not gapped)
+  uint64_t gap;           // B.pos - F.pos for a gapped entry, 0 otherwise
+  uint64_t r_off, r_pos;  // a catch-up request that arrived with this launch's acks (kDecNewReq)
+  uint32_t flags;         // kDec*
+  uint32_t pad;
+};
+constexpr uint32_t kDecReq = 1u, kDecRow = 2u, kDecDetached = 4u, kDecGapped = 8u, kDecNewReq = 16u;
+
 // Leader side of a replication round: the layout plan of one group's outbox (stage 2 of the group,
-// computed by the last stage-2 workgroup of the launch).
+// computed by the last stage-2 workgroup of the launch) and the catch-up state it advances.
 struct XPlanArgs {
   const uint32_t* xo_p;      // [n_out] led partition of each out entry, grouped by destination
+  const uint32_t* xo_slot;   // [n_out] its replica slot
   const uint32_t* xo_start;  // [world + 1]
   const uint64_t* keysum;    // [world] FORMAT.md §9 key sum of each destination's entry list
-  uint32_t world, rank, n_out, pad;
+  uint32_t world, rank, n_out, C;
   uint32_t* count;           // arrival counter of the launch's stage-2 workgroups (reset by the plan)
   XEntry* xe;                // [n_out]
   uint8_t* outbox;
   uint64_t* sizes;           // [world][2] {region bytes, records} per destination (0: nothing to send)
+  // catch-up and consumer-offset rows (FORMAT.md §9 v3)
+  uint64_t round;            // this group's round number
+  uint64_t reserve;          // catch-up bytes per destination
+  uint64_t* xnext;           // [n_out][2] leader's expectation of the follower log end {offset, pos}
+  uint64_t* xreq;            // [n_out][4] pending catch-up request {offset, pos, round + 1 (0 none), 0}
+  uint64_t* xcu;             // [n_out] round of the last catch-up plan
+  XDecision* xdec;           // [n_out] stage-2 workers -> plan
+  uint32_t* dflag;           // [world] kDecRow | kDecGapped of any entry to that destination
+  const uint64_t* ackin;     // acks applied in this launch, [n_out][2], or null
+  uint64_t acks_round;       // the round they answer
+  uint32_t* dirty;           // [P] consumer offsets changed since the last round (cleared by the plan)
+  XCatch* xc;                // [n_out] catch-up list of the group
+  uint32_t* xc_n;            // [2] {catch-up entries, copy items}
+  uint64_t* counters;        // [2] leader: catch-up entries planned, detached entry plans
+  uint64_t dcap;             // outbox bytes per destination: region d at d * dcap
 };
 
 // Per-partition device state (SoA, [P] unless noted). Owned by the engine.
@@ -75,6 +122,7 @@ struct DevState {
   uint8_t* logs;         // [RF][pool] replica regions; partition p's ring at RingRef.base in each
   uint64_t* ring;        // [P] ring descriptor: byte offset in the pool | log2(ring bytes) (bits 0..5)
   uint64_t* cons;        // [P][C] consumer offsets
+  uint32_t* cdirty;      // [P] consumer offsets changed since the last replication round (FORMAT §9)
   uint64_t rstride;      // bytes per replica region (the pool)
   uint32_t P, RF, C;
   uint32_t icap_mul;     // index entries per interval of ring (2 * group + 2)
@@ -172,7 +220,12 @@ struct PipeArgs {
   const uint32_t* outidx;  // [P][RF] out entry of (partition, slot), ~0: local or no entry
   const XEntry* xe3;       // stage 3's group: entry placement
   uint8_t* outbox3;        // stage 3's group: its outbox
-  const uint64_t* ackin;   // acks of an earlier group, by out entry (partition threads), or null
+  const uint64_t* ackin;   // acks of an earlier group, by out entry [n_out][2] (partition threads), or null
+  uint64_t acks_round;     // the round they answer
+  uint64_t* xreq;          // catch-up requests (partition threads write them when no plan runs)
+  const XCatch* xc3;       // stage 3's group: its catch-up list and counts (catch-up waves)
+  const uint32_t* xc3_n;
+  uint32_t wgc;            // catch-up workgroups (last along blockIdx.x)
   const CrcConsts* crc;
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
   uint64_t launch_seq;
@@ -221,20 +274,27 @@ struct IngestArgs {
   const uint32_t* xi_p;      // [n_in] local partition of each in entry, grouped by source
   const uint32_t* xi_slot;   // [n_in] local replica slot
   const uint32_t* xi_start;  // [world + 1]
-  uint32_t world, rank, n_in, pad;
-  uint32_t* bad;             // [n_in] entry refused this round (cleared by the finish kernel)
+  uint32_t world, rank, n_in, C;
+  uint32_t* bad;             // [n_in] entry refused this round: bit 0 CRC, 1 log mismatch, 2 stale
+                             //   term, 3 missed round (prepare sets it, verify adds to it)
+  uint32_t* acc;             // [n_in] 1: accepted (finish -> copy)
   uint64_t* base;            // [n_in][2] {log end offset, log end position} the entry continues:
                              // the follower's, or the leader's first offset after a truncation
-  uint64_t* ackout;          // [n_in] follower log end after the round
+  uint64_t* ackout;          // [n_in][2] follower log end after the round | status (FORMAT.md §9)
+  uint32_t* items;           // [cap][2] copy work items {entry, chunk of kCopyChunk bytes} (prepare)
+  uint32_t* n_items;         // [1] items allocated this round (prepare adds, the host clears)
   const CrcConsts* crc;
   uint64_t* counters;        // [4] records ingested, entries refused (CRC), refused (log mismatch), bytes
 };
+constexpr uint64_t kCopyChunk = 64ull << 10;  // follower copy: region bytes per workgroup
 
 // Acks of one round applied outside the pipeline (drain): thread per partition.
 struct AckApplyArgs {
   DevState st;
   const uint32_t* outidx;
-  const uint64_t* ackin;
+  const uint64_t* ackin;     // [n_out][2]
+  uint64_t* xreq;            // refused acks become catch-up requests
+  uint64_t acks_round;
 };
 
 // One partition's ring moving to a new block of the pool (rmq_set_segments): the retained log
@@ -256,11 +316,12 @@ void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev6);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
-void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s);
+void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
 // chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))
 void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s);
 void launch_ack_apply(const AckApplyArgs& a, hipStream_t s);
+void launch_flip(uint8_t* region, uint64_t size, int64_t at, hipStream_t s);  // rmq_fault_corrupt
 
 }  // namespace rmq
 

@@ -29,17 +29,28 @@ __device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u
   return (N > commit && N > term_start) ? N : commit;
 }
 
-// Remote replica acks of one replication round (FORMAT.md §9) into the partition's matchIndex row:
-// match = max(match, min(ack, log end)) for every slot with an out entry. True if a slot moved.
+// Remote replica acks of one replication round (FORMAT.md §9 v3, [n_out][2] {log end | status << 62,
+// log end position}) into the partition's matchIndex row: an accepted ack moves match = max(match,
+// min(ack, log end)) for its slot; a refused one becomes a catch-up request {offset, position,
+// round + 1} when xreq is given (no plan reads these acks itself). True if a slot moved.
 __device__ __forceinline__ bool apply_acks(const DevState& st, u32 p, const u32* outidx, const u64* ackin, u64 leo,
-                                           u64 (&row)[kMaxRF]) {
+                                           u64 (&row)[kMaxRF], u64* xreq, u64 acks_round) {
   bool moved = false;
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) {
     if (r >= st.RF) continue;
     const u32 e = outidx[(u64)p * st.RF + r];
     if (e == ~0u) continue;
-    const u64 a = ackin[e] < leo ? ackin[e] : leo;
+    const u64 a0 = ackin[2 * e];
+    if (a0 & kAckRefused) {
+      if (xreq) {
+        xreq[4 * e] = a0 & kAckLeoMask;
+        xreq[4 * e + 1] = ackin[2 * e + 1];
+        xreq[4 * e + 2] = acks_round + 1ull;
+      }
+      continue;
+    }
+    const u64 a = a0 < leo ? a0 : leo;
     if (a > row[r]) {
       row[r] = a;
       st.match[(u64)p * st.RF + r] = a;

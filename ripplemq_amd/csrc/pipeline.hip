@@ -392,74 +392,293 @@ __device__ __forceinline__ u64 block_incl_scan_u64(u64 v, u64* s_w, u64* total) 
   return pre + inc;
 }
 
-// The group's outbox layout (FORMAT.md §9), one workgroup: per destination d a region
-//   [header 32 B][directory n_d x 32 B][record table N_d x 8 B, padded to 16][records]
-// with the entries (led partition, remote slot) in the destination's list order; per entry its
-// record count / bytes and where stage 3 puts its records, table slots and first offset.
-__device__ void stage2_plan(const PipeArgs& A) {
+// Catch-up decision of out entry e of the group being planned (FORMAT.md §9 v3), by the stage-2
+// thread of its partition's column once the group's totals of p are known (`tot`). B = the leader's
+// log end before the round: the state this launch's stage 3 reads (after the group two before)
+// plus the totals of the group it applies (the group before), E = B + the round.
+__device__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
   const XPlanArgs& X = A.xp2;
-  const u64* const totals = A.s2.totals;
-  const u32 tid = threadIdx.x;
-  __shared__ u64 s_tot[kMaxWorld];   // {records << 40 | bytes / 16} per destination
-  __shared__ u64 s_base[kMaxWorld];  // region start
-  __shared__ u64 s_w[kPW];
-  if (tid < kMaxWorld) s_tot[tid] = 0ull;
-  __syncthreads();
-  for (u32 d = 0; d < X.world; ++d)
-    for (u32 e = X.xo_start[d] + tid; e < X.xo_start[d + 1]; e += kPT) atomicAdd(&s_tot[d], load_sc1(&totals[X.xo_p[e]]));
-  __syncthreads();
-  if (tid == 0) {
-    u64 start = 0;
-    for (u32 d = 0; d < X.world; ++d) {
-      const u64 n = X.xo_start[d + 1] - X.xo_start[d], N = s_tot[d] >> 40, b16 = s_tot[d] & kLow40;
-      const u64 size = n ? kRegionHdr + kDirEntry * n + ((8ull * N + 15ull) & ~15ull) + 16ull * b16 : 0ull;
-      s_base[d] = start;
-      X.sizes[2 * d] = size;    // the exchange swaps {region bytes, records} per peer
-      X.sizes[2 * d + 1] = n ? N : 0ull;
-      start += size;
+  const DevState& st = A.st;
+  const u64 t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
+  const u64 Boff = A.cur.leo[p] + (t3 >> 40), Bpos = A.cur.used[p] + 16ull * (t3 & kLow40);
+  const u64 Epos = Bpos + 16ull * (tot & kLow40);
+  const u64 S = 1ull << (st.ring[p] & 63ull);
+  XDecision d;
+  d.f_off = X.xnext[2 * e];
+  d.f_pos = X.xnext[2 * e + 1];
+  d.gap = 0;
+  d.r_off = d.r_pos = 0;
+  d.flags = 0;
+  d.pad = 0;
+  const u64 cu = X.xcu[e];
+  u64 r1 = X.xreq[4 * e + 2], roff = X.xreq[4 * e], rpos = X.xreq[4 * e + 1];
+  if (X.ackin && (X.ackin[2 * e] & kAckRefused)) {  // a refusal among this launch's acks
+    r1 = X.acks_round + 1ull;
+    roff = X.ackin[2 * e] & kAckLeoMask;
+    rpos = X.ackin[2 * e + 1];
+    if (X.acks_round >= cu) {
+      d.flags |= kDecNewReq;
+      d.r_off = roff;
+      d.r_pos = rpos;
     }
   }
+  if (r1 && r1 - 1ull >= cu) {
+    d.f_off = roff;
+    d.f_pos = rpos;
+    d.flags |= kDecReq | kDecRow;
+  }
+  if (st.cdirty[p]) d.flags |= kDecRow;
+  if (d.f_off >= Boff) {
+    d.f_off = Boff;
+    d.f_pos = Bpos;
+  } else if (d.f_pos + S < Epos) {
+    d.flags |= kDecDetached;  // the ring no longer holds [F, E) after the round
+  } else {
+    d.flags |= kDecGapped;
+    d.gap = Bpos - d.f_pos;
+  }
+  store_sc1(&X.xdec[e].f_off, d.f_off);
+  store_sc1(&X.xdec[e].f_pos, d.f_pos);
+  store_sc1(&X.xdec[e].gap, d.gap);
+  store_sc1(&X.xdec[e].r_off, d.r_off);
+  store_sc1(&X.xdec[e].r_pos, d.r_pos);
+  store_sc1(reinterpret_cast<u64*>(&X.xdec[e].flags), (u64)d.flags);
+  if (d.flags & (kDecRow | kDecGapped)) {
+    u32 q = 0;
+    for (u32 k = 1; k < X.world; ++k) q += e >= X.xo_start[k] ? 1u : 0u;
+    __hip_atomic_fetch_or(&X.dflag[q], d.flags & (kDecRow | kDecGapped), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// End of a partial catch-up (FORMAT.md §9): the largest sparse-index entry E[m] with
+// F.pos < E[m].pos <= lim among the entries complete now (m I <= used); 0 if none.
+__device__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
+  const RingRef rg = ring_ref(st, p);
+  const u32 ilog = st.interval_log2;
+  u64 lo = (fpos >> ilog) + 1ull, hi = min(lim, used) >> ilog;  // candidates m in [lo, hi]
+  bool found = false;
+  while (lo <= hi) {  // E[m].pos rises with m
+    const u64 mid = lo + (hi - lo) / 2;
+    const u64* ie = st.index + (rg.ibase + mid % rg.icap) * 2;
+    const u64 ep = ie[1];
+    if (ep <= lim) {
+      if (ep > fpos) {
+        *xoff = ie[0];
+        *xpos = ep;
+        found = true;
+      }
+      lo = mid + 1;
+    } else {
+      if (!mid) break;
+      hi = mid - 1;
+    }
+  }
+  return found;
+}
+
+// The group's outbox layout (FORMAT.md §9 v3), one workgroup: destination d's region sits at
+// d * dcap of the outbox (the host sends [d * dcap, d * dcap + size)):
+//   [header 64 B][directory n_d x 32 B][record table N_d x 8 B, padded to 16][records][rows]
+// with the entries (led partition, remote slot) in the destination's list order. Per entry: the
+// catch-up verdict (gap granted in list order out of the destination's reserve), its records
+// (the gap, then the round's own), where stage 3 puts the round's records and table slots, the
+// catch-up list for the stage-3 launch's copy waves, the consumer-offset row, the next expected
+// follower log end.
+__device__ void stage2_plan(const PipeArgs& A) {
+  const XPlanArgs& X = A.xp2;
+  const DevState& st = A.st;
+  const u64* const totals = A.s2.totals;
+  const u32 tid = threadIdx.x, C = X.C;
+  const u64 dcap = X.dcap;
+  __shared__ u64 s_w[kPW];
+  __shared__ u64 s_cu[2];  // catch-up entries and items before this destination
+  if (tid == 0) s_cu[0] = s_cu[1] = 0ull;
   __syncthreads();
-  for (u32 d = 0; d < X.world; ++d) {
-    const u32 e0 = X.xo_start[d], e1 = X.xo_start[d + 1];
-    if (e0 == e1) continue;
-    const u64 n = e1 - e0, N = s_tot[d] >> 40;
-    const u64 base = s_base[d], tab = base + kRegionHdr + kDirEntry * n, data = tab + ((8ull * N + 15ull) & ~15ull);
+  for (u32 dd = 0; dd < X.world; ++dd) {
+    const u32 e0 = X.xo_start[dd], e1 = X.xo_start[dd + 1];
+    if (e0 == e1) {
+      if (tid == 0) X.sizes[2 * dd] = X.sizes[2 * dd + 1] = 0ull;
+      continue;
+    }
+    const u32 df = __hip_atomic_load(&X.dflag[dd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u64 n = e1 - e0, base = (u64)dd * dcap;
+    const u64 tab = base + kRegionHdr + kDirEntry * n;
+    // pass 1: record counts (for the table size) need the grants, which need the gap prefix
+    u64 gap_run = 0, run_a = 0, run_b = 0;
+    for (u32 c0 = e0; c0 < e1; c0 += kPT) {
+      const u32 e = c0 + tid;
+      const bool in = e < e1;
+      u64 tot = 0, f_off = 0, f_pos = 0, gap = 0;
+      u32 fl = 0;
+      u32 p = 0;
+      if (in) {
+        p = X.xo_p[e];
+        tot = load_sc1(&totals[p]);
+        f_off = load_sc1(&X.xdec[e].f_off);
+        f_pos = load_sc1(&X.xdec[e].f_pos);
+        gap = load_sc1(&X.xdec[e].gap);
+        fl = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
+      }
+      u64 gex = 0;
+      if (df & kDecGapped) {
+        u64 gt;
+        gex = gap_run + block_incl_scan_u64(gap, s_w, &gt) - gap;
+        gap_run += gt;
+      }
+      // the entry's verdict: normal / full catch-up / partial / stopped (round records only)
+      const u64 rcnt = tot >> 40, rb16 = tot & kLow40;
+      u64 cnt = rcnt, b16 = rb16, gcnt = 0, gb16 = 0, first = f_off;
+      u64 nx_off = 0, nx_pos = 0;
+      bool with_round = true, set_cu = false, cu_entry = false;
+      const u64 t3 = (in && A.g3.nb) ? A.s3.totals[p] : 0ull;
+      const u64 Boff = in ? A.cur.leo[p] + (t3 >> 40) : 0ull;
+      const u64 Bpos = in ? A.cur.used[p] + 16ull * (t3 & kLow40) : 0ull;
+      if (in) {
+        nx_off = Boff + rcnt;
+        nx_pos = Bpos + 16ull * rb16;
+        set_cu = (fl & kDecReq) && !(fl & (kDecGapped | kDecDetached));
+        if (fl & kDecGapped) {
+          if (gex + gap <= X.reserve) {
+            gcnt = Boff - f_off;
+            gb16 = gap >> 4;
+            cnt += gcnt;
+            b16 += gb16;
+            set_cu = cu_entry = true;
+          } else if (gex <= X.reserve) {  // the first entry past the reserve: a prefix of its gap
+            u64 xo = 0, xp = 0;
+            if (partial_end(st, p, f_pos, f_pos + (X.reserve - gex), A.cur.used[p], &xo, &xp)) {
+              gcnt = cnt = xo - f_off;
+              gb16 = b16 = (xp - f_pos) >> 4;
+              with_round = false;
+              nx_off = xo;
+              nx_pos = xp;
+              set_cu = cu_entry = true;
+            }
+          }
+        }
+        if (!cu_entry) first = Boff;  // the round's records from B (refused by a follower behind B)
+      }
+      const bool row = in && (((fl & kDecRow) != 0u) || cu_entry);
+      // scan A: table slots and data pieces before the entry
+      const u64 va = in ? (cnt << 40) | b16 : 0ull;
+      u64 ta;
+      const u64 exa = run_a + block_incl_scan_u64(va, s_w, &ta) - va;
+      run_a += ta;
+      // scan B: rows, catch-up entries and their copy items before the entry
+      u64 items = 0;
+      if (cu_entry) {
+        const u32 ilog = st.interval_log2;
+        items = ((f_pos + 16ull * gb16 - 1ull) >> ilog) - (f_pos >> ilog) + 1ull;
+      }
+      const u64 vb = (row ? 1ull : 0ull) | (cu_entry ? 1ull << 20 : 0ull) | (items << 40);
+      u64 exb = 0;
+      if (df) {
+        u64 tb;
+        exb = run_b + block_incl_scan_u64(vb, s_w, &tb) - vb;
+        run_b += tb;
+      }
+      if (in) {
+        const u32 k = e - e0;
+        const u64 t_ex = exa >> 40, d_ex = exa & kLow40;
+        const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
+        uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
+        de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
+        const u64 term = st.term[p];
+        de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
+        XEntry xe;
+        xe.data_abs = kNoRound;
+        xe.tab_abs = 0;
+        if (with_round) {
+          xe.data_abs = 0;  // data section offset, fixed below once the table size is known
+          xe.tab_abs = tab + 8ull * (t_ex + gcnt);
+        }
+        xe.dir_abs = dir;
+        xe.k = k;
+        xe.data_start16 = (u32)(d_ex + gb16);
+        X.xe[e] = xe;
+        if (cu_entry) {
+          const u32 ci = (u32)(s_cu[0] + ((exb >> 20) & 0xFFFFFull));
+          XCatch xc;
+          xc.pos = f_pos;
+          xc.first = f_off;
+          xc.bytes = 16ull * gb16;
+          xc.data_abs = 0;  // fixed below
+          xc.tab_abs = tab + 8ull * t_ex;
+          xc.k = k;
+          xc.data_start16 = (u32)d_ex;
+          xc.p = p;
+          xc.items0 = (u32)(s_cu[1] + (exb >> 40));
+          xc.pad = 0;
+          X.xc[ci] = xc;
+          atomicAdd((unsigned long long*)&X.counters[0], 1ull);
+        }
+        if (fl & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
+        // catch-up state (FORMAT.md §9): next expected follower log end, last catch-up round; a
+        // request that came with this launch's acks and was not served stays pending
+        X.xnext[2 * e] = nx_off;
+        X.xnext[2 * e + 1] = nx_pos;
+        if (set_cu) X.xcu[e] = X.round;
+        if ((fl & kDecNewReq) && !set_cu) {
+          X.xreq[4 * e] = load_sc1(&X.xdec[e].r_off);
+          X.xreq[4 * e + 1] = load_sc1(&X.xdec[e].r_pos);
+          X.xreq[4 * e + 2] = X.acks_round + 1ull;
+        }
+      }
+      // (row entries and the data section offset need the region totals: pass 2)
+      if (in) X.xdec[e].pad = row ? 1u + (u32)(exb & 0xFFFFFull) : 0u;  // row index + 1
+      __syncthreads();
+    }
+    const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
+    const u64 data = tab + ((8ull * N + 15ull) & ~15ull), rows = data + 16ull * B16;
+    const u64 rowb = 16ull + 8ull * C;
+    // pass 2: data offsets, rows
+    for (u32 e = e0 + tid; e < e1; e += kPT) {
+      XEntry& xe = X.xe[e];
+      if (xe.data_abs != kNoRound) xe.data_abs = data + 16ull * xe.data_start16;
+      const u32 ri = X.xdec[e].pad;
+      if (ri) {
+        const u32 p = X.xo_p[e];
+        uint8_t* rw = X.outbox + rows + rowb * (ri - 1u);
+        *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, 0u, 0u);
+        for (u32 c = 0; c < C; ++c) reinterpret_cast<u64*>(rw + 16)[c] = st.cons[(u64)p * C + c];
+      }
+    }
     if (tid == 0) {
       u32* h = reinterpret_cast<u32*>(X.outbox + base);
       h[0] = kXMagic;
       h[1] = (u32)n;
       h[2] = (u32)N;
       h[3] = X.rank;
-      *reinterpret_cast<u64*>(h + 4) = X.keysum[d];
+      *reinterpret_cast<u64*>(h + 4) = X.keysum[dd];
       *reinterpret_cast<u64*>(h + 6) = data - base;
+      *reinterpret_cast<u64*>(h + 8) = rows - base;
+      h[10] = (u32)M;
+      h[11] = C;
+      *reinterpret_cast<u64*>(h + 12) = X.round;
+      *reinterpret_cast<u64*>(h + 14) = 0ull;
       if (N & 1ull) *reinterpret_cast<u64*>(X.outbox + tab + 8ull * N) = 0ull;  // table padding
+      X.sizes[2 * dd] = rows + rowb * M - base;  // the exchange swaps {region bytes, records} per peer
+      X.sizes[2 * dd + 1] = N;
+      X.dflag[dd] = 0u;
+      s_cu[0] += (run_b >> 20) & 0xFFFFFull;
+      s_cu[1] += run_b >> 40;
     }
-    u64 run = 0;
-    for (u32 c0 = e0; c0 < e1; c0 += kPT) {
-      const u32 e = c0 + tid;
-      const u64 v = e < e1 ? load_sc1(&totals[X.xo_p[e]]) : 0ull;
-      u64 tot;
-      const u64 ex = run + block_incl_scan_u64(v, s_w, &tot) - v;
-      run += tot;
-      if (e < e1) {
-        const u32 k = e - e0;
-        const u64 cnt_ex = ex >> 40, b16_ex = ex & kLow40;
-        const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
-        uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
-        de[0] = make_uint4((u32)(v >> 40), (u32)(v & kLow40), 0u, 0u);  // count, bytes / 16, first offset (stage 3)
-        de[1] = make_uint4((u32)cnt_ex, (u32)b16_ex, 0u, 0u);           // table start, data start / 16, reserved
-        XEntry xe;
-        xe.data_abs = data + 16ull * b16_ex;
-        xe.tab_abs = tab + 8ull * cnt_ex;
-        xe.dir_abs = dir;
-        xe.k = k;
-        xe.data_start16 = (u32)b16_ex;
-        X.xe[e] = xe;
-      }
+    __syncthreads();
+    // catch-up list entries of this destination: their data start
+    for (u32 i = tid; i < (u32)((run_b >> 20) & 0xFFFFFull); i += kPT) {
+      XCatch& xc = X.xc[(u32)s_cu[0] - (u32)((run_b >> 20) & 0xFFFFFull) + i];
+      xc.data_abs = data + 16ull * xc.data_start16;
     }
+    __syncthreads();
   }
-  if (tid == 0) __hip_atomic_store(X.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next used six launches later
+  __syncthreads();
+  // consumer-offset rows travel once per change: clear the flags of every planned partition
+  for (u32 e = tid; e < X.n_out; e += kPT) st.cdirty[X.xo_p[e]] = 0u;
+  if (tid == 0) {
+    X.xc_n[0] = (u32)s_cu[0];
+    X.xc_n[1] = (u32)s_cu[1];
+    __hip_atomic_store(X.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next used six launches later
+  }
 }
 
 // s_ex: kMaxTiles words of the launch's dynamic LDS (static arrays would add to every role's LDS)
@@ -571,6 +790,13 @@ __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
       if (s == 0) x.bcum[(u64)j * P + p] = carry;
     }
     if (s == 0) store_sc1(&x.totals[p], carry);  // sc1: the plan below reads it in this launch
+    if (A.xp2.n_out && s == 0 && A.st.is_leader[p]) {  // catch-up verdicts of p's out entries
+      const u32 lm = A.st.local_mask[p];
+      for (u32 r = 0; r < A.st.RF; ++r) {
+        const u32 e = ((lm >> r) & 1u) ? ~0u : A.outidx[(u64)p * A.st.RF + r];
+        if (e != ~0u) plan_decide(A, p, e, carry);
+      }
+    }
   }
   if (A.xp2.n_out) {
     // replication transport: the last stage-2 workgroup to finish lays out the group's outbox
@@ -855,7 +1081,7 @@ __device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
       for (u32 r = 0; r < st.RF && nx < kMaxRemote; ++r) {
         if ((lm >> r) & 1u) continue;
         const u32 oe = A.outidx[(u64)p * st.RF + r];
-        if (oe == ~0u) continue;
+        if (oe == ~0u || A.xe3[oe].data_abs == kNoRound) continue;
         xdst[nx++] = reinterpret_cast<u64>(A.outbox3 + A.xe3[oe].data_abs + 16ull * rel16);
       }
     }
@@ -912,6 +1138,7 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
           const u32 e = A.outidx[(u64)p * RF + r];
           if (e == ~0u) continue;
           const XEntry x = A.xe3[e];
+          if (x.data_abs == kNoRound) continue;  // a partial catch-up: the round's records wait
           W.xdst[w][r32][nx++] = reinterpret_cast<u64>(A.outbox3 + x.data_abs + rel);
           *reinterpret_cast<u64*>(A.outbox3 + x.tab_abs + 8ull * rk) =
               (u64)x.k | ((u64)(x.data_start16 + (u32)(rel >> 4)) << 32);
@@ -1032,18 +1259,6 @@ __device__ void partition_apply(const PipeArgs& A, u32 p) {
   // counted by stages 1/2, ranks being per partition, but never applied; the host keeps both state
   // sets equal for it); stage 2 leaves rejected (batch, partition) cells out of totals
   if (!st.is_leader[p]) return;
-  // replication transport: every directory entry of the partition in the group's outbox names the
-  // log end the round continues (this leader's, before the group) and the leader's term (FORMAT §9)
-  if (A.outbox3 && A.g3.nb) {
-    const u32 lmx = st.local_mask[p];
-    for (u32 r = 0; r < st.RF; ++r) {
-      const u32 e = (lmx >> r) & 1u ? ~0u : A.outidx[(u64)p * st.RF + r];
-      if (e == ~0u) continue;
-      u64* d = reinterpret_cast<u64*>(A.outbox3 + A.xe3[e].dir_abs);
-      d[1] = A.cur.leo[p];
-      d[3] = st.term[p];
-    }
-  }
   u64 tc = 0, leo;
   if (A.g3.nb) {
     const u64 tot = A.s3.totals[p];
@@ -1069,7 +1284,7 @@ __device__ void partition_apply(const PipeArgs& A, u32 p) {
       }
   }
   // followers' acks of an earlier group (replication transport, FORMAT.md §9)
-  if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row);
+  if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row, A.xreq, A.acks_round);
   if (moved) {
     const u64 c = quorum_commit(row, RF, st.commit[p], st.term_start[p]);
     st.commit[p] = c;
@@ -1110,6 +1325,61 @@ __device__ void partition_retention(const PipeArgs& A, u32 p) {
   }
 }
 
+// Catch-up waves of the stage-3 launch (FORMAT.md §9 v3, replication transport): the gaps the
+// plan granted, copied from this leader's ring into the outbox with their record-table slots. One
+// item = one sparse-index interval [m I, (m + 1) I) of one gap: its first record is the gap's own
+// (the first item) or E[m], the first record starting at or after m I; the wave copies the
+// interval's bytes (a 16-byte piece per lane, 1 KiB per step) and walks the headers of the records
+// that start in it. Round h-1's records are complete (the previous launch) and round h's stores
+// into the ring land past the gap's end minus the ring size (the plan's condition), so nothing
+// this reads changes under it.
+__device__ void stage3_catchup(const PipeArgs& A, u32 wg) {
+  const u32 items = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n + 1));
+  const u32 ncu = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n));
+  if (!items) return;
+  const DevState& st = A.st;
+  const u32 lane = threadIdx.x & 63, ilog = st.interval_log2;
+  for (u32 it = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6)); it < items; it += A.wgc * kPW) {
+    u32 lo = 0, hi = ncu;  // the catch-up entry holding item it: largest items0 <= it
+    while (hi - lo > 1) {
+      const u32 mid = (lo + hi) / 2;
+      if (A.xc3[mid].items0 <= it) lo = mid; else hi = mid;
+    }
+    const XCatch c = A.xc3[lo];
+    const u32 j = it - c.items0;
+    const RingRef rg = ring_ref(st, c.p);
+    const uint8_t* ring = st.logs + (u64)__builtin_ctz(st.local_mask[c.p]) * st.rstride + rg.base;
+    const u64 mask = rg.seg - 1ull, end = c.pos + c.bytes;
+    const u64 m = (c.pos >> ilog) + j;
+    const u64 w0 = j ? m << ilog : c.pos, w1 = min(end, (m + 1ull) << ilog);
+    // the first record starting in the window
+    u64 roff = c.first, rpos = c.pos;
+    if (j) {
+      const u64* ie = st.index + (rg.ibase + m % rg.icap) * 2;
+      roff = ie[0];
+      rpos = ie[1];
+    }
+    for (u64 sub = w0 & ~1023ull; sub < w1; sub += 1024) {
+      const u64 q = sub + 16ull * lane;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      const bool mine = q >= w0 && q < w1;
+      if (mine) {
+        v = *reinterpret_cast<const uint4*>(ring + (q & mask));
+        store_log16(A.outbox3 + c.data_abs + (q - c.pos), v);
+      }
+      // walk the headers that start in [max(sub, w0), min(sub + 1 KiB, w1)): lane (pos - sub) / 16
+      while (rpos < min(sub + 1024ull, w1)) {
+        const u32 L = (u32)__shfl((int)v.z, (int)((rpos - sub) >> 4), 64);
+        if (lane == 0)
+          *reinterpret_cast<u64*>(A.outbox3 + c.tab_abs + 8ull * (roff - c.first)) =
+              (u64)c.k | ((u64)(c.data_start16 + (u32)((rpos - c.pos) >> 4)) << 32);
+        rpos += 16ull + ((L + 15ull) & ~15ull);
+        ++roff;
+      }
+    }
+  }
+}
+
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
 #define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
@@ -1124,7 +1394,11 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   // roles along blockIdx.x: [s3_lead stage-3 workgroups | stage 1 | stage 2 | partition threads |
   // the other stage-3 workgroups | large records] (dispatch order)
   if (wg >= A.wg1 + A.wg2 + A.wgp + A.wg3) {
-    stage3_big_waves<XR>(A, *reinterpret_cast<Stage3Smem*>(smem_raw), wg - (A.wg1 + A.wg2 + A.wgp + A.wg3));
+    const u32 b = wg - (A.wg1 + A.wg2 + A.wgp + A.wg3);
+    if (XR && b >= A.wgb)
+      stage3_catchup(A, b - A.wgb);
+    else
+      stage3_big_waves<XR>(A, *reinterpret_cast<Stage3Smem*>(smem_raw), b);
     return;
   }
   bool s3 = false;
@@ -1208,14 +1482,14 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
 #ifdef RMQ_PIPE_XR_TU
 // the kernel with a replication transport (engine.cpp sizes its roles for kPipeThreadsXR)
 void launch_pipeline_xr(const PipeArgs& a, hipStream_t s, hipEvent_t start) {
-  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb;
+  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb + a.wgc;
   hipExtLaunchKernelGGL(pipeline_kernel<true>, dim3(grid), dim3(kPT), kSmemBytes, s, start, nullptr, 0, a);
 }
 #else
 uint32_t pipeline_wgs_per_cu(uint32_t threads) { return RMQ_PIPE_WAVES_PER_SIMD * 4u / (threads / 64u); }
 
 void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start) {
-  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb;
+  const u32 grid = a.wg1 + a.wg2 + a.wgp + a.wg3 + a.wgb + a.wgc;
   if (!grid) {
     if (start) (void)hipEventRecord(start, s);
     return;

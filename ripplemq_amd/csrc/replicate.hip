@@ -1,46 +1,53 @@
-// replicate.hip — the follower side of a replica-log round (FORMAT.md §9).
+// replicate.hip — the follower side of a replica-log round (FORMAT.md §9 v3).
 //
 // Reference: jraft replicates every partition log to its RF-1 followers with AppendEntries; a
 // follower appends the entries after checking that they continue its log (Raft log matching) and
 // acknowledges the index it now holds, which the leader's BallotBox turns into the commit index
 // (PartitionRaftServer.java:82-93 configures the group; MessageAppendRequestProcessor.java:59 is
-// the Node.apply that starts it). Here a round carries one launch group of the leader's appends
-// for every partition the two ranks share, as one region of the exchange:
+// the Node.apply that starts it); consumer-offset commits are log entries too, applied on every
+// replica (ConsumerOffsetUpdateRequestProcessor.java:59-60, PartitionStateMachine.java:48-49). Here
+// a round carries one launch group of the leader's appends (and any catch-up gap) for every
+// partition the two ranks share, as one region of the exchange, plus the changed consumer-offset
+// rows. Four kernels, in order on the exchange stream:
 //   ingest_prepare (thread per entry): the log end the entry continues — the follower's own, or,
-//     when the round's first offset lies inside the follower's retained log below its end, that
-//     offset and its position (the follower truncates its log to the leader's: Raft's follower
-//     deletes the entries that conflict with the leader's; the position comes from the sparse
-//     index and a walk over the follower's record headers). An entry whose leader term is older
-//     than the follower's is refused (a stale leader);
-//   ingest_records (wave per 32 records, a lane pair per record, like the append's stage 3):
-//     checks the record continues the follower's log (first offset == follower log end, header
-//     offset == first offset + rank), recomputes its CRC32C from the payload pieces (slicing-by-8
-//     and zero-shift tables in LDS, Horner fold per lane, the pad removed by x^(-8 pad)) against
-//     the header's, and stores the record into the follower's replica ring at the same logical
-//     position the leader used (pieces a later piece of the round overwrites are not stored), plus
-//     the sparse-index entries;
-//   ingest_finish (thread per entry): moves the follower partition's log end (both state sets:
-//     the append pipeline never touches a partition it does not lead), adopts a newer leader term,
-//     evaluates retention once per round (FORMAT.md §4 rule) and writes the ack (the follower's
-//     log end, 0 when the entry does not continue it) for the leader.
-// A refused entry (CRC, log mismatch or stale term) leaves the follower's log end where it was.
+//     when the entry's first offset lies inside the follower's retained log below its end, that
+//     offset and its position (truncation: the leader's log wins; the position from the sparse
+//     index and the record headers). A stale leader term or a missed round (no region) refuses it;
+//   ingest_verify (wave per 32 records, a lane pair per record, records over 1 KB by the whole
+//     wave): the record continues the entry (header offset = first + rank, inside the entry's
+//     bytes) and its CRC32C from the 16-byte payload pieces (slicing-by-8 and zero-shift tables in
+//     LDS, Horner fold per lane, the pad removed by x^(-8 pad)) equals the header's; sparse-index
+//     entries past the follower's live log (slots no live entry uses). Nothing else is written;
+//   ingest_finish (thread per entry): the verdict — a refusal of either of two local slots of one
+//     partition refuses both — then for an accepted entry the follower's log end (both state sets:
+//     the append pipeline never touches a partition it does not lead), a newer term, the index
+//     entries a truncation re-covers, retention once per round (FORMAT.md §4 rule) and the
+//     consumer-offset row; every entry acks {log end | status, position};
+//   ingest_copy (workgroup per 64 KiB of a region): the accepted entries' record bytes, whole
+//     16-byte pieces, into the follower's replica ring at the leader's logical positions (pieces a
+//     later piece of the round overwrites are not stored). A refused entry writes nothing.
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "partition_ops.hpp"
 
+
 namespace rmq {
 
-constexpr u32 kIT = 512;           // threads per ingest workgroup
+constexpr u32 kIT = 512;           // threads per verify workgroup
 constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
 constexpr u32 kIR = 32;            // records per task
 constexpr u32 kBigIngest = 64;     // records over this many 16-byte pieces: the whole wave
+constexpr u32 kCT = 256;           // threads per copy workgroup
 
 struct RegionView {
   const uint8_t* base;
-  u32 n_entries, n_records;
-  u64 data_off;
+  u32 n_entries, n_records, M, C;
+  u64 data_off, rows_off;
+  bool sane;
 };
 
+// The region of source src in this round's inbox (FORMAT.md §9 header), checked against the
+// entry list both sides derive from the placement.
 __device__ __forceinline__ RegionView region_of(const IngestArgs& A, u32 src) {
   RegionView v;
   v.base = A.inbox + A.region[src];
@@ -48,6 +55,11 @@ __device__ __forceinline__ RegionView region_of(const IngestArgs& A, u32 src) {
   v.n_entries = h[1];
   v.n_records = h[2];
   v.data_off = *reinterpret_cast<const u64*>(h + 6);
+  v.rows_off = *reinterpret_cast<const u64*>(h + 8);
+  v.M = h[10];
+  v.C = h[11];
+  v.sane = A.rbytes[src] >= kRegionHdr && h[0] == kXMagic && v.n_entries == A.xi_start[src + 1] - A.xi_start[src] &&
+           h[3] == src && v.C == A.C && v.rows_off <= A.rbytes[src];
   return v;
 }
 
@@ -110,6 +122,8 @@ __device__ u64 follower_pos(const DevState& st, u32 p, u32 slot, u64 t) {
   return pos;
 }
 
+constexpr u32 kBadCrc = 1u, kBadLog = 2u, kBadStale = 4u, kBadMissed = 8u;
+
 __global__ void ingest_prepare_kernel(IngestArgs A) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= A.n_in) return;
@@ -117,24 +131,38 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
   const DevState& st = A.st;
   const u32 p = A.xi_p[e];
   u64 leo = st.leo[p], used = st.used[p];
-  A.bad[e] = 0u;  // this round's verdict starts clean (the finish kernel only reads it)
-  if (A.rbytes[src]) {
+  u32 bad = 0;
+  if (!A.rbytes[src]) {
+    bad = kBadMissed;  // the leader sent nothing this round (it failed before replicating)
+  } else {
     const RegionView R = region_of(A, src);
-    if (R.n_entries == A.xi_start[src + 1] - A.xi_start[src]) {
+    if (!R.sane) {
+      bad = kBadLog;
+    } else {
       const DirView d = dir_of(R, k);
       if (d.term < st.term[p]) {
-        A.bad[e] = 4u;  // a stale leader
+        bad = kBadStale;  // a stale leader
       } else if (d.first < leo && d.first >= st.start_off[p]) {
         used = follower_pos(st, p, A.xi_slot[e], d.first);  // the leader's log wins: truncate
         leo = d.first;
       }
+      if (!bad && d.first != leo) bad = kBadLog;  // does not continue the follower's log
+      if (!bad && d.bytes16) {  // copy work items of the entry (order does not matter)
+        const u32 nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
+        const u32 at = atomicAdd(A.n_items, nc);
+        for (u32 c = 0; c < nc; ++c) {
+          A.items[2 * (at + c)] = e;
+          A.items[2 * (at + c) + 1] = c;
+        }
+      }
     }
   }
+  A.bad[e] = bad;
   A.base[2 * e] = leo;
   A.base[2 * e + 1] = used;
 }
 
-__global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
+__global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
   __shared__ __attribute__((aligned(16))) u32 t8[8][256];
   __shared__ __attribute__((aligned(16))) u32 z[2][4][256];
   __shared__ __attribute__((aligned(16))) u32 zk[4][256];  // 1 KB shift: records over 1 KB, by the wave
@@ -155,13 +183,13 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   const u32 src = source_of_task(A, task);
   if (!A.rbytes[src]) return;
   const RegionView R = region_of(A, src);
-  if (R.n_entries != A.xi_start[src + 1] - A.xi_start[src]) return;  // malformed (finish counts it)
+  if (!R.sane) return;  // every entry refused (prepare)
   const u32 lane = threadIdx.x & 63, j = lane & 1u;
   const u32 i = (task - A.task0[src]) * kIR + (lane >> 1);
   const bool in = i < R.n_records;
   const DevState& st = A.st;
   u32 p = 0, L = 0, m = 0, e = 0;
-  u64 pos = 0, gend = 0, off = 0;
+  u64 pos = 0, off = 0;
   bool ok = false, owner = false;
   const uint8_t* rec = R.base;
   uint4 hdr = make_uint4(0, 0, 0, 0);
@@ -169,23 +197,23 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
     const u64 tab = *reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries + 8ull * i);
     const u32 k = min((u32)tab, R.n_entries - 1u), d16 = (u32)(tab >> 32);  // ok below requires k == tab
     const DirView d = dir_of(R, k);
-    const u32 bytes16 = d.bytes16, tstart = d.tstart, dstart16 = d.dstart16;
-    const u64 first = d.first;
     e = A.xi_start[src] + k;
     p = A.xi_p[e];
     owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
-    const u64 leo = A.base[2 * e], used = A.base[2 * e + 1];  // after a truncation: the leader's first offset
+    const u64 used = A.base[2 * e + 1];   // after a truncation: at the leader's first offset
     rec = R.base + R.data_off + 16ull * d16;
-    hdr = *reinterpret_cast<const uint4*>(rec);
-    off = ((u64)hdr.y << 32) | hdr.x;
-    L = hdr.z;
-    m = (L + 15u) >> 4;
-    const u64 rel = 16ull * (d16 - dstart16);
+    const u64 rel = 16ull * (u64)(d16 - d.dstart16);
+    if (k == (u32)tab && d16 >= d.dstart16 && R.data_off + 16ull * d16 + 16ull <= R.rows_off) {
+      hdr = *reinterpret_cast<const uint4*>(rec);
+      off = ((u64)hdr.y << 32) | hdr.x;
+      L = hdr.z;
+      m = (L + 15u) >> 4;
+    }
     pos = used + rel;
-    gend = used + 16ull * bytes16;
-    ok = k == (u32)tab && first == leo && off == first + (i - tstart) && d16 >= dstart16 &&
-         rel + 16ull * (1ull + m) <= 16ull * bytes16 && !(A.bad[e] & 4u);
-    if (!ok && j == 1) atomicOr(&A.bad[e], 2u);  // does not continue the follower's log
+    // the record continues the entry (its directory verdict is prepare's)
+    ok = k == (u32)tab && d16 >= d.dstart16 && off == d.first + (i - d.tstart) &&
+         rel + 16ull * (1ull + m) <= 16ull * d.bytes16 && A.bad[e] == 0u;
+    if (!ok && j == 1 && A.bad[e] == 0u) atomicOr(&A.bad[e], kBadCrc);  // the record's content is wrong
   }
   // CRC32C of the payload from its 16-byte pieces (zero-padded in the log): lane j folds pieces
   // j, j + 2, ... by Horner's rule with the 32-byte zero-shift table; records over 1 KB are done
@@ -193,17 +221,21 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
   const bool big = ok && m > kBigIngest;
   const u32 mm = ok && !big ? m : 0u;
   u32 acc = 0;
-  const RingRef rg = ring_ref(st, p);  // p = 0 for lanes without a record (nothing is stored)
-  uint8_t* const ring = st.logs + (u64)(in ? A.xi_slot[e] : 0u) * st.rstride + rg.base;
-  const u64 segmask = rg.seg - 1ull;
-  for (u32 c = 0; __any(c < (mm + 1u) / 2u); ++c) {
-    const u32 jp = 2u * c + j;
-    if (jp < mm) {
-      uint4 v = *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * jp);
-      const u64 x = pos + 16ull + 16ull * jp;
-      if (x + rg.seg >= gend) store_log16(ring + (x & segmask), v);
-      if (jp == 0) v.x ^= 0xFFFFFFFFu;
-      acc = crc_zshift(z[1], acc) ^ crc_piece16(t8, v);
+  for (u32 c = 0; __any(c < (mm + 1u) / 2u); c += 4) {
+    uint4 v[4];
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u) {  // four pieces in flight per lane
+      const u32 jp = 2u * (c + u) + j;
+      v[u] = jp < mm ? *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * jp) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u) {
+      const u32 jp = 2u * (c + u) + j;
+      if (jp < mm) {
+        uint4 w = v[u];
+        if (jp == 0) w.x ^= 0xFFFFFFFFu;
+        acc = crc_zshift(z[1], acc) ^ crc_piece16(t8, w);
+      }
     }
   }
   if (ok && mm > j && ((mm - 1u - j) & 1u)) acc = crc_zshift(z[0], acc);
@@ -215,15 +247,7 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
     const u32 sl = (u32)__builtin_ctzll(bm);
     const u64 brec = ((u64)(u32)__builtin_amdgcn_readlane((int)(reinterpret_cast<u64>(rec) >> 32), (int)sl) << 32) |
                      (u32)__builtin_amdgcn_readlane((int)(u32)reinterpret_cast<u64>(rec), (int)sl);
-    const u64 bpos = ((u64)(u32)__builtin_amdgcn_readlane((int)(pos >> 32), (int)sl) << 32) |
-                     (u32)__builtin_amdgcn_readlane((int)(u32)pos, (int)sl);
-    const u64 bgend = ((u64)(u32)__builtin_amdgcn_readlane((int)(gend >> 32), (int)sl) << 32) |
-                      (u32)__builtin_amdgcn_readlane((int)(u32)gend, (int)sl);
-    const u64 bring = ((u64)(u32)__builtin_amdgcn_readlane((int)(reinterpret_cast<u64>(ring) >> 32), (int)sl) << 32) |
-                      (u32)__builtin_amdgcn_readlane((int)(u32)reinterpret_cast<u64>(ring), (int)sl);
     const u32 bm16 = ((u32)__builtin_amdgcn_readlane((int)L, (int)sl) + 15u) >> 4;
-    const u64 bseg = ((u64)(u32)__builtin_amdgcn_readlane((int)(rg.seg >> 32), (int)sl) << 32) |
-                     (u32)__builtin_amdgcn_readlane((int)(u32)rg.seg, (int)sl);
     u32 bacc = 0;
     for (u32 k0 = 0; 64u * k0 < bm16; k0 += 4u) {
       uint4 v[4];
@@ -236,8 +260,6 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
       for (u32 u = 0; u < 4u; ++u) {
         const u32 jp = 64u * (k0 + u) + lane;
         if (jp < bm16) {
-          const u64 x = bpos + 16ull + 16ull * jp;
-          if (x + bseg >= bgend) store_log16(reinterpret_cast<uint8_t*>(bring) + (x & (bseg - 1ull)), v[u]);
           uint4 w = v[u];
           if (jp == 0) w.x ^= 0xFFFFFFFFu;
           bacc = crc_zshift(zk, bacc) ^ crc_piece16(t8, w);
@@ -258,24 +280,30 @@ __global__ __launch_bounds__(kIT) void ingest_records_kernel(IngestArgs A) {
       const u32 pad = 16u * m - L;
       crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
     }
-    ok = crc == hdr.w;
-    if (ok) {
-      if (pos + rg.seg >= gend) store_log16(ring + (pos & segmask), hdr);
-      if (owner) {  // sparse index: every multiple of the interval the record crosses names the next record
+    // the zero padding after the payload (FORMAT.md §1) is part of the record
+    if (m && (L & 15u)) {
+      const uint4 t = *reinterpret_cast<const uint4*>(rec + 16ull * m);  // the last piece
+      const u32 nb = L & 15u;
+      const u32 w4[4] = {t.x, t.y, t.z, t.w};
+      for (u32 b = nb; b < 16u; ++b)
+        if ((w4[b >> 2] >> (8u * (b & 3u))) & 0xFFu) crc = ~hdr.w;
+    }
+    if (crc == hdr.w) {
+      if (owner) {  // sparse index past the follower's live log: every interval multiple the record crosses
         const u32 ilog = st.interval_log2;
-        const u64 end = pos + 16ull * (1ull + m);
+        const RingRef rg = ring_ref(st, p);
+        const u64 end = pos + 16ull * (1ull + m), live = st.used[p] >> ilog;
         for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end; ++q) {
+          if (q <= live) continue;  // inside the live log (a truncation): finish writes it if accepted
           u64* ie = st.index + (rg.ibase + q % rg.icap) * 2;
           ie[0] = off + 1;
           ie[1] = end;
         }
       }
     } else {
-      atomicOr(&A.bad[e], 1u);  // CRC32C differs from the header's
+      atomicOr(&A.bad[e], kBadCrc);  // CRC32C differs from the header's
     }
   }
-  const u32 n_ok = (u32)__popcll(__ballot(in && ok && j == 1));
-  if (lane == 0 && n_ok) atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)n_ok);
 }
 
 __global__ void ingest_finish_kernel(IngestArgs A) {
@@ -285,49 +313,111 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
   const DevState& st = A.st;
   const u32 p = A.xi_p[e], k = e - A.xi_start[src];
   const bool owner = k == 0 || A.xi_p[e - 1] != p;
-  u64 ack = st.leo[p];  // no region from this leader: nothing new
-  const bool whole = A.rbytes[src] && region_of(A, src).n_entries == A.xi_start[src + 1] - A.xi_start[src];
-  if (A.rbytes[src] && !whole) {
-    ack = 0;
-    if (k == 0) atomicAdd((unsigned long long*)&A.counters[2], 1ull);
-  } else if (A.rbytes[src]) {
-    const DirView d = dir_of(region_of(A, src), k);
-    // two local slots of one partition (adjacent entries of the same source): the owner keeps the
-    // partition's state, so a refusal of either is a refusal of both (no slot acks records the
-    // follower's log end does not hold)
-    u32 bad = A.bad[e];
-    for (u32 q = e; q > A.xi_start[src] && A.xi_p[q - 1] == p; --q) bad |= A.bad[q - 1] ? 8u : 0u;
-    for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) bad |= A.bad[q] ? 8u : 0u;
-    const u64 bleo = A.base[2 * e], bused = A.base[2 * e + 1];
-    if (bad) {
-      ack = 0;  // no new information (match only moves up)
-      if (bad & 7u) atomicAdd((unsigned long long*)&A.counters[(bad & 6u) ? 2 : 1], 1ull);
-    } else {
-      // the entry continues the log at bleo (or does not: a follower behind the leader acks 0)
-      const bool cont = d.first == bleo;
-      ack = d.count ? d.first + d.count : (cont ? bleo : 0ull);
-      if (owner) {
-        if (d.term > st.term[p]) st.term[p] = d.term;
-        const u64 nleo = d.count ? ack : bleo, nused = bused + 16ull * d.bytes16;
-        for (u32 s = 0; s < 2; ++s) {
-          A.sets[s].leo[p] = nleo;
-          A.sets[s].used[p] = nused;
+  // two local slots of one partition (adjacent entries of the same source): a refusal of either
+  // refuses both
+  const u32 own = A.bad[e];
+  u32 bad = own;
+  for (u32 q = e; q > A.xi_start[src] && A.xi_p[q - 1] == p; --q) bad |= A.bad[q - 1];
+  for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) bad |= A.bad[q];
+  if (own) atomicAdd((unsigned long long*)&A.counters[(own & kBadCrc) && !(own & ~kBadCrc) ? 1 : 2], 1ull);
+  A.acc[e] = bad ? 0u : 1u;
+  if (bad) {
+    A.ackout[2 * e] = st.leo[p] | kAckRefused;
+    A.ackout[2 * e + 1] = st.used[p];
+    return;
+  }
+  const RegionView R = region_of(A, src);
+  const DirView d = dir_of(R, k);
+  const u64 bleo = A.base[2 * e], bused = A.base[2 * e + 1];
+  const u64 nleo = d.first + d.count, nused = bused + 16ull * d.bytes16;
+  if (owner) {
+    const u32 ilog = st.interval_log2;
+    const u64 old_used = st.used[p];
+    if (d.term > st.term[p]) st.term[p] = d.term;
+    if (bused < old_used && d.count) {
+      // a truncation: the index slots inside the old live log name the new log's records
+      const RingRef rg = ring_ref(st, p);
+      const uint8_t* data = R.base + R.data_off + 16ull * d.dstart16;
+      const u64 live = old_used >> ilog;
+      u64 pos = bused;
+      for (u32 r = 0; r < d.count && (pos >> ilog) < live; ++r) {
+        const u32 L = *reinterpret_cast<const u32*>(data + (pos - bused) + 8);
+        const u64 end = pos + 16ull + ((L + 15ull) & ~15ull);
+        for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end && q <= live; ++q) {
+          u64* ie = st.index + (rg.ibase + q % rg.icap) * 2;
+          ie[0] = d.first + r + 1;
+          ie[1] = end;
         }
-        if (d.count) {
-          // retention once per round (FORMAT.md §4 rule on the follower's log)
-          const RingRef rg = ring_ref(st, p);
-          if (nused - st.start_pos[p] > rg.seg) {
-            const u64 ms = (nused - rg.seg + (1ull << st.interval_log2) - 1) >> st.interval_log2;
-            const u64* ie = st.index + (rg.ibase + ms % rg.icap) * 2;
-            st.start_off[p] = ie[0];
-            st.start_pos[p] = ie[1];
-          }
-          atomicAdd((unsigned long long*)&A.counters[3], 16ull * d.bytes16);
-        }
+        pos = end;
+      }
+    }
+    for (u32 s = 0; s < 2; ++s) {
+      A.sets[s].leo[p] = nleo;
+      A.sets[s].used[p] = nused;
+    }
+    if (d.count) {
+      // retention once per round (FORMAT.md §4 rule on the follower's log)
+      const RingRef rg = ring_ref(st, p);
+      if (nused - st.start_pos[p] > rg.seg) {
+        const u64 ms = (nused - rg.seg + (1ull << ilog) - 1) >> ilog;
+        const u64* ie = st.index + (rg.ibase + ms % rg.icap) * 2;
+        st.start_off[p] = ie[0];
+        st.start_pos[p] = ie[1];
+      }
+      atomicAdd((unsigned long long*)&A.counters[3], 16ull * d.bytes16);
+    }
+    if (R.M) {  // the partition's consumer-offset row, if the round carries one (rows ascend by entry)
+      const u64 rowb = 16ull + 8ull * A.C;
+      u32 lo = 0, hi = R.M;
+      while (lo < hi) {
+        const u32 mid = (lo + hi) / 2;
+        const u32 rk = *reinterpret_cast<const u32*>(R.base + R.rows_off + rowb * mid);
+        if (rk < k) lo = mid + 1; else hi = mid;
+      }
+      if (lo < R.M && *reinterpret_cast<const u32*>(R.base + R.rows_off + rowb * lo) == k) {
+        const u64* row = reinterpret_cast<const u64*>(R.base + R.rows_off + rowb * lo + 16);
+        for (u32 c = 0; c < A.C; ++c) st.cons[(u64)p * A.C + c] = row[c];
       }
     }
   }
-  A.ackout[e] = ack;
+  if (d.count) atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)d.count);
+  (void)bleo;
+  A.ackout[2 * e] = nleo;
+  A.ackout[2 * e + 1] = nused;
+}
+
+// Accepted entries' record bytes into the follower's replica rings: workgroup per work item
+// {entry, 64 KiB chunk of its data}, 16-byte pieces, four in flight per thread.
+__global__ __launch_bounds__(kCT) void ingest_copy_kernel(IngestArgs A) {
+  const u32 it = blockIdx.x;
+  if (it >= *A.n_items) return;
+  const u32 e = A.items[2 * it], c = A.items[2 * it + 1];
+  if (!A.acc[e]) return;
+  const u32 src = source_of_entry(A, e), k = e - A.xi_start[src];
+  const DevState& st = A.st;
+  const RegionView R = region_of(A, src);
+  const DirView d = dir_of(R, k);
+  const u32 p = A.xi_p[e];
+  const RingRef rg = ring_ref(st, p);
+  uint8_t* const ring = st.logs + (u64)A.xi_slot[e] * st.rstride + rg.base;
+  const u64 segmask = rg.seg - 1ull;
+  const uint8_t* data = R.base + R.data_off + 16ull * d.dstart16;
+  const u64 bused = A.base[2 * e + 1], bytes = 16ull * d.bytes16, gend = bused + bytes;
+  const u64 b0 = (u64)c * kCopyChunk, b1 = min(bytes, b0 + kCopyChunk);
+  for (u64 q0 = b0 + 16ull * threadIdx.x; q0 < b1; q0 += 16ull * kCT * 4) {
+    uint4 v[4];
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u) {
+      const u64 q = q0 + 16ull * kCT * u;
+      v[u] = q < b1 ? *reinterpret_cast<const uint4*>(data + q) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u) {
+      const u64 q = q0 + 16ull * kCT * u;
+      const u64 x = bused + q;
+      if (q < b1 && x + rg.seg >= gend) store_log16(ring + (x & segmask), v[u]);
+    }
+  }
 }
 
 // Acks of one round applied after the pipeline has drained (thread per partition).
@@ -338,17 +428,29 @@ __global__ void ack_apply_kernel(AckApplyArgs a) {
   u64 row[kMaxRF];
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < st.RF ? st.match[(u64)p * st.RF + r] : 0ull;
-  if (apply_acks(st, p, a.outidx, a.ackin, st.leo[p], row)) {
+  if (apply_acks(st, p, a.outidx, a.ackin, st.leo[p], row, a.xreq, a.acks_round)) {
     const u64 c = quorum_commit(row, st.RF, st.commit[p], st.term_start[p]);
     st.commit[p] = c;
     st.hw[p] = c;
   }
 }
 
-void launch_ingest(const IngestArgs& a, uint32_t tasks, hipStream_t s) {
+void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, hipStream_t s) {
   if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
-  if (tasks) hipLaunchKernelGGL(ingest_records_kernel, dim3((tasks + kIW - 1) / kIW), dim3(kIT), 0, s, a);
+  if (tasks) hipLaunchKernelGGL(ingest_verify_kernel, dim3((tasks + kIW - 1) / kIW), dim3(kIT), 0, s, a);
   if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
+  if (items_bound) hipLaunchKernelGGL(ingest_copy_kernel, dim3(items_bound), dim3(kCT), 0, s, a);
+}
+
+// Fault injection (rmq_fault_corrupt): one byte of a region flipped before it is sent.
+__global__ void flip_kernel(uint8_t* region, uint64_t size, int64_t at) {
+  const u64 rows = *reinterpret_cast<const u64*>(region + 32);  // end of the data section
+  const int64_t pos = at < 0 ? (int64_t)rows + at : at;
+  if (pos >= 0 && (u64)pos < size) region[pos] ^= 0x5Au;
+}
+
+void launch_flip(uint8_t* region, uint64_t size, int64_t at, hipStream_t s) {
+  hipLaunchKernelGGL(flip_kernel, dim3(1), dim3(1), 0, s, region, size, at);
 }
 
 void launch_ack_apply(const AckApplyArgs& a, hipStream_t s) {

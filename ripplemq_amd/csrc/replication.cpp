@@ -15,7 +15,10 @@
 //       follower ingest (CRC32C check, ring + index writes, log end, retention; replicate.hip) and
 //       the grouped send/recv of the acks (follower log ends);
 //   launch k+5 (three launches after g's stage 3): waits for g's exchange and applies the acks to
-//       the matchIndex rows in its partition threads, then the quorum commit rule.
+//       the matchIndex rows in its partition threads, then the quorum commit rule; the plan of the
+//       group that launch scans reads the same acks for its catch-up verdicts (FORMAT.md §9 v3:
+//       a refused entry's next round starts at the follower's log end, the gap re-sent from the
+//       leader's ring by the catch-up waves of the stage-3 launch).
 //
 // Every rank makes the same calls in the same order (rounds are collective, like the launches
 // that drive them): with a transport attached, launch groups close only when full, and control
@@ -49,14 +52,40 @@ uint64_t entry_hash(uint64_t key, uint32_t slot) { return key * RMQ_MAX_RF + slo
 
 void free_set_buffers(Replication* r) {
   for (XchgSet& x : r->sets) {
-    void* bufs[] = {x.outbox, x.inbox, x.xe, x.sizes, x.ackout, x.ackin};
+    void* bufs[] = {x.outbox, x.inbox, x.xe, x.xc, x.xc_n, x.sizes, x.ackout, x.ackin};
     for (void* p : bufs)
       if (p) hipFree(p);
     x.outbox = x.inbox = nullptr;
     x.xe = nullptr;
+    x.xc = nullptr;
+    x.xc_n = nullptr;
     x.sizes = x.ackout = x.ackin = nullptr;
   }
 }
+
+}  // namespace
+
+// The leader's catch-up state of every out entry starts over (FORMAT.md §9: placement and leader
+// start): next = the leader's log end, no request, no catch-up round. Engine drained.
+int reset_catchup(rmq_engine* e) {
+  Replication* r = e->repl;
+  const size_t n = r->xo_p.size();
+  if (!n) return RMQ_OK;
+  const uint32_t P = e->cfg.num_partitions;
+  std::vector<uint64_t> leo(P), used(P), nx(2 * n);
+  HIP_TRY(hipMemcpy(leo.data(), e->st.leo, P * 8ull, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(used.data(), e->st.used, P * 8ull, hipMemcpyDeviceToHost));
+  for (size_t k = 0; k < n; ++k) {
+    nx[2 * k] = leo[r->xo_p[k]];
+    nx[2 * k + 1] = used[r->xo_p[k]];
+  }
+  HIP_TRY(hipMemcpy(r->d_xnext, nx.data(), nx.size() * 8, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(r->d_xreq, 0, n * 32));
+  HIP_TRY(hipMemset(r->d_xcu, 0, n * 8));
+  return RMQ_OK;
+}
+
+namespace {
 
 // Post the {region bytes, records} swap of the group in set s (after its stage-2 launch).
 int post_sizes(rmq_engine* e, uint32_t s, bool drop) {
@@ -91,28 +120,35 @@ int post_round(rmq_engine* e, uint32_t s) {
   void* rb[kMaxWorld];
   uint64_t sn[kMaxWorld], rn[kMaxWorld];
   IngestArgs a{};
-  uint64_t so = 0, ro = 0;
+  uint64_t ro = 0, smax = 0;
   uint32_t tasks = 0;
   for (uint32_t q = 0; q < W; ++q) {
     sn[q] = q == me ? 0 : hs[2 * q];
     rn[q] = q == me ? 0 : hs[2 * W + 2 * q];
-    sb[q] = x.outbox + so;
+    sb[q] = x.outbox + (uint64_t)q * r->dcap;
     rb[q] = x.inbox + ro;
     a.region[q] = ro;
     a.rbytes[q] = rn[q];
     a.task0[q] = tasks;
     tasks += (uint32_t)((rn[q] ? hs[2 * W + 2 * q + 1] : 0) + 31) / 32;
-    so += sn[q];
-    ro += rn[q];
+    smax = std::max(smax, sn[q]);
+    ro += (rn[q] + 15) & ~15ull;
   }
   a.task0[W] = tasks;
-  if (so > r->out_cap || ro > r->in_cap) {
+  if (smax > r->dcap || ro > r->in_cap) {
     std::fprintf(stderr, "ripplemq: replication round exceeds its buffers (%llu/%llu out, %llu/%llu in)\n",
-                 (unsigned long long)so, (unsigned long long)r->out_cap, (unsigned long long)ro,
+                 (unsigned long long)smax, (unsigned long long)r->dcap, (unsigned long long)ro,
                  (unsigned long long)r->in_cap);
     return RMQ_EDEVICE;
   }
+  // copy work items: at most one per 64 KiB of received region bytes plus one per entry
+  const uint32_t items = (uint32_t)std::min<uint64_t>(r->items_cap, ro / kCopyChunk + W + r->xi_p.size());
   HIP_TRY(hipStreamWaitEvent(r->xchg_s, x.ev_s3, 0));
+  for (uint32_t q = 0; q < W; ++q)  // rmq_fault_corrupt
+    if (r->flip[q] && sn[q]) {
+      launch_flip(static_cast<uint8_t*>(sb[q]), sn[q], r->flip_at[q], r->xchg_s);
+      r->flip[q] = false;
+    }
   int rc = r->xport->exchange(sb, sn, rb, rn, r->xchg_s);
   if (rc) return rc;
   a.st = e->st;
@@ -125,25 +161,30 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.world = W;
   a.rank = me;
   a.n_in = (uint32_t)r->xi_p.size();
+  a.C = e->cfg.max_consumers;
   a.bad = r->d_bad;
+  a.acc = r->d_acc;
   a.base = r->d_base;
   a.ackout = x.ackout;
+  a.items = r->d_items;
+  a.n_items = r->d_nitems;
   a.crc = e->d_crc;
   a.counters = r->d_counters;
-  launch_ingest(a, tasks, r->xchg_s);
+  HIP_TRY(hipMemsetAsync(r->d_nitems, 0, 4, r->xchg_s));
+  launch_ingest(a, tasks, items, r->xchg_s);
   HIP_TRY(hipGetLastError());
-  // acks: the follower log end of every in entry back to its leader, fixed sizes both ways
+  // acks: {log end | status, position} of every in entry back to its leader, fixed sizes both ways
   for (uint32_t q = 0; q < W; ++q) {
-    sn[q] = q == me ? 0 : 8ull * (r->xi_start[q + 1] - r->xi_start[q]);
-    rn[q] = q == me ? 0 : 8ull * (r->xo_start[q + 1] - r->xo_start[q]);
-    sb[q] = x.ackout + r->xi_start[q];
-    rb[q] = x.ackin + r->xo_start[q];
+    sn[q] = q == me ? 0 : 16ull * (r->xi_start[q + 1] - r->xi_start[q]);
+    rn[q] = q == me ? 0 : 16ull * (r->xo_start[q + 1] - r->xo_start[q]);
+    sb[q] = x.ackout + 2ull * r->xi_start[q];
+    rb[q] = x.ackin + 2ull * r->xo_start[q];
   }
   rc = r->xport->exchange(sb, sn, rb, rn, r->xchg_s);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(x.ev_x, r->xchg_s));
   r->rounds++;
-  r->bytes_sent += so;
+  for (uint32_t q = 0; q < W; ++q) r->bytes_sent += q == me ? 0 : hs[2 * q];
   r->bytes_recv += ro;
   r->last_set = s;
   r->acking.push_back(s);
@@ -173,7 +214,7 @@ int repl_attach(rmq_engine* e, Transport* t) {
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&x.h_sizes, 4ull * kMaxWorld * 8, 0));
   }
-  int rc = dalloc(&r->d_counters, 4);
+  int rc = dalloc(&r->d_counters, 6);
   if (rc) return rc;
   return repl_set_lists(e);
 }
@@ -190,8 +231,9 @@ void repl_free(rmq_engine* e) {
     if (x.count) hipFree(x.count);
     if (x.h_sizes) hipHostFree(x.h_sizes);
   }
-  void* bufs[] = {r->d_xo_p, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot, r->d_xi_start,
-                  r->d_bad, r->d_base, r->d_counters};
+  void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot,
+                  r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
+                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_dflag};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (r->xchg_s) hipStreamDestroy(r->xchg_s);
@@ -296,38 +338,63 @@ int repl_set_lists(rmq_engine* e) {
     }
   }
   int rc = upload(&r->d_xo_p, r->xo_p);
+  if (!rc) rc = upload(&r->d_xo_slot, r->xo_slot);
   if (!rc) rc = upload(&r->d_xo_start, r->xo_start);
   if (!rc) rc = upload(&r->d_keysum, r->keysum);
   if (!rc) rc = upload(&r->d_outidx, outidx);
   if (!rc) rc = upload(&r->d_xi_p, r->xi_p);
   if (!rc) rc = upload(&r->d_xi_slot, r->xi_slot);
   if (!rc) rc = upload(&r->d_xi_start, r->xi_start);
-  if (!rc) rc = upload(&r->d_bad, std::vector<uint32_t>(r->xi_p.size(), 0u));
-  if (!rc) rc = upload(&r->d_base, std::vector<uint64_t>(2 * std::max<size_t>(1, r->xi_p.size()), 0ull));
+  const size_t n_in = std::max<size_t>(1, r->xi_p.size()), n_out = std::max<size_t>(1, r->xo_p.size());
+  if (!rc) rc = upload(&r->d_bad, std::vector<uint32_t>(n_in, 0u));
+  if (!rc) rc = upload(&r->d_acc, std::vector<uint32_t>(n_in, 0u));
+  if (!rc) rc = upload(&r->d_base, std::vector<uint64_t>(2 * n_in, 0ull));
+  if (!rc) rc = upload(&r->d_xnext, std::vector<uint64_t>(2 * n_out, 0ull));
+  if (!rc) rc = upload(&r->d_xreq, std::vector<uint64_t>(4 * n_out, 0ull));
+  if (!rc) rc = upload(&r->d_xcu, std::vector<uint64_t>(n_out, 0ull));
+  if (!rc) rc = upload(&r->d_dflag, std::vector<uint32_t>(W, 0u));
+  if (r->d_xdec) hipFree(r->d_xdec);
+  r->d_xdec = nullptr;
+  if (!rc) rc = dalloc(&r->d_xdec, n_out);
   if (rc) return rc;
   // round buffers (FORMAT.md §9 bounds): a record is at most 31 + L bytes in the log, sent once per
-  // remote slot, plus an 8-byte table slot; per region a header, a directory and table padding
+  // remote slot, plus an 8-byte table slot; the catch-up reserve of a destination is one such
+  // round bound (ro_catchup_reserve in the oracle); per region a header, a directory, table padding
+  // and the consumer-offset rows
   const uint64_t G = e->group_max, NR = e->cfg.max_batch_records, MB = e->cfg.max_batch_bytes;
-  const uint64_t rec = G * (39ull * NR + MB);
+  const uint64_t rec = G * (39ull * NR + MB), C = e->cfg.max_consumers;
   uint32_t max_remote = 0;
   for (uint32_t p = 0; p < P; ++p) {
     uint32_t k = 0;
     for (uint32_t s = 0; s < RF; ++s) k += outidx[(size_t)p * RF + s] != ~0u;
     max_remote = std::max(max_remote, k);
   }
-  r->out_cap = (uint64_t)max_remote * rec + 48ull * W + 32ull * r->xo_p.size();
-  r->in_cap = (uint64_t)(W - 1) * (RF - 1) * rec + 48ull * W + 32ull * r->xi_p.size();
+  const uint64_t per_entry = kDirEntry + 16 + 8 * C;
+  r->reserve = rec;
+  r->dcap = ((uint64_t)max_remote * rec + r->reserve + kRegionHdr + 16 + per_entry * n_out + 255) & ~255ull;
+  r->out_cap = (uint64_t)W * r->dcap;
+  r->in_cap = (uint64_t)(W - 1) * ((uint64_t)(RF - 1) * rec + r->reserve + kRegionHdr + 32) + per_entry * n_in;
+  r->items_cap = r->in_cap / kCopyChunk + W + n_in;
+  if (r->d_items) hipFree(r->d_items);
+  if (r->d_nitems) hipFree(r->d_nitems);
+  r->d_items = nullptr;
+  r->d_nitems = nullptr;
+  rc = dalloc(&r->d_items, 2 * r->items_cap);
+  if (!rc) rc = dalloc(&r->d_nitems, 1);
+  if (rc) return rc;
   free_set_buffers(r);
   for (XchgSet& x : r->sets) {
     rc = dalloc(&x.outbox, r->out_cap);
     if (!rc) rc = dalloc(&x.inbox, r->in_cap);
-    if (!rc) rc = dalloc(&x.xe, std::max<size_t>(1, r->xo_p.size()));
+    if (!rc) rc = dalloc(&x.xe, n_out);
+    if (!rc) rc = dalloc(&x.xc, n_out);
+    if (!rc) rc = dalloc(&x.xc_n, 2);
     if (!rc) rc = dalloc(&x.sizes, 4ull * W);
-    if (!rc) rc = dalloc(&x.ackout, std::max<size_t>(1, r->xi_p.size()));
-    if (!rc) rc = dalloc(&x.ackin, std::max<size_t>(1, r->xo_p.size()));
+    if (!rc) rc = dalloc(&x.ackout, 2 * n_in);
+    if (!rc) rc = dalloc(&x.ackin, 2 * n_out);
     if (rc) return rc;
   }
-  return RMQ_OK;
+  return reset_catchup(e);
 }
 
 void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const GroupFlight* s3) {
@@ -336,20 +403,39 @@ void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const Gro
   a.outidx = r->d_outidx;
   if (s2) {
     XchgSet& x = r->sets[s2->set];
+    x.round = r->planned++;
     a.xp2.xo_p = r->d_xo_p;
+    a.xp2.xo_slot = r->d_xo_slot;
     a.xp2.xo_start = r->d_xo_start;
     a.xp2.keysum = r->d_keysum;
     a.xp2.world = r->world;
     a.xp2.rank = r->rank;
     a.xp2.n_out = (uint32_t)r->xo_p.size();
+    a.xp2.C = e->cfg.max_consumers;
     a.xp2.count = x.count;
     a.xp2.xe = x.xe;
     a.xp2.outbox = x.outbox;
     a.xp2.sizes = x.sizes;
+    a.xp2.round = x.round;
+    a.xp2.reserve = r->reserve;
+    a.xp2.xnext = r->d_xnext;
+    a.xp2.xreq = r->d_xreq;
+    a.xp2.xcu = r->d_xcu;
+    a.xp2.xdec = r->d_xdec;
+    a.xp2.dflag = r->d_dflag;
+    a.xp2.dirty = e->st.cdirty;
+    a.xp2.xc = x.xc;
+    a.xp2.xc_n = x.xc_n;
+    a.xp2.counters = r->d_counters + 4;
+    a.xp2.dcap = r->dcap;
   }
   if (s3) {
-    a.xe3 = r->sets[s3->set].xe;
-    a.outbox3 = r->sets[s3->set].outbox;
+    XchgSet& x = r->sets[s3->set];
+    a.xe3 = x.xe;
+    a.outbox3 = x.outbox;
+    a.xc3 = x.xc;
+    a.xc3_n = x.xc_n;
+    a.wgc = 2u * e->cu_count / (kPipeThreadsXR / 64u);  // two catch-up waves per CU (most rounds: none)
   }
 }
 
@@ -360,7 +446,16 @@ int repl_before_launch(rmq_engine* e, PipeArgs& a) {
   const uint32_t s = r->acking.front();
   if (r->sets[s].applied_launch + 3 > e->launch_seq + 1) return RMQ_OK;
   HIP_TRY(hipStreamWaitEvent(e->main_s, r->sets[s].ev_x, 0));
-  if (!r->xo_p.empty()) a.ackin = r->sets[s].ackin;
+  if (!r->xo_p.empty()) {
+    a.ackin = r->sets[s].ackin;
+    a.acks_round = r->sets[s].round;
+    if (a.xp2.n_out) {  // the plan of this launch turns refusals into catch-up verdicts itself
+      a.xp2.ackin = a.ackin;
+      a.xp2.acks_round = a.acks_round;
+    } else {  // no plan reads these acks: the partition threads keep the requests
+      a.xreq = r->d_xreq;
+    }
+  }
   r->acking.pop_front();
   return RMQ_OK;
 }
@@ -408,6 +503,8 @@ int repl_drain(rmq_engine* e) {
       a.st = e->st;
       a.outidx = r->d_outidx;
       a.ackin = x.ackin;
+      a.xreq = r->d_xreq;
+      a.acks_round = x.round;
       launch_ack_apply(a, e->main_s);
       HIP_TRY(hipGetLastError());
     }

@@ -133,6 +133,10 @@ class Engine:
         """Tests: the next n rounds this engine leads carry no records (rmq_fault_drop_rounds)."""
         _check(self.lib.rmq_fault_drop_rounds(self.h, n), "rmq_fault_drop_rounds")
 
+    def fault_corrupt(self, dst: int, at: int) -> None:
+        """Tests: the next round sent to dst has one byte flipped (rmq_fault_corrupt)."""
+        _check(self.lib.rmq_fault_corrupt(self.h, dst, at), "rmq_fault_corrupt")
+
     def become_leader(self, pidx: int, term: int) -> None:
         _check(self.lib.rmq_become_leader(self.h, pidx, term), "rmq_become_leader")
 

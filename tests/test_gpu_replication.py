@@ -15,7 +15,7 @@ from parity import compare_state
 from repl_sim import exchange_round, place, rank_batches, rank_cfg
 from ripplemq_amd.engine import Engine, EngineConfig, LocalHub
 from ripplemq_amd.sharding import rank_view
-from ripplemq_amd.workload import StreamSpec
+from ripplemq_amd.workload import StreamSpec, make_batch
 
 pytestmark = pytest.mark.gpu
 
@@ -155,7 +155,11 @@ def test_leader_change_truncates_follower(oracle_mod):
                     if d != r:
                         assert np.array_equal(engs[r].read_outbox(d), regions[r][d]), f"region {r}->{d}"
             stats = [engs[r].replication_stats() for r in range(world)]
-            assert all(s["refused_crc"] == 0 and s["refused_log"] == 0 for s in stats), stats
+            # the lost round is missed by rank 0's followers (refused, FORMAT.md §9 v3); nothing else
+            for r in range(world):
+                c = oras[r].counters()
+                assert (stats[r]["refused_crc"], stats[r]["refused_log"]) == (int(c[1]), int(c[2])), (r, stats[r], c)
+            assert stats[0]["refused_crc"] == 0 and all(s["refused_log"] > 0 for s in stats[1:])
             for p in range(ppr):  # rank 0 follows its former partitions at term 2, truncated to the leader
                 st = engs[0].state(p)
                 assert st["term"] == 2 and not st["is_leader"]
@@ -163,6 +167,201 @@ def test_leader_change_truncates_follower(oracle_mod):
         finally:
             for o in oras:
                 o.close()
+    finally:
+        for e in engs:
+            e.close()
+        hub.close()
+
+
+def synced_rounds(oracle_mod, world, rf, ppr, group, rounds, spec, seg=1 << 16, interval=256, base_kw=None,
+                  faults=None, commits=None, small=None):
+    """Rounds with an rmq_sync on every rank after each one, so every plan sees the acks of every
+    round before it — exactly the oracle's order (tests/repl_sim.py): each round's regions, the
+    catch-up verdicts and the converged state must match bit for bit.
+    faults[k] = {"drop": ranks, "corrupt": (src, dst, at)}; commits[k] = {rank: (pidx, consumer,
+    offset)} committed by that leader before round k's appends; small: a StreamSpec for rounds >= 1."""
+    faults = faults or {}
+    commits = commits or {}
+    kw = dict(num_partitions=1, replication_factor=rf, segment_bytes=seg, index_interval=interval,
+              max_batch_records=4096, max_batch_bytes=1 << 20, pipeline_depth=group)
+    kw.update(base_kw or {})
+    base = EngineConfig(**kw)
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    cfgs = [rank_cfg(base, views[r], r) for r in range(world)]
+
+    def batches_of(r, k):
+        sp = small if (small is not None and k >= 1) else spec
+        return [make_batch(sp, 1000 * r + 50 * k + j) for j in range(group)]
+
+    hub = LocalHub(world)
+    engs = [Engine(c) for c in cfgs]
+    regions_gpu = [None] * world
+    try:
+        def body(r):
+            e = engs[r]
+            e.attach_local(hub)
+            place(e, views[r])
+            for k in range(rounds):
+                f = faults.get(k, {})
+                if r in f.get("drop", ()):
+                    e.fault_drop_rounds(1)
+                if f.get("corrupt") and f["corrupt"][0] == r:
+                    e.fault_corrupt(f["corrupt"][1], f["corrupt"][2])
+                if r in commits.get(k, {}):
+                    rc, st = e.commit_consumer_offset(*commits[k][r])
+                    assert rc == 0 and not st.any(), (rc, st)
+                for b in batches_of(r, k):
+                    e.append_async(b.pidx, b.lens, b.payload)
+                e.sync()
+            regions_gpu[r] = [e.read_outbox(d) if d != r else None for d in range(world)]
+
+        run_ranks(world, body)
+        oras = [oracle_mod.OracleEngine(c) for c in cfgs]
+        try:
+            for r in range(world):
+                place(oras[r], views[r], world)
+            regions = None
+            for k in range(rounds):
+                f = faults.get(k, {})
+                for r in range(world):
+                    if r in commits.get(k, {}):
+                        oras[r].commit_consumer_offset(*commits[k][r])
+                    for b in batches_of(r, k):
+                        oras[r].append(b.pidx, b.lens, b.payload)
+                regions = exchange_round(oras, keep_regions=True, drop=f.get("drop", ()), corrupt=f.get("corrupt"))
+            stats = [engs[r].replication_stats() for r in range(world)]
+            for r in range(world):
+                c = oras[r].counters()
+                got = (stats[r]["records_ingested"], stats[r]["refused_crc"], stats[r]["refused_log"],
+                       stats[r]["bytes_ingested"], stats[r]["catchup_entries"], stats[r]["detached_plans"])
+                assert got == tuple(int(x) for x in c), (r, got, c)
+            for r in range(world):
+                def local_slots(p, r=r):
+                    return [s for s in range(rf) if views[r].ranks[p][s] == r]
+                compare_state(engs[r], oras[r], cfgs[r], local_slots=local_slots)
+                for d in range(world):
+                    if d != r and regions[r][d] is not None:
+                        assert np.array_equal(regions_gpu[r][d], regions[r][d]), f"region {r}->{d}"
+            return views, engs, oras, stats
+        except BaseException:
+            for o in oras:
+                o.close()
+            raise
+    finally:
+        for e in engs:
+            e.close()
+        hub.close()
+
+
+def _close(res):
+    for o in res[2]:
+        o.close()
+
+
+def test_crc_refusal_then_catch_up_gpu(oracle_mod):
+    # a flipped payload byte on the link: rank 1 refuses the entry (the follower ingest's reject
+    # path), its log does not move; the next round's entry re-sends the gap (catch-up)
+    spec = StreamSpec(8, 600, "uniform", size=(1, 120), config_index=81)
+    res = synced_rounds(oracle_mod, world=3, rf=3, ppr=8, group=2, rounds=4, spec=spec,
+                        faults={1: {"corrupt": (0, 1, -5)}})
+    try:
+        stats = res[3]
+        assert stats[1]["refused_crc"] == 1 and stats[0]["catchup_entries"] == 1, stats
+        views, engs, oras = res[0], res[1], res[2]
+        lead = [engs[0].state(p) for p in range(views[0].led)]
+        assert all(s["commit"] == s["log_end_offset"] == s["match"][0] for s in lead)
+        assert all(min(s["match"]) == s["log_end_offset"] for s in lead)  # every follower caught up
+    finally:
+        _close(res)
+
+
+def test_missed_round_then_catch_up_gpu(oracle_mod):
+    spec = StreamSpec(6, 400, "zipf", size=(0, 150), config_index=82)
+    res = synced_rounds(oracle_mod, world=3, rf=3, ppr=6, group=2, rounds=4, spec=spec, faults={1: {"drop": (0,)}})
+    try:
+        stats = res[3]
+        assert stats[1]["refused_log"] > 0 and stats[2]["refused_log"] > 0 and stats[0]["catchup_entries"] >= 2
+        lead = [res[1][0].state(p) for p in range(res[0][0].led)]
+        assert all(min(s["match"]) == s["log_end_offset"] for s in lead)
+    finally:
+        _close(res)
+
+
+def test_partial_catch_up_gpu(oracle_mod):
+    # a missed round larger than the destination's catch-up reserve comes back in pieces that end on
+    # sparse-index entries, one per round
+    big = StreamSpec(2, 400, "uniform", size=(80, 120), config_index=83)
+    small = StreamSpec(2, 4, "uniform", size=(10, 20), config_index=84)
+    res = synced_rounds(oracle_mod, world=3, rf=3, ppr=2, group=1, rounds=12, spec=big, seg=1 << 17,
+                        base_kw=dict(max_batch_records=512, max_batch_bytes=1024), faults={0: {"drop": (0,)}},
+                        small=small)
+    try:
+        assert res[2][0].catchup_reserve() == 39 * 512 + 1024
+        assert res[3][0]["catchup_entries"] >= 4  # the gap took several rounds
+        lead = [res[1][0].state(p) for p in range(2)]
+        assert all(min(s["match"]) == s["log_end_offset"] for s in lead)
+    finally:
+        _close(res)
+
+
+def test_consumer_offsets_replicate_and_survive_leader_change_gpu(oracle_mod):
+    # ConsumerOffsetUpdateRequestProcessor.java:59-60: an offset commit is replicated; after the
+    # leadership moves, the new leader serves the same offsets (fetch starts there)
+    from repl_sim import moved_leadership
+    world, rf, ppr = 3, 3, 4
+    spec = StreamSpec(ppr, 300, "uniform", size=(1, 60), config_index=85)
+    commits = {1: {r: (np.repeat(np.arange(ppr, dtype=np.uint32), 2), np.tile(np.array([0, 3], np.uint32), ppr),
+                       np.arange(2 * ppr, dtype=np.uint64) * 7 + r) for r in range(world)}}
+    res = synced_rounds(oracle_mod, world, rf, ppr, group=2, rounds=3, spec=spec, commits=commits)
+    views, engs, oras = res[0], res[1], res[2]
+    try:
+        for g in range(world):
+            for p in range(ppr):
+                want = oras[g].consumer_offsets(p)
+                assert want.any()
+        # a fresh world of engines replays nothing: move leadership on the oracle-checked engines
+        # instead (their states equal the oracle's above) by a second GPU run with the move
+    finally:
+        _close(res)
+    new = moved_leadership(views)
+    base = EngineConfig(num_partitions=1, replication_factor=rf, segment_bytes=1 << 16, index_interval=256,
+                        max_batch_records=4096, max_batch_bytes=1 << 20, pipeline_depth=2)
+    cfgs = [rank_cfg(base, views[r], r) for r in range(world)]
+    hub = LocalHub(world)
+    engs = [Engine(c) for c in cfgs]
+    fetched = [None] * world
+    try:
+        def body(r):
+            e = engs[r]
+            e.attach_local(hub)
+            place(e, views[r])
+            for k in range(2):
+                if k == 1:
+                    rc, _ = e.commit_consumer_offset(*commits[1][r])
+                    assert rc == 0
+                for j in range(2):
+                    b = make_batch(spec, 1000 * r + 50 * k + j)
+                    e.append_async(b.pidx, b.lens, b.payload)
+                e.sync()
+            place(e, new[r])
+            moved = [p for p in range(len(views[r].gp))
+                     if new[r].ranks[p][new[r].leader_slot[p]] == r and views[r].ranks[p][views[r].leader_slot[p]] != r]
+            for p in moved:
+                e.become_leader(p, 2)
+            fetched[r] = {p: (e.consumer_offsets(p), e.fetch([p], [3], [5])[1]) for p in moved}
+            e.sync()
+
+        run_ranks(world, body)
+        for r in range(world):
+            for p, (offs, res_) in fetched[r].items():
+                g = int(views[r].gp[p])
+                src = g // ppr  # its old leader rank
+                q = int(np.flatnonzero(views[src].gp == g)[0])
+                want = np.zeros(cfgs[r].max_consumers, np.uint64)
+                want[0], want[3] = 14 * q + src, 14 * q + 7 + src
+                assert np.array_equal(offs, want), (r, p, offs, want)
+                assert int(res_["start_offset"][0]) == int(want[3]) and res_["status"][0] == 0
+        assert any(fetched[r] for r in range(world))
     finally:
         for e in engs:
             e.close()
