@@ -27,6 +27,7 @@ per batch.
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import glob
 import json
 import os
@@ -178,6 +179,54 @@ def host_leg(eng, batches, steps: int) -> dict:
                     "pidx + len + payload bytes over the wall time"}
 
 
+def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
+    """Appends and consumer fetches interleaved on one engine (configs[4]: concurrent consumer fetch
+    at lagging offsets): per round `appends` device-resident batches go to the pipeline, then one
+    rmq_fetch of every (partition, consumer) at max = 10 runs on the fetch stream, ordered after the
+    launches issued so far and before the next one (the pipeline is never flushed for it). Reports
+    both rates over the leg's wall time, and the consumers' lag bound. The consumers commit their
+    offsets (read-then-commit, ConsumerClientImpl.java:61-117) after each fetch, so they follow the
+    appends."""
+    P = spec.partitions
+    eng.sync()
+    hw = eng.commit_snapshot()
+    st0 = [eng.state(p) for p in range(0, P, max(1, P // 64))]
+    retained = int(np.mean([s["log_end_offset"] - s["log_start_offset"] for s in st0]))
+    g = np.random.default_rng(0x52495051)
+    pp = np.repeat(np.arange(P, dtype=np.uint32), consumers)
+    cc = np.tile(np.arange(consumers, dtype=np.uint32), P)
+    lag = (g.random(P * consumers) * (min(retained, int(hw.min())) // 2 + 1)).astype(np.int64)
+    off = (np.repeat(hw.astype(np.int64), consumers) - lag).astype(np.uint64)
+    eng.commit_consumer_offset(pp, cc, off)
+    hi = spec.size if isinstance(spec.size, int) else spec.size[1]
+    cap = P * consumers * mx * (16 + (hi + 15) // 16 * 16) + 4096
+    d_out = eng.device_alloc(cap)
+    maxr = np.full(P * consumers, mx, np.uint32)
+    recs = fetched = 0
+    k0 = 10_000
+    t0 = time.perf_counter()
+    for k in range(rounds):
+        for j in range(appends):
+            step(k0 + k * appends + j)
+        rc, res, _ = eng.fetch_device(pp, cc, maxr, d_out, cap)
+        if rc or np.any(res["status"] != 0):
+            raise SystemExit(f"bench: mixed leg fetch failed rc={rc} statuses={np.unique(res['status'])}")
+        n = res["count"].astype(np.uint64)
+        fetched += int(n.sum())
+        eng.commit_consumer_offset(pp, cc, res["start_offset"] + n)
+        recs += appends * spec.records
+    eng.sync()
+    dt = time.perf_counter() - t0
+    eng.device_free(d_out)
+    return {"append_msgs_per_s": recs / dt, "fetch_records_per_s": fetched / dt, "rounds": rounds,
+            "appends_per_round": appends, "fetch_requests_per_round": P * consumers, "max_records": mx,
+            "wall_s": dt, "lag_bound_records": min(retained, int(hw.min())) // 2,
+            "note": "appends (device-resident batches) and read-then-commit fetches of every (partition, "
+                    "consumer) interleaved; both rates over the same wall time; consumers start lagging "
+                    "the high watermark by U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not "
+                    "HBM-resident at 4,096 partitions, so it is bounded by what the rings retain)"}
+
+
 def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     """Consumer fetch over the bench engine's committed logs (SURVEY §8(d) B_fetch): per round every
     (partition, consumer) commits an offset lagging the high watermark by U[0, retained records]
@@ -195,7 +244,8 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     g = np.random.default_rng(0x52495050)
     pp = np.repeat(np.arange(P, dtype=np.uint32), consumers)
     cc = np.tile(np.arange(consumers, dtype=np.uint32), P)
-    out = {}
+    out = {"lag_bound": "U[0, retained records] per (partition, consumer): configs[4]'s U[0, 10^6] is not "
+                        "HBM-resident at 4,096 partitions"}
     for mx in (10, 1024):
         hi = spec.size if isinstance(spec.size, int) else spec.size[1]
         retained = int(sum(s["log_end_pos"] - s["log_start_pos"] for s in st))
@@ -313,6 +363,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     rank, world = grp.rank, grp.world
     spec = CONFIGS[args.config]
     rf = 5 if args.config == "D" else 3  # configs[4]: RF = 5
+    if args.config == "D" and world > 1:  # configs[4]: 4,096 partitions over the node, not per GPU
+        spec = dataclasses.replace(spec, partitions=max(1, spec.partitions // world))
     L = spec.size if isinstance(spec.size, int) else None
     view = rank_view(rank, world, spec.partitions, rf)  # world 1: every replica on this GPU
     # the rank's distinct input batches (rank-salted stream keys), made before the engine so that
@@ -432,7 +484,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
                        "parallelism": (f"partition-sharded x{world}, RF={rf} replicas over "
                                        + ("xGMI (RCCL)" if args.transport == "rccl" else
                                           "the in-process transport on ONE GPU (functional rehearsal)")
-                                       if world > 1 else "1 GPU, RF=3 replicas co-located"),
+                                       if world > 1 else f"1 GPU, RF={rf} replicas co-located"),
                        "batches_per_launch_group": args.group,
                        "rings": ring_report(rings, rf, args.group, len(view.gp))},
             "hbm_gbs_pipeline": alg * args.steps * world / t_max / 1e9,
@@ -457,6 +509,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
             out["host_path"] = host_leg(eng, host_batches, args.host_steps)
         if args.fetch_rounds > 0:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
+        if args.concurrent_rounds > 0 and world == 1:
+            out["mixed"] = mixed_leg(eng, step, spec, args.concurrent_rounds, 2 * args.group)
     if region is not None:
         eng.device_free(region)
     else:
@@ -496,8 +550,8 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
-    ap.add_argument("--concurrent-rounds", type=int, default=0,
-                    help="rounds of the append+fetch mixed leg (0: skip)")
+    ap.add_argument("--concurrent-rounds", type=int, default=20,
+                    help="rounds of the append+fetch mixed leg (1 GPU; 0: skip)")
     ap.add_argument("--host-steps", type=int, default=100,
                     help="batches of the host-memory leg (PCIe-inclusive rate, 1 GPU; 0: skip)")
     ap.add_argument("--watchdog", type=float, default=900.0, help="multi-GPU: exit a rank stuck this long [s]")

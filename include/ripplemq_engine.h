@@ -239,7 +239,11 @@ int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out);
 int rmq_sync(rmq_engine* e);
 
 /* Consumer-offset commits, applied in array order: last writer wins, no bounds or monotonic
-   check (PartitionStateMachine.java:71-77). status (nullable, host, [n]) reports per item. */
+   check (PartitionStateMachine.java:71-77). status (nullable, host, [n]) reports per item (not
+   leader, unknown partition, bad consumer id). The items reach the device table in order with the
+   append stream (one copy on the pipeline stream, no wait for the pipeline): a later rmq_fetch or
+   read-back sees them. With a replication transport the partition's row travels to every follower
+   with the next round (FORMAT.md §8, §9): it is on a quorum once that round's acks are in. */
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                                const uint64_t* offset, uint32_t n, int32_t* status);
 

@@ -445,6 +445,11 @@ void free_engine(rmq_engine* e) {
   if (e->done_host) hipHostFree(e->done_host);
   if (e->h_req) hipHostFree(e->h_req);
   if (e->h_res) hipHostFree(e->h_res);
+  for (auto& cs : e->cslot) {
+    if (cs.h) hipHostFree(cs.h);
+    if (cs.d) hipFree(cs.d);
+    if (cs.ev) hipEventDestroy(cs.ev);
+  }
   if (e->ev_main) hipEventDestroy(e->ev_main);
   if (e->ev_fetch) hipEventDestroy(e->ev_fetch);
   if (e->fetch_s) hipStreamDestroy(e->fetch_s);
@@ -1060,23 +1065,40 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
     vo.erase(vo.begin(), vo.begin() + k);
   }
   HIP_TRY(hipSetDevice(e->device));
-  int rc = quiesce(e);  // the ctl buffers are free; no flush: the pipeline never reads the table
-  if (rc) return rc;
+  // no flush and no wait for the pipeline (it never reads the table): the items go to the device
+  // with one copy on the pipeline stream, behind the launches issued so far, from a staging slot
+  // whose previous use has completed; a fetch or read-back issued later sees them
   const uint32_t m = (uint32_t)vp.size();
-  rc = ensure_ctl(e, m);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpy(e->d_ctl32, vp.data(), m * 4ull, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_ctl32 + e->ctl_cap, vc.data(), m * 4ull, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(e->d_ctl64, vo.data(), m * 8ull, hipMemcpyHostToDevice));
+  rmq_engine::CommitSlot& cs = e->cslot[e->cslot_next];
+  e->cslot_next ^= 1u;
+  if (cs.used) HIP_TRY(hipEventSynchronize(cs.ev));
+  if (m > cs.cap) {
+    if (cs.h) hipHostFree(cs.h);
+    if (cs.d) hipFree(cs.d);
+    cs.h = cs.d = nullptr;
+    cs.cap = 0;
+    const uint32_t cap = std::max<uint32_t>(m, 4096);
+    HIP_TRY(hipHostMalloc((void**)&cs.h, 16ull * cap, 0));
+    int rc = dalloc(&cs.d, 16ull * cap);
+    if (rc) return rc;
+    if (!cs.ev) HIP_TRY(hipEventCreateWithFlags(&cs.ev, hipEventDisableTiming));
+    cs.cap = cap;
+  }
+  std::memcpy(cs.h, vp.data(), 4ull * m);
+  std::memcpy(cs.h + 4ull * cs.cap, vc.data(), 4ull * m);
+  std::memcpy(cs.h + 8ull * cs.cap, vo.data(), 8ull * m);
+  HIP_TRY(hipMemcpyAsync(cs.d, cs.h, 16ull * cs.cap, hipMemcpyHostToDevice, e->main_s));
   ConsumerCommitArgs a{};
   a.st = e->st;
-  a.pidx = e->d_ctl32;
-  a.consumer = e->d_ctl32 + e->ctl_cap;
-  a.offset = e->d_ctl64;
+  a.pidx = reinterpret_cast<const uint32_t*>(cs.d);
+  a.consumer = reinterpret_cast<const uint32_t*>(cs.d + 4ull * cs.cap);
+  a.offset = reinterpret_cast<const uint64_t*>(cs.d + 8ull * cs.cap);
   a.n = m;
   launch_consumer_commit(a, e->main_s);
   HIP_TRY(hipGetLastError());
-  rc = quiesce(e);
+  HIP_TRY(hipEventRecord(cs.ev, e->main_s));
+  cs.used = true;
+  const int rc = check_err(e);
   return rc ? rc : rc_all;
 }
 

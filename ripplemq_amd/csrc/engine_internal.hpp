@@ -298,7 +298,17 @@ struct rmq_engine {
   uint32_t fetch_cap = 0;
   uint8_t* d_fetch_out = nullptr;
   uint64_t fetch_out_cap = 0;
-  // consumer-commit / ack scratch
+  // consumer-offset commits: two staging slots (pinned items -> device by one copy on the pipeline
+  // stream), so a commit is ordered with the append stream without waiting for it
+  struct CommitSlot {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;
+    uint32_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool used = false;
+  } cslot[2];
+  uint32_t cslot_next = 0;
+  // ack scratch
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;
   uint32_t ctl_cap = 0;

@@ -19,6 +19,14 @@ The engine's replica rings keep a retained window only (FORMAT.md §4): a fetch 
 * ``replay(directory, engine)`` rebuilds a fresh engine's logs from the files: the records are
   re-appended in offset order (the engine computes every CRC again) and the result is checked
   bit for bit against the files: offsets, and the ring bytes of the retained window.
+* The rest of a partition's durable state, as jraft keeps it in the partition's log and
+  ``raft_meta`` directory (``PartitionRaftServer.java:53,88-90``): every spill also writes the
+  partition's consumer-offset row (the reference's offset commits are log entries applied by
+  ``PartitionStateMachine.java:71-77``) to ``p<pidx>/offsets.bin`` and its term to
+  ``p<pidx>/meta.json``, each replaced atomically (write, fsync if asked, rename) when it changed;
+  ``replay`` restores both after the records (the term through ``rmq_become_leader``, so only
+  appends of the restored term advance the commit). Offsets and terms are durable at spill
+  granularity, like the records.
 
 Spill must run at least once per retained window of every partition (rings hold ``retain``
 batches of their traffic, ``ripplemq_amd/rings.py``); a cursor below a ring's start raises, since
@@ -26,6 +34,7 @@ records were lost before they were durable.
 """
 from __future__ import annotations
 
+import json
 import os
 
 import numpy as np
@@ -34,6 +43,8 @@ from . import _abi as A
 from .engine import EngineError
 
 SEG_SUFFIX = ".seg"
+OFFSETS_FILE = "offsets.bin"   # u64 consumer offsets of the partition (rmq_config.max_consumers)
+META_FILE = "meta.json"        # {"term": t}: the partition's raft_meta
 
 
 def record_positions(buf: np.ndarray, count: int | None = None) -> np.ndarray:
@@ -104,6 +115,38 @@ class _PartitionFiles:
 
     def _path(self, first: int) -> str:
         return os.path.join(self.dir, f"{first:020d}{SEG_SUFFIX}")
+
+    def _replace(self, name: str, data: bytes, fsync: bool) -> None:
+        tmp = os.path.join(self.dir, name + ".tmp")
+        with open(tmp, "wb") as f:
+            f.write(data)
+            if fsync:
+                f.flush()
+                os.fsync(f.fileno())
+        os.replace(tmp, os.path.join(self.dir, name))
+
+    def save_state(self, offsets: np.ndarray, term: int, fsync: bool) -> None:
+        """The partition's consumer-offset row and term, each rewritten only when it changed."""
+        row = np.ascontiguousarray(offsets, np.uint64).tobytes()
+        if row != self.load_offsets_bytes():
+            self._replace(OFFSETS_FILE, row, fsync)
+        meta = self.load_meta()
+        if meta.get("term") != int(term):
+            self._replace(META_FILE, json.dumps({"term": int(term)}).encode(), fsync)
+
+    def load_offsets_bytes(self) -> bytes:
+        try:
+            with open(os.path.join(self.dir, OFFSETS_FILE), "rb") as f:
+                return f.read()
+        except FileNotFoundError:
+            return b""
+
+    def load_meta(self) -> dict:
+        try:
+            with open(os.path.join(self.dir, META_FILE)) as f:
+                return json.load(f)
+        except FileNotFoundError:
+            return {}
 
     @property
     def end(self) -> int:
@@ -209,6 +252,10 @@ class DurableLog:
             self.engine.commit_consumer_offset(np.asarray(adv_p, np.uint32),
                                                np.full(len(adv_p), self.cursor, np.uint32),
                                                np.asarray(adv_o, np.uint64))
+        for k, p in enumerate(pidx.tolist()):  # offsets and term of the partitions led here
+            if int(res["status"][k]) == A.RMQ_ENOTLEADER:
+                continue
+            self.parts[p].save_state(self.engine.consumer_offsets(p), self.engine.state(p)["term"], self.fsync)
         return moved
 
     def read(self, p: int, off: int, max_messages: int) -> list[tuple[int, int, bytes]]:
@@ -224,7 +271,8 @@ def replay(directory: str, engine, partitions, *, batch_records: int = 65536) ->
     """Rebuild a fresh engine's logs from segment files: every record is appended again in offset
     order (the engine recomputes its CRC32C) and must get the offset the file holds; afterwards
     the retained window of every partition's lowest local ring must equal the files' bytes for it.
-    Returns {"records": n, "partitions": k}."""
+    Then each partition's term (rmq_become_leader) and consumer-offset row come back from its
+    meta and offsets files. Returns {"records": n, "partitions": k, "terms": t, "offset_rows": o}."""
     files = {int(p): _PartitionFiles(directory, int(p), 1 << 62) for p in partitions}
     recs = {}
     for p, f in files.items():
@@ -268,4 +316,18 @@ def replay(directory: str, engine, partitions, *, batch_records: int = 65536) ->
         if ring != data:
             raise EngineError(A.RMQ_EINVAL, f"replay of partition {p}: ring bytes differ from the files "
                                             f"(a CRC or payload changed)")
-    return {"records": total, "partitions": len(recs)}
+    terms = rows = 0
+    for p, f in files.items():
+        term = int(f.load_meta().get("term", 0))
+        if term > engine.state(p)["term"]:
+            engine.become_leader(p, term)
+            terms += 1
+        raw = f.load_offsets_bytes()
+        if raw:
+            offs = np.frombuffer(raw, np.uint64)
+            n = min(len(offs), engine.cfg.max_consumers)
+            rc, st = engine.commit_consumer_offset(np.full(n, p, np.uint32), np.arange(n, dtype=np.uint32), offs[:n])
+            if rc:
+                raise EngineError(rc, f"replay of partition {p}: consumer offsets")
+            rows += 1
+    return {"records": total, "partitions": len(recs), "terms": terms, "offset_rows": rows}

@@ -174,7 +174,7 @@ def test_leader_change_truncates_follower(oracle_mod):
 
 
 def synced_rounds(oracle_mod, world, rf, ppr, group, rounds, spec, seg=1 << 16, interval=256, base_kw=None,
-                  faults=None, commits=None, small=None):
+                  faults=None, commits=None, small=None, small_from=1):
     """Rounds with an rmq_sync on every rank after each one, so every plan sees the acks of every
     round before it — exactly the oracle's order (tests/repl_sim.py): each round's regions, the
     catch-up verdicts and the converged state must match bit for bit.
@@ -190,7 +190,7 @@ def synced_rounds(oracle_mod, world, rf, ppr, group, rounds, spec, seg=1 << 16, 
     cfgs = [rank_cfg(base, views[r], r) for r in range(world)]
 
     def batches_of(r, k):
-        sp = small if (small is not None and k >= 1) else spec
+        sp = small if (small is not None and k >= small_from) else spec
         return [make_batch(sp, 1000 * r + 50 * k + j) for j in range(group)]
 
     hub = LocalHub(world)
@@ -267,8 +267,8 @@ def test_crc_refusal_then_catch_up_gpu(oracle_mod):
     try:
         stats = res[3]
         assert stats[1]["refused_crc"] == 1 and stats[0]["catchup_entries"] == 1, stats
-        views, engs, oras = res[0], res[1], res[2]
-        lead = [engs[0].state(p) for p in range(views[0].led)]
+        views, oras = res[0], res[2]
+        lead = [oras[0].state(p) for p in range(views[0].led)]  # equal to the GPU's (checked above)
         assert all(s["commit"] == s["log_end_offset"] == s["match"][0] for s in lead)
         assert all(min(s["match"]) == s["log_end_offset"] for s in lead)  # every follower caught up
     finally:
@@ -281,7 +281,7 @@ def test_missed_round_then_catch_up_gpu(oracle_mod):
     try:
         stats = res[3]
         assert stats[1]["refused_log"] > 0 and stats[2]["refused_log"] > 0 and stats[0]["catchup_entries"] >= 2
-        lead = [res[1][0].state(p) for p in range(res[0][0].led)]
+        lead = [res[2][0].state(p) for p in range(res[0][0].led)]
         assert all(min(s["match"]) == s["log_end_offset"] for s in lead)
     finally:
         _close(res)
@@ -292,13 +292,15 @@ def test_partial_catch_up_gpu(oracle_mod):
     # sparse-index entries, one per round
     big = StreamSpec(2, 400, "uniform", size=(80, 120), config_index=83)
     small = StreamSpec(2, 4, "uniform", size=(10, 20), config_index=84)
-    res = synced_rounds(oracle_mod, world=3, rf=3, ppr=2, group=1, rounds=12, spec=big, seg=1 << 17,
-                        base_kw=dict(max_batch_records=512, max_batch_bytes=1024), faults={0: {"drop": (0,)}},
-                        small=small)
+    # three rounds of ~51 KB each are missed: the gap (~150 KB per follower) is over twice the
+    # reserve of one round bound (39 x 400 + 48 KiB)
+    res = synced_rounds(oracle_mod, world=3, rf=3, ppr=2, group=1, rounds=12, spec=big, seg=1 << 19,
+                        base_kw=dict(max_batch_records=400, max_batch_bytes=48 << 10),
+                        faults={k: {"drop": (0,)} for k in range(3)}, small=small, small_from=3)
     try:
-        assert res[2][0].catchup_reserve() == 39 * 512 + 1024
+        assert res[2][0].catchup_reserve() == 39 * 400 + (48 << 10)
         assert res[3][0]["catchup_entries"] >= 4  # the gap took several rounds
-        lead = [res[1][0].state(p) for p in range(2)]
+        lead = [res[2][0].state(p) for p in range(2)]
         assert all(min(s["match"]) == s["log_end_offset"] for s in lead)
     finally:
         _close(res)
@@ -313,7 +315,7 @@ def test_consumer_offsets_replicate_and_survive_leader_change_gpu(oracle_mod):
     commits = {1: {r: (np.repeat(np.arange(ppr, dtype=np.uint32), 2), np.tile(np.array([0, 3], np.uint32), ppr),
                        np.arange(2 * ppr, dtype=np.uint64) * 7 + r) for r in range(world)}}
     res = synced_rounds(oracle_mod, world, rf, ppr, group=2, rounds=3, spec=spec, commits=commits)
-    views, engs, oras = res[0], res[1], res[2]
+    views, oras = res[0], res[2]
     try:
         for g in range(world):
             for p in range(ppr):

@@ -6,7 +6,7 @@ import pytest
 from repl_sim import exchange_round, place, rank_batches, rank_cfg
 from ripplemq_amd.engine import EngineConfig
 from ripplemq_amd.sharding import rank_view, replica_ranks
-from ripplemq_amd.workload import StreamSpec
+from ripplemq_amd.workload import StreamSpec, make_batch
 
 BASE = EngineConfig(num_partitions=1, replication_factor=3, segment_bytes=1 << 16, index_interval=256,
                     max_batch_records=4096)
@@ -214,6 +214,27 @@ def test_missed_round_then_catch_up(oracle_mod):
                            for p in range(ppr))
         check_followers(views, oras, ppr, 3)
         assert oras[0].counters()[4] >= 2  # catch-up entries to both followers
+    finally:
+        for o in oras:
+            o.close()
+
+
+def test_partial_catch_up_after_three_missed_rounds(oracle_mod):
+    # the GPU test's scenario (test_partial_catch_up_gpu) on the oracle alone
+    world, ppr = 3, 2
+    base = EngineConfig(num_partitions=1, replication_factor=3, segment_bytes=1 << 19, index_interval=256,
+                        max_batch_records=400, max_batch_bytes=48 << 10, pipeline_depth=1)
+    views, oras = build(oracle_mod, world, ppr, base=base)
+    big = StreamSpec(2, 400, "uniform", size=(80, 120), config_index=83)
+    small = StreamSpec(2, 4, "uniform", size=(10, 20), config_index=84)
+    try:
+        for k in range(12):
+            for r in range(world):
+                b = make_batch(small if k >= 3 else big, 1000 * r + 50 * k)
+                oras[r].append(b.pidx, b.lens, b.payload)
+            exchange_round(oras, drop=(0,) if k < 3 else ())
+        assert oras[0].counters()[4] >= 4
+        check_followers(views, oras, ppr, 3)
     finally:
         for o in oras:
             o.close()

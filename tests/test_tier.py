@@ -63,13 +63,32 @@ def _flow(make_engine, tmp_path, seg_file_bytes):
         again = DurableLog(eng, str(tmp_path), range(P), cursor, segment_file_bytes=seg_file_bytes)
         assert [again.end(p) for p in range(P)] == ends
         assert [m for _, _, m in again.read(1, 5, 7)] == ref.sms[1].messages[5:12]
-    # replay into a fresh engine: offsets and ring bytes checked against the files by replay()
+        # the offsets and terms jraft keeps in the log and raft_meta: a new term and a consumer
+        # that read part of partition 2, then one more spill
+        eng.become_leader(2, 7)
+        sm = b.state_machine(f"{TOPIC}-2")
+        got = sm.handleBatchRead(MessageBatchReadRequest("mid-consumer", 25, TOPIC, 2))
+        assert sm.handleConsumerOffsetUpdateRequest(
+            ConsumerOffsetUpdateRequest("mid-consumer", got.getOffset() + len(got.getMessages()), TOPIC, 2)).isSuccess()
+        tier.spill()
+        saved = [eng.consumer_offsets(p).copy() for p in range(P)]
+        terms = [eng.state(p)["term"] for p in range(P)]
+        assert terms[2] == 7 and saved[2][d.consumer("mid-consumer")] == 25
+    # replay into a fresh engine: offsets and ring bytes checked against the files by replay(); the
+    # consumer offsets and terms come back from offsets.bin / meta.json
     big = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
                        max_consumers=4, max_batch_records=4096)
     with make_engine(big) as fresh:
         out = replay(str(tmp_path), fresh, range(P), batch_records=500)
-        assert out["records"] == sum(ends)
+        assert out["records"] == sum(ends) and out["terms"] == 1 and out["offset_rows"] == P
         assert [fresh.state(p)["log_end_offset"] for p in range(P)] == ends
+        assert [fresh.state(p)["term"] for p in range(P)] == terms
+        for p in range(P):
+            assert np.array_equal(fresh.consumer_offsets(p), saved[p]), p
+        # the restarted broker serves the mid consumer from where it committed
+        b2 = PartitionBroker(d, fresh, messages_as_str=False)
+        nxt = b2.state_machine(f"{TOPIC}-2").handleBatchRead(MessageBatchReadRequest("mid-consumer", 5, TOPIC, 2))
+        assert nxt.getOffset() == 25 and nxt.getMessages() == ref.sms[2].messages[25:30]
     return ends
 
 
