@@ -368,3 +368,48 @@ def test_consumer_offsets_replicate_and_survive_leader_change_gpu(oracle_mod):
         for e in engs:
             e.close()
         hub.close()
+
+
+def test_idle_ranks_keep_rounds_flowing_gpu():
+    # ripplemq_amd.pacer: every rank submits one batch per tick (empty when idle). Rank 0 produces
+    # once; ranks 1 and 2 never produce. Without any rmq_sync, rank 0's records commit on a quorum
+    # once enough ticks have passed, and its followers hold them.
+    from ripplemq_amd.pacer import RoundPacer
+    world, rf, ppr, group = 3, 3, 4, 2
+    base = EngineConfig(num_partitions=1, replication_factor=rf, segment_bytes=1 << 16, index_interval=256,
+                        max_batch_records=4096, max_batch_bytes=1 << 20, pipeline_depth=group)
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    cfgs = [rank_cfg(base, views[r], r) for r in range(world)]
+    spec = StreamSpec(ppr, 500, "uniform", size=(1, 100), config_index=86)
+    hub = LocalHub(world)
+    engs = [Engine(c) for c in cfgs]
+    got = [None] * world
+    try:
+        def body(r):
+            e = engs[r]
+            e.attach_local(hub)
+            place(e, views[r])
+            pacer = RoundPacer(e, epoch=0.0, tick_s=1.0, clock=lambda: 0.0)
+            if r == 0:
+                b = make_batch(spec, 7)
+                pacer.submit(b.pidx, b.lens, b.payload)
+            done, first = [], None
+            for ticks in range(1, 25):  # every rank ticks the same number of times (rounds are collective)
+                pacer.tick()
+                if r == 0 and first is None:
+                    done += pacer.committed()  # rmq_poll_commit without a flush: not collective
+                    if done:
+                        first = ticks
+            got[r] = (first, done)
+            e.sync()  # collective, before the engines go away
+
+        run_ranks(world, body)
+        first, done = got[0]
+        assert done and first is not None, "rank 0's records never committed without an rmq_sync"
+        pidx, offs = done[0]
+        assert len(pidx) == spec.records and np.all(offs != np.uint64(0xFFFFFFFFFFFFFFFF))
+        assert first <= 16, first  # ~ (3 pipeline launches + 3 ack launches) x 2 batches per round
+    finally:
+        for e in engs:
+            e.close()
+        hub.close()
