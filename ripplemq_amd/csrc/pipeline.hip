@@ -798,6 +798,8 @@ __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
       }
     }
   }
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(1);
   if (A.xp2.n_out) {
     // replication transport: the last stage-2 workgroup to finish lays out the group's outbox
     // (every storing wave drained, then one counter add per workgroup; the last adder reads the
@@ -811,7 +813,7 @@ __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
     if (s_last) stage2_plan(A);
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(1);
+  PIPE_STAMP(2);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -126,40 +126,46 @@ constexpr u32 kBadCrc = 1u, kBadLog = 2u, kBadStale = 4u, kBadMissed = 8u;
 
 __global__ void ingest_prepare_kernel(IngestArgs A) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= A.n_in) return;
-  const u32 src = source_of_entry(A, e), k = e - A.xi_start[src];
-  const DevState& st = A.st;
-  const u32 p = A.xi_p[e];
-  u64 leo = st.leo[p], used = st.used[p];
-  u32 bad = 0;
-  if (!A.rbytes[src]) {
-    bad = kBadMissed;  // the leader sent nothing this round (it failed before replicating)
-  } else {
-    const RegionView R = region_of(A, src);
-    if (!R.sane) {
-      bad = kBadLog;
+  const bool in = e < A.n_in;
+  u32 nc = 0;  // copy work items of the entry
+  if (in) {
+    const u32 src = source_of_entry(A, e), k = e - A.xi_start[src];
+    const DevState& st = A.st;
+    const u32 p = A.xi_p[e];
+    u64 leo = st.leo[p], used = st.used[p];
+    u32 bad = 0;
+    if (!A.rbytes[src]) {
+      bad = kBadMissed;  // the leader sent nothing this round (it failed before replicating)
     } else {
-      const DirView d = dir_of(R, k);
-      if (d.term < st.term[p]) {
-        bad = kBadStale;  // a stale leader
-      } else if (d.first < leo && d.first >= st.start_off[p]) {
-        used = follower_pos(st, p, A.xi_slot[e], d.first);  // the leader's log wins: truncate
-        leo = d.first;
-      }
-      if (!bad && d.first != leo) bad = kBadLog;  // does not continue the follower's log
-      if (!bad && d.bytes16) {  // copy work items of the entry (order does not matter)
-        const u32 nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
-        const u32 at = atomicAdd(A.n_items, nc);
-        for (u32 c = 0; c < nc; ++c) {
-          A.items[2 * (at + c)] = e;
-          A.items[2 * (at + c) + 1] = c;
+      const RegionView R = region_of(A, src);
+      if (!R.sane) {
+        bad = kBadLog;
+      } else {
+        const DirView d = dir_of(R, k);
+        if (d.term < st.term[p]) {
+          bad = kBadStale;  // a stale leader
+        } else if (d.first < leo && d.first >= st.start_off[p]) {
+          used = follower_pos(st, p, A.xi_slot[e], d.first);  // the leader's log wins: truncate
+          leo = d.first;
         }
+        if (!bad && d.first != leo) bad = kBadLog;  // does not continue the follower's log
+        if (!bad) nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
       }
     }
+    A.bad[e] = bad;
+    A.base[2 * e] = leo;
+    A.base[2 * e + 1] = used;
   }
-  A.bad[e] = bad;
-  A.base[2 * e] = leo;
-  A.base[2 * e + 1] = used;
+  // the items' slots (their order does not matter): one counter add per wave
+  const u32 inc = wave_incl_scan(nc);
+  const u32 tot = (u32)__shfl((int)inc, 63, 64);
+  u32 at = 0;
+  if (lane_id() == 0 && tot) at = atomicAdd(A.n_items, tot);
+  at = (u32)__shfl((int)at, 0, 64) + inc - nc;
+  for (u32 c = 0; c < nc; ++c) {
+    A.items[2 * (at + c)] = e;
+    A.items[2 * (at + c) + 1] = c;
+  }
 }
 
 __global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
@@ -328,7 +334,7 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
   }
   const RegionView R = region_of(A, src);
   const DirView d = dir_of(R, k);
-  const u64 bleo = A.base[2 * e], bused = A.base[2 * e + 1];
+  const u64 bused = A.base[2 * e + 1];
   const u64 nleo = d.first + d.count, nused = bused + 16ull * d.bytes16;
   if (owner) {
     const u32 ilog = st.interval_log2;
@@ -381,7 +387,6 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
     }
   }
   if (d.count) atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)d.count);
-  (void)bleo;
   A.ackout[2 * e] = nleo;
   A.ackout[2 * e + 1] = nused;
 }

@@ -72,6 +72,9 @@ for step in "$@"; do
         env "$var=$val" timeout -k 10 200 python bench.py --steps 600 --warmup 60 $Q > "gpurun_out/${T}_${var}_${val}_600.json" 2>&1 || exit 1
         env "$var=$val" timeout -k 10 200 python bench.py --steps 20 --warmup 5 $Q > "gpurun_out/${T}_${var}_${val}_20.json" 2>&1 || exit 1
       done ;;
+    xstamps)  # phase stamps of one launch of the 2-rank rehearsal (transport kernel, 8 waves/workgroup)
+      RMQ_STAMPS=gpurun_out/${T}_xst.csv RMQ_STAMPS_AT=60 run 300 "${T}_xstamped.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
+      python tools/pipe_stamps.py "gpurun_out/${T}_xst.csv" > "gpurun_out/${T}_xstamps.txt" 2>&1 ;;
     *) echo "[gpu.sh] unknown step $step"; exit 2 ;;
   esac
 done
