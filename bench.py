@@ -268,7 +268,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             t0 = time.perf_counter()
             rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
             t_wall += time.perf_counter() - t0
-            _, ms_f = eng.profile_query(3)  # the three kernels' own dispatch-recorded spans, summed
+            _, ms_f = eng.profile_query(3)  # the two kernels' own dispatch-recorded spans, summed
             _, ms_r = eng.profile_query(4)  # first kernel start to last kernel end: the fetch's GPU time
             eng.profile(False)
             if rc or np.any(res["status"] != 0):
@@ -278,7 +278,10 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             recs += int(res["count"].sum())
             nbytes += int(res["bytes"].sum())
         eng.device_free(d_out)
-        alg = 2 * nbytes + search_bytes * rounds
+        # B_fetch = 2 (H + L) per returned record (fixed-size configs: exact; mixed
+        # sizes: the records' bytes in the log layout, which adds their padding to 16 bytes)
+        rec_bytes = recs * (16 + spec.size) if isinstance(spec.size, int) else nbytes
+        alg = 2 * rec_bytes + search_bytes * rounds
         # the dispatch-recorded span of a launch starts when the command processor takes its packet,
         # which can precede the end of the launch before it, so the summed spans overstate the GPU
         # time; the roofline uses the region from the first start to the last end (no host gaps:
@@ -288,7 +291,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                            "requests": P * consumers, "rounds": rounds,
                            "roofline": {"bound": "hbm", "achieved": alg / t_reg / 1e9, "peak": HBM_PEAK_GBS,
                                         "unit": "GB/s", "frac": alg / t_reg / 1e9 / HBM_PEAK_GBS,
-                                        "kernels": "rmq::fetch_resolve + fetch_place + fetch_gather",
+                                        "kernels": "rmq::fetch_resolve + fetch_gather (placement fused)",
                                         "mean_us_per_fetch": t_reg / rounds * 1e6,
                                         "kernel_spans_us_summed": t_kern / rounds * 1e6}}
     return out

@@ -296,8 +296,8 @@ int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int ki
    kernels 0 and 1: the pipeline launches from the first one after enable up to the next drain
    (sync, control call, read-back) timed as ONE region (no events between launches): total_ms =
    region time; launches = pipeline launches in it (kernel 0) or batches they applied (kernel 1).
-   kernel 3: rmq_fetch, the summed durations of its three kernels; 4: rmq_fetch, first kernel start
-   to last kernel end (host launch gaps included). 2: unused. */
+   kernel 3: rmq_fetch, the summed durations of its two kernels (resolve, place + gather); 4:
+   rmq_fetch, first kernel start to last kernel end (host launch gaps included). 2: unused. */
 int rmq_profile_enable(rmq_engine* e, int enable);
 int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* total_ms);
 /* Device name / CU count for reports. */

@@ -422,7 +422,7 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, e->d_crc,
-                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_fetch_out,
+                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_csum, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -1118,6 +1118,8 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     hipFree(e->d_res);
     hipFree(e->d_aux);
     hipFree(e->d_cpre);
+    hipFree(e->d_csum);
+    e->d_csum = nullptr;
     if (e->h_req) hipHostFree(e->h_req);
     if (e->h_res) hipHostFree(e->h_res);
     e->d_req = nullptr;
@@ -1130,6 +1132,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4 + 2);
     if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
     if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 4);
+    if (!rc) rc = dalloc(&e->d_csum, (size_t)cap / kFetchChunk + 2);
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
@@ -1160,18 +1163,18 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     a.res = e->d_res;
     a.aux = e->d_aux;
     a.cpre = e->d_cpre;
+    a.csum = e->d_csum;
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
-    a.gather_wgs = std::max<uint32_t>(1u, 32u * e->cu_count);
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
     HIP_TRY(hipMemcpyAsync(e->d_req, e->h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
-    hipEvent_t ev[6] = {};
-    if (e->profile) {  // kernel 3: the three kernels' own durations; 4: first start to last end
+    hipEvent_t ev[4] = {};
+    if (e->profile) {  // kernel 3: the two kernels' own durations; 4: first start to last end
       for (hipEvent_t& x : ev) x = pool_event(e);
-      for (int k = 0; k < 3; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
-      e->prof[4].push_back({ev[0], ev[5]});
+      for (int k = 0; k < 2; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
+      e->prof[4].push_back({ev[0], ev[3]});
     }
     launch_fetch(a, e->fetch_s, e->profile ? ev : nullptr);
     HIP_TRY(hipGetLastError());

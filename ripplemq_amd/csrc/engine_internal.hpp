@@ -292,6 +292,7 @@ struct rmq_engine {
   uint64_t* d_res = nullptr;
   uint64_t* d_aux = nullptr;
   uint32_t* d_cpre = nullptr;
+  uint64_t* d_csum = nullptr;
   bool trace = false;           // RMQ_TRACE: print every launch's roles to stderr
   uint32_t* h_req = nullptr;   // pinned
   uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}

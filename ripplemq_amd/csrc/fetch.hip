@@ -7,12 +7,16 @@
 //          §5: E[m] = first record starting at or after m*I; 64 probes per round, one round per
 //          factor 64 of index entries), then the record headers of the 1 KiB after the entry found
 //          are loaded at once (a lane per 16 bytes) and walked in registers;
-//  place   (one workgroup): exclusive scan of the requests' bytes -> compact output positions
+//          each workgroup adds its requests' bytes to the sum of their chunk of 256 requests;
+//  gather  (workgroup per 16 requests, a wave per 4): the output position of its first request from
+//          the chunk sums before it and the byte counts of its chunk before it (at most 64 + 255
+//          values, L2-resident), an exclusive scan over its 16 requests -> compact output positions
 //          (into the result rows' out_pos), ENOSPC marking (every request's bytes count, served or
-//          not: FORMAT.md §7);
-//  gather  (wave per request): 16-byte loads from the lowest local replica ring, four in flight per
-//          lane, 16-byte stores to the output. Records and output positions are 16-byte aligned
+//          not: FORMAT.md §7); then 16-byte loads from the lowest local replica ring, four in flight
+//          per lane, 16-byte stores to the output. Records and output positions are 16-byte aligned
 //          (FORMAT.md §1), so no piece straddles a record, the ring end or an output boundary.
+//          (Round 2 placed with a single 1024-thread workgroup between the two: 12.6 us of the
+//          max = 10 fetch of 16,384 requests with the rest of the GPU idle.)
 //
 // The three kernels run on the engine's fetch stream, after the last pipeline launch the host had
 // issued and before the next one (engine.cpp orders the two streams with events), so the committed
@@ -144,87 +148,65 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
     a.aux[2 * r + 0] = pos0;
     a.aux[2 * r + 1] = (ring_off << 6) | (st.ring[p < st.P ? p : 0] & 63ull);  // ring | log2(ring bytes)
     a.cpre[r] = (u32)bytes;
+    if (bytes) atomicAdd((unsigned long long*)&a.csum[r / kFetchChunk], (unsigned long long)bytes);
   }
 }
 
-// One workgroup: output positions = exclusive scan of the requests' bytes in request order; each
-// thread scans 16 consecutive requests per pass (16-byte loads of the byte counts, 16-byte stores of
-// the compact positions: one load round per 16384 requests).
-__global__ __launch_bounds__(1024) void fetch_place_kernel(FetchArgs a) {
-  __shared__ u64 sh[16];
-  constexpr u32 kPer = 16;
-  const u32 tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  u64 carry = 0;
-  for (u32 b = 0; b < a.n; b += 1024 * kPer) {
-    const u32 r0 = b + tid * kPer;
-    u32 nb[kPer];
-    if (r0 + kPer <= a.n) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.cpre + r0);
-#pragma unroll
-      for (u32 k = 0; k < kPer / 4; ++k) {
-        const uint4 v = src[k];
-        nb[4 * k] = v.x;
-        nb[4 * k + 1] = v.y;
-        nb[4 * k + 2] = v.z;
-        nb[4 * k + 3] = v.w;
-      }
-    } else {
-#pragma unroll
-      for (u32 k = 0; k < kPer; ++k) nb[k] = r0 + k < a.n ? a.cpre[r0 + k] : 0u;
-    }
-    u64 loc = 0;
-#pragma unroll
-    for (u32 k = 0; k < kPer; ++k) loc += nb[k];
-    const u64 inc = wave_incl_scan(loc);
-    if (l == 63) sh[w] = inc;
-    __syncthreads();
-    u64 cur = carry + inc - loc, tot = 0;
-#pragma unroll
-    for (u32 k = 0; k < 16; ++k) {
-      cur += k < w ? sh[k] : 0ull;
-      tot += sh[k];
-    }
-    u64 pos[kPer];
-#pragma unroll
-    for (u32 k = 0; k < kPer; ++k) {
-      pos[k] = cur;
-      if (nb[k] && cur + nb[k] > a.out_cap && r0 + k < a.n) {  // does not fit: not served (rare)
-        a.res[4 * (r0 + k) + 2] = 0;
-        a.res[4 * (r0 + k) + 3] = (u64)(uint32_t)kNoSpc;
-      }
-      cur += nb[k];
-    }
-#pragma unroll
-    for (u32 k = 0; k < kPer; ++k)
-      if (r0 + k < a.n) a.res[4 * (r0 + k) + 1] = pos[k];  // out_pos (one result copy to the host)
-    carry += tot;
-    __syncthreads();
-  }
-  if (tid == 0) a.res[4ull * a.n] = carry;  // bytes needed
-}
+constexpr u32 kGQ = 4;          // requests per gather wave
+constexpr u32 kGR = kFW * kGQ;  // requests per gather workgroup
 
+// Placement + gather: workgroup per kGR consecutive requests.
 __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
+  __shared__ u64 s_red[kFW];
+  __shared__ u64 s_pos[kGR];
   const DevState& st = a.st;
-  const u32 lane = lane_id();
-  const u32 nw = gridDim.x * kFW;
-  for (u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6)); r < a.n; r += nw) {
-    const u64 nb = a.res[4 * r + 2] >> 32;  // 0 for requests not served
-    if (!nb) continue;
+  const u32 tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
+  const u32 r0 = blockIdx.x * kGR, c0 = r0 / kFetchChunk;
+  // bytes of every request before r0: the chunk sums before its chunk, then its chunk's requests
+  u64 v = 0;
+  for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[k];
+  for (u32 k = c0 * kFetchChunk + tid; k < r0; k += 64 * kFW) v += a.cpre[k];
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if (lane == 0) s_red[w] = v;
+  // this workgroup's requests: exclusive scan of their bytes
+  const u32 rr = r0 + tid;
+  const u64 nb = tid < kGR && rr < a.n ? a.cpre[rr] : 0ull;
+  const u64 inc = wave_incl_scan(nb);  // kGR <= 64: one wave holds them all
+  __syncthreads();
+  const u64 base = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+  if (tid < kGR && rr < a.n) {
+    const u64 pos = base + inc - nb;
+    s_pos[tid] = pos;
+    a.res[4 * rr + 1] = pos;  // out_pos (one result copy to the host)
+    if (nb && pos + nb > a.out_cap) {  // does not fit: not served (rare); its bytes still count
+      a.res[4 * rr + 2] = 0;
+      a.res[4 * rr + 3] = (u64)(uint32_t)kNoSpc;
+    }
+    if (rr + 1 == a.n) a.res[4ull * a.n] = pos + nb;  // bytes needed
+  }
+  __syncthreads();
+  for (u32 q = 0; q < kGQ; ++q) {
+    const u32 i = w * kGQ + q, r = r0 + i;
+    if (r >= a.n) break;
+    const u64 pos0_out = s_pos[i];
+    const u64 nbr = a.cpre[r];
+    if (!nbr || pos0_out + nbr > a.out_cap) continue;
     const u64 pos0 = a.aux[2 * r + 0];
     const uint8_t* ring = st.logs + (a.aux[2 * r + 1] >> 6);
     const u64 mask = (1ull << (a.aux[2 * r + 1] & 63ull)) - 1ull;
-    uint8_t* out = a.out + a.res[4 * r + 1];
-    const u64 pieces = nb >> 4;
-    u64 q = lane;
-    for (; q + 192 < pieces; q += 256) {  // four 16-byte pieces in flight per lane
-      uint4 v[4];
+    uint8_t* out = a.out + pos0_out;
+    const u64 pieces = nbr >> 4;
+    u64 p = lane;
+    for (; p + 192 < pieces; p += 256) {  // four 16-byte pieces in flight per lane
+      uint4 x[4];
 #pragma unroll
-      for (u32 u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (q + 64 * u)) & mask));
+      for (u32 u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 64 * u)) & mask));
 #pragma unroll
-      for (u32 u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(out + 16ull * (q + 64 * u)) = v[u];
+      for (u32 u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(out + 16ull * (p + 64 * u)) = x[u];
     }
-    for (; q < pieces; q += 64)
-      *reinterpret_cast<uint4*>(out + 16ull * q) = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * q) & mask));
+    for (; p < pieces; p += 64)
+      *reinterpret_cast<uint4*>(out + 16ull * p) = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * p) & mask));
   }
 }
 
@@ -233,11 +215,11 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
+  (void)hipMemsetAsync(a.csum, 0, 8ull * (a.n / kFetchChunk + 1), s);
   hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW - 1) / kFW), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);
-  hipExtLaunchKernelGGL(fetch_place_kernel, dim3(1), dim3(1024), 0, s, e ? e[2] : nullptr, e ? e[3] : nullptr, 0, a);
-  hipExtLaunchKernelGGL(fetch_gather_kernel, dim3(std::min<u32>((a.n + kFW - 1) / kFW, a.gather_wgs)), dim3(64 * kFW), 0,
-                        s, e ? e[4] : nullptr, e ? e[5] : nullptr, 0, a);
+  hipExtLaunchKernelGGL(fetch_gather_kernel, dim3((a.n + kGR - 1) / kGR), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
+                        e ? e[3] : nullptr, 0, a);
 }
 
 }  // namespace rmq

@@ -237,12 +237,15 @@ struct FetchArgs {
   const uint32_t* req;       // [n][4] {pidx, consumer, max, reserved}
   uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}, then {bytes needed}
   uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
-  uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> place), 16-byte aligned
+  uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> gather), 16-byte aligned
+  uint64_t* csum;            // [n / kFetchChunk + 1] bytes of each chunk of kFetchChunk requests
+                             //   (resolve adds, zeroed before it)
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
   uint32_t n;
-  uint32_t gather_wgs;       // gather grid cap (a wave per request, looping)
+  uint32_t pad;
 };
+constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
 
 
 
@@ -314,7 +317,7 @@ uint32_t pipeline_wgs_per_cu(uint32_t threads);  // resident workgroups per CU o
 void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
-void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev6);
+void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
