@@ -181,7 +181,8 @@ def host_leg(eng, batches, steps: int) -> dict:
 
 def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
     """Appends and consumer fetches interleaved on one engine (configs[4]: concurrent consumer fetch
-    at lagging offsets): per round `appends` device-resident batches go to the pipeline, then one
+    at lagging offsets): per round `appends` device-resident batches (one launch group) go to the
+    pipeline, then one
     rmq_fetch of every (partition, consumer) at max = 10 runs on the fetch stream, ordered after the
     launches issued so far and before the next one (the pipeline is never flushed for it). Reports
     both rates over the leg's wall time, and the consumers' lag bound. The consumers commit their
@@ -215,10 +216,9 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
         n = res["count"].astype(np.uint64)
         fetched += int(n.sum())
         nxt = res["start_offset"] + n
-        gone = np.flatnonzero(st == -6)  # RMQ_EOFFSET: the hot partitions' rings moved past a slow
-        if gone.size:                    # consumer (10 records per fetch); it skips to the log start
-            starts = {int(p): eng.state(int(p))["log_start_offset"] for p in np.unique(pp[gone])}
-            nxt[gone] = [starts[int(pp[i])] for i in gone]
+        gone = np.flatnonzero(st == -6)  # RMQ_EOFFSET: a partition's ring moved past a slow consumer
+        if gone.size:                    # (10 records per fetch): it skips to the high watermark
+            nxt[gone] = eng.commit_snapshot()[pp[gone]]
             resets += gone.size
         eng.commit_consumer_offset(pp, cc, nxt)
         recs += appends * spec.records
@@ -521,7 +521,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
         if args.fetch_rounds > 0:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
         if args.concurrent_rounds > 0 and world == 1:
-            out["mixed"] = mixed_leg(eng, step, spec, args.concurrent_rounds, 2 * args.group)
+            out["mixed"] = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group)
     if region is not None:
         eng.device_free(region)
     else:
