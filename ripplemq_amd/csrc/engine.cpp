@@ -182,7 +182,8 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   // the kernel with a transport (outboxes) runs 512-thread workgroups, the single-GPU one 256
   const uint32_t PT = a.outidx ? kPipeThreadsXR : kPipeThreads;
   if (s2) {
-    a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((P * kScanLanes + PT - 1) / PT, 2u * e->cu_count));
+    const uint32_t groups = (P + kScanCols - 1) / kScanCols;
+    a.wg2 = std::max<uint32_t>(1u, std::min<uint32_t>((groups * kScanLanes + PT - 1) / PT, 2u * e->cu_count));
     if (e->s2_wgs) a.wg2 = std::min(a.wg2, e->s2_wgs);
   }
   {
@@ -429,7 +430,7 @@ void free_engine(rmq_engine* e) {
     bufs.push_back(z.used);
   }
   for (const PipeScratch& x : e->scratch) {
-    void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.nbig, x.bigl};
+    void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.bacc, x.nbig, x.bigl};
     for (void* p : xs) bufs.push_back(p);
   }
   delete e->copy_pool;
@@ -611,7 +612,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
   CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));
-  e->max_group_tiles = std::min<uint32_t>(kMaxTiles, e->group_max * e->max_tiles);
+  // even: stage 2 reads hist columns with 16-byte loads
+  e->max_group_tiles = (std::min<uint32_t>(kMaxTiles, e->group_max * e->max_tiles) + 1u) & ~1u;
   for (PipeScratch& x : e->scratch) {
     const size_t GT = e->max_group_tiles, TP = GT * P;
     CREATE_TRY(dalloc(&x.hist, TP));
@@ -623,6 +625,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_TRY(dalloc(&x.tsum, GT * 4));
     CREATE_TRY(dalloc(&x.tile_base, GT));
     CREATE_TRY(dalloc(&x.binfo, (size_t)kMaxGroup * 4));
+    CREATE_TRY(dalloc(&x.bacc, (size_t)kMaxGroup * 2));
     CREATE_TRY(dalloc(&x.nbig, 1));
     CREATE_TRY(dalloc(&x.bigl, GT * kTileRecs));
   }

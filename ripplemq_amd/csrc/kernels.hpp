@@ -18,9 +18,13 @@ constexpr uint32_t kTileIdxBits = RMQ_TILE_BITS;       // log2(kTileRecs)
 constexpr uint32_t kTileRecs = 1u << kTileIdxBits;     // records per ranking tile (stage 1)
 constexpr uint32_t kMaxTiles = 512;      // tiles per group (stage 2 keeps their payload bases in LDS)
 #ifndef RMQ_SCAN_LANES
-#define RMQ_SCAN_LANES 16
+#define RMQ_SCAN_LANES 32
 #endif
 constexpr uint32_t kScanLanes = RMQ_SCAN_LANES;  // stage 2: threads per partition column
+#ifndef RMQ_SCAN_COLS
+#define RMQ_SCAN_COLS 1
+#endif
+constexpr uint32_t kScanCols = RMQ_SCAN_COLS;  // stage 2: adjacent columns per thread group
 constexpr uint32_t kTaskRecs = 32;       // records per apply task (one wave, 2 lanes per record)
 constexpr uint32_t kMaxGroup = 8;        // batches per pipeline group (cfg.pipeline_depth)
 constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-bit LDS radix passes)
@@ -196,6 +200,8 @@ struct PipeScratch {
   uint64_t* tsum;       // [tiles][4] {payload bytes, record bytes, invalid records, 0}
   uint64_t* tile_base;  // [tiles] payload offset of the tile's first record inside its batch
   uint64_t* binfo;      // [kMaxGroup][4] per batch {reject flags (2 invalid payload ranges), 0, payload bytes, 0}
+  uint64_t* bacc;       // [kMaxGroup][2] per batch {payload bytes, invalid records} (stage 1 adds,
+                        //   stage 2 reads, stage 4 resets)
   uint32_t* nbig;       // [1] records over 1 KB in the group (stage 1 appends, stage 4 resets)
   uint32_t* bigl;       // [tiles * kTileRecs] their group record slots, in no particular order
 };

@@ -254,6 +254,10 @@ __device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
       x.tsum[(u64)t * 4 + 1] = 0;
       x.tsum[(u64)t * 4 + 2] = ic;
       x.tsum[(u64)t * 4 + 3] = 0;
+      // the batch's sums for stage 2's batch rule (one add per tile instead of a pass over the
+      // tile sums in every stage-2 workgroup)
+      if (ps) __hip_atomic_fetch_add(&x.bacc[jb * 2 + 0], ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ic) __hip_atomic_fetch_add(&x.bacc[jb * 2 + 1], ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
@@ -682,6 +686,100 @@ __device__ void stage2_plan(const PipeArgs& A) {
 }
 
 // s_ex: kMaxTiles words of the launch's dynamic LDS (static arrays would add to every role's LDS)
+constexpr u32 kCL = 256 / kScanLanes;  // stage 2: tiles per thread per column chunk (chunks of 256 tiles)
+
+// Tiles [t, t + kCL) of a hist column (zero past the group's T tiles): 16-byte loads, the column
+// stride (gt) being even.
+__device__ __forceinline__ void load_column_chunk(const u64* col, u32 t, u32 T, u64 (&h)[kCL]) {
+#pragma unroll
+  for (u32 k = 0; k < kCL; k += 2) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (t + k < T) v = *reinterpret_cast<const uint4*>(col + t + k);
+    h[k] = ((u64)v.y << 32) | v.x;
+    h[k + 1] = t + k + 1 < T ? ((u64)v.w << 32) | v.z : 0ull;
+  }
+}
+
+__device__ __forceinline__ void load_column_group(const PipeScratch& x, u32 cg, u32 P, u32 GT, u32 s, u32 T,
+                                                  u64 (&h)[kScanCols][kCL]) {
+#pragma unroll
+  for (u32 c = 0; c < kScanCols; ++c) {
+    const u32 p = cg * kScanCols + c;
+    if (p < P) load_column_chunk(x.hist + (u64)p * GT, kCL * s, T, h[c]);
+  }
+}
+
+// Column p of the group: per batch, the exclusive scan of the column over the batch's tiles, read
+// in chunks of kScanLanes * kCL tiles (thread s holding tiles [kCL s, kCL s + kCL) of the chunk;
+// h = the first chunk, already loaded), the batches overlapping a chunk scanned from those registers
+// one after another.
+__device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u32 rm, u64 (&h)[kCL]) {
+  const PipeGroup& G = A.g2;
+  const PipeScratch& x = A.s2;
+  const u32 P = A.st.P, T = G.tiles, GT = A.gt;
+  // record bytes / 16 one batch may add to p: its ring less one index interval (FORMAT.md §3)
+  const u64 lim16 = ((1ull << (A.st.ring[p] & 63ull)) - (1ull << A.st.interval_log2)) >> 4;
+  u64* const col = x.hist + (u64)p * GT;
+  u64* const ecol = x.excl + (u64)p * GT;
+  u64 carry = 0, bsum = 0;  // aggregate through the batches before j; batch j so far
+  u32 j = 0;
+  for (u32 C = 0; C < T; C += kScanLanes * kCL) {
+    if (C) load_column_chunk(col, C + kCL * s, T, h);
+    const u32 ta = C + kCL * s;
+    for (; j < G.nb && G.tile0[j] < C + kScanLanes * kCL; ++j) {
+      const u32 t0 = G.tile0[j], t1 = G.tile0[j + 1];
+      const bool binv = (rm >> j) & 1u;  // invalid batch: its cells are cleared and count nothing
+      u64 loc = 0;
+#pragma unroll
+      for (u32 k = 0; k < kCL; ++k) loc += (ta + k >= t0 && ta + k < t1) ? h[k] : 0ull;
+      if (binv) loc = 0;
+      u64 inc = loc;
+#pragma unroll
+      for (u32 d = 1; d < kScanLanes; d <<= 1) {
+        const u64 o = __shfl_up(inc, d, kScanLanes);
+        if (s >= d) inc += o;
+      }
+      u64 run = carry + bsum + inc - loc;
+#pragma unroll
+      for (u32 k = 0; k < kCL; ++k) {
+        if (ta + k >= t0 && ta + k < t1 && h[k]) {
+          if (!binv) ecol[ta + k] = run;
+          col[ta + k] = 0ull;  // clear for the set's next group
+          if (!binv) run += h[k];
+        }
+      }
+      bsum += __shfl(inc, kScanLanes - 1, kScanLanes);
+      if (t1 > C + kScanLanes * kCL) break;  // batch j goes on in the next chunk
+      if (!binv) {
+        if ((bsum & kLow40) > lim16) {
+          // FORMAT.md §3: partition p takes no record of batch j. The same threads that wrote the
+          // cells flag them (program order), absent cells included (stage 3 never reads those).
+          for (u32 B = t0 - t0 % (kScanLanes * kCL); B < t1; B += kScanLanes * kCL)
+#pragma unroll
+            for (u32 k = 0; k < kCL; ++k) {
+              const u32 t = B + kCL * s + k;
+              if (t >= t0 && t < t1) ecol[t] = kExclNoSpace;
+            }
+        } else {
+          carry += bsum;
+        }
+      }
+      bsum = 0;
+      if (s == 0) x.bcum[(u64)j * P + p] = carry;
+    }
+  }
+  for (; j < G.nb; ++j)  // batches without tiles at the group's end
+    if (s == 0) x.bcum[(u64)j * P + p] = carry;
+  if (s == 0) store_sc1(&x.totals[p], carry);  // sc1: the plan below reads it in this launch
+  if (A.xp2.n_out && s == 0 && A.st.is_leader[p]) {  // catch-up verdicts of p's out entries
+    const u32 lm = A.st.local_mask[p];
+    for (u32 r = 0; r < A.st.RF; ++r) {
+      const u32 e = ((lm >> r) & 1u) ? ~0u : A.outidx[(u64)p * A.st.RF + r];
+      if (e != ~0u) plan_decide(A, p, e, carry);
+    }
+  }
+}
+
 __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
@@ -691,29 +789,30 @@ __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   __shared__ u64 s_w[kPW];
   __shared__ u32 s_rej;
   PIPE_STAMP(0);
-  // ---- batch rule from the tile sums (every workgroup, since the scans skip invalid batches)
-  if (tid < kMaxGroup * 2) (&s_acc[0][0])[tid] = 0ull;
-  __syncthreads();
-  // tiles t = tid, tid + kPT, ... (a group has at most kMaxTiles)
-  u64 carry = 0;
-  for (u32 t0 = 0; t0 < T; t0 += kPT) {
-    const u32 t = t0 + tid;
-    const bool in = t < T;
-    const u32 jt = in ? batch_of_tile(G, t) : 0u;
-    const u64 pay = in ? x.tsum[(u64)t * 4 + 0] : 0ull;
-    if (in) {
-      atomicAdd(&s_acc[jt][0], pay);
-      atomicAdd(&s_acc[jt][1], x.tsum[(u64)t * 4 + 2]);
-    }
-    if (wg == 0) {  // payload offset of every tile's first record in the group (packed payloads)
+  // kScanLanes consecutive threads (a column group) scan kScanCols adjacent partition columns
+  // (contiguous in hist / excl): the first chunk of each is loaded up front, in flight while the
+  // batch rule is worked out (a workgroup's lifetime is a few memory round trips, so fewer
+  // workgroups with more loads each hold fewer of the launch's slots)
+  const u32 s = tid % kScanLanes;
+  const u32 ncg = (P + kScanCols - 1) / kScanCols;
+  const u32 cstride = A.wg2 * (kPT / kScanLanes);
+  u32 cg = (wg * kPT + tid) / kScanLanes;
+  u64 h[kScanCols][kCL];
+  if (cg < ncg) load_column_group(x, cg, P, GT, s, T, h);
+  // ---- batch rule from stage 1's per-batch sums (every workgroup, since the scans skip invalid
+  // batches)
+  if (tid < kMaxGroup * 2) (&s_acc[0][0])[tid] = tid < G.nb * 2 ? x.bacc[tid] : 0ull;
+  if (wg == 0) {  // payload offset of every tile's first record in the group (packed payloads)
+    u64 carry = 0;
+    for (u32 t0 = 0; t0 < T; t0 += kPT) {  // tiles t = tid, tid + kPT, ... (at most kMaxTiles)
+      const u32 t = t0 + tid;
+      const u64 pay = t < T ? x.tsum[(u64)t * 4 + 0] : 0ull;
       u64 tot;
       const u64 inc = block_incl_scan_u64(pay, s_w, &tot);
-      if (in) s_ex[t] = carry + inc - pay;
+      if (t < T) s_ex[t] = carry + inc - pay;
       carry += tot;
     }
-  }
-  if (wg == 0) {  // ... and inside its batch
-    __syncthreads();
+    __syncthreads();  // ... and inside its batch
     for (u32 t = tid; t < T; t += kPT) x.tile_base[t] = s_ex[t] - s_ex[G.tile0[batch_of_tile(G, t)]];
   }
   __syncthreads();
@@ -734,69 +833,11 @@ __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   }
   __syncthreads();
   const u32 rm = s_rej;
-
-  // ---- column scans: kScanLanes consecutive threads share a partition column (contiguous in
-  // hist / excl); per batch, blocks of 8 * kScanLanes tiles, thread s holding tiles [8s, 8s + 8)
-  const u32 s = tid % kScanLanes;
-  for (u32 g = wg * kPT + tid; g < P * kScanLanes; g += A.wg2 * kPT) {  // whole columns per group
-    const u32 p = g / kScanLanes;
-    // record bytes / 16 one batch may add to p: its ring less one index interval (FORMAT.md §3)
-    const u64 lim16 = ((1ull << (A.st.ring[p] & 63ull)) - (1ull << A.st.interval_log2)) >> 4;
-    u64* const col = x.hist + (u64)p * GT;
-    u64* const ecol = x.excl + (u64)p * GT;
-    u64 carry = 0;
-    for (u32 j = 0; j < G.nb; ++j) {
-      const u32 t0 = G.tile0[j], t1 = G.tile0[j + 1];
-      const bool binv = (rm >> j) & 1u;  // invalid batch: its cells are cleared and count nothing
-      u64 bsum = 0;
-      for (u32 B = t0; B < t1; B += 8u * kScanLanes) {
-        const u32 ta = B + 8u * s;
-        u64 h[8];
+  for (; cg < ncg; cg += cstride) {
 #pragma unroll
-        for (u32 k = 0; k < 8; ++k) h[k] = ta + k < t1 ? col[ta + k] : 0ull;
-        u64 loc = 0;
-#pragma unroll
-        for (u32 k = 0; k < 8; ++k) loc += h[k];
-        if (binv) loc = 0;
-        u64 inc = loc;
-#pragma unroll
-        for (u32 d = 1; d < kScanLanes; d <<= 1) {
-          const u64 o = __shfl_up(inc, d, kScanLanes);
-          if (s >= d) inc += o;
-        }
-        u64 run = carry + bsum + inc - loc;
-#pragma unroll
-        for (u32 k = 0; k < 8; ++k) {
-          if (h[k]) {
-            if (!binv) ecol[ta + k] = run;
-            col[ta + k] = 0ull;  // clear for the set's next group
-          }
-          if (!binv) run += h[k];
-        }
-        bsum += __shfl(inc, kScanLanes - 1, kScanLanes);
-      }
-      if (!binv) {
-        if ((bsum & kLow40) > lim16) {
-          // FORMAT.md §3: partition p takes no record of batch j. The same threads that wrote the
-          // cells flag them (program order), absent cells included (stage 3 never reads those).
-          for (u32 B = t0; B < t1; B += 8u * kScanLanes)
-#pragma unroll
-            for (u32 k = 0; k < 8; ++k)
-              if (B + 8u * s + k < t1) ecol[B + 8u * s + k] = kExclNoSpace;
-        } else {
-          carry += bsum;
-        }
-      }
-      if (s == 0) x.bcum[(u64)j * P + p] = carry;
-    }
-    if (s == 0) store_sc1(&x.totals[p], carry);  // sc1: the plan below reads it in this launch
-    if (A.xp2.n_out && s == 0 && A.st.is_leader[p]) {  // catch-up verdicts of p's out entries
-      const u32 lm = A.st.local_mask[p];
-      for (u32 r = 0; r < A.st.RF; ++r) {
-        const u32 e = ((lm >> r) & 1u) ? ~0u : A.outidx[(u64)p * A.st.RF + r];
-        if (e != ~0u) plan_decide(A, p, e, carry);
-      }
-    }
+    for (u32 c = 0; c < kScanCols; ++c)
+      if (cg * kScanCols + c < P) stage2_column(A, cg * kScanCols + c, s, rm, h[c]);
+    if (cg + cstride < ncg) load_column_group(x, cg + cstride, P, GT, s, T, h);
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(1);
@@ -1252,30 +1293,86 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   }
 }
 
-// Thread per partition, stage 3: the group's new log end, matchIndex, quorum commit and high
-// watermark, into the next state set. The commit rule is monotone in the log end, so evaluating
-// it once after the group equals evaluating it after each batch.
-__device__ void partition_apply(const PipeArgs& A, u32 p) {
+// Thread per partition: stage 3's state advance and stage 4's retention. Everything either reads
+// is loaded first, in one round (speculatively: a partition this engine does not lead, or one
+// without records, discards it), so the chain is that round, the index entries retention needs,
+// and the stores.
+//  * stage 3: the group's new log end, matchIndex, quorum commit and high watermark, into the next
+//    state set. The commit rule is monotone in the log end, so evaluating it once after the group
+//    equals evaluating it after each batch. A partition this engine does not lead keeps its state
+//    outside the pipeline (its records are counted by stages 1/2, ranks being per partition, but
+//    never applied; the host keeps both state sets equal for it); stage 2 leaves rejected
+//    (batch, partition) cells out of totals.
+//  * stage 4: retention after each batch of the group applied one launch earlier (FORMAT.md §4),
+//    batch by batch, from the index entries that launch wrote. The state set this launch reads
+//    (cur) holds that group's final log end.
+__device__ void partition_threads(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
-  // a partition this engine does not lead keeps its state outside the pipeline (its records are
-  // counted by stages 1/2, ranks being per partition, but never applied; the host keeps both state
-  // sets equal for it); stage 2 leaves rejected (batch, partition) cells out of totals
-  if (!st.is_leader[p]) return;
-  u64 tc = 0, leo;
-  if (A.g3.nb) {
-    const u64 tot = A.s3.totals[p];
-    tc = tot >> 40;
-    leo = A.cur.leo[p] + tc;
-    A.nxt.leo[p] = leo;
-    A.nxt.used[p] = A.cur.used[p] + 16ull * (tot & kLow40);
-  } else {
-    leo = A.cur.leo[p];
-  }
-  if (!tc && !A.ackin) return;
-  const u32 RF = st.RF, lm = st.local_mask[p];
+  const u32 RF = st.RF;
+  const bool a3 = A.g3.nb != 0, a4 = A.g4.nb != 0;
+  const bool lead = st.is_leader[p];
+  const u64 tot3 = a3 ? A.s3.totals[p] : 0ull;
+  const u64 leo0 = A.cur.leo[p], used0 = A.cur.used[p];
+  const u32 lm = st.local_mask[p];
   u64 row[kMaxRF];
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
+  const u64 commit0 = st.commit[p], ts = st.term_start[p];
+  const u64 tot4 = a4 ? A.s4.totals[p] : 0ull;
+  const u64 soff0 = st.start_off[p], spos0 = st.start_pos[p];
+  const u64 desc = st.ring[p];
+  u64 bc[kMaxGroup];
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j) bc[j] = a4 && j < A.g4.nb ? A.s4.bcum[(u64)j * st.P + p] : 0ull;
+  if (!lead) return;
+
+  // ---- stage 4: retention of the group applied one launch earlier (reads cur, before any store)
+  if (tot4 >> 40) {
+    const u32 ilog = st.interval_log2;
+    const RingRef rg = ring_ref(desc, ilog, st.icap_mul);
+    // batch by batch: after batch j (log end fin_j) the start moves to index entry
+    // ceil((fin_j - seg) / I) when fin_j - start > seg. The start only grows, so a batch with
+    // fin_j - start0 <= seg never moves it: the entries of the others are loaded together, then
+    // the batches are replayed in order in registers.
+    u64 fin[kMaxGroup], eo[kMaxGroup], ep[kMaxGroup];
+    u64 prev = 0;
+#pragma unroll
+    for (u32 j = 0; j < kMaxGroup; ++j) {
+      const bool app = j < A.g4.nb && (bc[j] >> 40) != (prev >> 40);  // batch j appended records of p
+      fin[j] = app ? used0 - 16ull * ((tot4 - bc[j]) & kLow40) : 0ull;
+      eo[j] = ep[j] = 0ull;
+      if (app && fin[j] - spos0 > rg.seg) {
+        const u64 ms = (fin[j] - rg.seg + (1ull << ilog) - 1) >> ilog;
+        const u64* e = st.index + (rg.ibase + ms % rg.icap) * 2;
+        eo[j] = e[0];
+        ep[j] = e[1];
+      } else {
+        fin[j] = 0ull;  // cannot move the start
+      }
+      prev = j < A.g4.nb ? bc[j] : prev;
+    }
+    u64 soff = soff0, spos = spos0;
+#pragma unroll
+    for (u32 j = 0; j < kMaxGroup; ++j)
+      if (fin[j] && fin[j] - spos > rg.seg) {
+        soff = eo[j];
+        spos = ep[j];
+      }
+    if (soff != soff0 || spos != spos0) {
+      st.start_off[p] = soff;
+      st.start_pos[p] = spos;
+    }
+  }
+
+  // ---- stage 3: log end, matchIndex, commit
+  u64 tc = 0, leo = leo0;
+  if (a3) {
+    tc = tot3 >> 40;
+    leo = leo0 + tc;
+    A.nxt.leo[p] = leo;
+    A.nxt.used[p] = used0 + 16ull * (tot3 & kLow40);
+  }
+  if (!tc && !A.ackin) return;
   bool moved = tc != 0;
   if (tc) {
 #pragma unroll
@@ -1288,42 +1385,9 @@ __device__ void partition_apply(const PipeArgs& A, u32 p) {
   // followers' acks of an earlier group (replication transport, FORMAT.md §9)
   if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row, A.xreq, A.acks_round);
   if (moved) {
-    const u64 c = quorum_commit(row, RF, st.commit[p], st.term_start[p]);
+    const u64 c = quorum_commit(row, RF, commit0, ts);
     st.commit[p] = c;
     st.hw[p] = c;
-  }
-}
-
-// Thread per partition, stage 4: retention after each batch of the group applied one launch
-// earlier (FORMAT.md §4), batch by batch, from the index entries that launch wrote. The state set
-// this launch reads (cur) holds that group's final log end.
-__device__ void partition_retention(const PipeArgs& A, u32 p) {
-  const DevState& st = A.st;
-  const PipeScratch& x = A.s4;
-  if (!st.is_leader[p]) return;
-  const u64 gtot = x.totals[p];
-  if (!(gtot >> 40)) return;  // the partition took no record in the group
-  const u64 fin_g = A.cur.used[p];
-  const u32 ilog = st.interval_log2;
-  const u64 soff0 = st.start_off[p], spos0 = st.start_pos[p];
-  u64 soff = soff0, spos = spos0, prev = 0;
-  const RingRef rg = ring_ref(st, p);
-  for (u32 j = 0; j < A.g4.nb; ++j) {
-    const u64 c = x.bcum[(u64)j * st.P + p];
-    if ((c >> 40) != (prev >> 40)) {  // batch j appended records of p
-      const u64 fin = fin_g - 16ull * ((gtot - c) & kLow40);
-      if (fin - spos > rg.seg) {
-        const u64 ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
-        const u64* e = st.index + (rg.ibase + ms % rg.icap) * 2;
-        soff = e[0];
-        spos = e[1];
-      }
-    }
-    prev = c;
-  }
-  if (soff != soff0 || spos != spos0) {
-    st.start_off[p] = soff;
-    st.start_pos[p] = spos;
   }
 }
 
@@ -1432,11 +1496,11 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     wg -= A.wg2;
     // partition threads: stage 3's state advance and stage 4's retention
     PIPE_STAMP(0);
-    if (wg == 0 && threadIdx.x == 0 && A.g4.nb) *A.s4.nbig = 0u;  // the set's next group starts its list
-    for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) {
-      if (A.g3.nb || A.ackin) partition_apply(A, p);
-      if (A.g4.nb) partition_retention(A, p);
+    if (wg == 0 && A.g4.nb) {  // the set's next group starts its list and its batch sums
+      if (threadIdx.x == 0) *A.s4.nbig = 0u;
+      if (threadIdx.x < kMaxGroup * 2) A.s4.bacc[threadIdx.x] = 0ull;
     }
+    for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) partition_threads(A, p);
     if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     PIPE_STAMP(6);
     return;
