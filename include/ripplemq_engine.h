@@ -49,8 +49,9 @@
  * placement and commit on quorum. Rounds are collective, like the launches that drive them: every
  * rank must make the same sequence of rmq_append calls (empty batches count) and of the calls that
  * flush the pipeline (rmq_sync, rmq_set_placement, rmq_set_replicas, rmq_become_leader, rmq_ack);
- * rmq_poll_commit / rmq_ticket_stats never flush then (they answer RMQ_PENDING until an rmq_sync on
- * every rank applied the ticket), and rmq_sync before rmq_destroy.
+ * rmq_poll_commit / rmq_ticket_stats never flush then: they answer RMQ_PENDING until later launch
+ * groups (further rmq_append calls on every rank, empty batches included: ripplemq_amd/pacer.py) or
+ * an rmq_sync on every rank pushed the ticket through its stages; rmq_sync before rmq_destroy.
  *
  * Log byte format, offset index and retention are defined in FORMAT.md.
  */
@@ -64,7 +65,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 3u
+#define RMQ_ABI_VERSION 4u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -84,8 +85,16 @@ enum {
   RMQ_ENOMEM = -7
 };
 
-/* Memory kind of caller buffers. */
-enum { RMQ_MEM_HOST = 0, RMQ_MEM_DEVICE = 1 };
+/* Memory kind of caller buffers.
+   RMQ_MEM_HOST: pageable host memory (rmq_append packs it into a pinned staging slot with host
+     threads, then one DMA; payload ranges are checked on the host: RMQ_EINVAL).
+   RMQ_MEM_DEVICE: device memory (rmq_device_alloc).
+   RMQ_MEM_PINNED (rmq_append only): page-locked host memory (rmq_host_alloc, or pages registered
+     with rmq_host_register): every section goes to the device by its own DMA on the engine's copy
+     stream, with no host copy; out_offsets must be page-locked too and is written by a DMA. The
+     caller keeps all of them unchanged until the ticket completes (like device batches), and
+     payload ranges are checked on the device like device batches (rejected_invalid). */
+enum { RMQ_MEM_HOST = 0, RMQ_MEM_DEVICE = 1, RMQ_MEM_PINNED = 2 };
 
 typedef struct rmq_config {
   uint32_t num_partitions;     /* P: dense pidx in [0, P), P <= 65536 per engine */
@@ -106,7 +115,7 @@ typedef struct rmq_config {
 /* One append batch: records of many partitions, interleaved, in apply order (SoA). */
 typedef struct rmq_batch {
   uint32_t n;                  /* number of records */
-  uint32_t mem;                /* RMQ_MEM_HOST or RMQ_MEM_DEVICE for every pointer below */
+  uint32_t mem;                /* RMQ_MEM_HOST, RMQ_MEM_DEVICE or RMQ_MEM_PINNED for every pointer below */
   const uint32_t* pidx;        /* [n] partition of each record */
   const uint32_t* len;         /* [n] payload length of each record */
   const uint64_t* payload_off; /* [n] byte offset of each payload in `payload`, or NULL = packed
@@ -123,7 +132,8 @@ typedef struct rmq_fetch_req {
 } rmq_fetch_req;
 
 typedef struct rmq_fetch_res {
-  uint64_t start_offset;       /* reference: MessageBatchReadResponse.offset (the consumer offset) */
+  uint64_t start_offset;       /* reference: MessageBatchReadResponse.offset (the consumer offset);
+                                  RMQ_EOFFSET: the first retained offset, where the consumer can resume */
   uint64_t out_pos;            /* byte position of this request's records in the output buffer */
   uint32_t count;              /* records returned (reference: messages.size()) */
   uint32_t bytes;              /* bytes of the returned records (FORMAT.md record layout) */
@@ -292,6 +302,12 @@ int rmq_read_consumer_offsets(rmq_engine* e, uint32_t pidx, uint64_t* out /* max
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out);
 int rmq_device_free(rmq_engine* e, void* p);
 int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int kind /*0 h2d,1 d2h,2 d2d*/);
+/* Page-locked host memory for RMQ_MEM_PINNED batches (reference side: the JNI layer's direct
+   ByteBuffers): allocate, or register / unregister existing pages. */
+int rmq_host_alloc(rmq_engine* e, uint64_t bytes, void** out);
+int rmq_host_free(rmq_engine* e, void* p);  /* e may be NULL (buffers outliving the engine) */
+int rmq_host_register(rmq_engine* e, void* p, uint64_t bytes);
+int rmq_host_unregister(rmq_engine* e, void* p);
 /* Kernel timing with HIP events on the engine's stream (enable != 0 turns it on and resets it).
    kernels 0 and 1: the pipeline launches from the first one after enable up to the next drain
    (sync, control call, read-back) timed as ONE region (no events between launches): total_ms =

@@ -742,6 +742,7 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
     if (off >= end) continue; /* empty list */
     if (off < s->start_off) {
       x->status = RMQ_EOFFSET;
+      x->start_offset = s->start_off; /* where the consumer can resume (FORMAT.md §7) */
       continue;
     }
     uint64_t p0 = s->rec_pos.v[off];

@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 3
+RMQ_ABI_VERSION = 4
 RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
@@ -33,6 +33,7 @@ RMQ_ENOMEM = -7
 
 RMQ_MEM_HOST = 0
 RMQ_MEM_DEVICE = 1
+RMQ_MEM_PINNED = 2
 
 STATUS_NAMES = {
     RMQ_OK: "RMQ_OK", RMQ_PENDING: "RMQ_PENDING", RMQ_ENOTLEADER: "RMQ_ENOTLEADER",
@@ -126,6 +127,10 @@ _SIGS = {
     "rmq_device_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
     "rmq_device_free": (C.c_int, [vp, vp]),
     "rmq_memcpy": (C.c_int, [vp, vp, vp, u64, C.c_int]),
+    "rmq_host_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
+    "rmq_host_free": (C.c_int, [vp, vp]),
+    "rmq_host_register": (C.c_int, [vp, vp, u64]),
+    "rmq_host_unregister": (C.c_int, [vp, vp]),
     "rmq_profile_enable": (C.c_int, [vp, C.c_int]),
     "rmq_profile_query": (C.c_int, [vp, C.c_int, C.POINTER(u64), C.POINTER(C.c_double)]),
     "rmq_device_info": (C.c_int, [vp, C.c_char_p, u32, C.POINTER(u32)]),

@@ -491,6 +491,33 @@ extern "C" {
 
 uint32_t rmq_abi_version(void) { return RMQ_ABI_VERSION; }
 
+int rmq_host_alloc(rmq_engine* e, uint64_t bytes, void** out) {
+  if (!e || !out || !bytes) return RMQ_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  *out = nullptr;
+  if (hipHostMalloc(out, bytes, 0) != hipSuccess) return RMQ_ENOMEM;
+  return RMQ_OK;
+}
+
+int rmq_host_free(rmq_engine* e, void* p) {  // e may be NULL (after rmq_destroy)
+  (void)e;
+  if (p && hipHostFree(p) != hipSuccess) return RMQ_EDEVICE;
+  return RMQ_OK;
+}
+
+int rmq_host_register(rmq_engine* e, void* p, uint64_t bytes) {
+  if (!e || !p || !bytes) return RMQ_EINVAL;
+  HIP_TRY(hipSetDevice(e->device));
+  HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterDefault));
+  return RMQ_OK;
+}
+
+int rmq_host_unregister(rmq_engine* e, void* p) {
+  if (!e || !p) return RMQ_EINVAL;
+  HIP_TRY(hipHostUnregister(p));
+  return RMQ_OK;
+}
+
 const char* rmq_strerror(int s) {
   switch (s) {
     case RMQ_OK: return "ok";
@@ -848,7 +875,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   const uint32_t n = b->n;
   if (n > e->cfg.max_batch_records) return RMQ_ENOSPC;
   if (b->payload_bytes > e->cfg.max_batch_bytes) return RMQ_ENOSPC;
-  if (b->mem != RMQ_MEM_HOST && b->mem != RMQ_MEM_DEVICE) return RMQ_EINVAL;
+  if (b->mem != RMQ_MEM_HOST && b->mem != RMQ_MEM_DEVICE && b->mem != RMQ_MEM_PINNED) return RMQ_EINVAL;
   if (n && (!b->pidx || !b->len || !out_offsets)) return RMQ_EINVAL;
   if (b->payload_bytes && !b->payload) return RMQ_EINVAL;
   if (b->mem == RMQ_MEM_DEVICE && (reinterpret_cast<uintptr_t>(b->payload) & 3u)) return RMQ_EINVAL;
@@ -878,7 +905,8 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
   f.b.out_offsets = out_offsets;
   f.b.n = n;
   f.b.tiles = (n + kTileRecs - 1) / kTileRecs;
-  if (b->mem == RMQ_MEM_HOST && n) {
+  if (b->mem != RMQ_MEM_DEVICE && n) {
+    const bool pinned = b->mem == RMQ_MEM_PINNED;
     Staging& sg = e->staging[t % e->staging.size()];
     if (sg.ticket) {  // the batch that used this staging slot must be complete
       int rc = wait_ticket(e, sg.ticket);
@@ -897,21 +925,32 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
       }
     const uint64_t o_len = (4ull * n + 15) & ~15ull, o_poff = o_len + ((4ull * n + 15) & ~15ull);
     const uint64_t o_pay = o_poff + (b->payload_off ? (8ull * n + 15) & ~15ull : 0ull);
-    if (!e->copy_pool) {
-      // RMQ_COPY_THREADS: packing threads besides the caller's (default min(7, cores / 2))
-      const char* env = std::getenv("RMQ_COPY_THREADS");
-      const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
-      unsigned k = env ? (unsigned)std::atoi(env) : std::min(7u, hc / 2u);
-      e->copy_pool = new (std::nothrow) CopyPool(std::min(k, 64u));
-      if (!e->copy_pool) return RMQ_ENOMEM;
+    if (pinned) {
+      // caller-pinned sections: one DMA each straight into the device slot, no host copy
+      sg.ticket = t;
+      HIP_TRY(hipMemcpyAsync(sg.d_blk, b->pidx, 4ull * n, hipMemcpyHostToDevice, e->copy_s));
+      HIP_TRY(hipMemcpyAsync(sg.d_blk + o_len, b->len, 4ull * n, hipMemcpyHostToDevice, e->copy_s));
+      if (b->payload_off)
+        HIP_TRY(hipMemcpyAsync(sg.d_blk + o_poff, b->payload_off, 8ull * n, hipMemcpyHostToDevice, e->copy_s));
+      if (b->payload_bytes)
+        HIP_TRY(hipMemcpyAsync(sg.d_blk + o_pay, b->payload, b->payload_bytes, hipMemcpyHostToDevice, e->copy_s));
+    } else {
+      if (!e->copy_pool) {
+        // RMQ_COPY_THREADS: packing threads besides the caller's (default min(7, cores / 2))
+        const char* env = std::getenv("RMQ_COPY_THREADS");
+        const unsigned hc = std::max(1u, std::thread::hardware_concurrency());
+        unsigned k = env ? (unsigned)std::atoi(env) : std::min(7u, hc / 2u);
+        e->copy_pool = new (std::nothrow) CopyPool(std::min(k, 64u));
+        if (!e->copy_pool) return RMQ_ENOMEM;
+      }
+      std::vector<CopyPool::Seg> segs = {{sg.h_blk, reinterpret_cast<const uint8_t*>(b->pidx), 4ull * n},
+                                         {sg.h_blk + o_len, reinterpret_cast<const uint8_t*>(b->len), 4ull * n}};
+      if (b->payload_off) segs.push_back({sg.h_blk + o_poff, reinterpret_cast<const uint8_t*>(b->payload_off), 8ull * n});
+      if (b->payload_bytes) segs.push_back({sg.h_blk + o_pay, b->payload, b->payload_bytes});
+      sg.ticket = t;
+      e->copy_pool->run(segs, 512u << 10);
+      HIP_TRY(hipMemcpyAsync(sg.d_blk, sg.h_blk, o_pay + b->payload_bytes, hipMemcpyHostToDevice, e->copy_s));
     }
-    std::vector<CopyPool::Seg> segs = {{sg.h_blk, reinterpret_cast<const uint8_t*>(b->pidx), 4ull * n},
-                                       {sg.h_blk + o_len, reinterpret_cast<const uint8_t*>(b->len), 4ull * n}};
-    if (b->payload_off) segs.push_back({sg.h_blk + o_poff, reinterpret_cast<const uint8_t*>(b->payload_off), 8ull * n});
-    if (b->payload_bytes) segs.push_back({sg.h_blk + o_pay, b->payload, b->payload_bytes});
-    sg.ticket = t;
-    e->copy_pool->run(segs, 512u << 10);
-    HIP_TRY(hipMemcpyAsync(sg.d_blk, sg.h_blk, o_pay + b->payload_bytes, hipMemcpyHostToDevice, e->copy_s));
     HIP_TRY(hipEventRecord(sg.ev_in, e->copy_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, sg.ev_in, 0));  // before the group's first launch
     f.b.pidx = reinterpret_cast<const uint32_t*>(sg.d_blk);
@@ -919,8 +958,8 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     f.b.poff = b->payload_off ? reinterpret_cast<const uint64_t*>(sg.d_blk + o_poff) : nullptr;
     f.b.payload = sg.d_blk + o_pay;
     f.b.out_offsets = sg.d_out;
-    f.host_out = sg.h_out;
-    sg.user_out = out_offsets;
+    f.host_out = pinned ? out_offsets : sg.h_out;  // pinned: the DMA writes the caller's array
+    sg.user_out = pinned ? nullptr : out_offsets;
     sg.out_n = n;
   }
   e->last_ticket = t;
@@ -1054,10 +1093,23 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   // last writer wins (PartitionStateMachine.java:71-77): keep only the last item per
   // (partition, consumer), so the device scatter has no two writers to one slot
   {
-    std::unordered_set<uint64_t> seen;
+    // a generation stamp per (partition, consumer) slot instead of a hash set (16,384 items: tens
+    // of microseconds instead of about a millisecond)
+    const size_t slots = (size_t)e->cfg.num_partitions * e->cfg.max_consumers;
+    if (e->lww_stamp.size() != slots) {
+      e->lww_stamp.assign(slots, 0u);
+      e->lww_gen = 0;
+    }
+    if (++e->lww_gen == 0) {  // wrapped: stale stamps could alias the new generation
+      std::fill(e->lww_stamp.begin(), e->lww_stamp.end(), 0u);
+      e->lww_gen = 1;
+    }
+    const uint32_t gen = e->lww_gen;
     size_t k = vp.size();
     for (size_t i = vp.size(); i-- > 0;) {
-      if (!seen.insert((uint64_t)vp[i] * e->cfg.max_consumers + vc[i]).second) continue;
+      uint32_t& sl = e->lww_stamp[(size_t)vp[i] * e->cfg.max_consumers + vc[i]];
+      if (sl == gen) continue;
+      sl = gen;
       --k;
       vp[k] = vp[i];
       vc[k] = vc[i];

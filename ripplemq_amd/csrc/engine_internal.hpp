@@ -14,7 +14,6 @@
 #include <new>
 #include <string>
 #include <thread>
-#include <unordered_set>
 #include <vector>
 
 #include "../../include/ripplemq_engine.h"
@@ -309,6 +308,8 @@ struct rmq_engine {
     bool used = false;
   } cslot[2];
   uint32_t cslot_next = 0;
+  std::vector<uint32_t> lww_stamp;  // [P * C] generation of the last commit item seen per slot
+  uint32_t lww_gen = 0;
   // ack scratch
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;

@@ -3,10 +3,11 @@
 // committed state like MessageBatchReadRequestProcessor.java:39 (no read-index).
 //
 //  resolve (wave per request): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
-//          byte range of records [off, end): a 64-ary search of the sparse offset index (FORMAT.md
-//          §5: E[m] = first record starting at or after m*I; 64 probes per round, one round per
-//          factor 64 of index entries), then the record headers of the 1 KiB after the entry found
-//          are loaded at once (a lane per 16 bytes) and walked in registers;
+//          byte range of records [off, end): both ends found together, a half-wave each, by a
+//          32-ary search of the sparse offset index (FORMAT.md §5: E[m] = first record starting at
+//          or after m*I; 32 probes per round, one round per factor 32 of index entries), then the
+//          record headers of the 1 KiB after the entry found are loaded at once (two 16-byte pieces
+//          per lane of the half) and walked in registers;
 //          each workgroup adds its requests' bytes to the sum of their chunk of 256 requests;
 //  gather  (workgroup per 16 requests, a wave per 4): the output position of its first request from
 //          the chunk sums before it and the byte counts of its chunk before it (at most 64 + 255
@@ -18,7 +19,7 @@
 //          (Round 2 placed with a single 1024-thread workgroup between the two: 12.6 us of the
 //          max = 10 fetch of 16,384 requests with the rest of the GPU idle.)
 //
-// The three kernels run on the engine's fetch stream, after the last pipeline launch the host had
+// The kernels (a memset of the chunk sums, resolve, gather) run on the engine's fetch stream, after the last pipeline launch the host had
 // issued and before the next one (engine.cpp orders the two streams with events), so the committed
 // state they read is stable and the append pipeline is never flushed for a fetch.
 #include <hip/hip_ext.h>
@@ -128,6 +129,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
       v.start_pos = st.start_pos[p];
       if (off < v.start_off) {
         status = kOffset;
+        start = v.start_off;  // where the consumer can resume (FORMAT.md §7)
       } else {
         const u32 lm = st.local_mask[p];
         const u32 r0 = lm ? (u32)__ffs(lm) - 1u : 0u;
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   }
 }
 
-// ev[6]: start / end events of the three kernels, recorded by the dispatches themselves
+// ev[4]: start / end events of the two kernels, recorded by the dispatches themselves
 // (profiling: kernel time without the host's launch gaps), or null
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;

@@ -220,7 +220,7 @@ struct PipeArgs {
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
   uint32_t debug;          // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
-                           // 16 skip stages 1-2
+                           // 16 skip stages 1-2, 32 no leader / mask / totals gathers in stage 3
   // replication transport attached (else all null / n_out = 0)
   XPlanArgs xp2;           // stage 2's group: outbox plan
   const uint32_t* outidx;  // [P][RF] out entry of (partition, slot), ~0: local or no entry

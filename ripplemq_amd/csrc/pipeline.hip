@@ -977,13 +977,18 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   if (cand) {
     const u32 p = R.p;
     const u32 t = G.tile0[T.jb] + task_rec(T) / kTR;
-    lead = st.is_leader[p];
     ex = A.s3.excl[(u64)p * A.gt + t];
-    tot = A.s3.totals[p];
     leo = A.cur.leo[p];
     used = A.cur.used[p];
-    lm = st.local_mask[p];
     S.rdesc = st.ring[p];
+    if (A.debug & 32u) {  // timing experiment: three of the seven state gathers left out
+      lead = 1u;
+      lm = (1u << st.RF) - 1u;
+    } else {
+      lead = st.is_leader[p];
+      tot = A.s3.totals[p];
+      lm = st.local_mask[p];
+    }
   }
   // first round of payload blocks, speculatively (leadership is checked before any store)
   round_blocks(A, R, 0u, cand, S.blk);

@@ -79,6 +79,7 @@ class Engine:
         _check(self.lib.rmq_create(C.byref(c), C.byref(h)), "rmq_create")
         self.h = h
         self._keep: dict[int, tuple] = {}
+        self._pinned: dict[int, np.ndarray] = {}  # rmq_host_alloc buffers by address
         # append_device reuses one argument block: a producer loop calls it once per batch
         self._dbatch = A.RmqBatch(0, A.RMQ_MEM_DEVICE)
         self._dticket = C.c_uint64()
@@ -89,6 +90,9 @@ class Engine:
             self.lib.rmq_destroy(self.h)
             self.h = None
             self._keep.clear()
+            for p in list(self._pinned):  # after the engine: no DMA reads them any more
+                self.lib.rmq_host_free(None, C.c_void_p(p))
+            self._pinned.clear()
 
     def __enter__(self):
         return self
@@ -155,6 +159,38 @@ class Engine:
         _check(self.lib.rmq_append(self.h, C.byref(b), _ptr(out), C.byref(t)), "rmq_append")
         self._keep[t.value] = (pidx, lens, payload, payload_off, out)
         return t.value, out
+
+    # ---- page-locked host batches (RMQ_MEM_PINNED)
+    def host_empty(self, count: int, dtype) -> np.ndarray:
+        """A numpy array in page-locked host memory (rmq_host_alloc), freed with the engine or by
+        host_release. Batches whose arrays all come from here go to the device by DMA alone."""
+        dtype = np.dtype(dtype)
+        nbytes = max(int(count) * dtype.itemsize, 16)
+        p = C.c_void_p()
+        _check(self.lib.rmq_host_alloc(self.h, nbytes, C.byref(p)), "rmq_host_alloc")
+        buf = (C.c_uint8 * nbytes).from_address(p.value)
+        arr = np.frombuffer(buf, np.uint8, nbytes)[:int(count) * dtype.itemsize].view(dtype)
+        self._pinned[p.value] = arr
+        return arr
+
+    def host_release(self, arr: np.ndarray) -> None:
+        p = arr.__array_interface__["data"][0]
+        if self._pinned.pop(p, None) is not None:
+            _check(self.lib.rmq_host_free(self.h, C.c_void_p(p)), "rmq_host_free")
+
+    def append_pinned_async(self, pidx: np.ndarray, lens: np.ndarray, payload: np.ndarray, out: np.ndarray,
+                            payload_off: np.ndarray | None = None, payload_bytes: int | None = None) -> int:
+        """rmq_append of a batch whose arrays (and `out`, uint64[n]) are page-locked (host_empty):
+        one DMA per section, no host copy; the arrays must stay unchanged until the ticket
+        completes. Payload ranges are checked on the device (rejected_invalid), like device
+        batches."""
+        n = len(pidx)
+        nb = payload.size if payload_bytes is None else int(payload_bytes)
+        b = A.RmqBatch(n, A.RMQ_MEM_PINNED, _ptr(pidx), _ptr(lens), _ptr(payload_off),
+                       _ptr(payload) if nb else None, nb)
+        t = C.c_uint64()
+        _check(self.lib.rmq_append(self.h, C.byref(b), _ptr(out), C.byref(t)), "rmq_append")
+        return t.value
 
     def append_device(self, n: int, d_pidx: int, d_len: int, d_payload: int, payload_bytes: int,
                       d_out: int, d_payload_off: int | None = None) -> int:

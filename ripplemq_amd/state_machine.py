@@ -299,7 +299,9 @@ class PartitionBroker:
                     if not spilled:
                         self.durable.spill()
                         spilled = True
-                    off = int(res["start_offset"][k])
+                    # (the row's start_offset is the first retained offset there: the consumer's
+                    # own offset comes from the table)
+                    off = int(self.engine.consumer_offsets(p[k])[c[k]])
                     hw = int(self.engine.state(p[k])["high_watermark"])
                     recs = self.durable.read(p[k], off, min(mx[k], hw - off))
                     out[r] = MessageBatchReadResponse([_decode(b, self.as_str) for _, _, b in recs], off)

@@ -351,3 +351,32 @@ def test_multi_pass_sort(oracle_mod, P):
         run_ops(dev, ora, cfg, ops, check=False)
         parts = sorted({int(p) for b in range(3) for p in make_batch(spec, b).pidx if p < P})[:300]
         compare_state(dev, ora, cfg, parts=parts)
+
+
+def test_pinned_host_batches(oracle_mod):
+    # RMQ_MEM_PINNED: caller arrays in page-locked memory (rmq_host_alloc), one DMA per section
+    # and out offsets written by a DMA, submitted back to back (slots reused across groups);
+    # packed and explicit payload offsets, unknown partitions
+    cfg, dev, ora = pair(oracle_mod, num_partitions=256, replication_factor=3, segment_bytes=1 << 18,
+                         index_interval=256, max_batch_records=8192, pipeline_depth=4)
+    with dev, ora:
+        spec = StreamSpec(256, 5000, "zipf", size=(0, 300), config_index=31, invalid_frac=0.01)
+        batches = [make_batch(spec, b) for b in range(14)]
+        subs = []
+        for k, b in enumerate(batches):
+            n = b.n
+            pidx, lens, out = dev.host_empty(n, np.uint32), dev.host_empty(n, np.uint32), dev.host_empty(n, np.uint64)
+            pay = dev.host_empty(max(b.payload.size, 1), np.uint8)
+            pidx[:], lens[:], pay[:b.payload.size] = b.pidx, b.lens, b.payload
+            poff = None
+            if k % 3 == 2:  # explicit offsets
+                poff = dev.host_empty(n, np.uint64)
+                poff[:] = b.payload_offsets()
+            t = dev.append_pinned_async(pidx, lens, pay, out, payload_off=poff, payload_bytes=b.payload.size)
+            subs.append((t, out, poff))
+        for (t, out, poff), b in zip(subs, batches):
+            sd = dev.wait(t)
+            oo, so = ora.append(b.pidx, b.lens, b.payload)
+            assert sd == so, f"append stats gpu={sd} cpu={so}"
+            assert np.array_equal(out, oo)
+        compare_state(dev, ora, cfg, full_rings=True)

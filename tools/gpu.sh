@@ -11,7 +11,7 @@
 #   bench20    two driver-shaped lines (--steps 20 --warmup 5)
 #   steady     one 600-step line without the side legs
 #   benchD     config D (RF 5, 64 B..16 KB) line
-#   ab         A/B of the current library against variants/head/ (400- and 20-step lines, 2 pairs)
+#   ab[:NAME]  A/B of the current library against variants/NAME/ (default head; 400- and 20-step lines, 2 pairs)
 #   local2     2-rank rehearsal on one GPU over the in-process transport (+ kernel trace)
 #   local4     4-rank rehearsal (config C shape)
 #   prof       rocprofv3 --kernel-trace --stats of the default line (kernel stats CSV)
@@ -46,10 +46,11 @@ for step in "$@"; do
     bench20) for k in 1 2; do run 200 "${T}_bench20_$k.json" python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
     steady) run 300 "${T}_steady.json" python bench.py --steps 600 --warmup 60 $Q ;;
     benchD) run 300 "${T}_benchD.json" python bench.py --config D --pool 16 --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0 ;;
-    ab)
+    ab|ab:*)  # ab:NAME compares against variants/NAME/ (default head)
+      V=head; [ "$step" != ab ] && V=${step#ab:}
       for k in 1 2; do
-        for v in cur head; do
-          if [ $v = cur ]; then L=$R/ripplemq_amd/libripplemq_engine.so; else L=$R/variants/head/libripplemq_engine.so; fi
+        for v in cur $V; do
+          if [ $v = cur ]; then L=$R/ripplemq_amd/libripplemq_engine.so; else L=$R/variants/$V/libripplemq_engine.so; fi
           RMQ_LIB=$L run 200 "${T}_${v}_400_$k.json" python bench.py --steps 400 --warmup 40 $Q
           RMQ_LIB=$L run 200 "${T}_${v}_20_$k.json" python bench.py --steps 20 --warmup 5 $Q
         done
@@ -66,6 +67,9 @@ for step in "$@"; do
       RMQ_STAMPS=gpurun_out/${T}_st.csv RMQ_STAMPS_AT=100 run 200 "${T}_stamped.json" python bench.py --steps 600 --warmup 60 $Q
       python tools/pipe_stamps.py "gpurun_out/${T}_st.csv" > "gpurun_out/${T}_stamps.txt" 2>&1
       for d in 1 16; do RMQ_DEBUG=$d run 200 "${T}_dbg$d.json" python bench.py --steps 400 --warmup 40 $Q; done ;;
+    dbg:*)  # dbg:B1,B2,...: timing-only RMQ_DEBUG lines (results invalid) beside a plain one
+      run 200 "${T}_dbg0.json" python bench.py --steps 400 --warmup 40 $Q
+      for d in $(echo "${step#dbg:}" | tr , ' '); do RMQ_DEBUG=$d run 200 "${T}_dbg$d.json" python bench.py --steps 400 --warmup 40 $Q; done ;;
     knob:*)  # knob:VAR=v1,v2,...: steady and 20-step lines per value of one environment knob
       kv=${step#knob:}; var=${kv%%=*}
       for val in $(echo "${kv#*=}" | tr , ' '); do
