@@ -583,6 +583,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   hipDeviceProp_t prop;
   CREATE_HIP(hipGetDeviceProperties(&prop, e->device));
   e->cu_count = (uint32_t)prop.multiProcessorCount;
+  e->verify_wgs = 4u * e->cu_count;
+  if (const char* v = std::getenv("RMQ_VERIFY_WGS")) e->verify_wgs = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
@@ -1187,7 +1189,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4 + 2);
     if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
     if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 4);
-    if (!rc) rc = dalloc(&e->d_csum, (size_t)cap / kFetchChunk + 2);
+    if (!rc) rc = dalloc(&e->d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride);
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed

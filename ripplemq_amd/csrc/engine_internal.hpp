@@ -245,6 +245,7 @@ struct rmq_engine {
   std::mutex mu;
   int device = 0;
   uint32_t cu_count = 0;
+  uint32_t verify_wgs = 0;  // follower verify grid (RMQ_VERIFY_WGS; default 4 workgroups per CU)
   char dev_name[256] = {0};
   hipStream_t main_s = nullptr;
   DevState st{};            // leo/used point at sets[applied & 1]

@@ -46,18 +46,28 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   const u32 ilog = st.interval_log2;
   const u64 I = 1ull << ilog;
   const u64* E = st.index + v.rg.ibase * 2;
-  // per half: largest m in [lo, hi] with E[m].offset <= t (E rises with m), 32 probes per round;
-  // none: the log start
+  // per half: largest m in [lo, hi] with E[m].offset <= t (E rises with m); none: the log start.
+  // Round 0 probes the 32 entries around the interpolated position of t (records of one size:
+  // exact); a miss narrows [lo, hi] and the search goes on 32-ary, 32 probes per round.
   u64 c_off = v.start_off, c_pos = v.start_pos;
   long lo = (long)((v.start_pos + I - 1) >> ilog), hi = (long)(v.used >> ilog);
   bool open = t < v.leo && lo <= hi;
-  while (__any(open)) {
-    const long span = hi - lo + 1;
-    const long step = (span + 31) / 32;
-    const long m = lo + (long)hl * step;
+  long ws = lo, step = 1;
+  if (open) {
+    const double f = (double)(t - v.start_off) / (double)(v.leo - v.start_off);
+    const long me = (long)((v.start_pos + (u64)(f * (double)(v.used - v.start_pos))) >> ilog);
+    ws = max(lo, min(me - 15, hi - 31));
+  }
+  for (bool first = true; __any(open); first = false) {
+    if (!first) {
+      ws = lo;
+      step = (hi - lo + 32) / 32;
+    }
+    const long we = min(hi, ws + 31 * step);  // last probe of the round
+    const long m = ws + (long)hl * step;
     bool le = false;
     u64 eo = 0, ep = 0;
-    if (open && m <= hi) {
+    if (open && m <= we) {
       const u64* e = E + ((u64)m % v.rg.icap) * 2;
       eo = e[0];
       ep = e[1];
@@ -67,73 +77,89 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
     const u32 last = bal ? 31u - (u32)__builtin_clz(bal) : 0u;
     const u64 so = __shfl(eo, (int)(32u * h + last), 64), sp = __shfl(ep, (int)(32u * h + last), 64);
     if (open) {
-      if (!bal) {
-        open = false;  // every probe past t: the answer precedes this round's range
+      if (!bal) {  // every probe past t: the answer precedes this round's first probe
+        hi = ws - 1;
+        open = lo <= hi;
       } else {
         c_off = so;
         c_pos = sp;
-        if (step == 1) {
-          open = false;
+        const long mk = ws + (long)last * step;  // a probe at or before t
+        if (step == 1 && (mk < we || we == hi)) {
+          open = false;  // the next entry is past t (or there is none)
         } else {
-          lo = lo + (long)last * step + 1;  // the answer is that probe or one of the next step - 1
-          hi = min(hi, lo + step - 2);
+          lo = mk + 1;  // the answer is that probe or a later entry, up to the next probe
+          if (step > 1 && mk < we) hi = min(hi, mk + step - 1);
           open = lo <= hi;
         }
       }
     }
   }
   if (t >= v.leo) return v.used;
-  // walk the headers of the records in [c_off, t): they start in the interval after c_pos, so one
-  // 1 KiB window of 16-byte pieces holds them all (two pieces per lane of the half)
+  // walk the headers of the records in [c_off, t): they start within one index interval after
+  // c_pos, read as 1 KiB windows of 16-byte pieces (two pieces per lane of the half; one window
+  // when I <= 1 KiB)
   const u64 mask = v.rg.seg - 1;
-  const u32 Lw0 = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 32ull * hl + 8ull) & mask));
-  const u32 Lw1 = *reinterpret_cast<const u32*>(v.ring + ((c_pos + 32ull * hl + 24ull) & mask));
+  u64 wb = c_pos;
+  u32 Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
+  u32 Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
   u64 k = t - c_off;
   u32 cur = 0;  // window piece of the current record
   while (__any(k > 0)) {
+    const bool mv = k > 0 && cur >= 64u;  // half-uniform: the half walked off its window
+    if (__any(mv)) {
+      if (mv) {
+        wb += 16ull * cur;
+        cur = 0;
+        Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
+        Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
+      }
+    }
     const u32 src = 32u * h + (cur >> 1);
-    const u32 a0 = (u32)__shfl((int)Lw0, (int)src, 64), a1 = (u32)__shfl((int)Lw1, (int)src, 64);
+    const u32 a0 = (u32)__shfl((int)Lw0, (int)(src & 63u), 64), a1 = (u32)__shfl((int)Lw1, (int)(src & 63u), 64);
     if (k > 0) {
       cur += record_bytes((cur & 1u) ? a1 : a0) >> 4;
       --k;
     }
   }
-  return c_pos + 16ull * cur;
+  return wb + 16ull * cur;
 }
 
 __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
   const u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6));
-  if (r >= a.n) return;
+  const bool live = r < a.n;  // (no early return: the workgroup meets at a barrier below)
   const DevState& st = a.st;
-  const u32 p = a.req[4 * r], c = a.req[4 * r + 1], mx = a.req[4 * r + 2];
+  const u32 p = live ? a.req[4 * r] : 0u, c = live ? a.req[4 * r + 1] : 0u, mx = live ? a.req[4 * r + 2] : 0u;
   int status = kOk;
   u64 start = 0, count = 0, bytes = 0, pos0 = 0, ring_off = 0;
-  if (p >= st.P) {
+  if (!live) {
+  } else if (p >= st.P) {
     status = kNoPart;
   } else if (!st.is_leader[p]) {
     status = kNotLeader;
   } else if (c >= st.C) {
     status = kInval;
   } else {
+    // every word of the partition in one round (those of an empty slice go unused)
     const u64 off = st.cons[(u64)p * st.C + c];
+    const u64 hw = st.hw[p];
+    PartView v;
+    v.leo = st.leo[p];
+    v.used = st.used[p];
+    v.start_off = st.start_off[p];
+    v.start_pos = st.start_pos[p];
+    const u32 lm = st.local_mask[p];
+    const u64 desc = st.ring[p];
     start = off;
     u64 lim = off + mx;
     if (lim < off) lim = ~0ull;
-    const u64 hw = st.hw[p];
     const u64 end = lim < hw ? lim : hw;
     if (off < end) {
-      PartView v;
-      v.leo = st.leo[p];
-      v.used = st.used[p];
-      v.start_off = st.start_off[p];
-      v.start_pos = st.start_pos[p];
       if (off < v.start_off) {
         status = kOffset;
         start = v.start_off;  // where the consumer can resume (FORMAT.md §7)
       } else {
-        const u32 lm = st.local_mask[p];
         const u32 r0 = lm ? (u32)__ffs(lm) - 1u : 0u;
-        v.rg = ring_ref(st, p);
+        v.rg = ring_ref(desc, st.interval_log2, st.icap_mul);
         ring_off = (u64)r0 * st.rstride + v.rg.base;
         v.ring = st.logs + ring_off;
         const u64 pp = record_pos2(st, p, v, off, end);
@@ -143,14 +169,22 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
       }
     }
   }
-  if (lane_id() == 0) {
+  __shared__ u64 s_b[kFW];
+  if (lane_id() == 0) s_b[threadIdx.x >> 6] = bytes;
+  if (live && lane_id() == 0) {
     a.res[4 * r + 0] = start;
     a.res[4 * r + 2] = count | (bytes << 32);
     a.res[4 * r + 3] = (u64)(uint32_t)status;
     a.aux[2 * r + 0] = pos0;
     a.aux[2 * r + 1] = (ring_off << 6) | (st.ring[p < st.P ? p : 0] & 63ull);  // ring | log2(ring bytes)
     a.cpre[r] = (u32)bytes;
-    if (bytes) atomicAdd((unsigned long long*)&a.csum[r / kFetchChunk], (unsigned long long)bytes);
+  }
+  // one add per workgroup (its kFW requests share a chunk) into the chunk's own L2 line
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    u64 b = 0;
+    for (u32 k = 0; k < kFW; ++k) b += s_b[k];
+    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kFW / kFetchChunk) * kCsumStride], (unsigned long long)b);
   }
 }
 
@@ -166,7 +200,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   const u32 r0 = blockIdx.x * kGR, c0 = r0 / kFetchChunk;
   // bytes of every request before r0: the chunk sums before its chunk, then its chunk's requests
   u64 v = 0;
-  for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[k];
+  for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[(u64)k * kCsumStride];
   for (u32 k = c0 * kFetchChunk + tid; k < r0; k += 64 * kFW) v += a.cpre[k];
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -217,7 +251,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
-  (void)hipMemsetAsync(a.csum, 0, 8ull * (a.n / kFetchChunk + 1), s);
+  (void)hipMemsetAsync(a.csum, 0, 8ull * kCsumStride * (a.n / kFetchChunk + 1), s);
   hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW - 1) / kFW), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);
   hipExtLaunchKernelGGL(fetch_gather_kernel, dim3((a.n + kGR - 1) / kGR), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,

@@ -244,7 +244,9 @@ struct FetchArgs {
   uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}, then {bytes needed}
   uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
   uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> gather), 16-byte aligned
-  uint64_t* csum;            // [n / kFetchChunk + 1] bytes of each chunk of kFetchChunk requests
+  uint64_t* csum;            // [n / kFetchChunk + 1][kCsumStride] bytes of each chunk of kFetchChunk
+                             //   requests (one 128-byte line per chunk: the adds of different
+                             //   chunks never meet in one L2 line)
                              //   (resolve adds, zeroed before it)
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
@@ -252,6 +254,7 @@ struct FetchArgs {
   uint32_t pad;
 };
 constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
+constexpr uint32_t kCsumStride = 16;   // u64 words per chunk sum (128 bytes)
 
 
 
@@ -325,7 +328,7 @@ void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
-void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, hipStream_t s);
+void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
 // chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))
 void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s);

@@ -168,24 +168,8 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
   }
 }
 
-__global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
-  __shared__ __attribute__((aligned(16))) u32 t8[8][256];
-  __shared__ __attribute__((aligned(16))) u32 z[2][4][256];
-  __shared__ __attribute__((aligned(16))) u32 zk[4][256];  // 1 KB shift: records over 1 KB, by the wave
-  {
-    static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
-    static_assert(offsetof(CrcConsts, zshift1k) == offsetof(CrcConsts, zshift) + sizeof(A.crc->zshift), "zshift1k next");
-    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
-    uint4* d0 = reinterpret_cast<uint4*>(&t8[0][0]);
-    uint4* d1 = reinterpret_cast<uint4*>(&z[0][0][0]);
-    uint4* d2 = reinterpret_cast<uint4*>(&zk[0][0]);
-    for (u32 k = threadIdx.x; k < sizeof(t8) / 16; k += kIT) d0[k] = src[k];
-    for (u32 k = threadIdx.x; k < sizeof(z) / 16; k += kIT) d1[k] = src[sizeof(t8) / 16 + k];
-    for (u32 k = threadIdx.x; k < sizeof(zk) / 16; k += kIT) d2[k] = src[(sizeof(t8) + sizeof(z)) / 16 + k];
-  }
-  __syncthreads();
-  const u32 task = __builtin_amdgcn_readfirstlane(blockIdx.x * kIW + (threadIdx.x >> 6));
-  if (task >= A.task0[A.world]) return;
+// One task (32 records of one source region) of the verify kernel, by one wave.
+__device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)[256], const u32 (*z32)[256], u32 task) {
   const u32 src = source_of_task(A, task);
   if (!A.rbytes[src]) return;
   const RegionView R = region_of(A, src);
@@ -240,11 +224,12 @@ __global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
       if (jp < mm) {
         uint4 w = v[u];
         if (jp == 0) w.x ^= 0xFFFFFFFFu;
-        acc = crc_zshift(z[1], acc) ^ crc_piece16(t8, w);
+        acc = crc_zshift(z32, acc) ^ crc_piece16(t8, w);
       }
     }
   }
-  if (ok && mm > j && ((mm - 1u - j) & 1u)) acc = crc_zshift(z[0], acc);
+  // the lane whose last piece is one short of the record's end: shift past those 16 bytes
+  if (ok && mm > j && ((mm - 1u - j) & 1u)) acc = gf2_mulmod(acc, A.crc->sh16[1]);
   acc ^= pair_swap(acc);
   // records over 1 KB, one at a time by the wave: lane l takes pieces l, l + 64, ... (Horner with
   // the 1 KB shift), shifts past the pieces after its last one, XOR-reduce; the record's lane 1
@@ -268,7 +253,7 @@ __global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
         if (jp < bm16) {
           uint4 w = v[u];
           if (jp == 0) w.x ^= 0xFFFFFFFFu;
-          bacc = crc_zshift(zk, bacc) ^ crc_piece16(t8, w);
+          bacc = crc_zshift(A.crc->zshift1k, bacc) ^ crc_piece16(t8, w);  // (L1/L2-resident)
         }
       }
     }
@@ -310,6 +295,27 @@ __global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
       atomicOr(&A.bad[e], kBadCrc);  // CRC32C differs from the header's
     }
   }
+}
+
+// A grid of at most a few workgroups per CU: each copies the CRC tables into LDS once and its waves
+// take tasks w, w + waves, ... (the tables were 20 KB per 32 records' worth of workgroup before;
+// the 16-byte shift is a multiply, the 1 KB one of large records is read from global memory).
+__global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
+  __shared__ __attribute__((aligned(16))) u32 t8[8][256];
+  __shared__ __attribute__((aligned(16))) u32 z32[4][256];  // register shift past 32 zero bytes
+  {
+    static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
+    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+    const uint4* zs = reinterpret_cast<const uint4*>(&A.crc->zshift[1][0][0]);
+    uint4* d0 = reinterpret_cast<uint4*>(&t8[0][0]);
+    uint4* d1 = reinterpret_cast<uint4*>(&z32[0][0]);
+    for (u32 k = threadIdx.x; k < sizeof(t8) / 16; k += kIT) d0[k] = src[k];
+    for (u32 k = threadIdx.x; k < sizeof(z32) / 16; k += kIT) d1[k] = zs[k];
+  }
+  __syncthreads();
+  const u32 tasks = A.task0[A.world], stride = gridDim.x * kIW;
+  for (u32 task = __builtin_amdgcn_readfirstlane(blockIdx.x * kIW + (threadIdx.x >> 6)); task < tasks; task += stride)
+    verify_task(A, t8, z32, task);
 }
 
 __global__ void ingest_finish_kernel(IngestArgs A) {
@@ -440,9 +446,10 @@ __global__ void ack_apply_kernel(AckApplyArgs a) {
   }
 }
 
-void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, hipStream_t s) {
+void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s) {
   if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
-  if (tasks) hipLaunchKernelGGL(ingest_verify_kernel, dim3((tasks + kIW - 1) / kIW), dim3(kIT), 0, s, a);
+  if (tasks)
+    hipLaunchKernelGGL(ingest_verify_kernel, dim3(std::min<uint32_t>((tasks + kIW - 1) / kIW, verify_wgs)), dim3(kIT), 0, s, a);
   if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
   if (items_bound) hipLaunchKernelGGL(ingest_copy_kernel, dim3(items_bound), dim3(kCT), 0, s, a);
 }

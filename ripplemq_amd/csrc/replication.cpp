@@ -171,7 +171,7 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.crc = e->d_crc;
   a.counters = r->d_counters;
   HIP_TRY(hipMemsetAsync(r->d_nitems, 0, 4, r->xchg_s));
-  launch_ingest(a, tasks, items, r->xchg_s);
+  launch_ingest(a, tasks, items, e->verify_wgs, r->xchg_s);
   HIP_TRY(hipGetLastError());
   // acks: {log end | status, position} of every in entry back to its leader, fixed sizes both ways
   for (uint32_t q = 0; q < W; ++q) {

@@ -219,9 +219,12 @@ def test_explicit_payload_offsets(oracle_mod):
         run_ops(dev, ora, cfg, [("append", b, off, payload)], full_rings=True)
 
 
-def test_consumer_fetch_paths(oracle_mod):
-    cfg, dev, ora = pair(oracle_mod, num_partitions=32, replication_factor=3, segment_bytes=1 << 16,
-                         index_interval=256, max_consumers=4, max_batch_records=8192)
+@pytest.mark.parametrize("interval,seg", [(256, 1 << 16), (4096, 1 << 16)])
+def test_consumer_fetch_paths(oracle_mod, interval, seg):
+    # interval 4096: the records between an index entry and a fetch bound span several of the
+    # resolve's 1 KiB header windows
+    cfg, dev, ora = pair(oracle_mod, num_partitions=32, replication_factor=3, segment_bytes=seg,
+                         index_interval=interval, max_consumers=4, max_batch_records=8192)
     with dev, ora:
         # 450 records (~50 KB) per batch fit the 64 KB rings; hot partitions wrap them (eviction)
         spec = StreamSpec(32, 450, "zipf", size=(1, 180), config_index=17)

@@ -76,6 +76,13 @@ for step in "$@"; do
         env "$var=$val" timeout -k 10 200 python bench.py --steps 600 --warmup 60 $Q > "gpurun_out/${T}_${var}_${val}_600.json" 2>&1 || exit 1
         env "$var=$val" timeout -k 10 200 python bench.py --steps 20 --warmup 5 $Q > "gpurun_out/${T}_${var}_${val}_20.json" 2>&1 || exit 1
       done ;;
+    fetchprof|fetchprof:*)  # kernel trace of the fetch legs (short append run), current library and variants/NAME
+      V=${step#fetchprof}; V=${V#:}
+      FQ="--steps 100 --warmup 10 --no-cpu-baseline --concurrent-rounds 0 --host-steps 0"
+      prof 300 fetchprof_cur --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_fetchprof_cur" -o kt -- python3 "$R/bench.py" $FQ
+      if [ -n "$V" ]; then
+        RMQ_LIB=$R/variants/$V/libripplemq_engine.so prof 300 fetchprof_$V --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_fetchprof_$V" -o kt -- python3 "$R/bench.py" $FQ
+      fi ;;
     xstamps)  # phase stamps of one launch of the 2-rank rehearsal (transport kernel, 8 waves/workgroup)
       RMQ_STAMPS=gpurun_out/${T}_xst.csv RMQ_STAMPS_AT=60 run 300 "${T}_xstamped.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
       python tools/pipe_stamps.py "gpurun_out/${T}_xst.csv" > "gpurun_out/${T}_xstamps.txt" 2>&1 ;;
