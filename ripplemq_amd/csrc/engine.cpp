@@ -168,6 +168,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.gt = e->max_group_tiles;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
+  a.ret_late = e->done_dev + 1;
   a.debug = e->debug;
   if (s1) {
     a.g1 = make_group(e, *s1);
@@ -199,7 +200,14 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.g3 = make_group(e, *s3);
     a.s3 = e->scratch[s3->set];
     const uint32_t wpb = PT / 64;
-    const uint32_t want = std::max<uint32_t>(1u, (s3->tasks + wpb - 1) / wpb);
+    // wide form (a wave per task pair) when every batch of the group averages at most 112 payload
+    // bytes per record: a wave meeting a longer record falls back to lane pairs, task by task
+    bool wide = e->wide && !a.outidx;
+    for (uint32_t j = 0; j < s3->nb && wide; ++j)
+      wide = s3->b[j].b.payload_bytes <= 112ull * s3->b[j].b.n;
+    a.wide3 = wide ? 1u : 0u;
+    const uint32_t units = wide ? (s3->tasks + 1) / 2 : s3->tasks;
+    const uint32_t want = std::max<uint32_t>(1u, (units + wpb - 1) / wpb);
     // default: one wave per task (the workgroups past the resident slots start as stage-1/2
     // workgroups retire); RMQ_WG3_ALL=0 fills only the slots next to the other roles (resident
     // workgroups per CU from the kernel's launch bounds) and the task waves loop over the rest
@@ -260,6 +268,7 @@ int close_group(rmq_engine* e) {
   if (rc) return rc;
   e->has3 = e->has2;
   e->g3 = e->g2;
+  if (e->has3) e->g3_seq = e->launch_seq;  // the launch that applied it
   e->has2 = e->has1;
   e->g2 = e->g1;
   e->has1 = s1 != nullptr;
@@ -268,9 +277,12 @@ int close_group(rmq_engine* e) {
   return RMQ_OK;
 }
 
-// Push everything through stage 4 (at most four launches).
+// Push everything through stage 3 (at most three launches). The stage-3 launch of a group applies
+// its retention too unless a partition's group outgrew the entries written before it
+// (pipeline.hip partition_threads): drain() then adds the stage-4 launch. With a transport a flush
+// is collective and every rank makes the same launches: stage 4 always.
 int flush(rmq_engine* e) {
-  while (e->forming.nb || e->has1 || e->has2 || e->has3) {
+  while (e->forming.nb || e->has1 || e->has2 || (e->has3 && e->repl)) {
     int rc = close_group(e);
     if (rc) return rc;
   }
@@ -289,6 +301,16 @@ int drain(rmq_engine* e) {
   }
   rc = stream_wait(e->main_s);
   if (rc) return rc;
+  if (e->has3) {  // the last group's retention: finished by its own launch unless ret_late names it
+    if (__atomic_load_n(e->done_host + 1, __ATOMIC_ACQUIRE) >= e->g3_seq) {
+      rc = close_group(e);  // stage 4 alone
+      if (rc) return rc;
+      if (e->profile && e->prof_ended) HIP_TRY(hipEventRecord(e->prof_t1, e->main_s));
+      rc = stream_wait(e->main_s);
+      if (rc) return rc;
+    }
+    e->has3 = false;
+  }
   collect_done(e);
   return RMQ_OK;
 }
@@ -569,6 +591,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S2_WGS")) e->s2_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_WIDE")) e->wide = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
@@ -661,7 +684,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(2u * e->cu_count + kMaxTiles + (P + kPipeThreads - 1) / kPipeThreads +
                                                        kMaxTiles * kTileRecs / (kTaskRecs * kPipeThreads / 64)) * 64));
   CREATE_HIP(hipHostMalloc((void**)&e->done_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
-  *e->done_host = 0;
+  e->done_host[0] = e->done_host[1] = 0;
   CREATE_HIP(hipHostGetDevicePointer((void**)&e->done_dev, e->done_host, 0));
   {
     CrcConsts h;

@@ -266,11 +266,13 @@ struct rmq_engine {
   // and applied (need stage 4)
   GroupFlight forming, g1, g2, g3;
   bool has1 = false, has2 = false, has3 = false;
+  uint64_t g3_seq = 0;  // the launch that applied g3 (its retention is late if done_host[1] >= it)
   uint32_t group_max = 2;       // batches per group (cfg.pipeline_depth)
   uint32_t max_group_tiles = 0;
   uint64_t groups = 0;          // groups formed
   uint64_t launch_seq = 0;
-  uint64_t* done_host = nullptr;     // pinned: launch k-1 complete, written by launch k
+  uint64_t* done_host = nullptr;     // pinned: [0] launch k-1 complete, written by launch k;
+                                     // [1] the last launch whose retention stopped early
   uint64_t* done_dev = nullptr;
   uint64_t last_ticket = 0;
   std::vector<uint32_t> ticket_n;        // [kStatsRing] records of each recent ticket (stats)
@@ -335,6 +337,7 @@ struct rmq_engine {
   uint32_t s1_wgs = 0;    // RMQ_S1_WGS: stage-1 workgroups per launch (0: one per tile; fewer loop over tiles)
   uint32_t s2_wgs = 0;    // RMQ_S2_WGS: cap on stage-2 workgroups (0: one thread group per column)
   uint32_t s3_first = 1;  // stage-3 workgroups first in dispatch order (RMQ_S3_FIRST=0: last)
+  uint32_t wide = 1;      // stage 3's wide form for groups of short records (RMQ_WIDE=0: lane pairs only)
   uint32_t s3_lead = 0;   // stage-3 workgroups before the other roles (RMQ_S3_LEAD; 0: all of them)
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
   std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)

@@ -13,8 +13,9 @@
 //          the chunk sums before it and the byte counts of its chunk before it (at most 64 + 255
 //          values, L2-resident), an exclusive scan over its 16 requests -> compact output positions
 //          (into the result rows' out_pos), ENOSPC marking (every request's bytes count, served or
-//          not: FORMAT.md §7); then 16-byte loads from the lowest local replica ring, four in flight
-//          per lane, 16-byte stores to the output. Records and output positions are 16-byte aligned
+//          not: FORMAT.md §7); then each wave copies its 4 requests as one run of 16-byte pieces
+//          (the requests' loads in flight together, four per lane) from the lowest local replica
+//          ring to the output. Records and output positions are 16-byte aligned
 //          (FORMAT.md §1), so no piece straddles a record, the ring end or an output boundary.
 //          (Round 2 placed with a single 1024-thread workgroup between the two: 12.6 us of the
 //          max = 10 fetch of 16,384 requests with the rest of the GPU idle.)
@@ -131,24 +132,28 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
   const u32 p = live ? a.req[4 * r] : 0u, c = live ? a.req[4 * r + 1] : 0u, mx = live ? a.req[4 * r + 2] : 0u;
   int status = kOk;
   u64 start = 0, count = 0, bytes = 0, pos0 = 0, ring_off = 0;
+  // every word of the partition in one round, the leader flag included (a request refused by the
+  // checks below, or with an empty slice, leaves them unused)
+  const bool okp = live && p < st.P;
+  const u32 pp = okp ? p : 0u, cc = c < st.C ? c : 0u;
+  const u32 lead = okp ? st.is_leader[pp] : 0u;
+  const u64 off = okp ? st.cons[(u64)pp * st.C + cc] : 0ull;
+  const u64 hw = okp ? st.hw[pp] : 0ull;
+  PartView v;
+  v.leo = okp ? st.leo[pp] : 0ull;
+  v.used = okp ? st.used[pp] : 0ull;
+  v.start_off = okp ? st.start_off[pp] : 0ull;
+  v.start_pos = okp ? st.start_pos[pp] : 0ull;
+  const u32 lm = okp ? st.local_mask[pp] : 0u;
+  const u64 desc = okp ? st.ring[pp] : 0ull;
   if (!live) {
   } else if (p >= st.P) {
     status = kNoPart;
-  } else if (!st.is_leader[p]) {
+  } else if (!lead) {
     status = kNotLeader;
   } else if (c >= st.C) {
     status = kInval;
   } else {
-    // every word of the partition in one round (those of an empty slice go unused)
-    const u64 off = st.cons[(u64)p * st.C + c];
-    const u64 hw = st.hw[p];
-    PartView v;
-    v.leo = st.leo[p];
-    v.used = st.used[p];
-    v.start_off = st.start_off[p];
-    v.start_pos = st.start_pos[p];
-    const u32 lm = st.local_mask[p];
-    const u64 desc = st.ring[p];
     start = off;
     u64 lim = off + mx;
     if (lim < off) lim = ~0ull;
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
     a.res[4 * r + 2] = count | (bytes << 32);
     a.res[4 * r + 3] = (u64)(uint32_t)status;
     a.aux[2 * r + 0] = pos0;
-    a.aux[2 * r + 1] = (ring_off << 6) | (st.ring[p < st.P ? p : 0] & 63ull);  // ring | log2(ring bytes)
+    a.aux[2 * r + 1] = (ring_off << 6) | (desc & 63ull);  // ring | log2(ring bytes)
     a.cpre[r] = (u32)bytes;
   }
   // one add per workgroup (its kFW requests share a chunk) into the chunk's own L2 line
@@ -186,6 +191,11 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
     for (u32 k = 0; k < kFW; ++k) b += s_b[k];
     if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kFW / kFetchChunk) * kCsumStride], (unsigned long long)b);
   }
+}
+
+__device__ __forceinline__ u64 lane64(u64 v, u32 l) {  // lane l's value, wave-uniform
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+         (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
 }
 
 constexpr u32 kGQ = 4;          // requests per gather wave
@@ -221,28 +231,59 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
     }
     if (rr + 1 == a.n) a.res[4ull * a.n] = pos + nb;  // bytes needed
   }
+  // the wave's kGQ requests (lanes 0..kGQ-1 read one each; their ring words are loaded before the
+  // barrier, so they are in flight during the placement scan)
+  const u32 rq = r0 + w * kGQ + (lane < kGQ ? lane : 0u);
+  const bool qv = lane < kGQ && rq < a.n;
+  const u64 q_pos = qv ? a.aux[2 * rq + 0] : 0ull, q_ring = qv ? a.aux[2 * rq + 1] : 0ull;
+  const u64 q_nb = qv ? a.cpre[rq] : 0ull;
   __syncthreads();
+  // one run of 16-byte pieces over the wave's requests (each served request's pieces in order),
+  // so the loads of all of them are in flight together instead of one request after another
+  const u64 q_out = lane < kGQ ? s_pos[(w * kGQ + lane) & (kGR - 1u)] : 0ull;
+  const bool served = qv && q_nb && q_out + q_nb <= a.out_cap;
+  const u64 q_pc = served ? q_nb >> 4 : 0ull;
+  u64 pc[kGQ + 1], ps[kGQ], po[kGQ], pm[kGQ];
+  const uint8_t* pr[kGQ];
+  pc[0] = 0;
+#pragma unroll
   for (u32 q = 0; q < kGQ; ++q) {
-    const u32 i = w * kGQ + q, r = r0 + i;
-    if (r >= a.n) break;
-    const u64 pos0_out = s_pos[i];
-    const u64 nbr = a.cpre[r];
-    if (!nbr || pos0_out + nbr > a.out_cap) continue;
-    const u64 pos0 = a.aux[2 * r + 0];
-    const uint8_t* ring = st.logs + (a.aux[2 * r + 1] >> 6);
-    const u64 mask = (1ull << (a.aux[2 * r + 1] & 63ull)) - 1ull;
-    uint8_t* out = a.out + pos0_out;
-    const u64 pieces = nbr >> 4;
-    u64 p = lane;
-    for (; p + 192 < pieces; p += 256) {  // four 16-byte pieces in flight per lane
-      uint4 x[4];
+    pc[q + 1] = pc[q] + lane64(q_pc, q);
+    ps[q] = lane64(q_pos, q);
+    po[q] = lane64(q_out, q);
+    const u64 rw = lane64(q_ring, q);
+    pr[q] = st.logs + (rw >> 6);
+    pm[q] = (1ull << (rw & 63ull)) - 1ull;
+  }
+  const u64 total = pc[kGQ];
+  for (u64 b = 0; b < total; b += 64ull * 4) {  // four 16-byte pieces in flight per lane
+    uint4 x[4];
+    uint8_t* dst[4];
 #pragma unroll
-      for (u32 u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 64 * u)) & mask));
+    for (u32 u = 0; u < 4; ++u) {
+      const u64 k = b + 64ull * u + lane;
+      dst[u] = nullptr;
+      if (k < total) {
+        // the request holding piece k (kGQ wave-uniform candidates, selected without indexing)
+        u64 s = ps[0], o = po[0], m = pm[0], c = pc[0];
+        const uint8_t* rg = pr[0];
 #pragma unroll
-      for (u32 u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(out + 16ull * (p + 64 * u)) = x[u];
+        for (u32 q = 1; q < kGQ; ++q)
+          if (k >= pc[q]) {
+            s = ps[q];
+            o = po[q];
+            m = pm[q];
+            c = pc[q];
+            rg = pr[q];
+          }
+        const u64 j = k - c;
+        x[u] = *reinterpret_cast<const uint4*>(rg + ((s + 16ull * j) & m));
+        dst[u] = a.out + o + 16ull * j;
+      }
     }
-    for (; p < pieces; p += 64)
-      *reinterpret_cast<uint4*>(out + 16ull * p) = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * p) & mask));
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u)
+      if (dst[u]) *reinterpret_cast<uint4*>(dst[u]) = x[u];
   }
 }
 

@@ -166,7 +166,7 @@ __device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
-__device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
+__device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
   const PipeGroup& G = A.g1;
   const u32 jb = batch_of_tile(G, t);
   const PipeBatch& b = G.b[jb];
@@ -400,7 +400,7 @@ __device__ __forceinline__ u64 block_incl_scan_u64(u64 v, u64* s_w, u64* total) 
 // thread of its partition's column once the group's totals of p are known (`tot`). B = the leader's
 // log end before the round: the state this launch's stage 3 reads (after the group two before)
 // plus the totals of the group it applies (the group before), E = B + the round.
-__device__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
+__device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u64 t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
@@ -456,7 +456,7 @@ __device__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
 
 // End of a partial catch-up (FORMAT.md §9): the largest sparse-index entry E[m] with
 // F.pos < E[m].pos <= lim among the entries complete now (m I <= used); 0 if none.
-__device__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
+__device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
   const RingRef rg = ring_ref(st, p);
   const u32 ilog = st.interval_log2;
   u64 lo = (fpos >> ilog) + 1ull, hi = min(lim, used) >> ilog;  // candidates m in [lo, hi]
@@ -488,7 +488,7 @@ __device__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 us
 // (the gap, then the round's own), where stage 3 puts the round's records and table slots, the
 // catch-up list for the stage-3 launch's copy waves, the consumer-offset row, the next expected
 // follower log end.
-__device__ void stage2_plan(const PipeArgs& A) {
+__device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u64* const totals = A.s2.totals;
@@ -780,7 +780,7 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
   }
 }
 
-__device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
+__device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
   const u32 P = A.st.P, T = G.tiles, GT = A.gt;
@@ -925,18 +925,18 @@ struct TaskState {
   uint4 blk[kBL];
 };
 
-__device__ __forceinline__ TaskRec stage3_r1(const PipeArgs& A, const TaskPos& T) {
+// Record i of batch jb of the group in stage 3 (every lane: its own record, or its pair's).
+__device__ __forceinline__ TaskRec stage3_r1_at(const PipeArgs& A, u32 jb, u32 i) {
   const PipeGroup& G = A.g3;
   const PipeScratch& x = A.s3;
-  const PipeBatch& b = G.b[T.jb];
-  const u32 i = task_rec(T);
+  const PipeBatch& b = G.b[jb];
   TaskRec r;
   r.p = 0u;
   r.L = 0u;
   r.cr = make_uint2(kFlJunk << kFlagShift, 0u);
   r.src = reinterpret_cast<u64>(b.payload);
   if (i < b.n) {
-    const u64 gi = (u64)G.tile0[T.jb] * kTR + i;  // group record slot
+    const u64 gi = (u64)G.tile0[jb] * kTR + i;  // group record slot
     r.p = b.pidx[i];
     r.L = b.len[i];
     r.cr = x.crank[gi];
@@ -944,11 +944,16 @@ __device__ __forceinline__ TaskRec stage3_r1(const PipeArgs& A, const TaskPos& T
   }
   return r;
 }
+__device__ __forceinline__ TaskRec stage3_r1(const PipeArgs& A, const TaskPos& T) { return stage3_r1_at(A, T.jb, task_rec(T)); }
 
-__device__ __forceinline__ u32 batch_rej(const PipeArgs& A, const TaskPos& T) { return (u32)A.s3.binfo[T.jb * 4]; }
+__device__ __forceinline__ u32 batch_rej(const PipeArgs& A, u32 jb) { return (u32)A.s3.binfo[jb * 4]; }
+__device__ __forceinline__ u32 batch_rej(const PipeArgs& A, const TaskPos& T) { return batch_rej(A, T.jb); }
 
+__device__ __forceinline__ bool stage3_cand_at(const PipeArgs& A, u32 jb, u32 i, const TaskRec& R) {
+  return i < A.g3.b[jb].n && (R.cr.x >> kFlagShift) == 0u && batch_rej(A, jb) == 0u;
+}
 __device__ __forceinline__ bool stage3_cand(const PipeArgs& A, const TaskPos& T, const TaskRec& R) {
-  return task_rec(T) < A.g3.b[T.jb].n && (R.cr.x >> kFlagShift) == 0u && batch_rej(A, T) == 0u;
+  return stage3_cand_at(A, T.jb, task_rec(T), R);
 }
 
 // Aligned payload blocks of round c held by lane j: block 8c + j + 2q, q < kBL, loaded only if
@@ -965,44 +970,59 @@ __device__ __forceinline__ void round_blocks(const PipeArgs& A, const TaskRec& R
   }
 }
 
-__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos& T, const TaskRec& R, bool cand) {
-  const PipeGroup& G = A.g3;
+// The words of record i's partition state that place it (one round of gathers; lanes without a
+// candidate record load nothing).
+struct RecWords {
+  u64 ex, tot, leo, used, rdesc;
+  u32 lead, lm;
+};
+__device__ __forceinline__ RecWords rec_words(const PipeArgs& A, u32 jb, u32 i, u32 p, bool cand) {
   const DevState& st = A.st;
-  TaskState S;
-  S.pos = S.off = 0ull;
-  S.rdesc = 8ull;  // any valid descriptor (a 256-byte ring at 0) for lanes that store nothing
-  S.lm = S.dead = S.rel16 = S.rk = 0u;
-  u64 ex = 0, tot = 0, leo = 0, used = 0;
-  u32 lead = 0, lm = 0;
+  RecWords W;
+  W.ex = W.tot = W.leo = W.used = 0ull;
+  W.rdesc = 8ull;  // any valid descriptor (a 256-byte ring at 0) for lanes that store nothing
+  W.lead = W.lm = 0u;
   if (cand) {
-    const u32 p = R.p;
-    const u32 t = G.tile0[T.jb] + task_rec(T) / kTR;
-    ex = A.s3.excl[(u64)p * A.gt + t];
-    leo = A.cur.leo[p];
-    used = A.cur.used[p];
-    S.rdesc = st.ring[p];
+    const u32 t = A.g3.tile0[jb] + i / kTR;
+    W.ex = A.s3.excl[(u64)p * A.gt + t];
+    W.leo = A.cur.leo[p];
+    W.used = A.cur.used[p];
+    W.rdesc = st.ring[p];
     if (A.debug & 32u) {  // timing experiment: three of the seven state gathers left out
-      lead = 1u;
-      lm = (1u << st.RF) - 1u;
+      W.lead = 1u;
+      W.lm = (1u << st.RF) - 1u;
     } else {
-      lead = st.is_leader[p];
-      tot = A.s3.totals[p];
-      lm = st.local_mask[p];
+      W.lead = st.is_leader[p];
+      W.tot = A.s3.totals[p];
+      W.lm = st.local_mask[p];
     }
   }
+  return W;
+}
+
+// Offset and position of a candidate record, its leading dead pieces (0 = header, k = payload
+// piece k - 1 at pos + 16k: a piece whose ring slot a later piece of the same group overwrites,
+// pos + 16k + seg < group end, is not stored) and its mask word (local replicas | kLead | kNoSpace).
+__device__ __forceinline__ void rec_place(const RecWords& W, const TaskRec& R, u64& pos, u64& off, u32& dead,
+                                          u32& lmo, u32& rk, u32& rel16) {
+  rk = (u32)((W.ex >> 40) & kCnt23) + (R.cr.x & kRankMask);
+  rel16 = (u32)(W.ex & kLow40) + R.cr.y;
+  off = W.leo + rk;
+  pos = W.used + 16ull * rel16;
+  const u64 seg = 1ull << (W.rdesc & 63ull), gend = W.used + 16ull * (W.tot & kLow40);
+  dead = gend > pos + seg ? (u32)min((gend - seg - pos) >> 4, (u64)((R.L + 15u) >> 4) + 1ull) : 0u;
+  lmo = W.lm | (W.lead ? kLead : 0u) | ((W.ex & kExclNoSpace) ? kNoSpace : 0u);
+}
+
+__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos& T, const TaskRec& R, bool cand) {
+  TaskState S;
+  S.pos = S.off = 0ull;
+  S.lm = S.dead = S.rel16 = S.rk = 0u;
+  const RecWords W = rec_words(A, T.jb, task_rec(T), R.p, cand);
+  S.rdesc = W.rdesc;
   // first round of payload blocks, speculatively (leadership is checked before any store)
   round_blocks(A, R, 0u, cand, S.blk);
-  if (cand) {
-    S.rk = (u32)((ex >> 40) & kCnt23) + (R.cr.x & kRankMask);
-    S.rel16 = (u32)(ex & kLow40) + R.cr.y;
-    S.off = leo + S.rk;
-    S.pos = used + 16ull * S.rel16;
-    // pieces (0 = header, k = payload piece k - 1 at pos + 16k) whose ring slot a later piece of
-    // the same group overwrites (pos + 16k + seg < group end) are dead: not stored
-    const u64 seg = 1ull << (S.rdesc & 63ull), gend = used + 16ull * (tot & kLow40);
-    S.dead = gend > S.pos + seg ? (u32)min((gend - seg - S.pos) >> 4, (u64)((R.L + 15u) >> 4) + 1ull) : 0u;
-    S.lm = lm | (lead ? kLead : 0u) | ((ex & kExclNoSpace) ? kNoSpace : 0u);
-  }
+  if (cand) rec_place(W, R, S.pos, S.off, S.dead, S.lm, S.rk, S.rel16);
   return S;
 }
 
@@ -1017,7 +1037,7 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
 // l, l + 64, ... (kBU per lane in flight, the block after each from the neighbour lane), folds
 // them by Horner's rule with the 1 KB shift table, shifts its register past the pieces that follow
 // its last one and the wave XOR-reduces; lane 0 writes the header. xdst: the record's outbox copies.
-__device__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
+__device__ __forceinline__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
                            u64 off, u32 dead, uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx) {
   const u32 lane = threadIdx.x & 63, RF = A.st.RF;
   const u64 rstride = A.st.rstride;
@@ -1085,7 +1105,7 @@ __device__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*z
 // it with big_record. Their task waves leave these records to them (header and payload; the task
 // wave still writes the out offset, index entries, record-table slots and statistics).
 template <bool XR>
-__device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
+__device__ __forceinline__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
   const PipeGroup& G = A.g3;
   const PipeScratch& x = A.s3;
   const DevState& st = A.st;
@@ -1138,7 +1158,7 @@ __device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
 }
 
 template <bool XR>
-__device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
+__device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
                               const TaskState& Z, bool cand, uint4& stat_out) {
   const PipeBatch& b = A.g3.b[T.jb];
   const DevState& st = A.st;
@@ -1298,20 +1318,246 @@ __device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const Task
   }
 }
 
-// Thread per partition: stage 3's state advance and stage 4's retention. Everything either reads
-// is loaded first, in one round (speculatively: a partition this engine does not lead, or one
-// without records, discards it), so the chain is that round, the index entries retention needs,
-// and the stores.
+// ------------------------------------------------------------------------------------------
+// Stage 3, wide form (single-GPU kernel, PipeArgs::wide3): a wave applies two consecutive tasks
+// of one batch, a lane per record, so the loads of all 64 records are in flight together and a
+// four-batch group's tasks fit the resident wave slots in one generation (the lane-pair form
+// needs two: the second generation starts as the first retires). Only for records of at most
+// kWidePieces payload pieces; a wave that meets a longer candidate applies its two tasks with the
+// lane-pair code, one after the other.
+// ------------------------------------------------------------------------------------------
+constexpr u32 kWidePieces = 7;             // 112 payload bytes: header + pieces = one 128-byte image row
+constexpr u32 kWB = kWidePieces + 1u;      // aligned blocks covering 7 misaligned pieces
+
+struct WideState {
+  u64 pos, off, rdesc;
+  u32 lm, dead;
+  uint4 blk[kWB];
+};
+
+__device__ __forceinline__ WideState stage3_wide_r2(const PipeArgs& A, u32 jb, u32 i, const TaskRec& R, bool cand) {
+  WideState Z;
+  Z.pos = Z.off = 0ull;
+  Z.lm = Z.dead = 0u;
+  const RecWords W = rec_words(A, jb, i, R.p, cand);
+  Z.rdesc = W.rdesc;
+  // every block of the record, speculatively (leadership is checked before any store)
+  const u64 a0 = R.src & ~15ull, lim = R.src + R.L;
+#pragma unroll
+  for (u32 q = 0; q < kWB; ++q) {
+    const u64 ad = a0 + 16ull * q;
+    Z.blk[q] = make_uint4(0, 0, 0, 0);
+    if (cand && ad < lim && !(A.debug & 4u)) Z.blk[q] = *reinterpret_cast<const uint4*>(ad);
+  }
+  if (cand) {
+    u32 rk, rel16;
+    rec_place(W, R, Z.pos, Z.off, Z.dead, Z.lm, rk, rel16);
+  }
+  return Z;
+}
+
+// Records i0 .. i0 + 63 of batch jb (tasks tk, tk + 1 of the batch), lane l = record i0 + l: CRC by
+// Horner's rule over the record's pieces with the 16-byte zero-shift table, then the two halves of
+// the wave go through the wave's LDS log image one after the other (32 records of 128 bytes, 8
+// lanes per record per store), out offsets, sparse-index entries, the two tasks' statistics.
+__device__ __forceinline__ void stage3_wide_finish(const PipeArgs& A, Stage3Smem& S, u32 jb, u32 i0, u32 tk, const TaskRec& R,
+                                   const WideState& Z, bool cand) {
+  const PipeBatch& b = A.g3.b[jb];
+  const DevState& st = A.st;
+  const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6, RF = st.RF;
+  const u32 i = i0 + lane;
+  const bool in = i < b.n;
+  const u32 L = R.L, fl = R.cr.x >> kFlagShift, rej = batch_rej(A, jb);
+  const bool ns = (Z.lm & kNoSpace) != 0u, lead = (Z.lm & kLead) != 0u;
+  const u32 lm8 = Z.lm & 0xFFu;
+  const bool ok = cand && lead && !ns;
+  const u32 m = ok ? (L + 15u) >> 4 : 0u;  // <= kWidePieces (the caller checked)
+  const u32 sa = (u32)(R.src & 15u);
+  const u32 hl = lane >> 5, r32 = lane & 31u;
+  u32 acc = 0;
+#pragma unroll
+  for (u32 k = 0; k < kWidePieces; ++k) {
+    if (k < m) {
+      const u32 nb = L - 16u * k < 16u ? L - 16u * k : 16u;
+      const uint4 v = extract_piece(Z.blk[k], Z.blk[k + 1], sa, nb);
+      acc = crc_zshift(S.z[0], acc) ^ piece_crc(A, S, v, k);
+      if (hl == 0) S.img[w][r32][k + 1] = v;  // the first half's image rows now, the second's below
+    }
+  }
+  u32 crc = 0;
+  if (m) {  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad)); an empty record's is 0
+    const u32 pad = 16u * m - L;
+    crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
+  }
+  const uint4 h = make_uint4((u32)Z.off, (u32)(Z.off >> 32), L, crc);
+  const RingRef rg = ring_ref(Z.rdesc, st.interval_log2, st.icap_mul);
+  const u64 rstride = st.rstride;
+  const u32 lmw = (A.debug & 1u) ? 0u : 0xFFu;
+  for (u32 half = 0; half < 2; ++half) {
+    if (hl == half) {
+      if (half == 1) {
+#pragma unroll
+        for (u32 k = 0; k < kWidePieces; ++k)
+          if (k < m) {
+            const u32 nb = L - 16u * k < 16u ? L - 16u * k : 16u;
+            S.img[w][r32][k + 1] = extract_piece(Z.blk[k], Z.blk[k + 1], sa, nb);
+          }
+      }
+      S.img[w][r32][0] = h;
+      S.info[w][r32] = make_uint4((u32)Z.pos, (u32)(Z.pos >> 32), (u32)(rg.base >> 8),
+                                  ok ? lm8 | (m << 8) | (1u << 12) | (Z.dead << 13) | ((u32)(Z.rdesc & 63ull) << 24) : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (u32 s4 = 0; s4 < kTaskRecs * 8u / 64u; ++s4) {
+      const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
+      const uint4 inf = S.info[w][rr];
+      const u32 mr = (inf.w >> 8) & 0xFu;
+      if (((inf.w >> 12) & 1u) && k <= mr && k >= ((inf.w >> 13) & 0x1Fu)) {
+        const uint4 v = S.img[w][rr][k];
+        const u64 rpos = ((u64)inf.y << 32) | inf.x;
+        const u64 rmask = (1ull << (inf.w >> 24)) - 1ull;
+        uint8_t* dst = st.logs + ((u64)inf.z << 8) + ((rpos + 16ull * k) & rmask);
+        const u32 lmr = inf.w & lmw;
+        for (u32 r = 0; r < RF; ++r)
+          if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the image is rewritten by the second half / the next pair
+  }
+  if (in) b.out_offsets[i] = ok ? Z.off : ~0ull;
+  if (ok) {
+    const u32 ilog = st.interval_log2;
+    const u64 end = Z.pos + 16ull * (1ull + m);
+    for (u64 mm = (Z.pos >> ilog) + 1; (mm << ilog) <= end; ++mm) {
+      u64* e = st.index + (rg.ibase + mm % rg.icap) * 2;
+      e[0] = Z.off + 1;
+      e[1] = end;
+    }
+  }
+  const u64 b_in = __ballot(in), b_app = __ballot(ok), b_nl = __ballot(cand && !lead);
+  const u64 b_np = __ballot(in && fl == kFlNoPart), b_ns = __ballot(cand && lead && ns);
+  if (lane < 2) {
+    const u32 sh = 32u * lane;
+    const u32 n_in = (u32)__popcll((b_in >> sh) & 0xFFFFFFFFull);
+    const u32 n_app = (u32)__popcll((b_app >> sh) & 0xFFFFFFFFull);
+    const u32 n_nl = (u32)__popcll((b_nl >> sh) & 0xFFFFFFFFull);
+    const u32 n_np = rej ? 0u : (u32)__popcll((b_np >> sh) & 0xFFFFFFFFull);
+    const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
+    const u32 n_ns = (u32)__popcll((b_ns >> sh) & 0xFFFFFFFFull);
+    A.g3.stats[jb][tk + lane] = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
+  }
+}
+
+// The stage-3 workgroups of the wide form: wave v takes task pairs (2v, 2v + 1), then v + the
+// launch's stage-3 waves, ... (one pair per wave when the grid holds them all). A pair whose two
+// tasks lie in different batches, or that holds a candidate over kWidePieces pieces, is applied
+// by the lane-pair code, task by task.
+__device__ __forceinline__ void stage3_wide_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
+  const PipeGroup& G = A.g3;
+  const u32 tasks = G.task0[G.nb], pairs = (tasks + 1u) / 2u;
+  const u32 lane = threadIdx.x & 63;
+  u32 pr = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
+  PIPE_STAMP(0);
+  // the first pair's records are loaded while the CRC tables fill LDS
+  TaskPos T = task_pos(G, pr < pairs ? 2u * pr : 0u);
+  TaskRec R = stage3_r1_at(A, T.jb, T.i0 + lane);
+  if (!(A.debug & 8u)) {
+    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+    uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
+    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
+  }
+  __syncthreads();
+  PIPE_STAMP(1);
+  while (pr < pairs) {
+    PIPE_STAMP(2);
+    const u32 t0 = 2u * pr;
+    const bool same = t0 + 1u < tasks && batch_of_task(G, t0 + 1u) == T.jb;
+    const u32 i = T.i0 + lane;
+    const bool cand = same && stage3_cand_at(A, T.jb, i, R);
+    if (same && !__any(cand && R.L > 16u * kWidePieces)) {
+      const WideState Z = stage3_wide_r2(A, T.jb, i, R, cand);
+      stage3_wide_finish(A, S, T.jb, T.i0, t0 - G.task0[T.jb], R, Z, cand);
+    } else {
+      for (u32 t = t0; t < t0 + 2u && t < tasks; ++t) {
+        const TaskPos T1 = task_pos(G, t);
+        const TaskRec R1 = stage3_r1(A, T1);
+        const bool c1 = stage3_cand(A, T1, R1);
+        const TaskState Z1 = stage3_r2(A, T1, R1, c1);
+        uint4 so;
+        stage3_finish<false>(A, S, T1, R1, Z1, c1, so);
+        if (lane == 0) G.stats[T1.jb][t - G.task0[T1.jb]] = so;
+      }
+    }
+    PIPE_STAMP(3);
+    pr += A.wg3 * kPW;
+    if (pr < pairs) {
+      T = task_pos(G, 2u * pr);
+      R = stage3_r1_at(A, T.jb, T.i0 + lane);
+    }
+  }
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(6);
+}
+
+// Retention after each batch of a group (FORMAT.md §4), batch by batch: after batch j (log end
+// fin[j], 0 = the batch appended nothing of p) the start moves to index entry
+// ceil((fin_j - seg) / I) when fin_j - start > seg. The start only grows, so a batch with
+// fin_j - start0 <= seg never moves it: the entries of the others are loaded together, then the
+// batches are replayed in order in registers. An entry at or past position `lim` may be written by
+// the running launch: it is not read, the replay stops at its batch and the function returns
+// false (the next launch's stage 4 finishes the group; replaying applied batches moves nothing).
+__device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef& rg, const u64 (&fin)[kMaxGroup],
+                                               u64 lim, u64& soff, u64& spos) {
+  const u32 ilog = st.interval_log2;
+  u64 eo[kMaxGroup], ep[kMaxGroup];
+  bool late[kMaxGroup];
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j) {
+    eo[j] = ep[j] = 0ull;
+    late[j] = false;
+    if (fin[j] && fin[j] - spos > rg.seg) {
+      const u64 ms = (fin[j] - rg.seg + (1ull << ilog) - 1) >> ilog;
+      late[j] = (ms << ilog) > lim;
+      if (!late[j]) {
+        const u64* e = st.index + (rg.ibase + ms % rg.icap) * 2;
+        eo[j] = e[0];
+        ep[j] = e[1];
+      }
+    }
+  }
+  bool done = true;
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j)
+    if (done && fin[j] && fin[j] - spos > rg.seg) {
+      if (late[j]) {
+        done = false;
+      } else {
+        soff = eo[j];
+        spos = ep[j];
+      }
+    }
+  return done;
+}
+
+// Thread per partition: stage 3's state advance, retention of the group it applies, and stage 4.
+// Everything these read is loaded first, in one round (speculatively: a partition this engine
+// does not lead, or one without records, discards it), so the chain is that round, the index
+// entries retention needs, and the stores.
 //  * stage 3: the group's new log end, matchIndex, quorum commit and high watermark, into the next
 //    state set. The commit rule is monotone in the log end, so evaluating it once after the group
 //    equals evaluating it after each batch. A partition this engine does not lead keeps its state
 //    outside the pipeline (its records are counted by stages 1/2, ranks being per partition, but
 //    never applied; the host keeps both state sets equal for it); stage 2 leaves rejected
 //    (batch, partition) cells out of totals.
-//  * stage 4: retention after each batch of the group applied one launch earlier (FORMAT.md §4),
-//    batch by batch, from the index entries that launch wrote. The state set this launch reads
-//    (cur) holds that group's final log end.
-__device__ void partition_threads(const PipeArgs& A, u32 p) {
+//  * retention after each batch of the group applied by this launch, from index entries written
+//    before it (an entry this launch writes ends the replay: a group that adds more than a ring
+//    less one interval to the partition). Then a fetch ordered after the launch sees the log start
+//    of the records it sees, and a drain needs no stage-4 launch unless a partition stopped early
+//    (it writes the launch number into ret_late).
+//  * stage 4: retention after each batch of the group applied one launch earlier: the batches the
+//    launch before could not finish (the rest replay without moving the start).
+__device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
   const u32 RF = st.RF;
   const bool a3 = A.g3.nb != 0, a4 = A.g4.nb != 0;
@@ -1326,47 +1572,42 @@ __device__ void partition_threads(const PipeArgs& A, u32 p) {
   const u64 tot4 = a4 ? A.s4.totals[p] : 0ull;
   const u64 soff0 = st.start_off[p], spos0 = st.start_pos[p];
   const u64 desc = st.ring[p];
-  u64 bc[kMaxGroup];
+  u64 bc[kMaxGroup], bc3[kMaxGroup];
 #pragma unroll
-  for (u32 j = 0; j < kMaxGroup; ++j) bc[j] = a4 && j < A.g4.nb ? A.s4.bcum[(u64)j * st.P + p] : 0ull;
+  for (u32 j = 0; j < kMaxGroup; ++j) {
+    bc[j] = a4 && j < A.g4.nb ? A.s4.bcum[(u64)j * st.P + p] : 0ull;
+    bc3[j] = a3 && j < A.g3.nb ? A.s3.bcum[(u64)j * st.P + p] : 0ull;
+  }
   if (!lead) return;
+  const RingRef rg = ring_ref(desc, st.interval_log2, st.icap_mul);
+  u64 soff = soff0, spos = spos0;
 
-  // ---- stage 4: retention of the group applied one launch earlier (reads cur, before any store)
+  // ---- stage 4: retention of the group applied one launch earlier (cur: its final log end)
   if (tot4 >> 40) {
-    const u32 ilog = st.interval_log2;
-    const RingRef rg = ring_ref(desc, ilog, st.icap_mul);
-    // batch by batch: after batch j (log end fin_j) the start moves to index entry
-    // ceil((fin_j - seg) / I) when fin_j - start > seg. The start only grows, so a batch with
-    // fin_j - start0 <= seg never moves it: the entries of the others are loaded together, then
-    // the batches are replayed in order in registers.
-    u64 fin[kMaxGroup], eo[kMaxGroup], ep[kMaxGroup];
-    u64 prev = 0;
+    u64 fin[kMaxGroup], prev = 0;
 #pragma unroll
     for (u32 j = 0; j < kMaxGroup; ++j) {
       const bool app = j < A.g4.nb && (bc[j] >> 40) != (prev >> 40);  // batch j appended records of p
       fin[j] = app ? used0 - 16ull * ((tot4 - bc[j]) & kLow40) : 0ull;
-      eo[j] = ep[j] = 0ull;
-      if (app && fin[j] - spos0 > rg.seg) {
-        const u64 ms = (fin[j] - rg.seg + (1ull << ilog) - 1) >> ilog;
-        const u64* e = st.index + (rg.ibase + ms % rg.icap) * 2;
-        eo[j] = e[0];
-        ep[j] = e[1];
-      } else {
-        fin[j] = 0ull;  // cannot move the start
-      }
       prev = j < A.g4.nb ? bc[j] : prev;
     }
-    u64 soff = soff0, spos = spos0;
+    retain_batches(st, rg, fin, ~0ull, soff, spos);
+  }
+  // ---- retention of the group this launch applies (cur: the log end before it)
+  if (tot3 >> 40) {
+    u64 fin[kMaxGroup], prev = 0;
 #pragma unroll
-    for (u32 j = 0; j < kMaxGroup; ++j)
-      if (fin[j] && fin[j] - spos > rg.seg) {
-        soff = eo[j];
-        spos = ep[j];
-      }
-    if (soff != soff0 || spos != spos0) {
-      st.start_off[p] = soff;
-      st.start_pos[p] = spos;
+    for (u32 j = 0; j < kMaxGroup; ++j) {
+      const bool app = j < A.g3.nb && (bc3[j] >> 40) != (prev >> 40);
+      fin[j] = app ? used0 + 16ull * (bc3[j] & kLow40) : 0ull;
+      prev = j < A.g3.nb ? bc3[j] : prev;
     }
+    if (!retain_batches(st, rg, fin, used0, soff, spos) && A.ret_late)
+      __hip_atomic_store(A.ret_late, A.launch_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (soff != soff0 || spos != spos0) {
+    st.start_off[p] = soff;
+    st.start_pos[p] = spos;
   }
 
   // ---- stage 3: log end, matchIndex, commit
@@ -1404,7 +1645,7 @@ __device__ void partition_threads(const PipeArgs& A, u32 p) {
 // that start in it. Round h-1's records are complete (the previous launch) and round h's stores
 // into the ring land past the gap's end minus the ring size (the plan's condition), so nothing
 // this reads changes under it.
-__device__ void stage3_catchup(const PipeArgs& A, u32 wg) {
+__device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
   const u32 items = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n + 1));
   const u32 ncu = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n));
   if (!items) return;
@@ -1514,6 +1755,10 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   const PipeGroup& G = A.g3;
   const u32 tasks = G.task0[G.nb];
   const u32 lane = threadIdx.x & 63;
+  if (!XR && A.wide3) {
+    stage3_wide_waves(A, S, wg);
+    return;
+  }
   // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
   u32 task = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);

@@ -129,6 +129,40 @@ def test_fetch_during_pipelined_appends(oracle_mod):
         assert seen > 0, "no fetch saw committed records while appends were in flight"
 
 
+def test_fetch_sees_retention_of_applied_groups(oracle_mod):
+    """Hot partitions wrap their 64 KiB rings while batches are in flight: after every submission
+    the partition state (read without flushing) and a fetch from offset 0 must equal the oracle
+    after the batches applied so far, retention of the last applied group included (it runs in the
+    launch that applies the group, so no fetch reads ring bytes that group overwrote)."""
+    P = 16
+    cfg = EngineConfig(num_partitions=P, replication_factor=3, segment_bytes=1 << 16, index_interval=256,
+                       max_consumers=2, max_batch_records=4096, pipeline_depth=2)
+    spec = StreamSpec(P, 1500, "zipf", size=(1, 160), config_index=43)
+    batches = [make_batch(spec, b) for b in range(14)]
+    pp, cc = np.arange(P, dtype=np.uint32), np.zeros(P, np.uint32)
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        applied, checked, moved = 0, 0, 0
+        for b in batches:
+            dev.append_async(b.pidx, b.lens, b.payload)
+            st = [dev.state(p) for p in range(P)]
+            leo = [s["log_end_offset"] for s in st]
+            while [ora.state(p)["log_end_offset"] for p in range(P)] != leo:
+                assert applied < len(batches), "device state matches no prefix of the batches"
+                nb = batches[applied]
+                ora.append(nb.pidx, nb.lens, nb.payload)
+                applied += 1
+            assert st == [ora.state(p) for p in range(P)], f"state after {applied} applied batches"
+            _, res, buf, _ = dev.fetch(pp, cc, np.full(P, 1 << 20, np.uint32))
+            _, want, wbuf, _ = ora.fetch(pp, cc, np.full(P, 1 << 20, np.uint32))
+            for k in ("status", "start_offset", "count", "bytes"):
+                assert np.array_equal(res[k], want[k]), (k, applied)
+            assert np.array_equal(buf, wbuf)
+            checked += 1
+            moved += int(np.count_nonzero(res["start_offset"]))
+        assert checked == len(batches) and moved > 0, "scenario must fetch across retention"
+        dev.sync()
+
+
 def test_fetch_many_requests(oracle_mod):
     """One fetch call places 20k requests (several passes of the placement scan) with unknown
     partitions, bad consumers and zero-record slices mixed in, then the same requests into an
