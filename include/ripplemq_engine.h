@@ -181,7 +181,7 @@ typedef struct rmq_repl_stats {
                                   leader term, or the round missed (no region from the leader) */
   uint64_t bytes_ingested;
   uint64_t catchup_entries;    /* leader: entries that re-sent a follower's gap (FORMAT.md §9 catch-up) */
-  uint64_t detached_plans;     /* leader: entry plans whose follower lies beyond the ring (needs a re-sync) */
+  uint64_t detached_plans;     /* leader: entry plans whose follower lies beyond the ring and no rebase point was complete (FORMAT.md §9) */
 } rmq_repl_stats;
 
 typedef struct rmq_engine rmq_engine;

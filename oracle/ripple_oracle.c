@@ -116,6 +116,7 @@ typedef struct {
   uint64_t seg;            /* ring bytes of this partition (rmq_set_segments) */
   uint8_t* round;          /* records appended in the current replication round, log layout */
   uint64_t round_bytes, round_cap, round_count, round_first;
+  uint64_t prev_round_bytes; /* record bytes of the round before (C = B less them: FORMAT.md §9) */
   /* leader, per replica slot (FORMAT.md §9 catch-up): expected follower log end before the next
      round, pending catch-up request {offset, position, round + 1 (0: none)}, last catch-up round */
   uint64_t nx_off[RMQ_MAX_RF], nx_pos[RMQ_MAX_RF];
@@ -833,6 +834,7 @@ int ro_record_pos(ro_engine* e, uint32_t p, uint64_t offset, uint64_t* pos) {
 #define RO_DIR 32u
 #define RO_ACK_REFUSED (1ull << 62)
 #define RO_ACK_LEO_MASK ((1ull << 62) - 1ull)
+#define RO_REBASE (1ull << 63) /* directory term flag: the entry restarts the follower's log */
 
 typedef struct {
   uint64_t key;
@@ -888,6 +890,7 @@ typedef struct {
   uint64_t gap_count, gap_bytes; /* of which the catch-up part [first, B) read from the ring */
   uint64_t nx_off, nx_pos;    /* next after the round */
   int set_cu, row, detached, catchup;
+  int rebase;                 /* the catch-up part starts at the rebase point R, not at the follower */
 } ro_plan;
 
 /* Largest sparse-index entry E[m] (m I <= lim, E[m].pos <= lim, E[m].pos > pos0, m <= mmax):
@@ -918,6 +921,8 @@ static void plan_pair(const ro_engine* e, const ro_entry* v, uint32_t n, ro_plan
     ro_plan* x = &pl[k];
     memset(x, 0, sizeof *x);
     const uint64_t Boff = s->leo - s->round_count, Bpos = s->used - s->round_bytes;
+    /* index entries complete when the round is planned: up to C = B less the round before */
+    const uint64_t Cpos = Bpos - s->prev_round_bytes;
     uint64_t Foff = s->nx_off[sl], Fpos = s->nx_pos[sl];
     int req = 0;
     if (s->rq_r1[sl] && s->rq_r1[sl] - 1 >= s->cu[sl]) {
@@ -941,9 +946,20 @@ static void plan_pair(const ro_engine* e, const ro_entry* v, uint32_t n, ro_plan
       x->set_cu = req;
       continue;
     }
-    if (Fpos + s->seg < s->used) { /* the ring no longer holds [F, E) after the round */
-      x->detached = 1;
-      continue;
+    int rebase = 0;
+    if (Fpos + s->seg < s->used) {
+      /* the ring no longer holds [F, E) after the round: the follower's log restarts at the rebase
+         point R = E[m], m = ceil((E.pos - S) / I), the oldest index entry [R, E) fits the ring from
+         (Raft's InstallSnapshot, the leader's retained log as the snapshot); without a complete
+         E[m] (m I > C) the follower stays detached this round */
+      const uint64_t m = (s->used - s->seg + I - 1) / I;
+      if (m * I > Cpos) {
+        x->detached = 1;
+        continue;
+      }
+      Foff = s->idx_off.v[m];
+      Fpos = s->idx_pos.v[m];
+      rebase = 1;
     }
     const uint64_t g = Bpos - Fpos;
     if (!stop && g <= left) {
@@ -954,11 +970,12 @@ static void plan_pair(const ro_engine* e, const ro_entry* v, uint32_t n, ro_plan
       x->count += x->gap_count;
       x->bytes += g;
       x->set_cu = x->row = x->catchup = 1;
+      x->rebase = rebase;
       left -= g;
       continue;
     }
     uint64_t Xoff = 0, Xpos = 0;
-    if (!stop && partial_end(e, s, Fpos, Fpos + left, Bpos / I, &Xoff, &Xpos)) {
+    if (!stop && partial_end(e, s, Fpos, Fpos + left, Cpos / I, &Xoff, &Xpos)) {
       x->first = Foff;
       x->pos0 = Fpos;
       x->gap_count = x->count = Xoff - Foff;
@@ -966,6 +983,7 @@ static void plan_pair(const ro_engine* e, const ro_entry* v, uint32_t n, ro_plan
       x->nx_off = Xoff;
       x->nx_pos = Xpos;
       x->set_cu = x->row = x->catchup = 1;
+      x->rebase = rebase;
     }
     stop = 1;
     left = 0;
@@ -1026,7 +1044,8 @@ int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint
     memcpy(d + 8, &x->first, 8);
     memcpy(d + 16, &ts, 4);
     memcpy(d + 20, &ds, 4);
-    memcpy(d + 24, &s->term, 8);
+    const uint64_t tf = s->term | (x->rebase ? RO_REBASE : 0ull);
+    memcpy(d + 24, &tf, 8);
     uint8_t* dd = out + data + 16 * b16;
     /* the catch-up part from the leader's ring, then the round's records (if carried) */
     if (x->gap_bytes) ring_read(s->seg, ring_of(e, s->leader_slot, v[k].p), x->pos0, dd, x->gap_bytes);
@@ -1042,6 +1061,7 @@ int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint
     if (x->row) {
       uint8_t* rw = out + rows + rowb * mrow++;
       memcpy(rw, &k, 4);
+      if (x->rebase) memcpy(rw + 8, &x->pos0, 8); /* the rebase point's position */
       memcpy(rw + 16, s->cons, 8ull * C);
     }
     t += cnt;
@@ -1077,6 +1097,7 @@ void ro_end_round(ro_engine* e) {
     free(v);
   }
   for (uint32_t p = 0; p < e->cfg.num_partitions; ++p) {
+    e->parts[p].prev_round_bytes = e->parts[p].round_bytes;
     e->parts[p].round_bytes = e->parts[p].round_count = 0;
     e->parts[p].dirty = 0;
   }
@@ -1091,6 +1112,40 @@ static void truncate_log(ro_engine* e, ro_part* s, uint64_t t) {
   s->leo = t;
   s->rec_pos.n = t;
   s->idx_off.n = s->idx_pos.n = s->used / I + 1;
+}
+
+/* Follower: partition p's log restarts at offset t, position pos (a rebase entry, FORMAT.md §9):
+   the old records leave the log (their ring bytes and index slots stay, outside it); the dense
+   lookups get placeholders below the new start, which no lookup reads. */
+static int rebase_log(ro_engine* e, ro_part* s, uint64_t t, uint64_t pos) {
+  const uint64_t I = e->cfg.index_interval;
+  s->rec_pos.n = t < s->rec_pos.n ? t : s->rec_pos.n;
+  while (s->rec_pos.n < t)
+    if (vec_push(&s->rec_pos, 0)) return RMQ_ENOMEM;
+  const uint64_t ni = pos / I + 1;
+  s->idx_off.n = ni < s->idx_off.n ? ni : s->idx_off.n;
+  s->idx_pos.n = s->idx_off.n;
+  while (s->idx_off.n < ni)
+    if (vec_push(&s->idx_off, 0) || vec_push(&s->idx_pos, 0)) return RMQ_ENOMEM;
+  if (pos % I == 0) { /* E[m] of a start on an interval multiple is its first record (as the leader's) */
+    s->idx_off.v[ni - 1] = t;
+    s->idx_pos.v[ni - 1] = pos;
+  }
+  s->leo = s->start_off = t;
+  s->used = s->start_pos = pos;
+  return RMQ_OK;
+}
+
+/* The consumer-offset row of entry k in a region (rows ascend by entry), or NULL. */
+static const uint8_t* row_of(const uint8_t* region, uint64_t rows, uint32_t M, uint32_t C, uint32_t k) {
+  const uint64_t rowb = 16 + 8ull * C;
+  for (uint32_t r = 0; r < M; ++r) {
+    uint32_t rk;
+    memcpy(&rk, region + rows + rowb * r, 4);
+    if (rk == k) return region + rows + rowb * r;
+    if (rk > k) break;
+  }
+  return NULL;
 }
 
 static void ack_of(const ro_part* s, int refused, uint64_t* ack) {
@@ -1152,11 +1207,19 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     memcpy(&ts, d + 16, 4);
     memcpy(&ds, d + 20, 4);
     memcpy(&term, d + 24, 8);
+    const int rebase = (term & RO_REBASE) != 0;
+    term &= ~RO_REBASE;
     if (owner) {
       stale = term < s->term; /* a leader of an older term */
       leo = s->leo;
       used = s->used;
-      if (!stale && first < leo && first >= s->start_off) { /* the leader's log wins: truncate */
+      if (!stale && rebase) { /* the log restarts at the entry's first record (its row holds the position) */
+        const uint8_t* row = row_of(region, rows, mc[0], C, k);
+        leo = first;
+        used = 0;
+        if (row) memcpy(&used, row + 8, 8);
+        else stale = 1; /* malformed: a rebase entry always carries its row */
+      } else if (!stale && first < leo && first >= s->start_off) { /* the leader's log wins: truncate */
         used = s->rec_pos.v[first];
         leo = first;
       }
@@ -1200,6 +1263,8 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     memcpy(&term, d + 24, 8);
     leo = base[2 * k];
     used = base[2 * k + 1];
+    const int rebase = (term & RO_REBASE) != 0;
+    term &= ~RO_REBASE;
     /* this entry's consumer-offset row, if any (rows ascend by entry) */
     const uint8_t* row = NULL;
     while (mrow < mc[0]) {
@@ -1215,7 +1280,16 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     }
     if (owner) {
       if (term > s->term) s->term = term;
-      if (leo < s->leo) truncate_log(e, s, leo);
+      if (rebase) {
+        if (rebase_log(e, s, leo, used)) {
+          free(okv);
+          free(base);
+          free(v);
+          return RMQ_ENOMEM;
+        }
+      } else if (leo < s->leo) {
+        truncate_log(e, s, leo);
+      }
       if (row) memcpy(s->cons, row, 8ull * C);
     }
     if (cnt) {

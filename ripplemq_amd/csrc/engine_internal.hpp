@@ -179,6 +179,7 @@ struct Replication {
   uint32_t* d_items = nullptr;   // [items_cap][2] follower copy work items
   uint32_t* d_nitems = nullptr;  // [1]
   uint64_t* d_counters = nullptr;  // [6]: follower [0..4) (IngestArgs), leader [4..6) (XPlanArgs)
+  uint64_t* d_lastg = nullptr;     // [P] record bytes / 16 of the last group applied (PipeArgs::lastg)
   // leader catch-up state per out entry (FORMAT.md §9 v3)
   uint64_t* d_xnext = nullptr;   // [n_out][2]
   uint64_t* d_xreq = nullptr;    // [n_out][4]

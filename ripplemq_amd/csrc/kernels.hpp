@@ -37,6 +37,8 @@ constexpr uint32_t kDirEntry = 32;       // directory entry bytes
 constexpr uint64_t kAckRefused = 1ull << 62;  // ack status bit (FORMAT.md §9 acks)
 constexpr uint64_t kAckLeoMask = kAckRefused - 1ull;
 constexpr uint64_t kNoRound = ~0ull;     // XEntry::data_abs: the entry carries no round records
+constexpr uint64_t kTermRebase = 1ull << 63;  // directory term flag: the entry restarts the follower's log
+                                              // at its first record (position in the entry's row)
 
 struct CrcConsts;
 
@@ -77,6 +79,8 @@ struct XDecision {
   uint32_t pad;
 };
 constexpr uint32_t kDecReq = 1u, kDecRow = 2u, kDecDetached = 4u, kDecGapped = 8u, kDecNewReq = 16u;
+constexpr uint32_t kDecRebase = 32u;     // the gap starts at the leader's rebase point, not at the follower
+constexpr uint32_t kRowRebase = 1u << 31;  // XDecision::pad: the planned entry is a granted rebase
 
 // Leader side of a replication round: the layout plan of one group's outbox (stage 2 of the group,
 // computed by the last stage-2 workgroup of the launch) and the catch-up state it advances.
@@ -236,6 +240,7 @@ struct PipeArgs {
   uint32_t wgc;            // catch-up workgroups (last along blockIdx.x)
   const CrcConsts* crc;
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
+  uint64_t* lastg;         // replication: [P] record bytes / 16 of the last group applied (a plan's C)
   uint64_t* ret_late;      // host-visible: written with launch_seq when a partition's retention of
                            // the group applied stops early (its stage 4 in the next launch finishes it)
   uint64_t launch_seq;

@@ -407,6 +407,9 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
   const u64 Boff = A.cur.leo[p] + (t3 >> 40), Bpos = A.cur.used[p] + 16ull * (t3 & kLow40);
   const u64 Epos = Bpos + 16ull * (tot & kLow40);
   const u64 S = 1ull << (st.ring[p] & 63ull);
+  // index entries complete when the round is planned: up to C = B less the group before (whether
+  // that group is applied by this launch or was by an earlier one: FORMAT.md §9)
+  const u64 Cpos = A.g3.nb ? A.cur.used[p] : Bpos - 16ull * A.lastg[p];
   XDecision d;
   d.f_off = X.xnext[2 * e];
   d.f_pos = X.xnext[2 * e + 1];
@@ -436,7 +439,20 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
     d.f_off = Boff;
     d.f_pos = Bpos;
   } else if (d.f_pos + S < Epos) {
-    d.flags |= kDecDetached;  // the ring no longer holds [F, E) after the round
+    // the ring no longer holds [F, E) after the round: the follower's log restarts at the rebase
+    // point R = E[m], m = ceil((E.pos - S) / I), when that entry is complete (else detached)
+    const u32 ilog = st.interval_log2;
+    const u64 m = (Epos - S + (1ull << ilog) - 1ull) >> ilog;
+    if ((m << ilog) > Cpos) {
+      d.flags |= kDecDetached;
+    } else {
+      const RingRef rg = ring_ref(st, p);
+      const u64* ie = st.index + (rg.ibase + m % rg.icap) * 2;
+      d.f_off = ie[0];
+      d.f_pos = ie[1];
+      d.flags |= kDecGapped | kDecRebase;
+      d.gap = Bpos - d.f_pos;
+    }
   } else {
     d.flags |= kDecGapped;
     d.gap = Bpos - d.f_pos;
@@ -537,6 +553,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
       const u64 t3 = (in && A.g3.nb) ? A.s3.totals[p] : 0ull;
       const u64 Boff = in ? A.cur.leo[p] + (t3 >> 40) : 0ull;
       const u64 Bpos = in ? A.cur.used[p] + 16ull * (t3 & kLow40) : 0ull;
+      const u64 Cpos = !in ? 0ull : A.g3.nb ? A.cur.used[p] : Bpos - 16ull * A.lastg[p];  // as plan_decide
       if (in) {
         nx_off = Boff + rcnt;
         nx_pos = Bpos + 16ull * rb16;
@@ -550,7 +567,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
             set_cu = cu_entry = true;
           } else if (gex <= X.reserve) {  // the first entry past the reserve: a prefix of its gap
             u64 xo = 0, xp = 0;
-            if (partial_end(st, p, f_pos, f_pos + (X.reserve - gex), A.cur.used[p], &xo, &xp)) {
+            if (partial_end(st, p, f_pos, f_pos + (X.reserve - gex), Cpos, &xo, &xp)) {
               gcnt = cnt = xo - f_off;
               gb16 = b16 = (xp - f_pos) >> 4;
               with_round = false;
@@ -563,6 +580,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
         if (!cu_entry) first = Boff;  // the round's records from B (refused by a follower behind B)
       }
       const bool row = in && (((fl & kDecRow) != 0u) || cu_entry);
+      const bool rebase = cu_entry && (fl & kDecRebase);  // granted: the follower's log restarts at F
       // scan A: table slots and data pieces before the entry
       const u64 va = in ? (cnt << 40) | b16 : 0ull;
       u64 ta;
@@ -587,7 +605,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
         const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
         uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
         de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
-        const u64 term = st.term[p];
+        const u64 term = st.term[p] | (rebase ? kTermRebase : 0ull);
         de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
         XEntry xe;
         xe.data_abs = kNoRound;
@@ -629,7 +647,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
         }
       }
       // (row entries and the data section offset need the region totals: pass 2)
-      if (in) X.xdec[e].pad = row ? 1u + (u32)(exb & 0xFFFFFull) : 0u;  // row index + 1
+      if (in) X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
       __syncthreads();
     }
     const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
@@ -639,11 +657,13 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
     for (u32 e = e0 + tid; e < e1; e += kPT) {
       XEntry& xe = X.xe[e];
       if (xe.data_abs != kNoRound) xe.data_abs = data + 16ull * xe.data_start16;
-      const u32 ri = X.xdec[e].pad;
+      const u32 ri = X.xdec[e].pad & ~kRowRebase;
       if (ri) {
         const u32 p = X.xo_p[e];
         uint8_t* rw = X.outbox + rows + rowb * (ri - 1u);
-        *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, 0u, 0u);
+        // a rebase entry's row carries the rebase point's position (FORMAT.md §9)
+        const u64 rp = (X.xdec[e].pad & kRowRebase) ? load_sc1(&X.xdec[e].f_pos) : 0ull;
+        *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, (u32)rp, (u32)(rp >> 32));
         for (u32 c = 0; c < C; ++c) reinterpret_cast<u64*>(rw + 16)[c] = st.cons[(u64)p * C + c];
       }
     }
@@ -1578,6 +1598,7 @@ __device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
     bc[j] = a4 && j < A.g4.nb ? A.s4.bcum[(u64)j * st.P + p] : 0ull;
     bc3[j] = a3 && j < A.g3.nb ? A.s3.bcum[(u64)j * st.P + p] : 0ull;
   }
+  if (A.lastg && a3) A.lastg[p] = lead ? (tot3 & kLow40) : 0ull;  // the next plans' C (FORMAT.md §9)
   if (!lead) return;
   const RingRef rg = ring_ref(desc, st.interval_log2, st.icap_mul);
   u64 soff = soff0, spos = spos0;

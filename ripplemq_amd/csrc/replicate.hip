@@ -69,10 +69,12 @@ __device__ __forceinline__ u32 source_of_task(const IngestArgs& A, u32 task) {
   return q;
 }
 
-// Directory entry k of a region: {count, bytes / 16, first offset} and the leader's term.
+// Directory entry k of a region: {count, bytes / 16, first offset}, the leader's term and whether
+// the entry restarts the follower's log (a rebase, FORMAT.md §9: flag in the term's top bit).
 struct DirView {
   u32 count, bytes16, tstart, dstart16;
   u64 first, term;
+  bool rebase;
 };
 __device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
   const uint4* de = reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
@@ -84,7 +86,23 @@ __device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
   d.tstart = d1.x;
   d.dstart16 = d1.y;
   d.term = ((u64)d1.w << 32) | d1.z;
+  d.rebase = (d.term & kTermRebase) != 0ull;
+  d.term &= ~kTermRebase;
   return d;
+}
+
+// The consumer-offset row of entry k (rows ascend by entry), or null.
+__device__ __forceinline__ const uint8_t* row_of(const RegionView& R, u32 C, u32 k) {
+  const u64 rowb = 16ull + 8ull * C;
+  u32 lo = 0, hi = R.M;
+  while (lo < hi) {
+    const u32 mid = (lo + hi) / 2;
+    const u32 rk = *reinterpret_cast<const u32*>(R.base + R.rows_off + rowb * mid);
+    if (rk < k) lo = mid + 1; else hi = mid;
+  }
+  if (lo < R.M && *reinterpret_cast<const u32*>(R.base + R.rows_off + rowb * lo) == k)
+    return R.base + R.rows_off + rowb * lo;
+  return nullptr;
 }
 
 __device__ __forceinline__ u32 source_of_entry(const IngestArgs& A, u32 e) {
@@ -144,6 +162,14 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
         const DirView d = dir_of(R, k);
         if (d.term < st.term[p]) {
           bad = kBadStale;  // a stale leader
+        } else if (d.rebase) {  // the log restarts at the entry's first record (its row: the position)
+          const uint8_t* row = row_of(R, A.C, k);
+          if (row) {
+            leo = d.first;
+            used = *reinterpret_cast<const u64*>(row + 8);
+          } else {
+            bad = kBadLog;  // malformed: a rebase entry always carries its row
+          }
         } else if (d.first < leo && d.first >= st.start_off[p]) {
           used = follower_pos(st, p, A.xi_slot[e], d.first);  // the leader's log wins: truncate
           leo = d.first;
@@ -180,7 +206,7 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   const DevState& st = A.st;
   u32 p = 0, L = 0, m = 0, e = 0;
   u64 pos = 0, off = 0;
-  bool ok = false, owner = false;
+  bool ok = false, owner = false, reb = false;
   const uint8_t* rec = R.base;
   uint4 hdr = make_uint4(0, 0, 0, 0);
   if (in) {
@@ -190,6 +216,7 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
     e = A.xi_start[src] + k;
     p = A.xi_p[e];
     owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
+    reb = d.rebase;
     const u64 used = A.base[2 * e + 1];   // after a truncation: at the leader's first offset
     rec = R.base + R.data_off + 16ull * d16;
     const u64 rel = 16ull * (u64)(d16 - d.dstart16);
@@ -280,7 +307,10 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
         if ((w4[b >> 2] >> (8u * (b & 3u))) & 0xFFu) crc = ~hdr.w;
     }
     if (crc == hdr.w) {
-      if (owner) {  // sparse index past the follower's live log: every interval multiple the record crosses
+      // (a rebase entry's index entries are written by finish, once the entry is accepted: its
+      // positions lie past the live log but may share index slots with it)
+      if (owner && !reb) {
+        // sparse index past the follower's live log: every interval multiple the record crosses
         const u32 ilog = st.interval_log2;
         const RingRef rg = ring_ref(st, p);
         const u64 end = pos + 16ull * (1ull + m), live = st.used[p] >> ilog;
@@ -346,7 +376,31 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
     const u32 ilog = st.interval_log2;
     const u64 old_used = st.used[p];
     if (d.term > st.term[p]) st.term[p] = d.term;
-    if (bused < old_used && d.count) {
+    u64 spos = st.start_pos[p];
+    if (d.rebase) {
+      // the log restarts at the entry's first record: its start, and every index entry of the
+      // records (E[m] of a start on an interval multiple is that record, as in the leader's index)
+      const RingRef rg = ring_ref(st, p);
+      const uint8_t* data = R.base + R.data_off + 16ull * d.dstart16;
+      st.start_off[p] = d.first;
+      st.start_pos[p] = spos = bused;
+      if (!(bused & ((1ull << ilog) - 1ull))) {
+        u64* ie = st.index + (rg.ibase + (bused >> ilog) % rg.icap) * 2;
+        ie[0] = d.first;
+        ie[1] = bused;
+      }
+      u64 pos = bused;
+      for (u32 r = 0; r < d.count; ++r) {
+        const u32 L = *reinterpret_cast<const u32*>(data + (pos - bused) + 8);
+        const u64 end = pos + 16ull + ((L + 15ull) & ~15ull);
+        for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end; ++q) {
+          u64* ie = st.index + (rg.ibase + q % rg.icap) * 2;
+          ie[0] = d.first + r + 1;
+          ie[1] = end;
+        }
+        pos = end;
+      }
+    } else if (bused < old_used && d.count) {
       // a truncation: the index slots inside the old live log name the new log's records
       const RingRef rg = ring_ref(st, p);
       const uint8_t* data = R.base + R.data_off + 16ull * d.dstart16;
@@ -370,7 +424,7 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
     if (d.count) {
       // retention once per round (FORMAT.md §4 rule on the follower's log)
       const RingRef rg = ring_ref(st, p);
-      if (nused - st.start_pos[p] > rg.seg) {
+      if (nused - spos > rg.seg) {
         const u64 ms = (nused - rg.seg + (1ull << ilog) - 1) >> ilog;
         const u64* ie = st.index + (rg.ibase + ms % rg.icap) * 2;
         st.start_off[p] = ie[0];

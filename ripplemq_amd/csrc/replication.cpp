@@ -215,6 +215,7 @@ int repl_attach(rmq_engine* e, Transport* t) {
     HIP_TRY(hipHostMalloc((void**)&x.h_sizes, 4ull * kMaxWorld * 8, 0));
   }
   int rc = dalloc(&r->d_counters, 6);
+  if (!rc) rc = dalloc(&r->d_lastg, e->cfg.num_partitions);
   if (rc) return rc;
   return repl_set_lists(e);
 }
@@ -233,7 +234,7 @@ void repl_free(rmq_engine* e) {
   }
   void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot,
                   r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
-                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_dflag};
+                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_dflag, r->d_lastg};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (r->xchg_s) hipStreamDestroy(r->xchg_s);
@@ -399,7 +400,9 @@ int repl_set_lists(rmq_engine* e) {
 
 void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const GroupFlight* s3) {
   Replication* r = e->repl;
-  if (!r || r->xo_p.empty()) return;  // nothing led here has a remote replica
+  if (!r) return;
+  a.lastg = r->d_lastg;               // kept by every launch that applies a group
+  if (r->xo_p.empty()) return;        // nothing led here has a remote replica
   a.outidx = r->d_outidx;
   if (s2) {
     XchgSet& x = r->sets[s2->set];

@@ -306,6 +306,27 @@ def test_partial_catch_up_gpu(oracle_mod):
         _close(res)
 
 
+def test_follower_beyond_the_ring_rebases_gpu(oracle_mod):
+    # rank 0's regions are lost for 9 rounds: its followers' log ends fall more than the 8 KB ring
+    # behind, so the next plan restarts their logs at the leader's rebase point (FORMAT.md §9,
+    # Raft's InstallSnapshot with the retained log as the snapshot) instead of detaching them;
+    # regions, rings, index and state bit-exact with the oracle, and the quorum back to full
+    spec = StreamSpec(1, 10, "uniform", size=(100, 100), config_index=58)  # 1.3 KB per round
+    res = synced_rounds(oracle_mod, world=3, rf=3, ppr=1, group=1, rounds=12, spec=spec, seg=1 << 13,
+                        faults={k: {"drop": (0,)} for k in range(9)})
+    try:
+        stats = res[3]
+        assert stats[0]["detached_plans"] == 0 and stats[0]["catchup_entries"] >= 2, stats[0]
+        assert stats[1]["refused_log"] > 0 and stats[2]["refused_log"] > 0
+        lead = res[2][0].state(0)
+        assert lead["log_start_offset"] > 0 and min(lead["match"]) == lead["log_end_offset"]
+        starts = [res[2][r].state(p)["log_start_offset"] for r in (1, 2)
+                  for p in range(res[0][r].led, res[2][r].cfg.num_partitions)]
+        assert min(starts) > 0, "the followers' logs restarted past their old ends"
+    finally:
+        _close(res)
+
+
 def test_consumer_offsets_replicate_and_survive_leader_change_gpu(oracle_mod):
     # ConsumerOffsetUpdateRequestProcessor.java:59-60: an offset commit is replicated; after the
     # leadership moves, the new leader serves the same offsets (fetch starts there)

@@ -272,13 +272,25 @@ def test_partial_catch_up_within_the_reserve(oracle_mod):
             o.close()
 
 
-def test_gap_beyond_the_ring_detaches(oracle_mod):
-    # a follower whose log end the leader's ring no longer holds cannot be caught up from the ring
+def _logical(o, slot, p, a, b):
+    """Bytes [a, b) of partition p's log as stored in replica slot `slot` of engine o."""
+    ring = o.read_segment(slot, p)
+    S = ring.size
+    return np.array([ring[x % S] for x in range(a, b)], np.uint8)
+
+
+def test_gap_beyond_the_ring_rebases(oracle_mod):
+    # a follower whose log end the leader's ring no longer holds restarts its log at the rebase
+    # point (FORMAT.md §9: Raft's InstallSnapshot with the leader's retained log as the snapshot)
+    # and is caught up from there; its retained records equal the leader's
     world, ppr = 3, 1
     base = EngineConfig(num_partitions=1, replication_factor=3, segment_bytes=1 << 13, index_interval=256)
     views, oras = build(oracle_mod, world, ppr, base=base)
     spec = StreamSpec(ppr, 10, "uniform", size=(100, 100), config_index=58)  # 1.3 KB per round
     try:
+        gp = int(views[0].gp[0])
+        (r1, p1, s1), (r2, p2, s2) = _follower_views(views, oras, 0, gp)
+        far_rank, far_p, far_slot = (r1, p1, s1) if r1 == 1 else (r2, p2, s2)
         for k in range(12):
             for r in range(world):
                 b = rank_batches(spec, r, 12, 1)[k]
@@ -286,14 +298,18 @@ def test_gap_beyond_the_ring_detaches(oracle_mod):
             # round 0 is missed by both followers; rank 1 loses rounds 1..8 as well (no region, no
             # ack): by then its log end lies more than the 8 KB ring behind
             exchange_round(oras, drop=(0,) if k == 0 else (), skip=(0, 1) if 1 <= k <= 8 else None)
-        assert oras[0].counters()[5] > 0  # the plan toward rank 1 found its gap beyond the ring
-        gp = int(views[0].gp[0])
-        (r1, p1, _), (r2, p2, _) = _follower_views(views, oras, 0, gp)
+            if k == 8:
+                before = oras[far_rank].state(far_p)
+        assert oras[0].counters()[5] == 0  # every plan toward rank 1 found its rebase point
         lead = oras[0].state(0)
-        # the other follower caught up and keeps the quorum; the detached one stays behind
+        far = oras[far_rank].state(far_p)
+        assert before["log_end_offset"] < far["log_start_offset"], "the follower's log restarted"
+        assert far["log_end_offset"] == lead["log_end_offset"] and far["log_end_pos"] == lead["log_end_pos"]
         assert lead["commit"] == lead["log_end_offset"]
-        far = oras[1].state(p1) if r1 == 1 else oras[1].state(p2)
-        assert far["log_end_offset"] < lead["log_end_offset"]
+        a, b = far["log_start_pos"], far["log_end_pos"]
+        assert b > a
+        assert np.array_equal(_logical(oras[far_rank], far_slot, far_p, a, b),
+                              _logical(oras[0], lead["leader_slot"], 0, a, b))
     finally:
         for o in oras:
             o.close()
