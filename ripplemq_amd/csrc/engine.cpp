@@ -173,6 +173,11 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   if (s1) {
     a.g1 = make_group(e, *s1);
     a.s1 = e->scratch[s1->set];
+    if (e->set_reset & (1u << s1->set)) {  // a drain skipped the stage 4 that resets the set's list and sums
+      HIP_TRY(hipMemsetAsync(a.s1.bacc, 0, kMaxGroup * 2 * sizeof(uint64_t), e->main_s));
+      HIP_TRY(hipMemsetAsync(a.s1.nbig, 0, sizeof(uint32_t), e->main_s));
+      e->set_reset &= ~(1u << s1->set);
+    }
     a.wg1 = e->s1_wgs ? std::min<uint32_t>(s1->tiles, e->s1_wgs) : s1->tiles;
   }
   if (s2) {
@@ -308,6 +313,8 @@ int drain(rmq_engine* e) {
       if (e->profile && e->prof_ended) HIP_TRY(hipEventRecord(e->prof_t1, e->main_s));
       rc = stream_wait(e->main_s);
       if (rc) return rc;
+    } else {
+      e->set_reset |= 1u << e->g3.set;  // its stage 4 would reset the set's list and sums
     }
     e->has3 = false;
   }

@@ -267,7 +267,8 @@ struct rmq_engine {
   // and applied (need stage 4)
   GroupFlight forming, g1, g2, g3;
   bool has1 = false, has2 = false, has3 = false;
-  uint64_t g3_seq = 0;  // the launch that applied g3 (its retention is late if done_host[1] >= it)
+  uint64_t g3_seq = 0;
+  uint32_t set_reset = 0;  // scratch sets whose large-record list and batch sums the next stage 1 zeroes  // the launch that applied g3 (its retention is late if done_host[1] >= it)
   uint32_t group_max = 2;       // batches per group (cfg.pipeline_depth)
   uint32_t max_group_tiles = 0;
   uint64_t groups = 0;          // groups formed

@@ -1394,6 +1394,21 @@ __device__ __forceinline__ void stage3_wide_finish(const PipeArgs& A, Stage3Smem
   const u32 m = ok ? (L + 15u) >> 4 : 0u;  // <= kWidePieces (the caller checked)
   const u32 sa = (u32)(R.src & 15u);
   const u32 hl = lane >> 5, r32 = lane & 31u;
+  // the two tasks' statistics, from ballots taken here with the whole wave active (wave-uniform)
+  uint4 st2[2];
+  {
+    const u64 b_in = __ballot(in), b_app = __ballot(ok), b_nl = __ballot(cand && !lead);
+    const u64 b_np = __ballot(in && fl == kFlNoPart), b_ns = __ballot(cand && lead && ns);
+#pragma unroll
+    for (u32 h = 0; h < 2; ++h) {
+      const u32 sh = 32u * h;
+      const u32 n_in = (u32)__popcll((b_in >> sh) & 0xFFFFFFFFull);
+      const u32 n_np = rej ? 0u : (u32)__popcll((b_np >> sh) & 0xFFFFFFFFull);
+      const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
+      st2[h] = make_uint4((u32)__popcll((b_app >> sh) & 0xFFFFFFFFull), (u32)__popcll((b_nl >> sh) & 0xFFFFFFFFull), n_np,
+                          (u32)__popcll((b_ns >> sh) & 0xFFFFFFFFull) | (n_inv << 16));
+    }
+  }
   u32 acc = 0;
 #pragma unroll
   for (u32 k = 0; k < kWidePieces; ++k) {
@@ -1455,17 +1470,9 @@ __device__ __forceinline__ void stage3_wide_finish(const PipeArgs& A, Stage3Smem
       e[1] = end;
     }
   }
-  const u64 b_in = __ballot(in), b_app = __ballot(ok), b_nl = __ballot(cand && !lead);
-  const u64 b_np = __ballot(in && fl == kFlNoPart), b_ns = __ballot(cand && lead && ns);
-  if (lane < 2) {
-    const u32 sh = 32u * lane;
-    const u32 n_in = (u32)__popcll((b_in >> sh) & 0xFFFFFFFFull);
-    const u32 n_app = (u32)__popcll((b_app >> sh) & 0xFFFFFFFFull);
-    const u32 n_nl = (u32)__popcll((b_nl >> sh) & 0xFFFFFFFFull);
-    const u32 n_np = rej ? 0u : (u32)__popcll((b_np >> sh) & 0xFFFFFFFFull);
-    const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
-    const u32 n_ns = (u32)__popcll((b_ns >> sh) & 0xFFFFFFFFull);
-    A.g3.stats[jb][tk + lane] = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
+  if (lane == 0) {
+    A.g3.stats[jb][tk] = st2[0];
+    A.g3.stats[jb][tk + 1] = st2[1];
   }
 }
 
