@@ -169,6 +169,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
   a.ret_late = e->done_dev + 1;
+  a.rlate = e->d_rlate;
   a.debug = e->debug;
   if (s1) {
     a.g1 = make_group(e, *s1);
@@ -205,14 +206,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.g3 = make_group(e, *s3);
     a.s3 = e->scratch[s3->set];
     const uint32_t wpb = PT / 64;
-    // wide form (a wave per task pair) when every batch of the group averages at most 112 payload
-    // bytes per record: a wave meeting a longer record falls back to lane pairs, task by task
-    bool wide = e->wide && !a.outidx;
-    for (uint32_t j = 0; j < s3->nb && wide; ++j)
-      wide = s3->b[j].b.payload_bytes <= 112ull * s3->b[j].b.n;
-    a.wide3 = wide ? 1u : 0u;
-    const uint32_t units = wide ? (s3->tasks + 1) / 2 : s3->tasks;
-    const uint32_t want = std::max<uint32_t>(1u, (units + wpb - 1) / wpb);
+    const uint32_t want = std::max<uint32_t>(1u, (s3->tasks + wpb - 1) / wpb);
     // default: one wave per task (the workgroups past the resident slots start as stage-1/2
     // workgroups retire); RMQ_WG3_ALL=0 fills only the slots next to the other roles (resident
     // workgroups per CU from the kernel's launch bounds) and the task waves loop over the rest
@@ -453,7 +447,7 @@ void free_engine(rmq_engine* e) {
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, e->d_crc,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_csum, e->d_fetch_out,
-                             e->d_ctl32, e->d_ctl64, e->d_stamps};
+                             e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
     bufs.push_back(z.used);
@@ -598,7 +592,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S2_WGS")) e->s2_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("RMQ_WIDE")) e->wide = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
@@ -668,6 +661,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&s.cdirty, P));
+  CREATE_TRY(dalloc(&e->d_rlate, P));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
   CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));

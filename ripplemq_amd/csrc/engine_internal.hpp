@@ -253,6 +253,7 @@ struct rmq_engine {
   StateSet sets[2]{};
   uint64_t applied = 0;     // stage-3 launches issued
   CrcConsts* d_crc = nullptr;
+  uint32_t* d_rlate = nullptr;  // [P] partitions whose retention of the applied group stopped early
   uint4* d_stats = nullptr;  // [kStatsRing][max tasks]
   rmq::SegPool pool;         // ring space of each replica region
   std::vector<uint64_t> ring;  // [P] host copy of DevState::ring
@@ -339,7 +340,6 @@ struct rmq_engine {
   uint32_t s1_wgs = 0;    // RMQ_S1_WGS: stage-1 workgroups per launch (0: one per tile; fewer loop over tiles)
   uint32_t s2_wgs = 0;    // RMQ_S2_WGS: cap on stage-2 workgroups (0: one thread group per column)
   uint32_t s3_first = 1;  // stage-3 workgroups first in dispatch order (RMQ_S3_FIRST=0: last)
-  uint32_t wide = 1;      // stage 3's wide form for groups of short records (RMQ_WIDE=0: lane pairs only)
   uint32_t s3_lead = 0;   // stage-3 workgroups before the other roles (RMQ_S3_LEAD; 0: all of them)
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
   std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)

@@ -13,9 +13,9 @@
 //          the chunk sums before it and the byte counts of its chunk before it (at most 64 + 255
 //          values, L2-resident), an exclusive scan over its 16 requests -> compact output positions
 //          (into the result rows' out_pos), ENOSPC marking (every request's bytes count, served or
-//          not: FORMAT.md §7); then each wave copies its 4 requests as one run of 16-byte pieces
-//          (the requests' loads in flight together, four per lane) from the lowest local replica
-//          ring to the output. Records and output positions are 16-byte aligned
+//          not: FORMAT.md §7); then each wave copies its 4 requests one after the other (the
+//          requests' ring words loaded before the placement barrier), 16-byte loads from the
+//          lowest local replica ring, four in flight per lane, 16-byte stores to the output. Records and output positions are 16-byte aligned
 //          (FORMAT.md §1), so no piece straddles a record, the ring end or an output boundary.
 //          (Round 2 placed with a single 1024-thread workgroup between the two: 12.6 us of the
 //          max = 10 fetch of 16,384 requests with the rest of the GPU idle.)
@@ -238,52 +238,27 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   const u64 q_pos = qv ? a.aux[2 * rq + 0] : 0ull, q_ring = qv ? a.aux[2 * rq + 1] : 0ull;
   const u64 q_nb = qv ? a.cpre[rq] : 0ull;
   __syncthreads();
-  // one run of 16-byte pieces over the wave's requests (each served request's pieces in order),
-  // so the loads of all of them are in flight together instead of one request after another
+  // the wave's requests one after the other (one stream of 16-byte pieces per wave: four requests
+  // side by side, a quarter-wave or an interleaved run each, measured 1.7x slower at max = 1024)
   const u64 q_out = lane < kGQ ? s_pos[(w * kGQ + lane) & (kGR - 1u)] : 0ull;
-  const bool served = qv && q_nb && q_out + q_nb <= a.out_cap;
-  const u64 q_pc = served ? q_nb >> 4 : 0ull;
-  u64 pc[kGQ + 1], ps[kGQ], po[kGQ], pm[kGQ];
-  const uint8_t* pr[kGQ];
-  pc[0] = 0;
-#pragma unroll
   for (u32 q = 0; q < kGQ; ++q) {
-    pc[q + 1] = pc[q] + lane64(q_pc, q);
-    ps[q] = lane64(q_pos, q);
-    po[q] = lane64(q_out, q);
-    const u64 rw = lane64(q_ring, q);
-    pr[q] = st.logs + (rw >> 6);
-    pm[q] = (1ull << (rw & 63ull)) - 1ull;
-  }
-  const u64 total = pc[kGQ];
-  for (u64 b = 0; b < total; b += 64ull * 4) {  // four 16-byte pieces in flight per lane
-    uint4 x[4];
-    uint8_t* dst[4];
+    const u64 nbr = lane64(q_nb, q), pos0_out = lane64(q_out, q);
+    if (!nbr || pos0_out + nbr > a.out_cap) continue;  // nothing, past the end, or not served
+    const u64 pos0 = lane64(q_pos, q), rw = lane64(q_ring, q);
+    const uint8_t* ring = st.logs + (rw >> 6);
+    const u64 mask = (1ull << (rw & 63ull)) - 1ull;
+    uint8_t* out = a.out + pos0_out;
+    const u64 pieces = nbr >> 4;
+    u64 p = lane;
+    for (; p + 192 < pieces; p += 256) {  // four 16-byte pieces in flight per lane
+      uint4 x[4];
 #pragma unroll
-    for (u32 u = 0; u < 4; ++u) {
-      const u64 k = b + 64ull * u + lane;
-      dst[u] = nullptr;
-      if (k < total) {
-        // the request holding piece k (kGQ wave-uniform candidates, selected without indexing)
-        u64 s = ps[0], o = po[0], m = pm[0], c = pc[0];
-        const uint8_t* rg = pr[0];
+      for (u32 u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 64 * u)) & mask));
 #pragma unroll
-        for (u32 q = 1; q < kGQ; ++q)
-          if (k >= pc[q]) {
-            s = ps[q];
-            o = po[q];
-            m = pm[q];
-            c = pc[q];
-            rg = pr[q];
-          }
-        const u64 j = k - c;
-        x[u] = *reinterpret_cast<const uint4*>(rg + ((s + 16ull * j) & m));
-        dst[u] = a.out + o + 16ull * j;
-      }
+      for (u32 u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(out + 16ull * (p + 64 * u)) = x[u];
     }
-#pragma unroll
-    for (u32 u = 0; u < 4; ++u)
-      if (dst[u]) *reinterpret_cast<uint4*>(dst[u]) = x[u];
+    for (; p < pieces; p += 64)
+      *reinterpret_cast<uint4*>(out + 16ull * p) = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * p) & mask));
   }
 }
 

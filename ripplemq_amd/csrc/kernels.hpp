@@ -222,8 +222,6 @@ struct PipeArgs {
   uint32_t key_passes;     // 1 (P <= 256) or 2
   uint32_t gt;             // tiles per hist / excl column (group tile capacity)
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
-  uint32_t wide3;          // stage 3 in the wide form: a wave per task pair, a lane per record
-                           // (single-GPU kernel; wg3 counts pairs)
   uint32_t debug;         // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2, 32 no leader / mask / totals gathers in stage 3
@@ -241,6 +239,7 @@ struct PipeArgs {
   const CrcConsts* crc;
   uint64_t* done_word;     // host-visible: sequence number of the previous launch (written at start)
   uint64_t* lastg;         // replication: [P] record bytes / 16 of the last group applied (a plan's C)
+  uint32_t* rlate;         // [P] 1: the partition's retention of the group applied stopped early
   uint64_t* ret_late;      // host-visible: written with launch_seq when a partition's retention of
                            // the group applied stops early (its stage 4 in the next launch finishes it)
   uint64_t launch_seq;

@@ -166,7 +166,7 @@ __device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
+__device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
   const PipeGroup& G = A.g1;
   const u32 jb = batch_of_tile(G, t);
   const PipeBatch& b = G.b[jb];
@@ -400,7 +400,7 @@ __device__ __forceinline__ u64 block_incl_scan_u64(u64 v, u64* s_w, u64* total) 
 // thread of its partition's column once the group's totals of p are known (`tot`). B = the leader's
 // log end before the round: the state this launch's stage 3 reads (after the group two before)
 // plus the totals of the group it applies (the group before), E = B + the round.
-__device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
+__device__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u64 t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
@@ -472,7 +472,7 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
 
 // End of a partial catch-up (FORMAT.md §9): the largest sparse-index entry E[m] with
 // F.pos < E[m].pos <= lim among the entries complete now (m I <= used); 0 if none.
-__device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
+__device__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
   const RingRef rg = ring_ref(st, p);
   const u32 ilog = st.interval_log2;
   u64 lo = (fpos >> ilog) + 1ull, hi = min(lim, used) >> ilog;  // candidates m in [lo, hi]
@@ -496,6 +496,34 @@ __device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos,
   return found;
 }
 
+// Inputs of out entry e (partition p) to the plan: the group's totals and the stage-2 verdict of
+// the entry (sc1: written by other workgroups of this launch), the leader's log end before the
+// round (the state this launch's stage 3 reads plus the group it applies) and the group before's
+// bytes. e = ~0u: none (zeros).
+struct PlanIn {
+  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg;
+  u32 p, fl;
+};
+__device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
+  const XPlanArgs& X = A.xp2;
+  PlanIn v;
+  v.p = p;
+  v.tot = v.f_off = v.f_pos = v.gap = v.t3 = v.leo = v.used = v.lastg = 0ull;
+  v.fl = 0u;
+  if (e != ~0u) {
+    v.tot = load_sc1(&A.s2.totals[p]);
+    v.f_off = load_sc1(&X.xdec[e].f_off);
+    v.f_pos = load_sc1(&X.xdec[e].f_pos);
+    v.gap = load_sc1(&X.xdec[e].gap);
+    v.fl = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
+    v.t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
+    v.leo = A.cur.leo[p];
+    v.used = A.cur.used[p];
+    v.lastg = A.g3.nb ? 0ull : A.lastg[p];
+  }
+  return v;
+}
+
 // The group's outbox layout (FORMAT.md §9 v3), one workgroup: destination d's region sits at
 // d * dcap of the outbox (the host sends [d * dcap, d * dcap + size)):
 //   [header 64 B][directory n_d x 32 B][record table N_d x 8 B, padded to 16][records][rows]
@@ -504,7 +532,7 @@ __device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos,
 // (the gap, then the round's own), where stage 3 puts the round's records and table slots, the
 // catch-up list for the stage-3 launch's copy waves, the consumer-offset row, the next expected
 // follower log end.
-__device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
+__device__ void stage2_plan(const PipeArgs& A) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u64* const totals = A.s2.totals;
@@ -523,22 +551,19 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
     const u32 df = __hip_atomic_load(&X.dflag[dd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const u64 n = e1 - e0, base = (u64)dd * dcap;
     const u64 tab = base + kRegionHdr + kDirEntry * n;
-    // pass 1: record counts (for the table size) need the grants, which need the gap prefix
+    // pass 1: record counts (for the table size) need the grants, which need the gap prefix. The
+    // inputs of the thread's next entry are loaded while this one is planned (and the partition of
+    // the one after), so an iteration waits on barriers and scans, not on memory.
     u64 gap_run = 0, run_a = 0, run_b = 0;
+    PlanIn cur = plan_in(A, e0 + tid < e1 ? e0 + tid : ~0u, e0 + tid < e1 ? X.xo_p[e0 + tid] : 0u);
+    u32 p_next = e0 + kPT + tid < e1 ? X.xo_p[e0 + kPT + tid] : 0u;
     for (u32 c0 = e0; c0 < e1; c0 += kPT) {
       const u32 e = c0 + tid;
       const bool in = e < e1;
-      u64 tot = 0, f_off = 0, f_pos = 0, gap = 0;
-      u32 fl = 0;
-      u32 p = 0;
-      if (in) {
-        p = X.xo_p[e];
-        tot = load_sc1(&totals[p]);
-        f_off = load_sc1(&X.xdec[e].f_off);
-        f_pos = load_sc1(&X.xdec[e].f_pos);
-        gap = load_sc1(&X.xdec[e].gap);
-        fl = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
-      }
+      const PlanIn nxt = plan_in(A, e + kPT < e1 ? e + kPT : ~0u, p_next);
+      p_next = e + 2 * kPT < e1 ? X.xo_p[e + 2 * kPT] : 0u;
+      const u32 p = cur.p, fl = cur.fl;
+      const u64 tot = cur.tot, f_off = cur.f_off, f_pos = cur.f_pos, gap = cur.gap;
       u64 gex = 0;
       if (df & kDecGapped) {
         u64 gt;
@@ -550,10 +575,10 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
       u64 cnt = rcnt, b16 = rb16, gcnt = 0, gb16 = 0, first = f_off;
       u64 nx_off = 0, nx_pos = 0;
       bool with_round = true, set_cu = false, cu_entry = false;
-      const u64 t3 = (in && A.g3.nb) ? A.s3.totals[p] : 0ull;
-      const u64 Boff = in ? A.cur.leo[p] + (t3 >> 40) : 0ull;
-      const u64 Bpos = in ? A.cur.used[p] + 16ull * (t3 & kLow40) : 0ull;
-      const u64 Cpos = !in ? 0ull : A.g3.nb ? A.cur.used[p] : Bpos - 16ull * A.lastg[p];  // as plan_decide
+      const u64 t3 = cur.t3;
+      const u64 Boff = in ? cur.leo + (t3 >> 40) : 0ull;
+      const u64 Bpos = in ? cur.used + 16ull * (t3 & kLow40) : 0ull;
+      const u64 Cpos = !in ? 0ull : A.g3.nb ? cur.used : Bpos - 16ull * cur.lastg;  // as plan_decide
       if (in) {
         nx_off = Boff + rcnt;
         nx_pos = Bpos + 16ull * rb16;
@@ -648,6 +673,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
       }
       // (row entries and the data section offset need the region totals: pass 2)
       if (in) X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
+      cur = nxt;
       __syncthreads();
     }
     const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
@@ -800,7 +826,7 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
   }
 }
 
-__device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
+__device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
   const u32 P = A.st.P, T = G.tiles, GT = A.gt;
@@ -1057,7 +1083,7 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
 // l, l + 64, ... (kBU per lane in flight, the block after each from the neighbour lane), folds
 // them by Horner's rule with the 1 KB shift table, shifts its register past the pieces that follow
 // its last one and the wave XOR-reduces; lane 0 writes the header. xdst: the record's outbox copies.
-__device__ __forceinline__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
+__device__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
                            u64 off, u32 dead, uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx) {
   const u32 lane = threadIdx.x & 63, RF = A.st.RF;
   const u64 rstride = A.st.rstride;
@@ -1125,7 +1151,7 @@ __device__ __forceinline__ void big_record(const PipeArgs& A, const Stage3Smem& 
 // it with big_record. Their task waves leave these records to them (header and payload; the task
 // wave still writes the out offset, index entries, record-table slots and statistics).
 template <bool XR>
-__device__ __forceinline__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
+__device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
   const PipeGroup& G = A.g3;
   const PipeScratch& x = A.s3;
   const DevState& st = A.st;
@@ -1178,7 +1204,7 @@ __device__ __forceinline__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& 
 }
 
 template <bool XR>
-__device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
+__device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
                               const TaskState& Z, bool cand, uint4& stat_out) {
   const PipeBatch& b = A.g3.b[T.jb];
   const DevState& st = A.st;
@@ -1338,232 +1364,61 @@ __device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Sme
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Stage 3, wide form (single-GPU kernel, PipeArgs::wide3): a wave applies two consecutive tasks
-// of one batch, a lane per record, so the loads of all 64 records are in flight together and a
-// four-batch group's tasks fit the resident wave slots in one generation (the lane-pair form
-// needs two: the second generation starts as the first retires). Only for records of at most
-// kWidePieces payload pieces; a wave that meets a longer candidate applies its two tasks with the
-// lane-pair code, one after the other.
-// ------------------------------------------------------------------------------------------
-constexpr u32 kWidePieces = 7;             // 112 payload bytes: header + pieces = one 128-byte image row
-constexpr u32 kWB = kWidePieces + 1u;      // aligned blocks covering 7 misaligned pieces
-
-struct WideState {
-  u64 pos, off, rdesc;
-  u32 lm, dead;
-  uint4 blk[kWB];
-};
-
-__device__ __forceinline__ WideState stage3_wide_r2(const PipeArgs& A, u32 jb, u32 i, const TaskRec& R, bool cand) {
-  WideState Z;
-  Z.pos = Z.off = 0ull;
-  Z.lm = Z.dead = 0u;
-  const RecWords W = rec_words(A, jb, i, R.p, cand);
-  Z.rdesc = W.rdesc;
-  // every block of the record, speculatively (leadership is checked before any store)
-  const u64 a0 = R.src & ~15ull, lim = R.src + R.L;
-#pragma unroll
-  for (u32 q = 0; q < kWB; ++q) {
-    const u64 ad = a0 + 16ull * q;
-    Z.blk[q] = make_uint4(0, 0, 0, 0);
-    if (cand && ad < lim && !(A.debug & 4u)) Z.blk[q] = *reinterpret_cast<const uint4*>(ad);
-  }
-  if (cand) {
-    u32 rk, rel16;
-    rec_place(W, R, Z.pos, Z.off, Z.dead, Z.lm, rk, rel16);
-  }
-  return Z;
-}
-
-// Records i0 .. i0 + 63 of batch jb (tasks tk, tk + 1 of the batch), lane l = record i0 + l: CRC by
-// Horner's rule over the record's pieces with the 16-byte zero-shift table, then the two halves of
-// the wave go through the wave's LDS log image one after the other (32 records of 128 bytes, 8
-// lanes per record per store), out offsets, sparse-index entries, the two tasks' statistics.
-__device__ __forceinline__ void stage3_wide_finish(const PipeArgs& A, Stage3Smem& S, u32 jb, u32 i0, u32 tk, const TaskRec& R,
-                                   const WideState& Z, bool cand) {
-  const PipeBatch& b = A.g3.b[jb];
-  const DevState& st = A.st;
-  const u32 lane = threadIdx.x & 63, w = threadIdx.x >> 6, RF = st.RF;
-  const u32 i = i0 + lane;
-  const bool in = i < b.n;
-  const u32 L = R.L, fl = R.cr.x >> kFlagShift, rej = batch_rej(A, jb);
-  const bool ns = (Z.lm & kNoSpace) != 0u, lead = (Z.lm & kLead) != 0u;
-  const u32 lm8 = Z.lm & 0xFFu;
-  const bool ok = cand && lead && !ns;
-  const u32 m = ok ? (L + 15u) >> 4 : 0u;  // <= kWidePieces (the caller checked)
-  const u32 sa = (u32)(R.src & 15u);
-  const u32 hl = lane >> 5, r32 = lane & 31u;
-  // the two tasks' statistics, from ballots taken here with the whole wave active (wave-uniform)
-  uint4 st2[2];
-  {
-    const u64 b_in = __ballot(in), b_app = __ballot(ok), b_nl = __ballot(cand && !lead);
-    const u64 b_np = __ballot(in && fl == kFlNoPart), b_ns = __ballot(cand && lead && ns);
-#pragma unroll
-    for (u32 h = 0; h < 2; ++h) {
-      const u32 sh = 32u * h;
-      const u32 n_in = (u32)__popcll((b_in >> sh) & 0xFFFFFFFFull);
-      const u32 n_np = rej ? 0u : (u32)__popcll((b_np >> sh) & 0xFFFFFFFFull);
-      const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
-      st2[h] = make_uint4((u32)__popcll((b_app >> sh) & 0xFFFFFFFFull), (u32)__popcll((b_nl >> sh) & 0xFFFFFFFFull), n_np,
-                          (u32)__popcll((b_ns >> sh) & 0xFFFFFFFFull) | (n_inv << 16));
-    }
-  }
-  u32 acc = 0;
-#pragma unroll
-  for (u32 k = 0; k < kWidePieces; ++k) {
-    if (k < m) {
-      const u32 nb = L - 16u * k < 16u ? L - 16u * k : 16u;
-      const uint4 v = extract_piece(Z.blk[k], Z.blk[k + 1], sa, nb);
-      acc = crc_zshift(S.z[0], acc) ^ piece_crc(A, S, v, k);
-      if (hl == 0) S.img[w][r32][k + 1] = v;  // the first half's image rows now, the second's below
-    }
-  }
-  u32 crc = 0;
-  if (m) {  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad)); an empty record's is 0
-    const u32 pad = 16u * m - L;
-    crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
-  }
-  const uint4 h = make_uint4((u32)Z.off, (u32)(Z.off >> 32), L, crc);
-  const RingRef rg = ring_ref(Z.rdesc, st.interval_log2, st.icap_mul);
-  const u64 rstride = st.rstride;
-  const u32 lmw = (A.debug & 1u) ? 0u : 0xFFu;
-  for (u32 half = 0; half < 2; ++half) {
-    if (hl == half) {
-      if (half == 1) {
-#pragma unroll
-        for (u32 k = 0; k < kWidePieces; ++k)
-          if (k < m) {
-            const u32 nb = L - 16u * k < 16u ? L - 16u * k : 16u;
-            S.img[w][r32][k + 1] = extract_piece(Z.blk[k], Z.blk[k + 1], sa, nb);
-          }
-      }
-      S.img[w][r32][0] = h;
-      S.info[w][r32] = make_uint4((u32)Z.pos, (u32)(Z.pos >> 32), (u32)(rg.base >> 8),
-                                  ok ? lm8 | (m << 8) | (1u << 12) | (Z.dead << 13) | ((u32)(Z.rdesc & 63ull) << 24) : 0u);
-    }
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (u32 s4 = 0; s4 < kTaskRecs * 8u / 64u; ++s4) {
-      const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
-      const uint4 inf = S.info[w][rr];
-      const u32 mr = (inf.w >> 8) & 0xFu;
-      if (((inf.w >> 12) & 1u) && k <= mr && k >= ((inf.w >> 13) & 0x1Fu)) {
-        const uint4 v = S.img[w][rr][k];
-        const u64 rpos = ((u64)inf.y << 32) | inf.x;
-        const u64 rmask = (1ull << (inf.w >> 24)) - 1ull;
-        uint8_t* dst = st.logs + ((u64)inf.z << 8) + ((rpos + 16ull * k) & rmask);
-        const u32 lmr = inf.w & lmw;
-        for (u32 r = 0; r < RF; ++r)
-          if ((lmr >> r) & 1u) store_log16(dst + r * rstride, v);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // the image is rewritten by the second half / the next pair
-  }
-  if (in) b.out_offsets[i] = ok ? Z.off : ~0ull;
-  if (ok) {
-    const u32 ilog = st.interval_log2;
-    const u64 end = Z.pos + 16ull * (1ull + m);
-    for (u64 mm = (Z.pos >> ilog) + 1; (mm << ilog) <= end; ++mm) {
-      u64* e = st.index + (rg.ibase + mm % rg.icap) * 2;
-      e[0] = Z.off + 1;
-      e[1] = end;
-    }
-  }
-  if (lane == 0) {
-    A.g3.stats[jb][tk] = st2[0];
-    A.g3.stats[jb][tk + 1] = st2[1];
-  }
-}
-
-// The stage-3 workgroups of the wide form: wave v takes task pairs (2v, 2v + 1), then v + the
-// launch's stage-3 waves, ... (one pair per wave when the grid holds them all). A pair whose two
-// tasks lie in different batches, or that holds a candidate over kWidePieces pieces, is applied
-// by the lane-pair code, task by task.
-__device__ __forceinline__ void stage3_wide_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
-  const PipeGroup& G = A.g3;
-  const u32 tasks = G.task0[G.nb], pairs = (tasks + 1u) / 2u;
-  const u32 lane = threadIdx.x & 63;
-  u32 pr = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
-  PIPE_STAMP(0);
-  // the first pair's records are loaded while the CRC tables fill LDS
-  TaskPos T = task_pos(G, pr < pairs ? 2u * pr : 0u);
-  TaskRec R = stage3_r1_at(A, T.jb, T.i0 + lane);
-  if (!(A.debug & 8u)) {
-    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
-    uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
-  }
-  __syncthreads();
-  PIPE_STAMP(1);
-  while (pr < pairs) {
-    PIPE_STAMP(2);
-    const u32 t0 = 2u * pr;
-    const bool same = t0 + 1u < tasks && batch_of_task(G, t0 + 1u) == T.jb;
-    const u32 i = T.i0 + lane;
-    const bool cand = same && stage3_cand_at(A, T.jb, i, R);
-    if (same && !__any(cand && R.L > 16u * kWidePieces)) {
-      const WideState Z = stage3_wide_r2(A, T.jb, i, R, cand);
-      stage3_wide_finish(A, S, T.jb, T.i0, t0 - G.task0[T.jb], R, Z, cand);
-    } else {
-      for (u32 t = t0; t < t0 + 2u && t < tasks; ++t) {
-        const TaskPos T1 = task_pos(G, t);
-        const TaskRec R1 = stage3_r1(A, T1);
-        const bool c1 = stage3_cand(A, T1, R1);
-        const TaskState Z1 = stage3_r2(A, T1, R1, c1);
-        uint4 so;
-        stage3_finish<false>(A, S, T1, R1, Z1, c1, so);
-        if (lane == 0) G.stats[T1.jb][t - G.task0[T1.jb]] = so;
-      }
-    }
-    PIPE_STAMP(3);
-    pr += A.wg3 * kPW;
-    if (pr < pairs) {
-      T = task_pos(G, 2u * pr);
-      R = stage3_r1_at(A, T.jb, T.i0 + lane);
-    }
-  }
-  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(6);
-}
-
-// Retention after each batch of a group (FORMAT.md §4), batch by batch: after batch j (log end
-// fin[j], 0 = the batch appended nothing of p) the start moves to index entry
-// ceil((fin_j - seg) / I) when fin_j - start > seg. The start only grows, so a batch with
-// fin_j - start0 <= seg never moves it: the entries of the others are loaded together, then the
-// batches are replayed in order in registers. An entry at or past position `lim` may be written by
+// Retention after each batch of a group (FORMAT.md §4), batch by batch: after batch j the start
+// moves to index entry ceil((fin_j - seg) / I) when fin_j - start > seg, fin_j = the log end after
+// batch j: used0 + 16 (bc_j bytes) when used0 is the log end before the group (pre), else
+// used0 - 16 (tot - bc_j bytes) (used0 after it); bc = the group's aggregates through each batch
+// (a batch that appended nothing of p cannot move it). The start only grows, so a batch with
+// fin_j - start0 <= seg never moves it: the positions of the others' entries are loaded together,
+// the batches replayed in order in registers, and the offset of the last entry taken loaded after
+// (the same index entry: one cache line). An entry at or past position `lim` may be written by
 // the running launch: it is not read, the replay stops at its batch and the function returns
 // false (the next launch's stage 4 finishes the group; replaying applied batches moves nothing).
-__device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef& rg, const u64 (&fin)[kMaxGroup],
-                                               u64 lim, u64& soff, u64& spos) {
+__device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef& rg, const u64 (&bc)[kMaxGroup], u32 nb,
+                                               bool pre, u64 used0, u64 tot, u64 lim, u64& soff, u64& spos) {
   const u32 ilog = st.interval_log2;
-  u64 eo[kMaxGroup], ep[kMaxGroup];
-  bool late[kMaxGroup];
+  u64 ep[kMaxGroup];
+  u32 cand = 0, late = 0;  // bit j: batch j may move the start / its entry is not readable yet
+  u64 prev = 0;
 #pragma unroll
   for (u32 j = 0; j < kMaxGroup; ++j) {
-    eo[j] = ep[j] = 0ull;
-    late[j] = false;
-    if (fin[j] && fin[j] - spos > rg.seg) {
-      const u64 ms = (fin[j] - rg.seg + (1ull << ilog) - 1) >> ilog;
-      late[j] = (ms << ilog) > lim;
-      if (!late[j]) {
-        const u64* e = st.index + (rg.ibase + ms % rg.icap) * 2;
-        eo[j] = e[0];
-        ep[j] = e[1];
+    ep[j] = 0ull;
+    const bool app = j < nb && (bc[j] >> 40) != (prev >> 40);
+    const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
+    if (app && fin - spos > rg.seg) {
+      const u64 ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
+      cand |= 1u << j;
+      if ((ms << ilog) > lim) late |= 1u << j;
+      else ep[j] = st.index[(rg.ibase + ms % rg.icap) * 2 + 1];
+    }
+    prev = j < nb ? bc[j] : prev;
+  }
+  bool done = true;
+  int last = -1;
+  u64 sp = spos;
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j) {
+    const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
+    if (done && ((cand >> j) & 1u) && fin - sp > rg.seg) {
+      if ((late >> j) & 1u) {
+        done = false;
+      } else {
+        sp = ep[j];
+        last = (int)j;
       }
     }
   }
-  bool done = true;
+  if (last >= 0) {
+    u64 ms = 0;
 #pragma unroll
-  for (u32 j = 0; j < kMaxGroup; ++j)
-    if (done && fin[j] && fin[j] - spos > rg.seg) {
-      if (late[j]) {
-        done = false;
-      } else {
-        soff = eo[j];
-        spos = ep[j];
+    for (u32 j = 0; j < kMaxGroup; ++j)
+      if ((int)j == last) {
+        const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
+        ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
       }
-    }
+    soff = st.index[(rg.ibase + ms % rg.icap) * 2];
+    spos = sp;
+  }
   return done;
 }
 
@@ -1582,9 +1437,10 @@ __device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef
 //    less one interval to the partition). Then a fetch ordered after the launch sees the log start
 //    of the records it sees, and a drain needs no stage-4 launch unless a partition stopped early
 //    (it writes the launch number into ret_late).
-//  * stage 4: retention after each batch of the group applied one launch earlier: the batches the
-//    launch before could not finish (the rest replay without moving the start).
-__device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
+//  * stage 4: retention after each batch of the group applied one launch earlier, for the
+//    partitions whose replay that launch stopped (rlate[p]; the batch aggregates are loaded only
+//    for them, so the common case carries no stage-4 loads).
+__device__ void partition_threads(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
   const u32 RF = st.RF;
   const bool a3 = A.g3.nb != 0, a4 = A.g4.nb != 0;
@@ -1596,72 +1452,58 @@ __device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < RF ? st.match[(u64)p * RF + r] : 0ull;
   const u64 commit0 = st.commit[p], ts = st.term_start[p];
-  const u64 tot4 = a4 ? A.s4.totals[p] : 0ull;
   const u64 soff0 = st.start_off[p], spos0 = st.start_pos[p];
   const u64 desc = st.ring[p];
-  u64 bc[kMaxGroup], bc3[kMaxGroup];
+  const u32 late4 = a4 ? A.rlate[p] : 0u;  // the launch before stopped p's retention early
+  u64 bc3[kMaxGroup];
 #pragma unroll
-  for (u32 j = 0; j < kMaxGroup; ++j) {
-    bc[j] = a4 && j < A.g4.nb ? A.s4.bcum[(u64)j * st.P + p] : 0ull;
-    bc3[j] = a3 && j < A.g3.nb ? A.s3.bcum[(u64)j * st.P + p] : 0ull;
-  }
+  for (u32 j = 0; j < kMaxGroup; ++j) bc3[j] = a3 && j < A.g3.nb ? A.s3.bcum[(u64)j * st.P + p] : 0ull;
   if (A.lastg && a3) A.lastg[p] = lead ? (tot3 & kLow40) : 0ull;  // the next plans' C (FORMAT.md §9)
   if (!lead) return;
+  // ---- stage 3: log end, matchIndex, commit (first: the match row is dead before retention)
+  if (a3) {
+    A.nxt.leo[p] = leo0 + (tot3 >> 40);
+    A.nxt.used[p] = used0 + 16ull * (tot3 & kLow40);
+  }
+  const u64 tc = tot3 >> 40, leo = leo0 + tc;
+  if (tc || A.ackin) {
+    bool moved = tc != 0;
+    if (tc) {
+#pragma unroll
+      for (u32 r = 0; r < kMaxRF; ++r)
+        if (r < RF && ((lm >> r) & 1u)) {
+          row[r] = leo;
+          st.match[(u64)p * RF + r] = leo;
+        }
+    }
+    // followers' acks of an earlier group (replication transport, FORMAT.md §9)
+    if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row, A.xreq, A.acks_round);
+    if (moved) {
+      const u64 c = quorum_commit(row, RF, commit0, ts);
+      st.commit[p] = c;
+      st.hw[p] = c;
+    }
+  }
+
   const RingRef rg = ring_ref(desc, st.interval_log2, st.icap_mul);
   u64 soff = soff0, spos = spos0;
-
   // ---- stage 4: retention of the group applied one launch earlier (cur: its final log end)
-  if (tot4 >> 40) {
-    u64 fin[kMaxGroup], prev = 0;
+  if (late4) {
+    u64 bc[kMaxGroup];
 #pragma unroll
-    for (u32 j = 0; j < kMaxGroup; ++j) {
-      const bool app = j < A.g4.nb && (bc[j] >> 40) != (prev >> 40);  // batch j appended records of p
-      fin[j] = app ? used0 - 16ull * ((tot4 - bc[j]) & kLow40) : 0ull;
-      prev = j < A.g4.nb ? bc[j] : prev;
-    }
-    retain_batches(st, rg, fin, ~0ull, soff, spos);
+    for (u32 j = 0; j < kMaxGroup; ++j) bc[j] = j < A.g4.nb ? A.s4.bcum[(u64)j * st.P + p] : 0ull;
+    retain_batches(st, rg, bc, A.g4.nb, false, used0, A.s4.totals[p], ~0ull, soff, spos);
   }
   // ---- retention of the group this launch applies (cur: the log end before it)
-  if (tot3 >> 40) {
-    u64 fin[kMaxGroup], prev = 0;
-#pragma unroll
-    for (u32 j = 0; j < kMaxGroup; ++j) {
-      const bool app = j < A.g3.nb && (bc3[j] >> 40) != (prev >> 40);
-      fin[j] = app ? used0 + 16ull * (bc3[j] & kLow40) : 0ull;
-      prev = j < A.g3.nb ? bc3[j] : prev;
-    }
-    if (!retain_batches(st, rg, fin, used0, soff, spos) && A.ret_late)
-      __hip_atomic_store(A.ret_late, A.launch_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool late3 = false;
+  if (tc) {
+    late3 = !retain_batches(st, rg, bc3, A.g3.nb, true, used0, tot3, used0, soff, spos);
+    if (late3 && A.ret_late) __hip_atomic_store(A.ret_late, A.launch_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if (late3 || late4) A.rlate[p] = late3 ? 1u : 0u;
   if (soff != soff0 || spos != spos0) {
     st.start_off[p] = soff;
     st.start_pos[p] = spos;
-  }
-
-  // ---- stage 3: log end, matchIndex, commit
-  u64 tc = 0, leo = leo0;
-  if (a3) {
-    tc = tot3 >> 40;
-    leo = leo0 + tc;
-    A.nxt.leo[p] = leo;
-    A.nxt.used[p] = used0 + 16ull * (tot3 & kLow40);
-  }
-  if (!tc && !A.ackin) return;
-  bool moved = tc != 0;
-  if (tc) {
-#pragma unroll
-    for (u32 r = 0; r < kMaxRF; ++r)
-      if (r < RF && ((lm >> r) & 1u)) {
-        row[r] = leo;
-        st.match[(u64)p * RF + r] = leo;
-      }
-  }
-  // followers' acks of an earlier group (replication transport, FORMAT.md §9)
-  if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row, A.xreq, A.acks_round);
-  if (moved) {
-    const u64 c = quorum_commit(row, RF, commit0, ts);
-    st.commit[p] = c;
-    st.hw[p] = c;
   }
 }
 
@@ -1673,7 +1515,7 @@ __device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
 // that start in it. Round h-1's records are complete (the previous launch) and round h's stores
 // into the ring land past the gap's end minus the ring size (the plan's condition), so nothing
 // this reads changes under it.
-__device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
+__device__ void stage3_catchup(const PipeArgs& A, u32 wg) {
   const u32 items = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n + 1));
   const u32 ncu = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n));
   if (!items) return;
@@ -1783,10 +1625,6 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   const PipeGroup& G = A.g3;
   const u32 tasks = G.task0[G.nb];
   const u32 lane = threadIdx.x & 63;
-  if (!XR && A.wide3) {
-    stage3_wide_waves(A, S, wg);
-    return;
-  }
   // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
   u32 task = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);

@@ -330,7 +330,7 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
 // A grid of at most a few workgroups per CU: each copies the CRC tables into LDS once and its waves
 // take tasks w, w + waves, ... (the tables were 20 KB per 32 records' worth of workgroup before;
 // the 16-byte shift is a multiply, the 1 KB one of large records is read from global memory).
-__global__ __launch_bounds__(kIT) void ingest_verify_kernel(IngestArgs A) {
+__global__ __launch_bounds__(kIT, 8) void ingest_verify_kernel(IngestArgs A) {
   __shared__ __attribute__((aligned(16))) u32 t8[8][256];
   __shared__ __attribute__((aligned(16))) u32 z32[4][256];  // register shift past 32 zero bytes
   {

@@ -468,17 +468,20 @@ int repl_before_launch(rmq_engine* e, PipeArgs& a) {
 int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s3) {
   Replication* r = e->repl;
   if (!r) return RMQ_OK;
+  // the rounds of groups applied by earlier launches first: on the exchange stream they then wait
+  // only for their own apply launch, not behind the size swap of this launch's group (which waits
+  // for this whole launch)
+  while (!r->sized.empty() && r->sets[r->sized.front()].applied_launch < e->launch_seq) {
+    int rc = post_round(e, r->sized.front());
+    if (rc) return rc;
+    r->sized.pop_front();
+  }
   if (s2) {
     HIP_TRY(hipEventRecord(r->sets[s2->set].ev_s2, e->main_s));
     const bool drop = r->drop_n && s2->b[0].ticket >= r->drop_from;
     if (drop) r->drop_n--;
     int rc = post_sizes(e, s2->set, drop);
     if (rc) return rc;
-  }
-  while (!r->sized.empty() && r->sets[r->sized.front()].applied_launch < e->launch_seq) {
-    int rc = post_round(e, r->sized.front());
-    if (rc) return rc;
-    r->sized.pop_front();
   }
   if (s3) {
     XchgSet& x = r->sets[s3->set];

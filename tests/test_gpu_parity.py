@@ -293,13 +293,11 @@ def test_pipelined_groups(oracle_mod, group):
         assert dev.state(5)["log_end_offset"] == 0
 
 
-@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"},
-                                 {"RMQ_WIDE": "0"}])
+@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"}])
 def test_pipelined_dispatch_modes(oracle_mod, monkeypatch, env):
     # the non-default dispatch modes (read at rmq_create): resident task waves looping over the
-    # group's task pairs, stage-3 workgroups dispatched after the other roles, few large-record
-    # workgroups (each wave then takes many records of the list), and stage 3 in lane pairs only
-    # (no wide form)
+    # group's tasks, stage-3 workgroups dispatched after the other roles, and few large-record
+    # workgroups (each wave then takes many records of the list)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,
