@@ -54,10 +54,23 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   long lo = (long)((v.start_pos + I - 1) >> ilog), hi = (long)(v.used >> ilog);
   bool open = t < v.leo && lo <= hi;
   long ws = lo, step = 1;
+  const u64 mask = v.rg.seg - 1;
+  u64 sw = ~0ull;  // speculative header window: the interval the interpolation puts t in
   if (open) {
     const double f = (double)(t - v.start_off) / (double)(v.leo - v.start_off);
-    const long me = (long)((v.start_pos + (u64)(f * (double)(v.used - v.start_pos))) >> ilog);
+    const u64 gpos = v.start_pos + (u64)(f * (double)(v.used - v.start_pos));
+    const long me = (long)(gpos >> ilog);
     ws = max(lo, min(me - 15, hi - 31));
+    sw = max((u64)me << ilog, v.start_pos) & ~15ull;
+  } else if (t < v.leo) {
+    sw = v.start_pos;  // no index entry past the start: the walk starts at the log start
+  }
+  // loaded with the first probe round; used if the entry found lies inside it (records of one
+  // size: always), so the walk below needs no load of its own
+  u32 Sw0 = 0, Sw1 = 0;
+  if (sw != ~0ull) {
+    Sw0 = *reinterpret_cast<const u32*>(v.ring + ((sw + 32ull * hl + 8ull) & mask));
+    Sw1 = *reinterpret_cast<const u32*>(v.ring + ((sw + 32ull * hl + 24ull) & mask));
   }
   for (bool first = true; __any(open); first = false) {
     if (!first) {
@@ -98,13 +111,17 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   if (t >= v.leo) return v.used;
   // walk the headers of the records in [c_off, t): they start within one index interval after
   // c_pos, read as 1 KiB windows of 16-byte pieces (two pieces per lane of the half; one window
-  // when I <= 1 KiB)
-  const u64 mask = v.rg.seg - 1;
-  u64 wb = c_pos;
-  u32 Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
-  u32 Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
+  // when I <= 1 KiB), the first the speculative one when it holds c_pos
+  u64 wb = sw;
+  u32 Lw0 = Sw0, Lw1 = Sw1;
+  u32 cur = (u32)((c_pos - sw) >> 4);  // window piece of the current record
+  if (sw == ~0ull || c_pos < sw || c_pos >= sw + 1024ull) {
+    wb = c_pos;
+    cur = 0;
+    Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
+    Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
+  }
   u64 k = t - c_off;
-  u32 cur = 0;  // window piece of the current record
   while (__any(k > 0)) {
     const bool mv = k > 0 && cur >= 64u;  // half-uniform: the half walked off its window
     if (__any(mv)) {
@@ -241,6 +258,43 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   // the wave's requests one after the other (one stream of 16-byte pieces per wave: four requests
   // side by side, a quarter-wave or an interleaved run each, measured 1.7x slower at max = 1024)
   const u64 q_out = lane < kGQ ? s_pos[(w * kGQ + lane) & (kGR - 1u)] : 0ull;
+  // requests of at most 128 pieces each (max = 10 of short records): all four copied with one round
+  // of loads (two pieces per lane and request) instead of one round per request
+  {
+    bool small = true;
+#pragma unroll
+    for (u32 q = 0; q < kGQ; ++q) {
+      const u64 nbr = lane64(q_nb, q), po = lane64(q_out, q);
+      small = small && (!nbr || po + nbr > a.out_cap || (nbr >> 4) <= 128u);
+    }
+    if (small) {
+      uint4 x[kGQ][2];
+#pragma unroll
+      for (u32 q = 0; q < kGQ; ++q) {
+        const u64 nbr = lane64(q_nb, q), po = lane64(q_out, q);
+        const bool sv = nbr && po + nbr <= a.out_cap;
+        const u64 pos0 = lane64(q_pos, q), rw = lane64(q_ring, q);
+        const uint8_t* ring = st.logs + (rw >> 6);
+        const u64 mask = (1ull << (rw & 63ull)) - 1ull;
+#pragma unroll
+        for (u32 h = 0; h < 2; ++h) {
+          const u64 k = lane + 64u * h;
+          if (sv && k < (nbr >> 4)) x[q][h] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * k) & mask));
+        }
+      }
+#pragma unroll
+      for (u32 q = 0; q < kGQ; ++q) {
+        const u64 nbr = lane64(q_nb, q), po = lane64(q_out, q);
+        const bool sv = nbr && po + nbr <= a.out_cap;
+#pragma unroll
+        for (u32 h = 0; h < 2; ++h) {
+          const u64 k = lane + 64u * h;
+          if (sv && k < (nbr >> 4)) *reinterpret_cast<uint4*>(a.out + po + 16ull * k) = x[q][h];
+        }
+      }
+      return;
+    }
+  }
   for (u32 q = 0; q < kGQ; ++q) {
     const u64 nbr = lane64(q_nb, q), pos0_out = lane64(q_out, q);
     if (!nbr || pos0_out + nbr > a.out_cap) continue;  // nothing, past the end, or not served

@@ -166,7 +166,7 @@ __device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
-__device__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
+__device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
   const PipeGroup& G = A.g1;
   const u32 jb = batch_of_tile(G, t);
   const PipeBatch& b = G.b[jb];
@@ -400,7 +400,7 @@ __device__ __forceinline__ u64 block_incl_scan_u64(u64 v, u64* s_w, u64* total) 
 // thread of its partition's column once the group's totals of p are known (`tot`). B = the leader's
 // log end before the round: the state this launch's stage 3 reads (after the group two before)
 // plus the totals of the group it applies (the group before), E = B + the round.
-__device__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
+__device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u64 t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
@@ -472,7 +472,7 @@ __device__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64 tot) {
 
 // End of a partial catch-up (FORMAT.md §9): the largest sparse-index entry E[m] with
 // F.pos < E[m].pos <= lim among the entries complete now (m I <= used); 0 if none.
-__device__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
+__device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos, u64 lim, u64 used, u64* xoff, u64* xpos) {
   const RingRef rg = ring_ref(st, p);
   const u32 ilog = st.interval_log2;
   u64 lo = (fpos >> ilog) + 1ull, hi = min(lim, used) >> ilog;  // candidates m in [lo, hi]
@@ -532,7 +532,7 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
 // (the gap, then the round's own), where stage 3 puts the round's records and table slots, the
 // catch-up list for the stage-3 launch's copy waves, the consumer-offset row, the next expected
 // follower log end.
-__device__ void stage2_plan(const PipeArgs& A) {
+__device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u64* const totals = A.s2.totals;
@@ -676,23 +676,45 @@ __device__ void stage2_plan(const PipeArgs& A) {
       cur = nxt;
       __syncthreads();
     }
+    if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(2);  // first destination: pass 1
     const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
     const u64 data = tab + ((8ull * N + 15ull) & ~15ull), rows = data + 16ull * B16;
     const u64 rowb = 16ull + 8ull * C;
-    // pass 2: data offsets, rows
-    for (u32 e = e0 + tid; e < e1; e += kPT) {
-      XEntry& xe = X.xe[e];
-      if (xe.data_abs != kNoRound) xe.data_abs = data + 16ull * xe.data_start16;
-      const u32 ri = X.xdec[e].pad & ~kRowRebase;
-      if (ri) {
-        const u32 p = X.xo_p[e];
-        uint8_t* rw = X.outbox + rows + rowb * (ri - 1u);
-        // a rebase entry's row carries the rebase point's position (FORMAT.md §9)
-        const u64 rp = (X.xdec[e].pad & kRowRebase) ? load_sc1(&X.xdec[e].f_pos) : 0ull;
-        *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, (u32)rp, (u32)(rp >> 32));
-        for (u32 c = 0; c < C; ++c) reinterpret_cast<u64*>(rw + 16)[c] = st.cons[(u64)p * C + c];
+    // pass 2: data offsets, rows (the entries' words of eight iterations loaded at once); a row's
+    // partition has its consumer offsets sent: its change flag is cleared
+    constexpr u32 kP2 = 8;
+    for (u32 e8 = e0 + tid; e8 < e1; e8 += kP2 * kPT) {
+      u64 da[kP2];
+      u32 ds[kP2], pad[kP2];
+#pragma unroll
+      for (u32 k = 0; k < kP2; ++k) {
+        const u32 e = e8 + k * kPT;
+        da[k] = kNoRound;
+        ds[k] = pad[k] = 0u;
+        if (e < e1) {
+          da[k] = X.xe[e].data_abs;
+          ds[k] = X.xe[e].data_start16;
+          pad[k] = X.xdec[e].pad;
+        }
+      }
+#pragma unroll
+      for (u32 k = 0; k < kP2; ++k) {
+        const u32 e = e8 + k * kPT;
+        if (e >= e1) continue;
+        if (da[k] != kNoRound) X.xe[e].data_abs = data + 16ull * ds[k];
+        const u32 ri = pad[k] & ~kRowRebase;
+        if (ri) {
+          const u32 p = X.xo_p[e];
+          uint8_t* rw = X.outbox + rows + rowb * (ri - 1u);
+          // a rebase entry's row carries the rebase point's position (FORMAT.md §9)
+          const u64 rp = (pad[k] & kRowRebase) ? load_sc1(&X.xdec[e].f_pos) : 0ull;
+          *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, (u32)rp, (u32)(rp >> 32));
+          for (u32 c = 0; c < C; ++c) reinterpret_cast<u64*>(rw + 16)[c] = st.cons[(u64)p * C + c];
+          st.cdirty[p] = 0u;
+        }
       }
     }
+    if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(3);  // and pass 2
     if (tid == 0) {
       u32* h = reinterpret_cast<u32*>(X.outbox + base);
       h[0] = kXMagic;
@@ -722,8 +744,6 @@ __device__ void stage2_plan(const PipeArgs& A) {
     __syncthreads();
   }
   __syncthreads();
-  // consumer-offset rows travel once per change: clear the flags of every planned partition
-  for (u32 e = tid; e < X.n_out; e += kPT) st.cdirty[X.xo_p[e]] = 0u;
   if (tid == 0) {
     X.xc_n[0] = (u32)s_cu[0];
     X.xc_n[1] = (u32)s_cu[1];
@@ -826,7 +846,7 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
   }
 }
 
-__device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
+__device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
   const u32 P = A.st.P, T = G.tiles, GT = A.gt;
@@ -900,7 +920,7 @@ __device__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
     if (s_last) stage2_plan(A);
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(2);
+  PIPE_STAMP(4);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1083,7 +1103,7 @@ __device__ __forceinline__ u32 piece_crc(const PipeArgs& A, const Stage3Smem& S,
 // l, l + 64, ... (kBU per lane in flight, the block after each from the neighbour lane), folds
 // them by Horner's rule with the 1 KB shift table, shifts its register past the pieces that follow
 // its last one and the wave XOR-reduces; lane 0 writes the header. xdst: the record's outbox copies.
-__device__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
+__device__ __forceinline__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
                            u64 off, u32 dead, uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx) {
   const u32 lane = threadIdx.x & 63, RF = A.st.RF;
   const u64 rstride = A.st.rstride;
@@ -1151,7 +1171,7 @@ __device__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*z
 // it with big_record. Their task waves leave these records to them (header and payload; the task
 // wave still writes the out offset, index entries, record-table slots and statistics).
 template <bool XR>
-__device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
+__device__ __forceinline__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
   const PipeGroup& G = A.g3;
   const PipeScratch& x = A.s3;
   const DevState& st = A.st;
@@ -1204,7 +1224,7 @@ __device__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& S, u32 wg) {
 }
 
 template <bool XR>
-__device__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
+__device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Smem& S, const TaskPos& T, const TaskRec& R,
                               const TaskState& Z, bool cand, uint4& stat_out) {
   const PipeBatch& b = A.g3.b[T.jb];
   const DevState& st = A.st;
@@ -1440,7 +1460,7 @@ __device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef
 //  * stage 4: retention after each batch of the group applied one launch earlier, for the
 //    partitions whose replay that launch stopped (rlate[p]; the batch aggregates are loaded only
 //    for them, so the common case carries no stage-4 loads).
-__device__ void partition_threads(const PipeArgs& A, u32 p) {
+__device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
   const DevState& st = A.st;
   const u32 RF = st.RF;
   const bool a3 = A.g3.nb != 0, a4 = A.g4.nb != 0;
@@ -1515,7 +1535,7 @@ __device__ void partition_threads(const PipeArgs& A, u32 p) {
 // that start in it. Round h-1's records are complete (the previous launch) and round h's stores
 // into the ring land past the gap's end minus the ring size (the plan's condition), so nothing
 // this reads changes under it.
-__device__ void stage3_catchup(const PipeArgs& A, u32 wg) {
+__device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
   const u32 items = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n + 1));
   const u32 ncu = __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile const u32*>(A.xc3_n));
   if (!items) return;

@@ -12,7 +12,8 @@ import numpy as np
 
 PHASES = {
     1: ["loads+input scans", "radix passes", "seg scan+writes"],
-    2: ["column scans+tile scan", "arrival + outbox plan (transport)"],
+    2: ["column scans+tile scan", "arrival + plan pass 1 (a destination)", "plan pass 2 (that destination)",
+        "rest of the plan (transport)"],
     3: ["first task r1+tables+r2 issue", "(earlier tasks)", "last task finish", "(unused)",
         "(unused)", "(unused)"],
     4: ["(unused)", "(unused)", "(unused)", "(unused)", "(unused)", "partition apply + retention"],
