@@ -612,6 +612,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
+  preload_fetch_kernels();
   CREATE_HIP(hipStreamCreateWithFlags(&e->copy_s, hipStreamNonBlocking));
   CREATE_HIP(hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming));
   CREATE_HIP(hipEventCreateWithFlags(&e->ev_fetch, hipEventDisableTiming));

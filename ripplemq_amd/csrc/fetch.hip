@@ -318,6 +318,14 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
 
 // ev[4]: start / end events of the two kernels, recorded by the dispatches themselves
 // (profiling: kernel time without the host's launch gaps), or null
+// Load the fetch kernels' code at engine creation (a process's first launch of a kernel otherwise
+// loads it: ~20 ms inside the first rmq_fetch, profiles/r03q_prof).
+void preload_fetch_kernels() {
+  hipFuncAttributes fa;
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_resolve_kernel));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel));
+}
+
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;

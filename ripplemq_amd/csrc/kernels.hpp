@@ -335,6 +335,7 @@ void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
+void preload_fetch_kernels();
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move

@@ -501,14 +501,14 @@ __device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos,
 // round (the state this launch's stage 3 reads plus the group it applies) and the group before's
 // bytes. e = ~0u: none (zeros).
 struct PlanIn {
-  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg;
+  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg, term;
   u32 p, fl;
 };
 __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
   const XPlanArgs& X = A.xp2;
   PlanIn v;
   v.p = p;
-  v.tot = v.f_off = v.f_pos = v.gap = v.t3 = v.leo = v.used = v.lastg = 0ull;
+  v.tot = v.f_off = v.f_pos = v.gap = v.t3 = v.leo = v.used = v.lastg = v.term = 0ull;
   v.fl = 0u;
   if (e != ~0u) {
     v.tot = load_sc1(&A.s2.totals[p]);
@@ -520,6 +520,7 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
     v.leo = A.cur.leo[p];
     v.used = A.cur.used[p];
     v.lastg = A.g3.nb ? 0ull : A.lastg[p];
+    v.term = A.st.term[p];
   }
   return v;
 }
@@ -535,7 +536,6 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
 __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
-  const u64* const totals = A.s2.totals;
   const u32 tid = threadIdx.x, C = X.C;
   const u64 dcap = X.dcap;
   __shared__ u64 s_w[kPW];
@@ -630,7 +630,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
         const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
         uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
         de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
-        const u64 term = st.term[p] | (rebase ? kTermRebase : 0ull);
+        const u64 term = cur.term | (rebase ? kTermRebase : 0ull);
         de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
         XEntry xe;
         xe.data_abs = kNoRound;
@@ -673,8 +673,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
       }
       // (row entries and the data section offset need the region totals: pass 2)
       if (in) X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
-      cur = nxt;
-      __syncthreads();
+      cur = nxt;  // (the scans' own barriers order every reuse of s_w)
     }
     if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(2);  // first destination: pass 1
     const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
