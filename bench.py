@@ -545,7 +545,10 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
                 "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
                 "frac": sent_max / t_max / 1e9 / (XGMI_LINK_GBS * (world - 1)),
                 "note": "round regions sent per GPU (records + record table + directories) over the timed "
-                        "region / the links to the job's other GPUs (one direction)"},
+                        "region / the links to the job's other GPUs (one direction)",
+                "rounds": x1["rounds"] - x0["rounds"],
+                "general_plans": x1["general_plans"] - x0["general_plans"],
+                "catchup_entries": x1["catchup_entries"] - x0["catchup_entries"]},
             "append_stats_last": st,
             "device": dev_name,
             "cu_count": cus,

@@ -182,6 +182,9 @@ typedef struct rmq_repl_stats {
   uint64_t bytes_ingested;
   uint64_t catchup_entries;    /* leader: entries that re-sent a follower's gap (FORMAT.md §9 catch-up) */
   uint64_t detached_plans;     /* leader: entry plans whose follower lies beyond the ring and no rebase point was complete (FORMAT.md §9) */
+  uint64_t general_plans;      /* leader: destination plans by the general path (a consumer-offset row or
+                                  a catch-up gap among the entries, or over 4,096 entries); the
+                                  steady-state plan covers the rest. A diagnostic of the round's cost */
 } rmq_repl_stats;
 
 typedef struct rmq_engine rmq_engine;

@@ -1509,7 +1509,7 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   const Replication* r = e->repl;
   HIP_TRY(hipSetDevice(e->device));
   HIP_TRY(hipStreamSynchronize(r->xchg_s));
-  uint64_t c[6];
+  uint64_t c[7];
   HIP_TRY(hipMemcpy(c, r->d_counters, sizeof c, hipMemcpyDeviceToHost));
   out->world = r->world;
   out->rank = r->rank;
@@ -1524,6 +1524,7 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   out->bytes_ingested = c[3];
   out->catchup_entries = c[4];
   out->detached_plans = c[5];
+  out->general_plans = c[6];
   return RMQ_OK;
 }
 

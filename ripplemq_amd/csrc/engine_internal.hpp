@@ -178,7 +178,7 @@ struct Replication {
   uint64_t* d_base = nullptr;    // [n_in][2] IngestArgs::base
   uint32_t* d_items = nullptr;   // [items_cap][2] follower copy work items
   uint32_t* d_nitems = nullptr;  // [1]
-  uint64_t* d_counters = nullptr;  // [6]: follower [0..4) (IngestArgs), leader [4..6) (XPlanArgs)
+  uint64_t* d_counters = nullptr;  // [7]: follower [0..4) (IngestArgs), leader [4..7) (XPlanArgs)
   uint64_t* d_lastg = nullptr;     // [P] record bytes / 16 of the last group applied (PipeArgs::lastg)
   // leader catch-up state per out entry (FORMAT.md §9 v3)
   uint64_t* d_xnext = nullptr;   // [n_out][2]

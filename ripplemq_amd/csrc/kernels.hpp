@@ -107,7 +107,7 @@ struct XPlanArgs {
   uint32_t* dirty;           // [P] consumer offsets changed since the last round (cleared by the plan)
   XCatch* xc;                // [n_out] catch-up list of the group
   uint32_t* xc_n;            // [2] {catch-up entries, copy items}
-  uint64_t* counters;        // [2] leader: catch-up entries planned, detached entry plans
+  uint64_t* counters;        // [3] leader: catch-up entries planned, detached entry plans, general plans
   uint64_t dcap;             // outbox bytes per destination: region d at d * dcap
 };
 

@@ -499,7 +499,10 @@ __device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos,
 // Inputs of out entry e (partition p) to the plan: the group's totals and the stage-2 verdict of
 // the entry (sc1: written by other workgroups of this launch), the leader's log end before the
 // round (the state this launch's stage 3 reads plus the group it applies) and the group before's
-// bytes. e = ~0u: none (zeros).
+// bytes. Every load is issued whatever e is (e clamped into the destination's list, p a valid
+// partition): a path without them would make the compiler's counted wait for the prefetched entry
+// a wait for all memory operations. The caller ignores the values of an entry past the list, and
+// selects t3 / lastg by A.g3.nb where it uses them.
 struct PlanIn {
   u64 tot, f_off, f_pos, gap, t3, leo, used, lastg, term;
   u32 p, fl;
@@ -508,21 +511,129 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
   const XPlanArgs& X = A.xp2;
   PlanIn v;
   v.p = p;
-  v.tot = v.f_off = v.f_pos = v.gap = v.t3 = v.leo = v.used = v.lastg = v.term = 0ull;
-  v.fl = 0u;
-  if (e != ~0u) {
-    v.tot = load_sc1(&A.s2.totals[p]);
-    v.f_off = load_sc1(&X.xdec[e].f_off);
-    v.f_pos = load_sc1(&X.xdec[e].f_pos);
-    v.gap = load_sc1(&X.xdec[e].gap);
-    v.fl = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
-    v.t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
-    v.leo = A.cur.leo[p];
-    v.used = A.cur.used[p];
-    v.lastg = A.g3.nb ? 0ull : A.lastg[p];
-    v.term = A.st.term[p];
-  }
+  v.tot = load_sc1(&A.s2.totals[p]);
+  v.f_off = load_sc1(&X.xdec[e].f_off);
+  v.f_pos = load_sc1(&X.xdec[e].f_pos);
+  v.gap = load_sc1(&X.xdec[e].gap);
+  v.fl = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
+  v.t3 = (A.g3.nb ? A.s3.totals : A.cur.used)[p];
+  v.leo = A.cur.leo[p];
+  v.used = A.cur.used[p];
+  v.lastg = A.lastg[p];
+  v.term = A.st.term[p];
   return v;
+}
+
+// Steady-state plan of one destination (FORMAT.md §9 v3): no entry has a consumer-offset row or a
+// catch-up gap (the destination's dflag is clear), so each entry carries its round's records only,
+// its first record is the leader's log end B, and its table slots and data pieces are the exclusive
+// prefix of the round totals (scan A of the general plan: va = the totals word itself). Every entry
+// is planned in at most kFS sweeps of kFK rows: row k of sweep s = entries e0 + (s kFK + k) kPT +
+// tid, a sweep's loads issued together (partitions, then totals, then the log ends and terms of four
+// rows at a time), one block scan per row (s_f: kPW words), the data section offsets stored once
+// the destination's record count is known (no second pass over the entries' words). Returns the
+// destination's totals word (records << 40 | 16-byte units), as the general plan's run_a.
+constexpr u32 kFK = 8;  // rows per sweep
+// sweeps: a destination of up to kFS kFK kPT entries (the entries' data pieces wait in LDS)
+constexpr u32 kFS = (u32)((kSmemBytes - kPW * sizeof(u64)) / (sizeof(u32) * kFK * kPT));
+static_assert(kFS >= 2, "the steady plan covers two sweeps");
+static_assert(sizeof(XEntry) == 32 && offsetof(XEntry, k) == 24 && offsetof(XEntry, data_start16) == 28,
+              "plan_steady stores XEntry words");
+// (diagnostic, RMQ_STAMPS: event i of the first destination's steady plan in wave i / 3's slot 5 + i % 3)
+#define PLAN_STAMP(i)                                                                      \
+  do {                                                                                     \
+    if (stamp && threadIdx.x == 0)                                                         \
+      A.stamps[((u64)blockIdx.x * kPW + (i) / 3) * 8 + 5 + (i) % 3] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+__device__ __forceinline__ u64 plan_steady(const PipeArgs& A, u32 e0, u32 e1, u64 base, u64 tab, u64* s_f, bool stamp) {
+  const XPlanArgs& X = A.xp2;
+  const u32 tid = threadIdx.x;
+  const u32 el = e1 - 1u;
+  // s_f: the scans' wave totals, then the entries' data pieces before them (by sweep, row, thread)
+  u32* s_dk = reinterpret_cast<u32*>(s_f + kPW);
+  u64 run = 0;
+#pragma unroll 1
+  for (u32 sw = 0; sw < kFS; ++sw) {
+    const u32 b0 = e0 + sw * kFK * kPT;
+    if (b0 > el) break;
+    const bool st1 = stamp && sw == 0;
+    if (st1) PLAN_STAMP(0);
+    u32 pk[kFK];
+    u64 tk[kFK];
+#pragma unroll
+    for (u32 k = 0; k < kFK; ++k) pk[k] = X.xo_p[min(b0 + k * kPT + tid, el)];
+#pragma unroll
+    for (u32 k = 0; k < kFK; ++k) tk[k] = load_sc1(&A.s2.totals[pk[k]]);
+    if (st1) PLAN_STAMP(1);
+    // row by row (the scans' barriers are cheap next to the loads): the entries' slots and pieces,
+    // directory words 0-1 and 4-5, the stage-3 placement but for the data section offset
+#pragma unroll
+    for (u32 k = 0; k < kFK; ++k) {
+      const u32 e = b0 + k * kPT + tid;
+      if (e > el) tk[k] = 0ull;
+      u64 tot;
+      const u64 x = run + block_incl_scan_u64(tk[k], s_f, &tot) - tk[k];
+      run += tot;
+      if (st1 && k == 0) PLAN_STAMP(2);
+      const u64 t_ex = x >> 40, d_ex = x & kLow40;
+      s_dk[(sw * kFK + k) * kPT + tid] = (u32)d_ex;  // (a region is far below 64 GiB)
+      if (e <= el) {
+        const u64 dir = base + kRegionHdr + (u64)kDirEntry * (e - e0);
+        uint2* de = reinterpret_cast<uint2*>(X.outbox + dir);
+        de[0] = make_uint2((u32)(tk[k] >> 40), (u32)(tk[k] & kLow40));
+        de[2] = make_uint2((u32)t_ex, (u32)d_ex);
+        u64* xe = reinterpret_cast<u64*>(&X.xe[e]);
+        xe[1] = tab + 8ull * t_ex;
+        xe[2] = dir;
+        xe[3] = (u64)(e - e0) | (d_ex << 32);
+      }
+    }
+    if (st1) PLAN_STAMP(3);
+    // the leader's log end and term (directory words 2-3 and 6-7), the next expected follower end
+#pragma unroll
+    for (u32 h = 0; h < kFK; h += 4) {  // four rows' inputs in flight together
+      u32 fl[4];
+      u64 t3[4], leo[4], used[4], term[4];
+#pragma unroll
+      for (u32 j = 0; j < 4; ++j) {
+        const u32 p = pk[h + j], e = min(b0 + (h + j) * kPT + tid, el);
+        fl[j] = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
+        t3[j] = (A.g3.nb ? A.s3.totals : A.cur.used)[p];
+        leo[j] = A.cur.leo[p];
+        used[j] = A.cur.used[p];
+        term[j] = A.st.term[p];
+      }
+#pragma unroll
+      for (u32 j = 0; j < 4; ++j) {
+        const u32 e = b0 + (h + j) * kPT + tid;
+        if (e > el) continue;
+        const u64 t3v = A.g3.nb ? t3[j] : 0ull;
+        const u64 Boff = leo[j] + (t3v >> 40), Bpos = used[j] + 16ull * (t3v & kLow40);
+        uint2* de = reinterpret_cast<uint2*>(X.outbox + base + kRegionHdr + (u64)kDirEntry * (e - e0));
+        de[1] = make_uint2((u32)Boff, (u32)(Boff >> 32));
+        de[3] = make_uint2((u32)term[j], (u32)(term[j] >> 32));
+        if (fl[j] & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
+        X.xnext[2 * e] = Boff + (tk[h + j] >> 40);
+        X.xnext[2 * e + 1] = Bpos + 16ull * (tk[h + j] & kLow40);
+        if (fl[j] & kDecNewReq) {  // (a new request sets kDecRow: not in a steady destination)
+          X.xreq[4 * e] = load_sc1(&X.xdec[e].r_off);
+          X.xreq[4 * e + 1] = load_sc1(&X.xdec[e].r_pos);
+          X.xreq[4 * e + 2] = X.acks_round + 1ull;
+        }
+        X.xdec[e].pad = 0u;
+      }
+      if (st1) PLAN_STAMP(4 + h / 4);
+    }
+  }
+  if (stamp) PLAN_STAMP(6);
+  const u64 data = tab + ((8ull * (run >> 40) + 15ull) & ~15ull);
+  for (u32 i = tid; i <= el - e0; i += kPT) X.xe[e0 + i].data_abs = data + 16ull * s_dk[i];  // (own writes)
+  if (stamp) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PLAN_STAMP(7);
+  }
+  __syncthreads();  // s_f / s_dk free for the next destination
+  return run;
 }
 
 // The group's outbox layout (FORMAT.md §9 v3), one workgroup: destination d's region sits at
@@ -533,7 +644,7 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
 // (the gap, then the round's own), where stage 3 puts the round's records and table slots, the
 // catch-up list for the stage-3 launch's copy waves, the consumer-offset row, the next expected
 // follower log end.
-__device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
+__device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
   const XPlanArgs& X = A.xp2;
   const DevState& st = A.st;
   const u32 tid = threadIdx.x, C = X.C;
@@ -551,169 +662,192 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A) {
     const u32 df = __hip_atomic_load(&X.dflag[dd], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const u64 n = e1 - e0, base = (u64)dd * dcap;
     const u64 tab = base + kRegionHdr + kDirEntry * n;
-    // pass 1: record counts (for the table size) need the grants, which need the gap prefix. The
-    // inputs of the thread's next entry are loaded while this one is planned (and the partition of
-    // the one after), so an iteration waits on barriers and scans, not on memory.
-    u64 gap_run = 0, run_a = 0, run_b = 0;
-    PlanIn cur = plan_in(A, e0 + tid < e1 ? e0 + tid : ~0u, e0 + tid < e1 ? X.xo_p[e0 + tid] : 0u);
-    u32 p_next = e0 + kPT + tid < e1 ? X.xo_p[e0 + kPT + tid] : 0u;
-    for (u32 c0 = e0; c0 < e1; c0 += kPT) {
-      const u32 e = c0 + tid;
-      const bool in = e < e1;
-      const PlanIn nxt = plan_in(A, e + kPT < e1 ? e + kPT : ~0u, p_next);
-      p_next = e + 2 * kPT < e1 ? X.xo_p[e + 2 * kPT] : 0u;
-      const u32 p = cur.p, fl = cur.fl;
-      const u64 tot = cur.tot, f_off = cur.f_off, f_pos = cur.f_pos, gap = cur.gap;
-      u64 gex = 0;
-      if (df & kDecGapped) {
-        u64 gt;
-        gex = gap_run + block_incl_scan_u64(gap, s_w, &gt) - gap;
-        gap_run += gt;
-      }
-      // the entry's verdict: normal / full catch-up / partial / stopped (round records only)
-      const u64 rcnt = tot >> 40, rb16 = tot & kLow40;
-      u64 cnt = rcnt, b16 = rb16, gcnt = 0, gb16 = 0, first = f_off;
-      u64 nx_off = 0, nx_pos = 0;
-      bool with_round = true, set_cu = false, cu_entry = false;
-      const u64 t3 = cur.t3;
-      const u64 Boff = in ? cur.leo + (t3 >> 40) : 0ull;
-      const u64 Bpos = in ? cur.used + 16ull * (t3 & kLow40) : 0ull;
-      const u64 Cpos = !in ? 0ull : A.g3.nb ? cur.used : Bpos - 16ull * cur.lastg;  // as plan_decide
-      if (in) {
-        nx_off = Boff + rcnt;
-        nx_pos = Bpos + 16ull * rb16;
-        set_cu = (fl & kDecReq) && !(fl & (kDecGapped | kDecDetached));
-        if (fl & kDecGapped) {
-          if (gex + gap <= X.reserve) {
-            gcnt = Boff - f_off;
-            gb16 = gap >> 4;
-            cnt += gcnt;
-            b16 += gb16;
-            set_cu = cu_entry = true;
-          } else if (gex <= X.reserve) {  // the first entry past the reserve: a prefix of its gap
-            u64 xo = 0, xp = 0;
-            if (partial_end(st, p, f_pos, f_pos + (X.reserve - gex), Cpos, &xo, &xp)) {
-              gcnt = cnt = xo - f_off;
-              gb16 = b16 = (xp - f_pos) >> 4;
-              with_round = false;
-              nx_off = xo;
-              nx_pos = xp;
+    const bool first_dd = dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u);
+    u64 run_a = 0, run_b = 0;
+    if (!df && n <= (u64)kFS * kFK * kPT) {
+      run_a = plan_steady(A, e0, e1, base, tab, s_f, A.stamps && first_dd);
+      if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (first_dd) PIPE_STAMP(2);
+      if (first_dd) PIPE_STAMP(3);
+    } else {
+      if (tid == 0) atomicAdd((unsigned long long*)&X.counters[2], 1ull);  // (rmq_repl_stats.general_plans)
+      // pass 1: record counts (for the table size) need the grants, which need the gap prefix. The
+      // inputs of the thread's next entry are loaded while this one is planned (and the partition of
+      // the one after), so an iteration waits on barriers and scans, not on memory.
+      u64 gap_run = 0;
+      const u32 el = e1 - 1u;  // entries past the list load the last one's inputs (ignored)
+      PlanIn cur = plan_in(A, min(e0 + tid, el), X.xo_p[min(e0 + tid, el)]);
+      u32 p_next = X.xo_p[min(e0 + kPT + tid, el)];
+      const bool st_dd = A.stamps && first_dd;
+      for (u32 c0 = e0; c0 < e1; c0 += kPT) {
+        const u32 e = c0 + tid;
+        const bool in = e < e1;
+        // (diagnostic: wave w stamps iteration w's start, scan A and end in its slots 5..7)
+        const bool st_it = st_dd && (c0 - e0) / kPT == (tid >> 6);
+        if (st_it) PIPE_STAMP(5);
+        const PlanIn nxt = plan_in(A, min(e + kPT, el), p_next);
+        p_next = X.xo_p[min(e + 2 * kPT, el)];
+        const u32 p = cur.p, fl = cur.fl;
+        const u64 tot = cur.tot, f_off = cur.f_off, f_pos = cur.f_pos, gap = in ? cur.gap : 0ull;
+        u64 gex = 0;
+        if (df & kDecGapped) {
+          u64 gt;
+          gex = gap_run + block_incl_scan_u64(gap, s_w, &gt) - gap;
+          gap_run += gt;
+        }
+        // the entry's verdict: normal / full catch-up / partial / stopped (round records only)
+        const u64 rcnt = tot >> 40, rb16 = tot & kLow40;
+        u64 cnt = rcnt, b16 = rb16, gcnt = 0, gb16 = 0, first = f_off;
+        u64 nx_off = 0, nx_pos = 0;
+        bool with_round = true, set_cu = false, cu_entry = false;
+        const u64 t3 = A.g3.nb ? cur.t3 : 0ull;
+        const u64 Boff = in ? cur.leo + (t3 >> 40) : 0ull;
+        const u64 Bpos = in ? cur.used + 16ull * (t3 & kLow40) : 0ull;
+        const u64 Cpos = !in ? 0ull : A.g3.nb ? cur.used : Bpos - 16ull * cur.lastg;  // as plan_decide
+        if (in) {
+          nx_off = Boff + rcnt;
+          nx_pos = Bpos + 16ull * rb16;
+          set_cu = (fl & kDecReq) && !(fl & (kDecGapped | kDecDetached));
+          if (fl & kDecGapped) {
+            if (gex + gap <= X.reserve) {
+              gcnt = Boff - f_off;
+              gb16 = gap >> 4;
+              cnt += gcnt;
+              b16 += gb16;
               set_cu = cu_entry = true;
+            } else if (gex <= X.reserve) {  // the first entry past the reserve: a prefix of its gap
+              u64 xo = 0, xp = 0;
+              if (partial_end(st, p, f_pos, f_pos + (X.reserve - gex), Cpos, &xo, &xp)) {
+                gcnt = cnt = xo - f_off;
+                gb16 = b16 = (xp - f_pos) >> 4;
+                with_round = false;
+                nx_off = xo;
+                nx_pos = xp;
+                set_cu = cu_entry = true;
+              }
             }
           }
+          if (!cu_entry) first = Boff;  // the round's records from B (refused by a follower behind B)
         }
-        if (!cu_entry) first = Boff;  // the round's records from B (refused by a follower behind B)
-      }
-      const bool row = in && (((fl & kDecRow) != 0u) || cu_entry);
-      const bool rebase = cu_entry && (fl & kDecRebase);  // granted: the follower's log restarts at F
-      // scan A: table slots and data pieces before the entry
-      const u64 va = in ? (cnt << 40) | b16 : 0ull;
-      u64 ta;
-      const u64 exa = run_a + block_incl_scan_u64(va, s_w, &ta) - va;
-      run_a += ta;
-      // scan B: rows, catch-up entries and their copy items before the entry
-      u64 items = 0;
-      if (cu_entry) {
-        const u32 ilog = st.interval_log2;
-        items = ((f_pos + 16ull * gb16 - 1ull) >> ilog) - (f_pos >> ilog) + 1ull;
-      }
-      const u64 vb = (row ? 1ull : 0ull) | (cu_entry ? 1ull << 20 : 0ull) | (items << 40);
-      u64 exb = 0;
-      if (df) {
-        u64 tb;
-        exb = run_b + block_incl_scan_u64(vb, s_w, &tb) - vb;
-        run_b += tb;
-      }
-      if (in) {
-        const u32 k = e - e0;
-        const u64 t_ex = exa >> 40, d_ex = exa & kLow40;
-        const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
-        uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
-        de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
-        const u64 term = cur.term | (rebase ? kTermRebase : 0ull);
-        de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
-        XEntry xe;
-        xe.data_abs = kNoRound;
-        xe.tab_abs = 0;
-        if (with_round) {
-          xe.data_abs = 0;  // data section offset, fixed below once the table size is known
-          xe.tab_abs = tab + 8ull * (t_ex + gcnt);
-        }
-        xe.dir_abs = dir;
-        xe.k = k;
-        xe.data_start16 = (u32)(d_ex + gb16);
-        X.xe[e] = xe;
+        const bool row = in && (((fl & kDecRow) != 0u) || cu_entry);
+        const bool rebase = cu_entry && (fl & kDecRebase);  // granted: the follower's log restarts at F
+        // scan A: table slots and data pieces before the entry
+        const u64 va = in ? (cnt << 40) | b16 : 0ull;
+        u64 ta;
+        const u64 exa = run_a + block_incl_scan_u64(va, s_w, &ta) - va;
+        run_a += ta;
+        if (st_it) PIPE_STAMP(6);
+        // scan B: rows, catch-up entries and their copy items before the entry
+        u64 items = 0;
         if (cu_entry) {
-          const u32 ci = (u32)(s_cu[0] + ((exb >> 20) & 0xFFFFFull));
-          XCatch xc;
-          xc.pos = f_pos;
-          xc.first = f_off;
-          xc.bytes = 16ull * gb16;
-          xc.data_abs = 0;  // fixed below
-          xc.tab_abs = tab + 8ull * t_ex;
-          xc.k = k;
-          xc.data_start16 = (u32)d_ex;
-          xc.p = p;
-          xc.items0 = (u32)(s_cu[1] + (exb >> 40));
-          xc.pad = 0;
-          X.xc[ci] = xc;
-          atomicAdd((unsigned long long*)&X.counters[0], 1ull);
+          const u32 ilog = st.interval_log2;
+          items = ((f_pos + 16ull * gb16 - 1ull) >> ilog) - (f_pos >> ilog) + 1ull;
         }
-        if (fl & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
-        // catch-up state (FORMAT.md §9): next expected follower log end, last catch-up round; a
-        // request that came with this launch's acks and was not served stays pending
-        X.xnext[2 * e] = nx_off;
-        X.xnext[2 * e + 1] = nx_pos;
-        if (set_cu) X.xcu[e] = X.round;
-        if ((fl & kDecNewReq) && !set_cu) {
-          X.xreq[4 * e] = load_sc1(&X.xdec[e].r_off);
-          X.xreq[4 * e + 1] = load_sc1(&X.xdec[e].r_pos);
-          X.xreq[4 * e + 2] = X.acks_round + 1ull;
+        const u64 vb = (row ? 1ull : 0ull) | (cu_entry ? 1ull << 20 : 0ull) | (items << 40);
+        u64 exb = 0;
+        if (df) {
+          u64 tb;
+          exb = run_b + block_incl_scan_u64(vb, s_w, &tb) - vb;
+          run_b += tb;
+        }
+        if (in) {
+          const u32 k = e - e0;
+          const u64 t_ex = exa >> 40, d_ex = exa & kLow40;
+          const u64 dir = base + kRegionHdr + (u64)kDirEntry * k;
+          uint4* de = reinterpret_cast<uint4*>(X.outbox + dir);
+          de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
+          const u64 term = cur.term | (rebase ? kTermRebase : 0ull);
+          de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
+          XEntry xe;
+          xe.data_abs = kNoRound;
+          xe.tab_abs = 0;
+          if (with_round) {
+            xe.data_abs = 0;  // data section offset, fixed below once the table size is known
+            xe.tab_abs = tab + 8ull * (t_ex + gcnt);
+          }
+          xe.dir_abs = dir;
+          xe.k = k;
+          xe.data_start16 = (u32)(d_ex + gb16);
+          X.xe[e] = xe;
+          if (cu_entry) {
+            const u32 ci = (u32)(s_cu[0] + ((exb >> 20) & 0xFFFFFull));
+            XCatch xc;
+            xc.pos = f_pos;
+            xc.first = f_off;
+            xc.bytes = 16ull * gb16;
+            xc.data_abs = 0;  // fixed below
+            xc.tab_abs = tab + 8ull * t_ex;
+            xc.k = k;
+            xc.data_start16 = (u32)d_ex;
+            xc.p = p;
+            xc.items0 = (u32)(s_cu[1] + (exb >> 40));
+            xc.pad = 0;
+            X.xc[ci] = xc;
+            atomicAdd((unsigned long long*)&X.counters[0], 1ull);
+          }
+          if (fl & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
+          // catch-up state (FORMAT.md §9): next expected follower log end, last catch-up round; a
+          // request that came with this launch's acks and was not served stays pending
+          X.xnext[2 * e] = nx_off;
+          X.xnext[2 * e + 1] = nx_pos;
+          if (set_cu) X.xcu[e] = X.round;
+          if ((fl & kDecNewReq) && !set_cu) {
+            X.xreq[4 * e] = load_sc1(&X.xdec[e].r_off);
+            X.xreq[4 * e + 1] = load_sc1(&X.xdec[e].r_pos);
+            X.xreq[4 * e + 2] = X.acks_round + 1ull;
+          }
+        }
+        // (row entries and the data section offset need the region totals: pass 2)
+        if (in) X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
+        if (st_it) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          PIPE_STAMP(7);
+        }
+        cur = nxt;  // (the scans' own barriers order every reuse of s_w)
+      }
+      if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(2);  // first destination: pass 1
+      const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
+      const u64 data = tab + ((8ull * N + 15ull) & ~15ull), rows = data + 16ull * B16;
+      const u64 rowb = 16ull + 8ull * C;
+      // pass 2: data offsets, rows (the entries' words of eight iterations loaded at once); a row's
+      // partition has its consumer offsets sent: its change flag is cleared
+      constexpr u32 kP2 = 8;
+      for (u32 e8 = e0 + tid; e8 < e1; e8 += kP2 * kPT) {
+        u64 da[kP2];
+        u32 ds[kP2], pad[kP2];
+#pragma unroll
+        for (u32 k = 0; k < kP2; ++k) {
+          const u32 e = e8 + k * kPT;
+          da[k] = kNoRound;
+          ds[k] = pad[k] = 0u;
+          if (e < e1) {
+            da[k] = X.xe[e].data_abs;
+            ds[k] = X.xe[e].data_start16;
+            pad[k] = X.xdec[e].pad;
+          }
+        }
+#pragma unroll
+        for (u32 k = 0; k < kP2; ++k) {
+          const u32 e = e8 + k * kPT;
+          if (e >= e1) continue;
+          if (da[k] != kNoRound) X.xe[e].data_abs = data + 16ull * ds[k];
+          const u32 ri = pad[k] & ~kRowRebase;
+          if (ri) {
+            const u32 p = X.xo_p[e];
+            uint8_t* rw = X.outbox + rows + rowb * (ri - 1u);
+            // a rebase entry's row carries the rebase point's position (FORMAT.md §9)
+            const u64 rp = (pad[k] & kRowRebase) ? load_sc1(&X.xdec[e].f_pos) : 0ull;
+            *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, (u32)rp, (u32)(rp >> 32));
+            for (u32 c = 0; c < C; ++c) reinterpret_cast<u64*>(rw + 16)[c] = st.cons[(u64)p * C + c];
+            st.cdirty[p] = 0u;
+          }
         }
       }
-      // (row entries and the data section offset need the region totals: pass 2)
-      if (in) X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
-      cur = nxt;  // (the scans' own barriers order every reuse of s_w)
+      if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(3);  // and pass 2
     }
-    if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(2);  // first destination: pass 1
-    const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
-    const u64 data = tab + ((8ull * N + 15ull) & ~15ull), rows = data + 16ull * B16;
+    const u64 N = run_a >> 40, M = run_b & 0xFFFFFull;
+    const u64 data = tab + ((8ull * N + 15ull) & ~15ull), rows = data + 16ull * (run_a & kLow40);
     const u64 rowb = 16ull + 8ull * C;
-    // pass 2: data offsets, rows (the entries' words of eight iterations loaded at once); a row's
-    // partition has its consumer offsets sent: its change flag is cleared
-    constexpr u32 kP2 = 8;
-    for (u32 e8 = e0 + tid; e8 < e1; e8 += kP2 * kPT) {
-      u64 da[kP2];
-      u32 ds[kP2], pad[kP2];
-#pragma unroll
-      for (u32 k = 0; k < kP2; ++k) {
-        const u32 e = e8 + k * kPT;
-        da[k] = kNoRound;
-        ds[k] = pad[k] = 0u;
-        if (e < e1) {
-          da[k] = X.xe[e].data_abs;
-          ds[k] = X.xe[e].data_start16;
-          pad[k] = X.xdec[e].pad;
-        }
-      }
-#pragma unroll
-      for (u32 k = 0; k < kP2; ++k) {
-        const u32 e = e8 + k * kPT;
-        if (e >= e1) continue;
-        if (da[k] != kNoRound) X.xe[e].data_abs = data + 16ull * ds[k];
-        const u32 ri = pad[k] & ~kRowRebase;
-        if (ri) {
-          const u32 p = X.xo_p[e];
-          uint8_t* rw = X.outbox + rows + rowb * (ri - 1u);
-          // a rebase entry's row carries the rebase point's position (FORMAT.md §9)
-          const u64 rp = (pad[k] & kRowRebase) ? load_sc1(&X.xdec[e].f_pos) : 0ull;
-          *reinterpret_cast<uint4*>(rw) = make_uint4(e - e0, 0u, (u32)rp, (u32)(rp >> 32));
-          for (u32 c = 0; c < C; ++c) reinterpret_cast<u64*>(rw + 16)[c] = st.cons[(u64)p * C + c];
-          st.cdirty[p] = 0u;
-        }
-      }
-    }
-    if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(3);  // and pass 2
     if (tid == 0) {
       u32* h = reinterpret_cast<u32*>(X.outbox + base);
       h[0] = kXMagic;
@@ -845,6 +979,7 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
   }
 }
 
+template <bool XR>
 __device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
@@ -906,7 +1041,7 @@ __device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(1);
-  if (A.xp2.n_out) {
+  if (XR && A.xp2.n_out) {
     // replication transport: the last stage-2 workgroup to finish lays out the group's outbox
     // (every storing wave drained, then one counter add per workgroup; the last adder reads the
     // sc1-stored totals with sc1 loads: MI355X_MICROARCH.md inter-workgroup visibility, row 1)
@@ -916,7 +1051,7 @@ __device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
     if (tid == 0)
       s_last = __hip_atomic_fetch_add(A.xp2.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.wg2 - 1u;
     __syncthreads();
-    if (s_last) stage2_plan(A);
+    if (s_last) stage2_plan(A, s_ex);  // (s_ex: the tile bases are written)
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(4);
@@ -1625,7 +1760,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     }
     wg -= A.wg1;
     if (wg < A.wg2) {
-      stage2(A, wg, reinterpret_cast<u64*>(smem_raw));
+      stage2<XR>(A, wg, reinterpret_cast<u64*>(smem_raw));
       return;
     }
     wg -= A.wg2;

@@ -214,7 +214,7 @@ int repl_attach(rmq_engine* e, Transport* t) {
     if (rc) return rc;
     HIP_TRY(hipHostMalloc((void**)&x.h_sizes, 4ull * kMaxWorld * 8, 0));
   }
-  int rc = dalloc(&r->d_counters, 6);
+  int rc = dalloc(&r->d_counters, 7);
   if (!rc) rc = dalloc(&r->d_lastg, e->cfg.num_partitions);
   if (rc) return rc;
   return repl_set_lists(e);
