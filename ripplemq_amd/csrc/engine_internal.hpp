@@ -185,6 +185,7 @@ struct Replication {
   uint64_t* d_xreq = nullptr;    // [n_out][4]
   uint64_t* d_xcu = nullptr;     // [n_out]
   XDecision* d_xdec = nullptr;   // [n_out]
+  uint64_t* d_xtot = nullptr;    // [n_out]
   uint32_t* d_dflag = nullptr;   // [world]
   uint64_t dcap = 0;             // outbox bytes per destination
   uint64_t reserve = 0;          // catch-up bytes per destination

@@ -101,6 +101,7 @@ struct XPlanArgs {
   uint64_t* xreq;            // [n_out][4] pending catch-up request {offset, pos, round + 1 (0 none), 0}
   uint64_t* xcu;             // [n_out] round of the last catch-up plan
   XDecision* xdec;           // [n_out] stage-2 workers -> plan
+  uint64_t* xtot;            // [n_out] the group's totals word of the entry's partition (workers -> plan)
   uint32_t* dflag;           // [world] kDecRow | kDecGapped of any entry to that destination
   const uint64_t* ackin;     // acks applied in this launch, [n_out][2], or null
   uint64_t acks_round;       // the round they answer

@@ -115,13 +115,25 @@ struct Stage3Smem {
 constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
 static_assert(kSmemBytes >= kMaxTiles * sizeof(u64), "stage 2's tile bases fit the dynamic LDS");
 
+// A 64-bit DPP move (both halves): lanes the row mask leaves out, and lanes whose source lies
+// outside their row, read 0.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ u64 dpp_u64(u64 v) {
+  const u32 lo = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)v, kCtrl, kRowMask, 0xf, true);
+  const u32 hi = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)(v >> 32), kCtrl, kRowMask, 0xf, true);
+  return ((u64)hi << 32) | lo;
+}
+
+// Inclusive wave64 scan in VALU cross-lane moves (no LDS round trips): Hillis-Steele inside each
+// row of 16 lanes (row_shr 1, 2, 4, 8), then row 1 / 3 take row 0 / 2's last lane (row_bcast:15)
+// and rows 2-3 the second row's last lane (row_bcast:31).
 __device__ __forceinline__ u64 wave_incl_scan_u64(u64 v) {
-  const u32 l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const u64 o = __shfl_up(v, d, 64);
-    if (l >= (u32)d) v += o;
-  }
+  v += dpp_u64<0x111, 0xf>(v);
+  v += dpp_u64<0x112, 0xf>(v);
+  v += dpp_u64<0x114, 0xf>(v);
+  v += dpp_u64<0x118, 0xf>(v);
+  v += dpp_u64<0x142, 0xa>(v);
+  v += dpp_u64<0x143, 0xc>(v);
   return v;
 }
 
@@ -463,11 +475,22 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
   store_sc1(&X.xdec[e].r_off, d.r_off);
   store_sc1(&X.xdec[e].r_pos, d.r_pos);
   store_sc1(reinterpret_cast<u64*>(&X.xdec[e].flags), (u64)d.flags);
-  if (d.flags & (kDecRow | kDecGapped)) {
-    u32 q = 0;
-    for (u32 k = 1; k < X.world; ++k) q += e >= X.xo_start[k] ? 1u : 0u;
+  u32 q = 0;
+  for (u32 k = 1; k < X.world; ++k) q += e >= X.xo_start[k] ? 1u : 0u;
+  if (d.flags & (kDecRow | kDecGapped))
     __hip_atomic_fetch_or(&X.dflag[q], d.flags & (kDecRow | kDecGapped), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+  if (d.flags & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
+  // the entry's words as the steady-state plan has them (its round's records from B, FORMAT.md §9):
+  // directory words 0, 1 and 3 and the next expected follower log end; the plan adds word 2 (the
+  // slots and pieces before the entry) and the placement. Stored through (sc1): a general plan of
+  // the destination stores every one of these words later in this launch, and its stores win.
+  u64* dw = reinterpret_cast<u64*>(X.outbox + (u64)q * X.dcap + kRegionHdr + (u64)kDirEntry * (e - X.xo_start[q]));
+  store_sc1(&X.xtot[e], tot);
+  store_sc1(dw, (tot >> 40) | ((tot & kLow40) << 32));
+  store_sc1(dw + 1, Boff);
+  store_sc1(dw + 3, st.term[p]);
+  store_sc1(&X.xnext[2 * e], Boff + (tot >> 40));
+  store_sc1(&X.xnext[2 * e + 1], Bpos + 16ull * (tot & kLow40));
 }
 
 // End of a partial catch-up (FORMAT.md §9): the largest sparse-index entry E[m] with
@@ -526,17 +549,15 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
 
 // Steady-state plan of one destination (FORMAT.md §9 v3): no entry has a consumer-offset row or a
 // catch-up gap (the destination's dflag is clear), so each entry carries its round's records only,
-// its first record is the leader's log end B, and its table slots and data pieces are the exclusive
-// prefix of the round totals (scan A of the general plan: va = the totals word itself). Every entry
-// is planned in at most kFS sweeps of kFK rows: row k of sweep s = entries e0 + (s kFK + k) kPT +
-// tid, a sweep's loads issued together (partitions, then totals, then the log ends and terms of four
-// rows at a time), one block scan per row (s_f: kPW words), the data section offsets stored once
-// the destination's record count is known (no second pass over the entries' words). Returns the
-// destination's totals word (records << 40 | 16-byte units), as the general plan's run_a.
-constexpr u32 kFK = 8;  // rows per sweep
-// sweeps: a destination of up to kFS kFK kPT entries (the entries' data pieces wait in LDS)
-constexpr u32 kFS = (u32)((kSmemBytes - kPW * sizeof(u64)) / (sizeof(u32) * kFK * kPT));
-static_assert(kFS >= 2, "the steady plan covers two sweeps");
+// from the leader's log end B; the stage-2 workers already stored its directory words 0, 1, 3 and
+// next expected follower end (plan_decide). What is left needs the exclusive prefix of the round
+// totals over the destination's entries (scan A of the general plan: va = the totals word): word 2
+// and the stage-3 placement. Row k = entries e0 + k kPT + tid (at most kFK rows), every row's
+// totals loaded at once, one block scan per row (s_f: kPW words), the entries' data pieces kept in
+// LDS until the destination's record count fixes the data section. Returns the destination's
+// totals word (records << 40 | 16-byte units), as the general plan's run_a.
+constexpr u32 kFK = 16;
+static_assert(kSmemBytes >= kPW * sizeof(u64) + sizeof(u32) * kFK * kPT, "the steady plan's LDS");
 static_assert(sizeof(XEntry) == 32 && offsetof(XEntry, k) == 24 && offsetof(XEntry, data_start16) == 28,
               "plan_steady stores XEntry words");
 // (diagnostic, RMQ_STAMPS: event i of the first destination's steady plan in wave i / 3's slot 5 + i % 3)
@@ -549,88 +570,38 @@ __device__ __forceinline__ u64 plan_steady(const PipeArgs& A, u32 e0, u32 e1, u6
   const XPlanArgs& X = A.xp2;
   const u32 tid = threadIdx.x;
   const u32 el = e1 - 1u;
-  // s_f: the scans' wave totals, then the entries' data pieces before them (by sweep, row, thread)
-  u32* s_dk = reinterpret_cast<u32*>(s_f + kPW);
+  u32* s_dk = reinterpret_cast<u32*>(s_f + kPW);  // the entries' data pieces before them
+  PLAN_STAMP(0);
+  u64 tk[kFK];
+#pragma unroll
+  for (u32 k = 0; k < kFK; ++k) tk[k] = load_sc1(&X.xtot[min(e0 + k * kPT + tid, el)]);
   u64 run = 0;
-#pragma unroll 1
-  for (u32 sw = 0; sw < kFS; ++sw) {
-    const u32 b0 = e0 + sw * kFK * kPT;
-    if (b0 > el) break;
-    const bool st1 = stamp && sw == 0;
-    if (st1) PLAN_STAMP(0);
-    u32 pk[kFK];
-    u64 tk[kFK];
 #pragma unroll
-    for (u32 k = 0; k < kFK; ++k) pk[k] = X.xo_p[min(b0 + k * kPT + tid, el)];
-#pragma unroll
-    for (u32 k = 0; k < kFK; ++k) tk[k] = load_sc1(&A.s2.totals[pk[k]]);
-    if (st1) PLAN_STAMP(1);
-    // row by row (the scans' barriers are cheap next to the loads): the entries' slots and pieces,
-    // directory words 0-1 and 4-5, the stage-3 placement but for the data section offset
-#pragma unroll
-    for (u32 k = 0; k < kFK; ++k) {
-      const u32 e = b0 + k * kPT + tid;
-      if (e > el) tk[k] = 0ull;
-      u64 tot;
-      const u64 x = run + block_incl_scan_u64(tk[k], s_f, &tot) - tk[k];
-      run += tot;
-      if (st1 && k == 0) PLAN_STAMP(2);
-      const u64 t_ex = x >> 40, d_ex = x & kLow40;
-      s_dk[(sw * kFK + k) * kPT + tid] = (u32)d_ex;  // (a region is far below 64 GiB)
-      if (e <= el) {
-        const u64 dir = base + kRegionHdr + (u64)kDirEntry * (e - e0);
-        uint2* de = reinterpret_cast<uint2*>(X.outbox + dir);
-        de[0] = make_uint2((u32)(tk[k] >> 40), (u32)(tk[k] & kLow40));
-        de[2] = make_uint2((u32)t_ex, (u32)d_ex);
-        u64* xe = reinterpret_cast<u64*>(&X.xe[e]);
-        xe[1] = tab + 8ull * t_ex;
-        xe[2] = dir;
-        xe[3] = (u64)(e - e0) | (d_ex << 32);
-      }
-    }
-    if (st1) PLAN_STAMP(3);
-    // the leader's log end and term (directory words 2-3 and 6-7), the next expected follower end
-#pragma unroll
-    for (u32 h = 0; h < kFK; h += 4) {  // four rows' inputs in flight together
-      u32 fl[4];
-      u64 t3[4], leo[4], used[4], term[4];
-#pragma unroll
-      for (u32 j = 0; j < 4; ++j) {
-        const u32 p = pk[h + j], e = min(b0 + (h + j) * kPT + tid, el);
-        fl[j] = (u32)load_sc1(reinterpret_cast<const u64*>(&X.xdec[e].flags));
-        t3[j] = (A.g3.nb ? A.s3.totals : A.cur.used)[p];
-        leo[j] = A.cur.leo[p];
-        used[j] = A.cur.used[p];
-        term[j] = A.st.term[p];
-      }
-#pragma unroll
-      for (u32 j = 0; j < 4; ++j) {
-        const u32 e = b0 + (h + j) * kPT + tid;
-        if (e > el) continue;
-        const u64 t3v = A.g3.nb ? t3[j] : 0ull;
-        const u64 Boff = leo[j] + (t3v >> 40), Bpos = used[j] + 16ull * (t3v & kLow40);
-        uint2* de = reinterpret_cast<uint2*>(X.outbox + base + kRegionHdr + (u64)kDirEntry * (e - e0));
-        de[1] = make_uint2((u32)Boff, (u32)(Boff >> 32));
-        de[3] = make_uint2((u32)term[j], (u32)(term[j] >> 32));
-        if (fl[j] & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
-        X.xnext[2 * e] = Boff + (tk[h + j] >> 40);
-        X.xnext[2 * e + 1] = Bpos + 16ull * (tk[h + j] & kLow40);
-        if (fl[j] & kDecNewReq) {  // (a new request sets kDecRow: not in a steady destination)
-          X.xreq[4 * e] = load_sc1(&X.xdec[e].r_off);
-          X.xreq[4 * e + 1] = load_sc1(&X.xdec[e].r_pos);
-          X.xreq[4 * e + 2] = X.acks_round + 1ull;
-        }
-        X.xdec[e].pad = 0u;
-      }
-      if (st1) PLAN_STAMP(4 + h / 4);
+  for (u32 k = 0; k < kFK; ++k) {
+    const u32 e = e0 + k * kPT + tid;
+    if (k * kPT > el - e0) break;  // (uniform)
+    const u64 t = e <= el ? tk[k] : 0ull;
+    u64 tot;
+    const u64 x = run + block_incl_scan_u64(t, s_f, &tot) - t;
+    run += tot;
+    if (k == 0) PLAN_STAMP(1);
+    const u64 t_ex = x >> 40, d_ex = x & kLow40;
+    if (e <= el) {
+      s_dk[e - e0] = (u32)d_ex;  // (a region is far below 64 GiB)
+      const u64 dir = base + kRegionHdr + (u64)kDirEntry * (e - e0);
+      reinterpret_cast<u64*>(X.outbox + dir)[2] = t_ex | (d_ex << 32);
+      u64* xe = reinterpret_cast<u64*>(&X.xe[e]);
+      xe[1] = tab + 8ull * t_ex;
+      xe[2] = dir;
+      xe[3] = (u64)(e - e0) | (d_ex << 32);
     }
   }
-  if (stamp) PLAN_STAMP(6);
+  PLAN_STAMP(2);
   const u64 data = tab + ((8ull * (run >> 40) + 15ull) & ~15ull);
   for (u32 i = tid; i <= el - e0; i += kPT) X.xe[e0 + i].data_abs = data + 16ull * s_dk[i];  // (own writes)
   if (stamp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PLAN_STAMP(7);
+    PLAN_STAMP(3);
   }
   __syncthreads();  // s_f / s_dk free for the next destination
   return run;
@@ -664,7 +635,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
     const u64 tab = base + kRegionHdr + kDirEntry * n;
     const bool first_dd = dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u);
     u64 run_a = 0, run_b = 0;
-    if (!df && n <= (u64)kFS * kFK * kPT) {
+    if (!df && n <= (u64)kFK * kPT) {
       run_a = plan_steady(A, e0, e1, base, tab, s_f, A.stamps && first_dd);
       if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (first_dd) PIPE_STAMP(2);
@@ -785,8 +756,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
             X.xc[ci] = xc;
             atomicAdd((unsigned long long*)&X.counters[0], 1ull);
           }
-          if (fl & kDecDetached) atomicAdd((unsigned long long*)&X.counters[1], 1ull);
-          // catch-up state (FORMAT.md §9): next expected follower log end, last catch-up round; a
+            // catch-up state (FORMAT.md §9): next expected follower log end, last catch-up round; a
           // request that came with this launch's acks and was not served stays pending
           X.xnext[2 * e] = nx_off;
           X.xnext[2 * e + 1] = nx_pos;

@@ -234,7 +234,7 @@ void repl_free(rmq_engine* e) {
   }
   void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot,
                   r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
-                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_dflag, r->d_lastg};
+                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_xtot, r->d_dflag, r->d_lastg};
   for (void* p : bufs)
     if (p) hipFree(p);
   if (r->xchg_s) hipStreamDestroy(r->xchg_s);
@@ -355,8 +355,11 @@ int repl_set_lists(rmq_engine* e) {
   if (!rc) rc = upload(&r->d_xcu, std::vector<uint64_t>(n_out, 0ull));
   if (!rc) rc = upload(&r->d_dflag, std::vector<uint32_t>(W, 0u));
   if (r->d_xdec) hipFree(r->d_xdec);
+  if (r->d_xtot) hipFree(r->d_xtot);
   r->d_xdec = nullptr;
+  r->d_xtot = nullptr;
   if (!rc) rc = dalloc(&r->d_xdec, n_out);
+  if (!rc) rc = dalloc(&r->d_xtot, n_out);
   if (rc) return rc;
   // round buffers (FORMAT.md §9 bounds): a record is at most 31 + L bytes in the log, sent once per
   // remote slot, plus an 8-byte table slot; the catch-up reserve of a destination is one such
@@ -425,6 +428,7 @@ void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const Gro
     a.xp2.xreq = r->d_xreq;
     a.xp2.xcu = r->d_xcu;
     a.xp2.xdec = r->d_xdec;
+    a.xp2.xtot = r->d_xtot;
     a.xp2.dflag = r->d_dflag;
     a.xp2.dirty = e->st.cdirty;
     a.xp2.xc = x.xc;

@@ -46,14 +46,13 @@ def main(path):
             print(f"   {n:>26s}: p10 {np.percentile(d, 10):7.2f} p50 {np.percentile(d, 50):7.2f} "
                   f"p90 {np.percentile(d, 90):7.2f} max {d.max():7.2f} us")
     # steady plan events (PLAN_STAMP): wave i / 3's slot 5 + i % 3, relative to event 0
-    names = ["sweep 0 start", "partitions+totals issued", "first scan done (totals in)", "slots stored",
-             "log ends (rows 0-3) stored", "log ends (rows 4-7) stored", "sweeps done", "data offsets drained"]
+    names = ["start", "first scan done (totals in)", "scans and stores issued", "stores drained"]
     r = a[(a[:, 2] == 2) & (a[:, 1] == 0)]
     for wg in r[:, 0]:
         it = a[(a[:, 0] == wg) & (a[:, 2] == 2)]
         it = it[np.argsort(it[:, 1])]
         ev = [it[i // 3, 3 + 5 + i % 3] if i // 3 < len(it) else 0 for i in range(len(names))]
-        if ev[0] > 0 and ev[7] > 0 and it[0, 3 + 2] > 0:
+        if ev[0] > 0 and ev[-1] > 0 and it[0, 3 + 2] > 0:
             print("   steady plan: " + ", ".join(f"{n} {(t - ev[0]) * 0.01:.2f}" for n, t in zip(names, ev)) + " us")
     # the plan workgroup (stage 2 with a pass-1 stamp): wave w's slots 5..7 = pass-1 iteration w's
     # start, scan A done, stores drained
