@@ -307,7 +307,7 @@ struct IngestArgs {
   const CrcConsts* crc;
   uint64_t* counters;        // [4] records ingested, entries refused (CRC), refused (log mismatch), bytes
 };
-constexpr uint64_t kCopyChunk = 64ull << 10;  // follower copy: region bytes per workgroup
+constexpr uint64_t kCopyChunk = 16ull << 10;  // follower copy: region bytes per workgroup
 
 // Acks of one round applied outside the pipeline (drain): thread per partition.
 struct AckApplyArgs {

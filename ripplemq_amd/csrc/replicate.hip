@@ -23,7 +23,7 @@
 //     the append pipeline never touches a partition it does not lead), a newer term, the index
 //     entries a truncation re-covers, retention once per round (FORMAT.md §4 rule) and the
 //     consumer-offset row; every entry acks {log end | status, position};
-//   ingest_copy (workgroup per 64 KiB of a region): the accepted entries' record bytes, whole
+//   ingest_copy (wave per 16 KiB of an entry): the accepted entries' record bytes, whole
 //     16-byte pieces, into the follower's replica ring at the leader's logical positions (pieces a
 //     later piece of the round overwrites are not stored). A refused entry writes nothing.
 #include "device_common.hpp"
@@ -37,7 +37,7 @@ constexpr u32 kIT = 512;           // threads per verify workgroup
 constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
 constexpr u32 kIR = 32;            // records per task
 constexpr u32 kBigIngest = 64;     // records over this many 16-byte pieces: the whole wave
-constexpr u32 kCT = 256;           // threads per copy workgroup
+constexpr u32 kCT = 64;            // threads per copy workgroup (one wave: many items resident per CU)
 
 struct RegionView {
   const uint8_t* base;
@@ -452,7 +452,9 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
 }
 
 // Accepted entries' record bytes into the follower's replica rings: workgroup per work item
-// {entry, 64 KiB chunk of its data}, 16-byte pieces, four in flight per thread.
+// {entry, 16 KiB chunk of its data}, 16-byte pieces, four in flight per thread. A work item is a
+// chain of dependent lookups before its first data load, so items are one wave each: up to 32 per
+// CU in flight.
 __global__ __launch_bounds__(kCT) void ingest_copy_kernel(IngestArgs A) {
   const u32 it = blockIdx.x;
   if (it >= *A.n_items) return;

@@ -141,7 +141,7 @@ int post_round(rmq_engine* e, uint32_t s) {
                  (unsigned long long)r->in_cap);
     return RMQ_EDEVICE;
   }
-  // copy work items: at most one per 64 KiB of received region bytes plus one per entry
+  // copy work items: at most one per 16 KiB of received region bytes plus one per entry
   const uint32_t items = (uint32_t)std::min<uint64_t>(r->items_cap, ro / kCopyChunk + W + r->xi_p.size());
   HIP_TRY(hipStreamWaitEvent(r->xchg_s, x.ev_s3, 0));
   for (uint32_t q = 0; q < W; ++q)  // rmq_fault_corrupt
