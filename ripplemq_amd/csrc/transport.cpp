@@ -66,35 +66,33 @@ class LocalTransport : public Transport {
       h.device[me] = device_;
     }
     if (!h.barrier()) return RMQ_EDEVICE;
-    // 2. receive: copy from every peer's send range once its stream posted it
-    for (uint32_t q = 0; q < W; ++q) {
-      if (q == me) continue;
-      if (h.sbytes[(size_t)q * W + me] != h.rbytes[(size_t)me * W + q]) {
-        std::fprintf(stderr, "ripplemq: local exchange size mismatch %u->%u: sent %llu, expected %llu\n", q, me,
-                     (unsigned long long)h.sbytes[(size_t)q * W + me], (unsigned long long)h.rbytes[(size_t)me * W + q]);
-        std::lock_guard<std::mutex> g(h.mu);
-        h.mismatch = true;
-        continue;
-      }
-      const uint64_t n = h.rbytes[(size_t)me * W + q];
+    // 2. every rank sees every posted size: a mismatch anywhere fails the exchange on all ranks
+    //    (no shared flag to reset), then copy from every peer's send range once its stream posted it
+    bool bad = false;
+    for (uint32_t q = 0; q < W; ++q)
+      for (uint32_t t = 0; t < W; ++t)
+        if (q != t && h.sbytes[(size_t)q * W + t] != h.rbytes[(size_t)t * W + q]) {
+          if (t == me)
+            std::fprintf(stderr, "ripplemq: local exchange size mismatch %u->%u: sent %llu, expected %llu\n", q, me,
+                         (unsigned long long)h.sbytes[(size_t)q * W + me],
+                         (unsigned long long)h.rbytes[(size_t)me * W + q]);
+          bad = true;
+        }
+    for (uint32_t q = 0; q < W && !bad; ++q) {
+      const uint64_t n = q == me ? 0 : h.rbytes[(size_t)me * W + q];
       if (!n) continue;
       if (hipStreamWaitEvent(s, h.posted[q], 0) != hipSuccess) return RMQ_EDEVICE;
       if (hipMemcpyPeerAsync(rbuf[q], device_, h.sbuf[(size_t)q * W + me], h.device[q], n, s) != hipSuccess)
         return RMQ_EDEVICE;
     }
     if (hipEventRecord(h.copied[me], s) != hipSuccess) return RMQ_EDEVICE;
+    // every rank has read the posted table and recorded its copies: a rank may post the next
+    // exchange from here (it records `posted` again, never `copied` before the next barrier)
     if (!h.barrier()) return RMQ_EDEVICE;
     // 3. our send buffers may be rewritten only after every receiver's copies
     for (uint32_t q = 0; q < W; ++q)
       if (q != me && h.sbytes[(size_t)me * W + q] && hipStreamWaitEvent(s, h.copied[q], 0) != hipSuccess)
         return RMQ_EDEVICE;
-    const bool bad = h.mismatch;
-    if (!h.barrier()) return RMQ_EDEVICE;  // nobody posts the next round before all read this one
-    if (me == 0) {
-      std::lock_guard<std::mutex> g(h.mu);
-      h.mismatch = false;
-    }
-    if (!h.barrier()) return RMQ_EDEVICE;
     return bad ? RMQ_EINVAL : RMQ_OK;
   }
 

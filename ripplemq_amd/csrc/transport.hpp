@@ -50,7 +50,6 @@ struct LocalHub {
   std::vector<int> device;        // [rank]
   std::vector<hipEvent_t> posted;  // [rank] sends ready
   std::vector<hipEvent_t> copied;  // [rank] its receives done (the senders' buffers are free again)
-  bool mismatch = false;
 };
 
 Transport* make_local_transport(LocalHub* hub, uint32_t rank, int device);
