@@ -101,30 +101,53 @@ __device__ __forceinline__ u32 pair_swap(u32 v) {
 // Scans
 // ---------------------------------------------------------------------------------------------
 
+// DPP moves (VALU cross-lane, no LDS round trip): lanes the row mask leaves out, and lanes whose
+// source lies outside their row, read 0. 64-bit values move as two halves.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ u32 dpp_mov(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xf, true);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ u64 dpp_mov(u64 v) {
+  return ((u64)dpp_mov<kCtrl, kRowMask>((u32)(v >> 32)) << 32) | dpp_mov<kCtrl, kRowMask>((u32)v);
+}
+
+// Lane l's value in every lane (l wave-uniform).
+__device__ __forceinline__ u64 bcast_u64(u64 v, u32 l) {
+  return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
+         (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
+}
+
+// Inclusive wave64 scan (u32 / u64): Hillis-Steele inside each row of 16 lanes (row_shr 1, 2, 4,
+// 8), then rows 1 / 3 take the last lane of rows 0 / 2 (row_bcast:15) and rows 2-3 the last lane of
+// row 1 (row_bcast:31).
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
-  const u32 l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    T o = __shfl_up(v, d, 64);
-    if (l >= (u32)d) v += o;
-  }
+  v += dpp_mov<0x111, 0xf>(v);
+  v += dpp_mov<0x112, 0xf>(v);
+  v += dpp_mov<0x114, 0xf>(v);
+  v += dpp_mov<0x118, 0xf>(v);
+  v += dpp_mov<0x142, 0xa>(v);
+  v += dpp_mov<0x143, 0xc>(v);
   return v;
 }
 
-// Segmented inclusive scan step helpers: pairs (flag, value). A set flag starts a new segment.
+// Segmented inclusive scan of pairs (flag, value), a set flag starting a new segment; the same
+// moves, each combining (f, v) with the pair before: v += v' unless f, f |= f'. flag ends as the
+// OR of the flags up to the lane.
+template <typename T>
+__device__ __forceinline__ void seg_step_(u32& flag, T& v, u32 of, T ov) {
+  if (!flag) v += ov;
+  flag |= of;
+}
 template <typename T>
 __device__ __forceinline__ void wave_seg_incl_scan(u32& flag, T& v) {
-  const u32 l = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    u32 of = __shfl_up(flag, d, 64);
-    T ov = __shfl_up(v, d, 64);
-    if (l >= (u32)d) {
-      if (!flag) v += ov;
-      flag |= of;
-    }
-  }
+  seg_step_(flag, v, dpp_mov<0x111, 0xf>(flag), dpp_mov<0x111, 0xf>(v));
+  seg_step_(flag, v, dpp_mov<0x112, 0xf>(flag), dpp_mov<0x112, 0xf>(v));
+  seg_step_(flag, v, dpp_mov<0x114, 0xf>(flag), dpp_mov<0x114, 0xf>(v));
+  seg_step_(flag, v, dpp_mov<0x118, 0xf>(flag), dpp_mov<0x118, 0xf>(v));
+  seg_step_(flag, v, dpp_mov<0x142, 0xa>(flag), dpp_mov<0x142, 0xa>(v));
+  seg_step_(flag, v, dpp_mov<0x143, 0xc>(flag), dpp_mov<0x143, 0xc>(v));
 }
 
 }  // namespace rmq

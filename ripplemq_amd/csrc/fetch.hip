@@ -210,11 +210,6 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
   }
 }
 
-__device__ __forceinline__ u64 lane64(u64 v, u32 l) {  // lane l's value, wave-uniform
-  return ((u64)(u32)__builtin_amdgcn_readlane((int)(v >> 32), (int)l) << 32) |
-         (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
-}
-
 constexpr u32 kGQ = 4;          // requests per gather wave
 constexpr u32 kGR = kFW * kGQ;  // requests per gather workgroup
 
@@ -264,16 +259,16 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
     bool small = true;
 #pragma unroll
     for (u32 q = 0; q < kGQ; ++q) {
-      const u64 nbr = lane64(q_nb, q), po = lane64(q_out, q);
+      const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);
       small = small && (!nbr || po + nbr > a.out_cap || (nbr >> 4) <= 128u);
     }
     if (small) {
       uint4 x[kGQ][2];
 #pragma unroll
       for (u32 q = 0; q < kGQ; ++q) {
-        const u64 nbr = lane64(q_nb, q), po = lane64(q_out, q);
+        const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);
         const bool sv = nbr && po + nbr <= a.out_cap;
-        const u64 pos0 = lane64(q_pos, q), rw = lane64(q_ring, q);
+        const u64 pos0 = bcast_u64(q_pos, q), rw = bcast_u64(q_ring, q);
         const uint8_t* ring = st.logs + (rw >> 6);
         const u64 mask = (1ull << (rw & 63ull)) - 1ull;
 #pragma unroll
@@ -284,7 +279,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
       }
 #pragma unroll
       for (u32 q = 0; q < kGQ; ++q) {
-        const u64 nbr = lane64(q_nb, q), po = lane64(q_out, q);
+        const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);
         const bool sv = nbr && po + nbr <= a.out_cap;
 #pragma unroll
         for (u32 h = 0; h < 2; ++h) {
@@ -296,9 +291,9 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
     }
   }
   for (u32 q = 0; q < kGQ; ++q) {
-    const u64 nbr = lane64(q_nb, q), pos0_out = lane64(q_out, q);
+    const u64 nbr = bcast_u64(q_nb, q), pos0_out = bcast_u64(q_out, q);
     if (!nbr || pos0_out + nbr > a.out_cap) continue;  // nothing, past the end, or not served
-    const u64 pos0 = lane64(q_pos, q), rw = lane64(q_ring, q);
+    const u64 pos0 = bcast_u64(q_pos, q), rw = bcast_u64(q_ring, q);
     const uint8_t* ring = st.logs + (rw >> 6);
     const u64 mask = (1ull << (rw & 63ull)) - 1ull;
     uint8_t* out = a.out + pos0_out;

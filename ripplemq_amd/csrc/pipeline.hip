@@ -115,27 +115,7 @@ struct Stage3Smem {
 constexpr size_t kSmemBytes = sizeof(Stage1Smem) > sizeof(Stage3Smem) ? sizeof(Stage1Smem) : sizeof(Stage3Smem);
 static_assert(kSmemBytes >= kMaxTiles * sizeof(u64), "stage 2's tile bases fit the dynamic LDS");
 
-// A 64-bit DPP move (both halves): lanes the row mask leaves out, and lanes whose source lies
-// outside their row, read 0.
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ u64 dpp_u64(u64 v) {
-  const u32 lo = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)v, kCtrl, kRowMask, 0xf, true);
-  const u32 hi = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)(v >> 32), kCtrl, kRowMask, 0xf, true);
-  return ((u64)hi << 32) | lo;
-}
-
-// Inclusive wave64 scan in VALU cross-lane moves (no LDS round trips): Hillis-Steele inside each
-// row of 16 lanes (row_shr 1, 2, 4, 8), then row 1 / 3 take row 0 / 2's last lane (row_bcast:15)
-// and rows 2-3 the second row's last lane (row_bcast:31).
-__device__ __forceinline__ u64 wave_incl_scan_u64(u64 v) {
-  v += dpp_u64<0x111, 0xf>(v);
-  v += dpp_u64<0x112, 0xf>(v);
-  v += dpp_u64<0x114, 0xf>(v);
-  v += dpp_u64<0x118, 0xf>(v);
-  v += dpp_u64<0x142, 0xa>(v);
-  v += dpp_u64<0x143, 0xc>(v);
-  return v;
-}
+__device__ __forceinline__ u64 wave_incl_scan_u64(u64 v) { return wave_incl_scan<u64>(v); }
 
 __device__ __forceinline__ u32 record_rs16(u32 L) {  // (16 + align16(L)) / 16 without overflow
   return (L >> 4) + ((L & 15u) ? 1u : 0u) + 1u;
@@ -239,10 +219,9 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
       const u64 v = lenv[r];
       const u64 inc = wave_incl_scan_u64(v);
       pre_r[r] = (u32)(carry + inc - v);
-      carry += __shfl(inc, 63, 64);
+      carry += bcast_u64(inc, 63);
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) inv_cnt += __shfl_xor(inv_cnt, d, 64);
+    inv_cnt = bcast_u64(wave_incl_scan(inv_cnt), 63);  // (the wave's sum)
     if (lane == 0) {
       S.wsum[w][0] = carry;
       S.wsum[w][1] = inv_cnt;
@@ -355,7 +334,7 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
     u64 v = val[r];
     wave_seg_incl_scan(head, v);
     if (!head) v += carry;
-    carry = __shfl(v, 63, 64);
+    carry = bcast_u64(v, 63);
     hb[r] = head | any_head;
     any_head |= __ballot(head) ? 1u : 0u;
     inc[r] = v;

@@ -73,6 +73,9 @@ def scenario(oracle_mod, world, rf, ppr, group, rounds, spec, seg=1 << 16, inter
                 assert stats[r]["rounds"] == rounds and stats[r]["refused_crc"] == 0, stats
                 assert stats[r]["refused_log"] == 0, stats
                 assert stats[r]["records_ingested"] == int(oras[r].counters()[0]), (stats, oras[r].counters())
+                # no consumer commits and no missed rounds: every destination took the steady plan,
+                # so the regions compared below are that path's output
+                assert stats[r]["general_plans"] == 0, stats
             for r in range(world):
                 def local_slots(p, r=r):
                     return [s for s in range(rf) if views[r].ranks[p][s] == r]
