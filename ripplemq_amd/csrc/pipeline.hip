@@ -881,12 +881,15 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
 #pragma unroll
       for (u32 k = 0; k < kCL; ++k) loc += (ta + k >= t0 && ta + k < t1) ? h[k] : 0ull;
       if (binv) loc = 0;
+      // inclusive scan over the column's 32 lanes (a half-wave): DPP row moves inside each row of
+      // 16, then rows 1 / 3 take the last lane of rows 0 / 2 (the half-waves never mix)
+      static_assert(kScanLanes == 32, "stage 2 column scans are half-wave DPP scans");
       u64 inc = loc;
-#pragma unroll
-      for (u32 d = 1; d < kScanLanes; d <<= 1) {
-        const u64 o = __shfl_up(inc, d, kScanLanes);
-        if (s >= d) inc += o;
-      }
+      inc += dpp_mov<0x111, 0xf>(inc);
+      inc += dpp_mov<0x112, 0xf>(inc);
+      inc += dpp_mov<0x114, 0xf>(inc);
+      inc += dpp_mov<0x118, 0xf>(inc);
+      inc += dpp_mov<0x142, 0xa>(inc);
       u64 run = carry + bsum + inc - loc;
 #pragma unroll
       for (u32 k = 0; k < kCL; ++k) {
@@ -896,7 +899,7 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
           if (!binv) run += h[k];
         }
       }
-      bsum += __shfl(inc, kScanLanes - 1, kScanLanes);
+      bsum += lane_id() < 32u ? bcast_u64(inc, 31) : bcast_u64(inc, 63);  // the half-wave's last lane
       if (t1 > C + kScanLanes * kCL) break;  // batch j goes on in the next chunk
       if (!binv) {
         if ((bsum & kLow40) > lim16) {
