@@ -132,6 +132,17 @@ __device__ __forceinline__ T wave_incl_scan(T v) {
   return v;
 }
 
+// XOR of every lane's value, in every lane (the same moves as a scan, then lane 63's value).
+__device__ __forceinline__ u32 wave_xor_all(u32 v) {
+  v ^= dpp_mov<0x111, 0xf>(v);
+  v ^= dpp_mov<0x112, 0xf>(v);
+  v ^= dpp_mov<0x114, 0xf>(v);
+  v ^= dpp_mov<0x118, 0xf>(v);
+  v ^= dpp_mov<0x142, 0xa>(v);
+  v ^= dpp_mov<0x143, 0xc>(v);
+  return (u32)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Segmented inclusive scan of pairs (flag, value), a set flag starting a new segment; the same
 // moves, each combining (f, v) with the pair before: v += v' unless f, f |= f'. flag ends as the
 // OR of the flags up to the lane.

@@ -185,8 +185,8 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
         ring_off = (u64)r0 * st.rstride + v.rg.base;
         v.ring = st.logs + ring_off;
         const u64 pp = record_pos2(st, p, v, off, end);
-        pos0 = __shfl(pp, 0, 64);
-        bytes = __shfl(pp, 32, 64) - pos0;
+        pos0 = bcast_u64(pp, 0);
+        bytes = bcast_u64(pp, 32) - pos0;
         count = end - off;
       }
     }
@@ -224,8 +224,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   u64 v = 0;
   for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[(u64)k * kCsumStride];
   for (u32 k = c0 * kFetchChunk + tid; k < r0; k += 64 * kFW) v += a.cpre[k];
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  v = bcast_u64(wave_incl_scan(v), 63);  // the wave's sum
   if (lane == 0) s_red[w] = v;
   // this workgroup's requests: exclusive scan of their bytes
   const u32 rr = r0 + tid;

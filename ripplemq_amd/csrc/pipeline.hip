@@ -1239,8 +1239,7 @@ __device__ __forceinline__ void big_record(const PipeArgs& A, const Stage3Smem& 
     const u32 e = (m - 1u - lane) & 63u;
     if (e) acc = gf2_mulmod(acc, A.crc->sh16[e]);
   }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) acc ^= (u32)__shfl_xor((int)acc, d, 64);
+  acc = wave_xor_all(acc);
   if (lane == 0) {
     const u32 pad = 16u * m - L;
     const u32 crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);

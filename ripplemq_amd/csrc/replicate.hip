@@ -184,10 +184,10 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
   }
   // the items' slots (their order does not matter): one counter add per wave
   const u32 inc = wave_incl_scan(nc);
-  const u32 tot = (u32)__shfl((int)inc, 63, 64);
+  const u32 tot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
   u32 at = 0;
   if (lane_id() == 0 && tot) at = atomicAdd(A.n_items, tot);
-  at = (u32)__shfl((int)at, 0, 64) + inc - nc;
+  at = (u32)__builtin_amdgcn_readlane((int)at, 0) + inc - nc;
   for (u32 c = 0; c < nc; ++c) {
     A.items[2 * (at + c)] = e;
     A.items[2 * (at + c) + 1] = c;
@@ -288,8 +288,7 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
       const u32 eb = (bm16 - 1u - lane) & 63u;
       if (eb) bacc = gf2_mulmod(bacc, A.crc->sh16[eb]);
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) bacc ^= (u32)__shfl_xor((int)bacc, d, 64);
+    bacc = wave_xor_all(bacc);
     if (lane == sl + 1u) acc = bacc;
   }
   if (ok && j == 1) {
