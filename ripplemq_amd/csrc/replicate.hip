@@ -187,10 +187,24 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
   const u32 tot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
   u32 at = 0;
   if (lane_id() == 0 && tot) at = atomicAdd(A.n_items, tot);
-  at = (u32)__builtin_amdgcn_readlane((int)at, 0) + inc - nc;
-  for (u32 c = 0; c < nc; ++c) {
-    A.items[2 * (at + c)] = e;
-    A.items[2 * (at + c) + 1] = c;
+  at = (u32)__builtin_amdgcn_readlane((int)at, 0);
+  // the wave writes its items together (an entry of many chunks would otherwise keep one lane
+  // busy): item i belongs to the lane whose inclusive count first exceeds i (all lanes take part
+  // in every shuffle)
+  for (u32 b = 0; b < tot; b += 64) {
+    const u32 i = b + lane_id();
+    u32 lo = 0;
+#pragma unroll
+    for (u32 step = 32; step; step >>= 1) {
+      const u32 v = (u32)__shfl((int)inc, (int)(lo + step - 1u), 64);
+      if (v <= i) lo += step;
+    }
+    const u32 own_inc = (u32)__shfl((int)inc, (int)lo, 64), own_nc = (u32)__shfl((int)nc, (int)lo, 64);
+    const u32 own_e = (u32)__shfl((int)e, (int)lo, 64);
+    if (i < tot) {
+      A.items[2 * (at + i)] = own_e;
+      A.items[2 * (at + i) + 1] = i - (own_inc - own_nc);
+    }
   }
 }
 
