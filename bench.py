@@ -542,9 +542,13 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
                          "batches_per_launch": n_applied / max(n_launch, 1)},
             "xgmi": None if world == 1 else {
                 "bytes_sent_per_gpu_max": sent_max, "achieved": sent_max / t_max / 1e9,
-                "peak": XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
-                "frac": sent_max / t_max / 1e9 / (XGMI_LINK_GBS * (world - 1)),
-                "note": "round regions sent per GPU (records + record table + directories) over the timed "
+                # the in-process transport copies inside one GPU: no link is measured
+                "peak": None if args.transport == "local" else XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
+                "frac": None if args.transport == "local" else sent_max / t_max / 1e9 / (XGMI_LINK_GBS * (world - 1)),
+                "note": ("round regions sent per rank (records + record table + directories) over the timed region; "
+                         "in-process transport: device copies on one GPU, not an xGMI rate")
+                        if args.transport == "local" else
+                        "round regions sent per GPU (records + record table + directories) over the timed "
                         "region / the links to the job's other GPUs (one direction)",
                 "rounds": x1["rounds"] - x0["rounds"],
                 "general_plans": x1["general_plans"] - x0["general_plans"],
