@@ -121,7 +121,8 @@ def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float, name: str
     cfg = EngineConfig(num_partitions=spec.partitions, replication_factor=rf, segment_bytes=seg,
                        index_interval=1024, max_batch_records=spec.records)
     distinct = [make_batch(spec, 10_000 + i) for i in range(8)]
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    host = host_cpus()
+    threads = host["usable"]
     recs1, t1, nb1 = 0, 0.0, 0
     with OracleEngine(cfg) as ora:
         while t1 < budget_s / 4 and nb1 < 200:
@@ -147,11 +148,41 @@ def cpu_baseline(spec: StreamSpec, rf: int, seg: int, budget_s: float, name: str
         tp = time.perf_counter() - t0
     assert all(st["appended"] == spec.records for _, st in res)
     return {"value": nb * spec.records / tp, "unit": "msgs/s", "cores": threads, "kind": "port",
-            "single_thread_value": rate1,
+            "single_thread_value": rate1, "single_thread_cores": 1,
+            "label": "C restatement of the reference semantics (oracle/ripple_oracle.c), not the Java broker",
+            "host": host,
             "sample": f"{nb} batches x {spec.records} records (config {name} stream, "
                       f"{spec.partitions} partitions, RF={rf}) through oracle/ripple_oracle.c "
-                      f"ro_append_sharded: partitions sharded over {threads} pinned threads, {tp:.2f} s; "
-                      f"1 thread (ro_append): {nb1} batches, {rate1 / 1e6:.2f} M msgs/s"}
+                      f"ro_append_sharded: partitions sharded over {threads} pinned threads (every CPU "
+                      f"this process may use), {tp:.2f} s; 1 thread (ro_append): {nb1} batches, "
+                      f"{rate1 / 1e6:.2f} M msgs/s"}
+
+
+def host_cpus() -> dict:
+    """The GPU box's host CPUs as the baseline sees them: model, nproc, the CPUs this process may run
+    on (affinity) and the cgroup CPU quota if one is set; `usable` = the CPUs a thread pool can keep
+    busy (the affinity set, capped by the quota)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(quota)) if quota else aff)
+    return {"model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "usable": usable}
 
 
 def host_leg(eng, batches, steps: int) -> dict:

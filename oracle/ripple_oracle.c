@@ -1170,19 +1170,66 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     free(v);
     return n && size ? RMQ_EINVAL : RMQ_OK;
   }
-  uint32_t h[4], mc[2];
-  uint64_t keysum, data, rows, want = 0;
-  memcpy(h, region, 16);
-  memcpy(&keysum, region + 16, 8);
-  memcpy(&data, region + 24, 8);
-  memcpy(&rows, region + 32, 8);
-  memcpy(mc, region + 40, 8);
-  for (uint32_t k = 0; k < n; ++k) want += v[k].key * RMQ_MAX_RF + v[k].slot;
-  if (size < RO_HDR || h[0] != RO_XMAGIC || h[1] != n || h[3] != src || keysum != want || mc[1] != C) {
-    free(v);
-    return RMQ_EINVAL;
+  uint32_t h[4] = {0, 0, 0, 0}, mc[2] = {0, 0};
+  uint64_t keysum = 0, data = 0, rows = 0, want = 0;
+  if (size >= RO_HDR) {
+    memcpy(h, region, 16);
+    memcpy(&keysum, region + 16, 8);
+    memcpy(&data, region + 24, 8);
+    memcpy(&rows, region + 32, 8);
+    memcpy(mc, region + 40, 8);
   }
+  for (uint32_t k = 0; k < n; ++k) want += v[k].key * RMQ_MAX_RF + v[k].slot;
   const uint64_t tab = RO_HDR + (uint64_t)RO_DIR * n, rowb = 16 + 8ull * C;
+  /* the header (FORMAT.md §9): a region that does not describe this pair's entry list, or whose
+     sections do not fit it, is unreadable: every entry refused (counted as log, like a missed round) */
+  if (size < RO_HDR || h[0] != RO_XMAGIC || h[1] != n || h[3] != src || keysum != want || mc[1] != C ||
+      data != tab + ((8ull * h[2] + 15) & ~15ull) || rows < data || rows > size || (rows - data) % 16 ||
+      mc[0] > n || (size - rows) / rowb < mc[0]) {
+    for (uint32_t k = 0; k < n; ++k) {
+      ack_of(&e->parts[v[k].p], 1, acks + 2 * k);
+      e->counters[2]++;
+    }
+    free(v);
+    return RMQ_OK;
+  }
+  /* structure (FORMAT.md §9): the directory entries tile the record table and the data section in
+     list order, every table slot names the entry whose range holds it, and the consumer-offset rows
+     name ascending entries. A region that breaks any of these was corrupted on the way: every entry
+     is refused (the leader's catch-up sends it again) */
+  int insane = 0;
+  {
+    uint64_t t = 0, d16 = 0;
+    for (uint32_t k = 0; k < n && !insane; ++k) {
+      const uint8_t* d = region + RO_HDR + (uint64_t)RO_DIR * k;
+      uint32_t cnt, by16, ts, ds;
+      memcpy(&cnt, d, 4);
+      memcpy(&by16, d + 4, 4);
+      memcpy(&ts, d + 16, 4);
+      memcpy(&ds, d + 20, 4);
+      insane = ts != t || ds != d16;
+      t += cnt;
+      d16 += by16;
+    }
+    if (t != h[2] || 16 * d16 != rows - data) insane = 1;
+    t = 0;
+    for (uint32_t k = 0; k < n && !insane; ++k) {
+      uint32_t cnt;
+      memcpy(&cnt, region + RO_HDR + (uint64_t)RO_DIR * k, 4);
+      for (uint32_t r = 0; r < cnt && !insane; ++r) {
+        uint32_t sk;
+        memcpy(&sk, region + tab + 8 * (t + r), 4);
+        insane = sk != k;
+      }
+      t += cnt;
+    }
+    for (uint32_t r = 0; r < mc[0] && !insane; ++r) {
+      uint32_t rk, pk = 0;
+      memcpy(&rk, region + rows + rowb * r, 4);
+      if (r) memcpy(&pk, region + rows + rowb * (r - 1), 4);
+      insane = rk >= n || (r && pk >= rk);
+    }
+  }
   /* pass 1: the verdict of every entry against the state every entry of a partition sees (the log
      end it continues, decided once by the owner: two local slots, the first keeps the state) */
   int* okv = (int*)malloc((size_t)n * sizeof(int));
@@ -1226,21 +1273,23 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     }
     base[2 * k] = leo;
     base[2 * k + 1] = used;
-    int ok = !stale && first == leo;
+    int ok = !stale && first == leo && !insane;
     uint64_t rel = 0;
     for (uint32_t r = 0; r < cnt && ok; ++r) {
       uint64_t slot, off;
       uint32_t len, crc;
       memcpy(&slot, region + tab + 8ull * (ts + r), 8);
       const uint8_t* rec = region + data + 16ull * (ds + rel / 16);
+      ok = (slot >> 32) == ds + rel / 16 && rel + 16 <= 16ull * by16;
+      if (!ok) break;
       memcpy(&off, rec, 8);
       memcpy(&len, rec + 8, 4);
       memcpy(&crc, rec + 12, 4);
-      ok = (uint32_t)slot == k && (slot >> 32) == ds + rel / 16 && off == first + r &&
-           rel + rec_size(len) <= 16ull * by16 && ro_crc32c(rec + 16, len) == crc;
+      ok = off == first + r && rel + rec_size(len) <= 16ull * by16 && ro_crc32c(rec + 16, len) == crc;
       for (uint64_t z = 16 + len; ok && z < rec_size(len); ++z) ok = rec[z] == 0; /* zero padding (§1) */
       rel += rec_size(len);
     }
+    if (ok && rel != 16ull * by16) ok = 0; /* the records fill the entry's bytes exactly */
     okv[k] = ok;
     if (!ok) e->counters[!stale && first == leo ? 1 : 2]++;
   }

@@ -168,6 +168,7 @@ struct Replication {
   uint32_t* d_xo_p = nullptr;
   uint32_t* d_xo_start = nullptr;
   uint64_t* d_keysum = nullptr;
+  uint64_t* d_keysum_in = nullptr;  // [world] key sums of the in lists (the follower's side)
   uint32_t* d_outidx = nullptr;  // [P][RF]
   uint32_t* d_xi_p = nullptr;
   uint32_t* d_xi_slot = nullptr;
@@ -177,7 +178,7 @@ struct Replication {
   uint32_t* d_acc = nullptr;     // [n_in]
   uint64_t* d_base = nullptr;    // [n_in][2] IngestArgs::base
   uint32_t* d_items = nullptr;   // [items_cap][2] follower copy work items
-  uint32_t* d_nitems = nullptr;  // [1]
+  uint32_t* d_nitems = nullptr;  // [1 + kMaxWorld]: copy items allocated, structural flag per source
   uint64_t* d_counters = nullptr;  // [7]: follower [0..4) (IngestArgs), leader [4..7) (XPlanArgs)
   uint64_t* d_lastg = nullptr;     // [P] record bytes / 16 of the last group applied (PipeArgs::lastg)
   // leader catch-up state per out entry (FORMAT.md §9 v3)

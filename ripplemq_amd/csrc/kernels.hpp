@@ -304,6 +304,11 @@ struct IngestArgs {
   uint64_t* ackout;          // [n_in][2] follower log end after the round | status (FORMAT.md §9)
   uint32_t* items;           // [cap][2] copy work items {entry, chunk of kCopyChunk bytes} (prepare)
   uint32_t* n_items;         // [1] items allocated this round (prepare adds, the host clears)
+  uint32_t* insane;          // [kMaxWorld] a structural fault of that source's region (prepare and
+                             //   verify set it, the host clears it with n_items)
+  const uint64_t* keysum_in; // [world] FORMAT.md §9 key sum of each source's entry list (this side's)
+  uint32_t items_cap;        // slots of `items`
+  uint32_t items_grid;       // copy workgroups launched: items past it are never copied
   const CrcConsts* crc;
   uint64_t* counters;        // [4] records ingested, entries refused (CRC), refused (log mismatch), bytes
 };

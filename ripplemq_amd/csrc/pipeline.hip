@@ -755,7 +755,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
         cur = nxt;  // (the scans' own barriers order every reuse of s_w)
       }
       if (dd == X.rank + 1u - (X.rank + 1u == X.world ? X.world : 0u)) PIPE_STAMP(2);  // first destination: pass 1
-      const u64 N = run_a >> 40, B16 = run_a & kLow40, M = run_b & 0xFFFFFull;
+      const u64 N = run_a >> 40, B16 = run_a & kLow40;
       const u64 data = tab + ((8ull * N + 15ull) & ~15ull), rows = data + 16ull * B16;
       const u64 rowb = 16ull + 8ull * C;
       // pass 2: data offsets, rows (the entries' words of eight iterations loaded at once); a row's

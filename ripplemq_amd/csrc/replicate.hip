@@ -47,19 +47,29 @@ struct RegionView {
 };
 
 // The region of source src in this round's inbox (FORMAT.md §9 header), checked against the
-// entry list both sides derive from the placement.
+// entry list both sides derive from the placement (count and key sum) and against its own size:
+// the sections lie where the format puts them, inside the region. A region failing this is
+// unreadable (every entry refused, like a missed round).
 __device__ __forceinline__ RegionView region_of(const IngestArgs& A, u32 src) {
   RegionView v;
   v.base = A.inbox + A.region[src];
+  const u64 size = A.rbytes[src];
+  v.sane = size >= kRegionHdr;
   const u32* h = reinterpret_cast<const u32*>(v.base);
-  v.n_entries = h[1];
-  v.n_records = h[2];
-  v.data_off = *reinterpret_cast<const u64*>(h + 6);
-  v.rows_off = *reinterpret_cast<const u64*>(h + 8);
-  v.M = h[10];
-  v.C = h[11];
-  v.sane = A.rbytes[src] >= kRegionHdr && h[0] == kXMagic && v.n_entries == A.xi_start[src + 1] - A.xi_start[src] &&
-           h[3] == src && v.C == A.C && v.rows_off <= A.rbytes[src];
+  v.n_entries = v.sane ? h[1] : 0u;
+  v.n_records = v.sane ? h[2] : 0u;
+  v.data_off = v.sane ? *reinterpret_cast<const u64*>(h + 6) : 0ull;
+  v.rows_off = v.sane ? *reinterpret_cast<const u64*>(h + 8) : 0ull;
+  v.M = v.sane ? h[10] : 0u;
+  v.C = v.sane ? h[11] : 0u;
+  if (v.sane) {
+    const u64 tab = kRegionHdr + (u64)kDirEntry * v.n_entries, rowb = 16ull + 8ull * A.C;
+    v.sane = h[0] == kXMagic && v.n_entries == A.xi_start[src + 1] - A.xi_start[src] && h[3] == src &&
+             *reinterpret_cast<const u64*>(h + 4) == A.keysum_in[src] && v.C == A.C &&
+             v.data_off == tab + ((8ull * v.n_records + 15ull) & ~15ull) && v.rows_off >= v.data_off &&
+             v.rows_off <= size && !((v.rows_off - v.data_off) & 15ull) && v.M <= v.n_entries &&
+             (size - v.rows_off) / rowb >= v.M;
+  }
   return v;
 }
 
@@ -142,6 +152,13 @@ __device__ u64 follower_pos(const DevState& st, u32 p, u32 slot, u64 t) {
 
 constexpr u32 kBadCrc = 1u, kBadLog = 2u, kBadStale = 4u, kBadMissed = 8u;
 
+// A structural fault of source src's region this round (FORMAT.md §9: directory entries that do
+// not tile the table and data sections, a table slot outside its entry, rows out of order): every
+// entry of the region is refused.
+__device__ __forceinline__ void mark_insane(const IngestArgs& A, u32 src) {
+  __hip_atomic_fetch_or(&A.insane[src], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ void ingest_prepare_kernel(IngestArgs A) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = e < A.n_in;
@@ -160,6 +177,21 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
         bad = kBadLog;
       } else {
         const DirView d = dir_of(R, k);
+        // the entry's slice of the table and of the data section ends where the next entry's
+        // starts (the last: at the section ends), the first starts at 0; rows ascend by entry
+        const bool last = k + 1u == R.n_entries;
+        const DirView dn = dir_of(R, last ? k : k + 1u);
+        const u64 t_end = last ? (u64)R.n_records : (u64)dn.tstart;
+        const u64 d_end = last ? (R.rows_off - R.data_off) >> 4 : (u64)dn.dstart16;
+        bool tiled = (u64)d.tstart + d.count == t_end && (u64)d.dstart16 + d.bytes16 == d_end;
+        if (k == 0) tiled = tiled && d.tstart == 0u && d.dstart16 == 0u;
+        if (k < R.M) {
+          const u64 rowb = 16ull + 8ull * A.C;
+          const u32 rk = *reinterpret_cast<const u32*>(R.base + R.rows_off + rowb * k);
+          const u32 pk = k ? *reinterpret_cast<const u32*>(R.base + R.rows_off + rowb * (k - 1u)) : 0u;
+          tiled = tiled && rk < R.n_entries && (k == 0 || pk < rk);
+        }
+        if (!tiled) mark_insane(A, src);
         if (d.term < st.term[p]) {
           bad = kBadStale;  // a stale leader
         } else if (d.rebase) {  // the log restarts at the entry's first record (its row: the position)
@@ -175,14 +207,18 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
           leo = d.first;
         }
         if (!bad && d.first != leo) bad = kBadLog;  // does not continue the follower's log
-        if (!bad) nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
+        if (!bad && !d.count && d.bytes16) bad = kBadCrc;  // bytes without records
+        // copy items only for an entry whose bytes tile the data section (so the items of a round
+        // stay within the host's bound: one per 16 KiB of received bytes plus one per entry)
+        if (!bad && tiled) nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
       }
     }
     A.bad[e] = bad;
     A.base[2 * e] = leo;
     A.base[2 * e + 1] = used;
   }
-  // the items' slots (their order does not matter): one counter add per wave
+  // the items' slots (their order does not matter): one counter add per wave; slots past the
+  // capacity are not written (only a corrupted region can ask for them: finish refuses the round)
   const u32 inc = wave_incl_scan(nc);
   const u32 tot = (u32)__builtin_amdgcn_readlane((int)inc, 63);
   u32 at = 0;
@@ -201,7 +237,7 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
     }
     const u32 own_inc = (u32)__shfl((int)inc, (int)lo, 64), own_nc = (u32)__shfl((int)nc, (int)lo, 64);
     const u32 own_e = (u32)__shfl((int)e, (int)lo, 64);
-    if (i < tot) {
+    if (i < tot && at + i < A.items_cap) {
       A.items[2 * (at + i)] = own_e;
       A.items[2 * (at + i) + 1] = i - (own_inc - own_nc);
     }
@@ -224,9 +260,15 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   const uint8_t* rec = R.base;
   uint4 hdr = make_uint4(0, 0, 0, 0);
   if (in) {
-    const u64 tab = *reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries + 8ull * i);
+    const u64* tabp = reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries) + i;
+    const u64 tab = tabp[0];
+    const u64 tabn = i + 1u < R.n_records ? tabp[1] : 0ull;  // the next slot (the record after, if any)
     const u32 k = min((u32)tab, R.n_entries - 1u), d16 = (u32)(tab >> 32);  // ok below requires k == tab
     const DirView d = dir_of(R, k);
+    // structure: the slot lies in the range of the entry it names (prepare checked that the ranges
+    // tile the table)
+    const bool named = k == (u32)tab && i >= d.tstart && (u64)i < (u64)d.tstart + d.count;
+    if (!named && j == 1) mark_insane(A, src);
     e = A.xi_start[src] + k;
     p = A.xi_p[e];
     owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
@@ -241,9 +283,16 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
       m = (L + 15u) >> 4;
     }
     pos = used + rel;
-    // the record continues the entry (its directory verdict is prepare's)
-    ok = k == (u32)tab && d16 >= d.dstart16 && off == d.first + (i - d.tstart) &&
-         rel + 16ull * (1ull + m) <= 16ull * d.bytes16 && A.bad[e] == 0u;
+    // the record continues the entry (its directory verdict is prepare's): its offset, inside the
+    // entry's bytes (which lie inside the data section), the first at the entry's start, each one
+    // where the one before ends and the last at the entry's end (FORMAT.md §9)
+    const u64 rend16 = (u64)d16 + 1ull + m;
+    const bool last = (u64)i + 1ull == (u64)d.tstart + d.count;
+    const bool chained = (i != d.tstart || d16 == d.dstart16) &&
+                         (last ? rend16 == (u64)d.dstart16 + d.bytes16 : (u64)(u32)(tabn >> 32) == rend16);
+    ok = named && d16 >= d.dstart16 && (u64)d.dstart16 + d.bytes16 <= (R.rows_off - R.data_off) >> 4 &&
+         off == d.first + (i - d.tstart) && rel + 16ull * (1ull + m) <= 16ull * d.bytes16 && chained &&
+         A.bad[e] == 0u;
     if (!ok && j == 1 && A.bad[e] == 0u) atomicOr(&A.bad[e], kBadCrc);  // the record's content is wrong
   }
   // CRC32C of the payload from its 16-byte pieces (zero-padded in the log): lane j folds pieces
@@ -368,9 +417,14 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
   const DevState& st = A.st;
   const u32 p = A.xi_p[e], k = e - A.xi_start[src];
   const bool owner = k == 0 || A.xi_p[e - 1] != p;
+  // a structurally broken region refuses all its entries; so does a round whose copy items
+  // overflowed (only corrupted regions ask for more than the host's bound: no entry may be
+  // accepted with bytes left uncopied)
+  const bool broken = __hip_atomic_load(&A.insane[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                      *A.n_items > A.items_grid;
   // two local slots of one partition (adjacent entries of the same source): a refusal of either
   // refuses both
-  const u32 own = A.bad[e];
+  const u32 own = A.bad[e] | (broken ? kBadCrc : 0u);
   u32 bad = own;
   for (u32 q = e; q > A.xi_start[src] && A.xi_p[q - 1] == p; --q) bad |= A.bad[q - 1];
   for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) bad |= A.bad[q];

@@ -168,9 +168,13 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.ackout = x.ackout;
   a.items = r->d_items;
   a.n_items = r->d_nitems;
+  a.insane = r->d_nitems + 1;
+  a.keysum_in = r->d_keysum_in;
+  a.items_cap = (uint32_t)r->items_cap;
+  a.items_grid = items;
   a.crc = e->d_crc;
   a.counters = r->d_counters;
-  HIP_TRY(hipMemsetAsync(r->d_nitems, 0, 4, r->xchg_s));
+  HIP_TRY(hipMemsetAsync(r->d_nitems, 0, 4ull * (1 + kMaxWorld), r->xchg_s));  // items, structural flags
   launch_ingest(a, tasks, items, e->verify_wgs, r->xchg_s);
   HIP_TRY(hipGetLastError());
   // acks: {log end | status, position} of every in entry back to its leader, fixed sizes both ways
@@ -232,7 +236,7 @@ void repl_free(rmq_engine* e) {
     if (x.count) hipFree(x.count);
     if (x.h_sizes) hipHostFree(x.h_sizes);
   }
-  void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_outidx, r->d_xi_p, r->d_xi_slot,
+  void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_keysum_in, r->d_outidx, r->d_xi_p, r->d_xi_slot,
                   r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
                   r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_xtot, r->d_dflag, r->d_lastg};
   for (void* p : bufs)
@@ -342,6 +346,7 @@ int repl_set_lists(rmq_engine* e) {
   if (!rc) rc = upload(&r->d_xo_slot, r->xo_slot);
   if (!rc) rc = upload(&r->d_xo_start, r->xo_start);
   if (!rc) rc = upload(&r->d_keysum, r->keysum);
+  if (!rc) rc = upload(&r->d_keysum_in, keysum_in);
   if (!rc) rc = upload(&r->d_outidx, outidx);
   if (!rc) rc = upload(&r->d_xi_p, r->xi_p);
   if (!rc) rc = upload(&r->d_xi_slot, r->xi_slot);
@@ -384,7 +389,7 @@ int repl_set_lists(rmq_engine* e) {
   r->d_items = nullptr;
   r->d_nitems = nullptr;
   rc = dalloc(&r->d_items, 2 * r->items_cap);
-  if (!rc) rc = dalloc(&r->d_nitems, 1);
+  if (!rc) rc = dalloc(&r->d_nitems, 1 + kMaxWorld);
   if (rc) return rc;
   free_set_buffers(r);
   for (XchgSet& x : r->sets) {

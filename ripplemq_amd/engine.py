@@ -84,6 +84,7 @@ class Engine:
         self._dbatch = A.RmqBatch(0, A.RMQ_MEM_DEVICE)
         self._dticket = C.c_uint64()
         self._dargs = (C.byref(self._dbatch), C.byref(self._dticket))
+        self.transport = False  # a replication transport is attached (rounds are collective)
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -116,10 +117,12 @@ class Engine:
 
     def attach_local(self, hub: "LocalHub") -> None:
         _check(self.lib.rmq_attach_local(self.h, hub.h), "rmq_attach_local")
+        self.transport = True
 
     def attach_rccl(self, comm_id: bytes, world: int) -> None:
         buf = (C.c_uint8 * 128).from_buffer_copy(comm_id)
         _check(self.lib.rmq_attach_rccl(self.h, buf, world), "rmq_attach_rccl")
+        self.transport = True
 
     def replication_stats(self) -> dict:
         st = A.RmqReplStats()
@@ -226,7 +229,11 @@ class Engine:
     def append(self, pidx, lens, payload, payload_off=None) -> tuple[np.ndarray, dict]:
         """Synchronous append: offsets and stats of the batch. With a replication transport the
         batch is applied only by a collective rmq_sync, so this raises RMQ_PENDING (keep the
-        ticket: append_async + sync + wait)."""
+        ticket: append_async + sync + wait). The check comes before anything is queued, so a caller
+        that retries after the error never appends the records twice."""
+        if self.transport:
+            raise EngineError(A.RMQ_PENDING, "rmq_append (transport attached: use append_async, then rmq_sync "
+                                             "on every rank applies it)")
         t, out = self.append_async(pidx, lens, payload, payload_off)
         stats = self.wait(t)
         if stats is None:

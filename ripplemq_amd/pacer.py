@@ -25,8 +25,8 @@ import time
 
 import numpy as np
 
-from .engine import EngineError
 from . import _abi as A
+from .engine import EngineError
 
 
 class RoundPacer:
@@ -42,6 +42,7 @@ class RoundPacer:
         self._lens: list[np.ndarray] = []
         self._pay: list[np.ndarray] = []
         self.tickets: list[tuple[int, np.ndarray, np.ndarray]] = []  # (ticket, pidx, out offsets)
+        self.rejected: list[tuple[np.ndarray, np.ndarray, dict | None]] = []  # batches with rejected records
 
     def submit(self, pidx, lens, payload) -> None:
         """Queue records for the next tick (any partitions this rank leads)."""
@@ -80,7 +81,11 @@ class RoundPacer:
     def committed(self) -> list[tuple[np.ndarray, np.ndarray]]:
         """The queued requests whose every record is committed (offset < commit index), oldest
         first, as (pidx, offsets); they leave the pending list. A batch is complete (its offsets
-        written) once rmq_poll_commit answers RMQ_OK for its ticket, which needs no flush."""
+        written) once rmq_poll_commit answers RMQ_OK for its ticket, which needs no flush.
+
+        A batch with rejected records (RMQ_OFFSET_NONE) leaves the list too and is reported in
+        ``self.rejected`` as (pidx, offsets, stats): its accepted records still commit, and the
+        requests queued behind it are not held up by it."""
         done = []
         if not self.tickets:
             return done
@@ -92,8 +97,13 @@ class RoundPacer:
             ok = out != np.uint64(A.RMQ_OFFSET_NONE)
             if np.any(ok & (out >= commit[pidx])):
                 break
-            if not np.all(ok):
-                raise EngineError(A.RMQ_ENOTLEADER, "pacer: records of a partition this rank does not lead")
-            done.append((pidx, out))
             self.tickets.pop(0)
+            if not np.all(ok):
+                try:
+                    stats = self.engine.wait(t)  # which rule rejected them (not leader, no space, ...)
+                except EngineError:
+                    stats = None  # older than the engine's stats ring
+                self.rejected.append((pidx, out, stats))
+                continue
+            done.append((pidx, out))
         return done

@@ -437,3 +437,30 @@ def test_idle_ranks_keep_rounds_flowing_gpu():
         for e in engs:
             e.close()
         hub.close()
+
+
+@pytest.mark.parametrize("what", ["keysum", "count", "bytes16", "first", "dstart16", "table_slot"])
+def test_corrupted_region_refused_gpu(oracle_mod, what):
+    # a flipped header / directory / record-table byte (rmq_fault_corrupt at >= 0) is
+    # refused by the follower ingest exactly as the oracle refuses it (whole region for a structural
+    # fault, one entry otherwise), nothing past the refused bytes is written, and the catch-up of
+    # the next rounds brings every follower back bit-exact with the oracle
+    from test_replication_oracle import REGION_FAULTS
+    world, rf, ppr = 3, 3, 6
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    n01 = sum(1 for p in range(ppr) for s in range(1, rf) if int(views[0].ranks[p][s]) == 1)
+    at = REGION_FAULTS[what]
+    if at is None:
+        at = 64 + 32 * n01 + 8 * 3 + 4
+    spec = StreamSpec(ppr, 500, "uniform", size=(1, 120), config_index=87)
+    res = synced_rounds(oracle_mod, world, rf, ppr, group=2, rounds=5, spec=spec,
+                        faults={1: {"corrupt": (0, 1, at)}})
+    try:
+        stats = res[3]
+        refused = stats[1]["refused_crc"] + stats[1]["refused_log"]
+        structural = what in ("keysum", "count", "bytes16", "dstart16")
+        assert refused == (n01 if structural else 1), (what, stats[1])
+        lead = [res[2][0].state(p) for p in range(ppr)]
+        assert all(min(s["match"]) == s["log_end_offset"] for s in lead)  # every follower caught up
+    finally:
+        _close(res)

@@ -358,3 +358,47 @@ def test_consumer_offsets_replicate_and_survive_leader_change(oracle_mod):
     finally:
         for o in oras:
             o.close()
+
+
+# Byte positions of a region (FORMAT.md §9) a corrupted link may flip: header key sum, directory
+# words of entry 1 (count, bytes/16, first offset, table start, data start/16), the record-table
+# slot of record 3 (its data position), and a payload byte of the last record.
+REGION_FAULTS = {"keysum": 16, "count": 64 + 32 + 0, "bytes16": 64 + 32 + 4, "first": 64 + 32 + 8,
+                 "tstart": 64 + 32 + 16, "dstart16": 64 + 32 + 20, "table_slot": None, "payload": -5}
+
+
+@pytest.mark.parametrize("what", sorted(REGION_FAULTS))
+def test_corrupted_region_refused_then_caught_up(oracle_mod, what):
+    # a flipped directory / header / table byte must never be accepted (a wrong count or
+    # byte total would move the follower's log end over bytes no record fills): the region's
+    # structure (entries tile the table and data sections, every slot inside its entry, the records
+    # filling each entry exactly) refuses it; catch-up heals it in the next rounds
+    world, ppr = 3, 4
+    views, oras = build(oracle_mod, world, ppr)
+    spec = StreamSpec(ppr, 200, "uniform", size=(1, 100), config_index=55)
+    n_entries = oras[0].pair_entries(0, 1)
+    at = REGION_FAULTS[what]
+    if at is None:
+        at = 64 + 32 * n_entries + 8 * 3 + 4
+    try:
+        def rnd(k, **kw):
+            for r in range(world):
+                b = rank_batches(spec, r, 5, 1)[k]
+                oras[r].append(b.pidx, b.lens, b.payload)
+            return exchange_round(oras, keep_regions=True, **kw)
+
+        rnd(0)
+        c1 = oras[1].counters().copy()
+        rnd(1, corrupt=(0, 1, at))
+        c = oras[1].counters()
+        refused = int(c[1] - c1[1] + c[2] - c1[2])
+        structural = what not in ("payload", "first", "table_slot")
+        assert refused == (n_entries if structural else 1), (what, c, c1)
+        if what == "keysum":  # unreadable header: every entry refused like a missed round
+            assert c[2] - c1[2] == n_entries
+        for k in (2, 3, 4):
+            rnd(k)
+        check_followers(views, oras, ppr, 3)
+    finally:
+        for o in oras:
+            o.close()
