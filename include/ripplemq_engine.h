@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 4u
+#define RMQ_ABI_VERSION 5u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -82,7 +82,9 @@ enum {
   RMQ_ENOSPC = -4,     /* batch larger than configured capacity / fetch output buffer too small */
   RMQ_EDEVICE = -5,    /* HIP runtime error or no HIP device */
   RMQ_EOFFSET = -6,    /* fetch offset below the retained log start (evicted by retention) */
-  RMQ_ENOMEM = -7
+  RMQ_ENOMEM = -7,
+  RMQ_ESTALE = -8      /* rmq_become_leader: this replica lacks records its partition's leader
+                          committed (Raft's vote restriction: it may not lead) */
 };
 
 /* Memory kind of caller buffers.
@@ -155,6 +157,10 @@ typedef struct rmq_partition_state {
   uint32_t leader_slot;
   uint32_t is_leader;
   uint64_t segment_bytes;      /* ring bytes of this partition (retention keeps at most this much) */
+  uint64_t leader_commit;      /* the newest commit index of the partition's leader this replica knows
+                                  (the Raft leaderCommit of the rounds and commit notices it received,
+                                  FORMAT.md §9); on the leader its own commit. A replica whose log
+                                  ends below it lacks committed records (rmq_become_leader: RMQ_ESTALE) */
 } rmq_partition_state;
 
 typedef struct rmq_append_stats {
@@ -286,6 +292,11 @@ int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uin
    appended after the call send empty regions, as if the leader failed before replicating them
    (its own log keeps the records; followers neither see nor ack them). Not collective. */
 int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n);
+/* Fault injection (tests): the regions of the next n rounds this engine sends to rank dst are lost
+   (launch groups formed from batches appended after the call), as a failed link to dst would lose
+   them: dst misses those rounds (every entry refused); its other peers and the commit notices of a
+   drain still reach it. Not collective. */
+int rmq_fault_isolate(rmq_engine* e, uint32_t dst, uint32_t n);
 /* Fault injection (tests): the next round this engine sends to rank dst has the byte at `at` of its
    region XORed with 0x5A (at < 0: counted back from the end of the region's data section, i.e. a
    payload byte of its last record), as a link or memory corruption would; the follower refuses the
@@ -294,6 +305,8 @@ int rmq_fault_corrupt(rmq_engine* e, uint32_t dst, int64_t at);
 
 /* ---- read-back (tests, tools) ---- */
 int rmq_get_partition_state(rmq_engine* e, uint32_t pidx, rmq_partition_state* out);
+/* The states of partitions [first, first + n) at once (one device copy per field). */
+int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_partition_state* out);
 /* Raw ring bytes [ring_off, ring_off + len) of replica slot `replica` of pidx. */
 int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t pidx, uint64_t ring_off,
                      uint64_t len, uint8_t* out);

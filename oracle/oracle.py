@@ -13,7 +13,7 @@ import subprocess
 import numpy as np
 
 from ripplemq_amd import _abi as A
-from ripplemq_amd.engine import FETCH_RES_DTYPE, EngineConfig, EngineError, state_to_dict
+from ripplemq_amd.engine import FETCH_RES_DTYPE, STATE_DTYPE, EngineConfig, EngineError, state_to_dict
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libripple_oracle.so")
@@ -46,6 +46,9 @@ def load() -> C.CDLL:
         "ro_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp]),
         "ro_fetch": (C.c_int, [vp, vp, u32, vp, u64, vp, C.POINTER(u64)]),
         "ro_get_partition_state": (C.c_int, [vp, u32, C.POINTER(A.RmqPartitionState)]),
+        "ro_get_partition_states": (C.c_int, [vp, u32, u32, vp]),
+        "ro_commit_notice": (C.c_int, [vp, u32, vp]),
+        "ro_apply_notice": (C.c_int, [vp, u32, vp, u32]),
         "ro_read_segment": (C.c_int, [vp, u32, u32, u64, u64, vp]),
         "ro_read_index": (C.c_int, [vp, u32, u64, u64, vp]),
         "ro_read_consumer_offsets": (C.c_int, [vp, u32, vp]),
@@ -147,6 +150,21 @@ class OracleEngine:
         if rc:
             raise EngineError(rc, "oracle ingest")
         return acks[:n]
+
+    def commit_notice(self, dst) -> np.ndarray:
+        """FORMAT.md §9 v4 commit notices for the pair (me -> dst): [n][2] {commit, term}."""
+        n = self.pair_entries(self.cfg.rank, dst)
+        out = np.zeros((max(n, 1), 2), np.uint64)
+        rc = self.lib.ro_commit_notice(self.h, dst, _p(out))
+        if rc:
+            raise EngineError(rc, "oracle commit_notice")
+        return out[:n]
+
+    def apply_notice(self, src, notices):
+        notices = np.ascontiguousarray(notices, np.uint64).reshape(-1, 2)
+        rc = self.lib.ro_apply_notice(self.h, src, _p(notices) if notices.size else None, len(notices))
+        if rc:
+            raise EngineError(rc, "oracle apply_notice")
 
     def apply_acks(self, dst, acks, round_no):
         acks = np.ascontiguousarray(acks, np.uint64).reshape(-1, 2)
@@ -250,6 +268,14 @@ class OracleEngine:
         if rc:
             raise EngineError(rc, "oracle")
         return state_to_dict(s, self.cfg.replication_factor)
+
+    def states(self, first=0, n=None):
+        n = self.cfg.num_partitions - first if n is None else n
+        out = np.zeros(n, STATE_DTYPE)
+        rc = self.lib.ro_get_partition_states(self.h, first, n, _p(out))
+        if rc:
+            raise EngineError(rc, "oracle")
+        return out
 
     def commit_snapshot(self):
         return np.array([self.state(p)["commit"] for p in range(self.cfg.num_partitions)], np.uint64)

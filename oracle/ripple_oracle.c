@@ -122,6 +122,7 @@ typedef struct {
   uint64_t nx_off[RMQ_MAX_RF], nx_pos[RMQ_MAX_RF];
   uint64_t rq_off[RMQ_MAX_RF], rq_pos[RMQ_MAX_RF], rq_r1[RMQ_MAX_RF], cu[RMQ_MAX_RF];
   uint8_t dirty; /* consumer offsets changed since the last round (the row travels with it) */
+  uint64_t lc;   /* follower: the newest leader commit learned (round entries, commit notices) */
 } ro_part;
 
 struct ro_engine {
@@ -246,7 +247,10 @@ static void ring_read(uint64_t S, const uint8_t* ring, uint64_t pos, uint8_t* ds
 }
 
 /* Raft quorum commit: N = k-th largest match, k = RF/2 + 1; commit moves to N only
-   if N > commit and the N-th record belongs to the current term (N > term_start). */
+   if N > commit and N >= term_start. The leader's term starts with a virtual entry at term_start
+   (jraft appends a configuration entry at leader start [jraft]); a replica holds it once its match
+   in the new term reaches term_start (match is reset at leader start), and a quorum holding it
+   commits every earlier-term record before it (Raft's current-term rule; FORMAT.md §6). */
 static void commit_eval(ro_engine* e, ro_part* s) {
   uint32_t RF = e->cfg.replication_factor, k = RF / 2 + 1;
   uint64_t m[RMQ_MAX_RF];
@@ -258,7 +262,7 @@ static void commit_eval(ro_engine* e, ro_part* s) {
       m[j - 1] = t;
     }
   uint64_t N = m[k - 1];
-  if (N > s->commit && N > s->term_start) s->commit = N;
+  if (N > s->commit && N >= s->term_start) s->commit = N;
   s->hw = s->commit;
 }
 
@@ -279,9 +283,11 @@ int ro_set_replicas(ro_engine* e, uint32_t p, const uint32_t* ranks, uint32_t rf
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   if (!ranks || rf != e->cfg.replication_factor || leader_slot >= rf) return RMQ_EINVAL;
   ro_part* s = &e->parts[p];
+  const uint32_t lead = ranks[leader_slot] == e->cfg.rank;
+  if (s->is_leader && !lead && s->commit > s->lc) s->lc = s->commit; /* a deposed leader knows its commit */
   for (uint32_t r = 0; r < rf; ++r) s->ranks[r] = ranks[r];
   s->leader_slot = leader_slot;
-  s->is_leader = ranks[leader_slot] == e->cfg.rank;
+  s->is_leader = lead;
   reset_catchup(s);
   return RMQ_OK;
 }
@@ -296,25 +302,40 @@ static int become_leader_one(ro_engine* e, uint32_t p, uint64_t term) {
       break;
     }
   if (slot == RF) return RMQ_EINVAL; /* no replica of p lives here */
+  return RMQ_OK;
+}
+
+/* Raft's vote restriction as far as a replica can tell: not a leader of a partition whose leader
+   committed records its log does not hold. */
+static int become_leader_check(ro_engine* e, uint32_t p) { return e->parts[p].leo < e->parts[p].lc ? RMQ_ESTALE : RMQ_OK; }
+
+static void become_leader_apply(ro_engine* e, uint32_t p, uint64_t term) {
+  ro_part* s = &e->parts[p];
+  uint32_t RF = e->cfg.replication_factor, slot = 0;
+  while (s->ranks[slot] != e->cfg.rank) ++slot;
   s->leader_slot = slot;
   s->is_leader = 1;
   s->term = term;
   s->term_start = s->leo; /* jraft: pendingIndex = lastLogIndex + 1 at leader start */
   for (uint32_t r = 0; r < RF; ++r) s->match[r] = s->ranks[r] == e->cfg.rank ? s->leo : 0;
+  commit_eval(e, s);  /* the virtual leader-start entry: a local quorum holds it at once */
+  s->dirty = 1;       /* the new leader's consumer offsets go to every follower with the next round */
   reset_catchup(s);
-  return RMQ_OK;
 }
 
 int ro_become_leader(ro_engine* e, uint32_t p, uint64_t term) {
-  if (p == RMQ_ALL_PARTITIONS) {
-    for (uint32_t q = 0; q < e->cfg.num_partitions; ++q) {
-      int rc = become_leader_one(e, q, term);
-      if (rc) return rc;
-    }
-    return RMQ_OK;
+  if (p != RMQ_ALL_PARTITIONS && p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  const uint32_t lo = p == RMQ_ALL_PARTITIONS ? 0 : p, hi = p == RMQ_ALL_PARTITIONS ? e->cfg.num_partitions : p + 1;
+  for (uint32_t q = lo; q < hi; ++q) { /* every check before any change (as the engine) */
+    int rc = become_leader_one(e, q, term);
+    if (rc) return rc;
   }
-  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
-  return become_leader_one(e, p, term);
+  for (uint32_t q = lo; q < hi; ++q) {
+    int rc = become_leader_check(e, q);
+    if (rc) return rc;
+  }
+  for (uint32_t q = lo; q < hi; ++q) become_leader_apply(e, q, term);
+  return RMQ_OK;
 }
 
 /* ------------------------------------------------------------------------------------------ */
@@ -787,6 +808,13 @@ int ro_get_partition_state(ro_engine* e, uint32_t p, rmq_partition_state* o) {
   o->leader_slot = s->leader_slot;
   o->is_leader = s->is_leader;
   o->segment_bytes = s->seg;
+  o->leader_commit = s->is_leader ? s->commit : s->lc;
+  return RMQ_OK;
+}
+
+int ro_get_partition_states(ro_engine* e, uint32_t first, uint32_t n, rmq_partition_state* out) {
+  if (first > e->cfg.num_partitions || n > e->cfg.num_partitions - first) return RMQ_ENOPART;
+  for (uint32_t i = 0; i < n; ++i) ro_get_partition_state(e, first + i, &out[i]);
   return RMQ_OK;
 }
 
@@ -829,9 +857,9 @@ int ro_record_pos(ro_engine* e, uint32_t p, uint64_t offset, uint64_t* pos) {
 /* ------------------------------------------------------------------------------------------ */
 
 
-#define RO_XMAGIC 0x33514D52u /* "RMQ3" */
+#define RO_XMAGIC 0x34514D52u /* "RMQ4" */
 #define RO_HDR 64u
-#define RO_DIR 32u
+#define RO_DIR 48u
 #define RO_ACK_REFUSED (1ull << 62)
 #define RO_ACK_LEO_MASK ((1ull << 62) - 1ull)
 #define RO_REBASE (1ull << 63) /* directory term flag: the entry restarts the follower's log */
@@ -1046,6 +1074,9 @@ int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint
     memcpy(d + 20, &ds, 4);
     const uint64_t tf = s->term | (x->rebase ? RO_REBASE : 0ull);
     memcpy(d + 24, &tf, 8);
+    /* the leader's commit (v4: Raft's leaderCommit), as it stood before the round's records */
+    const uint64_t boff = s->leo - s->round_count, lcm = s->commit < boff ? s->commit : boff;
+    memcpy(d + 32, &lcm, 8);
     uint8_t* dd = out + data + 16 * b16;
     /* the catch-up part from the leader's ring, then the round's records (if carried) */
     if (x->gap_bytes) ring_read(s->seg, ring_of(e, s->leader_slot, v[k].p), x->pos0, dd, x->gap_bytes);
@@ -1146,6 +1177,16 @@ static const uint8_t* row_of(const uint8_t* region, uint64_t rows, uint32_t M, u
     if (rk > k) break;
   }
   return NULL;
+}
+
+/* A follower learns its leader's commit (FORMAT.md §9 v4): leader_commit = the newest, its own
+   commit = the part of its log below it (never past its log end). */
+static void learn_commit(ro_part* s, uint64_t c) {
+  if (c > s->lc) s->lc = c;
+  const uint64_t k = s->lc < s->leo ? s->lc : s->leo;
+  if (k > s->commit) s->commit = k;
+  if (s->commit > s->leo) s->commit = s->leo;
+  s->hw = s->commit;
 }
 
 static void ack_of(const ro_part* s, int refused, uint64_t* ack) {
@@ -1304,12 +1345,13 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     const int owner = k == 0 || v[k - 1].p != v[k].p;
     const uint8_t* d = region + RO_HDR + (uint64_t)RO_DIR * k;
     uint32_t cnt, by16, ds;
-    uint64_t first, term;
+    uint64_t first, term, lcm;
     memcpy(&cnt, d, 4);
     memcpy(&by16, d + 4, 4);
     memcpy(&first, d + 8, 8);
     memcpy(&ds, d + 20, 4);
     memcpy(&term, d + 24, 8);
+    memcpy(&lcm, d + 32, 8);
     leo = base[2 * k];
     used = base[2 * k + 1];
     const int rebase = (term & RO_REBASE) != 0;
@@ -1376,6 +1418,7 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
       }
       e->counters[0] += cnt; /* records written into this replica slot */
     }
+    if (owner) learn_commit(s, lcm); /* the leader's commit the entry carries (Raft leaderCommit) */
     /* the owner's state after the round: both slots ack it */
     acks[2 * k] = first + cnt;
     acks[2 * k + 1] = used + 16ull * by16;
@@ -1411,6 +1454,39 @@ int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_a
     if (m > s->match[sl]) s->match[sl] = m;
   }
   for (uint32_t k = 0; k < n; ++k) commit_eval(e, &e->parts[v[k].p]);
+  free(v);
+  return RMQ_OK;
+}
+
+/* Commit notices (FORMAT.md §9 v4, a drain's heartbeat): the leader's {commit, term} for every
+   entry of the pair (me -> dst), and the follower learning them (an older term is ignored, a newer
+   one adopted). */
+int ro_commit_notice(ro_engine* e, uint32_t dst, uint64_t* out) {
+  ro_entry* v = NULL;
+  const uint32_t n = pair_entries(e, e->cfg.rank, dst, &v);
+  if (!v) return RMQ_ENOMEM;
+  for (uint32_t k = 0; k < n; ++k) {
+    out[2 * k] = e->parts[v[k].p].commit;
+    out[2 * k + 1] = e->parts[v[k].p].term;
+  }
+  free(v);
+  return RMQ_OK;
+}
+
+int ro_apply_notice(ro_engine* e, uint32_t src, const uint64_t* in, uint32_t n_in) {
+  ro_entry* v = NULL;
+  const uint32_t n = pair_entries(e, src, e->cfg.rank, &v);
+  if (!v) return RMQ_ENOMEM;
+  if (n != n_in) {
+    free(v);
+    return RMQ_EINVAL;
+  }
+  for (uint32_t k = 0; k < n; ++k) {
+    ro_part* s = &e->parts[v[k].p];
+    if (in[2 * k + 1] < s->term) continue;
+    s->term = in[2 * k + 1];
+    learn_commit(s, in[2 * k]);
+  }
   free(v);
   return RMQ_OK;
 }

@@ -66,6 +66,7 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
              rmq_fetch_res* res, uint64_t* bytes_used);
 
 int ro_get_partition_state(ro_engine* e, uint32_t pidx, rmq_partition_state* out);
+int ro_get_partition_states(ro_engine* e, uint32_t first, uint32_t n, rmq_partition_state* out);
 int ro_read_segment(ro_engine* e, uint32_t replica, uint32_t pidx, uint64_t ring_off, uint64_t len,
                     uint8_t* out);
 int ro_read_index(ro_engine* e, uint32_t pidx, uint64_t m_first, uint64_t count, uint64_t* out);
@@ -88,6 +89,9 @@ uint64_t ro_round_no(ro_engine* e);
 int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, uint64_t* acks);
 int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_acks, uint64_t round);
 uint32_t ro_pair_entries(ro_engine* e, uint32_t src, uint32_t dst);
+/* Commit notices (a drain's heartbeat, FORMAT.md §9 v4): 2 words per entry of the pair {commit, term}. */
+int ro_commit_notice(ro_engine* e, uint32_t dst, uint64_t* out);
+int ro_apply_notice(ro_engine* e, uint32_t src, const uint64_t* in, uint32_t n);
 /* [0] records ingested, [1] entries refused (CRC), [2] refused (log / term / missed round),
    [3] bytes ingested, [4] catch-up entries sent, [5] detached entry plans (gap beyond the ring) */
 void ro_counters(ro_engine* e, uint64_t* out /* [6] */);

@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 4
+RMQ_ABI_VERSION = 5
 RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
@@ -30,6 +30,7 @@ RMQ_ENOSPC = -4
 RMQ_EDEVICE = -5
 RMQ_EOFFSET = -6
 RMQ_ENOMEM = -7
+RMQ_ESTALE = -8
 
 RMQ_MEM_HOST = 0
 RMQ_MEM_DEVICE = 1
@@ -39,6 +40,7 @@ STATUS_NAMES = {
     RMQ_OK: "RMQ_OK", RMQ_PENDING: "RMQ_PENDING", RMQ_ENOTLEADER: "RMQ_ENOTLEADER",
     RMQ_ENOPART: "RMQ_ENOPART", RMQ_EINVAL: "RMQ_EINVAL", RMQ_ENOSPC: "RMQ_ENOSPC",
     RMQ_EDEVICE: "RMQ_EDEVICE", RMQ_EOFFSET: "RMQ_EOFFSET", RMQ_ENOMEM: "RMQ_ENOMEM",
+    RMQ_ESTALE: "RMQ_ESTALE",
 }
 
 u32 = C.c_uint32
@@ -79,7 +81,7 @@ class RmqPartitionState(C.Structure):
         ("log_end_offset", u64), ("log_end_pos", u64), ("log_start_offset", u64),
         ("log_start_pos", u64), ("commit", u64), ("high_watermark", u64), ("term", u64),
         ("term_start", u64), ("match", u64 * RMQ_MAX_RF), ("replica_rank", u32 * RMQ_MAX_RF),
-        ("leader_slot", u32), ("is_leader", u32), ("segment_bytes", u64),
+        ("leader_slot", u32), ("is_leader", u32), ("segment_bytes", u64), ("leader_commit", u64),
     ]
 
 
@@ -122,6 +124,7 @@ _SIGS = {
     "rmq_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp]),
     "rmq_fetch": (C.c_int, [vp, vp, u32, u32, vp, u64, vp, C.POINTER(u64)]),
     "rmq_get_partition_state": (C.c_int, [vp, u32, C.POINTER(RmqPartitionState)]),
+    "rmq_get_partition_states": (C.c_int, [vp, u32, u32, vp]),
     "rmq_read_segment": (C.c_int, [vp, u32, u32, u64, u64, vp]),
     "rmq_read_index": (C.c_int, [vp, u32, u64, u64, vp]),
     "rmq_read_consumer_offsets": (C.c_int, [vp, u32, vp]),
@@ -145,6 +148,7 @@ _SIGS = {
     "rmq_read_outbox": (C.c_int, [vp, u32, vp, u64, C.POINTER(u64)]),
     "rmq_fault_drop_rounds": (C.c_int, [vp, u32]),
     "rmq_fault_corrupt": (C.c_int, [vp, u32, C.c_int64]),
+    "rmq_fault_isolate": (C.c_int, [vp, u32, u32]),
 }
 
 _lib = None

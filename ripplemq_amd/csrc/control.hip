@@ -26,6 +26,10 @@ __global__ void ack_kernel(AckArgs a) {
   atomicMax((unsigned long long*)&a.st.match[(u64)a.pidx[i] * a.st.RF + a.slot[i]], (unsigned long long)m);
 }
 
+// Leader start (Raft's leader initialisation, FORMAT.md §6): term_start = log end (the virtual
+// leader-start entry), local matchIndex = log end, remote 0; the commit rule runs at once (a quorum
+// of local replicas holds the leader-start entry already); the consumer-offset row goes to every
+// follower with the next round (the new leader's table replaces theirs).
 __global__ void become_leader_kernel(DevState st, u32 only) {
   const u32 p = only == 0xFFFFFFFFu ? blockIdx.x * blockDim.x + threadIdx.x : only;
   if (p >= st.P || (only != 0xFFFFFFFFu && (blockIdx.x | threadIdx.x))) return;
@@ -33,6 +37,8 @@ __global__ void become_leader_kernel(DevState st, u32 only) {
   st.term_start[p] = leo;
   const u32 lm = st.local_mask[p];
   for (u32 r = 0; r < st.RF; ++r) st.match[(u64)p * st.RF + r] = (lm >> r & 1u) ? leo : 0ull;
+  commit_rule(st, p);
+  st.cdirty[p] = 1u;
 }
 
 __global__ void consumer_apply_kernel(ConsumerCommitArgs a) {

@@ -197,7 +197,9 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     int rc = repl_before_launch(e, a);  // followers' acks of the group applied three launches ago
     if (rc) return rc;
   }
-  if (s3 || s4 || a.ackin) a.wgp = (P + PT - 1) / PT;
+  // partition threads: the group applied, retention, acks; with a transport in every launch (they
+  // also record each led partition's commit at the launch's end, which the next plan carries)
+  if (s3 || s4 || a.ackin || e->repl) a.wgp = (P + PT - 1) / PT;
   if (s4) {
     a.g4 = make_group(e, *s4);
     a.s4 = e->scratch[s4->set];
@@ -220,6 +222,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.s3_lead = e->s3_first ? std::min<uint32_t>(a.wg3, e->s3_lead ? e->s3_lead : a.wg3) : 0u;
   }
   a.launch_seq = ++e->launch_seq;
+  e->st.csnap_slot = (uint32_t)(a.launch_seq & 1ull);  // control kernels after this launch write its slot
   if (e->d_stamps && a.launch_seq == e->stamps_at) {
     a.stamps = e->d_stamps;
     e->stamps_wg[0] = a.wg1;
@@ -445,7 +448,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, e->d_crc,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, e->d_crc,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_csum, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (const StateSet& z : e->sets) {
@@ -552,6 +555,7 @@ const char* rmq_strerror(int s) {
     case RMQ_EDEVICE: return "device error";
     case RMQ_EOFFSET: return "offset out of range";
     case RMQ_ENOMEM: return "out of memory";
+    case RMQ_ESTALE: return "replica lags the committed log";
     default: return "unknown status";
   }
 }
@@ -662,6 +666,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&s.cdirty, P));
+  CREATE_TRY(dalloc(&s.lcommit, P));
   CREATE_TRY(dalloc(&e->d_rlate, P));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
@@ -739,12 +744,22 @@ int set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_
   if (!rc) rc = equalize_state_sets(e);
   if (rc) return rc;
   std::vector<uint32_t> mask(P);
+  std::vector<uint32_t> demoted;  // partitions this engine stops leading
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t p = pidx[i];
     for (uint32_t r = 0; r < RF; ++r) e->ranks[(size_t)p * RF + r] = ranks[(size_t)i * RF + r];
     e->leader_slot[p] = leader_slot[i];
-    e->is_leader[p] = ranks[(size_t)i * RF + leader_slot[i]] == e->cfg.rank;
+    const uint32_t lead = ranks[(size_t)i * RF + leader_slot[i]] == e->cfg.rank;
+    if (e->is_leader[p] && !lead) demoted.push_back(p);
+    e->is_leader[p] = lead;
     if (key) e->key[p] = key[i];
+  }
+  if (!demoted.empty()) {  // a former leader knows its own commit as the leader's (FORMAT.md §9 v4)
+    std::vector<uint64_t> c(P), lc(P);
+    HIP_TRY(hipMemcpy(c.data(), e->st.commit, P * 8ull, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lc.data(), e->st.lcommit, P * 8ull, hipMemcpyDeviceToHost));
+    for (uint32_t p : demoted) lc[p] = std::max(lc[p], c[p]);
+    HIP_TRY(hipMemcpy(e->st.lcommit, lc.data(), P * 8ull, hipMemcpyHostToDevice));
   }
   for (uint32_t p = 0; p < P; ++p) {
     mask[p] = 0;
@@ -794,6 +809,15 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   HIP_TRY(hipMemcpy(&e->term[lo], e->st.term + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
   for (uint32_t p = lo; p < hi; ++p)
     if (term < e->term[p]) return RMQ_EINVAL;
+  {
+    // Raft's vote restriction, as far as this replica can tell: it may not lead a partition whose
+    // leader committed records its log does not hold (leader_commit from rounds and commit notices)
+    std::vector<uint64_t> leo(hi - lo), lc(hi - lo);
+    HIP_TRY(hipMemcpy(leo.data(), e->st.leo + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lc.data(), e->st.lcommit + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
+    for (uint32_t p = lo; p < hi; ++p)
+      if (leo[p - lo] < lc[p - lo]) return RMQ_ESTALE;  // (a partition always led here: lc = 0)
+  }
   for (uint32_t p = lo; p < hi; ++p) {
     uint32_t slot = e->leader_slot[p];
     if (!e->repl) {
@@ -1320,6 +1344,47 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   o->leader_slot = e->leader_slot[p];
   o->is_leader = e->is_leader[p];
   o->segment_bytes = 1ull << (e->ring[p] & 63ull);
+  if (o->is_leader) o->leader_commit = o->commit;
+  else HIP_TRY(hipMemcpy(&o->leader_commit, s.lcommit + p, 8, hipMemcpyDeviceToHost));
+  return RMQ_OK;
+}
+
+int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_partition_state* o) {
+  if (!e || (n && !o)) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  if (first > P || n > P - first) return RMQ_ENOPART;
+  if (!n) return RMQ_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = quiesce(e);
+  if (rc) return rc;
+  const DevState& s = e->st;
+  uint64_t* const src[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term, s.term_start, s.lcommit};
+  std::vector<uint64_t> v((size_t)n * 9), m((size_t)n * RF);
+  for (int f = 0; f < 9; ++f)
+    HIP_TRY(hipMemcpy(v.data() + (size_t)f * n, src[f] + first, (size_t)n * 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(m.data(), s.match + (size_t)first * RF, (size_t)n * RF * 8, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t p = first + i;
+    rmq_partition_state& x = o[i];
+    std::memset(&x, 0, sizeof x);
+    x.log_end_offset = v[i];
+    x.log_end_pos = v[(size_t)n + i];
+    x.log_start_offset = v[2ull * n + i];
+    x.log_start_pos = v[3ull * n + i];
+    x.commit = v[4ull * n + i];
+    x.high_watermark = v[5ull * n + i];
+    x.term = v[6ull * n + i];
+    x.term_start = v[7ull * n + i];
+    for (uint32_t r = 0; r < RF; ++r) {
+      x.match[r] = m[(size_t)i * RF + r];
+      x.replica_rank[r] = e->ranks[(size_t)p * RF + r];
+    }
+    x.leader_slot = e->leader_slot[p];
+    x.is_leader = e->is_leader[p];
+    x.segment_bytes = 1ull << (e->ring[p] & 63ull);
+    x.leader_commit = x.is_leader ? x.commit : v[8ull * n + i];
+  }
   return RMQ_OK;
 }
 
@@ -1534,6 +1599,15 @@ int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n) {
   if (!e->repl) return RMQ_EINVAL;
   e->repl->drop_from = e->last_ticket + 1;
   e->repl->drop_n = n;
+  return RMQ_OK;
+}
+
+int rmq_fault_isolate(rmq_engine* e, uint32_t dst, uint32_t n) {
+  if (!e) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (!e->repl || dst >= e->repl->world || dst == e->repl->rank) return RMQ_EINVAL;
+  e->repl->iso_from[dst] = e->last_ticket + 1;
+  e->repl->iso_n[dst] = n;
   return RMQ_OK;
 }
 

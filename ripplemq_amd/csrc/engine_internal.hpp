@@ -188,6 +188,9 @@ struct Replication {
   XDecision* d_xdec = nullptr;   // [n_out]
   uint64_t* d_xtot = nullptr;    // [n_out]
   uint32_t* d_dflag = nullptr;   // [world]
+  uint64_t* d_nout = nullptr;    // [n_out][2] commit notices sent {commit, term} (FORMAT.md §9 v4)
+  uint64_t* d_nin = nullptr;     // [n_in][2] commit notices received
+  hipEvent_t ev_notice = nullptr;
   uint64_t dcap = 0;             // outbox bytes per destination
   uint64_t reserve = 0;          // catch-up bytes per destination
   uint64_t items_cap = 0;
@@ -202,6 +205,9 @@ struct Replication {
   // ticket is at least `drop_from` send empty regions
   uint64_t drop_from = 0;
   uint32_t drop_n = 0;
+  // rmq_fault_isolate: the next iso_n[q] rounds (groups from ticket iso_from[q] on) to q are lost
+  uint64_t iso_from[kMaxWorld] = {};
+  uint32_t iso_n[kMaxWorld] = {};
   // rmq_fault_corrupt: the next round to destination q flips the byte at flip_at[q]
   bool flip[kMaxWorld] = {};
   int64_t flip_at[kMaxWorld] = {};

@@ -31,9 +31,9 @@ constexpr uint32_t kMaxPartitions = 1u << 16;  // 16-bit partition keys (two 8-b
 constexpr uint32_t kMaxRF = 8;
 constexpr uint32_t kMaxWorld = 16;       // ranks of a replication transport
 constexpr uint32_t kMaxRemote = 4;       // remote replica slots per partition with a transport (RF <= 5)
-constexpr uint32_t kXMagic = 0x33514D52u;  // "RMQ3": replica-log round region v3 (FORMAT.md §9)
+constexpr uint32_t kXMagic = 0x34514D52u;  // "RMQ4": replica-log round region v4 (FORMAT.md §9)
 constexpr uint32_t kRegionHdr = 64;      // region header bytes
-constexpr uint32_t kDirEntry = 32;       // directory entry bytes
+constexpr uint32_t kDirEntry = 48;       // directory entry bytes (v4: + the leader's commit)
 constexpr uint64_t kAckRefused = 1ull << 62;  // ack status bit (FORMAT.md §9 acks)
 constexpr uint64_t kAckLeoMask = kAckRefused - 1ull;
 constexpr uint64_t kNoRound = ~0ull;     // XEntry::data_abs: the entry carries no round records
@@ -103,6 +103,7 @@ struct XPlanArgs {
   XDecision* xdec;           // [n_out] stage-2 workers -> plan
   uint64_t* xtot;            // [n_out] the group's totals word of the entry's partition (workers -> plan)
   uint32_t* dflag;           // [world] kDecRow | kDecGapped of any entry to that destination
+  const uint64_t* csnap;     // [P] the leader's commit when the launch started (the previous launch's slot)
   const uint64_t* ackin;     // acks applied in this launch, [n_out][2], or null
   uint64_t acks_round;       // the round they answer
   uint32_t* dirty;           // [P] consumer offsets changed since the last round (cleared by the plan)
@@ -132,6 +133,13 @@ struct DevState {
   uint64_t* ring;        // [P] ring descriptor: byte offset in the pool | log2(ring bytes) (bits 0..5)
   uint64_t* cons;        // [P][C] consumer offsets
   uint32_t* cdirty;      // [P] consumer offsets changed since the last replication round (FORMAT §9)
+  uint64_t* lcommit;     // [P] follower: the newest leader commit learned (rounds, commit notices;
+                         //   FORMAT.md §9); a leader's own is `commit`
+  uint64_t* csnap;       // [2][P] leader commit at the end of launch L, in slot L & 1 (partition threads
+                         //   of every transport launch, and the control kernels after it): the plan of
+                         //   launch L + 1 carries it in its directory (one value per round, whatever
+                         //   that launch's partition threads fold in meanwhile)
+  uint32_t csnap_slot;   // the slot of the last launch issued (control kernels write it)
   uint64_t rstride;      // bytes per replica region (the pool)
   uint32_t P, RF, C;
   uint32_t icap_mul;     // index entries per interval of ring (2 * group + 2)
@@ -314,6 +322,18 @@ struct IngestArgs {
 };
 constexpr uint64_t kCopyChunk = 16ull << 10;  // follower copy: region bytes per workgroup
 
+// Commit notices (FORMAT.md §9, a drain's heartbeat): the leader's {commit, term} per out entry,
+// and the follower's application per in entry.
+struct NoticeArgs {
+  DevState st;
+  StateSet sets[2];
+  const uint32_t* xo_p;      // [n_out]
+  uint64_t* out;             // [n_out][2] {commit, term}
+  const uint32_t* xi_p;      // [n_in]
+  const uint64_t* in;        // [n_in][2]
+  uint32_t n_out, n_in;
+};
+
 // Acks of one round applied outside the pipeline (drain): thread per partition.
 struct AckApplyArgs {
   DevState st;
@@ -348,6 +368,8 @@ constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgrou
 // chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))
 void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s);
 void launch_ack_apply(const AckApplyArgs& a, hipStream_t s);
+void launch_notice_fill(const NoticeArgs& a, hipStream_t s);   // leader: {commit, term} per out entry
+void launch_notice_apply(const NoticeArgs& a, hipStream_t s);  // follower: learn the leader's commit
 void launch_flip(uint8_t* region, uint64_t size, int64_t at, hipStream_t s);  // rmq_fault_corrupt
 
 }  // namespace rmq

@@ -8,8 +8,12 @@ namespace rmq {
 // Raft quorum commit (jraft BallotBox semantics; restated from the Raft paper since
 // jraft-core 1.3.15 is not in the container): N = k-th largest matchIndex of the partition's
 // replica row, k = RF/2 + 1 (the median for odd RF), held in registers and ordered by a
-// compare-exchange network; commit advances to N only if N > commit and the N-th record was
-// appended in the current term (N > term_start). hw (consumer-visible end) = commit.
+// compare-exchange network; commit advances to N only if N > commit and N >= term_start: the
+// leader's term starts with a virtual entry at term_start (jraft appends a configuration entry
+// when a leader starts, [jraft]), which a replica holds once it holds the log up to term_start in
+// the new term (its match is reset to 0 at leader start and only moves by acks of that term); a
+// quorum holding it commits every earlier-term record before it (Raft's current-term rule, FORMAT.md
+// §6). hw (consumer-visible end) = commit.
 __device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u64 commit, u64 term_start) {
   u64 m[kMaxRF];
 #pragma unroll
@@ -26,7 +30,7 @@ __device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u
   u64 N = 0;
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) N = (r == k - 1) ? m[r] : N;
-  return (N > commit && N > term_start) ? N : commit;
+  return (N > commit && N >= term_start) ? N : commit;
 }
 
 // Remote replica acks of one replication round (FORMAT.md §9 v3, [n_out][2] {log end | status << 62,
@@ -65,6 +69,21 @@ __device__ __forceinline__ void commit_rule(const DevState& st, u32 p) {
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < st.RF ? st.match[(u64)p * st.RF + r] : 0ull;
   const u64 c = quorum_commit(row, st.RF, st.commit[p], st.term_start[p]);
+  st.commit[p] = c;
+  st.hw[p] = c;
+  if (st.csnap) st.csnap[(u64)st.csnap_slot * st.P + p] = c;  // (the next plan's carried commit)
+}
+
+// A follower learns its leader's commit (FORMAT.md §9 v4: a round entry it accepted, or a commit
+// notice): leader_commit = the newest, and its own commit = the part of its log below it (never
+// past its log end: a replica whose log ends below the leader's commit lacks committed records).
+__device__ __forceinline__ void learn_commit(const DevState& st, u32 p, u64 lc, u64 leo) {
+  const u64 l = st.lcommit[p] > lc ? st.lcommit[p] : lc;
+  st.lcommit[p] = l;
+  u64 c = st.commit[p];
+  const u64 k = l < leo ? l : leo;
+  c = c > k ? c : k;
+  c = c < leo ? c : leo;
   st.commit[p] = c;
   st.hw[p] = c;
 }

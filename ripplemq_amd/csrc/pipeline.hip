@@ -468,6 +468,8 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
   store_sc1(dw, (tot >> 40) | ((tot & kLow40) << 32));
   store_sc1(dw + 1, Boff);
   store_sc1(dw + 3, st.term[p]);
+  store_sc1(dw + 4, X.csnap[p]);  // the leader's commit as the launch started (FORMAT.md §9 v4)
+  store_sc1(dw + 5, 0ull);
   store_sc1(&X.xnext[2 * e], Boff + (tot >> 40));
   store_sc1(&X.xnext[2 * e + 1], Bpos + 16ull * (tot & kLow40));
 }
@@ -506,7 +508,7 @@ __device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos,
 // a wait for all memory operations. The caller ignores the values of an entry past the list, and
 // selects t3 / lastg by A.g3.nb where it uses them.
 struct PlanIn {
-  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg, term;
+  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg, term, commit;
   u32 p, fl;
 };
 __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
@@ -523,6 +525,7 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
   v.used = A.cur.used[p];
   v.lastg = A.lastg[p];
   v.term = A.st.term[p];
+  v.commit = X.csnap[p];
   return v;
 }
 
@@ -708,6 +711,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
           de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
           const u64 term = cur.term | (rebase ? kTermRebase : 0ull);
           de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
+          de[2] = make_uint4((u32)cur.commit, (u32)(cur.commit >> 32), 0u, 0u);
           XEntry xe;
           xe.data_abs = kNoRound;
           xe.tab_abs = 0;
@@ -1565,6 +1569,7 @@ __device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
   for (u32 j = 0; j < kMaxGroup; ++j) bc3[j] = a3 && j < A.g3.nb ? A.s3.bcum[(u64)j * st.P + p] : 0ull;
   if (A.lastg && a3) A.lastg[p] = lead ? (tot3 & kLow40) : 0ull;  // the next plans' C (FORMAT.md §9)
   if (!lead) return;
+  u64 cfin = commit0;  // the partition's commit at the end of this launch (st.csnap)
   // ---- stage 3: log end, matchIndex, commit (first: the match row is dead before retention)
   if (a3) {
     A.nxt.leo[p] = leo0 + (tot3 >> 40);
@@ -1587,8 +1592,10 @@ __device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
       const u64 c = quorum_commit(row, RF, commit0, ts);
       st.commit[p] = c;
       st.hw[p] = c;
+      cfin = c;
     }
   }
+  if (st.csnap) st.csnap[(A.launch_seq & 1ull) * st.P + p] = cfin;  // the next launch's plan carries it
 
   const RingRef rg = ring_ref(desc, st.interval_log2, st.icap_mul);
   u64 soff = soff0, spos = spos0;

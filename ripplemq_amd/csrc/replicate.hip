@@ -83,12 +83,12 @@ __device__ __forceinline__ u32 source_of_task(const IngestArgs& A, u32 task) {
 // the entry restarts the follower's log (a rebase, FORMAT.md §9: flag in the term's top bit).
 struct DirView {
   u32 count, bytes16, tstart, dstart16;
-  u64 first, term;
+  u64 first, term, commit;
   bool rebase;
 };
 __device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
   const uint4* de = reinterpret_cast<const uint4*>(R.base + kRegionHdr + (u64)kDirEntry * k);
-  const uint4 d0 = de[0], d1 = de[1];
+  const uint4 d0 = de[0], d1 = de[1], d2 = de[2];
   DirView d;
   d.count = d0.x;
   d.bytes16 = d0.y;
@@ -96,6 +96,7 @@ __device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
   d.tstart = d1.x;
   d.dstart16 = d1.y;
   d.term = ((u64)d1.w << 32) | d1.z;
+  d.commit = ((u64)d2.y << 32) | d2.x;  // the leader's commit (v4)
   d.rebase = (d.term & kTermRebase) != 0ull;
   d.term &= ~kTermRebase;
   return d;
@@ -488,6 +489,7 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
       A.sets[s].leo[p] = nleo;
       A.sets[s].used[p] = nused;
     }
+    learn_commit(st, p, d.commit, nleo);  // the leader's commit the entry carries (Raft leaderCommit)
     if (d.count) {
       // retention once per round (FORMAT.md §4 rule on the follower's log)
       const RingRef rg = ring_ref(st, p);
@@ -566,7 +568,38 @@ __global__ void ack_apply_kernel(AckApplyArgs a) {
     const u64 c = quorum_commit(row, st.RF, st.commit[p], st.term_start[p]);
     st.commit[p] = c;
     st.hw[p] = c;
+    if (st.csnap) st.csnap[(u64)st.csnap_slot * st.P + p] = c;
   }
+}
+
+// Commit notices (FORMAT.md §9 v4), exchanged by a drain after its rounds' acks: the leader's
+// {commit, term} per out entry, and a follower learning it (a notice of an older term is ignored;
+// a newer term is adopted, as any Raft message of a newer term makes a replica do).
+__global__ void notice_fill_kernel(NoticeArgs a) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n_out) return;
+  const u32 p = a.xo_p[e];
+  a.out[2 * e] = a.st.commit[p];
+  a.out[2 * e + 1] = a.st.term[p];
+}
+
+__global__ void notice_apply_kernel(NoticeArgs a) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= a.n_in) return;
+  const DevState& st = a.st;
+  const u32 p = a.xi_p[e];
+  const u64 c = a.in[2 * e], t = a.in[2 * e + 1];
+  if (t < st.term[p]) return;
+  if (t > st.term[p]) st.term[p] = t;
+  learn_commit(st, p, c, a.sets[0].leo[p]);  // (two slots of one partition: the same values)
+}
+
+void launch_notice_fill(const NoticeArgs& a, hipStream_t s) {
+  if (a.n_out) hipLaunchKernelGGL(notice_fill_kernel, dim3((a.n_out + 255) / 256), dim3(256), 0, s, a);
+}
+
+void launch_notice_apply(const NoticeArgs& a, hipStream_t s) {
+  if (a.n_in) hipLaunchKernelGGL(notice_apply_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
 }
 
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s) {

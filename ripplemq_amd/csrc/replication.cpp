@@ -87,8 +87,9 @@ int reset_catchup(rmq_engine* e) {
 
 namespace {
 
-// Post the {region bytes, records} swap of the group in set s (after its stage-2 launch).
-int post_sizes(rmq_engine* e, uint32_t s, bool drop) {
+// Post the {region bytes, records} swap of the group in set s (after its stage-2 launch). drop: the
+// leader sends no region this round; lost: bit q, the region to q is lost (rmq_fault_isolate).
+int post_sizes(rmq_engine* e, uint32_t s, bool drop, uint32_t lost) {
   Replication* r = e->repl;
   XchgSet& x = r->sets[s];
   const uint32_t W = r->world;
@@ -102,6 +103,8 @@ int post_sizes(rmq_engine* e, uint32_t s, bool drop) {
   }
   HIP_TRY(hipStreamWaitEvent(r->xchg_s, x.ev_s2, 0));
   if (drop) HIP_TRY(hipMemsetAsync(x.sizes, 0, 2ull * W * 8, r->xchg_s));  // no region to anyone
+  for (uint32_t q = 0; q < W && !drop; ++q)
+    if ((lost >> q) & 1u) HIP_TRY(hipMemsetAsync(x.sizes + 2 * q, 0, 16, r->xchg_s));
   int rc = r->xport->exchange(sb, n16, rb, n16, r->xchg_s);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(x.h_sizes, x.sizes, 4ull * W * 8, hipMemcpyDeviceToHost, r->xchg_s));
@@ -209,6 +212,7 @@ int repl_attach(rmq_engine* e, Transport* t) {
   r->rank = t->rank();
   e->repl = r;
   HIP_TRY(hipStreamCreateWithFlags(&r->xchg_s, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&r->ev_notice, hipEventDisableTiming));
   for (XchgSet& x : r->sets) {
     HIP_TRY(hipEventCreateWithFlags(&x.ev_s2, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&x.ev_s3, hipEventDisableTiming));
@@ -220,7 +224,14 @@ int repl_attach(rmq_engine* e, Transport* t) {
   }
   int rc = dalloc(&r->d_counters, 7);
   if (!rc) rc = dalloc(&r->d_lastg, e->cfg.num_partitions);
+  if (!rc && !e->st.csnap) rc = dalloc(&e->st.csnap, 2ull * e->cfg.num_partitions);
   if (rc) return rc;
+  {
+    // both slots start at the current commits (the first plan reads the slot of the launch before)
+    for (uint32_t k = 0; k < 2; ++k)
+      HIP_TRY(hipMemcpy(e->st.csnap + (size_t)k * e->cfg.num_partitions, e->st.commit,
+                        e->cfg.num_partitions * 8ull, hipMemcpyDeviceToDevice));
+  }
   return repl_set_lists(e);
 }
 
@@ -238,9 +249,11 @@ void repl_free(rmq_engine* e) {
   }
   void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_keysum_in, r->d_outidx, r->d_xi_p, r->d_xi_slot,
                   r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
-                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_xtot, r->d_dflag, r->d_lastg};
+                  r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_xtot, r->d_dflag, r->d_lastg,
+                  r->d_nout, r->d_nin};
   for (void* p : bufs)
     if (p) hipFree(p);
+  if (r->ev_notice) hipEventDestroy(r->ev_notice);
   if (r->xchg_s) hipStreamDestroy(r->xchg_s);
   delete r->xport;
   delete r;
@@ -359,6 +372,8 @@ int repl_set_lists(rmq_engine* e) {
   if (!rc) rc = upload(&r->d_xreq, std::vector<uint64_t>(4 * n_out, 0ull));
   if (!rc) rc = upload(&r->d_xcu, std::vector<uint64_t>(n_out, 0ull));
   if (!rc) rc = upload(&r->d_dflag, std::vector<uint32_t>(W, 0u));
+  if (!rc) rc = upload(&r->d_nout, std::vector<uint64_t>(2 * n_out, 0ull));
+  if (!rc) rc = upload(&r->d_nin, std::vector<uint64_t>(2 * n_in, 0ull));
   if (r->d_xdec) hipFree(r->d_xdec);
   if (r->d_xtot) hipFree(r->d_xtot);
   r->d_xdec = nullptr;
@@ -435,6 +450,8 @@ void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const Gro
     a.xp2.xdec = r->d_xdec;
     a.xp2.xtot = r->d_xtot;
     a.xp2.dflag = r->d_dflag;
+  // the commit the round carries: the slot of the launch before this one (launch_seq not yet advanced)
+  a.xp2.csnap = e->st.csnap + (size_t)(e->launch_seq & 1ull) * e->cfg.num_partitions;
     a.xp2.dirty = e->st.cdirty;
     a.xp2.xc = x.xc;
     a.xp2.xc_n = x.xc_n;
@@ -489,7 +506,13 @@ int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s
     HIP_TRY(hipEventRecord(r->sets[s2->set].ev_s2, e->main_s));
     const bool drop = r->drop_n && s2->b[0].ticket >= r->drop_from;
     if (drop) r->drop_n--;
-    int rc = post_sizes(e, s2->set, drop);
+    uint32_t lost = 0;
+    for (uint32_t q = 0; q < r->world; ++q)
+      if (r->iso_n[q] && s2->b[0].ticket >= r->iso_from[q]) {
+        lost |= 1u << q;
+        r->iso_n[q]--;
+      }
+    int rc = post_sizes(e, s2->set, drop, lost);
     if (rc) return rc;
   }
   if (s3) {
@@ -501,10 +524,51 @@ int repl_after_launch(rmq_engine* e, const GroupFlight* s2, const GroupFlight* s
   return RMQ_OK;
 }
 
-// After the pipeline is flushed: post the remaining rounds and apply their acks.
+// Commit notices (FORMAT.md §9 v4, the heartbeat of a drain): every leader sends each follower its
+// {commit, term} per entry of their list after the drain's acks are in; the followers learn it.
+// Collective like the rounds before it (every rank drains the same rounds).
+int post_notices(rmq_engine* e) {
+  Replication* r = e->repl;
+  const uint32_t W = r->world, me = r->rank;
+  NoticeArgs a{};
+  a.st = e->st;
+  a.sets[0] = e->sets[0];
+  a.sets[1] = e->sets[1];
+  a.xo_p = r->d_xo_p;
+  a.out = r->d_nout;
+  a.xi_p = r->d_xi_p;
+  a.in = r->d_nin;
+  a.n_out = (uint32_t)r->xo_p.size();
+  a.n_in = (uint32_t)r->xi_p.size();
+  launch_notice_fill(a, e->main_s);  // after the acks applied on the pipeline stream
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(r->ev_notice, e->main_s));
+  HIP_TRY(hipStreamWaitEvent(r->xchg_s, r->ev_notice, 0));
+  void* sb[kMaxWorld];
+  void* rb[kMaxWorld];
+  uint64_t sn[kMaxWorld], rn[kMaxWorld];
+  for (uint32_t q = 0; q < W; ++q) {
+    sn[q] = q == me ? 0 : 16ull * (r->xo_start[q + 1] - r->xo_start[q]);
+    rn[q] = q == me ? 0 : 16ull * (r->xi_start[q + 1] - r->xi_start[q]);
+    sb[q] = r->d_nout + 2ull * r->xo_start[q];
+    rb[q] = r->d_nin + 2ull * r->xi_start[q];
+  }
+  int rc = r->xport->exchange(sb, sn, rb, rn, r->xchg_s);
+  if (rc) return rc;
+  launch_notice_apply(a, r->xchg_s);
+  HIP_TRY(hipGetLastError());
+  // the pipeline stream sees the followers' new commits before anything issued after the drain
+  HIP_TRY(hipEventRecord(r->ev_notice, r->xchg_s));
+  HIP_TRY(hipStreamWaitEvent(e->main_s, r->ev_notice, 0));
+  return RMQ_OK;
+}
+
+// After the pipeline is flushed: post the remaining rounds, apply their acks, and (if any round
+// was in flight) exchange the commit notices.
 int repl_drain(rmq_engine* e) {
   Replication* r = e->repl;
   if (!r) return RMQ_OK;
+  const bool rounds = !r->sized.empty() || !r->acking.empty();
   while (!r->sized.empty()) {
     int rc = post_round(e, r->sized.front());
     if (rc) return rc;
@@ -524,6 +588,10 @@ int repl_drain(rmq_engine* e) {
       HIP_TRY(hipGetLastError());
     }
     r->acking.pop_front();
+  }
+  if (rounds) {
+    int rc = post_notices(e);
+    if (rc) return rc;
   }
   HIP_TRY(hipStreamSynchronize(r->xchg_s));
   return RMQ_OK;

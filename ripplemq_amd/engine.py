@@ -34,7 +34,7 @@ FETCH_RES_DTYPE = np.dtype([
     ("status", "<i4"), ("reserved", "<u4"),
 ])
 STATE_FIELDS = ("log_end_offset", "log_end_pos", "log_start_offset", "log_start_pos", "commit",
-                "high_watermark", "term", "term_start")
+                "high_watermark", "term", "term_start", "leader_commit")
 
 
 @dataclass
@@ -56,6 +56,14 @@ class EngineConfig:
         for f, _ in A.RmqConfig._fields_:
             setattr(c, f, getattr(self, f))
         return c
+
+
+# numpy mirror of rmq_partition_state (bulk read-back)
+STATE_DTYPE = np.dtype({"names": [f for f, _ in A.RmqPartitionState._fields_],
+                        "formats": ["<u8"] * 8 + [("<u8", A.RMQ_MAX_RF), ("<u4", A.RMQ_MAX_RF), "<u4", "<u4",
+                                                  "<u8", "<u8"],
+                        "offsets": [getattr(A.RmqPartitionState, f).offset for f, _ in A.RmqPartitionState._fields_],
+                        "itemsize": C.sizeof(A.RmqPartitionState)})
 
 
 def state_to_dict(s: A.RmqPartitionState, rf: int) -> dict:
@@ -139,6 +147,10 @@ class Engine:
     def fault_drop_rounds(self, n: int = 1) -> None:
         """Tests: the next n rounds this engine leads carry no records (rmq_fault_drop_rounds)."""
         _check(self.lib.rmq_fault_drop_rounds(self.h, n), "rmq_fault_drop_rounds")
+
+    def fault_isolate(self, dst: int, n: int = 1) -> None:
+        """Tests: the next n rounds this engine sends to dst are lost (rmq_fault_isolate)."""
+        _check(self.lib.rmq_fault_isolate(self.h, dst, n), "rmq_fault_isolate")
 
     def fault_corrupt(self, dst: int, at: int) -> None:
         """Tests: the next round sent to dst has one byte flipped (rmq_fault_corrupt)."""
@@ -307,6 +319,14 @@ class Engine:
                                          sb.ctypes.data_as(C.POINTER(C.c_uint64))), "rmq_set_segments")
 
     # ---- read-back
+    def states(self, first: int = 0, n: int | None = None) -> np.ndarray:
+        """rmq_get_partition_states: the states of partitions [first, first + n) as a structured
+        array of rmq_partition_state (one device copy per field)."""
+        n = self.cfg.num_partitions - first if n is None else n
+        out = np.zeros(n, STATE_DTYPE)
+        _check(self.lib.rmq_get_partition_states(self.h, first, n, _ptr(out)), "rmq_get_partition_states")
+        return out
+
     def state(self, pidx: int) -> dict:
         s = A.RmqPartitionState()
         _check(self.lib.rmq_get_partition_state(self.h, pidx, C.byref(s)), "rmq_get_partition_state")

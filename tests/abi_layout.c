@@ -15,6 +15,7 @@ int main(void) {
   F(rmq_batch, pidx); F(rmq_batch, payload_bytes);
   F(rmq_fetch_res, count); F(rmq_fetch_res, status);
   F(rmq_partition_state, match); F(rmq_partition_state, replica_rank); F(rmq_partition_state, is_leader);
+  F(rmq_partition_state, leader_commit);
   F(rmq_append_stats, rejected_no_space);
   return 0;
 }

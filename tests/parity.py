@@ -111,3 +111,33 @@ def run_ops(dev, ora, cfg, ops, check=True, full_rings=False, parts=None, local_
     # logs and proves nothing
     assert not submitted or appended, "no record was appended: the scenario is vacuous"
     return log
+
+
+def compare_bulk(dev, ora, cfg, local_slots=None, chunk=4096):
+    """compare_state for many partitions: states by one bulk read-back per side
+    (rmq_get_partition_states), then each partition's retained ring window of every local slot, its
+    live index entries and consumer offsets."""
+    P, I = cfg.num_partitions, cfg.index_interval
+    for a in range(0, P, chunk):
+        n = min(chunk, P - a)
+        sd, so = dev.states(a, n), ora.states(a, n)
+        if not np.array_equal(sd, so):
+            bad = [a + i for i in range(n) if sd[i].tobytes() != so[i].tobytes()]
+            p = bad[0]
+            raise AssertionError(f"{len(bad)} partition states differ, first {p}\n gpu={dev.state(p)}\n cpu={ora.state(p)}")
+        for i in range(n):
+            p = a + i
+            st = {"segment_bytes": int(so[i]["segment_bytes"]), "log_start_pos": int(so[i]["log_start_pos"]),
+                  "log_end_pos": int(so[i]["log_end_pos"])}
+            slots = range(cfg.replication_factor) if local_slots is None else local_slots(p)
+            for r in slots:
+                x, y = ring_window(dev, cfg, r, p, st), ring_window(ora, cfg, r, p, st)
+                if not np.array_equal(x, y):
+                    bad = np.flatnonzero(x != y)
+                    raise AssertionError(f"ring p={p} r={r}: {bad.size} bytes differ, first at {bad[0]}")
+            m_lo = -(-st["log_start_pos"] // I)
+            m_hi = st["log_end_pos"] // I
+            if m_hi >= m_lo:
+                cnt = m_hi - m_lo + 1
+                assert np.array_equal(dev.read_index(p, m_lo, cnt), ora.read_index(p, m_lo, cnt)), f"index p={p}"
+            assert np.array_equal(dev.consumer_offsets(p), ora.consumer_offsets(p)), f"consumer offsets p={p}"

@@ -32,25 +32,28 @@ def rank_batches(spec: StreamSpec, rank: int, rounds: int, group: int):
     return [make_batch(spec, 1000 * rank + k) for k in range(rounds * group)]
 
 
-def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None, drop=()):
+def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None, drop=(), lost=()):
     """Regions of every leader to every follower, ingested there; acks back to the leaders (FORMAT.md
     §9 v3: a refused ack leaves a catch-up request for the next round's plan).
     corrupt=(src, dst, byte): flip one byte of that region (byte < 0: from the end of its data
     section, i.e. a payload byte of its last record); skip=(src, dst): drop that region and its
     acks; drop: leaders whose round sends no region (rmq_fault_drop_rounds: their followers miss
-    the round and refuse every entry of it)."""
+    the round and refuse every entry of it); lost: (src, dst) pairs whose region is lost on the way
+    (rmq_fault_isolate: dst misses src's round)."""
     W = len(oras)
     rnd = [o.round_no() for o in oras]
     regions = [[oras[s].round_region(d) if d != s else None for d in range(W)] for s in range(W)]
     for s in drop:
         regions[s] = [None if d == s else np.zeros(0, np.uint8) for d in range(W)]
+    for s, d in lost:
+        regions[s][d] = np.zeros(0, np.uint8)
     for o in oras:
         o.end_round()
     for s in range(W):
         for d in range(W):
             if d == s or (skip and (s, d) == tuple(skip)):
                 continue
-            if regions[s][d].size == 0 and s not in drop:
+            if regions[s][d].size == 0 and s not in drop and (s, d) not in lost:
                 continue
             reg = regions[s][d]
             if corrupt and (s, d) == tuple(corrupt[:2]):
@@ -62,6 +65,35 @@ def exchange_round(oras, keep_regions: bool = False, corrupt=None, skip=None, dr
             acks = oras[d].ingest(s, reg)
             oras[s].apply_acks(d, acks, rnd[s])
     return regions if keep_regions else None
+
+
+DIR = 48  # directory entry bytes of a round region (FORMAT.md §9 v4)
+
+
+def mask_commit(region: np.ndarray) -> np.ndarray:
+    """A region with the leader-commit word of every directory entry zeroed (FORMAT.md §9 v4). A
+    pipelined GPU run plans a round before the acks of the rounds just before it are in (it carries
+    the commit its launch started with), the oracle after them: the word is compared in the synced
+    runs, and masked in the pipelined ones."""
+    if region is None or region.size < 64:
+        return region
+    r = region.copy()
+    n = int(r[4:8].view(np.uint32)[0])
+    for k in range(n):
+        r[64 + DIR * k + 32:64 + DIR * k + 40] = 0
+    return r
+
+
+def notice_round(oras):
+    """The commit notices of a drain (FORMAT.md §9 v4): every leader's {commit, term} per entry to
+    each follower, which learns its leader's commit. The GPU engines exchange them at every drain
+    that had rounds in flight (rmq_sync, and the drain of a placement change)."""
+    W = len(oras)
+    notes = [[oras[s].commit_notice(d) if d != s else None for d in range(W)] for s in range(W)]
+    for s in range(W):
+        for d in range(W):
+            if d != s and len(notes[s][d]):
+                oras[d].apply_notice(s, notes[s][d])
 
 
 def moved_leadership(views, old_leader: int = 0, new_slot: int = 1):
@@ -129,4 +161,5 @@ def run_script_oracle(oras, views, phases, world):
             for b in batches[r]:
                 oras[r].append(b.pidx, b.lens, b.payload)
         regions = exchange_round(oras, keep_regions=True, drop=drop)
+        notice_round(oras)  # every phase ends in a drain (rmq_sync, or the next placement's)
     return regions

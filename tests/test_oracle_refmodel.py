@@ -89,9 +89,14 @@ def test_quorum_commit_rule(oracle_mod):
         assert ora.state(0)["commit"] == 7 and ora.state(0)["high_watermark"] == 7
         ora.ack([0], [4], [50])                                  # clamped to log end 10 -> 9
         assert ora.state(0)["commit"] == 9
-        ora.become_leader(0, 3)                                  # new term: nothing new committed
-        ora.ack([0, 0, 0, 0], [1, 2, 3, 4], [10, 10, 10, 10])
+        ora.become_leader(0, 3)                                  # new term: remote matches reset
+        assert ora.state(0)["commit"] == 9 and ora.state(0)["term_start"] == 10
+        ora.ack([0], [1], [10])                                  # 10,10,0,0,0: no quorum yet
         assert ora.state(0)["commit"] == 9
+        # a quorum holding the log up to term_start in the new term holds the leader-start entry
+        # (jraft's configuration entry, virtual here): the earlier-term records commit with it
+        ora.ack([0], [2], [10])                                  # 10,10,10,0,0 -> 10 >= term_start
+        assert ora.state(0)["commit"] == 10
         ora.append(np.zeros(1, np.uint32), np.ones(1, np.uint32), np.ones(1, np.uint8))
         ora.ack([0, 0], [1, 2], [11, 11])
         assert ora.state(0)["commit"] == 11

@@ -3,7 +3,7 @@ leader's log, bytes and offsets; quorum acks commit; refused rounds (CRC, log mi
 import numpy as np
 import pytest
 
-from repl_sim import exchange_round, place, rank_batches, rank_cfg
+from repl_sim import DIR, exchange_round, place, rank_batches, rank_cfg
 from ripplemq_amd.engine import EngineConfig
 from ripplemq_amd.sharding import rank_view, replica_ranks
 from ripplemq_amd.workload import StreamSpec, make_batch
@@ -363,8 +363,8 @@ def test_consumer_offsets_replicate_and_survive_leader_change(oracle_mod):
 # Byte positions of a region (FORMAT.md §9) a corrupted link may flip: header key sum, directory
 # words of entry 1 (count, bytes/16, first offset, table start, data start/16), the record-table
 # slot of record 3 (its data position), and a payload byte of the last record.
-REGION_FAULTS = {"keysum": 16, "count": 64 + 32 + 0, "bytes16": 64 + 32 + 4, "first": 64 + 32 + 8,
-                 "tstart": 64 + 32 + 16, "dstart16": 64 + 32 + 20, "table_slot": None, "payload": -5}
+REGION_FAULTS = {"keysum": 16, "count": 64 + DIR + 0, "bytes16": 64 + DIR + 4, "first": 64 + DIR + 8,
+                 "tstart": 64 + DIR + 16, "dstart16": 64 + DIR + 20, "table_slot": None, "payload": -5}
 
 
 @pytest.mark.parametrize("what", sorted(REGION_FAULTS))
@@ -379,7 +379,7 @@ def test_corrupted_region_refused_then_caught_up(oracle_mod, what):
     n_entries = oras[0].pair_entries(0, 1)
     at = REGION_FAULTS[what]
     if at is None:
-        at = 64 + 32 * n_entries + 8 * 3 + 4
+        at = 64 + DIR * n_entries + 8 * 3 + 4
     try:
         def rnd(k, **kw):
             for r in range(world):

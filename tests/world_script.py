@@ -1,0 +1,150 @@
+"""Step scripts over a world of replica-log ranks — test infrastructure.
+
+A script is a list of steps, each applied by every rank in order: on the GPU engines (one host
+thread per rank, the in-process transport, as each rank would be driven by its own process over
+RCCL) and on per-rank oracles (tests/repl_sim.py rounds). Steps:
+
+  ("place", views)                  rmq_set_placement of every rank's view (collective)
+  ("commit", {rank: (pidx, consumer, offset)})   leader consumer-offset commits
+  ("round", {rank: [batches]}, faults)          the batches form ONE launch group on every rank,
+        then rmq_sync (rounds, acks, commit notices); faults = {"drop": ranks, "lost": [(src, dst)],
+        "corrupt": (src, dst, at)}
+  ("lead", {rank: [(pidx, term)]})  rmq_become_leader; the status of each call is recorded
+  ("fetch", {rank: (pidx, consumer, max)})      rmq_fetch; results and bytes are recorded
+
+run_oracle / run_gpu return the recorded outcomes per step and rank, so a test compares them and
+then every rank's state, rings, index and consumer offsets.
+"""
+from __future__ import annotations
+
+import threading
+
+import numpy as np
+
+from repl_sim import exchange_round, notice_round, place
+from ripplemq_amd import _abi as A
+from ripplemq_amd.engine import EngineError
+
+
+def _lead(eng, p, t):
+    try:
+        eng.become_leader(int(p), int(t))
+        return A.RMQ_OK
+    except EngineError as ex:
+        return ex.status
+
+
+def run_oracle(oras, views0, script):
+    world = len(oras)
+    for r in range(world):
+        place(oras[r], views0[r], world)
+    out = []
+    for step in script:
+        kind = step[0]
+        rec = [None] * world
+        if kind == "place":
+            for r in range(world):
+                place(oras[r], step[1][r])
+        elif kind == "commit":
+            for r, args in step[1].items():
+                rc, st = oras[r].commit_consumer_offset(*args)
+                rec[r] = (rc, st)
+        elif kind == "round":
+            f = step[2] if len(step) > 2 else {}
+            for r in range(world):
+                for b in step[1].get(r, []):
+                    oras[r].append(b.pidx, b.lens, b.payload)
+            rec = exchange_round(oras, keep_regions=True, drop=f.get("drop", ()), lost=f.get("lost", ()),
+                                 corrupt=f.get("corrupt"))
+            notice_round(oras)
+        elif kind == "lead":
+            for r, items in step[1].items():
+                rec[r] = [_lead(oras[r], p, t) for p, t in items]
+        elif kind == "fetch":
+            for r, (pidx, cons, mx) in step[1].items():
+                rc, res, buf, used = oras[r].fetch(pidx, cons, mx)
+                rec[r] = (rc, res, buf[:used])
+        else:
+            raise ValueError(kind)
+        out.append(rec)
+    return out
+
+
+def run_gpu(engs, hub, views0, script, timeout=240):
+    world = len(engs)
+    out = [[None] * world for _ in script]
+    errs = [None] * world
+
+    def body(r):
+        try:
+            e = engs[r]
+            e.attach_local(hub)
+            place(e, views0[r])
+            for k, step in enumerate(script):
+                kind = step[0]
+                if kind == "place":
+                    place(e, step[1][r])
+                elif kind == "commit":
+                    if r in step[1]:
+                        out[k][r] = e.commit_consumer_offset(*step[1][r])
+                elif kind == "round":
+                    f = step[2] if len(step) > 2 else {}
+                    if r in f.get("drop", ()):
+                        e.fault_drop_rounds(1)
+                    for s, d in f.get("lost", ()):
+                        if s == r:
+                            e.fault_isolate(d, 1)
+                    if f.get("corrupt") and f["corrupt"][0] == r:
+                        e.fault_corrupt(f["corrupt"][1], f["corrupt"][2])
+                    for b in step[1].get(r, []):
+                        e.append_async(b.pidx, b.lens, b.payload)
+                    if not step[1].get(r):  # rounds are collective: an idle rank submits an empty batch
+                        e.append_async(np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+                    e.sync()
+                    out[k][r] = [e.read_outbox(d) if d != r else None for d in range(world)]
+                elif kind == "lead":
+                    if r in step[1]:
+                        out[k][r] = [_lead(e, p, t) for p, t in step[1][r]]
+                elif kind == "fetch":
+                    if r in step[1]:
+                        rc, res, buf, used = e.fetch(*step[1][r])
+                        out[k][r] = (rc, res, buf[:used])
+        except BaseException as ex:  # noqa: BLE001 - reported below
+            errs[r] = ex
+
+    ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+        assert not t.is_alive(), "a rank hung"
+    for r, ex in enumerate(errs):
+        if ex is not None:
+            raise AssertionError(f"rank {r}: {ex!r}") from ex
+    return out
+
+
+def rounds_of(script) -> list[int]:
+    """Indices of the round steps (the GPU side pads idle ranks with an empty batch: for the
+    oracle, a round with no batches on a rank is the same round)."""
+    return [k for k, s in enumerate(script) if s[0] == "round"]
+
+
+def compare_outcomes(script, got, want):
+    """The recorded outcomes of every step: become_leader statuses, fetch results and bytes, the
+    region every leader sent every follower in each round, consumer-commit statuses."""
+    for k, step in enumerate(script):
+        for r in range(len(want[k])):
+            g, w = got[k][r], want[k][r]
+            if step[0] == "round":  # w: the regions rank r sent, by destination
+                for d in range(len(want[k])):
+                    if d != r and w[d] is not None and w[d].size:
+                        assert np.array_equal(g[d], w[d]), f"step {k}: region {r}->{d}"
+            elif step[0] == "lead" and w is not None:
+                assert list(g) == list(w), (k, r, g, w)
+            elif step[0] == "fetch" and w is not None:
+                assert g[0] == w[0], (k, r, g[0], w[0])
+                assert np.array_equal(g[1], w[1]), f"step {k} rank {r} fetch results\n gpu={g[1]}\n cpu={w[1]}"
+                assert np.array_equal(g[2], w[2]), f"step {k} rank {r} fetched bytes"
+            elif step[0] == "commit" and w is not None:
+                assert g[0] == w[0] and np.array_equal(g[1], w[1]), (k, r, g, w)
