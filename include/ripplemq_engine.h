@@ -71,6 +71,7 @@ extern "C" {
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
 #define RMQ_RECORD_HEADER_BYTES 16u
 #define RMQ_RECORD_ALIGN 16u /* records start and end on 16-byte boundaries (FORMAT.md §1) */
+#define RMQ_TICKET_OFFSETS 0x8000000000000000ull /* tickets of rmq_commit_consumer_offset carry this bit */
 
 /* Status codes. Negative = error; RMQ_PENDING is a non-error poll result. */
 enum {
@@ -251,8 +252,16 @@ int rmq_append(rmq_engine* e, const rmq_batch* batch, uint64_t* out_offsets, uin
 int rmq_ack(rmq_engine* e, const uint32_t* pidx, const uint32_t* replica_slot,
             const uint64_t* match, uint32_t n);
 
-/* RMQ_OK if every operation up to `ticket` completed (then commit/hw snapshots of all P
-   partitions are copied to the optional host arrays), RMQ_PENDING if not yet. */
+/* Append tickets: RMQ_OK if every operation up to `ticket` completed (then commit/hw snapshots of all
+   P partitions are copied to the optional host arrays), RMQ_PENDING if not yet.
+   Consumer-offset tickets (RMQ_TICKET_OFFSETS set, from rmq_commit_consumer_offset): RMQ_OK once the
+   consumer-offset row of every partition the call committed to, as of that call or newer, is held
+   by a quorum of the partition's replicas (co-located replicas hold it once applied; a remote one
+   once it accepted a round carrying it, FORMAT.md §8) — the reference's PartitionClosure answering a
+   ConsumerOffsetUpdateRequest after the Raft commit (ConsumerOffsetUpdateRequestProcessor.java:40-49,
+   60, PartitionClosure.java:32-36); RMQ_PENDING until then; RMQ_ENOTLEADER if this engine stopped
+   leading one of those partitions first (the commit may be lost, like a jraft closure failed by a
+   leader change). A resolved offset ticket is forgotten (a second poll: RMQ_EINVAL). Never flushes. */
 int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64_t* hw_out);
 int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out);
 int rmq_sync(rmq_engine* e);
@@ -262,9 +271,11 @@ int rmq_sync(rmq_engine* e);
    leader, unknown partition, bad consumer id). The items reach the device table in order with the
    append stream (one copy on the pipeline stream, no wait for the pipeline): a later rmq_fetch or
    read-back sees them. With a replication transport the partition's row travels to every follower
-   with the next round (FORMAT.md §8, §9): it is on a quorum once that round's acks are in. */
+   with the next round (FORMAT.md §8, §9). ticket (nullable) gets a consumer-offset ticket
+   (RMQ_TICKET_OFFSETS set) that rmq_poll_commit resolves once the accepted items are on a quorum;
+   0 if no item was accepted. */
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
-                               const uint64_t* offset, uint32_t n, int32_t* status);
+                               const uint64_t* offset, uint32_t n, int32_t* status, uint64_t* ticket);
 
 /* Batched consumer fetch: for each request, off = committed consumer offset (default 0),
    returns records [off, min(off + max, high_watermark)) (PartitionStateMachine.java:85-110).

@@ -49,6 +49,7 @@ def load() -> C.CDLL:
         "ro_get_partition_states": (C.c_int, [vp, u32, u32, vp]),
         "ro_commit_notice": (C.c_int, [vp, u32, vp]),
         "ro_apply_notice": (C.c_int, [vp, u32, vp, u32]),
+        "ro_offset_quorum": (C.c_int, [vp, u32, C.POINTER(u64), C.POINTER(u64)]),
         "ro_read_segment": (C.c_int, [vp, u32, u32, u64, u64, vp]),
         "ro_read_index": (C.c_int, [vp, u32, u64, u64, vp]),
         "ro_read_consumer_offsets": (C.c_int, [vp, u32, vp]),
@@ -96,6 +97,9 @@ class OracleEngine:
         self.h = self.lib.ro_create(C.byref(c))
         if not self.h:
             raise ValueError("invalid oracle config")
+        self.last_offset_ticket = 0
+        self._tseq = 0
+        self._tickets: dict[int, list[tuple[int, int]]] = {}
 
     def close(self):
         if self.h:
@@ -247,7 +251,33 @@ class OracleEngine:
         offset = np.ascontiguousarray(offset, np.uint64)
         status = np.zeros(len(pidx), np.int32)
         rc = self.lib.ro_commit_consumer_offset(self.h, _p(pidx), _p(consumer), _p(offset), len(pidx), _p(status))
+        # the engine's consumer-offset ticket: the accepted partitions at their new row versions
+        parts = sorted(set(int(x) for x in pidx[status == 0]))
+        self.last_offset_ticket = 0
+        if parts:
+            self._tseq += 1
+            self.last_offset_ticket = A.RMQ_TICKET_OFFSETS | self._tseq
+            self._tickets[self.last_offset_ticket] = [(p, self.offset_quorum(p)[0]) for p in parts]
         return rc, status
+
+    def offset_quorum(self, p) -> tuple[int, int]:
+        """(row version, newest version a quorum holds) of partition p (FORMAT.md §8)."""
+        v, q = C.c_uint64(), C.c_uint64()
+        rc = self.lib.ro_offset_quorum(self.h, int(p), C.byref(v), C.byref(q))
+        if rc:
+            raise EngineError(rc, "oracle offset_quorum")
+        return int(v.value), int(q.value)
+
+    def poll_offsets(self, ticket) -> int:
+        """As rmq_poll_commit of a consumer-offset ticket: RMQ_OK once every partition's row is on a
+        quorum at the ticket's version, RMQ_ENOTLEADER if leadership moved first, else RMQ_PENDING."""
+        want = self._tickets[ticket]
+        done = all(self.offset_quorum(p)[1] >= v for p, v in want)
+        lost = not done and any(self.offset_quorum(p)[1] < v and not self.state(p)["is_leader"] for p, v in want)
+        if not done and not lost:
+            return A.RMQ_PENDING
+        del self._tickets[ticket]
+        return A.RMQ_OK if done else A.RMQ_ENOTLEADER
 
     def fetch(self, pidx, consumer, max_records, out_cap=None):
         n = len(pidx)

@@ -123,6 +123,10 @@ typedef struct {
   uint64_t rq_off[RMQ_MAX_RF], rq_pos[RMQ_MAX_RF], rq_r1[RMQ_MAX_RF], cu[RMQ_MAX_RF];
   uint8_t dirty; /* consumer offsets changed since the last round (the row travels with it) */
   uint64_t lc;   /* follower: the newest leader commit learned (round entries, commit notices) */
+  /* consumer-offset rows on a quorum (offset tickets, FORMAT.md §8): the leader's row version (one
+     per commit call touching the partition), per replica slot the newest version its follower
+     acknowledged, and the version the last round carried to it (0: no row) */
+  uint64_t cver, eackv[RMQ_MAX_RF], rowv[RMQ_MAX_RF];
 } ro_part;
 
 struct ro_engine {
@@ -289,6 +293,10 @@ int ro_set_replicas(ro_engine* e, uint32_t p, const uint32_t* ranks, uint32_t rf
   s->leader_slot = leader_slot;
   s->is_leader = lead;
   reset_catchup(s);
+  /* the followers acknowledge the rows afresh under the new placement: a led partition with
+     committed offsets sends its row with the next round */
+  for (uint32_t r = 0; r < RMQ_MAX_RF; ++r) s->eackv[r] = s->rowv[r] = 0;
+  if (lead && s->cver && e->world > 1) s->dirty = 1;
   return RMQ_OK;
 }
 
@@ -318,6 +326,7 @@ static void become_leader_apply(ro_engine* e, uint32_t p, uint64_t term) {
   s->term = term;
   s->term_start = s->leo; /* jraft: pendingIndex = lastLogIndex + 1 at leader start */
   for (uint32_t r = 0; r < RF; ++r) s->match[r] = s->ranks[r] == e->cfg.rank ? s->leo : 0;
+  for (uint32_t r = 0; r < RF; ++r) s->eackv[r] = 0; /* rows acknowledged afresh in the new term */
   commit_eval(e, s);  /* the virtual leader-start entry: a local quorum holds it at once */
   s->dirty = 1;       /* the new leader's consumer offsets go to every follower with the next round */
   reset_catchup(s);
@@ -714,6 +723,7 @@ int ro_ack(ro_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint6
 int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                               const uint64_t* offset, uint32_t n, int32_t* status) {
   int rc = RMQ_OK;
+  memset(e->touched, 0, e->cfg.num_partitions); /* the row version moves once per call */
   for (uint32_t i = 0; i < n; ++i) {
     int st = RMQ_OK;
     if (pidx[i] >= e->cfg.num_partitions)
@@ -725,6 +735,10 @@ int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t
     else {
       e->parts[pidx[i]].cons[consumer[i]] = offset[i];
       e->parts[pidx[i]].dirty = 1; /* the row travels with the next replication round (§9) */
+      if (!e->touched[pidx[i]]) {
+        e->touched[pidx[i]] = 1;
+        e->parts[pidx[i]].cver++;
+      }
     }
     if (status) status[i] = st;
     if (st && !rc) rc = st;
@@ -1119,6 +1133,7 @@ void ro_end_round(ro_engine* e) {
         const uint32_t sl = v[k].slot;
         s->nx_off[sl] = pl[k].nx_off;
         s->nx_pos[sl] = pl[k].nx_pos;
+        s->rowv[sl] = pl[k].row ? s->cver : 0; /* the row version this round carries to the slot */
         if (pl[k].set_cu) s->cu[sl] = e->round_no;
         e->counters[4] += pl[k].catchup ? 1u : 0u;
         e->counters[5] += pl[k].detached ? 1u : 0u;
@@ -1452,6 +1467,7 @@ int ro_apply_acks(ro_engine* e, uint32_t dst, const uint64_t* acks, uint32_t n_a
     }
     const uint64_t m = a < s->leo ? a : s->leo;
     if (m > s->match[sl]) s->match[sl] = m;
+    if (s->rowv[sl] > s->eackv[sl]) s->eackv[sl] = s->rowv[sl];
   }
   for (uint32_t k = 0; k < n; ++k) commit_eval(e, &e->parts[v[k].p]);
   free(v);
@@ -1488,6 +1504,25 @@ int ro_apply_notice(ro_engine* e, uint32_t src, const uint64_t* in, uint32_t n_i
     learn_commit(s, in[2 * k]);
   }
   free(v);
+  return RMQ_OK;
+}
+
+/* The row version of partition p and the newest one a quorum of its replicas holds (co-located
+   slots: the leader's own; a remote slot: what its follower acknowledged). */
+int ro_offset_quorum(ro_engine* e, uint32_t p, uint64_t* cver, uint64_t* cq) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  const ro_part* s = &e->parts[p];
+  const uint32_t RF = e->cfg.replication_factor, k = RF / 2 + 1;
+  uint64_t m[RMQ_MAX_RF];
+  for (uint32_t r = 0; r < RF; ++r) m[r] = s->ranks[r] == e->cfg.rank ? s->cver : s->eackv[r];
+  for (uint32_t i = 1; i < RF; ++i)
+    for (uint32_t j = i; j > 0 && m[j - 1] < m[j]; --j) {
+      uint64_t t = m[j];
+      m[j] = m[j - 1];
+      m[j - 1] = t;
+    }
+  *cver = s->cver;
+  *cq = m[k - 1];
   return RMQ_OK;
 }
 

@@ -92,6 +92,9 @@ uint32_t ro_pair_entries(ro_engine* e, uint32_t src, uint32_t dst);
 /* Commit notices (a drain's heartbeat, FORMAT.md §9 v4): 2 words per entry of the pair {commit, term}. */
 int ro_commit_notice(ro_engine* e, uint32_t dst, uint64_t* out);
 int ro_apply_notice(ro_engine* e, uint32_t src, const uint64_t* in, uint32_t n);
+/* Consumer-offset rows on a quorum (offset tickets, FORMAT.md §8): partition p's row version and the
+   newest version a quorum of its replicas holds. */
+int ro_offset_quorum(ro_engine* e, uint32_t p, uint64_t* cver, uint64_t* cq);
 /* [0] records ingested, [1] entries refused (CRC), [2] refused (log / term / missed round),
    [3] bytes ingested, [4] catch-up entries sent, [5] detached entry plans (gap beyond the ring) */
 void ro_counters(ro_engine* e, uint64_t* out /* [6] */);

@@ -20,6 +20,7 @@ RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
 RMQ_RECORD_HEADER_BYTES = 16
+RMQ_TICKET_OFFSETS = 1 << 63
 
 RMQ_OK = 0
 RMQ_PENDING = 1
@@ -121,7 +122,7 @@ _SIGS = {
     "rmq_poll_commit": (C.c_int, [vp, u64, vp, vp]),
     "rmq_ticket_stats": (C.c_int, [vp, u64, C.POINTER(RmqAppendStats)]),
     "rmq_sync": (C.c_int, [vp]),
-    "rmq_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp]),
+    "rmq_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp, C.POINTER(u64)]),
     "rmq_fetch": (C.c_int, [vp, vp, u32, u32, vp, u64, vp, C.POINTER(u64)]),
     "rmq_get_partition_state": (C.c_int, [vp, u32, C.POINTER(RmqPartitionState)]),
     "rmq_get_partition_states": (C.c_int, [vp, u32, u32, vp]),

@@ -36,19 +36,41 @@ __global__ void become_leader_kernel(DevState st, u32 only) {
   const u64 leo = st.leo[p];
   st.term_start[p] = leo;
   const u32 lm = st.local_mask[p];
-  for (u32 r = 0; r < st.RF; ++r) st.match[(u64)p * st.RF + r] = (lm >> r & 1u) ? leo : 0ull;
+  for (u32 r = 0; r < st.RF; ++r) {
+    st.match[(u64)p * st.RF + r] = (lm >> r & 1u) ? leo : 0ull;
+    // the followers acknowledge the new leader's rows afresh (tickets of the new term)
+    if (st.outidx && st.eackv && !(lm >> r & 1u)) {
+      const u32 e = st.outidx[(u64)p * st.RF + r];
+      if (e != ~0u) st.eackv[e] = 0ull;
+    }
+  }
   commit_rule(st, p);
   st.cdirty[p] = 1u;
+  st.cq[p] = row_quorum(st, p);
 }
 
 __global__ void consumer_apply_kernel(ConsumerCommitArgs a) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.n) return;
-  a.st.cons[(u64)a.pidx[i] * a.st.C + a.consumer[i]] = a.offset[i];
-  a.st.cdirty[a.pidx[i]] = 1u;  // the row travels with the next replication round (FORMAT.md §9)
+  const u32 p = a.pidx[i];
+  a.st.cons[(u64)p * a.st.C + a.consumer[i]] = a.offset[i];
+  a.st.cdirty[p] = 1u;  // the row travels with the next replication round (FORMAT.md §9)
+  // the row's new version (every item of p writes the same words); co-located replicas hold it now
+  a.st.cver[p] = a.ver[i];
+  a.st.cq[p] = row_quorum(a.st, p);
+}
+
+// Every partition's row quorum afresh (after a placement change reset the followers' row acks).
+__global__ void row_quorum_all_kernel(DevState st) {
+  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < st.P) st.cq[p] = row_quorum(st, p);
 }
 
 static inline dim3 grid_for(u32 n, u32 b) { return dim3((n + b - 1) / b ? (n + b - 1) / b : 1); }
+
+void launch_row_quorum_all(const DevState& st, hipStream_t s) {
+  hipLaunchKernelGGL(row_quorum_all_kernel, grid_for(st.P, 256), dim3(256), 0, s, st);
+}
 
 void launch_commit_all(const DevState& st, hipStream_t s) {
   hipLaunchKernelGGL(commit_all_kernel, grid_for(st.P, 256), dim3(256), 0, s, st);

@@ -448,7 +448,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, e->d_crc,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq, e->d_crc,
                              e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_csum, e->d_fetch_out,
                              e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (const StateSet& z : e->sets) {
@@ -667,6 +667,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&s.cdirty, P));
   CREATE_TRY(dalloc(&s.lcommit, P));
+  CREATE_TRY(dalloc(&s.cver, P));
+  CREATE_TRY(dalloc(&s.cq, P));
+  e->cver.assign(P, 0ull);
   CREATE_TRY(dalloc(&e->d_rlate, P));
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
@@ -1056,9 +1059,34 @@ int rmq_ack(rmq_engine* e, const uint32_t* pidx, const uint32_t* slot, const uin
   return drain(e);
 }
 
+// A consumer-offset ticket (RMQ_TICKET_OFFSETS): are its partitions' rows on a quorum?
+int poll_offsets(rmq_engine* e, uint64_t ticket) {
+  auto it = std::find_if(e->off_tickets.begin(), e->off_tickets.end(),
+                         [ticket](const auto& x) { return x.first == ticket; });
+  if (it == e->off_tickets.end()) return RMQ_EINVAL;  // unknown, or resolved already
+  int rc = quiesce(e);  // the commit kernels and the ack folds issued so far (no flush)
+  if (rc) return rc;
+  const size_t P = e->cfg.num_partitions;
+  std::vector<uint64_t> cq(P);
+  HIP_TRY(hipMemcpy(cq.data(), e->st.cq, P * 8, hipMemcpyDeviceToHost));
+  bool done = true, lost = false;
+  for (const auto& pv : it->second) {
+    if (cq[pv.first] >= pv.second) continue;
+    done = false;
+    if (!e->is_leader[pv.first]) lost = true;  // leadership moved before its row reached a quorum
+  }
+  if (!done && !lost) return RMQ_PENDING;
+  e->off_tickets.erase(it);
+  return done ? RMQ_OK : RMQ_ENOTLEADER;
+}
+
 int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64_t* hw_out) {
   if (!e) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
+  if (ticket & RMQ_TICKET_OFFSETS) {
+    HIP_TRY(hipSetDevice(e->device));
+    return poll_offsets(e, ticket);
+  }
   if (ticket > e->last_ticket) return RMQ_EINVAL;  // never issued
   HIP_TRY(hipSetDevice(e->device));
   if (ticket) {
@@ -1115,9 +1143,10 @@ int rmq_sync(rmq_engine* e) {
 }
 
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
-                               const uint64_t* offset, uint32_t n, int32_t* status) {
+                               const uint64_t* offset, uint32_t n, int32_t* status, uint64_t* ticket) {
   if (!e) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);
+  if (ticket) *ticket = 0;
   if (!n) return RMQ_OK;
   if (!pidx || !consumer || !offset) return RMQ_EINVAL;
   std::vector<uint32_t> vp, vc;
@@ -1170,6 +1199,28 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
     vc.erase(vc.begin(), vc.begin() + k);
     vo.erase(vo.begin(), vo.begin() + k);
   }
+  // the new row version of every partition the call commits to (one per call), and the ticket's
+  // (partition, version) pairs
+  std::vector<uint64_t> vv(vp.size());
+  std::vector<std::pair<uint32_t, uint64_t>> tv;
+  {
+    if (e->cstamp.size() != e->cfg.num_partitions) {
+      e->cstamp.assign(e->cfg.num_partitions, 0u);
+      e->cstamp_gen = 0;
+    }
+    if (++e->cstamp_gen == 0) {
+      std::fill(e->cstamp.begin(), e->cstamp.end(), 0u);
+      e->cstamp_gen = 1;
+    }
+    for (size_t i = 0; i < vp.size(); ++i) {
+      const uint32_t p = vp[i];
+      if (e->cstamp[p] != e->cstamp_gen) {  // the partition's first item in this call
+        e->cstamp[p] = e->cstamp_gen;
+        tv.emplace_back(p, ++e->cver[p]);
+      }
+      vv[i] = e->cver[p];
+    }
+  }
   HIP_TRY(hipSetDevice(e->device));
   // no flush and no wait for the pipeline (it never reads the table): the items go to the device
   // with one copy on the pipeline stream, behind the launches issued so far, from a staging slot
@@ -1184,8 +1235,8 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
     cs.h = cs.d = nullptr;
     cs.cap = 0;
     const uint32_t cap = std::max<uint32_t>(m, 4096);
-    HIP_TRY(hipHostMalloc((void**)&cs.h, 16ull * cap, 0));
-    int rc = dalloc(&cs.d, 16ull * cap);
+    HIP_TRY(hipHostMalloc((void**)&cs.h, 24ull * cap, 0));
+    int rc = dalloc(&cs.d, 24ull * cap);
     if (rc) return rc;
     if (!cs.ev) HIP_TRY(hipEventCreateWithFlags(&cs.ev, hipEventDisableTiming));
     cs.cap = cap;
@@ -1193,17 +1244,23 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   std::memcpy(cs.h, vp.data(), 4ull * m);
   std::memcpy(cs.h + 4ull * cs.cap, vc.data(), 4ull * m);
   std::memcpy(cs.h + 8ull * cs.cap, vo.data(), 8ull * m);
-  HIP_TRY(hipMemcpyAsync(cs.d, cs.h, 16ull * cs.cap, hipMemcpyHostToDevice, e->main_s));
+  std::memcpy(cs.h + 16ull * cs.cap, vv.data(), 8ull * m);
+  HIP_TRY(hipMemcpyAsync(cs.d, cs.h, 24ull * cs.cap, hipMemcpyHostToDevice, e->main_s));
   ConsumerCommitArgs a{};
   a.st = e->st;
   a.pidx = reinterpret_cast<const uint32_t*>(cs.d);
   a.consumer = reinterpret_cast<const uint32_t*>(cs.d + 4ull * cs.cap);
   a.offset = reinterpret_cast<const uint64_t*>(cs.d + 8ull * cs.cap);
+  a.ver = reinterpret_cast<const uint64_t*>(cs.d + 16ull * cs.cap);
   a.n = m;
   launch_consumer_commit(a, e->main_s);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(cs.ev, e->main_s));
   cs.used = true;
+  if (ticket) {
+    *ticket = RMQ_TICKET_OFFSETS | ++e->off_ticket_seq;
+    e->off_tickets.emplace_back(*ticket, std::move(tv));
+  }
   const int rc = check_err(e);
   return rc ? rc : rc_all;
 }

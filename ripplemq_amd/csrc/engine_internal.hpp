@@ -151,6 +151,7 @@ struct XchgSet {
   uint64_t* h_sizes = nullptr; // pinned copy
   uint64_t* ackout = nullptr;  // [n_in][2]
   uint64_t* ackin = nullptr;   // [n_out][2]
+  uint64_t* rowv = nullptr;    // [n_out] consumer-offset row version each entry of the round carries
   uint32_t* count = nullptr;   // stage-2 arrival counter
   hipEvent_t ev_s2 = nullptr, ev_s3 = nullptr, ev_sz = nullptr, ev_x = nullptr;
   uint64_t applied_launch = 0; // launch that ran the group's stage 3
@@ -190,6 +191,7 @@ struct Replication {
   uint32_t* d_dflag = nullptr;   // [world]
   uint64_t* d_nout = nullptr;    // [n_out][2] commit notices sent {commit, term} (FORMAT.md §9 v4)
   uint64_t* d_nin = nullptr;     // [n_in][2] commit notices received
+  uint64_t* d_eackv = nullptr;   // [n_out] row version each follower acknowledged (offset tickets)
   hipEvent_t ev_notice = nullptr;
   uint64_t dcap = 0;             // outbox bytes per destination
   uint64_t reserve = 0;          // catch-up bytes per destination
@@ -324,6 +326,13 @@ struct rmq_engine {
   uint32_t cslot_next = 0;
   std::vector<uint32_t> lww_stamp;  // [P * C] generation of the last commit item seen per slot
   uint32_t lww_gen = 0;
+  // consumer-offset tickets (rmq_commit_consumer_offset): the row version of every partition (host
+  // mirror of DevState::cver) and, per pending ticket, the (partition, version) pairs it waits for
+  std::vector<uint64_t> cver;
+  std::vector<uint32_t> cstamp;  // [P] generation of the last call that bumped the version
+  uint32_t cstamp_gen = 0;
+  uint64_t off_ticket_seq = 0;
+  std::deque<std::pair<uint64_t, std::vector<std::pair<uint32_t, uint64_t>>>> off_tickets;
   // ack scratch
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;

@@ -107,6 +107,7 @@ struct XPlanArgs {
   const uint64_t* ackin;     // acks applied in this launch, [n_out][2], or null
   uint64_t acks_round;       // the round they answer
   uint32_t* dirty;           // [P] consumer offsets changed since the last round (cleared by the plan)
+  uint64_t* rowv;            // [n_out] this round: the row version each entry carries (0: no row)
   XCatch* xc;                // [n_out] catch-up list of the group
   uint32_t* xc_n;            // [2] {catch-up entries, copy items}
   uint64_t* counters;        // [3] leader: catch-up entries planned, detached entry plans, general plans
@@ -140,6 +141,11 @@ struct DevState {
                          //   launch L + 1 carries it in its directory (one value per round, whatever
                          //   that launch's partition threads fold in meanwhile)
   uint32_t csnap_slot;   // the slot of the last launch issued (control kernels write it)
+  // consumer-offset rows on a quorum (rmq_commit_consumer_offset tickets, FORMAT.md §8)
+  uint64_t* cver;        // [P] leader: version of the partition's row (one per commit call touching it)
+  uint64_t* cq;          // [P] leader: the newest row version a quorum of its replicas holds
+  const uint32_t* outidx;  // [P][RF] out entry of (partition, remote slot), ~0: none (transport), or null
+  uint64_t* eackv;       // [n_out] newest row version the entry's follower acknowledged, or null
   uint64_t rstride;      // bytes per replica region (the pool)
   uint32_t P, RF, C;
   uint32_t icap_mul;     // index entries per interval of ring (2 * group + 2)
@@ -240,6 +246,7 @@ struct PipeArgs {
   const XEntry* xe3;       // stage 3's group: entry placement
   uint8_t* outbox3;        // stage 3's group: its outbox
   const uint64_t* ackin;   // acks of an earlier group, by out entry [n_out][2] (partition threads), or null
+  const uint64_t* ackrowv; // the row versions that group's round carried [n_out]
   uint64_t acks_round;     // the round they answer
   uint64_t* xreq;          // catch-up requests (partition threads write them when no plan runs)
   const XCatch* xc3;       // stage 3's group: its catch-up list and counts (catch-up waves)
@@ -280,6 +287,7 @@ struct ConsumerCommitArgs {  // one item per (partition, consumer): the host res
   const uint32_t* pidx;
   const uint32_t* consumer;
   const uint64_t* offset;
+  const uint64_t* ver;     // the partition's new row version (the same for every item of a partition)
   uint32_t n;
   uint32_t pad;
 };
@@ -339,6 +347,7 @@ struct AckApplyArgs {
   DevState st;
   const uint32_t* outidx;
   const uint64_t* ackin;     // [n_out][2]
+  const uint64_t* rowv;      // [n_out] the row versions that round carried
   uint64_t* xreq;            // refused acks become catch-up requests
   uint64_t acks_round;
 };
@@ -363,6 +372,7 @@ void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
 void preload_fetch_kernels();
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
+void launch_row_quorum_all(const DevState& st, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
 // chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))

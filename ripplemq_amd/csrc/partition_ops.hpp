@@ -14,7 +14,8 @@ namespace rmq {
 // the new term (its match is reset to 0 at leader start and only moves by acks of that term); a
 // quorum holding it commits every earlier-term record before it (Raft's current-term rule, FORMAT.md
 // §6). hw (consumer-visible end) = commit.
-__device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u64 commit, u64 term_start) {
+// k-th largest of a replica row, k = RF/2 + 1 (compare-exchange network in registers).
+__device__ __forceinline__ u64 quorum_value(const u64 (&row)[kMaxRF], u32 RF) {
   u64 m[kMaxRF];
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) m[r] = r < RF ? row[r] : 0ull;
@@ -30,16 +31,46 @@ __device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u
   u64 N = 0;
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) N = (r == k - 1) ? m[r] : N;
+  return N;
+}
+
+__device__ __forceinline__ u64 quorum_commit(const u64 (&row)[kMaxRF], u32 RF, u64 commit, u64 term_start) {
+  const u64 N = quorum_value(row, RF);
   return (N > commit && N >= term_start) ? N : commit;
+}
+
+// The newest consumer-offset row version a quorum of partition p's replicas holds (FORMAT.md §8):
+// co-located slots hold the leader's own (cver), a remote slot what its follower acknowledged.
+__device__ __forceinline__ u64 row_quorum(const DevState& st, u32 p) {
+  u64 v[kMaxRF];
+  const u64 own = st.cver[p];
+  const u32 lm = st.local_mask[p];
+#pragma unroll
+  for (u32 r = 0; r < kMaxRF; ++r) {
+    u64 x = 0;
+    if (r < st.RF) {
+      if ((lm >> r) & 1u) {
+        x = own;
+      } else if (st.outidx && st.eackv) {
+        const u32 e = st.outidx[(u64)p * st.RF + r];
+        x = e == ~0u ? 0ull : st.eackv[e];
+      }
+    }
+    v[r] = x;
+  }
+  return quorum_value(v, st.RF);
 }
 
 // Remote replica acks of one replication round (FORMAT.md §9 v3, [n_out][2] {log end | status << 62,
 // log end position}) into the partition's matchIndex row: an accepted ack moves match = max(match,
 // min(ack, log end)) for its slot; a refused one becomes a catch-up request {offset, position,
-// round + 1} when xreq is given (no plan reads these acks itself). True if a slot moved.
-__device__ __forceinline__ bool apply_acks(const DevState& st, u32 p, const u32* outidx, const u64* ackin, u64 leo,
-                                           u64 (&row)[kMaxRF], u64* xreq, u64 acks_round) {
-  bool moved = false;
+// round + 1} when xreq is given (no plan reads these acks itself). An accepted ack also acknowledges
+// the consumer-offset row version the round carried to that follower (rowv, 0: none).
+// Returns bit 0: a match moved, bit 1: an acknowledged row version moved.
+constexpr u32 kAckMatch = 1u, kAckRow = 2u;
+__device__ __forceinline__ u32 apply_acks(const DevState& st, u32 p, const u32* outidx, const u64* ackin, u64 leo,
+                                          u64 (&row)[kMaxRF], u64* xreq, u64 acks_round, const u64* rowv) {
+  u32 moved = 0;
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) {
     if (r >= st.RF) continue;
@@ -58,7 +89,14 @@ __device__ __forceinline__ bool apply_acks(const DevState& st, u32 p, const u32*
     if (a > row[r]) {
       row[r] = a;
       st.match[(u64)p * st.RF + r] = a;
-      moved = true;
+      moved |= kAckMatch;
+    }
+    if (rowv && st.eackv) {
+      const u64 v = rowv[e];
+      if (v > st.eackv[e]) {
+        st.eackv[e] = v;
+        moved |= kAckRow;
+      }
     }
   }
   return moved;

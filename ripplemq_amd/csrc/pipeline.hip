@@ -426,6 +426,8 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
     d.flags |= kDecReq | kDecRow;
   }
   if (st.cdirty[p]) d.flags |= kDecRow;
+  // the row version the entry carries if it carries a row (a general plan stores the final word)
+  X.rowv[e] = (d.flags & kDecRow) ? st.cver[p] : 0ull;
   if (d.f_off >= Boff) {
     d.f_off = Boff;
     d.f_pos = Bpos;
@@ -751,7 +753,10 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
           }
         }
         // (row entries and the data section offset need the region totals: pass 2)
-        if (in) X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
+        if (in) {
+          X.xdec[e].pad = (row ? 1u + (u32)(exb & 0xFFFFFull) : 0u) | (rebase ? kRowRebase : 0u);  // row index + 1
+          X.rowv[e] = row ? st.cver[p] : 0ull;  // (the version of the row pass 2 writes)
+        }
         if (st_it) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           PIPE_STAMP(7);
@@ -1587,7 +1592,11 @@ __device__ __forceinline__ void partition_threads(const PipeArgs& A, u32 p) {
         }
     }
     // followers' acks of an earlier group (replication transport, FORMAT.md §9)
-    if (A.ackin) moved |= apply_acks(st, p, A.outidx, A.ackin, leo, row, A.xreq, A.acks_round);
+    if (A.ackin) {
+      const u32 fl = apply_acks(st, p, A.outidx, A.ackin, leo, row, A.xreq, A.acks_round, A.ackrowv);
+      moved |= (fl & kAckMatch) != 0u;
+      if (fl & kAckRow) st.cq[p] = row_quorum(st, p);  // consumer-offset rows on a quorum (tickets)
+    }
     if (moved) {
       const u64 c = quorum_commit(row, RF, commit0, ts);
       st.commit[p] = c;

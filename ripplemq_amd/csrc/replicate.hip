@@ -564,7 +564,9 @@ __global__ void ack_apply_kernel(AckApplyArgs a) {
   u64 row[kMaxRF];
 #pragma unroll
   for (u32 r = 0; r < kMaxRF; ++r) row[r] = r < st.RF ? st.match[(u64)p * st.RF + r] : 0ull;
-  if (apply_acks(st, p, a.outidx, a.ackin, st.leo[p], row, a.xreq, a.acks_round)) {
+  const u32 fl = apply_acks(st, p, a.outidx, a.ackin, st.leo[p], row, a.xreq, a.acks_round, a.rowv);
+  if (fl & kAckRow) st.cq[p] = row_quorum(st, p);
+  if (fl & kAckMatch) {
     const u64 c = quorum_commit(row, st.RF, st.commit[p], st.term_start[p]);
     st.commit[p] = c;
     st.hw[p] = c;

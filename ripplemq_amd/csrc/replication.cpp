@@ -52,14 +52,14 @@ uint64_t entry_hash(uint64_t key, uint32_t slot) { return key * RMQ_MAX_RF + slo
 
 void free_set_buffers(Replication* r) {
   for (XchgSet& x : r->sets) {
-    void* bufs[] = {x.outbox, x.inbox, x.xe, x.xc, x.xc_n, x.sizes, x.ackout, x.ackin};
+    void* bufs[] = {x.outbox, x.inbox, x.xe, x.xc, x.xc_n, x.sizes, x.ackout, x.ackin, x.rowv};
     for (void* p : bufs)
       if (p) hipFree(p);
     x.outbox = x.inbox = nullptr;
     x.xe = nullptr;
     x.xc = nullptr;
     x.xc_n = nullptr;
-    x.sizes = x.ackout = x.ackin = nullptr;
+    x.sizes = x.ackout = x.ackin = x.rowv = nullptr;
   }
 }
 
@@ -250,9 +250,11 @@ void repl_free(rmq_engine* e) {
   void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_keysum_in, r->d_outidx, r->d_xi_p, r->d_xi_slot,
                   r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
                   r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_xtot, r->d_dflag, r->d_lastg,
-                  r->d_nout, r->d_nin};
+                  r->d_nout, r->d_nin, r->d_eackv};
   for (void* p : bufs)
     if (p) hipFree(p);
+  e->st.outidx = nullptr;
+  e->st.eackv = nullptr;
   if (r->ev_notice) hipEventDestroy(r->ev_notice);
   if (r->xchg_s) hipStreamDestroy(r->xchg_s);
   delete r->xport;
@@ -416,8 +418,33 @@ int repl_set_lists(rmq_engine* e) {
     if (!rc) rc = dalloc(&x.sizes, 4ull * W);
     if (!rc) rc = dalloc(&x.ackout, 2 * n_in);
     if (!rc) rc = dalloc(&x.ackin, 2 * n_out);
+    if (!rc) rc = dalloc(&x.rowv, n_out);
     if (rc) return rc;
   }
+  // consumer-offset rows: the followers acknowledge them afresh under the new lists (the rows of
+  // every led partition with committed offsets go out with the next round) and every partition's
+  // row quorum is recomputed (pending offset tickets wait for those rounds' acks)
+  if (r->d_eackv) hipFree(r->d_eackv);
+  r->d_eackv = nullptr;
+  rc = dalloc(&r->d_eackv, n_out);
+  if (rc) return rc;
+  e->st.outidx = r->d_outidx;
+  e->st.eackv = r->d_eackv;
+  {
+    std::vector<uint32_t> dirty(P, 0u);
+    bool any = false;
+    for (uint32_t p = 0; p < P; ++p)
+      if (e->is_leader[p] && e->cver[p]) dirty[p] = 1u, any = true;
+    if (any) {
+      std::vector<uint32_t> cur(P);
+      HIP_TRY(hipMemcpy(cur.data(), e->st.cdirty, P * 4ull, hipMemcpyDeviceToHost));
+      for (uint32_t p = 0; p < P; ++p) dirty[p] |= cur[p];
+      HIP_TRY(hipMemcpy(e->st.cdirty, dirty.data(), P * 4ull, hipMemcpyHostToDevice));
+    }
+  }
+  launch_row_quorum_all(e->st, e->main_s);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(e->main_s));
   return reset_catchup(e);
 }
 
@@ -453,6 +480,7 @@ void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const Gro
   // the commit the round carries: the slot of the launch before this one (launch_seq not yet advanced)
   a.xp2.csnap = e->st.csnap + (size_t)(e->launch_seq & 1ull) * e->cfg.num_partitions;
     a.xp2.dirty = e->st.cdirty;
+    a.xp2.rowv = x.rowv;
     a.xp2.xc = x.xc;
     a.xp2.xc_n = x.xc_n;
     a.xp2.counters = r->d_counters + 4;
@@ -477,6 +505,7 @@ int repl_before_launch(rmq_engine* e, PipeArgs& a) {
   HIP_TRY(hipStreamWaitEvent(e->main_s, r->sets[s].ev_x, 0));
   if (!r->xo_p.empty()) {
     a.ackin = r->sets[s].ackin;
+    a.ackrowv = r->sets[s].rowv;
     a.acks_round = r->sets[s].round;
     if (a.xp2.n_out) {  // the plan of this launch turns refusals into catch-up verdicts itself
       a.xp2.ackin = a.ackin;
@@ -582,6 +611,7 @@ int repl_drain(rmq_engine* e) {
       a.st = e->st;
       a.outidx = r->d_outidx;
       a.ackin = x.ackin;
+      a.rowv = x.rowv;
       a.xreq = r->d_xreq;
       a.acks_round = x.round;
       launch_ack_apply(a, e->main_s);

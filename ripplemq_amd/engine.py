@@ -93,6 +93,7 @@ class Engine:
         self._dticket = C.c_uint64()
         self._dargs = (C.byref(self._dbatch), C.byref(self._dticket))
         self.transport = False  # a replication transport is attached (rounds are collective)
+        self.last_offset_ticket = 0
 
     def close(self) -> None:
         if getattr(self, "h", None):
@@ -270,15 +271,27 @@ class Engine:
         _check(self.lib.rmq_ack(self.h, _ptr(pidx), _ptr(slot), _ptr(match), len(pidx)), "rmq_ack")
 
     def commit_consumer_offset(self, pidx, consumer, offset) -> tuple[int, np.ndarray]:
+        """rmq_commit_consumer_offset: (rc, per-item status); the call's ticket (0 if no item was
+        accepted) is in self.last_offset_ticket, for poll_offsets."""
         pidx = np.ascontiguousarray(pidx, np.uint32)
         consumer = np.ascontiguousarray(consumer, np.uint32)
         offset = np.ascontiguousarray(offset, np.uint64)
         status = np.zeros(len(pidx), np.int32)
+        t = C.c_uint64()
         rc = self.lib.rmq_commit_consumer_offset(self.h, _ptr(pidx), _ptr(consumer), _ptr(offset),
-                                                 len(pidx), _ptr(status))
+                                                 len(pidx), _ptr(status), C.byref(t))
         if rc in (A.RMQ_EDEVICE, A.RMQ_ENOMEM):
             raise EngineError(rc, "rmq_commit_consumer_offset")
+        self.last_offset_ticket = int(t.value)
         return rc, status
+
+    def poll_offsets(self, ticket: int) -> int:
+        """rmq_poll_commit of a consumer-offset ticket: RMQ_OK (the rows are on a quorum),
+        RMQ_PENDING, or RMQ_ENOTLEADER (leadership moved first: the commit may be lost)."""
+        rc = self.lib.rmq_poll_commit(self.h, ticket, None, None)
+        if rc not in (A.RMQ_OK, A.RMQ_PENDING, A.RMQ_ENOTLEADER):
+            raise EngineError(rc, "rmq_poll_commit (offsets)")
+        return rc
 
     def fetch(self, pidx, consumer, max_records, out_cap: int | None = None):
         n = len(pidx)

@@ -87,6 +87,7 @@ class ConsumerOffsetUpdateRequest:
 class ConsumerOffsetUpdateResponse:
     success: bool = False
     errorMsg: str | None = None
+    ticket: int = 0  # COMMIT_PENDING: the engine's offset ticket (PartitionBroker.offset_update_done)
 
     def isSuccess(self) -> bool:
         return self.success
@@ -262,12 +263,27 @@ class PartitionBroker:
         if idx:
             _, status = self.engine.commit_consumer_offset(np.asarray(p, np.uint32), np.asarray(c, np.uint32),
                                                            np.asarray(o, np.uint64))
+            # the reference answers from the Raft closure, once the update is committed
+            # (ConsumerOffsetUpdateRequestProcessor.java:40-49,60): success only when the rows are on a
+            # quorum (rmq_poll_commit of the call's offset ticket), else COMMIT_PENDING with the ticket
+            ticket = self.engine.last_offset_ticket
+            done = self.offset_update_done(ticket) if ticket else A.RMQ_OK
             for r, s in zip(idx, status.tolist()):
-                if s == A.RMQ_OK:
-                    out[r].success = True
-                else:
+                if s != A.RMQ_OK:
                     out[r].errorMsg = NOT_LEADER if s == A.RMQ_ENOTLEADER else A.STATUS_NAMES.get(s, str(s))
+                elif done == A.RMQ_OK:
+                    out[r].success = True
+                elif done == A.RMQ_PENDING:
+                    out[r].errorMsg = COMMIT_PENDING
+                    out[r].ticket = ticket
+                else:
+                    out[r].errorMsg = NOT_LEADER
         return out
+
+    def offset_update_done(self, ticket: int) -> int:
+        """A pending consumer-offset update: RMQ_OK once committed on a quorum (the reference's
+        closure then answers success), RMQ_PENDING, or RMQ_ENOTLEADER (failed by a leader change)."""
+        return self.engine.poll_offsets(ticket)
 
     # ---- MessageBatchReadRequestProcessor.handleRequest, batched
     def process_batch_read(self, requests: list[MessageBatchReadRequest]) -> list:

@@ -122,6 +122,34 @@ def fresh_replica_script(seg=1 << 16, world=4, rf=3, ppr=2):
     return views, script, dict(BASE, segment_bytes=seg), (f, g)
 
 
+def offset_ticket_script(world=3, rf=3, ppr=4):
+    """Consumer-offset completion (ConsumerOffsetUpdateRequestProcessor.java:40-49,60: the reply comes
+    from the Raft closure, after the commit). Rank 0 commits offsets (ticket T1): pending until a
+    round carries the row to a quorum — its first round is lost (rmq_fault_drop_rounds), so T1 stays
+    pending until the catch-up round; then T2 is committed and leadership moves before any round
+    carries it: T2 fails (RMQ_ENOTLEADER) and the new leaders hold T1's offsets, the acknowledged ones."""
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    spec = StreamSpec(ppr, 200, "uniform", size=(1, 60), config_index=94)
+    new = moved_leadership(views)
+    moved = {}
+    for r in range(world):
+        v = new[r]
+        m = [int(p) for p in range(len(v.gp))
+             if v.ranks[p][v.leader_slot[p]] == r and views[r].ranks[p][views[r].leader_slot[p]] != r]
+        if m:
+            moved[r] = m
+    c1 = (np.arange(ppr, dtype=np.uint32), np.ones(ppr, np.uint32), np.arange(ppr, dtype=np.uint64) + 7)
+    c2 = (np.arange(ppr, dtype=np.uint32), np.ones(ppr, np.uint32), np.arange(ppr, dtype=np.uint64) + 100)
+    script = [("round", _round(spec, world, 0)),
+              ("commit", {0: c1}), ("poll", {0: 1}),
+              ("round", _round(spec, world, 1), {"drop": (0,)}), ("poll", {0: 1}),
+              ("round", _round(spec, world, 2)), ("poll", {0: 1}),
+              ("commit", {0: c2}), ("poll", {0: 7}),
+              ("place", new), ("lead", {r: [(p, 2) for p in m] for r, m in moved.items()}),
+              ("poll", {0: 7})]
+    return views, script, BASE, c1
+
+
 def _cfgs(views, base):
     return [rank_cfg(EngineConfig(**base), views[r], r) for r in range(len(views))]
 
@@ -198,6 +226,21 @@ def test_replica_moved_to_a_fresh_rank(oracle_mod, seg):
         _close(oras)
 
 
+def test_offset_commit_waits_for_a_quorum(oracle_mod):
+    views, script, base, c1 = offset_ticket_script()
+    cfgs, oras, out = _oracle_run(oracle_mod, views, script, base)
+    try:
+        polls = [out[k][0] for k, s in enumerate(script) if s[0] == "poll"]
+        assert polls == [A.RMQ_PENDING, A.RMQ_PENDING, A.RMQ_OK, A.RMQ_PENDING, A.RMQ_ENOTLEADER], polls
+        for r in range(len(views)):  # the new leaders of rank 0's partitions hold T1's offsets
+            for p in range(len(views[r].gp)):
+                g = int(views[r].gp[p])
+                if g < 4 and r != 0 and oras[r].state(p)["is_leader"]:
+                    assert int(oras[r].consumer_offsets(p)[1]) == int(c1[2][g]), (r, p)
+    finally:
+        _close(oras)
+
+
 # ---------------------------------------------------------------------------------------------
 # GPU engines vs the oracle
 
@@ -249,3 +292,11 @@ def test_stale_replica_cannot_lead_gpu(oracle_mod):
 def test_replica_moved_to_a_fresh_rank_gpu(oracle_mod, seg):
     views, script, base, _ = fresh_replica_script(seg)
     _gpu_vs_oracle(oracle_mod, views, script, base)
+
+
+@pytest.mark.gpu
+def test_offset_commit_waits_for_a_quorum_gpu(oracle_mod):
+    views, script, base, _ = offset_ticket_script()
+    got, _ = _gpu_vs_oracle(oracle_mod, views, script, base)
+    polls = [got[k][0] for k, s in enumerate(script) if s[0] == "poll"]
+    assert polls == [A.RMQ_PENDING, A.RMQ_PENDING, A.RMQ_OK, A.RMQ_PENDING, A.RMQ_ENOTLEADER], polls

@@ -5,7 +5,8 @@ thread per rank, the in-process transport, as each rank would be driven by its o
 RCCL) and on per-rank oracles (tests/repl_sim.py rounds). Steps:
 
   ("place", views)                  rmq_set_placement of every rank's view (collective)
-  ("commit", {rank: (pidx, consumer, offset)})   leader consumer-offset commits
+  ("commit", {rank: (pidx, consumer, offset)})   leader consumer-offset commits (status and ticket)
+  ("poll", {rank: k})               rmq_poll_commit of the offset ticket that step k's commit got
   ("round", {rank: [batches]}, faults)          the batches form ONE launch group on every rank,
         then rmq_sync (rounds, acks, commit notices); faults = {"drop": ranks, "lost": [(src, dst)],
         "corrupt": (src, dst, at)}
@@ -48,7 +49,10 @@ def run_oracle(oras, views0, script):
         elif kind == "commit":
             for r, args in step[1].items():
                 rc, st = oras[r].commit_consumer_offset(*args)
-                rec[r] = (rc, st)
+                rec[r] = (rc, st, oras[r].last_offset_ticket)
+        elif kind == "poll":
+            for r, k in step[1].items():
+                rec[r] = oras[r].poll_offsets(out[k][r][2])
         elif kind == "round":
             f = step[2] if len(step) > 2 else {}
             for r in range(world):
@@ -86,7 +90,11 @@ def run_gpu(engs, hub, views0, script, timeout=240):
                     place(e, step[1][r])
                 elif kind == "commit":
                     if r in step[1]:
-                        out[k][r] = e.commit_consumer_offset(*step[1][r])
+                        rc, st = e.commit_consumer_offset(*step[1][r])
+                        out[k][r] = (rc, st, e.last_offset_ticket)
+                elif kind == "poll":
+                    if r in step[1]:
+                        out[k][r] = e.poll_offsets(out[step[1][r]][r][2])
                 elif kind == "round":
                     f = step[2] if len(step) > 2 else {}
                     if r in f.get("drop", ()):
@@ -148,3 +156,5 @@ def compare_outcomes(script, got, want):
                 assert np.array_equal(g[2], w[2]), f"step {k} rank {r} fetched bytes"
             elif step[0] == "commit" and w is not None:
                 assert g[0] == w[0] and np.array_equal(g[1], w[1]), (k, r, g, w)
+            elif step[0] == "poll" and w is not None:
+                assert g == w, (k, r, g, w)
