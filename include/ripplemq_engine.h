@@ -325,6 +325,17 @@ int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t pidx, uint64_t ri
 int rmq_read_index(rmq_engine* e, uint32_t pidx, uint64_t m_first, uint64_t count, uint64_t* out);
 int rmq_read_consumer_offsets(rmq_engine* e, uint32_t pidx, uint64_t* out /* max_consumers */);
 
+/* ---- host utilities ---- */
+/* FORMAT.md §1 records laid back to back in host memory (segment files of a durable tier, fetch
+   output): walks them from buf[0], expecting header offsets first, first + 1, ..., and stops at the
+   first record that is out of sequence or cut short, or (flags & RMQ_SCAN_CHECK) whose CRC32C or
+   zero padding is wrong, or after max_records. *count / *bytes = the whole records before that;
+   pos_out (nullable, max_records + 1 slots) gets each one's byte position and then the end. Needs no
+   engine (or GPU). */
+#define RMQ_SCAN_CHECK 1u
+int rmq_scan_records(const uint8_t* buf, uint64_t len, uint64_t first, uint64_t max_records, uint32_t flags,
+                     uint64_t* pos_out, uint64_t* count, uint64_t* bytes);
+
 /* ---- device buffers and timing (bench / tests keep inputs resident in HBM) ---- */
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out);
 int rmq_device_free(rmq_engine* e, void* p);

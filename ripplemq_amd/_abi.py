@@ -21,6 +21,7 @@ RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
 RMQ_RECORD_HEADER_BYTES = 16
 RMQ_TICKET_OFFSETS = 1 << 63
+RMQ_SCAN_CHECK = 1
 
 RMQ_OK = 0
 RMQ_PENDING = 1
@@ -150,6 +151,7 @@ _SIGS = {
     "rmq_fault_drop_rounds": (C.c_int, [vp, u32]),
     "rmq_fault_corrupt": (C.c_int, [vp, u32, C.c_int64]),
     "rmq_fault_isolate": (C.c_int, [vp, u32, u32]),
+    "rmq_scan_records": (C.c_int, [vp, u64, u64, u64, u32, vp, C.POINTER(u64), C.POINTER(u64)]),
 }
 
 _lib = None

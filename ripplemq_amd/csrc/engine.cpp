@@ -165,6 +165,8 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.cur = cur;
   a.nxt = nxt;
   a.key_passes = e->key_passes;
+  a.key_bits = e->key_bits;
+  a.rank_mode = e->rank_mode;
   a.gt = e->max_group_tiles;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
@@ -596,6 +598,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S2_WGS")) e->s2_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_RANK")) e->rank_mode = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
@@ -719,6 +722,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     uint32_t bits = 0;
     while ((1u << bits) < P) ++bits;  // keys in [0, P)
     e->key_passes = bits == 0 ? 0u : bits <= 8 ? 1u : 2u;
+    e->key_bits = bits;
   }
   e->staging.resize(4u * e->group_max + 1u);  // batches of the forming group and of three in flight
   CREATE_HIP(hipDeviceSynchronize());

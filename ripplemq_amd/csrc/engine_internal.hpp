@@ -270,6 +270,8 @@ struct rmq_engine {
   uint32_t max_tasks = 0;
   uint32_t max_tiles = 0;
   uint32_t key_passes = 0;
+  uint32_t key_bits = 0;
+  uint32_t rank_mode = 1;  // RMQ_RANK: stage 1 by hash counters (1) or by the LDS radix sort (0)
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
   CopyPool* copy_pool = nullptr;  // host batches (created with the first one)

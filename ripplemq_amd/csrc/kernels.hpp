@@ -235,6 +235,8 @@ struct PipeArgs {
   uint32_t wg1, wg2, wgp, wg3;  // workgroups per role, in this order along blockIdx.x
   uint32_t wgb;                 // stage 3's large-record workgroups (last along blockIdx.x)
   uint32_t key_passes;     // 1 (P <= 256) or 2
+  uint32_t key_bits;       // bits of the largest partition id (P - 1)
+  uint32_t rank_mode;      // stage 1: 0 LDS radix sort + segmented scan, 1 wave-ordered hash counters
   uint32_t gt;             // tiles per hist / excl column (group tile capacity)
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
   uint32_t debug;         // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring

@@ -367,6 +367,209 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
 }
 
 // ------------------------------------------------------------------------------------------
+// Stage 1 without a sort (RMQ_RANK=1): wave-ordered partition counters in an LDS hash table
+// ------------------------------------------------------------------------------------------
+// A record's place inside its (tile, partition) run is the number (and record bytes) of the tile's
+// earlier records of its partition. Each 64-record slot of a wave finds its peers (same partition)
+// by ballots over the key bits, and the count / bytes of the peers below each lane by popcounts over
+// ballots of the size bits; one leader per key then reads the partition's counter in the table (the
+// tile's records of that partition in earlier slots) and adds the slot's own. The slots are served
+// in input order (a wave's four in program order, the waves one after another), so the ranks are
+// the stable ranks the sort gave, with no sort, no segmented scan and three barriers fewer.
+constexpr u32 kHT = 2048;  // hash slots: at least twice the records of a tile
+static_assert(kHT >= 2 * kTR, "hash table load factor");
+struct Stage1HSmem {
+  u32 key[kHT];     // partition + 1 (0: empty)
+  u64 val[kHT];     // count << 40 | bytes/16 of the partition's records so far in the tile
+  u64 wsum[kPW][2];
+};
+static_assert(sizeof(Stage1HSmem) <= kSmemBytes, "stage 1's hash table fits the launch's LDS");
+
+__device__ __forceinline__ u32 wave_or_all(u32 v) {
+  v |= dpp_mov<0x111, 0xf>(v);
+  v |= dpp_mov<0x112, 0xf>(v);
+  v |= dpp_mov<0x114, 0xf>(v);
+  v |= dpp_mov<0x118, 0xf>(v);
+  v |= dpp_mov<0x142, 0xa>(v);
+  v |= dpp_mov<0x143, 0xc>(v);
+  return (u32)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage1HSmem& S) {
+  const PipeGroup& G = A.g1;
+  const u32 jb = batch_of_tile(G, t);
+  const PipeBatch& b = G.b[jb];
+  const PipeScratch& x = A.s1;
+  const u32 tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const u32 base = (t - G.tile0[jb]) * kTR;
+  const u64 gbase = (u64)t * kTR;
+  const u32 P = A.st.P;
+  const u64 lt = (1ull << lane) - 1ull;
+  const u32 nin = b.n - base < kTR ? b.n - base : kTR;
+  PIPE_STAMP(0);
+  for (u32 k = tid; k < kHT; k += kPT) S.key[k] = 0u;  // (ordered by the barrier of the scans below)
+
+  // ---- loads (input position q = kWR w + 64 r + lane)
+  u32 key[kTI], lenv[kTI], fl[kTI];
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 q = w * kWR + r * 64u + lane;
+    const bool in = q < nin;
+    const u32 p = in ? b.pidx[base + q] : 0u;
+    lenv[r] = in ? b.len[base + q] : 0u;
+    const bool bad = in && p >= P;
+    key[r] = (in && !bad) ? p : 0u;
+    fl[r] = !in ? kFlJunk : bad ? kFlNoPart : 0u;
+  }
+  u64 inv_cnt = 0;
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 q = w * kWR + r * 64u + lane;
+    if (fl[r] != kFlJunk && b.poff) {  // explicit payload offsets: per-record range check
+      const u64 o = b.poff[base + q];
+      const u32 L = lenv[r];
+      if (L && (o > b.payload_bytes || (u64)L > b.payload_bytes - o)) {
+        inv_cnt += 1;
+        if (fl[r] == 0u) fl[r] = kFlInvalid;
+      }
+    }
+    const bool bigr = fl[r] == 0u && lenv[r] > 16u * kBigPieces;  // stage 3's large-record waves
+    const u64 bm = __ballot(bigr);
+    if (bm) {
+      u32 at = 0;
+      if (lane == 0) at = atomicAdd(x.nbig, (u32)__popcll(bm));
+      at = readlane32(at, 0) + (u32)__popcll(bm & lt);
+      if (bigr) x.bigl[at] = (u32)(gbase + q);
+    }
+  }
+  // ---- input-order scans: payload prefix per record, tile sums {payload, invalid ranges}
+  {
+    u64 carry = 0;
+    u32 pre_r[kTI];
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) {
+      const u64 v = lenv[r];
+      const u64 inc = wave_incl_scan_u64(v);
+      pre_r[r] = (u32)(carry + inc - v);
+      carry += bcast_u64(inc, 63);
+    }
+    inv_cnt = bcast_u64(wave_incl_scan(inv_cnt), 63);
+    if (lane == 0) {
+      S.wsum[w][0] = carry;
+      S.wsum[w][1] = inv_cnt;
+    }
+    __syncthreads();
+    u64 wpre = 0;
+#pragma unroll
+    for (u32 ww = 0; ww < kPW; ++ww) wpre += ww < w ? S.wsum[ww][0] : 0ull;
+#pragma unroll
+    for (u32 r = 0; r < kTI; ++r) {
+      const u32 q = w * kWR + r * 64u + lane;
+      if (q < nin) x.pre[gbase + q] = (u32)wpre + pre_r[r];
+    }
+    if (tid == 0) {
+      u64 ps = 0, ic = 0;
+      for (u32 ww = 0; ww < kPW; ++ww) {
+        ps += S.wsum[ww][0];
+        ic += S.wsum[ww][1];
+      }
+      x.tsum[(u64)t * 4 + 0] = ps;
+      x.tsum[(u64)t * 4 + 1] = 0;
+      x.tsum[(u64)t * 4 + 2] = ic;
+      x.tsum[(u64)t * 4 + 3] = 0;
+      if (ps) __hip_atomic_fetch_add(&x.bacc[jb * 2 + 0], ps, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ic) __hip_atomic_fetch_add(&x.bacc[jb * 2 + 1], ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  PIPE_STAMP(1);
+
+  // ---- per slot, in registers: peers (same partition), the count and bytes/16 of the peers
+  // below the lane, and the slot's total of the lane's partition
+  u64 peers[kTI];
+  u32 wr[kTI], wb[kTI];
+  u64 stot[kTI];
+  const u32 kbits = A.key_bits;
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const bool valid = fl[r] == 0u;
+    u64 pm = __ballot(valid);
+    for (u32 bb = 0; bb < kbits; ++bb) {
+      const bool bit = (key[r] >> bb) & 1u;
+      const u64 m = __ballot(bit);
+      pm &= bit ? m : ~m;
+    }
+    pm = valid ? pm : 0ull;
+    const u64 below = pm & lt;
+    const u32 rs = valid ? record_rs16(lenv[r]) : 0u;
+    const u32 orv = wave_or_all(rs);
+    const u32 rbits = orv ? 32u - (u32)__builtin_clz(orv) : 0u;
+    u32 bsum = 0, btot = 0;
+    for (u32 bb = 0; bb < rbits; ++bb) {
+      const u64 m = __ballot((rs >> bb) & 1u);
+      bsum += (u32)__popcll(m & below) << bb;
+      btot += (u32)__popcll(m & pm) << bb;
+    }
+    peers[r] = pm;
+    wr[r] = (u32)__popcll(below);
+    wb[r] = bsum;
+    stot[r] = ((u64)__popcll(pm) << 40) | btot;
+  }
+  PIPE_STAMP(2);
+
+  // ---- the partitions' counters, slot after slot in input order (wave after wave)
+  u64 before[kTI];
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) before[r] = 0ull;
+  for (u32 ww = 0; ww < kPW; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (u32 r = 0; r < kTI; ++r) {
+        const u64 pm = peers[r];
+        u64 c = 0;
+        if (pm && !(pm & lt)) {  // the lowest lane of its partition in the slot
+          const u32 kv = key[r] + 1u;
+          u32 h = (kv * 2654435761u) >> (32u - 11u);
+          for (;;) {
+            const u32 k0 = S.key[h];
+            if (k0 == kv) break;
+            if (k0 == 0u) {
+              const u32 old = atomicCAS(&S.key[h], 0u, kv);
+              if (old == 0u) {
+                S.val[h] = 0ull;
+                break;
+              }
+              if (old == kv) break;
+            }
+            h = (h + 1u) & (kHT - 1u);
+          }
+          c = S.val[h];
+          S.val[h] = c + stot[r];
+        }
+        const u32 ll = pm ? (u32)__builtin_ctzll(pm) : lane;  // the partition's leader in the slot
+        const u32 lo = (u32)__shfl((int)(u32)c, (int)ll, 64), hi = (u32)__shfl((int)(u32)(c >> 32), (int)ll, 64);
+        before[r] = ((u64)hi << 32) | lo;
+      }
+    }
+    __syncthreads();
+  }
+  PIPE_STAMP(3);
+#pragma unroll
+  for (u32 r = 0; r < kTI; ++r) {
+    const u32 q = w * kWR + r * 64u + lane;
+    if (q < nin)
+      x.crank[gbase + q] = make_uint2(((u32)(before[r] >> 40) + wr[r]) | (fl[r] << kFlagShift),
+                                      (u32)(before[r] & kLow40) + wb[r]);
+  }
+  // ---- the tile's aggregate of every present partition (the sparse hist cells)
+  for (u32 k = tid; k < kHT; k += kPT) {
+    const u32 kv = S.key[k];
+    if (kv) x.hist[(u64)(kv - 1u) * A.gt + t] = S.val[k];
+  }
+  if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  PIPE_STAMP(4);
+}
+
+// ------------------------------------------------------------------------------------------
 // Stage 2: batch rules, column scans over the group's tiles, tile payload bases
 // ------------------------------------------------------------------------------------------
 
@@ -1720,7 +1923,10 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
     if (wg < A.wg1) {  // a workgroup ranks tiles wg, wg + wg1, ... (RMQ_S1_WGS < tiles: fewer slots held)
       for (u32 t = wg; t < A.g1.tiles; t += A.wg1) {
-        stage1_tile(A, t, *reinterpret_cast<Stage1Smem*>(smem_raw));
+        if (A.rank_mode)
+          stage1_tile_hash(A, t, *reinterpret_cast<Stage1HSmem*>(smem_raw));
+        else
+          stage1_tile(A, t, *reinterpret_cast<Stage1Smem*>(smem_raw));
         __syncthreads();  // the tile's LDS is reused by the next one
       }
       return;

@@ -1,0 +1,94 @@
+// segscan.cpp — host-side walk of FORMAT.md §1 records laid back to back (segment files of the
+// durable tier, ripplemq_amd/tier.py; fetch output buffers). The reference keeps every message in
+// its `messages` list and jraft persists the log under the partition's data path
+// (mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:26,64-69,
+// PartitionRaftServer.java:53,88-90); the tier restores that below the HBM rings, and reopening a
+// segment file after a crash must find where its whole records end. This was a Python loop over
+// the headers (tier.py round 3); it is one pass over the bytes here, with the CRC32C of every
+// payload checked by the SSE4.2 crc32 instruction when asked.
+#include <cstdint>
+#include <cstring>
+
+#include "../../include/ripplemq_engine.h"
+
+namespace {
+
+uint32_t crc_table[8][256];
+bool crc_ready = false;
+
+void crc_init() {
+  if (crc_ready) return;
+  for (uint32_t b = 0; b < 256; ++b) {
+    uint32_t c = b;
+    for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+    crc_table[0][b] = c;
+  }
+  for (uint32_t t = 1; t < 8; ++t)
+    for (uint32_t b = 0; b < 256; ++b) crc_table[t][b] = (crc_table[t - 1][b] >> 8) ^ crc_table[0][crc_table[t - 1][b] & 0xFF];
+  crc_ready = true;
+}
+
+uint32_t crc_sw(const uint8_t* p, uint64_t n) {
+  uint32_t c = 0xFFFFFFFFu;
+  while (n >= 8) {
+    uint32_t lo, hi;
+    std::memcpy(&lo, p, 4);
+    std::memcpy(&hi, p + 4, 4);
+    lo ^= c;
+    c = crc_table[7][lo & 0xFF] ^ crc_table[6][(lo >> 8) & 0xFF] ^ crc_table[5][(lo >> 16) & 0xFF] ^
+        crc_table[4][lo >> 24] ^ crc_table[3][hi & 0xFF] ^ crc_table[2][(hi >> 8) & 0xFF] ^
+        crc_table[1][(hi >> 16) & 0xFF] ^ crc_table[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) c = (c >> 8) ^ crc_table[0][(c ^ *p++) & 0xFF];
+  return c ^ 0xFFFFFFFFu;
+}
+
+__attribute__((target("sse4.2"))) uint32_t crc_hw(const uint8_t* p, uint64_t n) {
+  uint64_t c = 0xFFFFFFFFu;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = (uint32_t)c;
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return c32 ^ 0xFFFFFFFFu;
+}
+
+}  // namespace
+
+extern "C" int rmq_scan_records(const uint8_t* buf, uint64_t len, uint64_t first, uint64_t max_records,
+                                uint32_t flags, uint64_t* pos_out, uint64_t* count, uint64_t* bytes) {
+  if ((len && !buf) || !count || !bytes) return RMQ_EINVAL;
+  const bool check = (flags & RMQ_SCAN_CHECK) != 0;
+  const bool hw = __builtin_cpu_supports("sse4.2");
+  if (check && !hw) crc_init();
+  uint64_t pos = 0, k = 0;
+  while (k < max_records && pos + 16 <= len) {
+    uint64_t off;
+    uint32_t L, crc;
+    std::memcpy(&off, buf + pos, 8);
+    std::memcpy(&L, buf + pos + 8, 4);
+    std::memcpy(&crc, buf + pos + 12, 4);
+    const uint64_t rs = 16ull + ((L + 15ull) & ~15ull);
+    if (off != first + k || rs > len - pos) break;  // out of sequence, or cut short
+    if (check) {
+      const uint8_t* pl = buf + pos + 16;
+      if ((hw ? crc_hw(pl, L) : crc_sw(pl, L)) != crc) break;
+      bool pad_zero = true;  // the zero padding is part of the record (FORMAT.md §1)
+      for (uint64_t z = L; z < rs - 16; ++z) pad_zero &= pl[z] == 0;
+      if (!pad_zero) break;
+    }
+    if (pos_out) pos_out[k] = pos;
+    pos += rs;
+    ++k;
+  }
+  if (pos_out) pos_out[k] = pos;
+  *count = k;
+  *bytes = pos;
+  return RMQ_OK;
+}

@@ -34,6 +34,7 @@ records were lost before they were durable.
 """
 from __future__ import annotations
 
+import ctypes as C
 import json
 import os
 
@@ -47,31 +48,57 @@ OFFSETS_FILE = "offsets.bin"   # u64 consumer offsets of the partition (rmq_conf
 META_FILE = "meta.json"        # {"term": t}: the partition's raft_meta
 
 
-def record_positions(buf: np.ndarray, count: int | None = None) -> np.ndarray:
-    """Byte positions of the FORMAT.md §1 records laid back to back in ``buf`` (plus the end)."""
-    b = buf.tobytes() if not isinstance(buf, (bytes, bytearray)) else bytes(buf)
-    out, pos = [], 0
-    while pos + 16 <= len(b) and (count is None or len(out) < count):
-        out.append(pos)
-        ln = int.from_bytes(b[pos + 8:pos + 12], "little")
-        pos += 16 + ((ln + 15) & ~15)
-    out.append(pos)
-    return np.asarray(out, np.int64)
+def _as_u8(buf) -> np.ndarray:
+    if isinstance(buf, np.ndarray):
+        return np.ascontiguousarray(buf.view(np.uint8).reshape(-1))
+    return np.frombuffer(bytes(buf), np.uint8)
 
 
-def whole_records(b: bytes, first: int) -> tuple[int, int]:
+def _scan(buf, first: int, max_records: int, check: bool, positions: bool):
+    """rmq_scan_records (the engine library's native walk of back-to-back FORMAT.md §1 records)."""
+    a = _as_u8(buf)
+    pos = np.zeros(max_records + 1, np.uint64) if positions else None
+    n, nb = C.c_uint64(), C.c_uint64()
+    rc = A.load().rmq_scan_records(a.ctypes.data if a.size else None, a.size, first, max_records,
+                                   A.RMQ_SCAN_CHECK if check else 0,
+                                   pos.ctypes.data if pos is not None else None, C.byref(n), C.byref(nb))
+    if rc:
+        raise EngineError(rc, "rmq_scan_records")
+    k = int(n.value)
+    return k, int(nb.value), (pos[:k + 1].astype(np.int64) if pos is not None else None)
+
+
+def record_positions(buf: np.ndarray, count: int | None = None, first: int | None = None) -> np.ndarray:
+    """Byte positions of the FORMAT.md §1 records laid back to back in ``buf`` (plus the end); the
+    header offsets must run first, first + 1, ... (first: the first header's)."""
+    a = _as_u8(buf)
+    if first is None:
+        first = int(a[:8].view(np.uint64)[0]) if a.size >= 16 else 0
+    cap = a.size // 16 if count is None else int(count)
+    return _scan(a, first, cap, False, True)[2]
+
+
+def whole_records(b, first: int, durable_end: int | None = None) -> tuple[int, int]:
     """(records, bytes) of the longest prefix of ``b`` made of whole FORMAT.md §1 records whose
-    header offsets run first, first + 1, ...: a crash in the middle of a segment write leaves a
-    torn last record (cut short, or zero-filled by the file system), which this excludes."""
-    pos = k = 0
-    while pos + 16 <= len(b):
-        off = int.from_bytes(b[pos:pos + 8], "little")
-        ln = int.from_bytes(b[pos + 8:pos + 12], "little")
-        end = pos + 16 + ((ln + 15) & ~15)
-        if off != first + k or end > len(b):
-            break
-        pos, k = end, k + 1
-    return k, pos
+    header offsets run first, first + 1, ... and whose CRC32C and zero padding check out: a crash in
+    the middle of a segment write leaves a torn last record (cut short, garbage, or zero-filled by
+    the file system), which this excludes. A zero-filled record at offset `first` (header offset 0,
+    length 0, CRC 0) is also a valid empty message: past `durable_end` (the end the last completed
+    spill recorded) an all-zero record counts as torn."""
+    a = _as_u8(b)
+    k, nb, pos = _scan(a, first, a.size // 16, True, True)
+    if durable_end is not None:
+        for i in range(k):
+            if first + i >= durable_end and not a[pos[i]:pos[i + 1]].any():
+                return i, int(pos[i])
+    if nb + 16 <= a.size:
+        # a torn tail ends the file; whole records AFTER the bad one mean a record inside the log
+        # was corrupted (a flipped byte), which no cut may hide
+        ln = int(a[nb + 8:nb + 12].view(np.uint32)[0])
+        nxt = nb + 16 + ((ln + 15) & ~15)
+        if nxt + 16 <= a.size and _scan(a[nxt:], first + k + 1, 1, True, False)[0]:
+            raise EngineError(A.RMQ_EINVAL, f"record {first + k} is corrupted inside the segment")
+    return k, nb
 
 
 class _PartitionFiles:
@@ -88,9 +115,10 @@ class _PartitionFiles:
         self.seg_pos: list[int] = []     # its first logical byte
         names = sorted(int(f[:-len(SEG_SUFFIX)]) for f in os.listdir(self.dir) if f.endswith(SEG_SUFFIX))
         cat, acc = [], 0
+        durable = self.load_meta().get("end", 0)  # (no meta: no spill completed)
         for i, first in enumerate(names):  # reopen: walk the headers of every file, in offset order
             data = np.fromfile(self._path(first), np.uint8)
-            n, whole = whole_records(data.tobytes(), first)
+            n, whole = whole_records(data, first, durable)
             if whole != data.size:
                 # a torn tail (the spill that wrote it never advanced the durable cursor, so the next
                 # spill fetches those records again): cut the file back to its last whole record
@@ -101,7 +129,7 @@ class _PartitionFiles:
             if n == 0:
                 os.remove(self._path(first))
                 continue
-            rp = record_positions(data)
+            rp = record_positions(data, n, first)
             if not self.seg_first:
                 self.base = first
             elif first != self.base + sum(len(x) for x in cat):
@@ -126,13 +154,14 @@ class _PartitionFiles:
         os.replace(tmp, os.path.join(self.dir, name))
 
     def save_state(self, offsets: np.ndarray, term: int, fsync: bool) -> None:
-        """The partition's consumer-offset row and term, each rewritten only when it changed."""
+        """The partition's consumer-offset row, and its term with the durable end of its records
+        (what a reopen trusts without the zero-fill rule), each rewritten only when it changed."""
         row = np.ascontiguousarray(offsets, np.uint64).tobytes()
         if row != self.load_offsets_bytes():
             self._replace(OFFSETS_FILE, row, fsync)
-        meta = self.load_meta()
-        if meta.get("term") != int(term):
-            self._replace(META_FILE, json.dumps({"term": int(term)}).encode(), fsync)
+        meta = {"term": int(term), "end": int(self.end)}
+        if self.load_meta() != meta:
+            self._replace(META_FILE, json.dumps(meta).encode(), fsync)
 
     def load_offsets_bytes(self) -> bytes:
         try:
@@ -160,7 +189,7 @@ class _PartitionFiles:
             self.base = first
         elif first != self.end:
             raise EngineError(A.RMQ_EINVAL, f"{self.dir}: spill of offset {first} does not continue {self.end}")
-        rp = record_positions(data, count)
+        rp = record_positions(data, count, first)
         if len(rp) != count + 1 or int(rp[-1]) != len(data):
             raise EngineError(A.RMQ_EINVAL, f"{self.dir}: {count} records expected in {len(data)} bytes")
         total = int(self.pos[-1])

@@ -149,3 +149,43 @@ def test_durable_tier_reopen_torn_tail(oracle_mod, tmp_path, cut):
         assert again.spill() == 1 and again.end(0) == 40
         assert seg.read_bytes() == raw
         assert [m for _, _, m in again.read(0, 0, 100)] == msgs
+
+
+def test_zero_filled_first_segment_is_torn(oracle_mod, tmp_path):
+    # a segment whose first offset is 0 and whose first write was zero-filled by the file
+    # system would parse as an empty message at offset 0 (header 0, length 0, CRC32C of nothing = 0).
+    # No spill completed (no meta.json names a durable end), so the reopened tier drops it.
+    d = PartitionDirectory({TOPIC: 1}, max_consumers=2)
+    cfg = EngineConfig(num_partitions=1, replication_factor=1, segment_bytes=1 << 14, index_interval=256,
+                       max_consumers=2)
+    part = tmp_path / "p000000"
+    part.mkdir()
+    (part / f"{0:020d}.seg").write_bytes(bytes(48))
+    with oracle_mod.OracleEngine(cfg) as eng:
+        tier = DurableLog(eng, str(tmp_path), [0], d.consumer("__durable_tier"))
+        assert tier.end(0) == 0 and not list(part.glob("*.seg"))
+
+
+def test_native_record_scan_matches_the_format(oracle_mod):
+    # rmq_scan_records (host, engine library) on FORMAT.md records the oracle wrote: positions,
+    # whole-record counts, CRC32C and padding checks, cuts
+    from ripplemq_amd.tier import record_positions, whole_records
+    cfg = EngineConfig(num_partitions=1, replication_factor=1, segment_bytes=1 << 16, index_interval=256)
+    lens = np.array([0, 1, 15, 16, 17, 100, 1000], np.uint32)
+    pay = np.random.default_rng(5).integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    with oracle_mod.OracleEngine(cfg) as eng:
+        eng.append(np.zeros(len(lens), np.uint32), lens, pay)
+        st = eng.state(0)
+        buf = eng.read_segment(0, 0, 0, st["log_end_pos"])
+    rs = 16 + (lens.astype(np.int64) + 15) // 16 * 16
+    want = np.concatenate([[0], np.cumsum(rs)])
+    assert np.array_equal(record_positions(buf), want)
+    assert whole_records(buf, 0) == (len(lens), int(want[-1]))
+    assert whole_records(buf[:-1], 0) == (len(lens) - 1, int(want[-2]))  # cut short
+    bad = buf.copy()
+    bad[int(want[-2]) + 16 + 999] ^= 1  # the last payload byte: a CRC mismatch in the tail
+    assert whole_records(bad, 0) == (len(lens) - 1, int(want[-2]))
+    pad = buf.copy()
+    pad[int(want[2]) + 16 + 15] = 7  # record 2 (15 B payload): its pad byte, records follow
+    with pytest.raises(Exception):
+        whole_records(pad, 0)
