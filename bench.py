@@ -297,6 +297,68 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
                     "HBM-resident at 4,096 partitions, so it is bounded by what the rings retain)"}
 
 
+def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int = 512, consumers: int = 4) -> dict:
+    """The durable tier (ripplemq_amd/tier.py) on the bench engine: the first
+    `parts` partitions' committed records spill to segment files (one rmq_fetch per spill, the
+    native record scan, one file append per partition) while the workload appends: per round one
+    launch group of batches, then a spill. Then consumers lagging BELOW the rings (configs[4]'s
+    U[0, 10^6] lag: offsets the rings no longer hold) are served from the files at max = 1024
+    (DurableLog.read, as PartitionBroker.process_batch_read does on RMQ_EOFFSET). Both timed on the
+    host; the record bytes counted are the FORMAT.md §1 images written / read."""
+    import shutil
+    import tempfile
+
+    from ripplemq_amd.tier import DurableLog
+
+    P = min(parts, spec.partitions)
+    cursor = eng.cfg.max_consumers - 1  # the tier's durability cursor (a consumer slot of its own)
+    pidx = np.arange(P, dtype=np.uint32)
+    eng.sync()
+    st = eng.states(0, P)
+    eng.commit_consumer_offset(pidx, np.full(P, cursor, np.uint32), st["log_start_offset"])
+    root = tempfile.mkdtemp(prefix="rmq_tier_", dir=os.environ.get("RMQ_TIER_DIR"))
+    try:
+        tier = DurableLog(eng, root, pidx, cursor, segment_file_bytes=256 << 20)
+        first = tier.spill()  # untimed: the retained windows at the start
+        size0 = sum(int(f.pos[-1]) for f in tier.parts.values())
+        spilled, t_spill, k0 = 0, 0.0, 500_000
+        for k in range(rounds):
+            for j in range(appends):
+                step(k0 + k * appends + j)
+            t0 = time.perf_counter()
+            spilled += tier.spill()
+            t_spill += time.perf_counter() - t0
+        sbytes = sum(int(f.pos[-1]) for f in tier.parts.values()) - size0
+        eng.sync()
+        st = eng.states(0, P)
+        g = np.random.default_rng(0x5249504C)
+        reqs = []
+        for p in range(P):
+            f = tier.parts[p]
+            lo, hi = f.base, min(int(st["log_start_offset"][p]), f.end)
+            if hi > lo:
+                reqs += [(p, int(o)) for o in g.integers(lo, hi, consumers)]
+        recs = rbytes = 0
+        t0 = time.perf_counter()
+        for p, off in reqs:
+            got = tier.read(p, off, 1024)
+            recs += len(got)
+            rbytes += sum(16 + (len(b) + 15) // 16 * 16 for _, _, b in got)
+        t_read = time.perf_counter() - t0
+    finally:
+        shutil.rmtree(root, ignore_errors=True)
+    return {"partitions": P, "rounds": rounds, "appends_per_round": appends,
+            "spill": {"records": spilled, "records_per_s": spilled / t_spill if t_spill else None,
+                      "gb_per_s": sbytes / t_spill / 1e9 if t_spill else None, "initial_records": first,
+                      "ms_per_spill": t_spill * 1e3 / max(rounds, 1)},
+            "read_below_rings": {"requests": len(reqs), "records": recs,
+                                 "records_per_s": recs / t_read if t_read else None,
+                                 "gb_per_s": rbytes / t_read / 1e9 if t_read else None, "max_records": 1024},
+            "note": "host-side tier over the engine (spill = one rmq_fetch of the partitions' new records, "
+                    "segment-file appends, the consumer table and terms in bulk, one ends file); reads "
+                    "are consumers below the rings' retained windows served from the files"}
+
+
 def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     """Consumer fetch over the bench engine's committed logs (SURVEY §8(d) B_fetch): per round every
     (partition, consumer) commits an offset lagging the high watermark by U[0, retained records]
@@ -594,6 +656,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
         if args.concurrent_rounds > 0 and world == 1:
             out["mixed"] = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group)
+        if args.tier_rounds > 0 and world == 1:
+            out["tier"] = tier_leg(eng, step, spec, args.tier_rounds, args.group)
     if region is not None:
         eng.device_free(region)
     else:
@@ -635,6 +699,8 @@ def main() -> None:
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
     ap.add_argument("--concurrent-rounds", type=int, default=20,
                     help="rounds of the append+fetch mixed leg (1 GPU; 0: skip)")
+    ap.add_argument("--tier-rounds", type=int, default=20,
+                    help="rounds of the durable-tier leg (spills + reads below the rings, 1 GPU; 0: skip)")
     ap.add_argument("--host-steps", type=int, default=100,
                     help="batches of the host-memory leg (PCIe-inclusive rate, 1 GPU; 0: skip)")
     ap.add_argument("--watchdog", type=float, default=900.0, help="multi-GPU: exit a rank stuck this long [s]")

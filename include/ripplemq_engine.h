@@ -324,6 +324,8 @@ int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t pidx, uint64_t ri
 /* Offset-index entries m in [m_first, m_first + count): out[2k] = offset, out[2k+1] = pos. */
 int rmq_read_index(rmq_engine* e, uint32_t pidx, uint64_t m_first, uint64_t count, uint64_t* out);
 int rmq_read_consumer_offsets(rmq_engine* e, uint32_t pidx, uint64_t* out /* max_consumers */);
+/* The consumer-offset rows of partitions [first, first + n): out[n][max_consumers]. */
+int rmq_read_consumer_table(rmq_engine* e, uint32_t first, uint32_t n, uint64_t* out);
 
 /* ---- host utilities ---- */
 /* FORMAT.md §1 records laid back to back in host memory (segment files of a durable tier, fetch

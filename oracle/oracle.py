@@ -332,6 +332,11 @@ class OracleEngine:
             raise EngineError(rc, "oracle")
         return out
 
+    def consumer_table(self, first=0, n=None):
+        n = self.cfg.num_partitions - first if n is None else n
+        return np.stack([self.consumer_offsets(first + i) for i in range(n)]) if n else \
+            np.zeros((0, self.cfg.max_consumers), np.uint64)
+
     def consumer_offsets(self, pidx):
         out = np.empty(self.cfg.max_consumers, np.uint64)
         self.lib.ro_read_consumer_offsets(self.h, pidx, _p(out))

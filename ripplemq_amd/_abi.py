@@ -130,6 +130,7 @@ _SIGS = {
     "rmq_read_segment": (C.c_int, [vp, u32, u32, u64, u64, vp]),
     "rmq_read_index": (C.c_int, [vp, u32, u64, u64, vp]),
     "rmq_read_consumer_offsets": (C.c_int, [vp, u32, vp]),
+    "rmq_read_consumer_table": (C.c_int, [vp, u32, u32, vp]),
     "rmq_device_alloc": (C.c_int, [vp, u64, C.POINTER(vp)]),
     "rmq_device_free": (C.c_int, [vp, vp]),
     "rmq_memcpy": (C.c_int, [vp, vp, vp, u64, C.c_int]),

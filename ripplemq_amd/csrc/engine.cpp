@@ -1496,6 +1496,19 @@ int rmq_read_consumer_offsets(rmq_engine* e, uint32_t p, uint64_t* out) {
   return RMQ_OK;
 }
 
+int rmq_read_consumer_table(rmq_engine* e, uint32_t first, uint32_t n, uint64_t* out) {
+  if (!e || (n && !out)) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (first > e->cfg.num_partitions || n > e->cfg.num_partitions - first) return RMQ_ENOPART;
+  if (!n) return RMQ_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = quiesce(e);
+  if (rc) return rc;
+  const size_t C = e->cfg.max_consumers;
+  HIP_TRY(hipMemcpy(out, e->st.cons + (size_t)first * C, (size_t)n * C * 8, hipMemcpyDeviceToHost));
+  return RMQ_OK;
+}
+
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out) {
   if (!e || !out) return RMQ_EINVAL;
   std::lock_guard<std::mutex> g(e->mu);

@@ -356,6 +356,13 @@ class Engine:
         _check(self.lib.rmq_read_index(self.h, pidx, m_first, count, _ptr(out)), "rmq_read_index")
         return out
 
+    def consumer_table(self, first: int = 0, n: int | None = None) -> np.ndarray:
+        """rmq_read_consumer_table: the consumer-offset rows of partitions [first, first + n)."""
+        n = self.cfg.num_partitions - first if n is None else n
+        out = np.empty((n, self.cfg.max_consumers), np.uint64)
+        _check(self.lib.rmq_read_consumer_table(self.h, first, n, _ptr(out)), "rmq_read_consumer_table")
+        return out
+
     def consumer_offsets(self, pidx: int) -> np.ndarray:
         out = np.empty(self.cfg.max_consumers, np.uint64)
         _check(self.lib.rmq_read_consumer_offsets(self.h, pidx, _ptr(out)), "rmq_read_consumer_offsets")

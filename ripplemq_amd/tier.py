@@ -46,6 +46,16 @@ from .engine import EngineError
 SEG_SUFFIX = ".seg"
 OFFSETS_FILE = "offsets.bin"   # u64 consumer offsets of the partition (rmq_config.max_consumers)
 META_FILE = "meta.json"        # {"term": t}: the partition's raft_meta
+ENDS_FILE = "durable_ends.bin" # tier root: u64 pairs {partition, durable end} of the last spill
+
+
+def load_ends(root: str) -> dict[int, int]:
+    """The durable end of every partition the last completed spill recorded (empty if none)."""
+    try:
+        a = np.fromfile(os.path.join(root, ENDS_FILE), np.uint64).reshape(-1, 2)
+    except (FileNotFoundError, ValueError):
+        return {}
+    return {int(p): int(e) for p, e in a}
 
 
 def _as_u8(buf) -> np.ndarray:
@@ -105,8 +115,10 @@ class _PartitionFiles:
     """One partition's segment files: record k (offset base + k) at logical byte pos[k] of the
     concatenated files; segment s covers logical bytes [seg_pos[s], seg_pos[s + 1])."""
 
-    def __init__(self, root: str, p: int, segment_file_bytes: int):
+    def __init__(self, root: str, p: int, segment_file_bytes: int, durable: int = 0):
         self.dir = os.path.join(root, f"p{p:06d}")
+        self._row = None     # the consumer-offset row / meta last written (no re-read per spill)
+        self._meta = None
         os.makedirs(self.dir, exist_ok=True)
         self.limit = segment_file_bytes
         self.base = 0
@@ -115,7 +127,6 @@ class _PartitionFiles:
         self.seg_pos: list[int] = []     # its first logical byte
         names = sorted(int(f[:-len(SEG_SUFFIX)]) for f in os.listdir(self.dir) if f.endswith(SEG_SUFFIX))
         cat, acc = [], 0
-        durable = self.load_meta().get("end", 0)  # (no meta: no spill completed)
         for i, first in enumerate(names):  # reopen: walk the headers of every file, in offset order
             data = np.fromfile(self._path(first), np.uint8)
             n, whole = whole_records(data, first, durable)
@@ -154,14 +165,19 @@ class _PartitionFiles:
         os.replace(tmp, os.path.join(self.dir, name))
 
     def save_state(self, offsets: np.ndarray, term: int, fsync: bool) -> None:
-        """The partition's consumer-offset row, and its term with the durable end of its records
-        (what a reopen trusts without the zero-fill rule), each rewritten only when it changed."""
+        """The partition's consumer-offset row and term, each rewritten only when it changed."""
         row = np.ascontiguousarray(offsets, np.uint64).tobytes()
-        if row != self.load_offsets_bytes():
+        if self._row is None:
+            self._row = self.load_offsets_bytes()
+        if row != self._row:
             self._replace(OFFSETS_FILE, row, fsync)
-        meta = {"term": int(term), "end": int(self.end)}
-        if self.load_meta() != meta:
+            self._row = row
+        meta = {"term": int(term)}
+        if self._meta is None:
+            self._meta = self.load_meta()
+        if self._meta != meta:
             self._replace(META_FILE, json.dumps(meta).encode(), fsync)
+            self._meta = meta
 
     def load_offsets_bytes(self) -> bytes:
         try:
@@ -242,7 +258,9 @@ class DurableLog:
         self.dir = directory
         self.cursor = int(cursor)
         self.fsync = fsync
-        self.parts = {int(p): _PartitionFiles(directory, int(p), segment_file_bytes) for p in partitions}
+        ends = load_ends(directory)
+        self.parts = {int(p): _PartitionFiles(directory, int(p), segment_file_bytes, ends.get(int(p), 0))
+                      for p in partitions}
         # a reopened tier continues where its files end: the cursor slot names that offset
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
         ends = np.fromiter((f.end for f in self.parts.values()), np.uint64, len(self.parts))
@@ -281,10 +299,22 @@ class DurableLog:
             self.engine.commit_consumer_offset(np.asarray(adv_p, np.uint32),
                                                np.full(len(adv_p), self.cursor, np.uint32),
                                                np.asarray(adv_o, np.uint64))
-        for k, p in enumerate(pidx.tolist()):  # offsets and term of the partitions led here
+        # offsets and term of the partitions led here (one bulk read of each), then the durable ends
+        # of every partition in one file: a reopen trusts the records below them
+        rows = self.engine.consumer_table()
+        terms = self.engine.states()["term"]
+        for k, p in enumerate(pidx.tolist()):
             if int(res["status"][k]) == A.RMQ_ENOTLEADER:
                 continue
-            self.parts[p].save_state(self.engine.consumer_offsets(p), self.engine.state(p)["term"], self.fsync)
+            self.parts[p].save_state(rows[p], int(terms[p]), self.fsync)
+        ends = np.array([[p, f.end] for p, f in self.parts.items()], np.uint64).reshape(-1, 2)
+        tmp = os.path.join(self.dir, ENDS_FILE + ".tmp")
+        with open(tmp, "wb") as f:
+            f.write(ends.tobytes())
+            if self.fsync:
+                f.flush()
+                os.fsync(f.fileno())
+        os.replace(tmp, os.path.join(self.dir, ENDS_FILE))
         return moved
 
     def read(self, p: int, off: int, max_messages: int) -> list[tuple[int, int, bytes]]:
@@ -302,7 +332,8 @@ def replay(directory: str, engine, partitions, *, batch_records: int = 65536) ->
     the retained window of every partition's lowest local ring must equal the files' bytes for it.
     Then each partition's term (rmq_become_leader) and consumer-offset row come back from its
     meta and offsets files. Returns {"records": n, "partitions": k, "terms": t, "offset_rows": o}."""
-    files = {int(p): _PartitionFiles(directory, int(p), 1 << 62) for p in partitions}
+    ends = load_ends(directory)
+    files = {int(p): _PartitionFiles(directory, int(p), 1 << 62, ends.get(int(p), 0)) for p in partitions}
     recs = {}
     for p, f in files.items():
         if f.end == f.base:

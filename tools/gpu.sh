@@ -24,7 +24,7 @@ R=$GRAFT_REPO_ROOT
 T=$1
 shift
 mkdir -p gpurun_out
-Q="--no-cpu-baseline --fetch-rounds 0 --concurrent-rounds 0 --host-steps 0"
+Q="--no-cpu-baseline --fetch-rounds 0 --concurrent-rounds 0 --host-steps 0 --tier-rounds 0"
 run() {  # run <seconds> <out file> <command...>: stdout to the file, stderr to <file>.err
   local lim=$1 out=$2
   shift 2
