@@ -242,59 +242,105 @@ def host_leg(eng, batches, steps: int) -> dict:
 
 
 def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
-    """Appends and consumer fetches interleaved on one engine (configs[4]: concurrent consumer fetch
-    at lagging offsets): per round `appends` device-resident batches (one launch group) go to the
-    pipeline, then one
-    rmq_fetch of every (partition, consumer) at max = 10 runs on the fetch stream, ordered after the
-    launches issued so far and before the next one (the pipeline is never flushed for it). Reports
-    both rates over the leg's wall time, and the consumers' lag bound. The consumers commit their
-    offsets (read-then-commit, ConsumerClientImpl.java:61-117) after each fetch, so they follow the
-    appends."""
+    """Appends and consumer fetches at once on one engine (configs[4]: concurrent consumer fetch at
+    lagging offsets), as a broker runs them: a producer thread submits `rounds` x `appends`
+    device-resident batches; meanwhile the consumer loop fetches every (partition, consumer) at
+    max = 10 and commits the next offsets (read-then-commit, ConsumerClientImpl.java:61-117), with
+    the consumers split in two halves whose fetches alternate through rmq_fetch_async: while one
+    half's fetch runs on the GPU, the other half's results are read and committed, so a consumer
+    never fetches before its previous commit and the host never waits on the append pipeline.
+    Every fetch is ordered between two pipeline launches (the next launch waits for it). Reports
+    both rates over the same wall time."""
+    import threading
+
     P = spec.partitions
     eng.sync()
-    st0 = [eng.state(p) for p in range(P)]
-    hw = np.array([s["high_watermark"] for s in st0], np.int64)
-    retained = np.array([s["log_end_offset"] - s["log_start_offset"] for s in st0], np.int64)
+    st = eng.states()
+    hw = st["high_watermark"].astype(np.int64)
+    retained = (st["log_end_offset"] - st["log_start_offset"]).astype(np.int64)
     g = np.random.default_rng(0x52495051)
     pp = np.repeat(np.arange(P, dtype=np.uint32), consumers)
     cc = np.tile(np.arange(consumers, dtype=np.uint32), P)
     lag = (g.random(P * consumers) * (np.repeat(retained, consumers) // 2 + 1)).astype(np.int64)
     off = (np.repeat(hw, consumers) - lag).astype(np.uint64)
     eng.commit_consumer_offset(pp, cc, off)
+    half = [cc < consumers // 2, cc >= consumers // 2]
+    hp = [pp[m] for m in half]
+    hc = [cc[m] for m in half]
+    hmax = [np.full(int(m.sum()), mx, np.uint32) for m in half]
     hi = spec.size if isinstance(spec.size, int) else spec.size[1]
     cap = P * consumers * mx * (16 + (hi + 15) // 16 * 16) + 4096
-    d_out = eng.device_alloc(cap)
-    maxr = np.full(P * consumers, mx, np.uint32)
-    recs = fetched = resets = 0
+    d_out = [eng.device_alloc(cap), eng.device_alloc(cap)]
+    done = threading.Event()
+    err = []
     k0 = 10_000
-    t0 = time.perf_counter()
-    for k in range(rounds):
-        for j in range(appends):
-            step(k0 + k * appends + j)
-        rc, res, _ = eng.fetch_device(pp, cc, maxr, d_out, cap)
-        st = res["status"]
-        if rc or np.any((st != 0) & (st != -6)):
-            raise SystemExit(f"bench: mixed leg fetch failed rc={rc} statuses={np.unique(st)}")
+
+    def producer():
+        try:
+            for k in range(rounds):
+                for j in range(appends):
+                    step(k0 + k * appends + j)
+        except BaseException as ex:  # noqa: BLE001 - re-raised below
+            err.append(ex)
+        finally:
+            done.set()
+
+    fetched = resets = fetches = 0
+    t_wait = 0.0
+
+    def consume(h, tk):
+        nonlocal fetched, resets, t_wait
+        t1 = time.perf_counter()
+        rc, res, _ = eng.fetch_poll(tk, wait=True)
+        t_wait += time.perf_counter() - t1
+        stt = res["status"]
+        if rc or np.any((stt != 0) & (stt != -6)):
+            raise SystemExit(f"bench: mixed leg fetch failed rc={rc} statuses={np.unique(stt)}")
         n = res["count"].astype(np.uint64)
         fetched += int(n.sum())
         nxt = res["start_offset"] + n
-        gone = np.flatnonzero(st == -6)  # RMQ_EOFFSET: a partition's ring moved past a slow consumer
-        if gone.size:                    # (10 records per fetch): it resumes at the first retained
-            nxt[gone] = res["start_offset"][gone]  # offset, which the row carries
-            resets += gone.size
-        eng.commit_consumer_offset(pp, cc, nxt)
-        recs += appends * spec.records
+        gone = stt == -6  # RMQ_EOFFSET: the ring moved past a slow consumer; it resumes at the
+        resets += int(gone.sum())  # first retained offset, which the row carries
+        eng.commit_consumer_offset(hp[h], hc[h], nxt)
+
+    th = threading.Thread(target=producer, daemon=True)
+    t0 = time.perf_counter()
+    th.start()
+    tk = [eng.fetch_async(hp[0], hc[0], hmax[0], d_out=d_out[0], out_cap=cap), None]
+    fetches = 1
+    h = 0
+    while True:
+        o = h ^ 1
+        if tk[o] is not None:
+            consume(o, tk[o])
+            tk[o] = None
+        if done.is_set():
+            break
+        tk[o] = eng.fetch_async(hp[o], hc[o], hmax[o], d_out=d_out[o], out_cap=cap)
+        fetches += 1
+        h = o
+    for o in (0, 1):
+        if tk[o] is not None:
+            consume(o, tk[o])
+    th.join()
+    if err:
+        raise err[0]
     eng.sync()
     dt = time.perf_counter() - t0
-    eng.device_free(d_out)
+    for d in d_out:
+        eng.device_free(d)
+    recs = rounds * appends * spec.records
     return {"append_msgs_per_s": recs / dt, "fetch_records_per_s": fetched / dt, "rounds": rounds,
-            "appends_per_round": appends, "fetch_requests_per_round": P * consumers, "max_records": mx,
-            "wall_s": dt, "lag_bound": "U[0, retained records / 2] per partition at the start",
+            "appends_per_round": appends, "fetches": fetches, "requests_per_fetch": P * consumers // 2,
+            "max_records": mx, "wall_s": dt, "consumer_wait_s": t_wait,
+            "lag_bound": "U[0, retained records / 2] per partition at the start",
             "consumer_resets": resets,
-            "note": "appends (device-resident batches) and read-then-commit fetches of every (partition, "
-                    "consumer) interleaved; both rates over the same wall time; consumers start lagging "
-                    "the high watermark by U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not "
-                    "HBM-resident at 4,096 partitions, so it is bounded by what the rings retain)"}
+            "note": "a producer thread appends (device-resident batches) while the consumer loop fetches "
+                    "every (partition, consumer) at max = 10 through rmq_fetch_async, two halves of the "
+                    "consumers alternating, and commits each half's next offsets before its next fetch; "
+                    "both rates over the same wall time; consumers start lagging the high watermark by "
+                    "U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not HBM-resident at 4,096 "
+                    "partitions, so it is bounded by what the rings retain)"}
 
 
 def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int = 512, consumers: int = 4) -> dict:
@@ -310,11 +356,12 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
 
     from ripplemq_amd.tier import DurableLog
 
-    P = min(parts, spec.partitions)
+    stride = max(1, spec.partitions // parts)  # every stride-th partition: an even sample of the Zipf ranks
+    pidx = np.arange(0, spec.partitions, stride, dtype=np.uint32)
+    P = len(pidx)
     cursor = eng.cfg.max_consumers - 1  # the tier's durability cursor (a consumer slot of its own)
-    pidx = np.arange(P, dtype=np.uint32)
     eng.sync()
-    st = eng.states(0, P)
+    st = eng.states()[pidx]
     eng.commit_consumer_offset(pidx, np.full(P, cursor, np.uint32), st["log_start_offset"])
     root = tempfile.mkdtemp(prefix="rmq_tier_", dir=os.environ.get("RMQ_TIER_DIR"))
     try:
@@ -330,10 +377,10 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
             t_spill += time.perf_counter() - t0
         sbytes = sum(int(f.pos[-1]) for f in tier.parts.values()) - size0
         eng.sync()
-        st = eng.states(0, P)
+        st = eng.states()
         g = np.random.default_rng(0x5249504C)
         reqs = []
-        for p in range(P):
+        for p in pidx.tolist():
             f = tier.parts[p]
             lo, hi = f.base, min(int(st["log_start_offset"][p]), f.end)
             if hi > lo:
@@ -347,7 +394,7 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
         t_read = time.perf_counter() - t0
     finally:
         shutil.rmtree(root, ignore_errors=True)
-    return {"partitions": P, "rounds": rounds, "appends_per_round": appends,
+    return {"partitions": P, "partition_stride": stride, "rounds": rounds, "appends_per_round": appends,
             "spill": {"records": spilled, "records_per_s": spilled / t_spill if t_spill else None,
                       "gb_per_s": sbytes / t_spill / 1e9 if t_spill else None, "initial_records": first,
                       "ms_per_spill": t_spill * 1e3 / max(rounds, 1)},
@@ -404,6 +451,14 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             t_reg += ms_r / 1e3
             recs += int(res["count"].sum())
             nbytes += int(res["bytes"].sum())
+        # the same requests as 8 asynchronous calls back to back (rmq_fetch_async: 4 in flight, the
+        # host never waits on the GPU between issues), first issue to last result
+        maxr = np.full(P * consumers, mx, np.uint32)
+        eng.sync()
+        t0 = time.perf_counter()
+        tks = [eng.fetch_async(pp, cc, maxr, d_out=d_out, out_cap=cap) for _ in range(8)]
+        n_async = sum(int(eng.fetch_poll(t, wait=True)[1]["count"].sum()) for t in tks)
+        t_async = time.perf_counter() - t0
         eng.device_free(d_out)
         # B_fetch = 2 (H + L) per returned record (fixed-size configs: exact; mixed
         # sizes: the records' bytes in the log layout, which adds their padding to 16 bytes)
@@ -414,11 +469,12 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         # time; the roofline uses the region from the first start to the last end (no host gaps:
         # the events are recorded by the dispatches themselves)
         out[f"max{mx}"] = {"records_per_s_kernels": recs / t_reg, "records_per_s_call": recs / t_wall,
+                           "records_per_s_async_calls": n_async / t_async,
                            "records_per_request": recs / (rounds * P * consumers),
                            "requests": P * consumers, "rounds": rounds,
                            "roofline": {"bound": "hbm", "achieved": alg / t_reg / 1e9, "peak": HBM_PEAK_GBS,
                                         "unit": "GB/s", "frac": alg / t_reg / 1e9 / HBM_PEAK_GBS,
-                                        "kernels": "rmq::fetch_resolve + fetch_gather (placement fused)",
+                                        "kernels": "rmq::fetch_fused_kernel (resolve, look-back placement, gather)" if os.environ.get("RMQ_FETCH_FUSED", "1") != "0" else "rmq::fetch_resolve + fetch_gather",
                                         "mean_us_per_fetch": t_reg / rounds * 1e6,
                                         "kernel_spans_us_summed": t_kern / rounds * 1e6}}
     return out
@@ -697,7 +753,7 @@ def main() -> None:
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
-    ap.add_argument("--concurrent-rounds", type=int, default=20,
+    ap.add_argument("--concurrent-rounds", type=int, default=250,
                     help="rounds of the append+fetch mixed leg (1 GPU; 0: skip)")
     ap.add_argument("--tier-rounds", type=int, default=20,
                     help="rounds of the durable-tier leg (spills + reads below the rings, 1 GPU; 0: skip)")

@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 5u
+#define RMQ_ABI_VERSION 6u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -273,7 +273,8 @@ int rmq_sync(rmq_engine* e);
    read-back sees them. With a replication transport the partition's row travels to every follower
    with the next round (FORMAT.md §8, §9). ticket (nullable) gets a consumer-offset ticket
    (RMQ_TICKET_OFFSETS set) that rmq_poll_commit resolves once the accepted items are on a quorum;
-   0 if no item was accepted. */
+   0 if no item was accepted. The engine keeps the 256 newest unpolled offset tickets: an older
+   one polls as RMQ_EINVAL. */
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                                const uint64_t* offset, uint32_t n, int32_t* status, uint64_t* ticket);
 
@@ -284,6 +285,19 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
    fit in out_cap (those get count 0, status RMQ_ENOSPC). */
 int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
               uint64_t out_cap, rmq_fetch_res* res, uint64_t* bytes_used);
+/* rmq_fetch without blocking the host (ABI 6). The fetch is ordered after every launch and call
+   issued before it and before the ones issued after it, exactly like rmq_fetch, and returns at once
+   with a fetch ticket; reqs are copied before the call returns. res (and out with RMQ_MEM_HOST)
+   must stay valid until rmq_fetch_poll returns something other than RMQ_PENDING. Four fetches can
+   be in flight: a fifth first completes the oldest into its caller's arrays (its poll then returns
+   at once). MessageBatchReadRequestProcessor.java:36-42 answers each read from its own closure;
+   this is the batched, pipelined form of that call. */
+int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
+                    uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket);
+/* Completion of an rmq_fetch_async ticket: RMQ_PENDING while it runs (wait != 0: block instead), else
+   what rmq_fetch would have returned (RMQ_OK / RMQ_ENOSPC) with res, out and *bytes_used filled. A
+   ticket is answered once; an unknown or already answered ticket gets RMQ_EINVAL. */
+int rmq_fetch_poll(rmq_engine* e, uint64_t ticket, uint32_t wait, uint64_t* bytes_used);
 
 /* ---- replication transport (FORMAT.md §9) ---- */
 /* 128-byte communicator id: one rank creates it, the application hands it to every rank. */

@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 5
+RMQ_ABI_VERSION = 6
 RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF
@@ -125,6 +125,8 @@ _SIGS = {
     "rmq_sync": (C.c_int, [vp]),
     "rmq_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp, C.POINTER(u64)]),
     "rmq_fetch": (C.c_int, [vp, vp, u32, u32, vp, u64, vp, C.POINTER(u64)]),
+    "rmq_fetch_async": (C.c_int, [vp, vp, u32, u32, vp, u64, vp, C.POINTER(u64)]),
+    "rmq_fetch_poll": (C.c_int, [vp, u64, u32, C.POINTER(u64)]),
     "rmq_get_partition_state": (C.c_int, [vp, u32, C.POINTER(RmqPartitionState)]),
     "rmq_get_partition_states": (C.c_int, [vp, u32, u32, vp]),
     "rmq_read_segment": (C.c_int, [vp, u32, u32, u64, u64, vp]),

@@ -451,8 +451,15 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq, e->d_crc,
-                             e->d_stats, e->d_req, e->d_res, e->d_aux, e->d_cpre, e->d_csum, e->d_fetch_out,
-                             e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
+                             e->d_stats, e->d_lb_ticket, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
+  for (rmq_engine::FetchSlot& f : e->fslot) {
+    void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv, f.d_lbf, f.d_out};
+    for (void* p : fs) bufs.push_back(p);
+    if (f.h_req) hipHostFree(f.h_req);
+    if (f.h_res) hipHostFree(f.h_res);
+    if (f.ev) hipEventDestroy(f.ev);
+    if (f.ev_copy) hipEventDestroy(f.ev_copy);
+  }
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
     bufs.push_back(z.used);
@@ -472,15 +479,12 @@ void free_engine(rmq_engine* e) {
   for (void* p : bufs)
     if (p) hipFree(p);
   if (e->done_host) hipHostFree(e->done_host);
-  if (e->h_req) hipHostFree(e->h_req);
-  if (e->h_res) hipHostFree(e->h_res);
   for (auto& cs : e->cslot) {
     if (cs.h) hipHostFree(cs.h);
     if (cs.d) hipFree(cs.d);
     if (cs.ev) hipEventDestroy(cs.ev);
   }
   if (e->ev_main) hipEventDestroy(e->ev_main);
-  if (e->ev_fetch) hipEventDestroy(e->ev_fetch);
   if (e->fetch_s) hipStreamDestroy(e->fetch_s);
   if (e->copy_s) hipStreamDestroy(e->copy_s);
   for (auto& v : e->prof)
@@ -622,7 +626,13 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   preload_fetch_kernels();
   CREATE_HIP(hipStreamCreateWithFlags(&e->copy_s, hipStreamNonBlocking));
   CREATE_HIP(hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming));
-  CREATE_HIP(hipEventCreateWithFlags(&e->ev_fetch, hipEventDisableTiming));
+  for (rmq_engine::FetchSlot& f : e->fslot) {
+    CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
+  }
+  if (const char* v = std::getenv("RMQ_FETCH_FUSED")) e->fetch_fused = std::atoi(v) != 0;
+  CREATE_TRY(dalloc(&e->d_lb_ticket, 4));
+  CREATE_HIP(hipMemset(e->d_lb_ticket, 0, 4));
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
   DevState& s = e->st;
@@ -1264,61 +1274,137 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   if (ticket) {
     *ticket = RMQ_TICKET_OFFSETS | ++e->off_ticket_seq;
     e->off_tickets.emplace_back(*ticket, std::move(tv));
+    while (e->off_tickets.size() > rmq_engine::kMaxOffsetTickets) e->off_tickets.pop_front();  // never polled
   }
   const int rc = check_err(e);
   return rc ? rc : rc_all;
 }
 
-int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
-              uint64_t out_cap, rmq_fetch_res* res, uint64_t* bytes_used) {
-  if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> fg(e->fetch_mu);
-  if (bytes_used) *bytes_used = 0;
-  if (!n) return RMQ_OK;
-  if (!reqs || !res || (mem != RMQ_MEM_HOST && mem != RMQ_MEM_DEVICE)) return RMQ_EINVAL;
+namespace {
+
+// Scratch of a fetch slot for n requests and, for a host output, out_cap bytes of device staging.
+int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
+  if (n > f.cap) {
+    void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv, f.d_lbf};
+    for (void* p : ds)
+      if (p) hipFree(p);
+    if (f.h_req) hipHostFree(f.h_req);
+    if (f.h_res) hipHostFree(f.h_res);
+    f.d_req = f.d_cpre = f.d_lbf = f.h_req = nullptr;
+    f.d_res = f.d_aux = f.d_csum = f.d_lbv = f.h_res = nullptr;
+    f.cap = 0;
+    const uint32_t cap = std::max<uint32_t>(n, 1024);
+    const size_t wgs = fetch_fused_workgroups(cap) + 1;
+    int rc = dalloc(&f.d_req, (size_t)cap * 4);
+    if (!rc) rc = dalloc(&f.d_res, (size_t)cap * 4 + 2);
+    if (!rc) rc = dalloc(&f.d_aux, (size_t)cap * 2);
+    if (!rc) rc = dalloc(&f.d_cpre, (size_t)cap + 4);
+    if (!rc) rc = dalloc(&f.d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride);
+    if (!rc) rc = dalloc(&f.d_lbv, wgs);
+    if (!rc) rc = dalloc(&f.d_lbf, wgs);
+    if (rc) return rc;
+    HIP_TRY(hipMemset(f.d_lbf, 0, wgs * 4));  // epoch 0 is never a fetch's
+    HIP_TRY(hipHostMalloc((void**)&f.h_req, (size_t)cap * 16, 0));
+    HIP_TRY(hipHostMalloc((void**)&f.h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
+    f.cap = cap;
+  }
+  if (stage > f.out_alloc) {
+    if (f.d_out) hipFree(f.d_out);
+    f.d_out = nullptr;
+    f.out_alloc = 0;
+    const int rc = dalloc(&f.d_out, stage);
+    if (rc) return rc;
+    f.out_alloc = stage;
+  }
+  return RMQ_OK;
+}
+
+// Advance the fetch in slot f (fetch_mu held): RMQ_PENDING while its kernels or host copies run
+// (wait: block instead); else its result, with the caller's res (and host output) filled and the
+// slot idle again.
+int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t* bytes_used) {
+  if (f.phase == 1) {
+    if (wait) {
+      HIP_TRY(hipEventSynchronize(f.ev));
+    } else {
+      const hipError_t q = hipEventQuery(f.ev);
+      if (q == hipErrorNotReady) return RMQ_PENDING;
+      HIP_TRY(q);
+    }
+    // the device writes rmq_fetch_res rows (status zero-extended into its reserved word)
+    static_assert(sizeof(rmq_fetch_res) == 32, "result rows are four words");
+    std::memcpy(f.res, f.h_res, (size_t)f.n * 32);
+    int rc_all = RMQ_OK;
+    for (uint32_t r = 0; r < f.n; ++r)
+      if (f.res[r].status == RMQ_ENOSPC) {
+        rc_all = RMQ_ENOSPC;
+        break;
+      }
+    f.rc = rc_all;
+    f.phase = 2;
+    if (f.mem == RMQ_MEM_HOST && f.out_cap) {
+      // copy back the byte runs of the served requests only: the regions of requests that did not
+      // fit stay untouched in the caller's buffer, as with a device buffer the gather writes itself
+      uint64_t lo = 0, hi = 0;
+      for (uint32_t r = 0; r <= f.n; ++r) {
+        const bool served = r < f.n && f.res[r].status == RMQ_OK && f.res[r].bytes;
+        if (served && f.res[r].out_pos == hi && hi > lo) {
+          hi += f.res[r].bytes;
+          continue;
+        }
+        if (hi > lo) HIP_TRY(hipMemcpyAsync(f.out + lo, f.d_out + lo, hi - lo, hipMemcpyDeviceToHost, e->fetch_s));
+        lo = hi = served ? f.res[r].out_pos : 0;
+        if (served) hi += f.res[r].bytes;
+      }
+      HIP_TRY(hipEventRecord(f.ev_copy, e->fetch_s));
+    } else {
+      f.phase = 3;  // nothing to copy
+    }
+  }
+  if (f.phase == 2) {
+    if (wait) {
+      HIP_TRY(hipEventSynchronize(f.ev_copy));
+    } else {
+      const hipError_t q = hipEventQuery(f.ev_copy);
+      if (q == hipErrorNotReady) return RMQ_PENDING;
+      HIP_TRY(q);
+    }
+  }
+  if (bytes_used) *bytes_used = f.h_res[(size_t)f.n * 4];
+  f.phase = 0;
+  f.ticket = 0;
+  return f.rc;
+}
+
+}  // namespace
+
+int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
+                    uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
+  if (!e || !ticket) return RMQ_EINVAL;
+  if ((n && (!reqs || !res)) || (mem != RMQ_MEM_HOST && mem != RMQ_MEM_DEVICE)) return RMQ_EINVAL;
   if (out_cap && !out) return RMQ_EINVAL;
   if (mem == RMQ_MEM_DEVICE && (reinterpret_cast<uintptr_t>(out) & 15u)) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> fg(e->fetch_mu);
   HIP_TRY(hipSetDevice(e->device));
-  int rc = RMQ_OK;
-  if (n > e->fetch_cap) {
-    hipFree(e->d_req);
-    hipFree(e->d_res);
-    hipFree(e->d_aux);
-    hipFree(e->d_cpre);
-    hipFree(e->d_csum);
-    e->d_csum = nullptr;
-    if (e->h_req) hipHostFree(e->h_req);
-    if (e->h_res) hipHostFree(e->h_res);
-    e->d_req = nullptr;
-    e->d_res = e->d_aux = nullptr;
-    e->d_cpre = e->h_req = nullptr;
-    e->h_res = nullptr;
-    e->fetch_cap = 0;
-    const uint32_t cap = std::max<uint32_t>(n, 1024);
-    rc = dalloc(&e->d_req, (size_t)cap * 4);
-    if (!rc) rc = dalloc(&e->d_res, (size_t)cap * 4 + 2);
-    if (!rc) rc = dalloc(&e->d_aux, (size_t)cap * 2);
-    if (!rc) rc = dalloc(&e->d_cpre, (size_t)cap + 4);
-    if (!rc) rc = dalloc(&e->d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride);
-    if (rc) return rc;
-    HIP_TRY(hipHostMalloc((void**)&e->h_req, (size_t)cap * 16, 0));
-    HIP_TRY(hipHostMalloc((void**)&e->h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
-    e->fetch_cap = cap;
+  rmq_engine::FetchSlot& f = e->fslot[e->fslot_next];
+  if (f.ticket) {  // every slot taken: complete the oldest into its caller's arrays, keep its result
+    uint64_t used = 0;
+    const uint64_t old = f.ticket;
+    const int rc = fetch_slot_step(e, f, true, &used);
+    if (rc < 0 && rc != RMQ_ENOSPC) return rc;
+    e->fetch_done.push_back({old, (uint64_t)(int64_t)rc, used});
   }
-  uint8_t* d_out = out;
-  if (mem == RMQ_MEM_HOST && out_cap) {
-    if (out_cap > e->fetch_out_cap) {
-      hipFree(e->d_fetch_out);
-      e->d_fetch_out = nullptr;
-      e->fetch_out_cap = 0;
-      rc = dalloc(&e->d_fetch_out, out_cap);
-      if (rc) return rc;
-      e->fetch_out_cap = out_cap;
-    }
-    d_out = e->d_fetch_out;
+  const uint64_t tk = ++e->fetch_seq;
+  if (!n) {  // nothing to fetch: complete at once
+    e->fetch_done.push_back({tk, (uint64_t)(int64_t)RMQ_OK, 0});
+    while (e->fetch_done.size() > 256) e->fetch_done.pop_front();
+    *ticket = tk;
+    return RMQ_OK;
   }
-  std::memcpy(e->h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
-  uint64_t* const h_total = e->h_res + (size_t)n * 4;
+  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0);
+  if (rc) return rc;
+  uint8_t* d_out = mem == RMQ_MEM_HOST ? (out_cap ? f.d_out : nullptr) : out;
+  std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
   {
     // Order against the append pipeline without flushing it: the fetch reads the committed state
     // after the last launch issued so far, and the next launch waits for the fetch, so no ring
@@ -1326,60 +1412,77 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
     std::lock_guard<std::mutex> g(e->mu);
     FetchArgs a{};
     a.st = e->st;
-    a.req = e->d_req;
-    a.res = e->d_res;
-    a.aux = e->d_aux;
-    a.cpre = e->d_cpre;
-    a.csum = e->d_csum;
+    a.req = f.d_req;
+    a.res = f.d_res;
+    a.aux = f.d_aux;
+    a.cpre = f.d_cpre;
+    a.csum = f.d_csum;
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
+    a.epoch = (uint32_t)(tk & 0x3FFFFFFFull) ? (uint32_t)(tk & 0x3FFFFFFFull) : 1u;
+    if (e->fetch_fused) {
+      a.lb_val = f.d_lbv;
+      a.lb_flag = f.d_lbf;
+      a.lb_ticket = e->d_lb_ticket;
+    }
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
-    HIP_TRY(hipMemcpyAsync(e->d_req, e->h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
+    HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     hipEvent_t ev[4] = {};
-    if (e->profile) {  // kernel 3: the two kernels' own durations; 4: first start to last end
+    if (e->profile) {  // kernel 3: the kernels' own durations; 4: first start to last end
       for (hipEvent_t& x : ev) x = pool_event(e);
       for (int k = 0; k < 2; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
       e->prof[4].push_back({ev[0], ev[3]});
     }
     launch_fetch(a, e->fetch_s, e->profile ? ev : nullptr);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(e->h_res, e->d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
-    HIP_TRY(hipEventRecord(e->ev_fetch, e->fetch_s));
-    HIP_TRY(hipStreamWaitEvent(e->main_s, e->ev_fetch, 0));
+    HIP_TRY(hipMemcpyAsync(f.h_res, f.d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
+    HIP_TRY(hipEventRecord(f.ev, e->fetch_s));
+    HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev, 0));
   }
-  HIP_TRY(hipEventSynchronize(e->ev_fetch));
-  int rc_all = RMQ_OK;
-  for (uint32_t r = 0; r < n; ++r) {
-    const uint64_t* h = e->h_res + 4ull * r;
-    rmq_fetch_res& x = res[r];
-    std::memset(&x, 0, sizeof x);
-    x.start_offset = h[0];
-    x.out_pos = h[1];
-    x.count = (uint32_t)h[2];
-    x.bytes = (uint32_t)(h[2] >> 32);
-    x.status = (int32_t)(uint32_t)h[3];
-    if (x.status == RMQ_ENOSPC) rc_all = RMQ_ENOSPC;
-  }
-  if (mem == RMQ_MEM_HOST && out_cap) {
-    // copy back the byte runs of the served requests only: the regions of requests that did not
-    // fit stay untouched in the caller's buffer, as with a device buffer the gather writes itself
-    uint64_t lo = 0, hi = 0;
-    for (uint32_t r = 0; r <= n; ++r) {
-      const bool served = r < n && res[r].status == RMQ_OK && res[r].bytes;
-      if (served && res[r].out_pos == hi && hi > lo) {
-        hi += res[r].bytes;
-        continue;
-      }
-      if (hi > lo) HIP_TRY(hipMemcpyAsync(out + lo, d_out + lo, hi - lo, hipMemcpyDeviceToHost, e->fetch_s));
-      lo = hi = served ? res[r].out_pos : 0;
-      if (served) hi += res[r].bytes;
+  f.ticket = tk;
+  f.phase = 1;
+  f.rc = RMQ_OK;
+  f.n = n;
+  f.mem = mem;
+  f.out = out;
+  f.out_cap = out_cap;
+  f.res = res;
+  e->fslot_next = (e->fslot_next + 1) % rmq_engine::kFetchSlots;
+  while (e->fetch_done.size() > 256) e->fetch_done.pop_front();
+  *ticket = tk;
+  return RMQ_OK;
+}
+
+int rmq_fetch_poll(rmq_engine* e, uint64_t ticket, uint32_t wait, uint64_t* bytes_used) {
+  if (!e || !ticket) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> fg(e->fetch_mu);
+  if (bytes_used) *bytes_used = 0;
+  for (rmq_engine::FetchSlot& f : e->fslot)
+    if (f.ticket == ticket) {
+      HIP_TRY(hipSetDevice(e->device));
+      return fetch_slot_step(e, f, wait != 0, bytes_used);
     }
-    HIP_TRY(hipStreamSynchronize(e->fetch_s));
-  }
-  if (bytes_used) *bytes_used = h_total[0];
-  return rc_all;
+  for (auto it = e->fetch_done.begin(); it != e->fetch_done.end(); ++it)
+    if ((*it)[0] == ticket) {
+      const int rc = (int)(int64_t)(*it)[1];
+      if (bytes_used) *bytes_used = (*it)[2];
+      e->fetch_done.erase(it);
+      return rc;
+    }
+  return RMQ_EINVAL;
+}
+
+int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
+              uint64_t out_cap, rmq_fetch_res* res, uint64_t* bytes_used) {
+  if (bytes_used) *bytes_used = 0;
+  if (!e) return RMQ_EINVAL;
+  if (!n) return RMQ_OK;
+  uint64_t t = 0;
+  const int rc = rmq_fetch_async(e, reqs, n, mem, out, out_cap, res, &t);
+  if (rc) return rc;
+  return rmq_fetch_poll(e, t, 1, bytes_used);
 }
 
 int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {

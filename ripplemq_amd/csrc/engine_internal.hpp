@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <array>
 #include <deque>
 #include <mutex>
 #include <new>
@@ -304,18 +305,43 @@ struct rmq_engine {
   std::mutex fetch_mu;
   hipStream_t fetch_s = nullptr;
   hipStream_t copy_s = nullptr;  // host batches: pinned -> device DMA
-  hipEvent_t ev_main = nullptr, ev_fetch = nullptr;
-  uint32_t* d_req = nullptr;
-  uint64_t* d_res = nullptr;
-  uint64_t* d_aux = nullptr;
-  uint32_t* d_cpre = nullptr;
-  uint64_t* d_csum = nullptr;
+  hipEvent_t ev_main = nullptr;
   bool trace = false;           // RMQ_TRACE: print every launch's roles to stderr
-  uint32_t* h_req = nullptr;   // pinned
-  uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}
-  uint32_t fetch_cap = 0;
-  uint8_t* d_fetch_out = nullptr;
-  uint64_t fetch_out_cap = 0;
+  // fetches in flight (rmq_fetch_async), each with its own scratch: a fetch is ordered after the
+  // launches issued before it and before the ones issued after it; the host only waits in
+  // rmq_fetch_poll (or when every slot is taken: the oldest is completed into its caller's arrays
+  // and its result kept for its poll)
+  struct FetchSlot {
+    uint32_t* d_req = nullptr;
+    uint64_t* d_res = nullptr;
+    uint64_t* d_aux = nullptr;
+    uint32_t* d_cpre = nullptr;
+    uint64_t* d_csum = nullptr;
+    uint64_t* d_lbv = nullptr;   // single pass: look-back words per workgroup
+    uint32_t* d_lbf = nullptr;
+    uint32_t* h_req = nullptr;   // pinned
+    uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}
+    uint32_t cap = 0;
+    uint8_t* d_out = nullptr;    // device staging of a host output
+    uint64_t out_alloc = 0;
+    hipEvent_t ev = nullptr;     // kernels and the result copy done
+    hipEvent_t ev_copy = nullptr;  // host output copies done
+    // the fetch in flight: ticket 0 = idle; phase 1: kernels, 2: host output copies
+    uint64_t ticket = 0;
+    int phase = 0;
+    int rc = 0;
+    uint32_t n = 0, mem = 0;
+    uint8_t* out = nullptr;
+    uint64_t out_cap = 0;
+    rmq_fetch_res* res = nullptr;
+  };
+  static constexpr uint32_t kFetchSlots = 4;
+  FetchSlot fslot[kFetchSlots];
+  uint32_t fslot_next = 0;
+  uint64_t fetch_seq = 0;        // tickets (and the single pass's epochs)
+  std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
+  uint32_t* d_lb_ticket = nullptr;
+  bool fetch_fused = true;       // RMQ_FETCH_FUSED=0: resolve + gather kernels
   // consumer-offset commits: two staging slots (pinned items -> device by one copy on the pipeline
   // stream), so a commit is ordered with the append stream without waiting for it
   struct CommitSlot {
@@ -335,6 +361,7 @@ struct rmq_engine {
   uint32_t cstamp_gen = 0;
   uint64_t off_ticket_seq = 0;
   std::deque<std::pair<uint64_t, std::vector<std::pair<uint32_t, uint64_t>>>> off_tickets;
+  static constexpr size_t kMaxOffsetTickets = 256;   // the newest unpolled ones are kept
   // ack scratch
   uint32_t* d_ctl32 = nullptr;
   uint64_t* d_ctl64 = nullptr;

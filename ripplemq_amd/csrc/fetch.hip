@@ -41,7 +41,7 @@ struct PartView {
 
 // Logical byte positions of records t0 (lanes 0..31) and t1 (lanes 32..63), start_off <= t <= leo,
 // found together (wave-uniform arguments; the half-wave of each record returns its position).
-__device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0, u64 t1) {
+__device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0, u64 t1) {
   const u32 lane = lane_id(), h = lane >> 5, hl = lane & 31u;
   const u64 t = h ? t1 : t0;
   const u32 ilog = st.interval_log2;
@@ -142,9 +142,14 @@ __device__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0,
   return wb + 16ull * cur;
 }
 
-__global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
-  const u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6));
-  const bool live = r < a.n;  // (no early return: the workgroup meets at a barrier below)
+// One request, resolved by one wave (wave-uniform results): status, start offset, count, bytes, the
+// source position and the ring word {ring byte offset in logs << 6 | log2(ring bytes)}.
+struct Resolved {
+  u64 start, count, bytes, pos0, ring;
+  int status;
+};
+
+__device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, bool live) {
   const DevState& st = a.st;
   const u32 p = live ? a.req[4 * r] : 0u, c = live ? a.req[4 * r + 1] : 0u, mx = live ? a.req[4 * r + 2] : 0u;
   int status = kOk;
@@ -191,14 +196,22 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
       }
     }
   }
+  return Resolved{start, count, bytes, pos0, (ring_off << 6) | (desc & 63ull), status};
+}
+
+__global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
+  const u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6));
+  const bool live = r < a.n;  // (no early return: the workgroup meets at a barrier below)
+  const Resolved q = resolve_request(a, r, live);
+  const u64 bytes = q.bytes;
   __shared__ u64 s_b[kFW];
   if (lane_id() == 0) s_b[threadIdx.x >> 6] = bytes;
   if (live && lane_id() == 0) {
-    a.res[4 * r + 0] = start;
-    a.res[4 * r + 2] = count | (bytes << 32);
-    a.res[4 * r + 3] = (u64)(uint32_t)status;
-    a.aux[2 * r + 0] = pos0;
-    a.aux[2 * r + 1] = (ring_off << 6) | (desc & 63ull);  // ring | log2(ring bytes)
+    a.res[4 * r + 0] = q.start;
+    a.res[4 * r + 2] = q.count | (bytes << 32);
+    a.res[4 * r + 3] = (u64)(uint32_t)q.status;
+    a.aux[2 * r + 0] = q.pos0;
+    a.aux[2 * r + 1] = q.ring;
     a.cpre[r] = (u32)bytes;
   }
   // one add per workgroup (its kFW requests share a chunk) into the chunk's own L2 line
@@ -310,6 +323,124 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   }
 }
 
+// ---- single-pass fetch: resolve, placement and gather in one kernel -----------------------------
+// Workgroup per kFF consecutive requests, wave per request: the wave resolves its request, the
+// workgroup's byte total is published and the bytes of every earlier request are found by
+// decoupled look-back over the earlier workgroups' published totals (a wave reads 64 predecessors
+// per step; a predecessor publishes its aggregate at once and its inclusive prefix when it knows
+// it), then every wave copies its own request. Workgroups take their index from a counter in
+// arrival order (a workgroup only waits on ones that started before it; the last to arrive resets
+// it), and the published words carry the fetch's epoch, so nothing is cleared between fetches.
+constexpr u32 kFF = 8;  // requests (waves) per single-pass workgroup
+constexpr u32 kLbAgg = 1u, kLbPre = 2u;
+
+__device__ __forceinline__ void lb_publish(const FetchArgs& a, u32 id, u64 v, u32 state) {
+  __hip_atomic_store(a.lb_val + id, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(a.lb_flag + id, (a.epoch << 2) | state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// bytes of every request before workgroup id's first (wave-uniform; the calling wave only)
+__device__ __forceinline__ u64 lb_exclusive(const FetchArgs& a, u32 id) {
+  const u32 lane = lane_id();
+  u64 excl = 0;
+  long j = (long)id - 1 - (long)lane;  // the predecessor this lane reads
+  while (true) {
+    const bool valid = j >= 0;
+    u32 state = 0;
+    while (true) {
+      if (valid) {
+        const u32 f = __hip_atomic_load(a.lb_flag + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        state = (f >> 2) == a.epoch ? (f & 3u) : 0u;
+      }
+      if (!__any(valid && state == 0u)) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const u64 v = valid ? __hip_atomic_load(a.lb_val + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const u64 pm = __ballot(valid && state == kLbPre);
+    if (pm) {  // the nearest predecessor with its prefix ends the look-back
+      const u32 k = (u32)__builtin_ctzll(pm);
+      excl += bcast_u64(wave_incl_scan<u64>(lane <= k ? v : (u64)0), 63);
+      return excl;
+    }
+    excl += bcast_u64(wave_incl_scan(v), 63);
+    j -= 64;
+    if (!__any(j >= 0)) return excl;  // (workgroup 0 publishes its prefix: not reached)
+  }
+}
+
+__global__ __launch_bounds__(64 * kFF) void fetch_fused_kernel(FetchArgs a) {
+  __shared__ u32 s_id;
+  __shared__ u64 s_nb[kFF];
+  __shared__ u64 s_base;
+  const DevState& st = a.st;
+  const u32 w = threadIdx.x >> 6, lane = lane_id();
+  if (threadIdx.x == 0) {
+    const u32 t = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_id = t;
+    // the last workgroup to arrive resets the counter for the next fetch (every other one has
+    // taken its index; the kernel boundary orders the store before the next fetch's adds)
+    if (t == gridDim.x - 1u) __hip_atomic_store(a.lb_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const u32 id = __builtin_amdgcn_readfirstlane(s_id);
+  const u32 r = id * kFF + w;
+  const bool live = r < a.n;
+  const Resolved q = resolve_request(a, r, live);
+  if (lane == 0) s_nb[w] = live ? q.bytes : 0ull;
+  __syncthreads();
+  if (w == 0) {
+    const u64 agg = bcast_u64(wave_incl_scan<u64>(lane < kFF ? s_nb[lane] : (u64)0), 63);
+    u64 excl = 0;
+    if (id == 0) {
+      if (lane == 0) lb_publish(a, 0, agg, kLbPre);
+    } else {
+      if (lane == 0) lb_publish(a, id, agg, kLbAgg);
+      excl = lb_exclusive(a, id);
+      if (lane == 0) lb_publish(a, id, excl + agg, kLbPre);
+    }
+    if (lane == 0) s_base = excl;
+  }
+  __syncthreads();
+  if (!live) return;
+  u64 pos = s_base;
+  for (u32 k = 0; k < w; ++k) pos += s_nb[k];
+  const u64 nb = q.bytes;
+  const bool served = nb && pos + nb <= a.out_cap;
+  if (lane == 0) {
+    a.res[4 * r + 0] = q.start;
+    a.res[4 * r + 1] = pos;
+    a.res[4 * r + 2] = (nb && !served) ? 0ull : (q.count | (nb << 32));
+    a.res[4 * r + 3] = (u64)(uint32_t)((nb && !served) ? kNoSpc : q.status);  // does not fit: its bytes still count
+    if (r + 1 == a.n) a.res[4ull * a.n] = pos + nb;  // bytes needed
+  }
+  if (!served) return;
+  const uint8_t* ring = st.logs + (q.ring >> 6);
+  const u64 mask = (1ull << (q.ring & 63ull)) - 1ull;
+  uint8_t* out = a.out + pos;
+  const u64 pieces = nb >> 4;
+  // four 16-byte pieces in flight per lane (named registers: a local array here went to scratch)
+  auto ld = [&](u64 i) { return *reinterpret_cast<const uint4*>(ring + ((q.pos0 + 16ull * i) & mask)); };
+  auto st16 = [&](u64 i, uint4 v) { *reinterpret_cast<uint4*>(out + 16ull * i) = v; };
+  u64 k = lane;
+  for (; k + 192 < pieces; k += 256) {
+    const uint4 x0 = ld(k), x1 = ld(k + 64), x2 = ld(k + 128), x3 = ld(k + 192);
+    st16(k, x0);
+    st16(k + 64, x1);
+    st16(k + 128, x2);
+    st16(k + 192, x3);
+  }
+  const bool b0 = k < pieces, b1 = k + 64 < pieces, b2 = k + 128 < pieces;
+  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0, x2 = x0;
+  if (b0) x0 = ld(k);
+  if (b1) x1 = ld(k + 64);
+  if (b2) x2 = ld(k + 128);
+  if (b0) st16(k, x0);
+  if (b1) st16(k + 64, x1);
+  if (b2) st16(k + 128, x2);
+}
+
+uint32_t fetch_fused_workgroups(uint32_t n) { return (n + kFF - 1) / kFF; }
+
 // ev[4]: start / end events of the two kernels, recorded by the dispatches themselves
 // (profiling: kernel time without the host's launch gaps), or null
 // Load the fetch kernels' code at engine creation (a process's first launch of a kernel otherwise
@@ -318,11 +449,21 @@ void preload_fetch_kernels() {
   hipFuncAttributes fa;
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_resolve_kernel));
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_fused_kernel));
 }
 
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
+  if (a.lb_flag) {  // single pass (ev: its start and end twice, so the profile's slots line up)
+    hipExtLaunchKernelGGL(fetch_fused_kernel, dim3(fetch_fused_workgroups(a.n)), dim3(64 * kFF), 0, s,
+                          e ? e[0] : nullptr, e ? e[1] : nullptr, 0, a);
+    if (e) {
+      (void)hipEventRecord(e[2], s);
+      (void)hipEventRecord(e[3], s);
+    }
+    return;
+  }
   (void)hipMemsetAsync(a.csum, 0, 8ull * kCsumStride * (a.n / kFetchChunk + 1), s);
   hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW - 1) / kFW), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);

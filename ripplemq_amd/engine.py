@@ -76,6 +76,14 @@ def state_to_dict(s: A.RmqPartitionState, rf: int) -> dict:
     return d
 
 
+class FetchTicket:
+    """An rmq_fetch_async in flight: its ticket and the arrays the engine writes into."""
+    __slots__ = ("ticket", "req", "res", "out")
+
+    def __init__(self, ticket: int, req: np.ndarray, res: np.ndarray, out: np.ndarray | None):
+        self.ticket, self.req, self.res, self.out = ticket, req, res, out
+
+
 class Engine:
     """One engine = one HIP device, P partitions, RF co-located or placed replicas."""
 
@@ -322,6 +330,35 @@ class Engine:
         if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
             raise EngineError(rc, "rmq_fetch")
         return rc, res, int(used.value)
+
+    def fetch_async(self, pidx, consumer, max_records, d_out: int | None = None, out_cap: int = 0,
+                    out: np.ndarray | None = None) -> "FetchTicket":
+        """rmq_fetch_async into a device buffer (d_out, 16-byte aligned) or a host array (out): the
+        call returns at once; fetch_poll(ticket) gives (rc, res, bytes_used) once it completes. The
+        handle keeps the request, result and output arrays alive until then."""
+        n = len(pidx)
+        req = np.empty((n, 4), np.uint32)
+        req[:, 0], req[:, 1], req[:, 2], req[:, 3] = pidx, consumer, max_records, 0
+        res = np.empty(n, FETCH_RES_DTYPE)
+        if d_out is not None:
+            mem, ptr = A.RMQ_MEM_DEVICE, C.c_void_p(d_out)
+        else:
+            out_cap = 0 if out is None else min(int(out_cap) or out.size, out.size)
+            mem, ptr = A.RMQ_MEM_HOST, (_ptr(out) if out is not None else None)
+        t = C.c_uint64()
+        _check(self.lib.rmq_fetch_async(self.h, _ptr(req), n, mem, ptr, out_cap, _ptr(res), C.byref(t)),
+               "rmq_fetch_async")
+        return FetchTicket(t.value, req, res, out)
+
+    def fetch_poll(self, tk: "FetchTicket", wait: bool = False):
+        """(rc, res, bytes_used) of an rmq_fetch_async ticket, or None while it runs."""
+        used = C.c_uint64()
+        rc = self.lib.rmq_fetch_poll(self.h, tk.ticket, 1 if wait else 0, C.byref(used))
+        if rc == A.RMQ_PENDING:
+            return None
+        if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
+            raise EngineError(rc, "rmq_fetch_poll")
+        return rc, tk.res, int(used.value)
 
     def set_segments(self, pidx, segment_bytes) -> None:
         """Ring sizes of partitions pidx[i] (rmq_set_segments: retention at a smaller size first, the

@@ -1,0 +1,110 @@
+"""rmq_fetch_async / rmq_fetch_poll (ABI 6) and the single-pass fetch kernel.
+
+An asynchronous fetch is ordered exactly like rmq_fetch (after every launch issued before it,
+before the ones issued after it), so its result must equal a synchronous fetch issued right after
+it (whose parity with the oracle test_gpu_pinned.py checks; PartitionStateMachine.java:85-110;
+MessageBatchReadRequestProcessor.java:36-42 answers each read from its own closure: the ticket is
+that completion). The single-pass kernel (resolve, placement by
+decoupled look-back, gather) and the two-kernel path must give the oracle's results on the same
+requests, ENOSPC cuts and bad requests included.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from parity import run_ops
+from ripplemq_amd import _abi as A
+from ripplemq_amd.engine import Engine, EngineConfig, EngineError
+from ripplemq_amd.workload import StreamSpec, make_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_async_fetch_matches_sync_while_appending(oracle_mod, monkeypatch, fused):
+    monkeypatch.setenv("RMQ_FETCH_FUSED", fused)
+    P = 64
+    cfg = EngineConfig(num_partitions=P, replication_factor=3, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=2, max_batch_records=4096, pipeline_depth=2)
+    spec = StreamSpec(P, 3000, "zipf", size=(1, 300), config_index=44)
+    batches = [make_batch(spec, b) for b in range(14)]
+    pp = np.arange(P, dtype=np.uint32)
+    g = np.random.default_rng(3)
+    with Engine(cfg) as dev:
+        pending = []
+        for k, b in enumerate(batches):
+            dev.append_async(b.pidx, b.lens, b.payload)
+            if k % 3 == 2:  # consumer 1 moves; its commit is ordered before the next fetches
+                dev.commit_consumer_offset(pp, np.ones(P, np.uint32), g.integers(0, 40 * k, P).astype(np.uint64))
+            cc = np.full(P, k & 1, np.uint32)
+            mx = np.full(P, 1 << 20, np.uint32)
+            if k % 2:  # host output (copied back at poll time) / device output
+                out = np.zeros(2 << 20, np.uint8)
+                tk = dev.fetch_async(pp, cc, mx, out=out, out_cap=out.size)
+            else:
+                d_out = dev.device_alloc(2 << 20)
+                tk = dev.fetch_async(pp, cc, mx, d_out=d_out, out_cap=2 << 20)
+            _, res, buf, _ = dev.fetch(pp, cc, mx)  # the same requests, ordered right after it
+            pending.append((k, tk, res.copy(), buf.copy(), None if k % 2 else d_out))
+        # more than four in flight: the oldest were completed into their arrays when slots ran out
+        first = dev.fetch_poll(pending[-1][1], wait=False)  # may be pending or done
+        got_first = first is not None
+        for k, tk, want, wbuf, d_out in pending[::-1]:
+            if got_first and tk is pending[-1][1]:
+                r = first
+            else:
+                r = dev.fetch_poll(tk, wait=True)
+            assert r is not None
+            _, res, used = r
+            for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                assert np.array_equal(res[f], want[f]), (k, f)
+            assert used == int(want["bytes"].sum())
+            if d_out is None:
+                assert np.array_equal(tk.out[:used], wbuf[:used]), k
+            else:
+                got = np.empty(used, np.uint8)
+                dev.d2h(got, d_out)
+                assert np.array_equal(got, wbuf[:used]), k
+                dev.device_free(d_out)
+        with pytest.raises(EngineError) as ei:  # answered once
+            dev.fetch_poll(pending[0][1], wait=True)
+        assert ei.value.status == A.RMQ_EINVAL
+        dev.sync()
+
+
+def test_async_fetch_empty_and_unknown():
+    cfg = EngineConfig(num_partitions=8, replication_factor=1, segment_bytes=1 << 16, index_interval=256,
+                       max_consumers=1, max_batch_records=1024)
+    with Engine(cfg) as dev:
+        tk = dev.fetch_async(np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+        assert dev.fetch_poll(tk, wait=False)[0] == A.RMQ_OK
+        tk.ticket = 1 << 40
+        with pytest.raises(EngineError):
+            dev.fetch_poll(tk)
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_fetch_paths_agree_with_oracle(oracle_mod, monkeypatch, fused):
+    """20k requests (several thousand look-back workgroups), unknown partitions, bad consumers,
+    zero-record slices, an output that ends mid-way and records of 1..4000 bytes."""
+    monkeypatch.setenv("RMQ_FETCH_FUSED", fused)
+    P, C = 512, 4
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 21, index_interval=512,
+                       max_consumers=C, max_batch_records=65536)
+    spec = StreamSpec(P, 30000, "zipf", size=(1, 4000), config_index=8)
+    g = np.random.default_rng(9)
+    n = 20000
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        ops = [("append", make_batch(spec, b)) for b in range(2)]
+        p = g.integers(0, P + 8, n)
+        c = g.integers(0, C + 1, n)
+        pc = np.repeat(np.arange(P), C)
+        cc = np.tile(np.arange(C), P)
+        ops.append(("consumer_commit", pc, cc, g.integers(0, 150, P * C)))
+        mx = g.integers(0, 60, n)
+        ops.append(("fetch", p, c, mx))
+        ops.append(("fetch", p, c, mx, 3 << 20))
+        ops.append(("fetch", p[:7], c[:7], mx[:7]))
+        ops.append(("fetch", p, c, np.full(n, 1024)))
+        run_ops(dev, ora, cfg, ops, check=False)
