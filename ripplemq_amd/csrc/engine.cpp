@@ -453,7 +453,7 @@ void free_engine(rmq_engine* e) {
                              s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq, e->d_crc,
                              e->d_stats, e->d_lb_ticket, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (rmq_engine::FetchSlot& f : e->fslot) {
-    void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv, f.d_lbf, f.d_out};
+    void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv, f.d_out};
     for (void* p : fs) bufs.push_back(p);
     if (f.h_req) hipHostFree(f.h_req);
     if (f.h_res) hipHostFree(f.h_res);
@@ -1285,12 +1285,12 @@ namespace {
 // Scratch of a fetch slot for n requests and, for a host output, out_cap bytes of device staging.
 int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
   if (n > f.cap) {
-    void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv, f.d_lbf};
+    void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv};
     for (void* p : ds)
       if (p) hipFree(p);
     if (f.h_req) hipHostFree(f.h_req);
     if (f.h_res) hipHostFree(f.h_res);
-    f.d_req = f.d_cpre = f.d_lbf = f.h_req = nullptr;
+    f.d_req = f.d_cpre = f.h_req = nullptr;
     f.d_res = f.d_aux = f.d_csum = f.d_lbv = f.h_res = nullptr;
     f.cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
@@ -1301,9 +1301,9 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
     if (!rc) rc = dalloc(&f.d_cpre, (size_t)cap + 4);
     if (!rc) rc = dalloc(&f.d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride);
     if (!rc) rc = dalloc(&f.d_lbv, wgs);
-    if (!rc) rc = dalloc(&f.d_lbf, wgs);
     if (rc) return rc;
-    HIP_TRY(hipMemset(f.d_lbf, 0, wgs * 4));  // epoch 0 is never a fetch's
+    HIP_TRY(hipMemset(f.d_lbv, 0, wgs * 8));  // epoch 0 is never a fetch's
+    f.epoch = 0;
     HIP_TRY(hipHostMalloc((void**)&f.h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&f.h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
     f.cap = cap;
@@ -1420,14 +1420,17 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
-    a.epoch = (uint32_t)(tk & 0x3FFFFFFFull) ? (uint32_t)(tk & 0x3FFFFFFFull) : 1u;
-    if (e->fetch_fused) {
-      a.lb_val = f.d_lbv;
-      a.lb_flag = f.d_lbf;
-      a.lb_ticket = e->d_lb_ticket;
-    }
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
+    if (e->fetch_fused) {
+      if (++f.epoch == fetch_epoch_limit()) {  // the epochs wrap: no stale word may match again
+        HIP_TRY(hipMemsetAsync(f.d_lbv, 0, (fetch_fused_workgroups(f.cap) + 1) * 8ull, e->fetch_s));
+        f.epoch = 1;
+      }
+      a.epoch = f.epoch;
+      a.lb_val = f.d_lbv;
+      a.lb_ticket = e->d_lb_ticket;
+    }
     HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     hipEvent_t ev[4] = {};
     if (e->profile) {  // kernel 3: the kernels' own durations; 4: first start to last end

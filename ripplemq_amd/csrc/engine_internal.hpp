@@ -318,7 +318,7 @@ struct rmq_engine {
     uint32_t* d_cpre = nullptr;
     uint64_t* d_csum = nullptr;
     uint64_t* d_lbv = nullptr;   // single pass: look-back words per workgroup
-    uint32_t* d_lbf = nullptr;
+    uint32_t epoch = 0;          //   and the slot's fetch number (wraps to 1 after a clear)
     uint32_t* h_req = nullptr;   // pinned
     uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}
     uint32_t cap = 0;
@@ -338,7 +338,7 @@ struct rmq_engine {
   static constexpr uint32_t kFetchSlots = 4;
   FetchSlot fslot[kFetchSlots];
   uint32_t fslot_next = 0;
-  uint64_t fetch_seq = 0;        // tickets (and the single pass's epochs)
+  uint64_t fetch_seq = 0;        // tickets
   std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
   uint32_t* d_lb_ticket = nullptr;
   bool fetch_fused = true;       // RMQ_FETCH_FUSED=0: resolve + gather kernels

@@ -333,10 +333,13 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
 // it), and the published words carry the fetch's epoch, so nothing is cleared between fetches.
 constexpr u32 kFF = 8;  // requests (waves) per single-pass workgroup
 constexpr u32 kLbAgg = 1u, kLbPre = 2u;
+// A published word is one 8-byte granule {bytes << 16 | epoch << 2 | state}, stored and polled with
+// relaxed agent-scope (sc1, L2-coherent) accesses: a granule is written whole, so no fence orders
+// its parts (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
+constexpr u32 kLbEpochBits = 14;
 
 __device__ __forceinline__ void lb_publish(const FetchArgs& a, u32 id, u64 v, u32 state) {
-  __hip_atomic_store(a.lb_val + id, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(a.lb_flag + id, (a.epoch << 2) | state, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  store_sc1(a.lb_val + id, (v << 16) | ((u64)a.epoch << 2) | state);
 }
 
 // bytes of every request before workgroup id's first (wave-uniform; the calling wave only)
@@ -346,23 +349,24 @@ __device__ __forceinline__ u64 lb_exclusive(const FetchArgs& a, u32 id) {
   long j = (long)id - 1 - (long)lane;  // the predecessor this lane reads
   while (true) {
     const bool valid = j >= 0;
+    u64 g = 0;
     u32 state = 0;
     while (true) {
       if (valid) {
-        const u32 f = __hip_atomic_load(a.lb_flag + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        state = (f >> 2) == a.epoch ? (f & 3u) : 0u;
+        g = load_sc1(a.lb_val + j);
+        state = ((u32)(g >> 2) & ((1u << kLbEpochBits) - 1u)) == a.epoch ? (u32)(g & 3u) : 0u;
       }
       if (!__any(valid && state == 0u)) break;
       __builtin_amdgcn_s_sleep(1);
     }
-    const u64 v = valid ? __hip_atomic_load(a.lb_val + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const u64 v = valid ? (g >> 16) : 0ull;
     const u64 pm = __ballot(valid && state == kLbPre);
     if (pm) {  // the nearest predecessor with its prefix ends the look-back
       const u32 k = (u32)__builtin_ctzll(pm);
       excl += bcast_u64(wave_incl_scan<u64>(lane <= k ? v : (u64)0), 63);
       return excl;
     }
-    excl += bcast_u64(wave_incl_scan(v), 63);
+    excl += bcast_u64(wave_incl_scan<u64>(v), 63);
     j -= 64;
     if (!__any(j >= 0)) return excl;  // (workgroup 0 publishes its prefix: not reached)
   }
@@ -440,6 +444,7 @@ __global__ __launch_bounds__(64 * kFF) void fetch_fused_kernel(FetchArgs a) {
 }
 
 uint32_t fetch_fused_workgroups(uint32_t n) { return (n + kFF - 1) / kFF; }
+uint32_t fetch_epoch_limit() { return 1u << kLbEpochBits; }
 
 // ev[4]: start / end events of the two kernels, recorded by the dispatches themselves
 // (profiling: kernel time without the host's launch gaps), or null
@@ -455,7 +460,7 @@ void preload_fetch_kernels() {
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
-  if (a.lb_flag) {  // single pass (ev: its start and end twice, so the profile's slots line up)
+  if (a.lb_val) {  // single pass (ev: its start and end twice, so the profile's slots line up)
     hipExtLaunchKernelGGL(fetch_fused_kernel, dim3(fetch_fused_workgroups(a.n)), dim3(64 * kFF), 0, s,
                           e ? e[0] : nullptr, e ? e[1] : nullptr, 0, a);
     if (e) {
