@@ -642,6 +642,8 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
 
     t_max = grp.max(elapsed)
     sent_max = grp.max(float(x1["bytes_sent"] - x0["bytes_sent"]))
+    waits_max = grp.max(float(x1["host_waits"] - x0["host_waits"]))
+    wait_ms_max = grp.max(float(x1["host_wait_ns"] - x0["host_wait_ns"]) / 1e6)
     if grp.max(float(x1["refused_crc"] + x1["refused_log"])):
         raise SystemExit("bench: a follower refused replication rounds; the measurement would be void")
 
@@ -691,6 +693,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
                          "batches_per_launch": n_applied / max(n_launch, 1)},
             "xgmi": None if world == 1 else {
                 "bytes_sent_per_gpu_max": sent_max, "achieved": sent_max / t_max / 1e9,
+                "host_waits_for_round_sizes": int(waits_max), "host_wait_ms": wait_ms_max,
                 # the in-process transport copies inside one GPU: no link is measured
                 "peak": None if args.transport == "local" else XGMI_LINK_GBS * (world - 1), "unit": "GB/s",
                 "frac": None if args.transport == "local" else sent_max / t_max / 1e9 / (XGMI_LINK_GBS * (world - 1)),

@@ -192,6 +192,9 @@ typedef struct rmq_repl_stats {
   uint64_t general_plans;      /* leader: destination plans by the general path (a consumer-offset row or
                                   a catch-up gap among the entries, or over 4,096 entries); the
                                   steady-state plan covers the rest. A diagnostic of the round's cost */
+  uint64_t host_waits;         /* rounds whose {bytes, records} swap had not landed when the host
+                                  posted the round (RCCL's send/recv take host-side byte counts) */
+  uint64_t host_wait_ns;       /* host time spent in those waits */
 } rmq_repl_stats;
 
 typedef struct rmq_engine rmq_engine;

@@ -92,7 +92,7 @@ class RmqReplStats(C.Structure):
         ("world", u32), ("rank", u32), ("out_entries", u32), ("in_entries", u32), ("rounds", u64),
         ("bytes_sent", u64), ("bytes_received", u64), ("records_ingested", u64), ("refused_crc", u64),
         ("refused_log", u64), ("bytes_ingested", u64), ("catchup_entries", u64), ("detached_plans", u64),
-        ("general_plans", u64),
+        ("general_plans", u64), ("host_waits", u64), ("host_wait_ns", u64),
     ]
 
 

@@ -1770,6 +1770,8 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   out->catchup_entries = c[4];
   out->detached_plans = c[5];
   out->general_plans = c[6];
+  out->host_waits = r->host_waits;
+  out->host_wait_ns = r->host_wait_ns;
   return RMQ_OK;
 }
 

@@ -203,6 +203,7 @@ struct Replication {
   std::deque<uint32_t> sized;    // sets whose size exchange is posted, data exchange not yet
   std::deque<uint32_t> acking;   // sets whose data exchange is posted, acks not yet applied
   uint64_t rounds = 0, bytes_sent = 0, bytes_recv = 0;
+  uint64_t host_waits = 0, host_wait_ns = 0;  // post_round found the sizes not landed yet
   uint32_t last_set = ~0u;       // set of the last posted round (rmq_read_outbox)
   // fault injection (rmq_fault_drop_rounds): the rounds of the next `drop_n` groups whose first
   // ticket is at least `drop_from` send empty regions

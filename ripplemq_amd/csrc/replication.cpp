@@ -24,6 +24,7 @@
 // that drive them): with a transport attached, launch groups close only when full, and control
 // calls that flush (rmq_sync, placement, leadership) are collective. At a drain the remaining
 // rounds are exchanged and their acks applied by a separate kernel.
+#include <chrono>
 #include <numeric>
 
 #include "engine_internal.hpp"
@@ -117,7 +118,14 @@ int post_round(rmq_engine* e, uint32_t s) {
   Replication* r = e->repl;
   XchgSet& x = r->sets[s];
   const uint32_t W = r->world, me = r->rank;
-  HIP_TRY(hipEventSynchronize(x.ev_sz));
+  // RCCL's grouped send/recv take host-side byte counts: the sizes were swapped one launch earlier,
+  // so this normally finds them landed; a wait is counted (rmq_repl_stats.host_waits)
+  if (hipEventQuery(x.ev_sz) == hipErrorNotReady) {
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipEventSynchronize(x.ev_sz));
+    r->host_waits++;
+    r->host_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  }
   const uint64_t* hs = x.h_sizes;  // [q]: {send bytes, send records}, then [W + q]: {recv bytes, recv records}
   void* sb[kMaxWorld];
   void* rb[kMaxWorld];

@@ -17,6 +17,7 @@
 #   prof       rocprofv3 --kernel-trace --stats of the default line (kernel stats CSV)
 #   pmc        rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) of a 300-step line
 #   stamps     per-wave phase stamps of launch 100 (RMQ_STAMPS) + timing-only RMQ_DEBUG lines
+#   legs       fetch / mixed / tier legs of a short line, single-pass and two-kernel fetch
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -76,6 +77,8 @@ for step in "$@"; do
         env "$var=$val" timeout -k 10 200 python bench.py --steps 600 --warmup 60 $Q > "gpurun_out/${T}_${var}_${val}_600.json" 2>&1 || exit 1
         env "$var=$val" timeout -k 10 200 python bench.py --steps 20 --warmup 5 $Q > "gpurun_out/${T}_${var}_${val}_20.json" 2>&1 || exit 1
       done ;;
+    legs)  # the side legs (fetch, mixed, tier) on a short line, with the single-pass and the two-kernel fetch
+      for f in 1 0; do RMQ_FETCH_FUSED=$f run 300 "${T}_legs_fused$f.json" python bench.py --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0; done ;;
     fetchprof|fetchprof:*)  # kernel trace of the fetch legs (short append run), current library and variants/NAME
       V=${step#fetchprof}; V=${V#:}
       FQ="--steps 100 --warmup 10 --no-cpu-baseline --concurrent-rounds 0 --host-steps 0"
