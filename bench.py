@@ -243,16 +243,14 @@ def host_leg(eng, batches, steps: int) -> dict:
 
 def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
     """Appends and consumer fetches at once on one engine (configs[4]: concurrent consumer fetch at
-    lagging offsets), as a broker runs them: a producer thread submits `rounds` x `appends`
-    device-resident batches; meanwhile the consumer loop fetches every (partition, consumer) at
-    max = 10 and commits the next offsets (read-then-commit, ConsumerClientImpl.java:61-117), with
-    the consumers split in two halves whose fetches alternate through rmq_fetch_async: while one
-    half's fetch runs on the GPU, the other half's results are read and committed, so a consumer
-    never fetches before its previous commit and the host never waits on the append pipeline.
-    Every fetch is ordered between two pipeline launches (the next launch waits for it). Reports
-    both rates over the same wall time."""
-    import threading
-
+    lagging offsets), driven by ONE host thread as a broker's event loop would: per round `appends`
+    device-resident batches go to the pipeline; the consumers (split in two halves) fetch at
+    max = 10 through rmq_fetch_async and commit the next offsets (read-then-commit,
+    ConsumerClientImpl.java:61-117). A fetch is polled without waiting; once its results are in,
+    that half commits and the other half's fetch is issued, so a consumer never fetches before
+    its previous commit and the host never waits on the append pipeline. Every fetch is ordered
+    between two pipeline launches (the next launch waits for it). Reports both rates over the
+    same wall time."""
     P = spec.partitions
     eng.sync()
     st = eng.states()
@@ -270,74 +268,51 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     hmax = [np.full(int(m.sum()), mx, np.uint32) for m in half]
     hi = spec.size if isinstance(spec.size, int) else spec.size[1]
     cap = P * consumers * mx * (16 + (hi + 15) // 16 * 16) + 4096
-    d_out = [eng.device_alloc(cap), eng.device_alloc(cap)]
-    done = threading.Event()
-    err = []
+    d_out = eng.device_alloc(cap)
+    fetched = resets = fetches = 0
+    t_host = 0.0
     k0 = 10_000
 
-    def producer():
-        try:
-            for k in range(rounds):
-                for j in range(appends):
-                    step(k0 + k * appends + j)
-        except BaseException as ex:  # noqa: BLE001 - re-raised below
-            err.append(ex)
-        finally:
-            done.set()
-
-    fetched = resets = fetches = 0
-    t_wait = 0.0
-
-    def consume(h, tk):
-        nonlocal fetched, resets, t_wait
-        t1 = time.perf_counter()
-        rc, res, _ = eng.fetch_poll(tk, wait=True)
-        t_wait += time.perf_counter() - t1
+    def consume(h, r):
+        nonlocal fetched, resets
+        rc, res, _ = r
         stt = res["status"]
         if rc or np.any((stt != 0) & (stt != -6)):
             raise SystemExit(f"bench: mixed leg fetch failed rc={rc} statuses={np.unique(stt)}")
         n = res["count"].astype(np.uint64)
         fetched += int(n.sum())
-        nxt = res["start_offset"] + n
-        gone = stt == -6  # RMQ_EOFFSET: the ring moved past a slow consumer; it resumes at the
-        resets += int(gone.sum())  # first retained offset, which the row carries
-        eng.commit_consumer_offset(hp[h], hc[h], nxt)
+        resets += int(np.count_nonzero(stt == -6))  # RMQ_EOFFSET: the ring moved past a slow
+        eng.commit_consumer_offset(hp[h], hc[h], res["start_offset"] + n)  # consumer: it resumes at
+        # the first retained offset, which start_offset carries
 
-    th = threading.Thread(target=producer, daemon=True)
     t0 = time.perf_counter()
-    th.start()
-    tk = [eng.fetch_async(hp[0], hc[0], hmax[0], d_out=d_out[0], out_cap=cap), None]
-    fetches = 1
     h = 0
-    while True:
-        o = h ^ 1
-        if tk[o] is not None:
-            consume(o, tk[o])
-            tk[o] = None
-        if done.is_set():
-            break
-        tk[o] = eng.fetch_async(hp[o], hc[o], hmax[o], d_out=d_out[o], out_cap=cap)
-        fetches += 1
-        h = o
-    for o in (0, 1):
-        if tk[o] is not None:
-            consume(o, tk[o])
-    th.join()
-    if err:
-        raise err[0]
+    tk = eng.fetch_async(hp[h], hc[h], hmax[h], d_out=d_out, out_cap=cap)
+    fetches = 1
+    for k in range(rounds):
+        for j in range(appends):
+            step(k0 + k * appends + j)
+        t1 = time.perf_counter()
+        r = eng.fetch_poll(tk, wait=False)
+        if r is not None:
+            consume(h, r)
+            h ^= 1
+            tk = eng.fetch_async(hp[h], hc[h], hmax[h], d_out=d_out, out_cap=cap)
+            fetches += 1
+        t_host += time.perf_counter() - t1
+    consume(h, eng.fetch_poll(tk, wait=True))
     eng.sync()
     dt = time.perf_counter() - t0
-    for d in d_out:
-        eng.device_free(d)
+    eng.device_free(d_out)
     recs = rounds * appends * spec.records
     return {"append_msgs_per_s": recs / dt, "fetch_records_per_s": fetched / dt, "rounds": rounds,
             "appends_per_round": appends, "fetches": fetches, "requests_per_fetch": P * consumers // 2,
-            "max_records": mx, "wall_s": dt, "consumer_wait_s": t_wait,
+            "max_records": mx, "wall_s": dt, "consumer_host_s": t_host,
             "lag_bound": "U[0, retained records / 2] per partition at the start",
             "consumer_resets": resets,
-            "note": "a producer thread appends (device-resident batches) while the consumer loop fetches "
-                    "every (partition, consumer) at max = 10 through rmq_fetch_async, two halves of the "
-                    "consumers alternating, and commits each half's next offsets before its next fetch; "
+            "note": "one host thread: appends (device-resident batches) and, between them, the consumers' "
+                    "fetches at max = 10 through rmq_fetch_async (polled without waiting, two halves of the "
+                    "consumers alternating, each half committing its next offsets before its next fetch); "
                     "both rates over the same wall time; consumers start lagging the high watermark by "
                     "U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not HBM-resident at 4,096 "
                     "partitions, so it is bounded by what the rings retain)"}
@@ -432,9 +407,11 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         d_out = eng.device_alloc(cap)
         recs = nbytes = 0
         t_kern = t_wall = t_reg = 0.0
-        # one untimed call first: a process's first launch of a kernel loads its code object
-        # (~20 ms, measured between the first resolve and gather in profiles/r03q_prof)
-        eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+        # untimed calls first: a process's first launch of a kernel loads its code object
+        # (~20 ms, measured between the first resolve and gather in profiles/r03q_prof), and each
+        # of the engine's four fetch slots allocates its scratch on first use
+        for _ in range(4):
+            eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
         for k in range(rounds):
             lag = (g.random(P * consumers) * (np.repeat(hw - lo, consumers) + 1)).astype(np.int64)
             eng.commit_consumer_offset(pp, cc, (np.repeat(hw, consumers) - lag).astype(np.uint64))

@@ -167,6 +167,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.key_passes = e->key_passes;
   a.key_bits = e->key_bits;
   a.rank_mode = e->rank_mode;
+  a.steal = e->steal;
   a.gt = e->max_group_tiles;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
@@ -178,7 +179,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.s1 = e->scratch[s1->set];
     if (e->set_reset & (1u << s1->set)) {  // a drain skipped the stage 4 that resets the set's list and sums
       HIP_TRY(hipMemsetAsync(a.s1.bacc, 0, kMaxGroup * 2 * sizeof(uint64_t), e->main_s));
-      HIP_TRY(hipMemsetAsync(a.s1.nbig, 0, sizeof(uint32_t), e->main_s));
+      HIP_TRY(hipMemsetAsync(a.s1.nbig, 0, 4 * sizeof(uint32_t), e->main_s));
       e->set_reset &= ~(1u << s1->set);
     }
     a.wg1 = e->s1_wgs ? std::min<uint32_t>(s1->tiles, e->s1_wgs) : s1->tiles;
@@ -603,6 +604,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK")) e->rank_mode = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_STEAL")) e->steal = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
@@ -701,7 +703,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_TRY(dalloc(&x.tile_base, GT));
     CREATE_TRY(dalloc(&x.binfo, (size_t)kMaxGroup * 4));
     CREATE_TRY(dalloc(&x.bacc, (size_t)kMaxGroup * 2));
-    CREATE_TRY(dalloc(&x.nbig, 1));
+    CREATE_TRY(dalloc(&x.nbig, 4));
     CREATE_TRY(dalloc(&x.bigl, GT * kTileRecs));
   }
   if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(2u * e->cu_count + kMaxTiles + (P + kPipeThreads - 1) / kPipeThreads +
@@ -1283,7 +1285,15 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
 namespace {
 
 // Scratch of a fetch slot for n requests and, for a host output, out_cap bytes of device staging.
-int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
+// Plain hipMalloc (no zeroing, no device synchronisation: a slot first used while the pipeline
+// runs must not wait for it); the look-back words are zeroed on the fetch stream.
+int fetch_alloc(void** p, size_t bytes) {
+  *p = nullptr;
+  HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16)));
+  return RMQ_OK;
+}
+
+int fetch_slot_reserve(rmq_engine* e, rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
   if (n > f.cap) {
     void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv};
     for (void* p : ds)
@@ -1295,14 +1305,14 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
     f.cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
     const size_t wgs = fetch_fused_workgroups(cap) + 1;
-    int rc = dalloc(&f.d_req, (size_t)cap * 4);
-    if (!rc) rc = dalloc(&f.d_res, (size_t)cap * 4 + 2);
-    if (!rc) rc = dalloc(&f.d_aux, (size_t)cap * 2);
-    if (!rc) rc = dalloc(&f.d_cpre, (size_t)cap + 4);
-    if (!rc) rc = dalloc(&f.d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride);
-    if (!rc) rc = dalloc(&f.d_lbv, wgs);
+    int rc = fetch_alloc((void**)&f.d_req, (size_t)cap * 16);
+    if (!rc) rc = fetch_alloc((void**)&f.d_res, ((size_t)cap * 4 + 2) * 8);
+    if (!rc) rc = fetch_alloc((void**)&f.d_aux, (size_t)cap * 16);
+    if (!rc) rc = fetch_alloc((void**)&f.d_cpre, ((size_t)cap + 4) * 4);
+    if (!rc) rc = fetch_alloc((void**)&f.d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride * 8);
+    if (!rc) rc = fetch_alloc((void**)&f.d_lbv, wgs * 8);
     if (rc) return rc;
-    HIP_TRY(hipMemset(f.d_lbv, 0, wgs * 8));  // epoch 0 is never a fetch's
+    HIP_TRY(hipMemsetAsync(f.d_lbv, 0, wgs * 8, e->fetch_s));  // epoch 0 is never a fetch's
     f.epoch = 0;
     HIP_TRY(hipHostMalloc((void**)&f.h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&f.h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
@@ -1312,7 +1322,7 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
     if (f.d_out) hipFree(f.d_out);
     f.d_out = nullptr;
     f.out_alloc = 0;
-    const int rc = dalloc(&f.d_out, stage);
+    const int rc = fetch_alloc((void**)&f.d_out, stage);
     if (rc) return rc;
     f.out_alloc = stage;
   }
@@ -1401,7 +1411,7 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     *ticket = tk;
     return RMQ_OK;
   }
-  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0);
+  int rc = fetch_slot_reserve(e, f, n, mem == RMQ_MEM_HOST ? out_cap : 0);
   if (rc) return rc;
   uint8_t* d_out = mem == RMQ_MEM_HOST ? (out_cap ? f.d_out : nullptr) : out;
   std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));

@@ -273,7 +273,9 @@ struct rmq_engine {
   uint32_t max_tiles = 0;
   uint32_t key_passes = 0;
   uint32_t key_bits = 0;
-  uint32_t rank_mode = 1;  // RMQ_RANK: stage 1 by hash counters (1) or by the LDS radix sort (0)
+  uint32_t rank_mode = 0;  // RMQ_RANK: stage 1 by the LDS radix sort (0) or by hash counters (1;
+                           // 4.86 vs 5.14 G msgs/s at config B, profiles/r04c_*)
+  uint32_t steal = 1;      // RMQ_STEAL: stage-3 workgroups take stage-1 tiles when out of tasks
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
   CopyPool* copy_pool = nullptr;  // host batches (created with the first one)

@@ -221,7 +221,8 @@ struct PipeScratch {
   uint64_t* binfo;      // [kMaxGroup][4] per batch {reject flags (2 invalid payload ranges), 0, payload bytes, 0}
   uint64_t* bacc;       // [kMaxGroup][2] per batch {payload bytes, invalid records} (stage 1 adds,
                         //   stage 2 reads, stage 4 resets)
-  uint32_t* nbig;       // [1] records over 1 KB in the group (stage 1 appends, stage 4 resets)
+  uint32_t* nbig;       // [4] {records over 1 KB in the group (stage 1 appends), tiles taken by
+                        //   stage-1 workgroups, 0, 0} (stage 4 resets)
   uint32_t* bigl;       // [tiles * kTileRecs] their group record slots, in no particular order
 };
 
@@ -261,6 +262,7 @@ struct PipeArgs {
   uint64_t* ret_late;      // host-visible: written with launch_seq when a partition's retention of
                            // the group applied stops early (its stage 4 in the next launch finishes it)
   uint64_t launch_seq;
+  uint32_t steal;          // stage-3 workgroups rank stage-1 tiles once out of tasks (RMQ_STEAL)
   uint64_t* stamps;        // diagnostic only (RMQ_STAMPS): [workgroup][wave][8] s_memrealtime, or null
 };
 

@@ -75,14 +75,15 @@ constexpr u32 kRejInvalid = 2u;
 
 // Diagnostic phase stamps (RMQ_STAMPS): stamps[(workgroup * 8 + wave) * 8 + k], s_memrealtime
 // (100 MHz). Never read by the kernel.
-#define PIPE_STAMP(k)                                                                         \
+#define PIPE_STAMP_ROW(row, k)                                                                \
   do {                                                                                        \
     if (A.stamps) {                                                                           \
       const u64 t_ = __builtin_amdgcn_s_memrealtime();                                        \
       if ((threadIdx.x & 63) == 0)                                                            \
-        A.stamps[((u64)blockIdx.x * kPW + (threadIdx.x >> 6)) * 8 + (k)] = t_;               \
+        A.stamps[((u64)(row) * kPW + (threadIdx.x >> 6)) * 8 + (k)] = t_;                    \
     }                                                                                         \
   } while (0)
+#define PIPE_STAMP(k) PIPE_STAMP_ROW(blockIdx.x, k)
 
 struct Stage1Smem {
   u32 items[2][kTR];   // key << 10 | position in tile (ping-pong between radix passes)
@@ -158,7 +159,9 @@ __device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S) {
+// srow: the stamp row of the tile (diagnostics): its dedicated stage-1 workgroup's, also when a
+// stage-3 workgroup ranks it
+__device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S, u32 srow) {
   const PipeGroup& G = A.g1;
   const u32 jb = batch_of_tile(G, t);
   const PipeBatch& b = G.b[jb];
@@ -169,7 +172,7 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
   const u32 P = A.st.P;
   const u64 lt = (1ull << lane) - 1ull;
   const u32 nin = b.n - base < kTR ? b.n - base : kTR;
-  PIPE_STAMP(0);
+  PIPE_STAMP_ROW(srow, 0);
 
   // ---- loads (input position q = 128w + 64r + lane)
   u32 item[kTI], lenv[kTI], fl[kTI];
@@ -252,7 +255,7 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
     }
   }
 
-  PIPE_STAMP(1);
+  PIPE_STAMP_ROW(srow, 1);
   // ---- stable LDS radix sort of the tile by partition id, 8-bit digits
   u32 buf = 0;
   for (u32 pass = 0; pass < A.key_passes; ++pass) {
@@ -315,7 +318,7 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
     buf ^= 1u;
   }
   const u32* sorted = S.items[buf ^ 1u];
-  PIPE_STAMP(2);
+  PIPE_STAMP_ROW(srow, 2);
 
   // ---- segmented scan of {1, rs16} over the sorted tile (segments = partitions)
   u64 val[kTI], inc[kTI];
@@ -363,7 +366,7 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
     if (nkey != key && (v >> 40)) x.hist[(u64)key * A.gt + t] = v;
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(3);
+  PIPE_STAMP_ROW(srow, 3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -395,7 +398,7 @@ __device__ __forceinline__ u32 wave_or_all(u32 v) {
   return (u32)__builtin_amdgcn_readlane((int)v, 63);
 }
 
-__device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage1HSmem& S) {
+__device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage1HSmem& S, u32 srow) {
   const PipeGroup& G = A.g1;
   const u32 jb = batch_of_tile(G, t);
   const PipeBatch& b = G.b[jb];
@@ -406,7 +409,7 @@ __device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage
   const u32 P = A.st.P;
   const u64 lt = (1ull << lane) - 1ull;
   const u32 nin = b.n - base < kTR ? b.n - base : kTR;
-  PIPE_STAMP(0);
+  PIPE_STAMP_ROW(srow, 0);
   for (u32 k = tid; k < kHT; k += kPT) S.key[k] = 0u;  // (ordered by the barrier of the scans below)
 
   // ---- loads (input position q = kWR w + 64 r + lane)
@@ -481,7 +484,7 @@ __device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage
       if (ic) __hip_atomic_fetch_add(&x.bacc[jb * 2 + 1], ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  PIPE_STAMP(1);
+  PIPE_STAMP_ROW(srow, 1);
 
   // ---- per slot, in registers: peers (same partition), the count and bytes/16 of the peers
   // below the lane, and the slot's total of the lane's partition
@@ -514,7 +517,7 @@ __device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage
     wb[r] = bsum;
     stot[r] = ((u64)__popcll(pm) << 40) | btot;
   }
-  PIPE_STAMP(2);
+  PIPE_STAMP_ROW(srow, 2);
 
   // ---- the partitions' counters, slot after slot in input order (wave after wave)
   u64 before[kTI];
@@ -552,7 +555,7 @@ __device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage
     }
     __syncthreads();
   }
-  PIPE_STAMP(3);
+  PIPE_STAMP_ROW(srow, 3);
 #pragma unroll
   for (u32 r = 0; r < kTI; ++r) {
     const u32 q = w * kWR + r * 64u + lane;
@@ -566,7 +569,7 @@ __device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage
     if (kv) x.hist[(u64)(kv - 1u) * A.gt + t] = S.val[k];
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  PIPE_STAMP(4);
+  PIPE_STAMP_ROW(srow, 4);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1889,6 +1892,29 @@ __device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
 #define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
+// Stage 1 of the launch's group, tile by tile: a static share (tiles wg, wg + wg1, ...) or, with
+// RMQ_STEAL, tiles taken from the group's counter (s1.nbig[1]) by the dedicated stage-1 workgroups
+// and by stage-3 workgroups that ran out of tasks, so ranking starts as soon as stage 3 frees a
+// slot instead of when the dispatcher reaches the stage-1 workgroups.
+__device__ __forceinline__ void stage1_tiles(const PipeArgs& A, char* smem, u32 wg, bool take) {
+  __shared__ u32 s_t;
+  for (u32 t = wg;;) {
+    if (take) {
+      if (threadIdx.x == 0) s_t = __hip_atomic_fetch_add(A.s1.nbig + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      t = s_t;
+    }
+    if (t >= A.g1.tiles) break;
+    const u32 srow = A.s3_lead + t % A.wg1;
+    if (A.rank_mode)
+      stage1_tile_hash(A, t, *reinterpret_cast<Stage1HSmem*>(smem), srow);
+    else
+      stage1_tile(A, t, *reinterpret_cast<Stage1Smem*>(smem), srow);
+    __syncthreads();  // the tile's LDS (and s_t) are reused by the next one
+    if (!take) t += A.wg1;
+  }
+}
+
 // XR: a replication transport is attached (stage 3 also fills the group's outbox); a separate
 // instantiation so the single-GPU kernel keeps its register budget.
 template <bool XR>
@@ -1922,13 +1948,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (!s3) {
     if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
     if (wg < A.wg1) {  // a workgroup ranks tiles wg, wg + wg1, ... (RMQ_S1_WGS < tiles: fewer slots held)
-      for (u32 t = wg; t < A.g1.tiles; t += A.wg1) {
-        if (A.rank_mode)
-          stage1_tile_hash(A, t, *reinterpret_cast<Stage1HSmem*>(smem_raw));
-        else
-          stage1_tile(A, t, *reinterpret_cast<Stage1Smem*>(smem_raw));
-        __syncthreads();  // the tile's LDS is reused by the next one
-      }
+      stage1_tiles(A, smem_raw, wg, A.steal != 0u);
       return;
     }
     wg -= A.wg1;
@@ -1939,8 +1959,8 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     wg -= A.wg2;
     // partition threads: stage 3's state advance and stage 4's retention
     PIPE_STAMP(0);
-    if (wg == 0 && A.g4.nb) {  // the set's next group starts its list and its batch sums
-      if (threadIdx.x == 0) *A.s4.nbig = 0u;
+    if (wg == 0 && A.g4.nb) {  // the set's next group starts its list, tile counter and batch sums
+      if (threadIdx.x < 4) A.s4.nbig[threadIdx.x] = 0u;
       if (threadIdx.x < kMaxGroup * 2) A.s4.bacc[threadIdx.x] = 0ull;
     }
     for (u32 p = wg * kPT + threadIdx.x; p < A.st.P; p += A.wgp * kPT) partition_threads(A, p);
@@ -1986,6 +2006,10 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP(6);
+  if (A.steal && A.g1.nb && !(A.debug & 16u)) {  // out of tasks: rank tiles of the launch's group
+    __syncthreads();  // every wave is done with the stage-3 LDS
+    stage1_tiles(A, smem_raw, 0, true);
+  }
 }
 
 #ifdef RMQ_PIPE_XR_TU
