@@ -632,7 +632,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
   }
-  if (const char* v = std::getenv("RMQ_FETCH_FUSED")) e->fetch_fused = std::atoi(v) != 0;
+  if (const char* v = std::getenv("RMQ_FETCH_FUSED")) e->fetch_fused = (uint32_t)std::atoi(v);
   CREATE_TRY(dalloc(&e->d_lb_ticket, 4));
   CREATE_HIP(hipMemset(e->d_lb_ticket, 0, 4));
 
@@ -1439,7 +1439,7 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
       }
       a.epoch = f.epoch;
       a.lb_val = f.d_lbv;
-      a.lb_ticket = e->d_lb_ticket;
+      a.lb_ticket = e->fetch_fused == 2 ? e->d_lb_ticket : nullptr;
     }
     HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     hipEvent_t ev[4] = {};

@@ -275,7 +275,8 @@ struct rmq_engine {
   uint32_t key_bits = 0;
   uint32_t rank_mode = 0;  // RMQ_RANK: stage 1 by the LDS radix sort (0) or by hash counters (1;
                            // 4.86 vs 5.14 G msgs/s at config B, profiles/r04c_*)
-  uint32_t steal = 1;      // RMQ_STEAL: stage-3 workgroups take stage-1 tiles when out of tasks
+  uint32_t steal = 0;      // RMQ_STEAL=1: stage-3 workgroups take stage-1 tiles when out of tasks
+                           // (5.20 -> 4.00 G msgs/s: stage 2 and the second half of stage 3 start later)
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
   CopyPool* copy_pool = nullptr;  // host batches (created with the first one)
@@ -344,7 +345,8 @@ struct rmq_engine {
   uint64_t fetch_seq = 0;        // tickets
   std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
   uint32_t* d_lb_ticket = nullptr;
-  bool fetch_fused = true;       // RMQ_FETCH_FUSED=0: resolve + gather kernels
+  uint32_t fetch_fused = 1;      // RMQ_FETCH_FUSED: 1 single pass (dispatch-order look-back), 2 the
+                                 // same with arrival-order indices, 0 resolve + gather kernels
   // consumer-offset commits: two staging slots (pinned items -> device by one copy on the pipeline
   // stream), so a commit is ordered with the append stream without waiting for it
   struct CommitSlot {

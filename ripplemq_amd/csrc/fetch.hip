@@ -275,30 +275,36 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
       small = small && (!nbr || po + nbr > a.out_cap || (nbr >> 4) <= 128u);
     }
     if (small) {
-      uint4 x[kGQ][2];
-#pragma unroll
-      for (u32 q = 0; q < kGQ; ++q) {
-        const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);
-        const bool sv = nbr && po + nbr <= a.out_cap;
-        const u64 pos0 = bcast_u64(q_pos, q), rw = bcast_u64(q_ring, q);
-        const uint8_t* ring = st.logs + (rw >> 6);
-        const u64 mask = (1ull << (rw & 63ull)) - 1ull;
-#pragma unroll
-        for (u32 h = 0; h < 2; ++h) {
-          const u64 k = lane + 64u * h;
-          if (sv && k < (nbr >> 4)) x[q][h] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * k) & mask));
-        }
-      }
-#pragma unroll
-      for (u32 q = 0; q < kGQ; ++q) {
-        const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);
-        const bool sv = nbr && po + nbr <= a.out_cap;
-#pragma unroll
-        for (u32 h = 0; h < 2; ++h) {
-          const u64 k = lane + 64u * h;
-          if (sv && k < (nbr >> 4)) *reinterpret_cast<uint4*>(a.out + po + 16ull * k) = x[q][h];
-        }
-      }
+      // named registers (a local array here went to scratch): request q's two pieces per lane
+#define RMQ_GQ_LOAD(q, x0, x1)                                                                        \
+  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;                                                        \
+  {                                                                                                   \
+    const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);                                     \
+    const bool sv = nbr && po + nbr <= a.out_cap;                                                     \
+    const u64 pos0 = bcast_u64(q_pos, q), rw = bcast_u64(q_ring, q);                                  \
+    const uint8_t* ring = st.logs + (rw >> 6);                                                        \
+    const u64 mask = (1ull << (rw & 63ull)) - 1ull;                                                   \
+    if (sv && lane < (nbr >> 4)) x0 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * lane) & mask)); \
+    if (sv && lane + 64u < (nbr >> 4)) x1 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (lane + 64u)) & mask)); \
+  }
+#define RMQ_GQ_STORE(q, x0, x1)                                                                       \
+  {                                                                                                   \
+    const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);                                     \
+    const bool sv = nbr && po + nbr <= a.out_cap;                                                     \
+    if (sv && lane < (nbr >> 4)) *reinterpret_cast<uint4*>(a.out + po + 16ull * lane) = x0;         \
+    if (sv && lane + 64u < (nbr >> 4)) *reinterpret_cast<uint4*>(a.out + po + 16ull * (lane + 64u)) = x1; \
+  }
+      static_assert(kGQ == 4, "four requests per gather wave");
+      RMQ_GQ_LOAD(0, a0, a1)
+      RMQ_GQ_LOAD(1, b0, b1)
+      RMQ_GQ_LOAD(2, c0, c1)
+      RMQ_GQ_LOAD(3, d0, d1)
+      RMQ_GQ_STORE(0, a0, a1)
+      RMQ_GQ_STORE(1, b0, b1)
+      RMQ_GQ_STORE(2, c0, c1)
+      RMQ_GQ_STORE(3, d0, d1)
+#undef RMQ_GQ_LOAD
+#undef RMQ_GQ_STORE
       return;
     }
   }
@@ -312,11 +318,14 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
     const u64 pieces = nbr >> 4;
     u64 p = lane;
     for (; p + 192 < pieces; p += 256) {  // four 16-byte pieces in flight per lane
-      uint4 x[4];
-#pragma unroll
-      for (u32 u = 0; u < 4; ++u) x[u] = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 64 * u)) & mask));
-#pragma unroll
-      for (u32 u = 0; u < 4; ++u) *reinterpret_cast<uint4*>(out + 16ull * (p + 64 * u)) = x[u];
+      const uint4 x0 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * p) & mask));
+      const uint4 x1 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 64)) & mask));
+      const uint4 x2 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 128)) & mask));
+      const uint4 x3 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (p + 192)) & mask));
+      *reinterpret_cast<uint4*>(out + 16ull * p) = x0;
+      *reinterpret_cast<uint4*>(out + 16ull * (p + 64)) = x1;
+      *reinterpret_cast<uint4*>(out + 16ull * (p + 128)) = x2;
+      *reinterpret_cast<uint4*>(out + 16ull * (p + 192)) = x3;
     }
     for (; p < pieces; p += 64)
       *reinterpret_cast<uint4*>(out + 16ull * p) = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * p) & mask));
@@ -378,12 +387,16 @@ __global__ __launch_bounds__(64 * kFF) void fetch_fused_kernel(FetchArgs a) {
   __shared__ u64 s_base;
   const DevState& st = a.st;
   const u32 w = threadIdx.x >> 6, lane = lane_id();
-  if (threadIdx.x == 0) {
-    const u32 t = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_id = t;
-    // the last workgroup to arrive resets the counter for the next fetch (every other one has
-    // taken its index; the kernel boundary orders the store before the next fetch's adds)
-    if (t == gridDim.x - 1u) __hip_atomic_store(a.lb_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (a.lb_ticket) {  // RMQ_FETCH_FUSED=2: indices in arrival order from a counter (one word: ~88 adds/us)
+    if (threadIdx.x == 0) {
+      const u32 t = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_id = t;
+      // the last workgroup to arrive resets the counter for the next fetch (every other one has
+      // taken its index; the kernel boundary orders the store before the next fetch's adds)
+      if (t == gridDim.x - 1u) __hip_atomic_store(a.lb_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else if (threadIdx.x == 0) {
+    s_id = blockIdx.x;  // dispatch order (workgroups start first to last: a predecessor is resident or done)
   }
   __syncthreads();
   const u32 id = __builtin_amdgcn_readfirstlane(s_id);

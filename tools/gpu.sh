@@ -79,6 +79,10 @@ for step in "$@"; do
       done ;;
     legs)  # the side legs (fetch, mixed, tier) on a short line, with the single-pass and the two-kernel fetch
       for f in 1 0; do RMQ_FETCH_FUSED=$f run 300 "${T}_legs_fused$f.json" python bench.py --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0; done ;;
+    fetchkt)  # kernel trace of the fetch leg alone, per fetch path (RMQ_FETCH_FUSED = 1, 2, 0)
+      for f in 1 2 0; do
+        RMQ_FETCH_FUSED=$f prof 200 fetchkt$f --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_fetchkt$f" -o kt -- python3 "$R/bench.py" --steps 20 --warmup 5 --fetch-rounds 10 --concurrent-rounds 0 --tier-rounds 0 --no-cpu-baseline --host-steps 0
+      done ;;
     fetchprof|fetchprof:*)  # kernel trace of the fetch legs (short append run), current library and variants/NAME
       V=${step#fetchprof}; V=${V#:}
       FQ="--steps 100 --warmup 10 --no-cpu-baseline --concurrent-rounds 0 --host-steps 0"
