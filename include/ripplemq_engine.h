@@ -369,8 +369,11 @@ int rmq_host_unregister(rmq_engine* e, void* p);
    kernels 0 and 1: the pipeline launches from the first one after enable up to the next drain
    (sync, control call, read-back) timed as ONE region (no events between launches): total_ms =
    region time; launches = pipeline launches in it (kernel 0) or batches they applied (kernel 1).
-   kernel 3: rmq_fetch, the summed durations of its two kernels (resolve, place + gather); 4:
-   rmq_fetch, first kernel start to last kernel end (host launch gaps included). 2: unused. */
+   kernel 3: rmq_fetch, the summed dispatch-recorded spans of its kernels; 4: rmq_fetch, an event
+   before its first kernel to one after its last (the request copy before and the result copy after
+   outside), launches = kernel executions. enable = k >= 2 also runs every fetch's kernels k times
+   back to back (idempotent: the same results), so kernel 4 / launches is a kernel time that no
+   copy or host gap inflates and a rocprofv3 trace shows the kernels back to back. 2: unused. */
 int rmq_profile_enable(rmq_engine* e, int enable);
 int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* total_ms);
 /* Device name / CU count for reports. */

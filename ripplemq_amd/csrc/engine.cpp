@@ -1433,23 +1433,33 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
     if (e->fetch_fused) {
-      if (++f.epoch == fetch_epoch_limit()) {  // the epochs wrap: no stale word may match again
-        HIP_TRY(hipMemsetAsync(f.d_lbv, 0, (fetch_fused_workgroups(f.cap) + 1) * 8ull, e->fetch_s));
-        f.epoch = 1;
-      }
-      a.epoch = f.epoch;
       a.lb_val = f.d_lbv;
       a.lb_ticket = e->fetch_fused == 2 ? e->d_lb_ticket : nullptr;
     }
     HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
-    hipEvent_t ev[4] = {};
-    if (e->profile) {  // kernel 3: the kernels' own durations; 4: first start to last end
+    hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
+    const uint32_t runs = e->profile ? e->fetch_replay : 1u;
+    if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run, copies outside
       for (hipEvent_t& x : ev) x = pool_event(e);
       for (int k = 0; k < 2; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
-      e->prof[4].push_back({ev[0], ev[3]});
+      r0 = pool_event(e);
+      r1 = pool_event(e);
+      e->prof[4].push_back({r0, r1});
+      e->prof_fetch_runs += runs;
+      HIP_TRY(hipEventRecord(r0, e->fetch_s));
     }
-    launch_fetch(a, e->fetch_s, e->profile ? ev : nullptr);
-    HIP_TRY(hipGetLastError());
+    for (uint32_t k = 0; k < runs; ++k) {
+      if (e->fetch_fused) {
+        if (++f.epoch == fetch_epoch_limit()) {  // the epochs wrap: no stale word may match again
+          HIP_TRY(hipMemsetAsync(f.d_lbv, 0, (fetch_fused_workgroups(f.cap) + 1) * 8ull, e->fetch_s));
+          f.epoch = 1;
+        }
+        a.epoch = f.epoch;  // a new epoch per run (a replay must not read the last run's words)
+      }
+      launch_fetch(a, e->fetch_s, e->profile && k == 0 ? ev : nullptr);
+      HIP_TRY(hipGetLastError());
+    }
+    if (e->profile) HIP_TRY(hipEventRecord(r1, e->fetch_s));
     HIP_TRY(hipMemcpyAsync(f.h_res, f.d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
     HIP_TRY(hipEventRecord(f.ev, e->fetch_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev, 0));
@@ -1671,7 +1681,8 @@ int rmq_profile_enable(rmq_engine* e, int enable) {
     v.clear();
   }
   e->profile = enable > 0 ? 1u : 0u;
-  e->prof_launches = e->prof_batches = 0;
+  e->fetch_replay = enable > 1 ? (uint32_t)enable : 1u;
+  e->prof_launches = e->prof_batches = e->prof_fetch_runs = 0;
   e->prof_started = e->prof_ended = false;
   if (e->profile && !e->prof_t0) {
     HIP_TRY(hipEventCreate(&e->prof_t0));
@@ -1699,7 +1710,7 @@ int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* tot
     HIP_TRY(hipEventElapsedTime(&ms, p.a, p.b));
     tot += ms;
   }
-  if (launches) *launches = e->prof[kernel].size();
+  if (launches) *launches = kernel == 4 ? e->prof_fetch_runs : e->prof[kernel].size();
   if (total_ms) *total_ms = tot;
   return RMQ_OK;
 }

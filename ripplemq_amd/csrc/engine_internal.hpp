@@ -375,6 +375,8 @@ struct rmq_engine {
   // enable, event at the next drain) so no per-launch events sit between kernels; fetch kernels
   // keep per-launch event pairs (prof[3], prof[4])
   uint32_t profile = 0;
+  uint32_t fetch_replay = 1;     // rmq_profile_enable(k >= 2): each fetch's kernels run k times
+  uint64_t prof_fetch_runs = 0;
   uint64_t prof_launches = 0, prof_batches = 0;
   hipEvent_t prof_t0 = nullptr, prof_t1 = nullptr;
   bool prof_started = false, prof_ended = false;

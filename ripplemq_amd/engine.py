@@ -421,7 +421,8 @@ class Engine:
     def d2h(self, dst: np.ndarray, src: int) -> None:
         _check(self.lib.rmq_memcpy(self.h, _ptr(dst), src, dst.nbytes, 1), "rmq_memcpy")
 
-    def profile(self, enable: bool) -> None:
+    def profile(self, enable: int) -> None:
+        """rmq_profile_enable: 0 off, 1 on, k >= 2 on with every fetch's kernels run k times."""
         _check(self.lib.rmq_profile_enable(self.h, int(enable)), "rmq_profile_enable")
 
     def profile_query(self, kernel: int) -> tuple[int, float]:
