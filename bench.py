@@ -460,7 +460,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                            "requests": P * consumers, "rounds": rounds,
                            "roofline": {"bound": "hbm", "achieved": alg / t_reg / 1e9, "peak": HBM_PEAK_GBS,
                                         "unit": "GB/s", "frac": alg / t_reg / 1e9 / HBM_PEAK_GBS,
-                                        "kernels": "rmq::fetch_fused_kernel (resolve, look-back placement, gather)" if os.environ.get("RMQ_FETCH_FUSED", "1") != "0" else "rmq::fetch_resolve + fetch_gather",
+                                        "kernels": "rmq::fetch_resolve (two requests per wave) + fetch_gather (placement fused)",
                                         "mean_us_per_fetch": t_reg / rounds * 1e6,
                                         "timing": f"per fetch: its kernels run {REPLAY}x back to back between two "
                                                   "HIP events on the fetch stream, divided by the runs",

@@ -268,6 +268,19 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
 // One launch: ranks the group being formed (if any) and advances the groups ahead of it.
 int close_group(rmq_engine* e) {
   const GroupFlight* s1 = e->forming.nb ? &e->forming : nullptr;
+  // bounded run-ahead (RMQ_AHEAD launches queued at most, no transport): a fetch or an offset
+  // commit is ordered after the launches issued before it, so an unbounded queue would make its
+  // latency grow with how far the host runs ahead (device batches are never waited for otherwise).
+  // Launch L's first lane reports L - 1 complete (done word).
+  if (e->max_ahead && !e->repl) {
+    const uint64_t need = e->launch_seq + 1 > e->max_ahead ? e->launch_seq + 1 - e->max_ahead : 0;
+    while (need > __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE)) {
+      const hipError_t q = hipStreamQuery(e->main_s);
+      if (q == hipSuccess) break;
+      if (q != hipErrorNotReady) return hip_fail(q);
+      std::this_thread::yield();
+    }
+  }
   int rc = launch_stages(e, s1, e->has1 ? &e->g1 : nullptr, e->has2 ? &e->g2 : nullptr,
                          e->has3 ? &e->g3 : nullptr);
   if (rc) return rc;
@@ -452,9 +465,9 @@ void free_engine(rmq_engine* e) {
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
                              s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq, e->d_crc,
-                             e->d_stats, e->d_lb_ticket, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
+                             e->d_stats, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (rmq_engine::FetchSlot& f : e->fslot) {
-    void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv, f.d_out};
+    void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_out};
     for (void* p : fs) bufs.push_back(p);
     if (f.h_req) hipHostFree(f.h_req);
     if (f.h_res) hipHostFree(f.h_res);
@@ -605,6 +618,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK")) e->rank_mode = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STEAL")) e->steal = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_AHEAD")) e->max_ahead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
 #define CREATE_TRY(x)      \
   do {                     \
@@ -632,9 +646,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
   }
-  if (const char* v = std::getenv("RMQ_FETCH_FUSED")) e->fetch_fused = (uint32_t)std::atoi(v);
-  CREATE_TRY(dalloc(&e->d_lb_ticket, 4));
-  CREATE_HIP(hipMemset(e->d_lb_ticket, 0, 4));
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
   DevState& s = e->st;
@@ -1286,34 +1297,30 @@ namespace {
 
 // Scratch of a fetch slot for n requests and, for a host output, out_cap bytes of device staging.
 // Plain hipMalloc (no zeroing, no device synchronisation: a slot first used while the pipeline
-// runs must not wait for it); the look-back words are zeroed on the fetch stream.
+// runs must not wait for it; every word a fetch reads is written by it first).
 int fetch_alloc(void** p, size_t bytes) {
   *p = nullptr;
   HIP_TRY(hipMalloc(p, std::max<size_t>(bytes, 16)));
   return RMQ_OK;
 }
 
-int fetch_slot_reserve(rmq_engine* e, rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
+int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
   if (n > f.cap) {
-    void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_lbv};
+    void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum};
     for (void* p : ds)
       if (p) hipFree(p);
     if (f.h_req) hipHostFree(f.h_req);
     if (f.h_res) hipHostFree(f.h_res);
     f.d_req = f.d_cpre = f.h_req = nullptr;
-    f.d_res = f.d_aux = f.d_csum = f.d_lbv = f.h_res = nullptr;
+    f.d_res = f.d_aux = f.d_csum = f.h_res = nullptr;
     f.cap = 0;
     const uint32_t cap = std::max<uint32_t>(n, 1024);
-    const size_t wgs = fetch_fused_workgroups(cap) + 1;
     int rc = fetch_alloc((void**)&f.d_req, (size_t)cap * 16);
     if (!rc) rc = fetch_alloc((void**)&f.d_res, ((size_t)cap * 4 + 2) * 8);
     if (!rc) rc = fetch_alloc((void**)&f.d_aux, (size_t)cap * 16);
     if (!rc) rc = fetch_alloc((void**)&f.d_cpre, ((size_t)cap + 4) * 4);
     if (!rc) rc = fetch_alloc((void**)&f.d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride * 8);
-    if (!rc) rc = fetch_alloc((void**)&f.d_lbv, wgs * 8);
     if (rc) return rc;
-    HIP_TRY(hipMemsetAsync(f.d_lbv, 0, wgs * 8, e->fetch_s));  // epoch 0 is never a fetch's
-    f.epoch = 0;
     HIP_TRY(hipHostMalloc((void**)&f.h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&f.h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
     f.cap = cap;
@@ -1411,7 +1418,7 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     *ticket = tk;
     return RMQ_OK;
   }
-  int rc = fetch_slot_reserve(e, f, n, mem == RMQ_MEM_HOST ? out_cap : 0);
+  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0);
   if (rc) return rc;
   uint8_t* d_out = mem == RMQ_MEM_HOST ? (out_cap ? f.d_out : nullptr) : out;
   std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
@@ -1432,10 +1439,6 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     a.n = n;
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
-    if (e->fetch_fused) {
-      a.lb_val = f.d_lbv;
-      a.lb_ticket = e->fetch_fused == 2 ? e->d_lb_ticket : nullptr;
-    }
     HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     const uint32_t runs = e->profile ? e->fetch_replay : 1u;
@@ -1449,13 +1452,6 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
       HIP_TRY(hipEventRecord(r0, e->fetch_s));
     }
     for (uint32_t k = 0; k < runs; ++k) {
-      if (e->fetch_fused) {
-        if (++f.epoch == fetch_epoch_limit()) {  // the epochs wrap: no stale word may match again
-          HIP_TRY(hipMemsetAsync(f.d_lbv, 0, (fetch_fused_workgroups(f.cap) + 1) * 8ull, e->fetch_s));
-          f.epoch = 1;
-        }
-        a.epoch = f.epoch;  // a new epoch per run (a replay must not read the last run's words)
-      }
       launch_fetch(a, e->fetch_s, e->profile && k == 0 ? ev : nullptr);
       HIP_TRY(hipGetLastError());
     }

@@ -275,6 +275,7 @@ struct rmq_engine {
   uint32_t key_bits = 0;
   uint32_t rank_mode = 0;  // RMQ_RANK: stage 1 by the LDS radix sort (0) or by hash counters (1;
                            // 4.86 vs 5.14 G msgs/s at config B, profiles/r04c_*)
+  uint32_t max_ahead = 4;  // RMQ_AHEAD: pipeline launches queued at most (0: unbounded)
   uint32_t steal = 0;      // RMQ_STEAL=1: stage-3 workgroups take stage-1 tiles when out of tasks
                            // (5.20 -> 4.00 G msgs/s: stage 2 and the second half of stage 3 start later)
   PipeScratch scratch[kSets]{};
@@ -321,8 +322,6 @@ struct rmq_engine {
     uint64_t* d_aux = nullptr;
     uint32_t* d_cpre = nullptr;
     uint64_t* d_csum = nullptr;
-    uint64_t* d_lbv = nullptr;   // single pass: look-back words per workgroup
-    uint32_t epoch = 0;          //   and the slot's fetch number (wraps to 1 after a clear)
     uint32_t* h_req = nullptr;   // pinned
     uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}
     uint32_t cap = 0;
@@ -344,9 +343,6 @@ struct rmq_engine {
   uint32_t fslot_next = 0;
   uint64_t fetch_seq = 0;        // tickets
   std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
-  uint32_t* d_lb_ticket = nullptr;
-  uint32_t fetch_fused = 1;      // RMQ_FETCH_FUSED: 1 single pass (dispatch-order look-back), 2 the
-                                 // same with arrival-order indices, 0 resolve + gather kernels
   // consumer-offset commits: two staging slots (pinned items -> device by one copy on the pipeline
   // stream), so a commit is ordered with the append stream without waiting for it
   struct CommitSlot {

@@ -2,12 +2,13 @@
 // (mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:85-110), served directly from
 // committed state like MessageBatchReadRequestProcessor.java:39 (no read-index).
 //
-//  resolve (wave per request): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
-//          byte range of records [off, end): both ends found together, a half-wave each, by a
-//          32-ary search of the sparse offset index (FORMAT.md §5: E[m] = first record starting at
-//          or after m*I; 32 probes per round, one round per factor 32 of index entries), then the
-//          record headers of the 1 KiB after the entry found are loaded at once (two 16-byte pieces
-//          per lane of the half) and walked in registers;
+//  resolve (half-wave per request, two per wave: 16,384 requests fit the chip's resident waves in
+//          one round): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
+//          byte range of records [off, end): both ends found together, a quarter-wave each, by a
+//          16-ary search of the sparse offset index (FORMAT.md §5: E[m] = first record starting at
+//          or after m*I; 16 probes per round, one round per factor 16 of index entries), then the
+//          record headers of the 512 B after the entry found are loaded at once (two 16-byte pieces
+//          per lane of the quarter) and walked in registers;
 //          each workgroup adds its requests' bytes to the sum of their chunk of 256 requests;
 //  gather  (workgroup per 16 requests, a wave per 4): the output position of its first request from
 //          the chunk sums before it and the byte counts of its chunk before it (at most 64 + 255
@@ -39,45 +40,52 @@ struct PartView {
   const uint8_t* ring;  // lowest local replica ring of the partition
 };
 
-// Logical byte positions of records t0 (lanes 0..31) and t1 (lanes 32..63), start_off <= t <= leo,
-// found together (wave-uniform arguments; the half-wave of each record returns its position).
-__device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const PartView& v, u64 t0, u64 t1) {
-  const u32 lane = lane_id(), h = lane >> 5, hl = lane & 31u;
-  const u64 t = h ? t1 : t0;
+// A wave resolves two requests (lanes 0..31 and 32..63), and each request's two ends are found
+// together by a quarter-wave each: kQL lanes per searched position.
+constexpr u32 kQL = 16;
+constexpr u32 kRPW = 2;  // requests per resolve wave
+
+// Logical byte position of record t (start_off <= t <= leo) in the lane's view, found by the kQL
+// lanes of its quarter (t, v, act quarter-uniform; an inactive quarter loads nothing and gets 0).
+// The largest index entry at or before t: E[m] = first record starting at or after m I rises with
+// m, so a kQL-ary search over the live entries (round 0 probes the kQL entries around the
+// interpolated position of t: records of one size give it exactly), then the record headers after
+// that entry, read as windows of 2 kQL 16-byte pieces (two per lane) and walked in registers; the
+// window the interpolation puts t in is loaded with the first probe round and used when the entry
+// found lies inside it.
+__device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v, u64 t, bool act) {
+  const u32 lane = lane_id(), h = lane / kQL, hl = lane % kQL;
+  constexpr u32 kWin = 2 * kQL;  // pieces per header window
   const u32 ilog = st.interval_log2;
   const u64 I = 1ull << ilog;
   const u64* E = st.index + v.rg.ibase * 2;
-  // per half: largest m in [lo, hi] with E[m].offset <= t (E rises with m); none: the log start.
-  // Round 0 probes the 32 entries around the interpolated position of t (records of one size:
-  // exact); a miss narrows [lo, hi] and the search goes on 32-ary, 32 probes per round.
   u64 c_off = v.start_off, c_pos = v.start_pos;
   long lo = (long)((v.start_pos + I - 1) >> ilog), hi = (long)(v.used >> ilog);
-  bool open = t < v.leo && lo <= hi;
+  bool open = act && t < v.leo && lo <= hi;
   long ws = lo, step = 1;
   const u64 mask = v.rg.seg - 1;
-  u64 sw = ~0ull;  // speculative header window: the interval the interpolation puts t in
+  u64 sw = ~0ull;  // speculative header window
   if (open) {
     const double f = (double)(t - v.start_off) / (double)(v.leo - v.start_off);
     const u64 gpos = v.start_pos + (u64)(f * (double)(v.used - v.start_pos));
     const long me = (long)(gpos >> ilog);
-    ws = max(lo, min(me - 15, hi - 31));
+    ws = max(lo, min(me - (long)(kQL / 2 - 1), hi - (long)(kQL - 1)));
     sw = max((u64)me << ilog, v.start_pos) & ~15ull;
-  } else if (t < v.leo) {
+  } else if (act && t < v.leo) {
     sw = v.start_pos;  // no index entry past the start: the walk starts at the log start
   }
-  // loaded with the first probe round; used if the entry found lies inside it (records of one
-  // size: always), so the walk below needs no load of its own
   u32 Sw0 = 0, Sw1 = 0;
   if (sw != ~0ull) {
     Sw0 = *reinterpret_cast<const u32*>(v.ring + ((sw + 32ull * hl + 8ull) & mask));
     Sw1 = *reinterpret_cast<const u32*>(v.ring + ((sw + 32ull * hl + 24ull) & mask));
   }
+  constexpr u32 kQMask = (1u << kQL) - 1u;
   for (bool first = true; __any(open); first = false) {
     if (!first) {
       ws = lo;
-      step = (hi - lo + 32) / 32;
+      step = (hi - lo + (long)kQL) / (long)kQL;
     }
-    const long we = min(hi, ws + 31 * step);  // last probe of the round
+    const long we = min(hi, ws + (long)(kQL - 1) * step);  // last probe of the round
     const long m = ws + (long)hl * step;
     bool le = false;
     u64 eo = 0, ep = 0;
@@ -87,9 +95,9 @@ __device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const Part
       ep = e[1];
       le = eo <= t;
     }
-    const u32 bal = (u32)(__ballot(le) >> (32u * h));  // this half's probes
+    const u32 bal = (u32)(__ballot(le) >> (kQL * h)) & kQMask;  // this quarter's probes
     const u32 last = bal ? 31u - (u32)__builtin_clz(bal) : 0u;
-    const u64 so = __shfl(eo, (int)(32u * h + last), 64), sp = __shfl(ep, (int)(32u * h + last), 64);
+    const u64 so = __shfl(eo, (int)(kQL * h + last), 64), sp = __shfl(ep, (int)(kQL * h + last), 64);
     if (open) {
       if (!bal) {  // every probe past t: the answer precedes this round's first probe
         hi = ws - 1;
@@ -108,14 +116,12 @@ __device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const Part
       }
     }
   }
+  if (!act) return 0;
   if (t >= v.leo) return v.used;
-  // walk the headers of the records in [c_off, t): they start within one index interval after
-  // c_pos, read as 1 KiB windows of 16-byte pieces (two pieces per lane of the half; one window
-  // when I <= 1 KiB), the first the speculative one when it holds c_pos
   u64 wb = sw;
   u32 Lw0 = Sw0, Lw1 = Sw1;
   u32 cur = (u32)((c_pos - sw) >> 4);  // window piece of the current record
-  if (sw == ~0ull || c_pos < sw || c_pos >= sw + 1024ull) {
+  if (sw == ~0ull || c_pos < sw || c_pos >= sw + 16ull * kWin) {
     wb = c_pos;
     cur = 0;
     Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
@@ -123,7 +129,7 @@ __device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const Part
   }
   u64 k = t - c_off;
   while (__any(k > 0)) {
-    const bool mv = k > 0 && cur >= 64u;  // half-uniform: the half walked off its window
+    const bool mv = k > 0 && cur >= kWin;  // quarter-uniform: the quarter walked off its window
     if (__any(mv)) {
       if (mv) {
         wb += 16ull * cur;
@@ -132,7 +138,7 @@ __device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const Part
         Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
       }
     }
-    const u32 src = 32u * h + (cur >> 1);
+    const u32 src = kQL * h + (cur >> 1);
     const u32 a0 = (u32)__shfl((int)Lw0, (int)(src & 63u), 64), a1 = (u32)__shfl((int)Lw1, (int)(src & 63u), 64);
     if (k > 0) {
       cur += record_bytes((cur & 1u) ? a1 : a0) >> 4;
@@ -142,8 +148,8 @@ __device__ __forceinline__ u64 record_pos2(const DevState& st, u32 p, const Part
   return wb + 16ull * cur;
 }
 
-// One request, resolved by one wave (wave-uniform results): status, start offset, count, bytes, the
-// source position and the ring word {ring byte offset in logs << 6 | log2(ring bytes)}.
+// Request r, resolved by one half-wave (half-uniform results): status, start offset, count,
+// bytes, the source position and the ring word {ring byte offset in logs << 6 | log2(ring bytes)}.
 struct Resolved {
   u64 start, count, bytes, pos0, ring;
   int status;
@@ -153,7 +159,7 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
   const DevState& st = a.st;
   const u32 p = live ? a.req[4 * r] : 0u, c = live ? a.req[4 * r + 1] : 0u, mx = live ? a.req[4 * r + 2] : 0u;
   int status = kOk;
-  u64 start = 0, count = 0, bytes = 0, pos0 = 0, ring_off = 0;
+  u64 start = 0, count = 0, end = 0, ring_off = 0;
   // every word of the partition in one round, the leader flag included (a request refused by the
   // checks below, or with an empty slice, leaves them unused)
   const bool okp = live && p < st.P;
@@ -168,6 +174,9 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
   v.start_pos = okp ? st.start_pos[pp] : 0ull;
   const u32 lm = okp ? st.local_mask[pp] : 0u;
   const u64 desc = okp ? st.ring[pp] : 0ull;
+  v.rg = ring_ref(desc, st.interval_log2, st.icap_mul);
+  v.ring = st.logs;
+  bool need = false;  // the slice is not empty: both its ends are searched
   if (!live) {
   } else if (p >= st.P) {
     status = kNoPart;
@@ -179,47 +188,50 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
     start = off;
     u64 lim = off + mx;
     if (lim < off) lim = ~0ull;
-    const u64 end = lim < hw ? lim : hw;
+    end = lim < hw ? lim : hw;
     if (off < end) {
       if (off < v.start_off) {
         status = kOffset;
         start = v.start_off;  // where the consumer can resume (FORMAT.md §7)
       } else {
         const u32 r0 = lm ? (u32)__ffs(lm) - 1u : 0u;
-        v.rg = ring_ref(desc, st.interval_log2, st.icap_mul);
         ring_off = (u64)r0 * st.rstride + v.rg.base;
         v.ring = st.logs + ring_off;
-        const u64 pp = record_pos2(st, p, v, off, end);
-        pos0 = bcast_u64(pp, 0);
-        bytes = bcast_u64(pp, 32) - pos0;
         count = end - off;
+        need = true;
       }
     }
   }
-  return Resolved{start, count, bytes, pos0, (ring_off << 6) | (desc & 63ull), status};
+  // quarter 0 of the half: the slice's first record, quarter 1: one past its last
+  const u32 hb = lane_id() & 32u;
+  const u64 pq = record_posq(st, v, (lane_id() & 16u) ? end : off, need);
+  const u64 pos0 = __shfl(pq, (int)hb, 64), pend = __shfl(pq, (int)(hb + 16u), 64);
+  return Resolved{start, count, need ? pend - pos0 : 0ull, pos0, (ring_off << 6) | (desc & 63ull), status};
 }
 
 __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
-  const u32 r = __builtin_amdgcn_readfirstlane(blockIdx.x * kFW + (threadIdx.x >> 6));
+  const u32 lane = lane_id(), w = threadIdx.x >> 6;
+  const u32 r = (blockIdx.x * kFW + w) * kRPW + (lane >> 5);
   const bool live = r < a.n;  // (no early return: the workgroup meets at a barrier below)
   const Resolved q = resolve_request(a, r, live);
-  const u64 bytes = q.bytes;
   __shared__ u64 s_b[kFW];
-  if (lane_id() == 0) s_b[threadIdx.x >> 6] = bytes;
-  if (live && lane_id() == 0) {
+  const u64 b2 = bcast_u64(q.bytes, 0) + bcast_u64(q.bytes, 32);  // the wave's two requests
+  if (lane == 0) s_b[w] = b2;
+  if (live && (lane & 31u) == 0) {
     a.res[4 * r + 0] = q.start;
-    a.res[4 * r + 2] = q.count | (bytes << 32);
+    a.res[4 * r + 2] = q.count | (q.bytes << 32);
     a.res[4 * r + 3] = (u64)(uint32_t)q.status;
     a.aux[2 * r + 0] = q.pos0;
     a.aux[2 * r + 1] = q.ring;
-    a.cpre[r] = (u32)bytes;
+    a.cpre[r] = (u32)q.bytes;
   }
-  // one add per workgroup (its kFW requests share a chunk) into the chunk's own L2 line
+  // one add per workgroup (its kFW * kRPW requests share a chunk) into the chunk's own L2 line
+  static_assert(kFetchChunk % (kFW * kRPW) == 0, "a resolve workgroup never straddles a chunk");
   __syncthreads();
   if (threadIdx.x == 0) {
     u64 b = 0;
     for (u32 k = 0; k < kFW; ++k) b += s_b[k];
-    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kFW / kFetchChunk) * kCsumStride], (unsigned long long)b);
+    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kFW * kRPW / kFetchChunk) * kCsumStride], (unsigned long long)b);
   }
 }
 
@@ -332,133 +344,6 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   }
 }
 
-// ---- single-pass fetch: resolve, placement and gather in one kernel -----------------------------
-// Workgroup per kFF consecutive requests, wave per request: the wave resolves its request, the
-// workgroup's byte total is published and the bytes of every earlier request are found by
-// decoupled look-back over the earlier workgroups' published totals (a wave reads 64 predecessors
-// per step; a predecessor publishes its aggregate at once and its inclusive prefix when it knows
-// it), then every wave copies its own request. Workgroups take their index from a counter in
-// arrival order (a workgroup only waits on ones that started before it; the last to arrive resets
-// it), and the published words carry the fetch's epoch, so nothing is cleared between fetches.
-constexpr u32 kFF = 8;  // requests (waves) per single-pass workgroup
-constexpr u32 kLbAgg = 1u, kLbPre = 2u;
-// A published word is one 8-byte granule {bytes << 16 | epoch << 2 | state}, stored and polled with
-// relaxed agent-scope (sc1, L2-coherent) accesses: a granule is written whole, so no fence orders
-// its parts (MI355X_MICROARCH.md, inter-workgroup visibility, R2).
-constexpr u32 kLbEpochBits = 14;
-
-__device__ __forceinline__ void lb_publish(const FetchArgs& a, u32 id, u64 v, u32 state) {
-  store_sc1(a.lb_val + id, (v << 16) | ((u64)a.epoch << 2) | state);
-}
-
-// bytes of every request before workgroup id's first (wave-uniform; the calling wave only)
-__device__ __forceinline__ u64 lb_exclusive(const FetchArgs& a, u32 id) {
-  const u32 lane = lane_id();
-  u64 excl = 0;
-  long j = (long)id - 1 - (long)lane;  // the predecessor this lane reads
-  while (true) {
-    const bool valid = j >= 0;
-    u64 g = 0;
-    u32 state = 0;
-    while (true) {
-      if (valid) {
-        g = load_sc1(a.lb_val + j);
-        state = ((u32)(g >> 2) & ((1u << kLbEpochBits) - 1u)) == a.epoch ? (u32)(g & 3u) : 0u;
-      }
-      if (!__any(valid && state == 0u)) break;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    const u64 v = valid ? (g >> 16) : 0ull;
-    const u64 pm = __ballot(valid && state == kLbPre);
-    if (pm) {  // the nearest predecessor with its prefix ends the look-back
-      const u32 k = (u32)__builtin_ctzll(pm);
-      excl += bcast_u64(wave_incl_scan<u64>(lane <= k ? v : (u64)0), 63);
-      return excl;
-    }
-    excl += bcast_u64(wave_incl_scan<u64>(v), 63);
-    j -= 64;
-    if (!__any(j >= 0)) return excl;  // (workgroup 0 publishes its prefix: not reached)
-  }
-}
-
-__global__ __launch_bounds__(64 * kFF) void fetch_fused_kernel(FetchArgs a) {
-  __shared__ u32 s_id;
-  __shared__ u64 s_nb[kFF];
-  __shared__ u64 s_base;
-  const DevState& st = a.st;
-  const u32 w = threadIdx.x >> 6, lane = lane_id();
-  if (a.lb_ticket) {  // RMQ_FETCH_FUSED=2: indices in arrival order from a counter (one word: ~88 adds/us)
-    if (threadIdx.x == 0) {
-      const u32 t = __hip_atomic_fetch_add(a.lb_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_id = t;
-      // the last workgroup to arrive resets the counter for the next fetch (every other one has
-      // taken its index; the kernel boundary orders the store before the next fetch's adds)
-      if (t == gridDim.x - 1u) __hip_atomic_store(a.lb_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  } else if (threadIdx.x == 0) {
-    s_id = blockIdx.x;  // dispatch order (workgroups start first to last: a predecessor is resident or done)
-  }
-  __syncthreads();
-  const u32 id = __builtin_amdgcn_readfirstlane(s_id);
-  const u32 r = id * kFF + w;
-  const bool live = r < a.n;
-  const Resolved q = resolve_request(a, r, live);
-  if (lane == 0) s_nb[w] = live ? q.bytes : 0ull;
-  __syncthreads();
-  if (w == 0) {
-    const u64 agg = bcast_u64(wave_incl_scan<u64>(lane < kFF ? s_nb[lane] : (u64)0), 63);
-    u64 excl = 0;
-    if (id == 0) {
-      if (lane == 0) lb_publish(a, 0, agg, kLbPre);
-    } else {
-      if (lane == 0) lb_publish(a, id, agg, kLbAgg);
-      excl = lb_exclusive(a, id);
-      if (lane == 0) lb_publish(a, id, excl + agg, kLbPre);
-    }
-    if (lane == 0) s_base = excl;
-  }
-  __syncthreads();
-  if (!live) return;
-  u64 pos = s_base;
-  for (u32 k = 0; k < w; ++k) pos += s_nb[k];
-  const u64 nb = q.bytes;
-  const bool served = nb && pos + nb <= a.out_cap;
-  if (lane == 0) {
-    a.res[4 * r + 0] = q.start;
-    a.res[4 * r + 1] = pos;
-    a.res[4 * r + 2] = (nb && !served) ? 0ull : (q.count | (nb << 32));
-    a.res[4 * r + 3] = (u64)(uint32_t)((nb && !served) ? kNoSpc : q.status);  // does not fit: its bytes still count
-    if (r + 1 == a.n) a.res[4ull * a.n] = pos + nb;  // bytes needed
-  }
-  if (!served) return;
-  const uint8_t* ring = st.logs + (q.ring >> 6);
-  const u64 mask = (1ull << (q.ring & 63ull)) - 1ull;
-  uint8_t* out = a.out + pos;
-  const u64 pieces = nb >> 4;
-  // four 16-byte pieces in flight per lane (named registers: a local array here went to scratch)
-  auto ld = [&](u64 i) { return *reinterpret_cast<const uint4*>(ring + ((q.pos0 + 16ull * i) & mask)); };
-  auto st16 = [&](u64 i, uint4 v) { *reinterpret_cast<uint4*>(out + 16ull * i) = v; };
-  u64 k = lane;
-  for (; k + 192 < pieces; k += 256) {
-    const uint4 x0 = ld(k), x1 = ld(k + 64), x2 = ld(k + 128), x3 = ld(k + 192);
-    st16(k, x0);
-    st16(k + 64, x1);
-    st16(k + 128, x2);
-    st16(k + 192, x3);
-  }
-  const bool b0 = k < pieces, b1 = k + 64 < pieces, b2 = k + 128 < pieces;
-  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0, x2 = x0;
-  if (b0) x0 = ld(k);
-  if (b1) x1 = ld(k + 64);
-  if (b2) x2 = ld(k + 128);
-  if (b0) st16(k, x0);
-  if (b1) st16(k + 64, x1);
-  if (b2) st16(k + 128, x2);
-}
-
-uint32_t fetch_fused_workgroups(uint32_t n) { return (n + kFF - 1) / kFF; }
-uint32_t fetch_epoch_limit() { return 1u << kLbEpochBits; }
-
 // ev[4]: start / end events of the two kernels, recorded by the dispatches themselves
 // (profiling: kernel time without the host's launch gaps), or null
 // Load the fetch kernels' code at engine creation (a process's first launch of a kernel otherwise
@@ -467,23 +352,13 @@ void preload_fetch_kernels() {
   hipFuncAttributes fa;
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_resolve_kernel));
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel));
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_fused_kernel));
 }
 
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
-  if (a.lb_val) {  // single pass (ev: its start and end twice, so the profile's slots line up)
-    hipExtLaunchKernelGGL(fetch_fused_kernel, dim3(fetch_fused_workgroups(a.n)), dim3(64 * kFF), 0, s,
-                          e ? e[0] : nullptr, e ? e[1] : nullptr, 0, a);
-    if (e) {
-      (void)hipEventRecord(e[2], s);
-      (void)hipEventRecord(e[3], s);
-    }
-    return;
-  }
   (void)hipMemsetAsync(a.csum, 0, 8ull * kCsumStride * (a.n / kFetchChunk + 1), s);
-  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW - 1) / kFW), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
+  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW * kRPW - 1) / (kFW * kRPW)), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);
   hipExtLaunchKernelGGL(fetch_gather_kernel, dim3((a.n + kGR - 1) / kGR), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
                         e ? e[3] : nullptr, 0, a);

@@ -279,10 +279,7 @@ struct FetchArgs {
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
   uint32_t n;
-  uint32_t epoch;            // single pass: the slot's fetch number, 1 .. fetch_epoch_limit() - 1
-  uint64_t* lb_val;          // single pass: [workgroups] {bytes << 16 | epoch << 2 | 1: aggregate,
-                             //   2: inclusive prefix}, or null (two kernels)
-  uint32_t* lb_ticket;       //   workgroup arrival counter (zero between fetches)
+  uint32_t pad;
 };
 constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
 constexpr uint32_t kCsumStride = 16;   // u64 words per chunk sum (128 bytes)
@@ -378,8 +375,7 @@ void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
 void preload_fetch_kernels();
-uint32_t fetch_fused_workgroups(uint32_t n);
-uint32_t fetch_epoch_limit();
+
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_row_quorum_all(const DevState& st, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);

@@ -4,9 +4,9 @@ An asynchronous fetch is ordered exactly like rmq_fetch (after every launch issu
 before the ones issued after it), so its result must equal a synchronous fetch issued right after
 it (whose parity with the oracle test_gpu_pinned.py checks; PartitionStateMachine.java:85-110;
 MessageBatchReadRequestProcessor.java:36-42 answers each read from its own closure: the ticket is
-that completion). The single-pass kernel (resolve, placement by
-decoupled look-back, gather) and the two-kernel path must give the oracle's results on the same
-requests, ENOSPC cuts and bad requests included.
+that completion). The fetch kernels (a resolve of two requests per wave,
+a gather with placement) must give the oracle's results on the same requests, ENOSPC cuts and
+bad requests included.
 """
 from __future__ import annotations
 
@@ -21,9 +21,7 @@ from ripplemq_amd.workload import StreamSpec, make_batch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_async_fetch_matches_sync_while_appending(oracle_mod, monkeypatch, fused):
-    monkeypatch.setenv("RMQ_FETCH_FUSED", fused)
+def test_async_fetch_matches_sync_while_appending():
     P = 64
     cfg = EngineConfig(num_partitions=P, replication_factor=3, segment_bytes=1 << 18, index_interval=256,
                        max_consumers=2, max_batch_records=4096, pipeline_depth=2)
@@ -84,11 +82,12 @@ def test_async_fetch_empty_and_unknown():
             dev.fetch_poll(tk)
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
-def test_fetch_paths_agree_with_oracle(oracle_mod, monkeypatch, fused):
-    """20k requests (several thousand look-back workgroups), unknown partitions, bad consumers,
-    zero-record slices, an output that ends mid-way and records of 1..4000 bytes."""
-    monkeypatch.setenv("RMQ_FETCH_FUSED", fused)
+@pytest.mark.parametrize("replay", [1, 3])
+def test_fetch_agrees_with_oracle(oracle_mod, replay):
+    """20k requests (two per resolve wave, odd counts too), unknown partitions, bad consumers,
+    zero-record slices, an output that ends mid-way and records of 1..4000 bytes; with the
+    profiling replay (rmq_profile_enable(3): every fetch's kernels run three times) the results
+    are the same."""
     P, C = 512, 4
     cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 21, index_interval=512,
                        max_consumers=C, max_batch_records=65536)
@@ -96,6 +95,7 @@ def test_fetch_paths_agree_with_oracle(oracle_mod, monkeypatch, fused):
     g = np.random.default_rng(9)
     n = 20000
     with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        dev.profile(replay if replay > 1 else 0)
         ops = [("append", make_batch(spec, b)) for b in range(2)]
         p = g.integers(0, P + 8, n)
         c = g.integers(0, C + 1, n)
@@ -106,5 +106,6 @@ def test_fetch_paths_agree_with_oracle(oracle_mod, monkeypatch, fused):
         ops.append(("fetch", p, c, mx))
         ops.append(("fetch", p, c, mx, 3 << 20))
         ops.append(("fetch", p[:7], c[:7], mx[:7]))
+        ops.append(("fetch", p[:1], c[:1], mx[:1]))
         ops.append(("fetch", p, c, np.full(n, 1024)))
         run_ops(dev, ora, cfg, ops, check=False)

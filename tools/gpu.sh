@@ -17,7 +17,8 @@
 #   prof       rocprofv3 --kernel-trace --stats of the default line (kernel stats CSV)
 #   pmc        rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) of a 300-step line
 #   stamps     per-wave phase stamps of launch 100 (RMQ_STAMPS) + timing-only RMQ_DEBUG lines
-#   legs       fetch / mixed / tier legs of a short line, single-pass and two-kernel fetch
+#   legs       fetch / mixed / tier legs of a short line
+#   fetchkt    rocprofv3 kernel trace of the fetch leg (replayed kernels)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -77,12 +78,10 @@ for step in "$@"; do
         env "$var=$val" timeout -k 10 200 python bench.py --steps 600 --warmup 60 $Q > "gpurun_out/${T}_${var}_${val}_600.json" 2>&1 || exit 1
         env "$var=$val" timeout -k 10 200 python bench.py --steps 20 --warmup 5 $Q > "gpurun_out/${T}_${var}_${val}_20.json" 2>&1 || exit 1
       done ;;
-    legs)  # the side legs (fetch, mixed, tier) on a short line, with the single-pass and the two-kernel fetch
-      for f in 1 0; do RMQ_FETCH_FUSED=$f run 300 "${T}_legs_fused$f.json" python bench.py --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0; done ;;
-    fetchkt)  # kernel trace of the fetch leg alone, per fetch path (RMQ_FETCH_FUSED = 1, 2, 0)
-      for f in 1 2 0; do
-        RMQ_FETCH_FUSED=$f prof 200 fetchkt$f --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_fetchkt$f" -o kt -- python3 "$R/bench.py" --steps 20 --warmup 5 --fetch-rounds 10 --concurrent-rounds 0 --tier-rounds 0 --no-cpu-baseline --host-steps 0
-      done ;;
+    legs)  # the side legs (fetch, mixed, tier) on a short line
+      run 300 "${T}_legs.json" python bench.py --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0 ;;
+    fetchkt)  # kernel trace of the fetch leg alone (its kernels replayed back to back, bench.py REPLAY)
+      prof 200 fetchkt --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_fetchkt" -o kt -- python3 "$R/bench.py" --steps 20 --warmup 5 --fetch-rounds 10 --concurrent-rounds 0 --tier-rounds 0 --no-cpu-baseline --host-steps 0 ;;
     fetchprof|fetchprof:*)  # kernel trace of the fetch legs (short append run), current library and variants/NAME
       V=${step#fetchprof}; V=${V#:}
       FQ="--steps 100 --warmup 10 --no-cpu-baseline --concurrent-rounds 0 --host-steps 0"
