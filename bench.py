@@ -43,7 +43,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
-from ripplemq_amd.engine import Engine, EngineConfig, rccl_unique_id  # noqa: E402
+from ripplemq_amd.engine import FETCH_RES_DTYPE, Engine, EngineConfig, rccl_unique_id  # noqa: E402
 from ripplemq_amd.sharding import max_over_ranks, rank_view  # noqa: E402
 from ripplemq_amd.rings import partition_traffic, pool_layout, ring_sizes  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
@@ -265,7 +265,13 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     half = [cc < consumers // 2, cc >= consumers // 2]
     hp = [pp[m] for m in half]
     hc = [cc[m] for m in half]
-    hmax = [np.full(int(m.sum()), mx, np.uint32) for m in half]
+    # each half's request and result arrays, reused by every fetch of that half
+    hreq = []
+    for m in half:
+        r = np.zeros((int(m.sum()), 4), np.uint32)
+        r[:, 0], r[:, 1], r[:, 2] = pp[m], cc[m], mx
+        hreq.append(r)
+    hres = [np.zeros(len(r), FETCH_RES_DTYPE) for r in hreq]
     hi = spec.size if isinstance(spec.size, int) else spec.size[1]
     cap = P * consumers * mx * (16 + (hi + 15) // 16 * 16) + 4096
     d_out = eng.device_alloc(cap)
@@ -287,7 +293,7 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
 
     t0 = time.perf_counter()
     h = 0
-    tk = eng.fetch_async(hp[h], hc[h], hmax[h], d_out=d_out, out_cap=cap)
+    tk = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[h], res=hres[h])
     fetches = 1
     for k in range(rounds):
         for j in range(appends):
@@ -297,7 +303,7 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
         if r is not None:
             consume(h, r)
             h ^= 1
-            tk = eng.fetch_async(hp[h], hc[h], hmax[h], d_out=d_out, out_cap=cap)
+            tk = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[h], res=hres[h])
             fetches += 1
         t_host += time.perf_counter() - t1
     consume(h, eng.fetch_poll(tk, wait=True))
@@ -440,10 +446,12 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             nbytes += int(res["bytes"].sum())
         # the same requests as 8 asynchronous calls back to back (rmq_fetch_async: 4 in flight, the
         # host never waits on the GPU between issues), first issue to last result
-        maxr = np.full(P * consumers, mx, np.uint32)
+        areq = np.zeros((P * consumers, 4), np.uint32)
+        areq[:, 0], areq[:, 1], areq[:, 2] = pp, cc, mx
+        ares = [np.zeros(P * consumers, FETCH_RES_DTYPE) for _ in range(8)]  # (reused arrays, pages touched)
         eng.sync()
         t0 = time.perf_counter()
-        tks = [eng.fetch_async(pp, cc, maxr, d_out=d_out, out_cap=cap) for _ in range(8)]
+        tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=areq, res=ares[k]) for k in range(8)]
         n_async = sum(int(eng.fetch_poll(t, wait=True)[1]["count"].sum()) for t in tks)
         t_async = time.perf_counter() - t0
         eng.device_free(d_out)

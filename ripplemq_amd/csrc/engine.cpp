@@ -1254,7 +1254,7 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   // whose previous use has completed; a fetch or read-back issued later sees them
   const uint32_t m = (uint32_t)vp.size();
   rmq_engine::CommitSlot& cs = e->cslot[e->cslot_next];
-  e->cslot_next ^= 1u;
+  e->cslot_next = (e->cslot_next + 1) % rmq_engine::kCommitSlots;
   if (cs.used) HIP_TRY(hipEventSynchronize(cs.ev));
   if (m > cs.cap) {
     if (cs.h) hipHostFree(cs.h);

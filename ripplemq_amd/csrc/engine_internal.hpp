@@ -275,7 +275,7 @@ struct rmq_engine {
   uint32_t key_bits = 0;
   uint32_t rank_mode = 0;  // RMQ_RANK: stage 1 by the LDS radix sort (0) or by hash counters (1;
                            // 4.86 vs 5.14 G msgs/s at config B, profiles/r04c_*)
-  uint32_t max_ahead = 4;  // RMQ_AHEAD: pipeline launches queued at most (0: unbounded)
+  uint32_t max_ahead = 8;  // RMQ_AHEAD: pipeline launches queued at most (0: unbounded)
   uint32_t steal = 0;      // RMQ_STEAL=1: stage-3 workgroups take stage-1 tiles when out of tasks
                            // (5.20 -> 4.00 G msgs/s: stage 2 and the second half of stage 3 start later)
   PipeScratch scratch[kSets]{};
@@ -343,7 +343,7 @@ struct rmq_engine {
   uint32_t fslot_next = 0;
   uint64_t fetch_seq = 0;        // tickets
   std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
-  // consumer-offset commits: two staging slots (pinned items -> device by one copy on the pipeline
+  // consumer-offset commits: staging slots (pinned items -> device by one copy on the pipeline
   // stream), so a commit is ordered with the append stream without waiting for it
   struct CommitSlot {
     uint8_t* h = nullptr;
@@ -351,7 +351,11 @@ struct rmq_engine {
     uint32_t cap = 0;
     hipEvent_t ev = nullptr;
     bool used = false;
-  } cslot[2];
+  };
+  // a slot is reused once the commit that last used it has run on the pipeline stream, which may
+  // queue a few launches ahead of it (RMQ_AHEAD): enough slots that a commit rarely waits
+  static constexpr uint32_t kCommitSlots = 16;
+  CommitSlot cslot[kCommitSlots];
   uint32_t cslot_next = 0;
   std::vector<uint32_t> lww_stamp;  // [P * C] generation of the last commit item seen per slot
   uint32_t lww_gen = 0;

@@ -332,14 +332,22 @@ class Engine:
         return rc, res, int(used.value)
 
     def fetch_async(self, pidx, consumer, max_records, d_out: int | None = None, out_cap: int = 0,
-                    out: np.ndarray | None = None) -> "FetchTicket":
+                    out: np.ndarray | None = None, req: np.ndarray | None = None,
+                    res: np.ndarray | None = None) -> "FetchTicket":
         """rmq_fetch_async into a device buffer (d_out, 16-byte aligned) or a host array (out): the
         call returns at once; fetch_poll(ticket) gives (rc, res, bytes_used) once it completes. The
-        handle keeps the request, result and output arrays alive until then."""
-        n = len(pidx)
-        req = np.empty((n, 4), np.uint32)
-        req[:, 0], req[:, 1], req[:, 2], req[:, 3] = pidx, consumer, max_records, 0
-        res = np.empty(n, FETCH_RES_DTYPE)
+        handle keeps the request, result and output arrays alive until then. req ([n, 4] uint32)
+        and res (FETCH_RES_DTYPE[n]) may be a caller's arrays reused from call to call; with req
+        given, pidx / consumer / max_records None leave those columns as they are."""
+        n = len(pidx) if pidx is not None else len(req)
+        if req is None:
+            req = np.empty((n, 4), np.uint32)
+            req[:, 3] = 0
+        for col, v in ((0, pidx), (1, consumer), (2, max_records)):
+            if v is not None:
+                req[:, col] = v
+        if res is None:
+            res = np.empty(n, FETCH_RES_DTYPE)
         if d_out is not None:
             mem, ptr = A.RMQ_MEM_DEVICE, C.c_void_p(d_out)
         else:
