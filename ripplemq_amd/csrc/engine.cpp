@@ -274,11 +274,15 @@ int close_group(rmq_engine* e) {
   // Launch L's first lane reports L - 1 complete (done word).
   if (e->max_ahead && !e->repl) {
     const uint64_t need = e->launch_seq + 1 > e->max_ahead ? e->launch_seq + 1 - e->max_ahead : 0;
-    while (need > __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE)) {
-      const hipError_t q = hipStreamQuery(e->main_s);
-      if (q == hipSuccess) break;
-      if (q != hipErrorNotReady) return hip_fail(q);
-      std::this_thread::yield();
+    // poll the done word (host memory); the stream itself only now and then (a faulted launch
+    // never moves the word: its sticky error ends the wait)
+    for (uint32_t spin = 1; need > __atomic_load_n(e->done_host, __ATOMIC_ACQUIRE); ++spin) {
+      if ((spin & 1023u) == 0) {
+        const hipError_t q = hipStreamQuery(e->main_s);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) return hip_fail(q);
+      }
+      __builtin_ia32_pause();
     }
   }
   int rc = launch_stages(e, s1, e->has1 ? &e->g1 : nullptr, e->has2 ? &e->g2 : nullptr,
