@@ -27,6 +27,7 @@ per batch.
 from __future__ import annotations
 
 import argparse
+import collections
 import dataclasses
 import glob
 import json
@@ -291,22 +292,41 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
         eng.commit_consumer_offset(hp[h], hc[h], res["start_offset"] + n)  # consumer: it resumes at
         # the first retained offset, which start_offset carries
 
-    t0 = time.perf_counter()
-    h = 0
-    tk = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[h], res=hres[h])
-    fetches = 1
-    for k in range(rounds):
-        for j in range(appends):
-            step(k0 + k * appends + j)
+    state = {"h": 0, "tk": None}
+
+    def service() -> bool:
+        """One step of the consumer loop: the running fetch's results in, that half's commit, the
+        other half's fetch out. False while the fetch is still running."""
+        nonlocal fetches, t_host
         t1 = time.perf_counter()
-        r = eng.fetch_poll(tk, wait=False)
+        r = eng.fetch_poll(state["tk"], wait=False)
         if r is not None:
-            consume(h, r)
-            h ^= 1
-            tk = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[h], res=hres[h])
+            consume(state["h"], r)
+            state["h"] ^= 1
+            h = state["h"]
+            state["tk"] = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[h], res=hres[h])
             fetches += 1
         t_host += time.perf_counter() - t1
-    consume(h, eng.fetch_poll(tk, wait=True))
+        return r is not None
+
+    t0 = time.perf_counter()
+    state["tk"] = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[0], res=hres[0])
+    fetches = 1
+    # the broker bounds its own run-ahead (the engine queues every launch it is given): at most
+    # `window` batches not yet complete, so a fetch ordered behind them returns within about eight
+    # launches; while it waits for the oldest one, it serves the consumers
+    window = 8 * appends
+    inflight = collections.deque()
+    for k in range(rounds):
+        for j in range(appends):
+            while len(inflight) >= window:
+                if eng.poll(inflight[0]) is not None:
+                    inflight.popleft()
+                elif not service():
+                    time.sleep(0)
+            inflight.append(step(k0 + k * appends + j))
+        service()
+    consume(state["h"], eng.fetch_poll(state["tk"], wait=True))
     eng.sync()
     dt = time.perf_counter() - t0
     eng.device_free(d_out)
@@ -316,9 +336,10 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
             "max_records": mx, "wall_s": dt, "consumer_host_s": t_host,
             "lag_bound": "U[0, retained records / 2] per partition at the start",
             "consumer_resets": resets,
-            "note": "one host thread: appends (device-resident batches) and, between them, the consumers' "
-                    "fetches at max = 10 through rmq_fetch_async (polled without waiting, two halves of the "
-                    "consumers alternating, each half committing its next offsets before its next fetch); "
+            "note": "one host thread: appends (device-resident batches, at most 8 launch groups not yet "
+                    "complete) and, between them, the consumers' fetches at max = 10 through rmq_fetch_async "
+                    "(polled without waiting, two halves of the consumers alternating, each half committing "
+                    "its next offsets before its next fetch); "
                     "both rates over the same wall time; consumers start lagging the high watermark by "
                     "U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not HBM-resident at 4,096 "
                     "partitions, so it is bounded by what the rings retain)"}

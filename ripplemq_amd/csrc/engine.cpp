@@ -1180,109 +1180,92 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   if (ticket) *ticket = 0;
   if (!n) return RMQ_OK;
   if (!pidx || !consumer || !offset) return RMQ_EINVAL;
-  std::vector<uint32_t> vp, vc;
-  std::vector<uint64_t> vo;
-  int rc_all = RMQ_OK;
-  for (uint32_t i = 0; i < n; ++i) {
-    int st = RMQ_OK;
-    if (pidx[i] >= e->cfg.num_partitions)
-      st = RMQ_ENOPART;
-    else if (!e->is_leader[pidx[i]])
-      st = RMQ_ENOTLEADER;
-    else if (consumer[i] >= e->cfg.max_consumers)
-      st = RMQ_EINVAL;
-    if (status) status[i] = st;
-    if (st) {
-      if (!rc_all) rc_all = st;
-      continue;
-    }
-    vp.push_back(pidx[i]);
-    vc.push_back(consumer[i]);
-    vo.push_back(offset[i]);
-  }
-  if (vp.empty()) return rc_all;
-  // last writer wins (PartitionStateMachine.java:71-77): keep only the last item per
-  // (partition, consumer), so the device scatter has no two writers to one slot
-  {
-    // a generation stamp per (partition, consumer) slot instead of a hash set (16,384 items: tens
-    // of microseconds instead of about a millisecond)
-    const size_t slots = (size_t)e->cfg.num_partitions * e->cfg.max_consumers;
-    if (e->lww_stamp.size() != slots) {
-      e->lww_stamp.assign(slots, 0u);
-      e->lww_gen = 0;
-    }
-    if (++e->lww_gen == 0) {  // wrapped: stale stamps could alias the new generation
-      std::fill(e->lww_stamp.begin(), e->lww_stamp.end(), 0u);
-      e->lww_gen = 1;
-    }
-    const uint32_t gen = e->lww_gen;
-    size_t k = vp.size();
-    for (size_t i = vp.size(); i-- > 0;) {
-      uint32_t& sl = e->lww_stamp[(size_t)vp[i] * e->cfg.max_consumers + vc[i]];
-      if (sl == gen) continue;
-      sl = gen;
-      --k;
-      vp[k] = vp[i];
-      vc[k] = vc[i];
-      vo[k] = vo[i];
-    }
-    vp.erase(vp.begin(), vp.begin() + k);
-    vc.erase(vc.begin(), vc.begin() + k);
-    vo.erase(vo.begin(), vo.begin() + k);
-  }
-  // the new row version of every partition the call commits to (one per call), and the ticket's
-  // (partition, version) pairs
-  std::vector<uint64_t> vv(vp.size());
-  std::vector<std::pair<uint32_t, uint64_t>> tv;
-  {
-    if (e->cstamp.size() != e->cfg.num_partitions) {
-      e->cstamp.assign(e->cfg.num_partitions, 0u);
-      e->cstamp_gen = 0;
-    }
-    if (++e->cstamp_gen == 0) {
-      std::fill(e->cstamp.begin(), e->cstamp.end(), 0u);
-      e->cstamp_gen = 1;
-    }
-    for (size_t i = 0; i < vp.size(); ++i) {
-      const uint32_t p = vp[i];
-      if (e->cstamp[p] != e->cstamp_gen) {  // the partition's first item in this call
-        e->cstamp[p] = e->cstamp_gen;
-        tv.emplace_back(p, ++e->cver[p]);
-      }
-      vv[i] = e->cver[p];
-    }
-  }
   HIP_TRY(hipSetDevice(e->device));
   // no flush and no wait for the pipeline (it never reads the table): the items go to the device
   // with one copy on the pipeline stream, behind the launches issued so far, from a staging slot
   // whose previous use has completed; a fetch or read-back issued later sees them
-  const uint32_t m = (uint32_t)vp.size();
   rmq_engine::CommitSlot& cs = e->cslot[e->cslot_next];
   e->cslot_next = (e->cslot_next + 1) % rmq_engine::kCommitSlots;
   if (cs.used) HIP_TRY(hipEventSynchronize(cs.ev));
-  if (m > cs.cap) {
+  cs.used = false;
+  if (n > cs.cap) {
     if (cs.h) hipHostFree(cs.h);
     if (cs.d) hipFree(cs.d);
     cs.h = cs.d = nullptr;
     cs.cap = 0;
-    const uint32_t cap = std::max<uint32_t>(m, 4096);
+    const uint32_t cap = std::max<uint32_t>(n, 4096);
     HIP_TRY(hipHostMalloc((void**)&cs.h, 24ull * cap, 0));
     int rc = dalloc(&cs.d, 24ull * cap);
     if (rc) return rc;
     if (!cs.ev) HIP_TRY(hipEventCreateWithFlags(&cs.ev, hipEventDisableTiming));
     cs.cap = cap;
   }
-  std::memcpy(cs.h, vp.data(), 4ull * m);
-  std::memcpy(cs.h + 4ull * cs.cap, vc.data(), 4ull * m);
-  std::memcpy(cs.h + 8ull * cs.cap, vo.data(), 8ull * m);
-  std::memcpy(cs.h + 16ull * cs.cap, vv.data(), 8ull * m);
+  // ONE pass from the last item back, straight into the staging slot: the per-item checks, last
+  // writer wins (PartitionStateMachine.java:71-77: only the last item per (partition, consumer) is
+  // kept, so the device scatter has no two writers to one slot; a generation stamp per slot instead
+  // of a hash set), and the new row version of every partition the call commits to (one per call)
+  // with the ticket's (partition, version) pairs. The kept items end up at [k, n) in call order.
+  const size_t slots = (size_t)e->cfg.num_partitions * e->cfg.max_consumers;
+  if (e->lww_stamp.size() != slots) {
+    e->lww_stamp.assign(slots, 0u);
+    e->lww_gen = 0;
+  }
+  if (++e->lww_gen == 0) {  // wrapped: stale stamps could alias the new generation
+    std::fill(e->lww_stamp.begin(), e->lww_stamp.end(), 0u);
+    e->lww_gen = 1;
+  }
+  if (e->cstamp.size() != e->cfg.num_partitions) {
+    e->cstamp.assign(e->cfg.num_partitions, 0u);
+    e->cstamp_gen = 0;
+  }
+  if (++e->cstamp_gen == 0) {
+    std::fill(e->cstamp.begin(), e->cstamp.end(), 0u);
+    e->cstamp_gen = 1;
+  }
+  const uint32_t gen = e->lww_gen, cgen = e->cstamp_gen, C = e->cfg.max_consumers;
+  uint32_t* const hp = reinterpret_cast<uint32_t*>(cs.h);
+  uint32_t* const hc = reinterpret_cast<uint32_t*>(cs.h + 4ull * cs.cap);
+  uint64_t* const ho = reinterpret_cast<uint64_t*>(cs.h + 8ull * cs.cap);
+  uint64_t* const hv = reinterpret_cast<uint64_t*>(cs.h + 16ull * cs.cap);
+  std::vector<std::pair<uint32_t, uint64_t>> tv;
+  int rc_all = RMQ_OK;
+  uint32_t k = n;
+  for (uint32_t i = n; i-- > 0;) {
+    const uint32_t p = pidx[i], c = consumer[i];
+    int st = RMQ_OK;
+    if (p >= e->cfg.num_partitions)
+      st = RMQ_ENOPART;
+    else if (!e->is_leader[p])
+      st = RMQ_ENOTLEADER;
+    else if (c >= C)
+      st = RMQ_EINVAL;
+    if (status) status[i] = st;
+    if (st) {
+      rc_all = st;  // scanning back, the last one set is the first failing item in call order
+      continue;
+    }
+    uint32_t& sl = e->lww_stamp[(size_t)p * C + c];
+    if (sl == gen) continue;  // a later item of the call wins
+    sl = gen;
+    if (e->cstamp[p] != cgen) {  // the partition's first kept item
+      e->cstamp[p] = cgen;
+      tv.emplace_back(p, ++e->cver[p]);
+    }
+    --k;
+    hp[k] = p;
+    hc[k] = c;
+    ho[k] = offset[i];
+    hv[k] = e->cver[p];
+  }
+  const uint32_t m = n - k;
+  if (!m) return rc_all;
   HIP_TRY(hipMemcpyAsync(cs.d, cs.h, 24ull * cs.cap, hipMemcpyHostToDevice, e->main_s));
   ConsumerCommitArgs a{};
   a.st = e->st;
-  a.pidx = reinterpret_cast<const uint32_t*>(cs.d);
-  a.consumer = reinterpret_cast<const uint32_t*>(cs.d + 4ull * cs.cap);
-  a.offset = reinterpret_cast<const uint64_t*>(cs.d + 8ull * cs.cap);
-  a.ver = reinterpret_cast<const uint64_t*>(cs.d + 16ull * cs.cap);
+  a.pidx = reinterpret_cast<const uint32_t*>(cs.d) + k;
+  a.consumer = reinterpret_cast<const uint32_t*>(cs.d + 4ull * cs.cap) + k;
+  a.offset = reinterpret_cast<const uint64_t*>(cs.d + 8ull * cs.cap) + k;
+  a.ver = reinterpret_cast<const uint64_t*>(cs.d + 16ull * cs.cap) + k;
   a.n = m;
   launch_consumer_commit(a, e->main_s);
   HIP_TRY(hipGetLastError());

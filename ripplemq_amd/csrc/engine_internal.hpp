@@ -275,7 +275,8 @@ struct rmq_engine {
   uint32_t key_bits = 0;
   uint32_t rank_mode = 0;  // RMQ_RANK: stage 1 by the LDS radix sort (0) or by hash counters (1;
                            // 4.86 vs 5.14 G msgs/s at config B, profiles/r04c_*)
-  uint32_t max_ahead = 8;  // RMQ_AHEAD: pipeline launches queued at most (0: unbounded)
+  uint32_t max_ahead = 0;  // RMQ_AHEAD: pipeline launches queued at most (0: unbounded; a bound of
+                           // 4 or 8 cost 4-6 % at config B, profiles/r04i_*: bound it in the app)
   uint32_t steal = 0;      // RMQ_STEAL=1: stage-3 workgroups take stage-1 tiles when out of tasks
                            // (5.20 -> 4.00 G msgs/s: stage 2 and the second half of stage 3 start later)
   PipeScratch scratch[kSets]{};
