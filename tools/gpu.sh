@@ -14,6 +14,7 @@
 #   ab[:NAME]  A/B of the current library against variants/NAME/ (default head; 400- and 20-step lines, 2 pairs)
 #   local2     2-rank rehearsal on one GPU over the in-process transport (+ kernel trace)
 #   local4     4-rank rehearsal (config C shape)
+#   ab2[:NAME] A/B of the 2-rank rehearsal against variants/NAME/ (default head)
 #   prof       rocprofv3 --kernel-trace --stats of the default line (kernel stats CSV)
 #   pmc        rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) of a 300-step line
 #   stamps     per-wave phase stamps of launch 100 (RMQ_STAMPS) + timing-only RMQ_DEBUG lines
@@ -60,6 +61,14 @@ for step in "$@"; do
     local2)
       run 300 "${T}_local2.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
       prof 300 local2_prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_local2_kt" -o kt -- python3 "$R/bench.py" --gpus 2 --transport local --steps 100 --warmup 10 --segment-mb 2 --pool 8 $Q ;;
+    ab2|ab2:*)  # A/B of the 2-rank rehearsal: current library vs variants/NAME/ (default head), two pairs
+      V=head; [ "$step" != ab2 ] && V=${step#ab2:}
+      for k in 1 2; do
+        for v in cur $V; do
+          if [ $v = cur ]; then L=$R/ripplemq_amd/libripplemq_engine.so; else L=$R/variants/$V/libripplemq_engine.so; fi
+          RMQ_LIB=$L run 300 "${T}_local2_${v}_$k.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
+        done
+      done ;;
     local4) run 300 "${T}_local4.json" python bench.py --gpus 4 --transport local --steps 100 --warmup 10 --segment-mb 1 --pool 4 --config C $Q ;;
     prof) prof 500 prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_prof" -o kt -- python3 "$R/bench.py" --no-cpu-baseline --host-steps 0 ;;
     pmc)
