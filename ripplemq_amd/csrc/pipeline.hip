@@ -716,7 +716,7 @@ __device__ __forceinline__ bool partial_end(const DevState& st, u32 p, u64 fpos,
 // a wait for all memory operations. The caller ignores the values of an entry past the list, and
 // selects t3 / lastg by A.g3.nb where it uses them.
 struct PlanIn {
-  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg, term, commit;
+  u64 tot, f_off, f_pos, gap, t3, leo, used, lastg, term;
   u32 p, fl;
 };
 __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
@@ -733,7 +733,6 @@ __device__ __forceinline__ PlanIn plan_in(const PipeArgs& A, u32 e, u32 p) {
   v.used = A.cur.used[p];
   v.lastg = A.lastg[p];
   v.term = A.st.term[p];
-  v.commit = X.csnap[p];
   return v;
 }
 
@@ -919,7 +918,10 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
           de[0] = make_uint4((u32)cnt, (u32)b16, (u32)first, (u32)(first >> 32));
           const u64 term = cur.term | (rebase ? kTermRebase : 0ull);
           de[1] = make_uint4((u32)t_ex, (u32)d_ex, (u32)term, (u32)(term >> 32));
-          de[2] = make_uint4((u32)cur.commit, (u32)(cur.commit >> 32), 0u, 0u);
+          // (loaded here, not with the entry's prefetched inputs: two more live registers per
+          // prefetched entry pushed the transport kernel into 3.5 KB of scratch per lane)
+          const u64 lcm = X.csnap[p];
+          de[2] = make_uint4((u32)lcm, (u32)(lcm >> 32), 0u, 0u);
           XEntry xe;
           xe.data_abs = kNoRound;
           xe.tab_abs = 0;
@@ -1918,7 +1920,12 @@ __device__ __forceinline__ void stage1_tiles(const PipeArgs& A, char* smem, u32 
 // XR: a replication transport is attached (stage 3 also fills the group's outbox); a separate
 // instantiation so the single-GPU kernel keeps its register budget.
 template <bool XR>
-__global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(PipeArgs A) {
+__global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(PipeArgs args) {
+  // The arguments are read in place from the kernarg segment: with the by-value parameter, a select
+  // between two of its fields (batch lookups) made the compiler copy all 3.4 KB of it into scratch
+  // in every lane of the transport kernel (6x slower launches, round 4)
+  (void)args;
+  const PipeArgs& A = *(const PipeArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   if (blockIdx.x == 0 && threadIdx.x == 0 && A.done_word)
     __hip_atomic_store(A.done_word, A.launch_seq - 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
