@@ -33,9 +33,6 @@
 
 namespace rmq {
 
-#ifndef RMQ_VERIFY_OCC
-#define RMQ_VERIFY_OCC 6  // waves per SIMD of the verify kernel (its speculative payload round: 80 VGPRs)
-#endif
 constexpr u32 kIT = 512;           // threads per verify workgroup
 constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
 constexpr u32 kIR = 32;            // records per task
@@ -263,7 +260,6 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   bool ok = false, owner = false, reb = false;
   const uint8_t* rec = R.base;
   uint4 hdr = make_uint4(0, 0, 0, 0);
-  uint4 v0[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   if (in) {
     const u64* tabp = reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries) + i;
     const u64 tab = tabp[0];
@@ -283,14 +279,6 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
     const u64 rel = 16ull * (u64)(d16 - d.dstart16);
     if (k == (u32)tab && d16 >= d.dstart16 && R.data_off + 16ull * d16 + 16ull <= R.rows_off) {
       hdr = *reinterpret_cast<const uint4*>(rec);
-      // the first round of payload pieces (j, j + 2, j + 4, j + 6) with the header, before its
-      // length is known: the record's bytes follow its header in the data section (pieces past
-      // the record are ignored, none is read past the section)
-#pragma unroll
-      for (u32 u = 0; u < 4; ++u) {
-        const u64 at = R.data_off + 16ull * ((u64)d16 + 1ull + 2u * u + j);
-        if (at + 16ull <= R.rows_off) v0[u] = *reinterpret_cast<const uint4*>(R.base + at);
-      }
       off = ((u64)hdr.y << 32) | hdr.x;
       L = hdr.z;
       m = (L + 15u) >> 4;
@@ -317,9 +305,9 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   for (u32 c = 0; __any(c < (mm + 1u) / 2u); c += 4) {
     uint4 v[4];
 #pragma unroll
-    for (u32 u = 0; u < 4; ++u) {  // four pieces in flight per lane (the first four loaded above)
+    for (u32 u = 0; u < 4; ++u) {  // four pieces in flight per lane
       const u32 jp = 2u * (c + u) + j;
-      v[u] = c == 0 ? v0[u] : jp < mm ? *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * jp) : make_uint4(0, 0, 0, 0);
+      v[u] = jp < mm ? *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * jp) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (u32 u = 0; u < 4; ++u) {
@@ -405,7 +393,7 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
 // A grid of at most a few workgroups per CU: each copies the CRC tables into LDS once and its waves
 // take tasks w, w + waves, ... (the tables were 20 KB per 32 records' worth of workgroup before;
 // the 16-byte shift is a multiply, the 1 KB one of large records is read from global memory).
-__global__ __launch_bounds__(kIT, RMQ_VERIFY_OCC) void ingest_verify_kernel(IngestArgs A) {
+__global__ __launch_bounds__(kIT, 8) void ingest_verify_kernel(IngestArgs A) {
   __shared__ __attribute__((aligned(16))) u32 t8[8][256];
   __shared__ __attribute__((aligned(16))) u32 z32[4][256];  // register shift past 32 zero bytes
   {
