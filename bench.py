@@ -351,8 +351,9 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
     native record scan, one file append per partition) while the workload appends: per round one
     launch group of batches, then a spill. Then consumers lagging BELOW the rings (configs[4]'s
     U[0, 10^6] lag: offsets the rings no longer hold) are served from the files at max = 1024
-    (DurableLog.read, as PartitionBroker.process_batch_read does on RMQ_EOFFSET). Both timed on the
-    host; the record bytes counted are the FORMAT.md §1 images written / read."""
+    (DurableLog.read_images: the record images, as rmq_fetch returns them; PartitionBroker's
+    process_batch_read falls back to DurableLog.read on RMQ_EOFFSET). Both timed on the host; the
+    record bytes counted are the FORMAT.md §1 images written / read."""
     import shutil
     import tempfile
 
@@ -390,9 +391,9 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
         recs = rbytes = 0
         t0 = time.perf_counter()
         for p, off in reqs:
-            got = tier.read(p, off, 1024)
-            recs += len(got)
-            rbytes += sum(16 + (len(b) + 15) // 16 * 16 for _, _, b in got)
+            n, img = tier.read_images(p, off, 1024)
+            recs += n
+            rbytes += len(img)
         t_read = time.perf_counter() - t0
     finally:
         shutil.rmtree(root, ignore_errors=True)

@@ -22,7 +22,8 @@ The engine's replica rings keep a retained window only (FORMAT.md §4): a fetch 
 * The rest of a partition's durable state, as jraft keeps it in the partition's log and
   ``raft_meta`` directory (``PartitionRaftServer.java:53,88-90``): every spill also writes the
   partition's consumer-offset row (the reference's offset commits are log entries applied by
-  ``PartitionStateMachine.java:71-77``) to ``p<pidx>/offsets.bin`` and its term to
+  ``PartitionStateMachine.java:71-77``; the tier's own cursor slot stored as 0, the durable end
+  being in the ends file) to ``p<pidx>/offsets.bin`` and its term and cursor slot to
   ``p<pidx>/meta.json``, each replaced atomically (write, fsync if asked, rename) when it changed;
   ``replay`` restores both after the records (the term through ``rmq_become_leader``, so only
   appends of the restored term advance the commit). Offsets and terms are durable at spill
@@ -122,7 +123,8 @@ class _PartitionFiles:
         os.makedirs(self.dir, exist_ok=True)
         self.limit = segment_file_bytes
         self.base = 0
-        self.pos = np.zeros(1, np.int64)
+        self._pos = np.zeros(1024, np.int64)  # record positions with room to grow (pos: the live part)
+        self._n = 1
         self.seg_first: list[int] = []   # first offset of every segment file
         self.seg_pos: list[int] = []     # its first logical byte
         names = sorted(int(f[:-len(SEG_SUFFIX)]) for f in os.listdir(self.dir) if f.endswith(SEG_SUFFIX))
@@ -150,7 +152,18 @@ class _PartitionFiles:
             cat.append(rp[:-1] + acc)
             acc += int(rp[-1])
         if cat:
-            self.pos = np.concatenate(cat + [np.asarray([acc], np.int64)])
+            self._set_pos(np.concatenate(cat + [np.asarray([acc], np.int64)]))
+
+    @property
+    def pos(self) -> np.ndarray:
+        """Logical byte position of every durable record, then the end."""
+        return self._pos[:self._n]
+
+    def _set_pos(self, v: np.ndarray) -> None:
+        if len(v) > len(self._pos):
+            self._pos = np.zeros(max(len(v), 2 * len(self._pos)), np.int64)
+        self._pos[:len(v)] = v
+        self._n = len(v)
 
     def _path(self, first: int) -> str:
         return os.path.join(self.dir, f"{first:020d}{SEG_SUFFIX}")
@@ -164,15 +177,20 @@ class _PartitionFiles:
                 os.fsync(f.fileno())
         os.replace(tmp, os.path.join(self.dir, name))
 
-    def save_state(self, offsets: np.ndarray, term: int, fsync: bool) -> None:
-        """The partition's consumer-offset row and term, each rewritten only when it changed."""
-        row = np.ascontiguousarray(offsets, np.uint64).tobytes()
+    def save_state(self, offsets: np.ndarray, term: int, cursor: int, fsync: bool) -> None:
+        """The partition's consumer-offset row and term, each rewritten only when it changed. The
+        tier's own cursor slot is stored as 0 (the durable end is in the ends file and moves with
+        every spill: the row then changes only when consumers commit)."""
+        row = np.array(offsets, np.uint64)
+        if 0 <= cursor < len(row):
+            row[cursor] = 0
+        row = row.tobytes()
         if self._row is None:
             self._row = self.load_offsets_bytes()
         if row != self._row:
             self._replace(OFFSETS_FILE, row, fsync)
             self._row = row
-        meta = {"term": int(term)}
+        meta = {"term": int(term), "cursor": int(cursor)}
         if self._meta is None:
             self._meta = self.load_meta()
         if self._meta != meta:
@@ -213,11 +231,17 @@ class _PartitionFiles:
             self.seg_first.append(first)
             self.seg_pos.append(total)
         with open(self._path(self.seg_first[-1]), "ab") as f:
-            f.write(data.tobytes())
+            f.write(memoryview(np.ascontiguousarray(data)))
             if fsync:
                 f.flush()
                 os.fsync(f.fileno())
-        self.pos = np.concatenate([self.pos[:-1], rp + total])
+        n0 = self._n - 1  # the end entry is overwritten by the first new record's position
+        if n0 + len(rp) > len(self._pos):
+            grown = np.zeros(max(n0 + len(rp), 2 * len(self._pos)), np.int64)
+            grown[:self._n] = self._pos[:self._n]
+            self._pos = grown
+        self._pos[n0:n0 + len(rp)] = rp + total
+        self._n = n0 + len(rp)
 
     def read_bytes(self, a: int, b: int) -> bytes:
         """Logical bytes [a, b) across the segment files."""
@@ -306,7 +330,7 @@ class DurableLog:
         for k, p in enumerate(pidx.tolist()):
             if int(res["status"][k]) == A.RMQ_ENOTLEADER:
                 continue
-            self.parts[p].save_state(rows[p], int(terms[p]), self.fsync)
+            self.parts[p].save_state(rows[p], int(terms[p]), self.cursor, self.fsync)
         ends = np.array([[p, f.end] for p, f in self.parts.items()], np.uint64).reshape(-1, 2)
         tmp = os.path.join(self.dir, ENDS_FILE + ".tmp")
         with open(tmp, "wb") as f:
@@ -319,11 +343,17 @@ class DurableLog:
 
     def read(self, p: int, off: int, max_messages: int) -> list[tuple[int, int, bytes]]:
         """Records [off, min(off + max, durable end)) of partition p from the files."""
+        return split_records(self.read_images(p, off, max_messages)[1])
+
+    def read_images(self, p: int, off: int, max_messages: int) -> tuple[int, bytes]:
+        """(count, record images) of [off, min(off + max, durable end)): the FORMAT.md §1 bytes as
+        rmq_fetch returns them, one read per segment file touched (a broker forwarding record
+        images, as the fetch output, needs no per-record split)."""
         f = self.parts[p]
         end = min(off + max(int(max_messages), 0), f.end)
         if off < f.base or off >= end:
-            return []
-        return split_records(f.read_records(off, end))
+            return 0, b""
+        return end - off, f.read_records(off, end)
 
 
 def replay(directory: str, engine, partitions, *, batch_records: int = 65536) -> dict:
@@ -378,14 +408,18 @@ def replay(directory: str, engine, partitions, *, batch_records: int = 65536) ->
                                             f"(a CRC or payload changed)")
     terms = rows = 0
     for p, f in files.items():
-        term = int(f.load_meta().get("term", 0))
+        meta = f.load_meta()
+        term = int(meta.get("term", 0))
         if term > engine.state(p)["term"]:
             engine.become_leader(p, term)
             terms += 1
         raw = f.load_offsets_bytes()
         if raw:
-            offs = np.frombuffer(raw, np.uint64)
+            offs = np.frombuffer(raw, np.uint64).copy()
             n = min(len(offs), engine.cfg.max_consumers)
+            c = int(meta.get("cursor", -1))
+            if 0 <= c < n:
+                offs[c] = f.end  # the tier's cursor: the durable end
             rc, st = engine.commit_consumer_offset(np.full(n, p, np.uint32), np.arange(n, dtype=np.uint32), offs[:n])
             if rc:
                 raise EngineError(rc, f"replay of partition {p}: consumer offsets")
