@@ -44,6 +44,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
+from ripplemq_amd._abi import RMQ_FETCH_COMMIT  # noqa: E402
 from ripplemq_amd.engine import FETCH_RES_DTYPE, Engine, EngineConfig, rccl_unique_id  # noqa: E402
 from ripplemq_amd.sharding import max_over_ranks, rank_view  # noqa: E402
 from ripplemq_amd.rings import partition_traffic, pool_layout, ring_sizes  # noqa: E402
@@ -245,13 +246,14 @@ def host_leg(eng, batches, steps: int) -> dict:
 def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
     """Appends and consumer fetches at once on one engine (configs[4]: concurrent consumer fetch at
     lagging offsets), driven by ONE host thread as a broker's event loop would: per round `appends`
-    device-resident batches go to the pipeline; the consumers (split in two halves) fetch at
-    max = 10 through rmq_fetch_async and commit the next offsets (read-then-commit,
-    ConsumerClientImpl.java:61-117). A fetch is polled without waiting; once its results are in,
-    that half commits and the other half's fetch is issued, so a consumer never fetches before
-    its previous commit and the host never waits on the append pipeline. Every fetch is ordered
-    between two pipeline launches (the next launch waits for it). Reports both rates over the
-    same wall time."""
+    device-resident batches go to the pipeline, and every (partition, consumer) reads max = 10 and
+    commits what it read (ConsumerClientImpl.java:61-117) through rmq_fetch_async with
+    RMQ_FETCH_COMMIT: the read-then-commit of each consumer happens on the device, so the next fetch,
+    ordered after it on the fetch stream, reads on from there and two fetches can be in flight
+    without a host round trip between them. Fetches are polled without waiting; every fetch runs
+    between two pipeline launches (the next launch waits for it). The broker bounds its own
+    run-ahead to eight launch groups (rmq_poll_commit), so a fetch returns within about eight
+    launches. Reports both rates over the same wall time."""
     P = spec.partitions
     eng.sync()
     st = eng.states()
@@ -263,58 +265,52 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     lag = (g.random(P * consumers) * (np.repeat(retained, consumers) // 2 + 1)).astype(np.int64)
     off = (np.repeat(hw, consumers) - lag).astype(np.uint64)
     eng.commit_consumer_offset(pp, cc, off)
-    half = [cc < consumers // 2, cc >= consumers // 2]
-    hp = [pp[m] for m in half]
-    hc = [cc[m] for m in half]
-    # each half's request and result arrays, reused by every fetch of that half
-    hreq = []
-    for m in half:
-        r = np.zeros((int(m.sum()), 4), np.uint32)
-        r[:, 0], r[:, 1], r[:, 2] = pp[m], cc[m], mx
-        hreq.append(r)
-    hres = [np.zeros(len(r), FETCH_RES_DTYPE) for r in hreq]
+    req = np.zeros((P * consumers, 4), np.uint32)
+    req[:, 0], req[:, 1], req[:, 2], req[:, 3] = pp, cc, mx, RMQ_FETCH_COMMIT
+    inflight_f = 2
+    res = [np.zeros(P * consumers, FETCH_RES_DTYPE) for _ in range(inflight_f)]
     hi = spec.size if isinstance(spec.size, int) else spec.size[1]
     cap = P * consumers * mx * (16 + (hi + 15) // 16 * 16) + 4096
-    d_out = eng.device_alloc(cap)
+    d_out = [eng.device_alloc(cap) for _ in range(inflight_f)]
     fetched = resets = fetches = 0
     t_host = 0.0
     k0 = 10_000
+    fq = collections.deque()  # (ticket, slot) of the fetches in flight, oldest first
+    nslot = 0
 
-    def consume(h, r):
+    def take(r):
         nonlocal fetched, resets
-        rc, res, _ = r
-        stt = res["status"]
+        rc, rs, _ = r
+        stt = rs["status"]
         if rc or np.any((stt != 0) & (stt != -6)):
             raise SystemExit(f"bench: mixed leg fetch failed rc={rc} statuses={np.unique(stt)}")
-        n = res["count"].astype(np.uint64)
-        fetched += int(n.sum())
+        fetched += int(rs["count"].sum())
         resets += int(np.count_nonzero(stt == -6))  # RMQ_EOFFSET: the ring moved past a slow
-        eng.commit_consumer_offset(hp[h], hc[h], res["start_offset"] + n)  # consumer: it resumes at
-        # the first retained offset, which start_offset carries
-
-    state = {"h": 0, "tk": None}
+        # consumer, which resumes at the first retained offset (committed on the device)
 
     def service() -> bool:
-        """One step of the consumer loop: the running fetch's results in, that half's commit, the
-        other half's fetch out. False while the fetch is still running."""
-        nonlocal fetches, t_host
+        """Completed fetches in, new ones out (at most two in flight). False if nothing moved."""
+        nonlocal fetches, t_host, nslot
         t1 = time.perf_counter()
-        r = eng.fetch_poll(state["tk"], wait=False)
-        if r is not None:
-            consume(state["h"], r)
-            state["h"] ^= 1
-            h = state["h"]
-            state["tk"] = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[h], res=hres[h])
+        moved = False
+        while fq:
+            r = eng.fetch_poll(fq[0][0], wait=False)
+            if r is None:
+                break
+            take(r)
+            fq.popleft()
+            moved = True
+        while len(fq) < inflight_f:
+            k = nslot % inflight_f
+            nslot += 1
+            fq.append((eng.fetch_async(None, None, None, d_out=d_out[k], out_cap=cap, req=req, res=res[k]), k))
             fetches += 1
+            moved = True
         t_host += time.perf_counter() - t1
-        return r is not None
+        return moved
 
     t0 = time.perf_counter()
-    state["tk"] = eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=hreq[0], res=hres[0])
-    fetches = 1
-    # the broker bounds its own run-ahead (the engine queues every launch it is given): at most
-    # `window` batches not yet complete, so a fetch ordered behind them returns within about eight
-    # launches; while it waits for the oldest one, it serves the consumers
+    service()
     window = 8 * appends
     inflight = collections.deque()
     for k in range(rounds):
@@ -326,23 +322,24 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
                     time.sleep(0)
             inflight.append(step(k0 + k * appends + j))
         service()
-    consume(state["h"], eng.fetch_poll(state["tk"], wait=True))
+    while fq:
+        take(eng.fetch_poll(fq.popleft()[0], wait=True))
     eng.sync()
     dt = time.perf_counter() - t0
-    eng.device_free(d_out)
+    for d in d_out:
+        eng.device_free(d)
     recs = rounds * appends * spec.records
     return {"append_msgs_per_s": recs / dt, "fetch_records_per_s": fetched / dt, "rounds": rounds,
-            "appends_per_round": appends, "fetches": fetches, "requests_per_fetch": P * consumers // 2,
+            "appends_per_round": appends, "fetches": fetches, "requests_per_fetch": P * consumers,
             "max_records": mx, "wall_s": dt, "consumer_host_s": t_host,
             "lag_bound": "U[0, retained records / 2] per partition at the start",
             "consumer_resets": resets,
             "note": "one host thread: appends (device-resident batches, at most 8 launch groups not yet "
-                    "complete) and, between them, the consumers' fetches at max = 10 through rmq_fetch_async "
-                    "(polled without waiting, two halves of the consumers alternating, each half committing "
-                    "its next offsets before its next fetch); "
-                    "both rates over the same wall time; consumers start lagging the high watermark by "
-                    "U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not HBM-resident at 4,096 "
-                    "partitions, so it is bounded by what the rings retain)"}
+                    "complete) and, between them, every consumer's read-and-commit at max = 10 through "
+                    "rmq_fetch_async with RMQ_FETCH_COMMIT (two fetches in flight, polled without "
+                    "waiting); both rates over the same wall time; consumers start lagging the high "
+                    "watermark by U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not "
+                    "HBM-resident at 4,096 partitions, so it is bounded by what the rings retain)"}
 
 
 def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int = 512, consumers: int = 4) -> dict:

@@ -131,8 +131,15 @@ typedef struct rmq_fetch_req {
   uint32_t pidx;
   uint32_t consumer;           /* dense consumer id in [0, max_consumers) */
   uint32_t max_records;        /* reference: MessageBatchReadRequest.maxMessages */
-  uint32_t reserved;
+  uint32_t flags;              /* RMQ_FETCH_COMMIT, or 0 */
 } rmq_fetch_req;
+/* rmq_fetch_req.flags: once the request is served (RMQ_OK, its records in the output) or answered
+   RMQ_EOFFSET, commit the consumer's next offset — start_offset + count (the first retained offset
+   for RMQ_EOFFSET) — as rmq_commit_consumer_offset would (no ticket; with a transport the row
+   travels with the next round). The consumer client's read-then-commit
+   (ConsumerClientImpl.java:61-117) in one device pass. At most one committing request per
+   (partition, consumer) in a call (RMQ_EINVAL otherwise). */
+#define RMQ_FETCH_COMMIT 1u
 
 typedef struct rmq_fetch_res {
   uint64_t start_offset;       /* reference: MessageBatchReadResponse.offset (the consumer offset);

@@ -752,6 +752,16 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
              rmq_fetch_res* res, uint64_t* bytes_used) {
   uint64_t cursor = 0;
   int rc = RMQ_OK;
+  /* RMQ_FETCH_COMMIT: at most one committing request per (partition, consumer) */
+  for (uint32_t r = 0; r < n; ++r) {
+    if (reqs[r].flags & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
+    if (!(reqs[r].flags & RMQ_FETCH_COMMIT) || reqs[r].pidx >= e->cfg.num_partitions ||
+        reqs[r].consumer >= e->cfg.max_consumers)
+      continue;
+    for (uint32_t q = 0; q < r; ++q)
+      if ((reqs[q].flags & RMQ_FETCH_COMMIT) && reqs[q].pidx == reqs[r].pidx && reqs[q].consumer == reqs[r].consumer)
+        return RMQ_EINVAL;
+  }
   for (uint32_t r = 0; r < n; ++r) {
     rmq_fetch_res* x = &res[r];
     memset(x, 0, sizeof *x);
@@ -794,6 +804,14 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
     x->count = (uint32_t)(end - off);
     x->bytes = (uint32_t)nb;
     cursor += nb;
+  }
+  /* the committing requests' next offsets, after every request read its own (read-then-commit) */
+  for (uint32_t r = 0; r < n; ++r) {
+    const rmq_fetch_res* x = &res[r];
+    if (!(reqs[r].flags & RMQ_FETCH_COMMIT) || (x->status != RMQ_OK && x->status != RMQ_EOFFSET)) continue;
+    ro_part* s = &e->parts[reqs[r].pidx];
+    s->cons[reqs[r].consumer] = x->start_offset + (x->status == RMQ_OK ? x->count : 0);
+    s->dirty = 1;
   }
   if (bytes_used) *bytes_used = cursor;
   return rc;

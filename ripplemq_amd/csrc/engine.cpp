@@ -1398,6 +1398,33 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     if (rc < 0 && rc != RMQ_ENOSPC) return rc;
     e->fetch_done.push_back({old, (uint64_t)(int64_t)rc, used});
   }
+  // RMQ_FETCH_COMMIT: known flags only, one committing request per (partition, consumer)
+  {
+    bool any = false;
+    for (uint32_t r = 0; r < n; ++r) {
+      if (reqs[r].flags & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
+      any |= (reqs[r].flags & RMQ_FETCH_COMMIT) != 0;
+    }
+    if (any) {
+      const size_t slots = (size_t)e->cfg.num_partitions * e->cfg.max_consumers;
+      if (e->fetch_stamp.size() != slots) {
+        e->fetch_stamp.assign(slots, 0u);
+        e->fetch_gen = 0;
+      }
+      if (++e->fetch_gen == 0) {
+        std::fill(e->fetch_stamp.begin(), e->fetch_stamp.end(), 0u);
+        e->fetch_gen = 1;
+      }
+      for (uint32_t r = 0; r < n; ++r) {
+        const rmq_fetch_req& q = reqs[r];
+        if (!(q.flags & RMQ_FETCH_COMMIT) || q.pidx >= e->cfg.num_partitions || q.consumer >= e->cfg.max_consumers)
+          continue;
+        uint32_t& sl = e->fetch_stamp[(size_t)q.pidx * e->cfg.max_consumers + q.consumer];
+        if (sl == e->fetch_gen) return RMQ_EINVAL;
+        sl = e->fetch_gen;
+      }
+    }
+  }
   const uint64_t tk = ++e->fetch_seq;
   if (!n) {  // nothing to fetch: complete at once
     e->fetch_done.push_back({tk, (uint64_t)(int64_t)RMQ_OK, 0});

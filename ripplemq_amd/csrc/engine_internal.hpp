@@ -343,6 +343,8 @@ struct rmq_engine {
   FetchSlot fslot[kFetchSlots];
   uint32_t fslot_next = 0;
   uint64_t fetch_seq = 0;        // tickets
+  std::vector<uint32_t> fetch_stamp;  // RMQ_FETCH_COMMIT duplicate check ([P][C] generation stamps)
+  uint32_t fetch_gen = 0;
   std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
   // consumer-offset commits: staging slots (pinned items -> device by one copy on the pipeline
   // stream), so a commit is ordered with the append stream without waiting for it

@@ -261,11 +261,23 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
     const u64 pos = base + inc - nb;
     s_pos[tid] = pos;
     a.res[4 * rr + 1] = pos;  // out_pos (one result copy to the host)
-    if (nb && pos + nb > a.out_cap) {  // does not fit: not served (rare); its bytes still count
+    const bool nospc = nb && pos + nb > a.out_cap;
+    if (nospc) {  // does not fit: not served (rare); its bytes still count
       a.res[4 * rr + 2] = 0;
       a.res[4 * rr + 3] = (u64)(uint32_t)kNoSpc;
     }
     if (rr + 1 == a.n) a.res[4ull * a.n] = pos + nb;  // bytes needed
+    // RMQ_FETCH_COMMIT: the consumer's next offset once its records are in the output (or the
+    // first retained offset after RMQ_EOFFSET); every request's offset was read by the resolve
+    // kernel before (the host refuses two committing requests for one consumer in a call)
+    if (a.req[4 * rr + 3] & 1u) {
+      const int s0 = (int)(uint32_t)a.res[4 * rr + 3];
+      if (!nospc && (s0 == kOk || s0 == kOffset)) {
+        const u32 p = a.req[4 * rr], c = a.req[4 * rr + 1];
+        a.st.cons[(u64)p * a.st.C + c] = a.res[4 * rr] + (s0 == kOk ? (u64)(uint32_t)a.res[4 * rr + 2] : 0ull);
+        a.st.cdirty[p] = 1u;  // (with a transport the row travels with the next round)
+      }
+    }
   }
   // the wave's kGQ requests (lanes 0..kGQ-1 read one each; their ring words are loaded before the
   // barrier, so they are in flight during the placement scan)

@@ -301,7 +301,9 @@ class Engine:
             raise EngineError(rc, "rmq_poll_commit (offsets)")
         return rc
 
-    def fetch(self, pidx, consumer, max_records, out_cap: int | None = None):
+    def fetch(self, pidx, consumer, max_records, out_cap: int | None = None, commit: bool = False):
+        """rmq_fetch into a host array (sized by a first call when out_cap is None); commit:
+        RMQ_FETCH_COMMIT on every request (the size query commits nothing)."""
         n = len(pidx)
         req = np.zeros((n, 4), np.uint32)
         req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
@@ -312,6 +314,8 @@ class Engine:
             if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
                 raise EngineError(rc, "rmq_fetch")
             out_cap = int(used.value)
+        if commit:
+            req[:, 3] = A.RMQ_FETCH_COMMIT
         out = np.zeros(max(out_cap, 1), np.uint8)
         used = C.c_uint64()
         rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, _ptr(out), out_cap, _ptr(res), C.byref(used))
@@ -319,11 +323,12 @@ class Engine:
             raise EngineError(rc, "rmq_fetch")
         return rc, res, out[:out_cap], int(used.value)
 
-    def fetch_device(self, pidx, consumer, max_records, d_out: int, out_cap: int):
+    def fetch_device(self, pidx, consumer, max_records, d_out: int, out_cap: int, commit: bool = False):
         """rmq_fetch into a device buffer (16-byte aligned); returns (rc, res, bytes_used)."""
         n = len(pidx)
         req = np.zeros((n, 4), np.uint32)
         req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
+        req[:, 3] = A.RMQ_FETCH_COMMIT if commit else 0
         res = np.zeros(n, FETCH_RES_DTYPE)
         used = C.c_uint64()
         rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_DEVICE, d_out, out_cap, _ptr(res), C.byref(used))
@@ -338,7 +343,8 @@ class Engine:
         call returns at once; fetch_poll(ticket) gives (rc, res, bytes_used) once it completes. The
         handle keeps the request, result and output arrays alive until then. req ([n, 4] uint32)
         and res (FETCH_RES_DTYPE[n]) may be a caller's arrays reused from call to call; with req
-        given, pidx / consumer / max_records None leave those columns as they are."""
+        given, pidx / consumer / max_records None leave those columns as they are (column 3: the
+        requests' flags, RMQ_FETCH_COMMIT)."""
         n = len(pidx) if pidx is not None else len(req)
         if req is None:
             req = np.empty((n, 4), np.uint32)

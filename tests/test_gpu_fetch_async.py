@@ -109,3 +109,45 @@ def test_fetch_agrees_with_oracle(oracle_mod, replay):
         ops.append(("fetch", p[:1], c[:1], mx[:1]))
         ops.append(("fetch", p, c, np.full(n, 1024)))
         run_ops(dev, ora, cfg, ops, check=False)
+
+
+def _commit_loop(eng, P, C, rounds, batches, mx, cap):
+    """Appends interleaved with read-and-commit fetches of every (partition, consumer)."""
+    pp = np.repeat(np.arange(P, dtype=np.uint32), C)
+    cc = np.tile(np.arange(C, dtype=np.uint32), P)
+    out = []
+    for k in range(rounds):
+        for b in batches[k]:
+            eng.append(b.pidx, b.lens, b.payload)
+        rc, res, buf, used = eng.fetch(pp, cc, np.full(P * C, mx, np.uint32), out_cap=cap, commit=True)
+        out.append((rc, res.copy(), bytes(buf[:used])))
+    return out
+
+
+def test_fetch_commit_matches_oracle(oracle_mod):
+    """RMQ_FETCH_COMMIT: the consumers advance by what they were served (ConsumerClientImpl's
+    read-then-commit in one call); an output cut mid-way commits nothing for the requests that did
+    not fit; rings small enough that slow consumers fall below retention (RMQ_EOFFSET: they resume
+    at the first retained offset)."""
+    P, C = 64, 2
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 14, index_interval=256,
+                       max_consumers=C, max_batch_records=4096)
+    spec = StreamSpec(P, 1500, "zipf", size=(1, 300), config_index=46)
+    batches = [[make_batch(spec, 2 * k), make_batch(spec, 2 * k + 1)] for k in range(6)]
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        for cap in (1 << 20, 20000):
+            got = _commit_loop(dev, P, C, 6, batches if cap > 20000 else batches[::-1], 7, cap)
+            want = _commit_loop(ora, P, C, 6, batches if cap > 20000 else batches[::-1], 7, cap)
+            for k, (g, w) in enumerate(zip(got, want)):
+                assert g[0] == w[0], (cap, k)
+                for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                    assert np.array_equal(g[1][f], w[1][f]), (cap, k, f)
+                assert g[2] == w[2], (cap, k)
+            assert np.array_equal(dev.consumer_table(), ora.consumer_table())
+        st = np.concatenate([g[1]["status"] for g in got])
+        assert (st == A.RMQ_EOFFSET).any() and (st == A.RMQ_ENOSPC).any()
+        # two committing requests for one consumer in a call: refused as a whole
+        with pytest.raises(EngineError) as ei:
+            dev.fetch(np.zeros(2, np.uint32), np.zeros(2, np.uint32), np.full(2, 5, np.uint32), out_cap=1 << 16,
+                      commit=True)
+        assert ei.value.status == A.RMQ_EINVAL
