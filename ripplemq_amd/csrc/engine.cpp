@@ -477,6 +477,7 @@ void free_engine(rmq_engine* e) {
     if (f.h_res) hipHostFree(f.h_res);
     if (f.ev) hipEventDestroy(f.ev);
     if (f.ev_copy) hipEventDestroy(f.ev_copy);
+    if (f.ev_k) hipEventDestroy(f.ev_k);
   }
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -649,6 +650,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   for (rmq_engine::FetchSlot& f : e->fslot) {
     CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&f.ev_k, hipEventDisableTiming));
   }
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
@@ -1451,9 +1453,11 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
+    // the requests' copy first (it depends on nothing the pipeline writes: it overlaps the running
+    // launch), then the kernels behind the launches issued so far
+    HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
-    HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     const uint32_t runs = e->profile ? e->fetch_replay : 1u;
     if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run, copies outside
@@ -1470,9 +1474,11 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
       HIP_TRY(hipGetLastError());
     }
     if (e->profile) HIP_TRY(hipEventRecord(r1, e->fetch_s));
+    // the next launch waits for the kernels only (not for the result copy to the host)
+    HIP_TRY(hipEventRecord(f.ev_k, e->fetch_s));
+    HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_k, 0));
     HIP_TRY(hipMemcpyAsync(f.h_res, f.d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
     HIP_TRY(hipEventRecord(f.ev, e->fetch_s));
-    HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev, 0));
   }
   f.ticket = tk;
   f.phase = 1;

@@ -330,6 +330,7 @@ struct rmq_engine {
     uint64_t out_alloc = 0;
     hipEvent_t ev = nullptr;     // kernels and the result copy done
     hipEvent_t ev_copy = nullptr;  // host output copies done
+    hipEvent_t ev_k = nullptr;     // its kernels done (the pipeline stream waits for this one)
     // the fetch in flight: ticket 0 = idle; phase 1: kernels, 2: host output copies
     uint64_t ticket = 0;
     int phase = 0;
