@@ -45,7 +45,7 @@ sys.path.insert(0, REPO)
 
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
 from ripplemq_amd._abi import RMQ_FETCH_COMMIT  # noqa: E402
-from ripplemq_amd.engine import FETCH_RES_DTYPE, Engine, EngineConfig, rccl_unique_id  # noqa: E402
+from ripplemq_amd.engine import Engine, EngineConfig, rccl_unique_id  # noqa: E402
 from ripplemq_amd.sharding import max_over_ranks, rank_view  # noqa: E402
 from ripplemq_amd.rings import partition_traffic, pool_layout, ring_sizes  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
@@ -265,10 +265,10 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     lag = (g.random(P * consumers) * (np.repeat(retained, consumers) // 2 + 1)).astype(np.int64)
     off = (np.repeat(hw, consumers) - lag).astype(np.uint64)
     eng.commit_consumer_offset(pp, cc, off)
-    req = np.zeros((P * consumers, 4), np.uint32)
-    req[:, 0], req[:, 1], req[:, 2], req[:, 3] = pp, cc, mx, RMQ_FETCH_COMMIT
     inflight_f = 2
-    res = [np.zeros(P * consumers, FETCH_RES_DTYPE) for _ in range(inflight_f)]
+    rows = [eng.fetch_rows(P * consumers) for _ in range(inflight_f)]  # page-locked request / result rows
+    for rq, _ in rows:
+        rq[:, 0], rq[:, 1], rq[:, 2], rq[:, 3] = pp, cc, mx, RMQ_FETCH_COMMIT
     hi = spec.size if isinstance(spec.size, int) else spec.size[1]
     cap = P * consumers * mx * (16 + (hi + 15) // 16 * 16) + 4096
     d_out = [eng.device_alloc(cap) for _ in range(inflight_f)]
@@ -303,7 +303,8 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
         while len(fq) < inflight_f:
             k = nslot % inflight_f
             nslot += 1
-            fq.append((eng.fetch_async(None, None, None, d_out=d_out[k], out_cap=cap, req=req, res=res[k]), k))
+            fq.append((eng.fetch_async(None, None, None, d_out=d_out[k], out_cap=cap, req=rows[k][0], res=rows[k][1],
+                                       pinned_rows=True), k))
             fetches += 1
             moved = True
         t_host += time.perf_counter() - t1
@@ -328,6 +329,9 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     dt = time.perf_counter() - t0
     for d in d_out:
         eng.device_free(d)
+    for rq, rs in rows:
+        eng.host_release(rq)
+        eng.host_release(rs)
     recs = rounds * appends * spec.records
     return {"append_msgs_per_s": recs / dt, "fetch_records_per_s": fetched / dt, "rounds": rounds,
             "appends_per_round": appends, "fetches": fetches, "requests_per_fetch": P * consumers,
@@ -440,13 +444,22 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         # of the engine's four fetch slots allocates its scratch on first use
         for _ in range(4):
             eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+        # the request and result rows in page-locked arrays, reused from call to call
+        # (RMQ_FETCH_PINNED_ROWS: DMA both ways, no host copy)
+        rows = [eng.fetch_rows(P * consumers) for _ in range(8)]
+        for rq, _ in rows:
+            rq[:, 0], rq[:, 1], rq[:, 2] = pp, cc, mx
         for k in range(rounds):
             lag = (g.random(P * consumers) * (np.repeat(hw - lo, consumers) + 1)).astype(np.int64)
             eng.commit_consumer_offset(pp, cc, (np.repeat(hw, consumers) - lag).astype(np.uint64))
-            eng.profile(True)
+            # one call as an application makes it: issue, wait, results in the caller's rows
+            # (a fetch commits nothing here, so the calls below see the same offsets)
             t0 = time.perf_counter()
-            rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+            rc_c, _, _ = eng.fetch_poll(eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rows[0][0],
+                                                        res=rows[0][1], pinned_rows=True), wait=True)
             t_wall += time.perf_counter() - t0
+            eng.profile(True)
+            rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
             _, ms_f = eng.profile_query(3)  # the kernels' own dispatch-recorded spans, summed
             eng.profile(False)
             # kernel time: the same fetch's kernels run REPLAY times back to back between two events
@@ -457,23 +470,24 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             runs, ms_all = eng.profile_query(4)
             ms_r = ms_all / max(runs, 1)
             eng.profile(False)
-            if rc or np.any(res["status"] != 0):
+            if rc or rc_c or np.any(res["status"] != 0) or not np.array_equal(rows[0][1]["count"], res["count"]):
                 raise SystemExit(f"bench: fetch leg failed rc={rc} statuses={np.unique(res['status'])}")
             t_kern += ms_f / 1e3
             t_reg += ms_r / 1e3
             recs += int(res["count"].sum())
             nbytes += int(res["bytes"].sum())
         # the same requests as 8 asynchronous calls back to back (rmq_fetch_async: 4 in flight, the
-        # host never waits on the GPU between issues), first issue to last result
-        areq = np.zeros((P * consumers, 4), np.uint32)
-        areq[:, 0], areq[:, 1], areq[:, 2] = pp, cc, mx
-        ares = [np.zeros(P * consumers, FETCH_RES_DTYPE) for _ in range(8)]  # (reused arrays, pages touched)
+        # host never waits on the GPU between issues; pinned rows), first issue to last result
         eng.sync()
         t0 = time.perf_counter()
-        tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=areq, res=ares[k]) for k in range(8)]
+        tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rq, res=rs, pinned_rows=True)
+               for rq, rs in rows]
         n_async = sum(int(eng.fetch_poll(t, wait=True)[1]["count"].sum()) for t in tks)
         t_async = time.perf_counter() - t0
         eng.device_free(d_out)
+        for rq, rs in rows:
+            eng.host_release(rq)
+            eng.host_release(rs)
         # B_fetch = 2 (H + L) per returned record (fixed-size configs: exact; mixed
         # sizes: the records' bytes in the log layout, which adds their padding to 16 bytes)
         rec_bytes = recs * (16 + spec.size) if isinstance(spec.size, int) else nbytes

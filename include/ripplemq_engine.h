@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 6u
+#define RMQ_ABI_VERSION 7u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -301,7 +301,12 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
    must stay valid until rmq_fetch_poll returns something other than RMQ_PENDING. Four fetches can
    be in flight: a fifth first completes the oldest into its caller's arrays (its poll then returns
    at once). MessageBatchReadRequestProcessor.java:36-42 answers each read from its own closure;
-   this is the batched, pipelined form of that call. */
+   this is the batched, pipelined form of that call.
+   mem | RMQ_FETCH_PINNED_ROWS (ABI 7; rmq_fetch too): reqs and res are page-locked host memory
+   (rmq_host_alloc or rmq_host_register): the requests go to the device and the result rows come back
+   by DMA with no host copy. The caller then keeps reqs unchanged until the ticket completes (as
+   with pinned batches); res is written by the DMA before the poll that returns the result. */
+#define RMQ_FETCH_PINNED_ROWS 0x100u
 int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
                     uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket);
 /* Completion of an rmq_fetch_async ticket: RMQ_PENDING while it runs (wait != 0: block instead), else

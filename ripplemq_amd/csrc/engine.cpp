@@ -478,6 +478,7 @@ void free_engine(rmq_engine* e) {
     if (f.ev) hipEventDestroy(f.ev);
     if (f.ev_copy) hipEventDestroy(f.ev_copy);
     if (f.ev_k) hipEventDestroy(f.ev_k);
+    if (f.ev_in) hipEventDestroy(f.ev_in);
   }
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -505,6 +506,7 @@ void free_engine(rmq_engine* e) {
   }
   if (e->ev_main) hipEventDestroy(e->ev_main);
   if (e->fetch_s) hipStreamDestroy(e->fetch_s);
+  if (e->fetch_out_s) hipStreamDestroy(e->fetch_out_s);
   if (e->copy_s) hipStreamDestroy(e->copy_s);
   for (auto& v : e->prof)
     for (EvPair& p : v) {
@@ -638,12 +640,13 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   hipDeviceProp_t prop;
   CREATE_HIP(hipGetDeviceProperties(&prop, e->device));
   e->cu_count = (uint32_t)prop.multiProcessorCount;
-  e->verify_wgs = 4u * e->cu_count;
+  e->verify_wgs = verify_wgs_per_cu() * e->cu_count;
   if (const char* v = std::getenv("RMQ_VERIFY_WGS")) e->verify_wgs = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
   CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
+  CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_out_s, hipStreamNonBlocking));
   preload_fetch_kernels();
   CREATE_HIP(hipStreamCreateWithFlags(&e->copy_s, hipStreamNonBlocking));
   CREATE_HIP(hipEventCreateWithFlags(&e->ev_main, hipEventDisableTiming));
@@ -651,6 +654,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_k, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&f.ev_in, hipEventDisableTiming));
   }
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
@@ -1293,7 +1297,7 @@ int fetch_alloc(void** p, size_t bytes) {
   return RMQ_OK;
 }
 
-int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
+int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage, hipStream_t e_fetch_s) {
   if (n > f.cap) {
     void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum};
     for (void* p : ds)
@@ -1308,8 +1312,13 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage) {
     if (!rc) rc = fetch_alloc((void**)&f.d_res, ((size_t)cap * 4 + 2) * 8);
     if (!rc) rc = fetch_alloc((void**)&f.d_aux, (size_t)cap * 16);
     if (!rc) rc = fetch_alloc((void**)&f.d_cpre, ((size_t)cap + 4) * 4);
-    if (!rc) rc = fetch_alloc((void**)&f.d_csum, ((size_t)cap / kFetchChunk + 2) * kCsumStride * 8);
+    const uint32_t lines = cap / kFetchChunk + 2;
+    if (!rc) rc = fetch_alloc((void**)&f.d_csum, 2ull * lines * kCsumStride * 8);
     if (rc) return rc;
+    // both halves start zeroed (stream-ordered before the slot's first fetch)
+    HIP_TRY(hipMemsetAsync(f.d_csum, 0, 2ull * lines * kCsumStride * 8, e_fetch_s));
+    f.csum_lines = lines;
+    f.csum_par = 0;
     HIP_TRY(hipHostMalloc((void**)&f.h_req, (size_t)cap * 16, 0));
     HIP_TRY(hipHostMalloc((void**)&f.h_res, ((size_t)cap * 4 + 2) * 8, 0));  // res, bytes needed
     f.cap = cap;
@@ -1339,7 +1348,7 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
     }
     // the device writes rmq_fetch_res rows (status zero-extended into its reserved word)
     static_assert(sizeof(rmq_fetch_res) == 32, "result rows are four words");
-    std::memcpy(f.res, f.h_res, (size_t)f.n * 32);
+    if (!f.rows_pinned) std::memcpy(f.res, f.h_res, (size_t)f.n * 32);  // (pinned: DMA'd in place)
     int rc_all = RMQ_OK;
     for (uint32_t r = 0; r < f.n; ++r)
       if (f.res[r].status == RMQ_ENOSPC) {
@@ -1358,11 +1367,11 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
           hi += f.res[r].bytes;
           continue;
         }
-        if (hi > lo) HIP_TRY(hipMemcpyAsync(f.out + lo, f.d_out + lo, hi - lo, hipMemcpyDeviceToHost, e->fetch_s));
+        if (hi > lo) HIP_TRY(hipMemcpyAsync(f.out + lo, f.d_out + lo, hi - lo, hipMemcpyDeviceToHost, e->fetch_out_s));
         lo = hi = served ? f.res[r].out_pos : 0;
         if (served) hi += f.res[r].bytes;
       }
-      HIP_TRY(hipEventRecord(f.ev_copy, e->fetch_s));
+      HIP_TRY(hipEventRecord(f.ev_copy, e->fetch_out_s));
     } else {
       f.phase = 3;  // nothing to copy
     }
@@ -1387,6 +1396,8 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
 int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
                     uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
   if (!e || !ticket) return RMQ_EINVAL;
+  const bool rows_pinned = (mem & RMQ_FETCH_PINNED_ROWS) != 0;
+  mem &= ~RMQ_FETCH_PINNED_ROWS;
   if ((n && (!reqs || !res)) || (mem != RMQ_MEM_HOST && mem != RMQ_MEM_DEVICE)) return RMQ_EINVAL;
   if (out_cap && !out) return RMQ_EINVAL;
   if (mem == RMQ_MEM_DEVICE && (reinterpret_cast<uintptr_t>(out) & 15u)) return RMQ_EINVAL;
@@ -1434,10 +1445,10 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     *ticket = tk;
     return RMQ_OK;
   }
-  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0);
+  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0, e->fetch_s);
   if (rc) return rc;
   uint8_t* d_out = mem == RMQ_MEM_HOST ? (out_cap ? f.d_out : nullptr) : out;
-  std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
+  if (!rows_pinned) std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
   {
     // Order against the append pipeline without flushing it: the fetch reads the committed state
     // after the last launch issued so far, and the next launch waits for the fetch, so no ring
@@ -1449,15 +1460,19 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     a.res = f.d_res;
     a.aux = f.d_aux;
     a.cpre = f.d_cpre;
-    a.csum = f.d_csum;
+    a.csum_lines = f.csum_lines;
     a.out = d_out;
     a.out_cap = out_cap;
     a.n = n;
-    // the requests' copy first (it depends on nothing the pipeline writes: it overlaps the running
-    // launch), then the kernels behind the launches issued so far
-    HIP_TRY(hipMemcpyAsync(f.d_req, f.h_req, (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->fetch_s));
+    // the requests' copy on the copy stream (it depends on nothing the pipeline or an earlier fetch
+    // writes: it overlaps the running launch and fetch), then the kernels behind the launches
+    // issued so far and the copy
+    HIP_TRY(hipMemcpyAsync(f.d_req, rows_pinned ? static_cast<const void*>(reqs) : f.h_req,
+                           (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->copy_s));
+    HIP_TRY(hipEventRecord(f.ev_in, e->copy_s));
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
+    HIP_TRY(hipStreamWaitEvent(e->fetch_s, f.ev_in, 0));
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     const uint32_t runs = e->profile ? e->fetch_replay : 1u;
     if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run, copies outside
@@ -1470,6 +1485,10 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
       HIP_TRY(hipEventRecord(r0, e->fetch_s));
     }
     for (uint32_t k = 0; k < runs; ++k) {
+      const size_t half = (size_t)f.csum_lines * kCsumStride;
+      a.csum = f.d_csum + half * f.csum_par;
+      a.csum_next = f.d_csum + half * (f.csum_par ^ 1u);
+      f.csum_par ^= 1u;
       launch_fetch(a, e->fetch_s, e->profile && k == 0 ? ev : nullptr);
       HIP_TRY(hipGetLastError());
     }
@@ -1477,9 +1496,17 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     // the next launch waits for the kernels only (not for the result copy to the host)
     HIP_TRY(hipEventRecord(f.ev_k, e->fetch_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_k, 0));
-    HIP_TRY(hipMemcpyAsync(f.h_res, f.d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_s));
-    HIP_TRY(hipEventRecord(f.ev, e->fetch_s));
+    // the result rows on their own stream: the next fetch's kernels do not wait for this copy
+    HIP_TRY(hipStreamWaitEvent(e->fetch_out_s, f.ev_k, 0));
+    if (rows_pinned) {
+      HIP_TRY(hipMemcpyAsync(res, f.d_res, (size_t)n * 32, hipMemcpyDeviceToHost, e->fetch_out_s));
+      HIP_TRY(hipMemcpyAsync(f.h_res + 4ull * n, f.d_res + 4ull * n, 16, hipMemcpyDeviceToHost, e->fetch_out_s));
+    } else {
+      HIP_TRY(hipMemcpyAsync(f.h_res, f.d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_out_s));
+    }
+    HIP_TRY(hipEventRecord(f.ev, e->fetch_out_s));
   }
+  f.rows_pinned = rows_pinned;
   f.ticket = tk;
   f.phase = 1;
   f.rc = RMQ_OK;

@@ -180,7 +180,9 @@ struct Replication {
   uint32_t* d_acc = nullptr;     // [n_in]
   uint64_t* d_base = nullptr;    // [n_in][2] IngestArgs::base
   uint32_t* d_items = nullptr;   // [items_cap][2] follower copy work items
-  uint32_t* d_nitems = nullptr;  // [1 + kMaxWorld]: copy items allocated, structural flag per source
+  uint32_t* d_nitems = nullptr;  // [2][1 + kMaxWorld]: copy items allocated, structural flag per source;
+                                 // rounds alternate halves, each round's prepare clears the other
+  uint32_t nitems_par = 0;
   uint64_t* d_counters = nullptr;  // [7]: follower [0..4) (IngestArgs), leader [4..7) (XPlanArgs)
   uint64_t* d_lastg = nullptr;     // [P] record bytes / 16 of the last group applied (PipeArgs::lastg)
   // leader catch-up state per out entry (FORMAT.md §9 v3)
@@ -310,7 +312,9 @@ struct rmq_engine {
   // the fetch is ordered against the pipeline stream)
   std::mutex fetch_mu;
   hipStream_t fetch_s = nullptr;
-  hipStream_t copy_s = nullptr;  // host batches: pinned -> device DMA
+  hipStream_t fetch_out_s = nullptr;  // fetch results (and host outputs) -> host, after the kernels:
+                                      // a fetch's result copy overlaps the next fetch's kernels
+  hipStream_t copy_s = nullptr;  // host batches and fetch requests: pinned -> device DMA
   hipEvent_t ev_main = nullptr;
   bool trace = false;           // RMQ_TRACE: print every launch's roles to stderr
   // fetches in flight (rmq_fetch_async), each with its own scratch: a fetch is ordered after the
@@ -322,7 +326,10 @@ struct rmq_engine {
     uint64_t* d_res = nullptr;
     uint64_t* d_aux = nullptr;
     uint32_t* d_cpre = nullptr;
-    uint64_t* d_csum = nullptr;
+    uint64_t* d_csum = nullptr;   // two halves of csum_lines lines: a fetch adds into one, its gather
+                                  // zeroes the other for the next fetch of the slot (same stream)
+    uint32_t csum_lines = 0;
+    uint32_t csum_par = 0;
     uint32_t* h_req = nullptr;   // pinned
     uint64_t* h_res = nullptr;   // pinned [cap][4] + {bytes needed, 0}
     uint32_t cap = 0;
@@ -331,6 +338,8 @@ struct rmq_engine {
     hipEvent_t ev = nullptr;     // kernels and the result copy done
     hipEvent_t ev_copy = nullptr;  // host output copies done
     hipEvent_t ev_k = nullptr;     // its kernels done (the pipeline stream waits for this one)
+    hipEvent_t ev_in = nullptr;    // its requests on the device (copy stream)
+    bool rows_pinned = false;      // RMQ_FETCH_PINNED_ROWS: the caller's rows are DMA'd directly
     // the fetch in flight: ticket 0 = idle; phase 1: kernels, 2: host output copies
     uint64_t ticket = 0;
     int phase = 0;

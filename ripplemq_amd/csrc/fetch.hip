@@ -245,6 +245,8 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   const DevState& st = a.st;
   const u32 tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const u32 r0 = blockIdx.x * kGR, c0 = r0 / kFetchChunk;
+  // the next fetch's chunk sums (its resolve runs after this kernel on the same stream)
+  for (u32 k = blockIdx.x * 64 * kFW + tid; k < a.csum_lines; k += gridDim.x * 64 * kFW) a.csum_next[(u64)k * kCsumStride] = 0;
   // bytes of every request before r0: the chunk sums before its chunk, then its chunk's requests
   u64 v = 0;
   for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[(u64)k * kCsumStride];
@@ -369,7 +371,6 @@ void preload_fetch_kernels() {
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
-  (void)hipMemsetAsync(a.csum, 0, 8ull * kCsumStride * (a.n / kFetchChunk + 1), s);
   hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW * kRPW - 1) / (kFW * kRPW)), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);
   hipExtLaunchKernelGGL(fetch_gather_kernel, dim3((a.n + kGR - 1) / kGR), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,

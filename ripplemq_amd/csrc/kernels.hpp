@@ -275,11 +275,13 @@ struct FetchArgs {
   uint64_t* csum;            // [n / kFetchChunk + 1][kCsumStride] bytes of each chunk of kFetchChunk
                              //   requests (one 128-byte line per chunk: the adds of different
                              //   chunks never meet in one L2 line)
-                             //   (resolve adds, zeroed before it)
+                             //   (resolve adds; zeroed by the previous fetch of the slot)
+  uint64_t* csum_next;       // the slot's other chunk-sum half, which the gather zeroes for the next
+                             //   fetch (word 0 of csum_lines lines; no memset between the fetches)
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
   uint32_t n;
-  uint32_t pad;
+  uint32_t csum_lines;
 };
 constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
 constexpr uint32_t kCsumStride = 16;   // u64 words per chunk sum (128 bytes)
@@ -323,9 +325,11 @@ struct IngestArgs {
                              // the follower's, or the leader's first offset after a truncation
   uint64_t* ackout;          // [n_in][2] follower log end after the round | status (FORMAT.md §9)
   uint32_t* items;           // [cap][2] copy work items {entry, chunk of kCopyChunk bytes} (prepare)
-  uint32_t* n_items;         // [1] items allocated this round (prepare adds, the host clears)
+  uint32_t* n_items;         // [1] items allocated this round (prepare adds; zero at the start)
   uint32_t* insane;          // [kMaxWorld] a structural fault of that source's region (prepare and
-                             //   verify set it, the host clears it with n_items)
+                             //   verify set it; zero at the start)
+  uint32_t* n_items_next;    // the next round's n_items and insane words: prepare clears them (no
+                             //   memset node between the rounds)
   const uint64_t* keysum_in; // [world] FORMAT.md §9 key sum of each source's entry list (this side's)
   uint32_t items_cap;        // slots of `items`
   uint32_t items_grid;       // copy workgroups launched: items past it are never copied
@@ -379,6 +383,7 @@ void preload_fetch_kernels();
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_row_quorum_all(const DevState& st, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);
+uint32_t verify_wgs_per_cu();
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
 // chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))
 void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s);

@@ -36,6 +36,14 @@ namespace rmq {
 constexpr u32 kIT = 512;           // threads per verify workgroup
 constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
 constexpr u32 kIR = 32;            // records per task
+#ifndef RMQ_VSPEC
+#define RMQ_VSPEC 2
+#endif
+#ifndef RMQ_VERIFY_WAVES
+#define RMQ_VERIFY_WAVES 8
+#endif
+constexpr u32 kVSpec = RMQ_VSPEC;    // pieces per lane loaded with the table slot (0..4)
+static_assert(kVSpec <= 4, "at most four speculative pieces per lane");
 constexpr u32 kBigIngest = 64;     // records over this many 16-byte pieces: the whole wave
 constexpr u32 kCT = 64;            // threads per copy workgroup (one wave: many items resident per CU)
 
@@ -163,6 +171,9 @@ __device__ __forceinline__ void mark_insane(const IngestArgs& A, u32 src) {
 __global__ void ingest_prepare_kernel(IngestArgs A) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = e < A.n_in;
+  // the next round's counters (the round before used them; its kernels ran before this one)
+  static_assert(1 + kMaxWorld <= 256, "one workgroup clears them");
+  if (blockIdx.x == 0 && threadIdx.x < 1 + kMaxWorld) A.n_items_next[threadIdx.x] = 0u;
   u32 nc = 0;  // copy work items of the entry
   if (in) {
     const u32 src = source_of_entry(A, e), k = e - A.xi_start[src];
@@ -260,11 +271,23 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   bool ok = false, owner = false, reb = false;
   const uint8_t* rec = R.base;
   uint4 hdr = make_uint4(0, 0, 0, 0);
+  // the header and this lane's first four pieces are loaded with the directory entry, from the
+  // table slot alone (inside the data section; used only once the checks below pass): one round
+  // trip instead of three (directory, then header, then payload)
+  uint4 sp0 = make_uint4(0, 0, 0, 0), sp1 = sp0, sp2 = sp0, sp3 = sp0;
   if (in) {
     const u64* tabp = reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries) + i;
     const u64 tab = tabp[0];
     const u64 tabn = i + 1u < R.n_records ? tabp[1] : 0ull;  // the next slot (the record after, if any)
     const u32 k = min((u32)tab, R.n_entries - 1u), d16 = (u32)(tab >> 32);  // ok below requires k == tab
+    rec = R.base + R.data_off + 16ull * d16;
+    const u64 dsz16 = (R.rows_off - R.data_off) >> 4;  // pieces in the data section
+    uint4 sh = make_uint4(0, 0, 0, 0);
+    if ((u64)d16 + 1ull <= dsz16) sh = *reinterpret_cast<const uint4*>(rec);
+    if (kVSpec > 0 && (u64)d16 + 2ull + j <= dsz16) sp0 = *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * j);
+    if (kVSpec > 1 && (u64)d16 + 4ull + j <= dsz16) sp1 = *reinterpret_cast<const uint4*>(rec + 48ull + 16ull * j);
+    if (kVSpec > 2 && (u64)d16 + 6ull + j <= dsz16) sp2 = *reinterpret_cast<const uint4*>(rec + 80ull + 16ull * j);
+    if (kVSpec > 3 && (u64)d16 + 8ull + j <= dsz16) sp3 = *reinterpret_cast<const uint4*>(rec + 112ull + 16ull * j);
     const DirView d = dir_of(R, k);
     // structure: the slot lies in the range of the entry it names (prepare checked that the ranges
     // tile the table)
@@ -275,10 +298,9 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
     owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
     reb = d.rebase;
     const u64 used = A.base[2 * e + 1];   // after a truncation: at the leader's first offset
-    rec = R.base + R.data_off + 16ull * d16;
     const u64 rel = 16ull * (u64)(d16 - d.dstart16);
-    if (k == (u32)tab && d16 >= d.dstart16 && R.data_off + 16ull * d16 + 16ull <= R.rows_off) {
-      hdr = *reinterpret_cast<const uint4*>(rec);
+    if (k == (u32)tab && d16 >= d.dstart16 && (u64)d16 + 1ull <= dsz16) {
+      hdr = sh;
       off = ((u64)hdr.y << 32) | hdr.x;
       L = hdr.z;
       m = (L + 15u) >> 4;
@@ -302,7 +324,19 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   const bool big = ok && m > kBigIngest;
   const u32 mm = ok && !big ? m : 0u;
   u32 acc = 0;
-  for (u32 c = 0; __any(c < (mm + 1u) / 2u); c += 4) {
+  {  // pieces j, j + 2, ...: the speculative loads (inside the record once ok)
+    const uint4 sv[4] = {sp0, sp1, sp2, sp3};
+#pragma unroll
+    for (u32 u = 0; u < kVSpec; ++u) {
+      const u32 jp = 2u * u + j;
+      if (jp < mm) {
+        uint4 w = sv[u];
+        if (jp == 0) w.x ^= 0xFFFFFFFFu;
+        acc = crc_zshift(z32, acc) ^ crc_piece16(t8, w);
+      }
+    }
+  }
+  for (u32 c = kVSpec; __any(c < (mm + 1u) / 2u); c += 4) {
     uint4 v[4];
 #pragma unroll
     for (u32 u = 0; u < 4; ++u) {  // four pieces in flight per lane
@@ -393,7 +427,7 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
 // A grid of at most a few workgroups per CU: each copies the CRC tables into LDS once and its waves
 // take tasks w, w + waves, ... (the tables were 20 KB per 32 records' worth of workgroup before;
 // the 16-byte shift is a multiply, the 1 KB one of large records is read from global memory).
-__global__ __launch_bounds__(kIT, 8) void ingest_verify_kernel(IngestArgs A) {
+__global__ __launch_bounds__(kIT, RMQ_VERIFY_WAVES) void ingest_verify_kernel(IngestArgs A) {
   __shared__ __attribute__((aligned(16))) u32 t8[8][256];
   __shared__ __attribute__((aligned(16))) u32 z32[4][256];  // register shift past 32 zero bytes
   {
@@ -603,6 +637,9 @@ void launch_notice_fill(const NoticeArgs& a, hipStream_t s) {
 void launch_notice_apply(const NoticeArgs& a, hipStream_t s) {
   if (a.n_in) hipLaunchKernelGGL(notice_apply_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
 }
+
+// resident verify workgroups per CU at the kernel's launch bounds (the default verify grid)
+uint32_t verify_wgs_per_cu() { return RMQ_VERIFY_WAVES * 4u / kIW; }
 
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s) {
   if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);

@@ -178,15 +178,20 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.base = r->d_base;
   a.ackout = x.ackout;
   a.items = r->d_items;
-  a.n_items = r->d_nitems;
-  a.insane = r->d_nitems + 1;
+  {
+    constexpr uint32_t NW = 1 + kMaxWorld;
+    uint32_t* cur = r->d_nitems + (r->nitems_par ? NW : 0u);
+    a.n_items = cur;
+    a.insane = cur + 1;
+    a.n_items_next = r->d_nitems + (r->nitems_par ? 0u : NW);
+  }
   a.keysum_in = r->d_keysum_in;
   a.items_cap = (uint32_t)r->items_cap;
   a.items_grid = items;
   a.crc = e->d_crc;
   a.counters = r->d_counters;
-  HIP_TRY(hipMemsetAsync(r->d_nitems, 0, 4ull * (1 + kMaxWorld), r->xchg_s));  // items, structural flags
   launch_ingest(a, tasks, items, e->verify_wgs, r->xchg_s);
+  if (a.n_in) r->nitems_par ^= 1u;  // (prepare ran: it cleared the other half)
   HIP_TRY(hipGetLastError());
   // acks: {log end | status, position} of every in entry back to its leader, fixed sizes both ways
   for (uint32_t q = 0; q < W; ++q) {
@@ -414,7 +419,8 @@ int repl_set_lists(rmq_engine* e) {
   r->d_items = nullptr;
   r->d_nitems = nullptr;
   rc = dalloc(&r->d_items, 2 * r->items_cap);
-  if (!rc) rc = dalloc(&r->d_nitems, 1 + kMaxWorld);
+  if (!rc) rc = dalloc(&r->d_nitems, 2 * (1 + kMaxWorld));  // both halves zero
+  r->nitems_par = 0;
   if (rc) return rc;
   free_set_buffers(r);
   for (XchgSet& x : r->sets) {

@@ -338,14 +338,18 @@ class Engine:
 
     def fetch_async(self, pidx, consumer, max_records, d_out: int | None = None, out_cap: int = 0,
                     out: np.ndarray | None = None, req: np.ndarray | None = None,
-                    res: np.ndarray | None = None) -> "FetchTicket":
+                    res: np.ndarray | None = None, pinned_rows: bool = False) -> "FetchTicket":
         """rmq_fetch_async into a device buffer (d_out, 16-byte aligned) or a host array (out): the
         call returns at once; fetch_poll(ticket) gives (rc, res, bytes_used) once it completes. The
         handle keeps the request, result and output arrays alive until then. req ([n, 4] uint32)
         and res (FETCH_RES_DTYPE[n]) may be a caller's arrays reused from call to call; with req
         given, pidx / consumer / max_records None leave those columns as they are (column 3: the
-        requests' flags, RMQ_FETCH_COMMIT)."""
+        requests' flags, RMQ_FETCH_COMMIT). pinned_rows: req and res are page-locked (fetch_rows)
+        and go to and from the device by DMA alone (RMQ_FETCH_PINNED_ROWS); req then stays
+        unchanged until the ticket completes."""
         n = len(pidx) if pidx is not None else len(req)
+        if pinned_rows and (req is None or res is None):
+            raise ValueError("pinned_rows needs the caller's page-locked req and res (fetch_rows)")
         if req is None:
             req = np.empty((n, 4), np.uint32)
             req[:, 3] = 0
@@ -359,10 +363,19 @@ class Engine:
         else:
             out_cap = 0 if out is None else min(int(out_cap) or out.size, out.size)
             mem, ptr = A.RMQ_MEM_HOST, (_ptr(out) if out is not None else None)
+        if pinned_rows:
+            mem |= A.RMQ_FETCH_PINNED_ROWS
         t = C.c_uint64()
         _check(self.lib.rmq_fetch_async(self.h, _ptr(req), n, mem, ptr, out_cap, _ptr(res), C.byref(t)),
                "rmq_fetch_async")
         return FetchTicket(t.value, req, res, out)
+
+    def fetch_rows(self, n: int):
+        """A page-locked request array ([n, 4] uint32, zeroed) and result array (FETCH_RES_DTYPE[n])
+        for fetch_async(..., pinned_rows=True); freed with the engine or by host_release."""
+        req = self.host_empty(4 * n, np.uint32).reshape(n, 4)
+        req[:] = 0
+        return req, self.host_empty(n, FETCH_RES_DTYPE)
 
     def fetch_poll(self, tk: "FetchTicket", wait: bool = False):
         """(rc, res, bytes_used) of an rmq_fetch_async ticket, or None while it runs."""

@@ -151,3 +151,58 @@ def test_fetch_commit_matches_oracle(oracle_mod):
             dev.fetch(np.zeros(2, np.uint32), np.zeros(2, np.uint32), np.full(2, 5, np.uint32), out_cap=1 << 16,
                       commit=True)
         assert ei.value.status == A.RMQ_EINVAL
+
+
+def test_pinned_rows_match_sync():
+    """RMQ_FETCH_PINNED_ROWS (ABI 7): requests and result rows in page-locked arrays go by DMA alone;
+    six fetches in flight (more than the four slots), host and device outputs, one output cut
+    mid-way (ENOSPC): every result equals a synchronous fetch of the same requests issued right
+    after it, and sizes change from call to call through the same slots (the chunk sums a gather
+    zeroes for its slot's next fetch)."""
+    P, C = 256, 2
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=C, max_batch_records=8192)
+    spec = StreamSpec(P, 6000, "zipf", size=(1, 400), config_index=47)
+    g = np.random.default_rng(11)
+    with Engine(cfg) as dev:
+        for b in range(6):
+            bt = make_batch(spec, b)
+            dev.append_async(bt.pidx, bt.lens, bt.payload)
+        pending, cap_of = [], []
+        for k in range(6):
+            n = [P * C, 5, P * C, 77, 1, P * C][k]
+            req, res = dev.fetch_rows(n)
+            req[:, 0] = g.integers(0, P + 3, n)
+            req[:, 1] = g.integers(0, C, n)
+            req[:, 2] = g.integers(0, 2000, n)
+            cap = 1 << 16 if k == 2 else 8 << 20
+            cap_of.append(cap)
+            if k % 2:
+                out = np.zeros(cap, np.uint8)
+                tk = dev.fetch_async(None, None, None, out=out, out_cap=cap, req=req, res=res, pinned_rows=True)
+                d_out = None
+            else:
+                d_out = dev.device_alloc(cap)
+                tk = dev.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=req, res=res, pinned_rows=True)
+            rc_w, want, wbuf, used_w = dev.fetch(req[:, 0].copy(), req[:, 1].copy(), req[:, 2].copy(), out_cap=cap)
+            pending.append((tk, rc_w, want.copy(), wbuf.copy(), used_w, d_out))
+        for k, (tk, rc_w, want, wbuf, used_w, d_out) in enumerate(pending):
+            rc, res, used = dev.fetch_poll(tk, wait=True)
+            assert rc == rc_w, k
+            for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                assert np.array_equal(res[f], want[f]), (k, f)
+            assert used == used_w, k
+            served = (res["status"] == 0) & (res["bytes"] > 0)
+            if d_out is None:
+                got = tk.out
+            else:
+                n_cp = min(used, cap_of[k])  # (bytes needed can exceed the output after a cut)
+                got = np.empty(max(n_cp, 1), np.uint8)
+                if n_cp:
+                    dev.d2h(got[:n_cp], d_out)
+                dev.device_free(d_out)
+            for r in np.flatnonzero(served):
+                a, b = int(res["out_pos"][r]), int(res["out_pos"][r] + res["bytes"][r])
+                assert np.array_equal(got[a:b], wbuf[a:b]), (k, r)
+        assert pending[2][1] == A.RMQ_ENOSPC
+        dev.sync()

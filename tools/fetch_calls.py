@@ -53,6 +53,20 @@ def main():
                                                                             req=req, res=res), wait=True))
     out["fetch_async_issue_us"] = tm(lambda: eng.fetch_poll(eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap,
                                                                              req=req, res=res), wait=True), 3)
+    prq, prs = eng.fetch_rows(P * C)
+    prq[:] = req
+    out["fetch_pinned_sync_us"] = tm(lambda: eng.fetch_poll(eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap,
+                                                                             req=prq, res=prs, pinned_rows=True), wait=True))
+    rows = [eng.fetch_rows(P * C) for _ in range(8)]
+    for rq, _ in rows:
+        rq[:] = req
+
+    def burst():
+        tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rq, res=rs, pinned_rows=True)
+               for rq, rs in rows]
+        for t in tks:
+            eng.fetch_poll(t, wait=True)
+    out["fetch_pinned_burst8_us_per_call"] = [round(x / 8, 1) for x in tm(burst, 5)]
     eng.device_free(d_out)
     eng.close()
     print(json.dumps(out))

@@ -19,6 +19,7 @@
 #   pmc        rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) of a 300-step line
 #   stamps     per-wave phase stamps of launch 100 (RMQ_STAMPS) + timing-only RMQ_DEBUG lines
 #   legs       fetch / mixed / tier legs of a short line
+#   calls      host-side cost per fetch call (tools/fetch_calls.py)
 #   fetchkt    rocprofv3 kernel trace of the fetch leg (replayed kernels)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -89,6 +90,7 @@ for step in "$@"; do
       done ;;
     legs)  # the side legs (fetch, mixed, tier) on a short line
       run 300 "${T}_legs.json" python bench.py --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0 ;;
+    calls) run 200 "${T}_calls.json" python tools/fetch_calls.py ;;
     fetchkt)  # kernel trace of the fetch leg alone (its kernels replayed back to back, bench.py REPLAY)
       prof 200 fetchkt --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_fetchkt" -o kt -- python3 "$R/bench.py" --steps 20 --warmup 5 --fetch-rounds 10 --concurrent-rounds 0 --tier-rounds 0 --no-cpu-baseline --host-steps 0 ;;
     fetchprof|fetchprof:*)  # kernel trace of the fetch legs (short append run), current library and variants/NAME
