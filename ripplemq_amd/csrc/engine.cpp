@@ -499,6 +499,7 @@ void free_engine(rmq_engine* e) {
   for (void* p : bufs)
     if (p) hipFree(p);
   if (e->done_host) hipHostFree(e->done_host);
+  if (e->fetch_need_host) hipHostFree(e->fetch_need_host);
   for (auto& cs : e->cslot) {
     if (cs.h) hipHostFree(cs.h);
     if (cs.d) hipFree(cs.d);
@@ -729,6 +730,12 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   }
   if (e->stamps_path) CREATE_TRY(dalloc(&e->d_stamps, (size_t)(2u * e->cu_count + kMaxTiles + (P + kPipeThreads - 1) / kPipeThreads +
                                                        kMaxTiles * kTileRecs / (kTaskRecs * kPipeThreads / 64)) * 64));
+  CREATE_HIP(hipHostMalloc((void**)&e->fetch_need_host, 8 * rmq_engine::kFetchSlots, hipHostMallocCoherent | hipHostMallocMapped));
+  for (uint32_t k = 0; k < rmq_engine::kFetchSlots; ++k) {
+    e->fslot[k].need = e->fetch_need_host + k;
+    *e->fslot[k].need = 0;
+    CREATE_HIP(hipHostGetDevicePointer((void**)&e->fslot[k].need_dev, e->fslot[k].need, 0));
+  }
   CREATE_HIP(hipHostMalloc((void**)&e->done_host, 64, hipHostMallocCoherent | hipHostMallocMapped));
   e->done_host[0] = e->done_host[1] = 0;
   CREATE_HIP(hipHostGetDevicePointer((void**)&e->done_dev, e->done_host, 0));
@@ -1349,13 +1356,9 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
     // the device writes rmq_fetch_res rows (status zero-extended into its reserved word)
     static_assert(sizeof(rmq_fetch_res) == 32, "result rows are four words");
     if (!f.rows_pinned) std::memcpy(f.res, f.h_res, (size_t)f.n * 32);  // (pinned: DMA'd in place)
-    int rc_all = RMQ_OK;
-    for (uint32_t r = 0; r < f.n; ++r)
-      if (f.res[r].status == RMQ_ENOSPC) {
-        rc_all = RMQ_ENOSPC;
-        break;
-      }
-    f.rc = rc_all;
+    // some request did not fit iff the bytes needed exceed the output (requests are placed in
+    // order: the one holding byte out_cap is cut), so no pass over the rows
+    f.rc = __atomic_load_n(f.need, __ATOMIC_ACQUIRE) > f.out_cap ? RMQ_ENOSPC : RMQ_OK;
     f.phase = 2;
     if (f.mem == RMQ_MEM_HOST && f.out_cap) {
       // copy back the byte runs of the served requests only: the regions of requests that did not
@@ -1385,7 +1388,7 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
       HIP_TRY(q);
     }
   }
-  if (bytes_used) *bytes_used = f.h_res[(size_t)f.n * 4];
+  if (bytes_used) *bytes_used = __atomic_load_n(f.need, __ATOMIC_ACQUIRE);
   f.phase = 0;
   f.ticket = 0;
   return f.rc;
@@ -1463,6 +1466,7 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     a.csum_lines = f.csum_lines;
     a.out = d_out;
     a.out_cap = out_cap;
+    a.need_host = f.need_dev;
     a.n = n;
     // the requests' copy on the copy stream (it depends on nothing the pipeline or an earlier fetch
     // writes: it overlaps the running launch and fetch), then the kernels behind the launches
@@ -1498,12 +1502,9 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_k, 0));
     // the result rows on their own stream: the next fetch's kernels do not wait for this copy
     HIP_TRY(hipStreamWaitEvent(e->fetch_out_s, f.ev_k, 0));
-    if (rows_pinned) {
-      HIP_TRY(hipMemcpyAsync(res, f.d_res, (size_t)n * 32, hipMemcpyDeviceToHost, e->fetch_out_s));
-      HIP_TRY(hipMemcpyAsync(f.h_res + 4ull * n, f.d_res + 4ull * n, 16, hipMemcpyDeviceToHost, e->fetch_out_s));
-    } else {
-      HIP_TRY(hipMemcpyAsync(f.h_res, f.d_res, (size_t)n * 32 + 16, hipMemcpyDeviceToHost, e->fetch_out_s));
-    }
+    // (the bytes needed reach the host by the gather's own store into f.need)
+    HIP_TRY(hipMemcpyAsync(rows_pinned ? static_cast<void*>(res) : static_cast<void*>(f.h_res), f.d_res, (size_t)n * 32,
+                           hipMemcpyDeviceToHost, e->fetch_out_s));
     HIP_TRY(hipEventRecord(f.ev, e->fetch_out_s));
   }
   f.rows_pinned = rows_pinned;

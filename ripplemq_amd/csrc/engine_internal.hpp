@@ -340,6 +340,8 @@ struct rmq_engine {
     hipEvent_t ev_k = nullptr;     // its kernels done (the pipeline stream waits for this one)
     hipEvent_t ev_in = nullptr;    // its requests on the device (copy stream)
     bool rows_pinned = false;      // RMQ_FETCH_PINNED_ROWS: the caller's rows are DMA'd directly
+    uint64_t* need = nullptr;      // bytes needed: a word of fetch_need_host (the gather stores it)
+    uint64_t* need_dev = nullptr;  // its device address
     // the fetch in flight: ticket 0 = idle; phase 1: kernels, 2: host output copies
     uint64_t ticket = 0;
     int phase = 0;
@@ -352,6 +354,7 @@ struct rmq_engine {
   static constexpr uint32_t kFetchSlots = 4;
   FetchSlot fslot[kFetchSlots];
   uint32_t fslot_next = 0;
+  uint64_t* fetch_need_host = nullptr;  // [kFetchSlots] coherent pinned words (FetchSlot::need)
   uint64_t fetch_seq = 0;        // tickets
   std::vector<uint32_t> fetch_stamp;  // RMQ_FETCH_COMMIT duplicate check ([P][C] generation stamps)
   uint32_t fetch_gen = 0;

@@ -268,7 +268,10 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
       a.res[4 * rr + 2] = 0;
       a.res[4 * rr + 3] = (u64)(uint32_t)kNoSpc;
     }
-    if (rr + 1 == a.n) a.res[4ull * a.n] = pos + nb;  // bytes needed
+    if (rr + 1 == a.n) {  // bytes needed
+      a.res[4ull * a.n] = pos + nb;
+      __hip_atomic_store(a.need_host, pos + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     // RMQ_FETCH_COMMIT: the consumer's next offset once its records are in the output (or the
     // first retained offset after RMQ_EOFFSET); every request's offset was read by the resolve
     // kernel before (the host refuses two committing requests for one consumer in a call)

@@ -280,6 +280,8 @@ struct FetchArgs {
                              //   fetch (word 0 of csum_lines lines; no memset between the fetches)
   uint8_t* out;              // 16-byte aligned
   uint64_t out_cap;
+  uint64_t* need_host;       // host-visible word (coherent pinned): bytes needed, written by the
+                             //   gather with a system-scope store (no copy node for it)
   uint32_t n;
   uint32_t csum_lines;
 };

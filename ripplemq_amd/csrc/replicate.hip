@@ -445,9 +445,9 @@ __global__ __launch_bounds__(kIT, RMQ_VERIFY_WAVES) void ingest_verify_kernel(In
     verify_task(A, t8, z32, task);
 }
 
-__global__ void ingest_finish_kernel(IngestArgs A) {
-  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= A.n_in) return;
+// The verdict and state of entry e (thread per entry); its records and bytes ingested are added
+// to n_rec / n_bytes (the kernel sums them over the wave: one atomic per wave, not per entry).
+__device__ __forceinline__ void finish_entry(const IngestArgs& A, u32 e, u64& n_rec, u64& n_bytes) {
   const u32 src = source_of_entry(A, e);
   const DevState& st = A.st;
   const u32 p = A.xi_p[e], k = e - A.xi_start[src];
@@ -533,7 +533,7 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
         st.start_off[p] = ie[0];
         st.start_pos[p] = ie[1];
       }
-      atomicAdd((unsigned long long*)&A.counters[3], 16ull * d.bytes16);
+      n_bytes += 16ull * d.bytes16;
     }
     if (R.M) {  // the partition's consumer-offset row, if the round carries one (rows ascend by entry)
       const u64 rowb = 16ull + 8ull * A.C;
@@ -549,9 +549,24 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
       }
     }
   }
-  if (d.count) atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)d.count);
+  n_rec += d.count;
   A.ackout[2 * e] = nleo;
   A.ackout[2 * e + 1] = nused;
+}
+
+__global__ void ingest_finish_kernel(IngestArgs A) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  u64 n_rec = 0, n_bytes = 0;
+  if (e < A.n_in) finish_entry(A, e, n_rec, n_bytes);
+  // every lane of the wave is back here (blockDim is a multiple of 64)
+  for (int o = 32; o; o >>= 1) {
+    n_rec += __shfl_xor(n_rec, o, 64);
+    n_bytes += __shfl_xor(n_bytes, o, 64);
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    if (n_rec) atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)n_rec);
+    if (n_bytes) atomicAdd((unsigned long long*)&A.counters[3], (unsigned long long)n_bytes);
+  }
 }
 
 // Accepted entries' record bytes into the follower's replica rings: workgroup per work item

@@ -1,4 +1,4 @@
-"""rmq_fetch_async / rmq_fetch_poll (ABI 6) and the single-pass fetch kernel.
+"""rmq_fetch_async / rmq_fetch_poll (ABI 6), page-locked rows (ABI 7) and the fetch kernels.
 
 An asynchronous fetch is ordered exactly like rmq_fetch (after every launch issued before it,
 before the ones issued after it), so its result must equal a synchronous fetch issued right after
