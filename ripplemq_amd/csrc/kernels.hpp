@@ -386,6 +386,7 @@ void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_row_quorum_all(const DevState& st, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);
 uint32_t verify_wgs_per_cu();
+uint32_t verify_records_per_task();  // the host sizes the verify tasks with it
 constexpr uint64_t kMigrateChunk = 256ull << 10;  // new-ring bytes per workgroup of a move
 // chunks = total workgroups (sum over the items of ceil(new ring bytes / kMigrateChunk))
 void launch_migrate(const DevState& st, const MigrateItem* items, uint32_t n, uint32_t chunks, hipStream_t s);

@@ -35,9 +35,14 @@ namespace rmq {
 
 constexpr u32 kIT = 512;           // threads per verify workgroup
 constexpr u32 kIW = kIT / 64;      // waves = tasks per workgroup
-constexpr u32 kIR = 32;            // records per task
+#ifndef RMQ_VERIFY_LANE
+#define RMQ_VERIFY_LANE 1
+#endif
+// verify: a lane per record (a task = 64 records: one resident generation of waves for a round of
+// 2 x 262,144 records) or a lane pair per record (RMQ_VERIFY_LANE=0: 32 records per task)
+constexpr u32 kIR = RMQ_VERIFY_LANE ? 64 : 32;  // records per task
 #ifndef RMQ_VSPEC
-#define RMQ_VSPEC 2
+#define RMQ_VSPEC (RMQ_VERIFY_LANE ? 4 : 2)  // (more spills at 8 waves per SIMD)
 #endif
 #ifndef RMQ_VERIFY_WAVES
 #define RMQ_VERIFY_WAVES 8
@@ -424,6 +429,156 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   }
 }
 
+// One task (64 records of one source region) of the verify kernel, by one wave: a lane per record.
+// The lane runs the CRC32C register through the record's payload pieces in order (slicing-by-8 from
+// LDS, two steps per 16-byte piece, no zero-shift tables); records over 1 KB by the whole wave.
+__device__ __forceinline__ void verify_task_lane(const IngestArgs& A, const u32 (*t8)[256], u32 task) {
+  const u32 src = source_of_task(A, task);
+  if (!A.rbytes[src]) return;
+  const RegionView R = region_of(A, src);
+  if (!R.sane) return;  // every entry refused (prepare)
+  const u32 lane = threadIdx.x & 63;
+  const u32 i = (task - A.task0[src]) * kIR + lane;
+  const bool in = i < R.n_records;
+  const DevState& st = A.st;
+  u32 p = 0, L = 0, m = 0, e = 0;
+  u64 pos = 0, off = 0;
+  bool ok = false, owner = false, reb = false;
+  const uint8_t* rec = R.base;
+  uint4 hdr = make_uint4(0, 0, 0, 0);
+  // the header and the first kVSpec pieces are loaded with the directory entry, from the table slot
+  // alone (inside the data section; used only once the checks below pass)
+  uint4 sp0 = make_uint4(0, 0, 0, 0), sp1 = sp0, sp2 = sp0, sp3 = sp0;
+  if (in) {
+    const u64* tabp = reinterpret_cast<const u64*>(R.base + kRegionHdr + (u64)kDirEntry * R.n_entries) + i;
+    const u64 tab = tabp[0];
+    const u64 tabn = i + 1u < R.n_records ? tabp[1] : 0ull;  // the next slot (the record after, if any)
+    const u32 k = min((u32)tab, R.n_entries - 1u), d16 = (u32)(tab >> 32);  // ok below requires k == tab
+    rec = R.base + R.data_off + 16ull * d16;
+    const u64 dsz16 = (R.rows_off - R.data_off) >> 4;  // pieces in the data section
+    uint4 sh = make_uint4(0, 0, 0, 0);
+    if ((u64)d16 + 1ull <= dsz16) sh = *reinterpret_cast<const uint4*>(rec);
+    if (kVSpec > 0 && (u64)d16 + 2ull <= dsz16) sp0 = *reinterpret_cast<const uint4*>(rec + 16ull);
+    if (kVSpec > 1 && (u64)d16 + 3ull <= dsz16) sp1 = *reinterpret_cast<const uint4*>(rec + 32ull);
+    if (kVSpec > 2 && (u64)d16 + 4ull <= dsz16) sp2 = *reinterpret_cast<const uint4*>(rec + 48ull);
+    if (kVSpec > 3 && (u64)d16 + 5ull <= dsz16) sp3 = *reinterpret_cast<const uint4*>(rec + 64ull);
+    const DirView d = dir_of(R, k);
+    // structure: the slot lies in the range of the entry it names (prepare checked that the ranges
+    // tile the table)
+    const bool named = k == (u32)tab && i >= d.tstart && (u64)i < (u64)d.tstart + d.count;
+    if (!named) mark_insane(A, src);
+    e = A.xi_start[src] + k;
+    p = A.xi_p[e];
+    owner = k == 0 || A.xi_p[e - 1] != p;  // two local slots of one partition: the first owns the state
+    reb = d.rebase;
+    const u64 used = A.base[2 * e + 1];   // after a truncation: at the leader's first offset
+    const u64 rel = 16ull * (u64)(d16 - d.dstart16);
+    if (k == (u32)tab && d16 >= d.dstart16 && (u64)d16 + 1ull <= dsz16) {
+      hdr = sh;
+      off = ((u64)hdr.y << 32) | hdr.x;
+      L = hdr.z;
+      m = (L + 15u) >> 4;
+    }
+    pos = used + rel;
+    // the record continues the entry (its directory verdict is prepare's): its offset, inside the
+    // entry's bytes (which lie inside the data section), the first at the entry's start, each one
+    // where the one before ends and the last at the entry's end (FORMAT.md §9)
+    const u64 rend16 = (u64)d16 + 1ull + m;
+    const bool last = (u64)i + 1ull == (u64)d.tstart + d.count;
+    const bool chained = (i != d.tstart || d16 == d.dstart16) &&
+                         (last ? rend16 == (u64)d.dstart16 + d.bytes16 : (u64)(u32)(tabn >> 32) == rend16);
+    ok = named && d16 >= d.dstart16 && (u64)d.dstart16 + d.bytes16 <= (R.rows_off - R.data_off) >> 4 &&
+         off == d.first + (i - d.tstart) && rel + 16ull * (1ull + m) <= 16ull * d.bytes16 && chained &&
+         A.bad[e] == 0u;
+    if (!ok && A.bad[e] == 0u) atomicOr(&A.bad[e], kBadCrc);  // the record's content is wrong
+  }
+  const bool big = ok && m > kBigIngest;
+  const u32 mm = ok && !big ? m : 0u;
+  // the CRC register over the payload pieces in order (zero-padded in the log), from ~0
+  u32 acc = 0xFFFFFFFFu;
+  {
+    const uint4 sv[4] = {sp0, sp1, sp2, sp3};
+#pragma unroll
+    for (u32 u = 0; u < kVSpec; ++u)
+      if (u < mm) acc = crc_step8(t8, crc_step8(t8, acc, sv[u].x, sv[u].y), sv[u].z, sv[u].w);
+  }
+  for (u32 c = kVSpec; __any(c < mm); c += 4) {
+    uint4 v[4];
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u)  // four pieces in flight per lane
+      v[u] = c + u < mm ? *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * (c + u)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (u32 u = 0; u < 4; ++u)
+      if (c + u < mm) acc = crc_step8(t8, crc_step8(t8, acc, v[u].x, v[u].y), v[u].z, v[u].w);
+  }
+  // records over 1 KB, one at a time by the wave: lane l takes pieces l, l + 64, ... (Horner with
+  // the 1 KB shift), shifts past the pieces after its last one, XOR-reduce; the record's lane gets
+  // the register
+  for (u64 bm = __ballot(big); bm; bm &= bm - 1ull) {
+    const u32 sl = (u32)__builtin_ctzll(bm);
+    const u64 brec = ((u64)(u32)__builtin_amdgcn_readlane((int)(reinterpret_cast<u64>(rec) >> 32), (int)sl) << 32) |
+                     (u32)__builtin_amdgcn_readlane((int)(u32)reinterpret_cast<u64>(rec), (int)sl);
+    const u32 bm16 = ((u32)__builtin_amdgcn_readlane((int)L, (int)sl) + 15u) >> 4;
+    u32 bacc = 0;
+    for (u32 k0 = 0; 64u * k0 < bm16; k0 += 4u) {
+      uint4 v[4];
+#pragma unroll
+      for (u32 u = 0; u < 4u; ++u) {
+        const u32 jp = 64u * (k0 + u) + lane;
+        v[u] = jp < bm16 ? *reinterpret_cast<const uint4*>(brec + 16ull + 16ull * jp) : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (u32 u = 0; u < 4u; ++u) {
+        const u32 jp = 64u * (k0 + u) + lane;
+        if (jp < bm16) {
+          uint4 w = v[u];
+          if (jp == 0) w.x ^= 0xFFFFFFFFu;
+          bacc = crc_zshift(A.crc->zshift1k, bacc) ^ crc_piece16(t8, w);  // (L1/L2-resident)
+        }
+      }
+    }
+    if (lane < bm16) {
+      const u32 eb = (bm16 - 1u - lane) & 63u;
+      if (eb) bacc = gf2_mulmod(bacc, A.crc->sh16[eb]);
+    }
+    bacc = wave_xor_all(bacc);
+    if (lane == sl) acc = bacc;
+  }
+  if (ok) {
+    u32 crc = 0;
+    if (L) {
+      const u32 pad = 16u * m - L;
+      crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
+    }
+    // the zero padding after the payload (FORMAT.md §1) is part of the record
+    if (m && (L & 15u)) {
+      const uint4 t = *reinterpret_cast<const uint4*>(rec + 16ull * m);  // the last piece
+      const u32 nb = L & 15u;
+      const u32 w4[4] = {t.x, t.y, t.z, t.w};
+      for (u32 b = nb; b < 16u; ++b)
+        if ((w4[b >> 2] >> (8u * (b & 3u))) & 0xFFu) crc = ~hdr.w;
+    }
+    if (crc == hdr.w) {
+      // (a rebase entry's index entries are written by finish, once the entry is accepted: its
+      // positions lie past the live log but may share index slots with it)
+      if (owner && !reb) {
+        // sparse index past the follower's live log: every interval multiple the record crosses
+        const u32 ilog = st.interval_log2;
+        const RingRef rg = ring_ref(st, p);
+        const u64 end = pos + 16ull * (1ull + m), live = st.used[p] >> ilog;
+        for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end; ++q) {
+          if (q <= live) continue;  // inside the live log (a truncation): finish writes it if accepted
+          u64* ie = st.index + (rg.ibase + q % rg.icap) * 2;
+          ie[0] = off + 1;
+          ie[1] = end;
+        }
+      }
+    } else {
+      atomicOr(&A.bad[e], kBadCrc);  // CRC32C differs from the header's
+    }
+  }
+}
+
 // A grid of at most a few workgroups per CU: each copies the CRC tables into LDS once and its waves
 // take tasks w, w + waves, ... (the tables were 20 KB per 32 records' worth of workgroup before;
 // the 16-byte shift is a multiply, the 1 KB one of large records is read from global memory).
@@ -437,12 +592,17 @@ __global__ __launch_bounds__(kIT, RMQ_VERIFY_WAVES) void ingest_verify_kernel(In
     uint4* d0 = reinterpret_cast<uint4*>(&t8[0][0]);
     uint4* d1 = reinterpret_cast<uint4*>(&z32[0][0]);
     for (u32 k = threadIdx.x; k < sizeof(t8) / 16; k += kIT) d0[k] = src[k];
-    for (u32 k = threadIdx.x; k < sizeof(z32) / 16; k += kIT) d1[k] = zs[k];
+    if (!RMQ_VERIFY_LANE)  // (a lane per record needs no zero-shift table)
+      for (u32 k = threadIdx.x; k < sizeof(z32) / 16; k += kIT) d1[k] = zs[k];
   }
   __syncthreads();
   const u32 tasks = A.task0[A.world], stride = gridDim.x * kIW;
-  for (u32 task = __builtin_amdgcn_readfirstlane(blockIdx.x * kIW + (threadIdx.x >> 6)); task < tasks; task += stride)
-    verify_task(A, t8, z32, task);
+  for (u32 task = __builtin_amdgcn_readfirstlane(blockIdx.x * kIW + (threadIdx.x >> 6)); task < tasks; task += stride) {
+    if (RMQ_VERIFY_LANE)
+      verify_task_lane(A, t8, task);
+    else
+      verify_task(A, t8, z32, task);
+  }
 }
 
 // The verdict and state of entry e (thread per entry); its records and bytes ingested are added
@@ -655,6 +815,7 @@ void launch_notice_apply(const NoticeArgs& a, hipStream_t s) {
 
 // resident verify workgroups per CU at the kernel's launch bounds (the default verify grid)
 uint32_t verify_wgs_per_cu() { return RMQ_VERIFY_WAVES * 4u / kIW; }
+uint32_t verify_records_per_task() { return kIR; }
 
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s) {
   if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);

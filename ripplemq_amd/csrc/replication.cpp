@@ -133,6 +133,7 @@ int post_round(rmq_engine* e, uint32_t s) {
   IngestArgs a{};
   uint64_t ro = 0, smax = 0;
   uint32_t tasks = 0;
+  const uint64_t kvr = verify_records_per_task();
   for (uint32_t q = 0; q < W; ++q) {
     sn[q] = q == me ? 0 : hs[2 * q];
     rn[q] = q == me ? 0 : hs[2 * W + 2 * q];
@@ -141,7 +142,7 @@ int post_round(rmq_engine* e, uint32_t s) {
     a.region[q] = ro;
     a.rbytes[q] = rn[q];
     a.task0[q] = tasks;
-    tasks += (uint32_t)((rn[q] ? hs[2 * W + 2 * q + 1] : 0) + 31) / 32;
+    tasks += (uint32_t)((rn[q] ? hs[2 * W + 2 * q + 1] : 0) + kvr - 1) / kvr;
     smax = std::max(smax, sn[q]);
     ro += (rn[q] + 15) & ~15ull;
   }
