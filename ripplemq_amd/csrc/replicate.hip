@@ -13,10 +13,10 @@
 //     when the entry's first offset lies inside the follower's retained log below its end, that
 //     offset and its position (truncation: the leader's log wins; the position from the sparse
 //     index and the record headers). A stale leader term or a missed round (no region) refuses it;
-//   ingest_verify (wave per 32 records, a lane pair per record, records over 1 KB by the whole
-//     wave): the record continues the entry (header offset = first + rank, inside the entry's
-//     bytes) and its CRC32C from the 16-byte payload pieces (slicing-by-8 and zero-shift tables in
-//     LDS, Horner fold per lane, the pad removed by x^(-8 pad)) equals the header's; sparse-index
+//   ingest_verify (wave per 64 records, a lane per record, records over 1 KB by the whole wave;
+//     RMQ_VERIFY_LANE=0: 32 records, a lane pair each): the record continues the entry (header
+//     offset = first + rank, inside the entry's bytes) and its CRC32C from the 16-byte payload
+//     pieces (slicing-by-8 tables in LDS, the pad removed by x^(-8 pad)) equals the header's; sparse-index
 //     entries past the follower's live log (slots no live entry uses). Nothing else is written;
 //   ingest_finish (thread per entry): the verdict — a refusal of either of two local slots of one
 //     partition refuses both — then for an accepted entry the follower's log end (both state sets:
