@@ -168,6 +168,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   a.key_bits = e->key_bits;
   a.rank_mode = e->rank_mode;
   a.steal = e->steal;
+  a.prio = e->prio;
   a.gt = e->max_group_tiles;
   a.crc = e->d_crc;
   a.done_word = e->done_dev;
@@ -623,6 +624,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_S1_WGS")) e->s1_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S2_WGS")) e->s2_wgs = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_FIRST")) e->s3_first = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_PRIO")) e->prio = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_LEAD")) e->s3_lead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK")) e->rank_mode = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STEAL")) e->steal = (uint32_t)std::atoi(v);

@@ -263,6 +263,7 @@ struct PipeArgs {
                            // the group applied stops early (its stage 4 in the next launch finishes it)
   uint64_t launch_seq;
   uint32_t steal;          // stage-3 workgroups rank stage-1 tiles once out of tasks (RMQ_STEAL)
+  uint32_t prio;           // stage-1/2 and partition waves at raised issue priority (RMQ_PRIO)
   uint64_t* stamps;        // diagnostic only (RMQ_STAMPS): [workgroup][wave][8] s_memrealtime, or null
 };
 

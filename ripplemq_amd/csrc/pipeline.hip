@@ -1954,6 +1954,9 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   }
   if (!s3) {
     if ((A.debug & 16u) && wg < A.wg1 + A.wg2) return;
+    // the ranking / scan / partition chains are latency-bound: their waves first at the issue
+    // arbiter, stage 3's fill the rest (RMQ_PRIO)
+    if (A.prio) __builtin_amdgcn_s_setprio(3);
     if (wg < A.wg1) {  // a workgroup ranks tiles wg, wg + wg1, ... (RMQ_S1_WGS < tiles: fewer slots held)
       stage1_tiles(A, smem_raw, wg, A.steal != 0u);
       return;
