@@ -452,11 +452,12 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         for k in range(rounds):
             lag = (g.random(P * consumers) * (np.repeat(hw - lo, consumers) + 1)).astype(np.int64)
             eng.commit_consumer_offset(pp, cc, (np.repeat(hw, consumers) - lag).astype(np.uint64))
-            # one call as an application makes it: issue, wait, results in the caller's rows
-            # (a fetch commits nothing here, so the calls below see the same offsets)
+            # one synchronous rmq_fetch as an application makes it (page-locked rows, results in place),
+            # timed once the round's offset commit is applied (a fetch commits nothing here, so the
+            # calls below see the same offsets)
+            eng.sync()
             t0 = time.perf_counter()
-            rc_c, _, _ = eng.fetch_poll(eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rows[0][0],
-                                                        res=rows[0][1], pinned_rows=True), wait=True)
+            rc_c, _, _ = eng.fetch_device(None, None, None, d_out, cap, req=rows[0][0], res=rows[0][1], pinned_rows=True)
             t_wall += time.perf_counter() - t0
             eng.profile(True)
             rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)

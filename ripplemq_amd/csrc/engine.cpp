@@ -1398,8 +1398,12 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
 
 }  // namespace
 
-int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
-                    uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
+namespace {
+// Issue a fetch into the next slot. sync (rmq_fetch: the caller waits at once): the request and
+// result copies on the fetch stream itself, so the call's chain has no cross-stream hops; else on
+// the copy stream and the result stream, overlapping the fetches and launches around it.
+int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
+                uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket, bool sync) {
   if (!e || !ticket) return RMQ_EINVAL;
   const bool rows_pinned = (mem & RMQ_FETCH_PINNED_ROWS) != 0;
   mem &= ~RMQ_FETCH_PINNED_ROWS;
@@ -1473,12 +1477,13 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     // the requests' copy on the copy stream (it depends on nothing the pipeline or an earlier fetch
     // writes: it overlaps the running launch and fetch), then the kernels behind the launches
     // issued so far and the copy
+    hipStream_t in_s = sync ? e->fetch_s : e->copy_s, out_s = sync ? e->fetch_s : e->fetch_out_s;
     HIP_TRY(hipMemcpyAsync(f.d_req, rows_pinned ? static_cast<const void*>(reqs) : f.h_req,
-                           (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->copy_s));
-    HIP_TRY(hipEventRecord(f.ev_in, e->copy_s));
+                           (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, in_s));
+    if (!sync) HIP_TRY(hipEventRecord(f.ev_in, in_s));
     HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
-    HIP_TRY(hipStreamWaitEvent(e->fetch_s, f.ev_in, 0));
+    if (!sync) HIP_TRY(hipStreamWaitEvent(e->fetch_s, f.ev_in, 0));
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     const uint32_t runs = e->profile ? e->fetch_replay : 1u;
     if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run, copies outside
@@ -1503,11 +1508,11 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
     HIP_TRY(hipEventRecord(f.ev_k, e->fetch_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_k, 0));
     // the result rows on their own stream: the next fetch's kernels do not wait for this copy
-    HIP_TRY(hipStreamWaitEvent(e->fetch_out_s, f.ev_k, 0));
+    if (!sync) HIP_TRY(hipStreamWaitEvent(out_s, f.ev_k, 0));
     // (the bytes needed reach the host by the gather's own store into f.need)
     HIP_TRY(hipMemcpyAsync(rows_pinned ? static_cast<void*>(res) : static_cast<void*>(f.h_res), f.d_res, (size_t)n * 32,
-                           hipMemcpyDeviceToHost, e->fetch_out_s));
-    HIP_TRY(hipEventRecord(f.ev, e->fetch_out_s));
+                           hipMemcpyDeviceToHost, out_s));
+    HIP_TRY(hipEventRecord(f.ev, out_s));
   }
   f.rows_pinned = rows_pinned;
   f.ticket = tk;
@@ -1522,6 +1527,13 @@ int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32
   while (e->fetch_done.size() > 256) e->fetch_done.pop_front();
   *ticket = tk;
   return RMQ_OK;
+}
+
+}  // namespace
+
+int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
+                    uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
+  return fetch_issue(e, reqs, n, mem, out, out_cap, res, ticket, false);
 }
 
 int rmq_fetch_poll(rmq_engine* e, uint64_t ticket, uint32_t wait, uint64_t* bytes_used) {
@@ -1549,7 +1561,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
   if (!e) return RMQ_EINVAL;
   if (!n) return RMQ_OK;
   uint64_t t = 0;
-  const int rc = rmq_fetch_async(e, reqs, n, mem, out, out_cap, res, &t);
+  const int rc = fetch_issue(e, reqs, n, mem, out, out_cap, res, &t, true);
   if (rc) return rc;
   return rmq_fetch_poll(e, t, 1, bytes_used);
 }

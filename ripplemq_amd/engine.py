@@ -323,15 +323,23 @@ class Engine:
             raise EngineError(rc, "rmq_fetch")
         return rc, res, out[:out_cap], int(used.value)
 
-    def fetch_device(self, pidx, consumer, max_records, d_out: int, out_cap: int, commit: bool = False):
-        """rmq_fetch into a device buffer (16-byte aligned); returns (rc, res, bytes_used)."""
-        n = len(pidx)
-        req = np.zeros((n, 4), np.uint32)
-        req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
-        req[:, 3] = A.RMQ_FETCH_COMMIT if commit else 0
-        res = np.zeros(n, FETCH_RES_DTYPE)
+    def fetch_device(self, pidx, consumer, max_records, d_out: int, out_cap: int, commit: bool = False,
+                     req: np.ndarray | None = None, res: np.ndarray | None = None, pinned_rows: bool = False):
+        """rmq_fetch into a device buffer (16-byte aligned); returns (rc, res, bytes_used). req / res:
+        the caller's arrays (pidx / consumer / max_records None leave req's columns as they are);
+        pinned_rows: page-locked ones (fetch_rows), DMA'd with no host copy (RMQ_FETCH_PINNED_ROWS)."""
+        n = len(pidx) if pidx is not None else len(req)
+        if req is None:
+            req = np.zeros((n, 4), np.uint32)
+            req[:, 3] = A.RMQ_FETCH_COMMIT if commit else 0
+        for col, v in ((0, pidx), (1, consumer), (2, max_records)):
+            if v is not None:
+                req[:, col] = v
+        if res is None:
+            res = np.zeros(n, FETCH_RES_DTYPE)
         used = C.c_uint64()
-        rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_DEVICE, d_out, out_cap, _ptr(res), C.byref(used))
+        mem = A.RMQ_MEM_DEVICE | (A.RMQ_FETCH_PINNED_ROWS if pinned_rows else 0)
+        rc = self.lib.rmq_fetch(self.h, _ptr(req), n, mem, d_out, out_cap, _ptr(res), C.byref(used))
         if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
             raise EngineError(rc, "rmq_fetch")
         return rc, res, int(used.value)

@@ -55,8 +55,10 @@ def main():
                                                                              req=req, res=res), wait=True), 3)
     prq, prs = eng.fetch_rows(P * C)
     prq[:] = req
-    out["fetch_pinned_sync_us"] = tm(lambda: eng.fetch_poll(eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap,
-                                                                             req=prq, res=prs, pinned_rows=True), wait=True))
+    out["fetch_pinned_async_wait_us"] = tm(lambda: eng.fetch_poll(eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap,
+                                                                                   req=prq, res=prs, pinned_rows=True), wait=True))
+    out["fetch_pinned_sync_us"] = tm(lambda: eng.fetch_device(None, None, None, d_out, cap, req=prq, res=prs,
+                                                              pinned_rows=True))
     rows = [eng.fetch_rows(P * C) for _ in range(8)]
     for rq, _ in rows:
         rq[:] = req
