@@ -654,6 +654,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     last = 0
     for k in range(args.steps):
         last = step(args.warmup + k)
+    t_issue = time.perf_counter() - t0  # host time to submit the steps (diagnostic)
     barrier()
     elapsed = time.perf_counter() - t0
     x1 = eng.replication_stats()
@@ -697,6 +698,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": t_max * 1e3 / args.steps,
+            "host_issue_us_per_step": t_issue * 1e6 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
