@@ -32,7 +32,11 @@
 namespace rmq {
 
 constexpr int kOk = 0, kNotLeader = -1, kNoPart = -2, kInval = -3, kNoSpc = -4, kOffset = -6;
-constexpr u32 kFW = 4;  // waves per workgroup (resolve, gather)
+constexpr u32 kFW = 4;  // waves per workgroup (gather)
+#ifndef RMQ_RESOLVE_WAVES
+#define RMQ_RESOLVE_WAVES 4
+#endif
+constexpr u32 kRW = RMQ_RESOLVE_WAVES;  // waves per resolve workgroup
 
 struct PartView {
   u64 leo, used, start_off, start_pos;
@@ -209,12 +213,12 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
   return Resolved{start, count, need ? pend - pos0 : 0ull, pos0, (ring_off << 6) | (desc & 63ull), status};
 }
 
-__global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
+__global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
   const u32 lane = lane_id(), w = threadIdx.x >> 6;
-  const u32 r = (blockIdx.x * kFW + w) * kRPW + (lane >> 5);
+  const u32 r = (blockIdx.x * kRW + w) * kRPW + (lane >> 5);
   const bool live = r < a.n;  // (no early return: the workgroup meets at a barrier below)
   const Resolved q = resolve_request(a, r, live);
-  __shared__ u64 s_b[kFW];
+  __shared__ u64 s_b[kRW];
   const u64 b2 = bcast_u64(q.bytes, 0) + bcast_u64(q.bytes, 32);  // the wave's two requests
   if (lane == 0) s_b[w] = b2;
   if (live && (lane & 31u) == 0) {
@@ -225,13 +229,13 @@ __global__ __launch_bounds__(64 * kFW) void fetch_resolve_kernel(FetchArgs a) {
     a.aux[2 * r + 1] = q.ring;
     a.cpre[r] = (u32)q.bytes;
   }
-  // one add per workgroup (its kFW * kRPW requests share a chunk) into the chunk's own L2 line
-  static_assert(kFetchChunk % (kFW * kRPW) == 0, "a resolve workgroup never straddles a chunk");
+  // one add per workgroup (its kRW * kRPW requests share a chunk) into the chunk's own L2 line
+  static_assert(kFetchChunk % (kRW * kRPW) == 0, "a resolve workgroup never straddles a chunk");
   __syncthreads();
   if (threadIdx.x == 0) {
     u64 b = 0;
-    for (u32 k = 0; k < kFW; ++k) b += s_b[k];
-    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kFW * kRPW / kFetchChunk) * kCsumStride], (unsigned long long)b);
+    for (u32 k = 0; k < kRW; ++k) b += s_b[k];
+    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kRW * kRPW / kFetchChunk) * kCsumStride], (unsigned long long)b);
   }
 }
 
@@ -374,7 +378,7 @@ void preload_fetch_kernels() {
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
   const hipEvent_t* e = ev;
-  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kFW * kRPW - 1) / (kFW * kRPW)), dim3(64 * kFW), 0, s, e ? e[0] : nullptr,
+  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kRW * kRPW - 1) / (kRW * kRPW)), dim3(64 * kRW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, a);
   hipExtLaunchKernelGGL(fetch_gather_kernel, dim3((a.n + kGR - 1) / kGR), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
                         e ? e[3] : nullptr, 0, a);
