@@ -205,4 +205,26 @@ def test_pinned_rows_match_sync():
                 a, b = int(res["out_pos"][r]), int(res["out_pos"][r] + res["bytes"][r])
                 assert np.array_equal(got[a:b], wbuf[a:b]), (k, r)
         assert pending[2][1] == A.RMQ_ENOSPC
+        # the synchronous call with page-locked rows (its copies on the fetch stream itself)
+        for k, cap in ((0, 8 << 20), (1, 1 << 16)):
+            n = P * C
+            req, res = dev.fetch_rows(n)
+            req[:, 0] = g.integers(0, P + 3, n)
+            req[:, 1] = g.integers(0, C, n)
+            req[:, 2] = g.integers(0, 2000, n)
+            d_out = dev.device_alloc(cap)
+            rc, got, used = dev.fetch_device(None, None, None, d_out, cap, req=req, res=res, pinned_rows=True)
+            rc_w, want, wbuf, used_w = dev.fetch(req[:, 0].copy(), req[:, 1].copy(), req[:, 2].copy(), out_cap=cap)
+            assert rc == rc_w and used == used_w, k
+            assert got is res
+            for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                assert np.array_equal(res[f], want[f]), (k, f)
+            n_cp = min(used, cap)
+            buf = np.empty(max(n_cp, 1), np.uint8)
+            if n_cp:
+                dev.d2h(buf[:n_cp], d_out)
+            for r in np.flatnonzero((res["status"] == 0) & (res["bytes"] > 0)):
+                a, b = int(res["out_pos"][r]), int(res["out_pos"][r] + res["bytes"][r])
+                assert np.array_equal(buf[a:b], wbuf[a:b]), (k, r)
+            dev.device_free(d_out)
         dev.sync()
