@@ -179,6 +179,7 @@ struct Replication {
   uint32_t* d_bad = nullptr;     // [n_in]
   uint32_t* d_acc = nullptr;     // [n_in]
   uint64_t* d_base = nullptr;    // [n_in][2] IngestArgs::base
+  uint64_t* d_cdesc = nullptr;   // [n_in][4] IngestArgs::cdesc
   uint32_t* d_items = nullptr;   // [items_cap][2] follower copy work items
   uint32_t* d_nitems = nullptr;  // [2][1 + kMaxWorld]: copy items allocated, structural flag per source;
                                  // rounds alternate halves, each round's prepare clears the other

@@ -327,6 +327,9 @@ struct IngestArgs {
   uint64_t* base;            // [n_in][2] {log end offset, log end position} the entry continues:
                              // the follower's, or the leader's first offset after a truncation
   uint64_t* ackout;          // [n_in][2] follower log end after the round | status (FORMAT.md §9)
+  uint64_t* cdesc;           // [n_in][4] copy descriptor of an entry with copy items (prepare ->
+                             //   copy): {data address, ring address, log end position it continues,
+                             //   bytes << 6 | log2(ring bytes)}
   uint32_t* items;           // [cap][2] copy work items {entry, chunk of kCopyChunk bytes} (prepare)
   uint32_t* n_items;         // [1] items allocated this round (prepare adds; zero at the start)
   uint32_t* insane;          // [kMaxWorld] a structural fault of that source's region (prepare and

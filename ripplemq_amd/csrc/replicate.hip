@@ -227,7 +227,16 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
         if (!bad && !d.count && d.bytes16) bad = kBadCrc;  // bytes without records
         // copy items only for an entry whose bytes tile the data section (so the items of a round
         // stay within the host's bound: one per 16 KiB of received bytes plus one per entry)
-        if (!bad && tiled) nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
+        if (!bad && tiled) {
+          nc = (u32)((16ull * d.bytes16 + kCopyChunk - 1) / kCopyChunk);
+          // the copy's addresses, so its workgroups start their data loads after two lookups
+          const RingRef rg = ring_ref(st, p);
+          u64* cd = A.cdesc + 4ull * e;
+          cd[0] = reinterpret_cast<u64>(R.base + R.data_off + 16ull * d.dstart16);
+          cd[1] = reinterpret_cast<u64>(st.logs + (u64)A.xi_slot[e] * st.rstride + rg.base);
+          cd[2] = used;
+          cd[3] = (16ull * d.bytes16) << 6 | (u64)(63 - __builtin_clzll(rg.seg));
+        }
       }
     }
     A.bad[e] = bad;
@@ -737,17 +746,15 @@ __global__ __launch_bounds__(kCT) void ingest_copy_kernel(IngestArgs A) {
   const u32 it = blockIdx.x;
   if (it >= *A.n_items) return;
   const u32 e = A.items[2 * it], c = A.items[2 * it + 1];
-  if (!A.acc[e]) return;
-  const u32 src = source_of_entry(A, e), k = e - A.xi_start[src];
-  const DevState& st = A.st;
-  const RegionView R = region_of(A, src);
-  const DirView d = dir_of(R, k);
-  const u32 p = A.xi_p[e];
-  const RingRef rg = ring_ref(st, p);
-  uint8_t* const ring = st.logs + (u64)A.xi_slot[e] * st.rstride + rg.base;
-  const u64 segmask = rg.seg - 1ull;
-  const uint8_t* data = R.base + R.data_off + 16ull * d.dstart16;
-  const u64 bused = A.base[2 * e + 1], bytes = 16ull * d.bytes16, gend = bused + bytes;
+  // the verdict and the entry's descriptor (prepare) in one round of loads
+  const u32 ok = A.acc[e];
+  const u64* cd = A.cdesc + 4ull * e;
+  const u64 d0 = cd[0], d1 = cd[1], bused = cd[2], d3 = cd[3];
+  if (!ok) return;
+  const uint8_t* data = reinterpret_cast<const uint8_t*>(d0);
+  uint8_t* const ring = reinterpret_cast<uint8_t*>(d1);
+  const u64 seg = 1ull << (d3 & 63ull), segmask = seg - 1ull;
+  const u64 bytes = d3 >> 6, gend = bused + bytes;
   const u64 b0 = (u64)c * kCopyChunk, b1 = min(bytes, b0 + kCopyChunk);
   for (u64 q0 = b0 + 16ull * threadIdx.x; q0 < b1; q0 += 16ull * kCT * 4) {
     uint4 v[4];
@@ -760,7 +767,7 @@ __global__ __launch_bounds__(kCT) void ingest_copy_kernel(IngestArgs A) {
     for (u32 u = 0; u < 4; ++u) {
       const u64 q = q0 + 16ull * kCT * u;
       const u64 x = bused + q;
-      if (q < b1 && x + rg.seg >= gend) store_log16(ring + (x & segmask), v[u]);
+      if (q < b1 && x + seg >= gend) store_log16(ring + (x & segmask), v[u]);
     }
   }
 }

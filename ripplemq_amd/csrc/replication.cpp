@@ -177,6 +177,7 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.bad = r->d_bad;
   a.acc = r->d_acc;
   a.base = r->d_base;
+  a.cdesc = r->d_cdesc;
   a.ackout = x.ackout;
   a.items = r->d_items;
   {
@@ -262,7 +263,7 @@ void repl_free(rmq_engine* e) {
     if (x.h_sizes) hipHostFree(x.h_sizes);
   }
   void* bufs[] = {r->d_xo_p, r->d_xo_slot, r->d_xo_start, r->d_keysum, r->d_keysum_in, r->d_outidx, r->d_xi_p, r->d_xi_slot,
-                  r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_items, r->d_nitems, r->d_counters,
+                  r->d_xi_start, r->d_bad, r->d_acc, r->d_base, r->d_cdesc, r->d_items, r->d_nitems, r->d_counters,
                   r->d_xnext, r->d_xreq, r->d_xcu, r->d_xdec, r->d_xtot, r->d_dflag, r->d_lastg,
                   r->d_nout, r->d_nin, r->d_eackv};
   for (void* p : bufs)
@@ -384,6 +385,7 @@ int repl_set_lists(rmq_engine* e) {
   if (!rc) rc = upload(&r->d_bad, std::vector<uint32_t>(n_in, 0u));
   if (!rc) rc = upload(&r->d_acc, std::vector<uint32_t>(n_in, 0u));
   if (!rc) rc = upload(&r->d_base, std::vector<uint64_t>(2 * n_in, 0ull));
+  if (!rc) rc = upload(&r->d_cdesc, std::vector<uint64_t>(4 * n_in, 0ull));
   if (!rc) rc = upload(&r->d_xnext, std::vector<uint64_t>(2 * n_out, 0ull));
   if (!rc) rc = upload(&r->d_xreq, std::vector<uint64_t>(4 * n_out, 0ull));
   if (!rc) rc = upload(&r->d_xcu, std::vector<uint64_t>(n_out, 0ull));
