@@ -49,6 +49,13 @@ constexpr u32 kIR = RMQ_VERIFY_LANE ? 64 : 32;  // records per task
 #endif
 constexpr u32 kVSpec = RMQ_VSPEC;    // pieces per lane loaded with the table slot (0..4)
 static_assert(kVSpec <= 4, "at most four speculative pieces per lane");
+#ifndef RMQ_ENTRY_THREADS
+#define RMQ_ENTRY_THREADS 256
+#endif
+// threads per prepare / finish workgroup (a thread per entry; one-wave workgroups, spreading a
+// round's entries over more CUs, measured the same: 1.554 vs 1.550 G in the rehearsal, round 4)
+constexpr u32 kEntryT = RMQ_ENTRY_THREADS;
+static_assert(kEntryT % 64 == 0, "whole waves (finish sums its counters per wave)");
 constexpr u32 kBigIngest = 64;     // records over this many 16-byte pieces: the whole wave
 constexpr u32 kCT = 64;            // threads per copy workgroup (one wave: many items resident per CU)
 
@@ -177,7 +184,7 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = e < A.n_in;
   // the next round's counters (the round before used them; its kernels ran before this one)
-  static_assert(1 + kMaxWorld <= 256, "one workgroup clears them");
+  static_assert(1 + kMaxWorld <= kEntryT, "one workgroup clears them");
   if (blockIdx.x == 0 && threadIdx.x < 1 + kMaxWorld) A.n_items_next[threadIdx.x] = 0u;
   u32 nc = 0;  // copy work items of the entry
   if (in) {
@@ -825,10 +832,10 @@ uint32_t verify_wgs_per_cu() { return RMQ_VERIFY_WAVES * 4u / kIW; }
 uint32_t verify_records_per_task() { return kIR; }
 
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s) {
-  if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
+  if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + kEntryT - 1) / kEntryT), dim3(kEntryT), 0, s, a);
   if (tasks)
     hipLaunchKernelGGL(ingest_verify_kernel, dim3(std::min<uint32_t>((tasks + kIW - 1) / kIW, verify_wgs)), dim3(kIT), 0, s, a);
-  if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + 255) / 256), dim3(256), 0, s, a);
+  if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + kEntryT - 1) / kEntryT), dim3(kEntryT), 0, s, a);
   if (items_bound) hipLaunchKernelGGL(ingest_copy_kernel, dim3(items_bound), dim3(kCT), 0, s, a);
 }
 
