@@ -29,6 +29,7 @@ from __future__ import annotations
 import argparse
 import collections
 import dataclasses
+import gc
 import glob
 import json
 import os
@@ -439,11 +440,17 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         d_out = eng.device_alloc(cap)
         recs = nbytes = 0
         t_kern = t_wall = t_reg = 0.0
+        t_calls = []
         # untimed calls first: a process's first launch of a kernel loads its code object
         # (~20 ms, measured between the first resolve and gather in profiles/r03q_prof), and each
         # of the engine's four fetch slots allocates its scratch on first use
         for _ in range(4):
             eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+        # and every consumer-commit staging slot once (each allocates its pinned and device buffers
+        # on first use; one of them, on some boxes, stalled the next fetch by ~8 ms)
+        for _ in range(16):
+            eng.commit_consumer_offset(pp, cc, np.zeros(P * consumers, np.uint64))
+        eng.sync()
         # the request and result rows in page-locked arrays, reused from call to call
         # (RMQ_FETCH_PINNED_ROWS: DMA both ways, no host copy)
         rows = [eng.fetch_rows(P * consumers) for _ in range(8)]
@@ -456,9 +463,14 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             # timed once the round's offset commit is applied (a fetch commits nothing here, so the
             # calls below see the same offsets)
             eng.sync()
+            gc.disable()  # (as timeit does: a collector pass is not the call's cost)
             t0 = time.perf_counter()
             rc_c, _, _ = eng.fetch_device(None, None, None, d_out, cap, req=rows[0][0], res=rows[0][1], pinned_rows=True)
-            t_wall += time.perf_counter() - t0
+            t_calls.append(time.perf_counter() - t0)
+            t_wall += t_calls[-1]
+            gc.enable()
+            if os.environ.get("RMQ_BENCH_CALLS"):  # diagnostic: each timed call's wall time
+                print(f"bench: fetch max {mx} call {(time.perf_counter() - t0) * 1e6:.1f} us", file=sys.stderr)
             eng.profile(True)
             rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
             _, ms_f = eng.profile_query(3)  # the kernels' own dispatch-recorded spans, summed
@@ -479,12 +491,18 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             nbytes += int(res["bytes"].sum())
         # the same requests as 8 asynchronous calls back to back (rmq_fetch_async: 4 in flight, the
         # host never waits on the GPU between issues; pinned rows), first issue to last result
-        eng.sync()
-        t0 = time.perf_counter()
-        tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rq, res=rs, pinned_rows=True)
-               for rq, rs in rows]
-        n_async = sum(int(eng.fetch_poll(t, wait=True)[1]["count"].sum()) for t in tks)
-        t_async = time.perf_counter() - t0
+        # (three bursts: the median, as for the single calls below, so that one host stall of a
+        # few ms — seen once per run at random points on some boxes — does not stand for the rate)
+        bursts = []
+        for _ in range(3):
+            eng.sync()
+            gc.disable()
+            t0 = time.perf_counter()
+            tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rq, res=rs, pinned_rows=True)
+                   for rq, rs in rows]
+            n_async = sum(int(eng.fetch_poll(t, wait=True)[1]["count"].sum()) for t in tks)
+            bursts.append(n_async / (time.perf_counter() - t0))
+            gc.enable()
         eng.device_free(d_out)
         for rq, rs in rows:
             eng.host_release(rq)
@@ -496,8 +514,13 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         # the dispatch-recorded span of a launch starts when the command processor takes its packet,
         # which can precede the end of the work before it on the stream (the request copy), so
         # spans overstate kernel time; the roofline uses the replayed kernels' region instead
-        out[f"max{mx}"] = {"records_per_s_kernels": recs / t_reg, "records_per_s_call": recs / t_wall,
-                           "records_per_s_async_calls": n_async / t_async,
+        # per call: the median call's time (the mean over all calls beside it)
+        out[f"max{mx}"] = {"records_per_s_kernels": recs / t_reg,
+                           "records_per_s_call": recs / rounds / float(np.median(t_calls)),
+                           "records_per_s_call_mean": recs / t_wall,
+                           "call_us": [round(x * 1e6, 1) for x in t_calls],
+                           "records_per_s_async_calls": float(np.median(bursts)),
+                           "records_per_s_async_bursts": bursts,
                            "records_per_request": recs / (rounds * P * consumers),
                            "requests": P * consumers, "rounds": rounds,
                            "roofline": {"bound": "hbm", "achieved": alg / t_reg / 1e9, "peak": HBM_PEAK_GBS,

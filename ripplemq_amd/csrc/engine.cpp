@@ -111,6 +111,20 @@ int check_err(rmq_engine* e) {
 // Wait for everything issued on stream s. A blocking hipStreamSynchronize returns ~10 us after the
 // last kernel ends (interrupt wake-up); a sync sits on the producer's path (rmq_sync, a poll that
 // needs commit indices), so poll the stream for up to 20 ms first, then block.
+// Wait for an event the same way: a blocking hipEventSynchronize now and then woke milliseconds
+// late (8 ms stalls in one synchronous fetch of ten, round 4), so spin on queries first.
+int event_wait(hipEvent_t ev) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return RMQ_OK;
+    if (q != hipErrorNotReady) return hip_fail(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+  }
+  HIP_TRY(hipEventSynchronize(ev));
+  return RMQ_OK;
+}
+
 int stream_wait(hipStream_t s) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
@@ -1201,7 +1215,10 @@ int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32
   // whose previous use has completed; a fetch or read-back issued later sees them
   rmq_engine::CommitSlot& cs = e->cslot[e->cslot_next];
   e->cslot_next = (e->cslot_next + 1) % rmq_engine::kCommitSlots;
-  if (cs.used) HIP_TRY(hipEventSynchronize(cs.ev));
+  if (cs.used) {
+    const int rc = event_wait(cs.ev);
+    if (rc) return rc;
+  }
   cs.used = false;
   if (n > cs.cap) {
     if (cs.h) hipHostFree(cs.h);
@@ -1349,7 +1366,8 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage, hip
 int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t* bytes_used) {
   if (f.phase == 1) {
     if (wait) {
-      HIP_TRY(hipEventSynchronize(f.ev));
+      const int rc = event_wait(f.ev);
+      if (rc) return rc;
     } else {
       const hipError_t q = hipEventQuery(f.ev);
       if (q == hipErrorNotReady) return RMQ_PENDING;
@@ -1383,7 +1401,8 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
   }
   if (f.phase == 2) {
     if (wait) {
-      HIP_TRY(hipEventSynchronize(f.ev_copy));
+      const int rc = event_wait(f.ev_copy);
+      if (rc) return rc;
     } else {
       const hipError_t q = hipEventQuery(f.ev_copy);
       if (q == hipErrorNotReady) return RMQ_PENDING;

@@ -449,6 +449,7 @@ int flush(rmq_engine* e);
 int drain(rmq_engine* e);
 int quiesce(rmq_engine* e);
 int check_err(rmq_engine* e);
+int event_wait(hipEvent_t ev);  // spin on queries (20 ms), then block
 // replication.cpp
 int repl_attach(rmq_engine* e, Transport* t);
 void repl_free(rmq_engine* e);

@@ -242,24 +242,53 @@ __global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
 constexpr u32 kGQ = 4;          // requests per gather wave
 constexpr u32 kGR = kFW * kGQ;  // requests per gather workgroup
 
-// Placement + gather: workgroup per kGR consecutive requests.
+// Placement + gather: workgroup per kGR consecutive requests. Two rounds of loads: the wave's
+// request words with the placement sums, then (requests of at most 128 pieces) the records' pieces,
+// issued before the placement barriers; only the stores wait for the output positions.
 __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   __shared__ u64 s_red[kFW];
   __shared__ u64 s_pos[kGR];
   const DevState& st = a.st;
   const u32 tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
   const u32 r0 = blockIdx.x * kGR, c0 = r0 / kFetchChunk;
+  // the wave's kGQ requests (lanes 0..kGQ-1 read one each)
+  const u32 rq = r0 + w * kGQ + (lane < kGQ ? lane : 0u);
+  const bool qv = lane < kGQ && rq < a.n;
+  const u64 q_pos = qv ? a.aux[2 * rq + 0] : 0ull, q_ring = qv ? a.aux[2 * rq + 1] : 0ull;
+  const u64 q_nb = qv ? a.cpre[rq] : 0ull;
   // the next fetch's chunk sums (its resolve runs after this kernel on the same stream)
   for (u32 k = blockIdx.x * 64 * kFW + tid; k < a.csum_lines; k += gridDim.x * 64 * kFW) a.csum_next[(u64)k * kCsumStride] = 0;
   // bytes of every request before r0: the chunk sums before its chunk, then its chunk's requests
   u64 v = 0;
   for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[(u64)k * kCsumStride];
   for (u32 k = c0 * kFetchChunk + tid; k < r0; k += 64 * kFW) v += a.cpre[k];
+  const u32 rr = r0 + tid;
+  const u64 nb = tid < kGR && rr < a.n ? a.cpre[rr] : 0ull;
+  // requests of at most 128 pieces each (max = 10 of short records): all four copied with one round
+  // of loads (two pieces per lane and request), loaded now, stored once placed (named registers:
+  // a local array here went to scratch)
+  bool small = true;
+#pragma unroll
+  for (u32 q = 0; q < kGQ; ++q) small = small && (bcast_u64(q_nb, q) >> 4) <= 128u;
+#define RMQ_GQ_LOAD(q, x0, x1)                                                                        \
+  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;                                                        \
+  if (small) {                                                                                        \
+    const u64 nbr = bcast_u64(q_nb, q);                                                               \
+    const u64 pos0 = bcast_u64(q_pos, q), rw = bcast_u64(q_ring, q);                                  \
+    const uint8_t* ring = st.logs + (rw >> 6);                                                        \
+    const u64 mask = (1ull << (rw & 63ull)) - 1ull;                                                   \
+    if (lane < (nbr >> 4)) x0 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * lane) & mask)); \
+    if (lane + 64u < (nbr >> 4)) x1 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (lane + 64u)) & mask)); \
+  }
+  static_assert(kGQ == 4, "four requests per gather wave");
+  RMQ_GQ_LOAD(0, a0, a1)
+  RMQ_GQ_LOAD(1, b0, b1)
+  RMQ_GQ_LOAD(2, c0_, c1_)
+  RMQ_GQ_LOAD(3, d0, d1)
+#undef RMQ_GQ_LOAD
   v = bcast_u64(wave_incl_scan(v), 63);  // the wave's sum
   if (lane == 0) s_red[w] = v;
   // this workgroup's requests: exclusive scan of their bytes
-  const u32 rr = r0 + tid;
-  const u64 nb = tid < kGR && rr < a.n ? a.cpre[rr] : 0ull;
   const u64 inc = wave_incl_scan(nb);  // kGR <= 64: one wave holds them all
   __syncthreads();
   const u64 base = s_red[0] + s_red[1] + s_red[2] + s_red[3];
@@ -288,58 +317,24 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
       }
     }
   }
-  // the wave's kGQ requests (lanes 0..kGQ-1 read one each; their ring words are loaded before the
-  // barrier, so they are in flight during the placement scan)
-  const u32 rq = r0 + w * kGQ + (lane < kGQ ? lane : 0u);
-  const bool qv = lane < kGQ && rq < a.n;
-  const u64 q_pos = qv ? a.aux[2 * rq + 0] : 0ull, q_ring = qv ? a.aux[2 * rq + 1] : 0ull;
-  const u64 q_nb = qv ? a.cpre[rq] : 0ull;
   __syncthreads();
   // the wave's requests one after the other (one stream of 16-byte pieces per wave: four requests
   // side by side, a quarter-wave or an interleaved run each, measured 1.7x slower at max = 1024)
   const u64 q_out = lane < kGQ ? s_pos[(w * kGQ + lane) & (kGR - 1u)] : 0ull;
-  // requests of at most 128 pieces each (max = 10 of short records): all four copied with one round
-  // of loads (two pieces per lane and request) instead of one round per request
-  {
-    bool small = true;
-#pragma unroll
-    for (u32 q = 0; q < kGQ; ++q) {
-      const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);
-      small = small && (!nbr || po + nbr > a.out_cap || (nbr >> 4) <= 128u);
-    }
-    if (small) {
-      // named registers (a local array here went to scratch): request q's two pieces per lane
-#define RMQ_GQ_LOAD(q, x0, x1)                                                                        \
-  uint4 x0 = make_uint4(0, 0, 0, 0), x1 = x0;                                                        \
-  {                                                                                                   \
-    const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);                                     \
-    const bool sv = nbr && po + nbr <= a.out_cap;                                                     \
-    const u64 pos0 = bcast_u64(q_pos, q), rw = bcast_u64(q_ring, q);                                  \
-    const uint8_t* ring = st.logs + (rw >> 6);                                                        \
-    const u64 mask = (1ull << (rw & 63ull)) - 1ull;                                                   \
-    if (sv && lane < (nbr >> 4)) x0 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * lane) & mask)); \
-    if (sv && lane + 64u < (nbr >> 4)) x1 = *reinterpret_cast<const uint4*>(ring + ((pos0 + 16ull * (lane + 64u)) & mask)); \
-  }
+  if (small) {
 #define RMQ_GQ_STORE(q, x0, x1)                                                                       \
   {                                                                                                   \
     const u64 nbr = bcast_u64(q_nb, q), po = bcast_u64(q_out, q);                                     \
-    const bool sv = nbr && po + nbr <= a.out_cap;                                                     \
+    const bool sv = nbr && po + nbr <= a.out_cap;  /* served (loaded speculatively either way) */   \
     if (sv && lane < (nbr >> 4)) *reinterpret_cast<uint4*>(a.out + po + 16ull * lane) = x0;         \
     if (sv && lane + 64u < (nbr >> 4)) *reinterpret_cast<uint4*>(a.out + po + 16ull * (lane + 64u)) = x1; \
   }
-      static_assert(kGQ == 4, "four requests per gather wave");
-      RMQ_GQ_LOAD(0, a0, a1)
-      RMQ_GQ_LOAD(1, b0, b1)
-      RMQ_GQ_LOAD(2, c0, c1)
-      RMQ_GQ_LOAD(3, d0, d1)
-      RMQ_GQ_STORE(0, a0, a1)
-      RMQ_GQ_STORE(1, b0, b1)
-      RMQ_GQ_STORE(2, c0, c1)
-      RMQ_GQ_STORE(3, d0, d1)
-#undef RMQ_GQ_LOAD
+    RMQ_GQ_STORE(0, a0, a1)
+    RMQ_GQ_STORE(1, b0, b1)
+    RMQ_GQ_STORE(2, c0_, c1_)
+    RMQ_GQ_STORE(3, d0, d1)
 #undef RMQ_GQ_STORE
-      return;
-    }
+    return;
   }
   for (u32 q = 0; q < kGQ; ++q) {
     const u64 nbr = bcast_u64(q_nb, q), pos0_out = bcast_u64(q_out, q);

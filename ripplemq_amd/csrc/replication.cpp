@@ -122,7 +122,8 @@ int post_round(rmq_engine* e, uint32_t s) {
   // so this normally finds them landed; a wait is counted (rmq_repl_stats.host_waits)
   if (hipEventQuery(x.ev_sz) == hipErrorNotReady) {
     const auto t0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipEventSynchronize(x.ev_sz));
+    const int rc = event_wait(x.ev_sz);
+    if (rc) return rc;
     r->host_waits++;
     r->host_wait_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   }
