@@ -500,9 +500,13 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             t0 = time.perf_counter()
             tks = [eng.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=rq, res=rs, pinned_rows=True)
                    for rq, rs in rows]
+            t_iss = time.perf_counter() - t0
             n_async = sum(int(eng.fetch_poll(t, wait=True)[1]["count"].sum()) for t in tks)
             bursts.append(n_async / (time.perf_counter() - t0))
             gc.enable()
+            if os.environ.get("RMQ_BENCH_CALLS"):
+                print(f"bench: fetch max {mx} burst issue {t_iss * 1e6:.1f} us total {n_async / bursts[-1] * 1e6:.1f} us "
+                      f"records {n_async}", file=sys.stderr)
         eng.device_free(d_out)
         for rq, rs in rows:
             eng.host_release(rq)
