@@ -57,9 +57,29 @@ constexpr u32 kRPW = 2;  // requests per resolve wave
 // that entry, read as windows of 2 kQL 16-byte pieces (two per lane) and walked in registers; the
 // window the interpolation puts t in is loaded with the first probe round and used when the entry
 // found lies inside it.
+#ifndef RMQ_FETCH_PPL
+#define RMQ_FETCH_PPL 2
+#endif
+// header-window pieces per lane: 2 (512 B windows); 4 (1 KB: the whole 1 KB interval in one window)
+// measured slower, 28.1-29.1 vs 26.5-26.8 us per max = 10 fetch (more loads, 6 waves per SIMD)
+constexpr u32 kPPL = RMQ_FETCH_PPL;
+static_assert(kPPL == 2 || kPPL == 4, "two or four pieces per lane");
+
+// The length words of window pieces kPPL*hl .. kPPL*hl + kPPL-1 (16-byte pieces from byte wb).
+struct WinWords {
+  u32 w[4];
+};
+__device__ __forceinline__ WinWords load_window(const uint8_t* ring, u64 wb, u32 hl, u64 mask) {
+  WinWords x{};
+#pragma unroll
+  for (u32 k = 0; k < kPPL; ++k)
+    x.w[k] = *reinterpret_cast<const u32*>(ring + ((wb + 16ull * (kPPL * hl + k) + 8ull) & mask));
+  return x;
+}
+
 __device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v, u64 t, bool act) {
   const u32 lane = lane_id(), h = lane / kQL, hl = lane % kQL;
-  constexpr u32 kWin = 2 * kQL;  // pieces per header window
+  constexpr u32 kWin = kPPL * kQL;  // pieces per header window
   const u32 ilog = st.interval_log2;
   const u64 I = 1ull << ilog;
   const u64* E = st.index + v.rg.ibase * 2;
@@ -78,11 +98,8 @@ __device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v
   } else if (act && t < v.leo) {
     sw = v.start_pos;  // no index entry past the start: the walk starts at the log start
   }
-  u32 Sw0 = 0, Sw1 = 0;
-  if (sw != ~0ull) {
-    Sw0 = *reinterpret_cast<const u32*>(v.ring + ((sw + 32ull * hl + 8ull) & mask));
-    Sw1 = *reinterpret_cast<const u32*>(v.ring + ((sw + 32ull * hl + 24ull) & mask));
-  }
+  WinWords Sw{};
+  if (sw != ~0ull) Sw = load_window(v.ring, sw, hl, mask);
   constexpr u32 kQMask = (1u << kQL) - 1u;
   for (bool first = true; __any(open); first = false) {
     if (!first) {
@@ -123,13 +140,12 @@ __device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v
   if (!act) return 0;
   if (t >= v.leo) return v.used;
   u64 wb = sw;
-  u32 Lw0 = Sw0, Lw1 = Sw1;
+  WinWords Lw = Sw;
   u32 cur = (u32)((c_pos - sw) >> 4);  // window piece of the current record
   if (sw == ~0ull || c_pos < sw || c_pos >= sw + 16ull * kWin) {
     wb = c_pos;
     cur = 0;
-    Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
-    Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
+    Lw = load_window(v.ring, wb, hl, mask);
   }
   u64 k = t - c_off;
   while (__any(k > 0)) {
@@ -138,14 +154,18 @@ __device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v
       if (mv) {
         wb += 16ull * cur;
         cur = 0;
-        Lw0 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 8ull) & mask));
-        Lw1 = *reinterpret_cast<const u32*>(v.ring + ((wb + 32ull * hl + 24ull) & mask));
+        Lw = load_window(v.ring, wb, hl, mask);
       }
     }
-    const u32 src = kQL * h + (cur >> 1);
-    const u32 a0 = (u32)__shfl((int)Lw0, (int)(src & 63u), 64), a1 = (u32)__shfl((int)Lw1, (int)(src & 63u), 64);
+    const u32 src = kQL * h + (cur / kPPL);
+    u32 a = 0;
+#pragma unroll
+    for (u32 q = 0; q < kPPL; ++q) {
+      const u32 x = (u32)__shfl((int)Lw.w[q], (int)(src & 63u), 64);
+      a = (cur % kPPL) == q ? x : a;
+    }
     if (k > 0) {
-      cur += record_bytes((cur & 1u) ? a1 : a0) >> 4;
+      cur += record_bytes(a) >> 4;
       --k;
     }
   }
