@@ -770,7 +770,9 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
         }
         if args.host_steps > 0 and world == 1:
             out["host_path"] = host_leg(eng, host_batches, args.host_steps)
-        if args.fetch_rounds > 0:
+        # the side legs measure one GPU's engine (at N > 1 rank 0 leads only its share of the
+        # partitions, and a rank-0-only rmq_sync could not be collective)
+        if args.fetch_rounds > 0 and world == 1:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
         if args.concurrent_rounds > 0 and world == 1:
             out["mixed"] = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group)
