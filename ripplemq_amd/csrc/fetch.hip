@@ -2,8 +2,8 @@
 // (mq-broker/src/main/java/metadata/raft/PartitionStateMachine.java:85-110), served directly from
 // committed state like MessageBatchReadRequestProcessor.java:39 (no read-index).
 //
-//  resolve (half-wave per request, two per wave: 16,384 requests fit the chip's resident waves in
-//          one round): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
+//  resolve (half-wave per request, two per wave: 16,384 requests are 8,192 waves, about one round
+//          of the chip's resident waves): off = consumerOffsets.getOrDefault(id, 0); end = min(off + max, hw);
 //          byte range of records [off, end): both ends found together, a quarter-wave each, by a
 //          16-ary search of the sparse offset index (FORMAT.md §5: E[m] = first record starting at
 //          or after m*I; 16 probes per round, one round per factor 16 of index entries), then the
@@ -21,7 +21,7 @@
 //          (Round 2 placed with a single 1024-thread workgroup between the two: 12.6 us of the
 //          max = 10 fetch of 16,384 requests with the rest of the GPU idle.)
 //
-// The kernels (a memset of the chunk sums, resolve, gather) run on the engine's fetch stream, after the last pipeline launch the host had
+// The kernels (resolve, gather; the chunk sums a slot's previous gather cleared) run on the engine's fetch stream, after the last pipeline launch the host had
 // issued and before the next one (engine.cpp orders the two streams with events), so the committed
 // state they read is stable and the append pipeline is never flushed for a fetch.
 #include <hip/hip_ext.h>
