@@ -22,6 +22,9 @@
  *   rmq_fetch                   <- PartitionStateMachine.handleBatchRead (:85-110) called from
  *                                  MessageBatchReadRequestProcessor.java:39 (direct read, no read-index)
  *   rmq_become_leader           <- PartitionStateMachine.onLeaderStart(term) (:121-126)
+ *   rmq_vote / rmq_leader_silent <- jraft's RequestVote and election timer of each partition group
+ *                                  (PartitionRaftServer.setupRaft: electionTimeoutMs 1000, raft_meta
+ *                                  term/votedFor, PartitionRaftServer.java:85,89)  [jraft]
  *   rmq_set_replicas            <- PartitionRaftServer.setupRaft initial Configuration(peers)
  *                                  (mq-broker/src/main/java/metadata/raft/PartitionRaftServer.java:82-86)
  *   rmq_create / rmq_destroy    <- PartitionManager.startPartition / PartitionRaftServer.shutdown
@@ -65,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 7u
+#define RMQ_ABI_VERSION 8u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -84,9 +87,12 @@ enum {
   RMQ_EDEVICE = -5,    /* HIP runtime error or no HIP device */
   RMQ_EOFFSET = -6,    /* fetch offset below the retained log start (evicted by retention) */
   RMQ_ENOMEM = -7,
-  RMQ_ESTALE = -8      /* rmq_become_leader: this replica lacks records its partition's leader
+  RMQ_ESTALE = -8,     /* rmq_become_leader: this replica lacks records its partition's leader
                           committed (Raft's vote restriction: it may not lead) */
+  RMQ_ETERM = -9       /* rmq_become_leader: the term already has a leader here (this replica led it,
+                          or voted for another candidate in it: Raft's one vote per term) */
 };
+#define RMQ_NO_VOTE 0xFFFFFFFFu /* rmq_partition_state.voted_for: no vote in voted_term */
 
 /* Memory kind of caller buffers.
    RMQ_MEM_HOST: pageable host memory (rmq_append packs it into a pinned staging slot with host
@@ -169,6 +175,17 @@ typedef struct rmq_partition_state {
                                   (the Raft leaderCommit of the rounds and commit notices it received,
                                   FORMAT.md §9); on the leader its own commit. A replica whose log
                                   ends below it lacks committed records (rmq_become_leader: RMQ_ESTALE) */
+  /* ABI 8: leader election (PartitionRaftServer.java:85,89) */
+  uint64_t last_log_term;      /* Raft's lastLogTerm: the newest term whose leader-start entry this
+                                  replica's log holds (its own term once it leads; on a follower the
+                                  term of the last round entry it accepted that reached its leader's
+                                  term start, 0 = unknown older); compared by rmq_vote */
+  uint64_t voted_term;         /* the term of this replica's last vote (raft_meta votedFor's term) */
+  uint32_t voted_for;          /* the rank it voted for in voted_term (RMQ_NO_VOTE: none) */
+  uint32_t led;                /* 1: this replica led voted_term (rmq_become_leader succeeded in it) */
+  uint64_t heard_round;        /* the round stamp at which this replica last heard its partition's
+                                  leader (a round entry or a commit notice of the current term);
+                                  rmq_leader_silent compares it with the engine's round count */
 } rmq_partition_state;
 
 typedef struct rmq_append_stats {
@@ -240,6 +257,24 @@ int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint
 /* New leader term for pidx (or RMQ_ALL_PARTITIONS): term_start = log_end_offset, so only
    entries appended in this term can advance the commit (Raft current-term rule). */
 int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
+/* Raft RequestVote on this replica (jraft's election, PartitionRaftServer.java:85; the vote persists
+   in raft_meta, :89): a request of an older term is denied; a newer term is adopted first (a leader
+   of pidx steps down: it stops accepting appends, offset commits and fetches); the vote is granted
+   when this replica has not voted for another candidate in `term` and the candidate's log is at least
+   as up to date, (cand_last_log_term, cand_log_end) >= (last_log_term, log_end_offset) in that order.
+   *granted = 1 records the vote (voted_term = term, voted_for = candidate). A candidate votes for
+   itself through this call too, then rmq_become_leader(pidx, term) once a quorum granted. */
+int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, uint64_t cand_last_log_term,
+             uint64_t cand_log_end, uint32_t* granted);
+/* Replay of a persisted vote (raft_meta): voted_term / voted_for of pidx, and the term if newer. */
+int rmq_set_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t voted_for);
+/* Partitions this replica follows whose leader has been silent (jraft's election timeout, 1000 ms,
+   PartitionRaftServer.java:85): no round entry or commit notice of the current term from the leader
+   in the last `silent_rounds` rounds (heard_round + silent_rounds <= the engine's round count) AND
+   none for at least timeout_ms of wall time. out_pidx gets at most cap of them in ascending order,
+   *n = how many there are. A placement change restarts every partition's timer. */
+int rmq_leader_silent(rmq_engine* e, uint32_t silent_rounds, uint32_t timeout_ms, uint32_t* out_pidx,
+                      uint32_t cap, uint32_t* n);
 
 /* Append one batch. Assigns offsets (stable per partition, in batch order), writes the records
    with CRC32C into every local replica log, advances the offset index, the quorum commit and
@@ -337,6 +372,10 @@ int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n);
    them: dst misses those rounds (every entry refused); its other peers and the commit notices of a
    drain still reach it. Not collective. */
 int rmq_fault_isolate(rmq_engine* e, uint32_t dst, uint32_t n);
+/* Fault injection (tests): as rmq_fault_isolate, and the commit notices of the next drain to dst are
+   lost as well: a network partition between this leader and dst (dst's rmq_leader_silent reports the
+   partitions this engine leads toward it). Not collective. */
+int rmq_fault_cut(rmq_engine* e, uint32_t dst, uint32_t n);
 /* Fault injection (tests): the next round this engine sends to rank dst has the byte at `at` of its
    region XORed with 0x5A (at < 0: counted back from the end of the region's data section, i.e. a
    payload byte of its last record), as a link or memory corruption would; the follower refuses the
@@ -385,7 +424,8 @@ int rmq_host_unregister(rmq_engine* e, void* p);
    before its first kernel to one after its last (the request copy before and the result copy after
    outside), launches = kernel executions. enable = k >= 2 also runs every fetch's kernels k times
    back to back (idempotent: the same results), so kernel 4 / launches is a kernel time that no
-   copy or host gap inflates and a rocprofv3 trace shows the kernels back to back. 2: unused. */
+   copy or host gap inflates and a rocprofv3 trace shows the kernels back to back; a fetch with an
+   RMQ_FETCH_COMMIT request runs once (each run would commit). 2: unused. */
 int rmq_profile_enable(rmq_engine* e, int enable);
 int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* total_ms);
 /* Device name / CU count for reports. */

@@ -67,6 +67,9 @@ def load() -> C.CDLL:
         "ro_pair_entries": (u32, [vp, u32, u32]),
         "ro_counters": (None, [vp, vp]),
         "ro_set_segments": (C.c_int, [vp, u32, vp, vp]),
+        "ro_vote": (C.c_int, [vp, u32, u64, u32, u64, u64, C.POINTER(u32)]),
+        "ro_set_vote": (C.c_int, [vp, u32, u64, u32]),
+        "ro_leader_silent": (C.c_int, [vp, u32, vp, u32, C.POINTER(u32)]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -194,6 +197,27 @@ class OracleEngine:
         rc = self.lib.ro_become_leader(self.h, pidx, term)
         if rc:
             raise EngineError(rc, "oracle")
+
+    def vote(self, pidx, term, candidate, cand_last_log_term, cand_log_end) -> bool:
+        g = C.c_uint32(0)
+        rc = self.lib.ro_vote(self.h, pidx, term, candidate, cand_last_log_term, cand_log_end, C.byref(g))
+        if rc:
+            raise EngineError(rc, "oracle")
+        return bool(g.value)
+
+    def set_vote(self, pidx, term, voted_for):
+        rc = self.lib.ro_set_vote(self.h, pidx, term, voted_for)
+        if rc:
+            raise EngineError(rc, "oracle")
+
+    def leader_silent(self, silent_rounds: int, timeout_ms: int = 0) -> np.ndarray:
+        """Followed partitions whose leader was silent for silent_rounds rounds (the oracle keeps no
+        wall clock: timeout_ms is not modelled)."""
+        n = C.c_uint32(0)
+        self.lib.ro_leader_silent(self.h, silent_rounds, None, 0, C.byref(n))
+        out = np.zeros(max(n.value, 1), np.uint32)
+        self.lib.ro_leader_silent(self.h, silent_rounds, _p(out), n.value, C.byref(n))
+        return out[:n.value]
 
     def append(self, pidx, lens, payload, payload_off=None):
         pidx = np.ascontiguousarray(pidx, np.uint32)

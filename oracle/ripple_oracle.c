@@ -127,6 +127,15 @@ typedef struct {
      per commit call touching the partition), per replica slot the newest version its follower
      acknowledged, and the version the last round carried to it (0: no row) */
   uint64_t cver, eackv[RMQ_MAX_RF], rowv[RMQ_MAX_RF];
+  /* leader election (jraft's RequestVote, election timer and raft_meta,
+     PartitionRaftServer.java:85,89): lterm = Raft's lastLogTerm, the newest term whose leader-start
+     entry this log holds (0 = unknown older); mterm = the term in which this log was last verified
+     against its leader's (a round entry accepted, or its own leadership): a commit notice of another
+     term cannot move the commit over a tail never matched in it; heard = the round stamp of the last
+     round entry or commit notice of the current term from the leader; vterm / vfor / led = the last
+     vote (term, candidate) and whether this replica led that term */
+  uint64_t lterm, mterm, heard, vterm;
+  uint32_t vfor, led;
 } ro_part;
 
 struct ro_engine {
@@ -187,6 +196,9 @@ ro_engine* ro_create(const rmq_config* cfg) {
     s->is_leader = 1; /* this engine leads every partition it hosts, term 1 */
     s->term = 1;
     s->term_start = 0;
+    s->lterm = s->mterm = s->vterm = 1; /* led term 1 from creation, its vote its own */
+    s->vfor = cfg->rank;
+    s->led = 1;
     s->key = p;
     s->seg = cfg->segment_bytes;
     s->cons = (uint64_t*)calloc(cfg->max_consumers, sizeof(uint64_t));
@@ -291,7 +303,10 @@ int ro_set_replicas(ro_engine* e, uint32_t p, const uint32_t* ranks, uint32_t rf
   if (s->is_leader && !lead && s->commit > s->lc) s->lc = s->commit; /* a deposed leader knows its commit */
   for (uint32_t r = 0; r < rf; ++r) s->ranks[r] = ranks[r];
   s->leader_slot = leader_slot;
-  s->is_leader = lead;
+  /* a placement keeps or ends this replica's leadership; it never starts one: a replica the placement
+     names leader leads once rmq_become_leader passes Raft's checks (a refused one stays a follower) */
+  s->is_leader = lead && s->is_leader;
+  s->heard = e->round_no; /* the election timer restarts */
   reset_catchup(s);
   /* the followers acknowledge the rows afresh under the new placement: a led partition with
      committed offsets sends its row with the next round */
@@ -310,12 +325,20 @@ static int become_leader_one(ro_engine* e, uint32_t p, uint64_t term) {
       break;
     }
   if (slot == RF) return RMQ_EINVAL; /* no replica of p lives here */
+  /* one leader per term: not a term this replica led, nor one it gave its vote to another candidate */
+  if (s->vterm == term && (s->led || s->vfor != e->cfg.rank)) return RMQ_ETERM;
   return RMQ_OK;
 }
 
 /* Raft's vote restriction as far as a replica can tell: not a leader of a partition whose leader
    committed records its log does not hold. */
-static int become_leader_check(ro_engine* e, uint32_t p) { return e->parts[p].leo < e->parts[p].lc ? RMQ_ESTALE : RMQ_OK; }
+static int become_leader_check(ro_engine* e, uint32_t p) {
+  /* the records this replica's log verifiably shares with its leader: all of it when it was matched in
+     the current term, else its commit (committed records never change) */
+  const ro_part* s = &e->parts[p];
+  const uint64_t verified = s->mterm == s->term ? s->leo : s->commit;
+  return verified < s->lc ? RMQ_ESTALE : RMQ_OK;
+}
 
 static void become_leader_apply(ro_engine* e, uint32_t p, uint64_t term) {
   ro_part* s = &e->parts[p];
@@ -325,6 +348,10 @@ static void become_leader_apply(ro_engine* e, uint32_t p, uint64_t term) {
   s->is_leader = 1;
   s->term = term;
   s->term_start = s->leo; /* jraft: pendingIndex = lastLogIndex + 1 at leader start */
+  s->lterm = s->mterm = term; /* its leader-start entry */
+  s->vterm = term;
+  s->vfor = e->cfg.rank;
+  s->led = 1;
   for (uint32_t r = 0; r < RF; ++r) s->match[r] = s->ranks[r] == e->cfg.rank ? s->leo : 0;
   for (uint32_t r = 0; r < RF; ++r) s->eackv[r] = 0; /* rows acknowledged afresh in the new term */
   commit_eval(e, s);  /* the virtual leader-start entry: a local quorum holds it at once */
@@ -841,6 +868,11 @@ int ro_get_partition_state(ro_engine* e, uint32_t p, rmq_partition_state* o) {
   o->is_leader = s->is_leader;
   o->segment_bytes = s->seg;
   o->leader_commit = s->is_leader ? s->commit : s->lc;
+  o->last_log_term = s->lterm;
+  o->voted_term = s->vterm;
+  o->voted_for = s->vfor;
+  o->led = s->led;
+  o->heard_round = s->heard;
   return RMQ_OK;
 }
 
@@ -1109,6 +1141,10 @@ int ro_round_region(ro_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint
     /* the leader's commit (v4: Raft's leaderCommit), as it stood before the round's records */
     const uint64_t boff = s->leo - s->round_count, lcm = s->commit < boff ? s->commit : boff;
     memcpy(d + 32, &lcm, 8);
+    /* (v5) the term of the entry's last entry as far as the follower may count it: the leader's term
+       when the entry reaches its term start (the leader-start entry), else 0 (an older, unknown term) */
+    const uint64_t ltm = x->first + x->count >= s->term_start ? s->term : 0;
+    memcpy(d + 40, &ltm, 8);
     uint8_t* dd = out + data + 16 * b16;
     /* the catch-up part from the leader's ring, then the round's records (if carried) */
     if (x->gap_bytes) ring_read(s->seg, ring_of(e, s->leader_slot, v[k].p), x->pos0, dd, x->gap_bytes);
@@ -1332,6 +1368,7 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     term &= ~RO_REBASE;
     if (owner) {
       stale = term < s->term; /* a leader of an older term */
+      if (!stale) s->heard = e->round_no; /* its current leader is alive (the election timer restarts) */
       leo = s->leo;
       used = s->used;
       if (!stale && rebase) { /* the log restarts at the entry's first record (its row holds the position) */
@@ -1404,6 +1441,10 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
     }
     if (owner) {
       if (term > s->term) s->term = term;
+      uint64_t ltm;
+      memcpy(&ltm, d + 40, 8);
+      s->lterm = ltm;   /* the entry's last entry term (0: older, unknown) */
+      s->mterm = term;  /* the log now matches the term-`term` leader's through the entry's end */
       if (rebase) {
         if (rebase_log(e, s, leo, used)) {
           free(okv);
@@ -1517,9 +1558,13 @@ int ro_apply_notice(ro_engine* e, uint32_t src, const uint64_t* in, uint32_t n_i
   }
   for (uint32_t k = 0; k < n; ++k) {
     ro_part* s = &e->parts[v[k].p];
-    if (in[2 * k + 1] < s->term) continue;
+    if (in[2 * k + 1] < s->term) continue; /* an older term's (or a lost notice, term 0) */
     s->term = in[2 * k + 1];
-    learn_commit(s, in[2 * k]);
+    s->heard = e->round_no;
+    /* the commit moves over this log only if it was matched in the notice's term; the leader's commit
+       is learned either way (rmq_become_leader's RMQ_ESTALE) */
+    if (s->mterm == s->term) learn_commit(s, in[2 * k]);
+    else if (in[2 * k] > s->lc) s->lc = in[2 * k];
   }
   free(v);
   return RMQ_OK;
@@ -1549,6 +1594,57 @@ uint32_t ro_pair_entries(ro_engine* e, uint32_t src, uint32_t dst) {
   const uint32_t n = pair_entries(e, src, dst, &v);
   free(v);
   return n;
+}
+
+/* Raft RequestVote (rmq_vote): an older term is denied; a newer one adopted (a leader steps down and
+   keeps its commit as the leader's); the vote goes to a candidate whose (lastLogTerm, log end) is at
+   least this replica's, once per term. */
+int ro_vote(ro_engine* e, uint32_t p, uint64_t term, uint32_t cand, uint64_t cand_lterm, uint64_t cand_leo,
+            uint32_t* granted) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  ro_part* s = &e->parts[p];
+  *granted = 0;
+  if (term < s->term) return RMQ_OK;
+  if (term > s->term) {
+    s->term = term;
+    if (s->is_leader) {
+      s->is_leader = 0;
+      if (s->commit > s->lc) s->lc = s->commit;
+    }
+  }
+  const int up = cand_lterm > s->lterm || (cand_lterm == s->lterm && cand_leo >= s->leo);
+  const int free_vote = s->vterm != term || (!s->led && s->vfor == cand);
+  if (up && free_vote) {
+    s->vterm = term;
+    s->vfor = cand;
+    s->led = 0;
+    *granted = 1;
+  }
+  return RMQ_OK;
+}
+
+int ro_set_vote(ro_engine* e, uint32_t p, uint64_t term, uint32_t voted_for) {
+  if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
+  ro_part* s = &e->parts[p];
+  if (term > s->term) s->term = term;
+  s->vterm = term;
+  s->vfor = voted_for;
+  s->led = 0;
+  return RMQ_OK;
+}
+
+/* Followed partitions whose leader was not heard in the last `silent_rounds` rounds (rmq_leader_silent
+   without the wall-clock part). */
+int ro_leader_silent(ro_engine* e, uint32_t silent_rounds, uint32_t* out, uint32_t cap, uint32_t* n) {
+  uint32_t k = 0;
+  for (uint32_t p = 0; p < e->cfg.num_partitions; ++p) {
+    const ro_part* s = &e->parts[p];
+    if (s->is_leader || s->heard + silent_rounds > e->round_no) continue;
+    if (k < cap && out) out[k] = p;
+    ++k;
+  }
+  *n = k;
+  return RMQ_OK;
 }
 
 void ro_counters(ro_engine* e, uint64_t* out) { memcpy(out, e->counters, sizeof e->counters); }

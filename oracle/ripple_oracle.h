@@ -98,6 +98,11 @@ int ro_offset_quorum(ro_engine* e, uint32_t p, uint64_t* cver, uint64_t* cq);
 /* [0] records ingested, [1] entries refused (CRC), [2] refused (log / term / missed round),
    [3] bytes ingested, [4] catch-up entries sent, [5] detached entry plans (gap beyond the ring) */
 void ro_counters(ro_engine* e, uint64_t* out /* [6] */);
+/* Leader election (rmq_vote, rmq_set_vote, rmq_leader_silent without its wall-clock part). */
+int ro_vote(ro_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, uint64_t cand_last_log_term,
+            uint64_t cand_log_end, uint32_t* granted);
+int ro_set_vote(ro_engine* e, uint32_t pidx, uint64_t term, uint32_t voted_for);
+int ro_leader_silent(ro_engine* e, uint32_t silent_rounds, uint32_t* out_pidx, uint32_t cap, uint32_t* n);
 /* Catch-up reserve per destination (FORMAT.md §9): pipeline_depth x (39 max_batch_records +
    max_batch_bytes) bytes. */
 uint64_t ro_catchup_reserve(const rmq_config* cfg);

@@ -15,7 +15,7 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 7
+RMQ_ABI_VERSION = 8
 RMQ_FETCH_COMMIT = 1
 RMQ_FETCH_PINNED_ROWS = 0x100
 RMQ_MAX_RF = 8
@@ -35,6 +35,8 @@ RMQ_EDEVICE = -5
 RMQ_EOFFSET = -6
 RMQ_ENOMEM = -7
 RMQ_ESTALE = -8
+RMQ_ETERM = -9
+RMQ_NO_VOTE = 0xFFFFFFFF
 
 RMQ_MEM_HOST = 0
 RMQ_MEM_DEVICE = 1
@@ -44,7 +46,7 @@ STATUS_NAMES = {
     RMQ_OK: "RMQ_OK", RMQ_PENDING: "RMQ_PENDING", RMQ_ENOTLEADER: "RMQ_ENOTLEADER",
     RMQ_ENOPART: "RMQ_ENOPART", RMQ_EINVAL: "RMQ_EINVAL", RMQ_ENOSPC: "RMQ_ENOSPC",
     RMQ_EDEVICE: "RMQ_EDEVICE", RMQ_EOFFSET: "RMQ_EOFFSET", RMQ_ENOMEM: "RMQ_ENOMEM",
-    RMQ_ESTALE: "RMQ_ESTALE",
+    RMQ_ESTALE: "RMQ_ESTALE", RMQ_ETERM: "RMQ_ETERM",
 }
 
 u32 = C.c_uint32
@@ -86,6 +88,7 @@ class RmqPartitionState(C.Structure):
         ("log_start_pos", u64), ("commit", u64), ("high_watermark", u64), ("term", u64),
         ("term_start", u64), ("match", u64 * RMQ_MAX_RF), ("replica_rank", u32 * RMQ_MAX_RF),
         ("leader_slot", u32), ("is_leader", u32), ("segment_bytes", u64), ("leader_commit", u64),
+        ("last_log_term", u64), ("voted_term", u64), ("voted_for", u32), ("led", u32), ("heard_round", u64),
     ]
 
 
@@ -119,6 +122,9 @@ _SIGS = {
     "rmq_destroy": (None, [vp]),
     "rmq_set_replicas": (C.c_int, [vp, u32, C.POINTER(u32), u32, u32]),
     "rmq_become_leader": (C.c_int, [vp, u32, u64]),
+    "rmq_vote": (C.c_int, [vp, u32, u64, u32, u64, u64, C.POINTER(u32)]),
+    "rmq_set_vote": (C.c_int, [vp, u32, u64, u32]),
+    "rmq_leader_silent": (C.c_int, [vp, u32, u32, vp, u32, C.POINTER(u32)]),
     "rmq_set_segments": (C.c_int, [vp, u32, C.POINTER(u32), C.POINTER(u64)]),
     "rmq_append": (C.c_int, [vp, C.POINTER(RmqBatch), vp, C.POINTER(u64)]),
     "rmq_ack": (C.c_int, [vp, vp, vp, vp, u32]),
@@ -156,6 +162,7 @@ _SIGS = {
     "rmq_fault_drop_rounds": (C.c_int, [vp, u32]),
     "rmq_fault_corrupt": (C.c_int, [vp, u32, C.c_int64]),
     "rmq_fault_isolate": (C.c_int, [vp, u32, u32]),
+    "rmq_fault_cut": (C.c_int, [vp, u32, u32]),
     "rmq_scan_records": (C.c_int, [vp, u64, u64, u64, u32, vp, C.POINTER(u64), C.POINTER(u64)]),
 }
 

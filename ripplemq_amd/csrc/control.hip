@@ -35,6 +35,7 @@ __global__ void become_leader_kernel(DevState st, u32 only) {
   if (p >= st.P || (only != 0xFFFFFFFFu && (blockIdx.x | threadIdx.x))) return;
   const u64 leo = st.leo[p];
   st.term_start[p] = leo;
+  st.lterm[p] = st.mterm[p] = st.term[p];  // its leader-start entry (the host wrote the new term)
   const u32 lm = st.local_mask[p];
   for (u32 r = 0; r < st.RF; ++r) {
     st.match[(u64)p * st.RF + r] = (lm >> r & 1u) ? leo : 0ull;

@@ -230,7 +230,8 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     // default: one wave per task (the workgroups past the resident slots start as stage-1/2
     // workgroups retire); RMQ_WG3_ALL=0 fills only the slots next to the other roles (resident
     // workgroups per CU from the kernel's launch bounds) and the task waves loop over the rest
-    const uint32_t slots = pipeline_wgs_per_cu(PT) * e->cu_count, busy = a.wg1 + a.wg2 + a.wgp;
+    const bool split = e->split && !a.outidx;  // (the apply launch holds no stage-1/2 workgroups)
+    const uint32_t slots = pipeline_wgs_per_cu(PT) * e->cu_count, busy = (split ? 0u : a.wg1 + a.wg2) + a.wgp;
     const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
     a.wg3 = e->wg3_all ? want : std::min<uint32_t>(want, room);
     a.wgb = e->big_wgs ? e->big_wgs : 32u * e->cu_count / (PT / 64u);  // 32 large-record waves per CU
@@ -261,8 +262,39 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
   if (e->trace)  // RMQ_TRACE: the roles of every launch (diagnostics only)
     std::fprintf(stderr, "rmq launch %llu: s1 %u batches %u wgs | s2 %u batches %u wgs | parts %u wgs | s3 %u batches %u wgs + %u big | s4 %u batches\n",
                  (unsigned long long)a.launch_seq, a.g1.nb, a.wg1, a.g2.nb, a.wg2, a.wgp, a.g3.nb, a.wg3, a.wgb, a.g4.nb);
-  launch_pipeline(a, e->main_s, ev_start);
-  HIP_TRY(hipGetLastError());
+  if (e->split && !a.outidx) {
+    // two launches side by side: ranking on rank_s, apply on main_s (rmq_engine::split)
+    PipeArgs ra = a, aa = a;
+    ra.wgp = ra.wg3 = ra.wgb = ra.wgc = ra.s3_lead = 0;
+    ra.done_word = nullptr;
+    aa.wg1 = aa.wg2 = 0;
+    if (ra.wg1 + ra.wg2) {
+      HIP_TRY(hipEventRecord(e->ev_pre_rank, e->main_s));  // apply L - 1 and the control work before it
+      HIP_TRY(hipStreamWaitEvent(e->rank_s, e->ev_pre_rank, 0));
+      launch_pipeline(ra, e->rank_s, ev_start);
+      HIP_TRY(hipGetLastError());
+      ev_start = nullptr;
+      if (e->split == 2) {  // (timing experiment: the two launches one after the other)
+        HIP_TRY(hipEventRecord(e->ev_rank[a.launch_seq & 1u], e->rank_s));
+        e->rank_seq = a.launch_seq;
+      }
+    }
+    if (aa.wgp + aa.wg3 + aa.wgb + aa.wgc) {
+      if (e->rank_seq) {  // the scans of the group it applies (the last rank launch before this one)
+        HIP_TRY(hipStreamWaitEvent(e->main_s, e->ev_rank[e->rank_seq & 1u], 0));
+        e->rank_seq = 0;
+      }
+      launch_pipeline(aa, e->main_s, ev_start);
+      HIP_TRY(hipGetLastError());
+    }
+    if (ra.wg1 + ra.wg2) {
+      HIP_TRY(hipEventRecord(e->ev_rank[a.launch_seq & 1u], e->rank_s));
+      e->rank_seq = a.launch_seq;
+    }
+  } else {
+    launch_pipeline(a, e->main_s, ev_start);
+    HIP_TRY(hipGetLastError());
+  }
   if (s3) {
     e->applied++;
     e->st.leo = nxt.leo;
@@ -478,12 +510,14 @@ void free_engine(rmq_engine* e) {
     // a flush is collective, so the application must have called rmq_sync on every rank
     if (!e->repl) flush(e);
     hipStreamSynchronize(e->main_s);
+    if (e->rank_s) hipStreamSynchronize(e->rank_s);
     dump_stamps(e);
   }
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq, e->d_crc,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq,
+                             s.lterm, s.mterm, s.heard, e->d_crc,
                              e->d_stats, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (rmq_engine::FetchSlot& f : e->fslot) {
     void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_out};
@@ -500,7 +534,7 @@ void free_engine(rmq_engine* e) {
     bufs.push_back(z.used);
   }
   for (const PipeScratch& x : e->scratch) {
-    void* xs[] = {x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.bacc, x.nbig, x.bigl};
+    void* xs[] = {x.hist32, x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.bacc, x.nbig, x.bigl};
     for (void* p : xs) bufs.push_back(p);
   }
   delete e->copy_pool;
@@ -521,6 +555,10 @@ void free_engine(rmq_engine* e) {
     if (cs.ev) hipEventDestroy(cs.ev);
   }
   if (e->ev_main) hipEventDestroy(e->ev_main);
+  for (hipEvent_t ev : e->ev_rank)
+    if (ev) hipEventDestroy(ev);
+  if (e->ev_pre_rank) hipEventDestroy(e->ev_pre_rank);
+  if (e->rank_s) hipStreamDestroy(e->rank_s);
   if (e->fetch_s) hipStreamDestroy(e->fetch_s);
   if (e->fetch_out_s) hipStreamDestroy(e->fetch_out_s);
   if (e->copy_s) hipStreamDestroy(e->copy_s);
@@ -644,6 +682,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_STEAL")) e->steal = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_AHEAD")) e->max_ahead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
+  if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
+  if (e->stamps_path || e->steal) e->split = 0;  // (phase stamps and stealing read one launch's roles)
 #define CREATE_TRY(x)      \
   do {                     \
     int _r = (x);          \
@@ -661,7 +702,21 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_VERIFY_WGS")) e->verify_wgs = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("RMQ_BIG_WGS")) e->big_wgs = (uint32_t)std::atoi(v);
   std::snprintf(e->dev_name, sizeof e->dev_name, "%s (%s)", prop.name, prop.gcnArchName);
-  CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
+  if (e->split && e->rank_cus && e->rank_cus < e->cu_count) {
+    // CU masks (bit i = the i-th CU in the runtime's numbering): the rank stream takes the first
+    // rank_cus bits, the pipeline stream the rest
+    std::vector<uint32_t> mr((e->cu_count + 31) / 32, 0u), mm(mr.size(), 0u);
+    for (uint32_t i = 0; i < e->cu_count; ++i) (i < e->rank_cus ? mr : mm)[i / 32] |= 1u << (i % 32);
+    CREATE_HIP(hipExtStreamCreateWithCUMask(&e->main_s, (uint32_t)mm.size(), mm.data()));
+    CREATE_HIP(hipExtStreamCreateWithCUMask(&e->rank_s, (uint32_t)mr.size(), mr.data()));
+  } else {
+    CREATE_HIP(hipStreamCreateWithFlags(&e->main_s, hipStreamNonBlocking));
+    if (e->split) CREATE_HIP(hipStreamCreateWithFlags(&e->rank_s, hipStreamNonBlocking));
+  }
+  if (e->split) {
+    for (hipEvent_t& ev : e->ev_rank) CREATE_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&e->ev_pre_rank, hipEventDisableTiming));
+  }
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_out_s, hipStreamNonBlocking));
   preload_fetch_kernels();
@@ -720,6 +775,9 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&s.cdirty, P));
   CREATE_TRY(dalloc(&s.lcommit, P));
+  CREATE_TRY(dalloc(&s.lterm, P));
+  CREATE_TRY(dalloc(&s.mterm, P));
+  CREATE_TRY(dalloc(&s.heard, P));
   CREATE_TRY(dalloc(&s.cver, P));
   CREATE_TRY(dalloc(&s.cq, P));
   e->cver.assign(P, 0ull);
@@ -727,10 +785,11 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->max_tiles = (cfg->max_batch_records + kTileRecs - 1) / kTileRecs;
   e->max_tasks = (cfg->max_batch_records + kTaskRecs - 1) / kTaskRecs;
   CREATE_TRY(dalloc(&e->d_stats, (size_t)kStatsRing * e->max_tasks));
-  // even: stage 2 reads hist columns with 16-byte loads
-  e->max_group_tiles = (std::min<uint32_t>(kMaxTiles, e->group_max * e->max_tiles) + 1u) & ~1u;
+  // a multiple of four: stage 2 reads u32 hist columns with 16-byte loads
+  e->max_group_tiles = (std::min<uint32_t>(kMaxTiles, e->group_max * e->max_tiles) + 3u) & ~3u;
   for (PipeScratch& x : e->scratch) {
     const size_t GT = e->max_group_tiles, TP = GT * P;
+    CREATE_TRY(dalloc(&x.hist32, TP));
     CREATE_TRY(dalloc(&x.hist, TP));
     CREATE_TRY(dalloc(&x.excl, TP));
     CREATE_TRY(dalloc(&x.totals, P));
@@ -771,6 +830,12 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   e->ranks.assign((size_t)P * RF, cfg->rank);
   e->term.assign(P, 1ull);
   CREATE_HIP(hipMemcpy(s.term, e->term.data(), P * 8ull, hipMemcpyHostToDevice));
+  // every partition is led here from term 1 (its leader-start entry, its own vote)
+  CREATE_HIP(hipMemcpy(s.lterm, e->term.data(), P * 8ull, hipMemcpyHostToDevice));
+  CREATE_HIP(hipMemcpy(s.mterm, e->term.data(), P * 8ull, hipMemcpyHostToDevice));
+  e->vterm.assign(P, 1ull);
+  e->vfor.assign(P, cfg->rank);
+  e->vled.assign(P, 1u);
   e->key.resize(P);
   for (uint32_t p = 0; p < P; ++p) e->key[p] = p;
   e->ticket_n.assign(kStatsRing, 0u);
@@ -814,7 +879,9 @@ int set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_
     e->leader_slot[p] = leader_slot[i];
     const uint32_t lead = ranks[(size_t)i * RF + leader_slot[i]] == e->cfg.rank;
     if (e->is_leader[p] && !lead) demoted.push_back(p);
-    e->is_leader[p] = lead;
+    // a placement keeps or ends this replica's leadership; it never starts one: a replica the
+    // placement names leader leads once rmq_become_leader passes Raft's checks
+    e->is_leader[p] = lead && e->is_leader[p];
     if (key) e->key[p] = key[i];
   }
   if (!demoted.empty()) {  // a former leader knows its own commit as the leader's (FORMAT.md §9 v4)
@@ -830,6 +897,14 @@ int set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_
   }
   HIP_TRY(hipMemcpy(e->st.is_leader, e->is_leader.data(), P * 4ull, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->st.local_mask, mask.data(), P * 4ull, hipMemcpyHostToDevice));
+  if (n) {  // the election timer of every placed partition restarts
+    std::vector<uint64_t> hd(P);
+    HIP_TRY(hipMemcpy(hd.data(), e->st.heard, P * 8ull, hipMemcpyDeviceToHost));
+    const uint64_t cur = e->repl ? e->repl->stamp : 0ull;
+    for (uint32_t i = 0; i < n; ++i) hd[pidx[i]] = cur;
+    HIP_TRY(hipMemcpy(e->st.heard, hd.data(), P * 8ull, hipMemcpyHostToDevice));
+    e->place_time = std::chrono::steady_clock::now();
+  }
   return e->repl ? repl_set_lists(e) : RMQ_OK;
 }
 
@@ -870,16 +945,27 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   // a follower adopts newer leader terms from replication rounds (FORMAT.md §9): the device holds
   // the current terms
   HIP_TRY(hipMemcpy(&e->term[lo], e->st.term + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
-  for (uint32_t p = lo; p < hi; ++p)
+  for (uint32_t p = lo; p < hi; ++p) {
     if (term < e->term[p]) return RMQ_EINVAL;
+    // one leader per term: not a term this replica led, nor one it gave its vote to another candidate
+    if (e->vterm[p] == term && (e->vled[p] || e->vfor[p] != e->cfg.rank)) return RMQ_ETERM;
+  }
   {
     // Raft's vote restriction, as far as this replica can tell: it may not lead a partition whose
-    // leader committed records its log does not hold (leader_commit from rounds and commit notices)
-    std::vector<uint64_t> leo(hi - lo), lc(hi - lo);
-    HIP_TRY(hipMemcpy(leo.data(), e->st.leo + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(lc.data(), e->st.lcommit + lo, (size_t)(hi - lo) * 8, hipMemcpyDeviceToHost));
-    for (uint32_t p = lo; p < hi; ++p)
-      if (leo[p - lo] < lc[p - lo]) return RMQ_ESTALE;  // (a partition always led here: lc = 0)
+    // leader committed records its log does not verifiably hold (leader_commit from rounds and
+    // commit notices; verified: the whole log when it was matched in the current term, else the
+    // replica's own commit)
+    const size_t m = hi - lo;
+    std::vector<uint64_t> leo(m), lc(m), mt(m), cm(m);
+    HIP_TRY(hipMemcpy(leo.data(), e->st.leo + lo, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(lc.data(), e->st.lcommit + lo, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(mt.data(), e->st.mterm + lo, m * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cm.data(), e->st.commit + lo, m * 8, hipMemcpyDeviceToHost));
+    for (uint32_t p = lo; p < hi; ++p) {
+      const size_t i = p - lo;
+      const uint64_t verified = mt[i] == e->term[p] ? leo[i] : cm[i];
+      if (verified < lc[i]) return RMQ_ESTALE;  // (a partition always led here: lc = 0)
+    }
   }
   for (uint32_t p = lo; p < hi; ++p) {
     uint32_t slot = e->leader_slot[p];
@@ -890,6 +976,9 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
     e->leader_slot[p] = slot;
     e->is_leader[p] = 1;
     e->term[p] = term;
+    e->vterm[p] = term;  // a leader's vote is its own
+    e->vfor[p] = e->cfg.rank;
+    e->vled[p] = 1;
   }
   HIP_TRY(hipMemcpy(e->st.is_leader + lo, &e->is_leader[lo], (size_t)(hi - lo) * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(e->st.term + lo, &e->term[lo], (size_t)(hi - lo) * 8, hipMemcpyHostToDevice));
@@ -899,6 +988,94 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   // Raft's leader start: nextIndex of every follower = the leader's last index + 1
   if (!rc && e->repl) rc = reset_catchup(e);
   return rc;
+}
+
+int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, uint64_t cand_last_log_term,
+             uint64_t cand_log_end, uint32_t* granted) {
+  if (!e || !granted) return RMQ_EINVAL;
+  *granted = 0;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = drain(e);
+  if (rc) return rc;
+  uint64_t cur = 0, lterm = 0, leo = 0;
+  HIP_TRY(hipMemcpy(&cur, e->st.term + pidx, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&lterm, e->st.lterm + pidx, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&leo, e->st.leo + pidx, 8, hipMemcpyDeviceToHost));
+  if (term < cur) return RMQ_OK;  // a candidate of an older term
+  if (term > cur) {  // Raft: a newer term is adopted; a leader steps down
+    e->term[pidx] = term;
+    HIP_TRY(hipMemcpy(e->st.term + pidx, &term, 8, hipMemcpyHostToDevice));
+    if (e->is_leader[pidx]) {
+      rc = equalize_state_sets(e);
+      if (rc) return rc;
+      uint64_t c = 0, lc = 0;
+      HIP_TRY(hipMemcpy(&c, e->st.commit + pidx, 8, hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(&lc, e->st.lcommit + pidx, 8, hipMemcpyDeviceToHost));
+      if (c > lc) HIP_TRY(hipMemcpy(e->st.lcommit + pidx, &c, 8, hipMemcpyHostToDevice));  // (FORMAT.md §9 v4)
+      e->is_leader[pidx] = 0;
+      const uint32_t z = 0;
+      HIP_TRY(hipMemcpy(e->st.is_leader + pidx, &z, 4, hipMemcpyHostToDevice));
+    }
+  }
+  const bool up = cand_last_log_term > lterm || (cand_last_log_term == lterm && cand_log_end >= leo);
+  const bool free_vote = e->vterm[pidx] != term || (!e->vled[pidx] && e->vfor[pidx] == candidate);
+  if (up && free_vote) {
+    e->vterm[pidx] = term;
+    e->vfor[pidx] = candidate;
+    e->vled[pidx] = 0;
+    *granted = 1;
+  }
+  return RMQ_OK;
+}
+
+int rmq_set_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t voted_for) {
+  if (!e) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = drain(e);
+  if (rc) return rc;
+  uint64_t cur = 0;
+  HIP_TRY(hipMemcpy(&cur, e->st.term + pidx, 8, hipMemcpyDeviceToHost));
+  if (term > cur) {
+    e->term[pidx] = term;
+    HIP_TRY(hipMemcpy(e->st.term + pidx, &term, 8, hipMemcpyHostToDevice));
+  }
+  e->vterm[pidx] = term;
+  e->vfor[pidx] = voted_for;
+  e->vled[pidx] = 0;
+  return RMQ_OK;
+}
+
+int rmq_leader_silent(rmq_engine* e, uint32_t silent_rounds, uint32_t timeout_ms, uint32_t* out_pidx, uint32_t cap,
+                      uint32_t* n) {
+  if (!e || !n || (cap && !out_pidx)) return RMQ_EINVAL;
+  *n = 0;
+  std::lock_guard<std::mutex> g(e->mu);
+  const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
+  HIP_TRY(hipSetDevice(e->device));
+  if (e->repl) HIP_TRY(hipStreamSynchronize(e->repl->xchg_s));  // (the rounds' ingest writes the words)
+  std::vector<uint64_t> hd(P);
+  HIP_TRY(hipMemcpy(hd.data(), e->st.heard, P * 8ull, hipMemcpyDeviceToHost));
+  const uint64_t cur = e->repl ? e->repl->stamp : 0ull;
+  const auto now = std::chrono::steady_clock::now();
+  uint32_t k = 0;
+  for (uint32_t p = 0; p < P; ++p) {
+    if (e->is_leader[p]) continue;
+    bool local = false;
+    for (uint32_t r = 0; r < RF; ++r) local |= e->ranks[(size_t)p * RF + r] == e->cfg.rank;
+    if (!local || hd[p] + silent_rounds > cur) continue;
+    // wall time since the leader was last heard (the round's posting, or the placement)
+    auto at = e->place_time;
+    if (e->repl && hd[p] && cur - hd[p] < 64) at = std::max(at, e->repl->stamp_time[hd[p] % 64]);
+    if (std::chrono::duration_cast<std::chrono::milliseconds>(now - at).count() < (long long)timeout_ms) continue;
+    if (k < cap) out_pidx[k] = p;
+    ++k;
+  }
+  *n = k;
+  return RMQ_OK;
 }
 
 int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* seg) {
@@ -1067,6 +1244,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
     }
     HIP_TRY(hipEventRecord(sg.ev_in, e->copy_s));
     HIP_TRY(hipStreamWaitEvent(e->main_s, sg.ev_in, 0));  // before the group's first launch
+    if (e->rank_s) HIP_TRY(hipStreamWaitEvent(e->rank_s, sg.ev_in, 0));  // (its ranking, split launches)
     f.b.pidx = reinterpret_cast<const uint32_t*>(sg.d_blk);
     f.b.len = reinterpret_cast<const uint32_t*>(sg.d_blk + o_len);
     f.b.poff = b->payload_off ? reinterpret_cast<const uint64_t*>(sg.d_blk + o_poff) : nullptr;
@@ -1440,8 +1618,8 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     e->fetch_done.push_back({old, (uint64_t)(int64_t)rc, used});
   }
   // RMQ_FETCH_COMMIT: known flags only, one committing request per (partition, consumer)
+  bool any = false;
   {
-    bool any = false;
     for (uint32_t r = 0; r < n; ++r) {
       if (reqs[r].flags & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
       any |= (reqs[r].flags & RMQ_FETCH_COMMIT) != 0;
@@ -1504,7 +1682,9 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
     if (!sync) HIP_TRY(hipStreamWaitEvent(e->fetch_s, f.ev_in, 0));
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
-    const uint32_t runs = e->profile ? e->fetch_replay : 1u;
+    // (profiling replays a fetch's kernels back to back; a committing fetch runs once: each run
+    // would commit again and the next would read from the committed offset)
+    const uint32_t runs = e->profile && !any ? e->fetch_replay : 1u;
     if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run, copies outside
       for (hipEvent_t& x : ev) x = pool_event(e);
       for (int k = 0; k < 2; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
@@ -1610,6 +1790,11 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   o->segment_bytes = 1ull << (e->ring[p] & 63ull);
   if (o->is_leader) o->leader_commit = o->commit;
   else HIP_TRY(hipMemcpy(&o->leader_commit, s.lcommit + p, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&o->last_log_term, s.lterm + p, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&o->heard_round, s.heard + p, 8, hipMemcpyDeviceToHost));
+  o->voted_term = e->vterm[p];
+  o->voted_for = e->vfor[p];
+  o->led = e->vled[p];
   return RMQ_OK;
 }
 
@@ -1623,9 +1808,11 @@ int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_part
   int rc = quiesce(e);
   if (rc) return rc;
   const DevState& s = e->st;
-  uint64_t* const src[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term, s.term_start, s.lcommit};
-  std::vector<uint64_t> v((size_t)n * 9), m((size_t)n * RF);
-  for (int f = 0; f < 9; ++f)
+  uint64_t* const src[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term, s.term_start, s.lcommit,
+                           s.lterm, s.heard};
+  constexpr int NF = sizeof src / sizeof src[0];
+  std::vector<uint64_t> v((size_t)n * NF), m((size_t)n * RF);
+  for (int f = 0; f < NF; ++f)
     HIP_TRY(hipMemcpy(v.data() + (size_t)f * n, src[f] + first, (size_t)n * 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(m.data(), s.match + (size_t)first * RF, (size_t)n * RF * 8, hipMemcpyDeviceToHost));
   for (uint32_t i = 0; i < n; ++i) {
@@ -1648,6 +1835,11 @@ int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_part
     x.is_leader = e->is_leader[p];
     x.segment_bytes = 1ull << (e->ring[p] & 63ull);
     x.leader_commit = x.is_leader ? x.commit : v[8ull * n + i];
+    x.last_log_term = v[9ull * n + i];
+    x.heard_round = v[10ull * n + i];
+    x.voted_term = e->vterm[p];
+    x.voted_for = e->vfor[p];
+    x.led = e->vled[p];
   }
   return RMQ_OK;
 }
@@ -1879,6 +2071,14 @@ int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n) {
   if (!e->repl) return RMQ_EINVAL;
   e->repl->drop_from = e->last_ticket + 1;
   e->repl->drop_n = n;
+  return RMQ_OK;
+}
+
+int rmq_fault_cut(rmq_engine* e, uint32_t dst, uint32_t n) {
+  int rc = rmq_fault_isolate(e, dst, n);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> g(e->mu);
+  e->repl->cut_notice |= 1u << dst;
   return RMQ_OK;
 }
 

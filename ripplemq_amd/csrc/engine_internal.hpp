@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <array>
+#include <chrono>
 #include <deque>
 #include <mutex>
 #include <new>
@@ -215,6 +216,9 @@ struct Replication {
   // rmq_fault_isolate: the next iso_n[q] rounds (groups from ticket iso_from[q] on) to q are lost
   uint64_t iso_from[kMaxWorld] = {};
   uint32_t iso_n[kMaxWorld] = {};
+  uint32_t cut_notice = 0;      // rmq_fault_cut: bit q, the next drain's commit notices to q are lost
+  uint64_t stamp = 0;           // round stamp: the last round posted for ingest, + 1 (heard words)
+  std::chrono::steady_clock::time_point stamp_time[64];  // when stamp s was posted, at [s % 64]
   // rmq_fault_corrupt: the next round to destination q flips the byte at flip_at[q]
   bool flip[kMaxWorld] = {};
   int64_t flip_at[kMaxWorld] = {};
@@ -310,6 +314,11 @@ struct rmq_engine {
   // host mirrors of control state
   std::vector<uint32_t> is_leader, leader_slot, ranks;  // ranks [P][RF]
   std::vector<uint64_t> term;
+  // votes (Raft's votedFor per term, raft_meta): the term of the last vote, the candidate, and whether
+  // this replica led that term (rmq_become_leader succeeded in it)
+  std::vector<uint64_t> vterm;
+  std::vector<uint32_t> vfor, vled;
+  std::chrono::steady_clock::time_point place_time = std::chrono::steady_clock::now();  // last placement
   // fetch: its own stream and scratch, serialised by fetch_mu (engine state under mu only while
   // the fetch is ordered against the pipeline stream)
   std::mutex fetch_mu;
@@ -413,6 +422,19 @@ struct rmq_engine {
   uint32_t s3_first = 1;  // stage-3 workgroups first in dispatch order (RMQ_S3_FIRST=0: last)
   uint32_t s3_lead = 0;   // stage-3 workgroups before the other roles (RMQ_S3_LEAD; 0: all of them)
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
+  // Split launches (single-GPU kernel, no transport): each pipeline step is two launches of the
+  // pipeline kernel that run side by side, the ranking roles (stage 1 of group g, stage 2 of g - 1)
+  // on rank_s and the apply roles (stage 3 of g - 2, partition threads, stage 4) on main_s. Rank
+  // launch L waits for everything main_s issued before it (apply L - 1 resets the set stage 1 of L
+  // reuses); apply launch L waits for rank launch L - 1 (the scans of the group it applies).
+  // RMQ_SPLIT=1 (2: the two launches one after the other, timing only); 0 default: one launch per
+  // step with every role (the split measured slower: 60 vs 49 us per step).
+  uint32_t split = 0;
+  uint32_t rank_cus = 0;        // RMQ_RANK_CUS=n: rank_s runs on n CUs and main_s on the others
+  hipStream_t rank_s = nullptr;
+  hipEvent_t ev_rank[2] = {nullptr, nullptr};  // rank launch L recorded in slot L & 1
+  hipEvent_t ev_pre_rank = nullptr;            // main_s before a rank launch
+  uint64_t rank_seq = 0;        // the last launch that had a rank launch (0: none)
   std::vector<uint64_t> key;  // [P] placement key of each partition (FORMAT.md §9 list order)
   rmq::Replication* repl = nullptr;  // replication transport attached (collective mode)
 };

@@ -18,9 +18,16 @@ constexpr uint32_t kTileIdxBits = RMQ_TILE_BITS;       // log2(kTileRecs)
 constexpr uint32_t kTileRecs = 1u << kTileIdxBits;     // records per ranking tile (stage 1)
 constexpr uint32_t kMaxTiles = 512;      // tiles per group (stage 2 keeps their payload bases in LDS)
 #ifndef RMQ_SCAN_LANES
-#define RMQ_SCAN_LANES 32
+#define RMQ_SCAN_LANES 16
 #endif
-constexpr uint32_t kScanLanes = RMQ_SCAN_LANES;  // stage 2: threads per partition column
+constexpr uint32_t kScanLanes = RMQ_SCAN_LANES;  // stage 2: threads per partition column (8, 16 or 32)
+// Stage 1 -> 2 tile cells (hist32): count of the (tile, partition) run in the high bits, its record
+// bytes / 16 in the low kCellCntShift bits; kCellWide marks a run too large for that (its value is in
+// the u64 hist cell at the same index). A count never reaches the field's all-ones value.
+constexpr uint32_t kCellCntShift = kTileRecs <= 1024u ? 21u : 20u;
+constexpr uint32_t kCellB16 = (1u << kCellCntShift) - 1u;
+constexpr uint32_t kCellWide = ~0u;
+static_assert((kTileRecs >> (32u - kCellCntShift)) == 0u, "a tile's count fits its cell field below all-ones");
 #ifndef RMQ_SCAN_COLS
 #define RMQ_SCAN_COLS 1
 #endif
@@ -142,6 +149,11 @@ struct DevState {
                          //   that launch's partition threads fold in meanwhile)
   uint32_t csnap_slot;   // the slot of the last launch issued (control kernels write it)
   // consumer-offset rows on a quorum (rmq_commit_consumer_offset tickets, FORMAT.md §8)
+  // leader election: Raft's lastLogTerm, the term this log was last verified in
+  // against its leader's, and the round stamp of the last entry or notice heard from the leader
+  uint64_t* lterm;       // [P]
+  uint64_t* mterm;       // [P]
+  uint64_t* heard;       // [P]
   uint64_t* cver;        // [P] leader: version of the partition's row (one per commit call touching it)
   uint64_t* cq;          // [P] leader: the newest row version a quorum of its replicas holds
   const uint32_t* outidx;  // [P][RF] out entry of (partition, remote slot), ~0: none (transport), or null
@@ -209,7 +221,8 @@ struct PipeGroup {
 // Group-local scratch of one pipeline set (four sets rotate: a group is ranked in launch k,
 // scanned in k+1, applied in k+2 and its retention evaluated in k+3).
 struct PipeScratch {
-  uint64_t* hist;       // [P][gt] tile aggregate {count << 40 | bytes/16}; 0 = absent (stage 2 clears)
+  uint32_t* hist32;     // [P][gt] tile cell (kCellCntShift packing, kCellWide); 0 = absent (stage 2 clears)
+  uint64_t* hist;       // [P][gt] tile aggregate {count << 40 | bytes/16} of a kCellWide cell only
   uint64_t* excl;       // [P][gt] exclusive prefix over the group's accepted cells (bit 63: the
                         //   cell's (batch, partition) is rejected for space, FORMAT.md §3)
   uint64_t* totals;     // [P] group aggregate over accepted cells
@@ -341,6 +354,7 @@ struct IngestArgs {
   uint32_t items_grid;       // copy workgroups launched: items past it are never copied
   const CrcConsts* crc;
   uint64_t* counters;        // [4] records ingested, entries refused (CRC), refused (log mismatch), bytes
+  uint64_t stamp;            // the round's stamp (its number + 1): heard words of the entries from a live leader
 };
 constexpr uint64_t kCopyChunk = 16ull << 10;  // follower copy: region bytes per workgroup
 
@@ -354,6 +368,7 @@ struct NoticeArgs {
   const uint32_t* xi_p;      // [n_in]
   const uint64_t* in;        // [n_in][2]
   uint32_t n_out, n_in;
+  uint64_t stamp;            // the drain's round stamp (heard words)
 };
 
 // Acks of one round applied outside the pipeline (drain): thread per partition.

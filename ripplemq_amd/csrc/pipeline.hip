@@ -159,6 +159,19 @@ __device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
+// A present (tile, partition) run's cell {count << 40 | bytes/16}: packed into the u32 column that
+// stage 2 reads, or, for a run of more than kCellB16 16-byte units, kCellWide there and the value in
+// the u64 cell at the same index.
+__device__ __forceinline__ void put_cell(const PipeScratch& x, u64 at, u64 v) {
+  const u64 b16 = v & kLow40;
+  u32 c = ((u32)(v >> 40) << kCellCntShift) | (u32)b16;
+  if (b16 > kCellB16) {
+    x.hist[at] = v;
+    c = kCellWide;
+  }
+  x.hist32[at] = c;
+}
+
 // srow: the stamp row of the tile (diagnostics): its dedicated stage-1 workgroup's, also when a
 // stage-3 workgroup ranks it
 __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem& S, u32 srow) {
@@ -363,7 +376,7 @@ __device__ __forceinline__ void stage1_tile(const PipeArgs& A, u32 t, Stage1Smem
       x.crank[gbase + q] = make_uint2((u32)(ex >> 40) | (f << kFlagShift), (u32)(ex & kLow40));
     }
     const u32 nkey = s + 1 < kTR ? (sorted[s + 1] >> kIB) : 0xFFFFFFFFu;
-    if (nkey != key && (v >> 40)) x.hist[(u64)key * A.gt + t] = v;
+    if (nkey != key && (v >> 40)) put_cell(x, (u64)key * A.gt + t, v);
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP_ROW(srow, 3);
@@ -566,7 +579,7 @@ __device__ __forceinline__ void stage1_tile_hash(const PipeArgs& A, u32 t, Stage
   // ---- the tile's aggregate of every present partition (the sparse hist cells)
   for (u32 k = tid; k < kHT; k += kPT) {
     const u32 kv = S.key[k];
-    if (kv) x.hist[(u64)(kv - 1u) * A.gt + t] = S.val[k];
+    if (kv) put_cell(x, (u64)(kv - 1u) * A.gt + t, S.val[k]);
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   PIPE_STAMP_ROW(srow, 4);
@@ -677,7 +690,7 @@ __device__ __forceinline__ void plan_decide(const PipeArgs& A, u32 p, u32 e, u64
   store_sc1(dw + 1, Boff);
   store_sc1(dw + 3, st.term[p]);
   store_sc1(dw + 4, X.csnap[p]);  // the leader's commit as the launch started (FORMAT.md §9 v4)
-  store_sc1(dw + 5, 0ull);
+  store_sc1(dw + 5, st.term[p]);  // (v5) the entry reaches the leader's term start: its term
   store_sc1(&X.xnext[2 * e], Boff + (tot >> 40));
   store_sc1(&X.xnext[2 * e + 1], Bpos + 16ull * (tot & kLow40));
 }
@@ -860,6 +873,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
         u64 cnt = rcnt, b16 = rb16, gcnt = 0, gb16 = 0, first = f_off;
         u64 nx_off = 0, nx_pos = 0;
         bool with_round = true, set_cu = false, cu_entry = false;
+        bool below_ts = false;  // a partial catch-up ending below the leader's term start (v5 word: 0)
         const u64 t3 = A.g3.nb ? cur.t3 : 0ull;
         const u64 Boff = in ? cur.leo + (t3 >> 40) : 0ull;
         const u64 Bpos = in ? cur.used + 16ull * (t3 & kLow40) : 0ull;
@@ -881,6 +895,7 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
                 gcnt = cnt = xo - f_off;
                 gb16 = b16 = (xp - f_pos) >> 4;
                 with_round = false;
+                below_ts = xo < st.term_start[p];
                 nx_off = xo;
                 nx_pos = xp;
                 set_cu = cu_entry = true;
@@ -921,7 +936,8 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
           // (loaded here, not with the entry's prefetched inputs: two more live registers per
           // prefetched entry pushed the transport kernel into 3.5 KB of scratch per lane)
           const u64 lcm = X.csnap[p];
-          de[2] = make_uint4((u32)lcm, (u32)(lcm >> 32), 0u, 0u);
+          const u64 ltm = below_ts ? 0ull : cur.term;  // (v5) the term of the entry's last entry, as counted
+          de[2] = make_uint4((u32)lcm, (u32)(lcm >> 32), (u32)ltm, (u32)(ltm >> 32));
           XEntry xe;
           xe.data_abs = kNoRound;
           xe.tab_abs = 0;
@@ -1052,87 +1068,171 @@ __device__ __forceinline__ void stage2_plan(const PipeArgs& A, u64* s_f) {
 
 // s_ex: kMaxTiles words of the launch's dynamic LDS (static arrays would add to every role's LDS)
 constexpr u32 kCL = 256 / kScanLanes;  // stage 2: tiles per thread per column chunk (chunks of 256 tiles)
+static_assert(kScanLanes == 8 || kScanLanes == 16 || kScanLanes == 32, "stage 2 lane groups: 8, 16 or 32 lanes");
+static_assert(kCL % 4 == 0, "stage 2 loads four u32 cells at a time");
 
-// Tiles [t, t + kCL) of a hist column (zero past the group's T tiles): 16-byte loads, the column
-// stride (gt) being even.
-__device__ __forceinline__ void load_column_chunk(const u64* col, u32 t, u32 T, u64 (&h)[kCL]) {
+// A packed tile cell as stage 2 scans it: {count << 40 | bytes/16} of one (tile, partition) run.
+__device__ __forceinline__ u64 cell_value(u32 c) {
+  return ((u64)(c >> kCellCntShift) << 40) | (c & kCellB16);
+}
+
+// Tiles [t, t + kCL) of a hist column: 16-byte loads of four u32 cells, the column stride (gt) being
+// a multiple of four. A cell past the group's T tiles inside the column is zero (stage 1 writes the
+// present cells of tiles below T, stage 2 clears what it reads), and no load passes the column.
+__device__ __forceinline__ void load_column_chunk(const u32* col, u32 t, u32 T, u32 (&h)[kCL]) {
 #pragma unroll
-  for (u32 k = 0; k < kCL; k += 2) {
+  for (u32 k = 0; k < kCL; k += 4) {
     uint4 v = make_uint4(0, 0, 0, 0);
     if (t + k < T) v = *reinterpret_cast<const uint4*>(col + t + k);
-    h[k] = ((u64)v.y << 32) | v.x;
-    h[k + 1] = t + k + 1 < T ? ((u64)v.w << 32) | v.z : 0ull;
+    h[k] = v.x;
+    h[k + 1] = v.y;
+    h[k + 2] = v.z;
+    h[k + 3] = v.w;
   }
 }
 
 __device__ __forceinline__ void load_column_group(const PipeScratch& x, u32 cg, u32 P, u32 GT, u32 s, u32 T,
-                                                  u64 (&h)[kScanCols][kCL]) {
+                                                  u32 (&h)[kScanCols][kCL]) {
 #pragma unroll
   for (u32 c = 0; c < kScanCols; ++c) {
     const u32 p = cg * kScanCols + c;
-    if (p < P) load_column_chunk(x.hist + (u64)p * GT, kCL * s, T, h[c]);
+    if (p < P) load_column_chunk(x.hist32 + (u64)p * GT, kCL * s, T, h[c]);
   }
 }
 
-// Column p of the group: per batch, the exclusive scan of the column over the batch's tiles, read
-// in chunks of kScanLanes * kCL tiles (thread s holding tiles [kCL s, kCL s + kCL) of the chunk;
-// h = the first chunk, already loaded), the batches overlapping a chunk scanned from those registers
-// one after another.
-__device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u32 rm, u64 (&h)[kCL]) {
+// Inclusive scan inside aligned groups of kScanLanes lanes: DPP row moves inside each row of 16
+// (a lane below the shift inside its group takes nothing), and for 32-lane groups rows 1 / 3 take
+// the last lane of rows 0 / 2 (row_bcast:15; the half-waves never mix).
+__device__ __forceinline__ u64 lane_group_incl_scan(u64 v) {
+  const u32 ls = lane_id() & (kScanLanes - 1u);
+  u64 t = dpp_mov<0x111, 0xf>(v);
+  v += ls >= 1u ? t : 0ull;
+  t = dpp_mov<0x112, 0xf>(v);
+  v += ls >= 2u ? t : 0ull;
+  t = dpp_mov<0x114, 0xf>(v);
+  v += ls >= 4u ? t : 0ull;
+  if (kScanLanes > 8) {
+    t = dpp_mov<0x118, 0xf>(v);
+    v += ls >= 8u ? t : 0ull;
+  }
+  if (kScanLanes > 16) v += dpp_mov<0x142, 0xa>(v);
+  return v;
+}
+// The last lane of the caller's lane group (every lane of the group gets it).
+__device__ __forceinline__ u64 lane_group_last(u64 v) {
+  const int src = (int)(lane_id() | (kScanLanes - 1u));
+  return ((u64)(u32)__shfl((int)(v >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)v, src, 64);
+}
+
+// FORMAT.md §3: partition p takes no record of batch j (tiles [t0, t1)). The same threads that wrote
+// the batch's cells flag them (program order), absent cells included (stage 3 never reads those).
+__device__ __forceinline__ void flag_no_space(u64* ecol, u32 s, u32 t0, u32 t1) {
+  for (u32 B = t0 - t0 % (kScanLanes * kCL); B < t1; B += kScanLanes * kCL)
+#pragma unroll
+    for (u32 k = 0; k < kCL; ++k) {
+      const u32 t = B + kCL * s + k;
+      if (t >= t0 && t < t1) ecol[t] = kExclNoSpace;
+    }
+}
+
+// Column p's batch scans when some cell of the wave's columns is kCellWide (a tile run of more than
+// kCellB16 16-byte units, i.e. records averaging over 32 KB) or the group spans more than one chunk
+// of kScanLanes * kCL tiles: the same scans as stage2_column, the cells read from memory one by one.
+// Returns the group aggregate over accepted cells.
+__device__ __attribute__((noinline)) u64 stage2_column_general(const PipeArgs& A, u32 p, u32 s, u32 rm) {
   const PipeGroup& G = A.g2;
   const PipeScratch& x = A.s2;
   const u32 P = A.st.P, T = G.tiles, GT = A.gt;
-  // record bytes / 16 one batch may add to p: its ring less one index interval (FORMAT.md §3)
   const u64 lim16 = ((1ull << (A.st.ring[p] & 63ull)) - (1ull << A.st.interval_log2)) >> 4;
-  u64* const col = x.hist + (u64)p * GT;
+  u32* const col = x.hist32 + (u64)p * GT;
+  const u64* const wcol = x.hist + (u64)p * GT;
   u64* const ecol = x.excl + (u64)p * GT;
-  u64 carry = 0, bsum = 0;  // aggregate through the batches before j; batch j so far
+  u64 carry = 0, bsum = 0;
   u32 j = 0;
   for (u32 C = 0; C < T; C += kScanLanes * kCL) {
-    if (C) load_column_chunk(col, C + kCL * s, T, h);
     const u32 ta = C + kCL * s;
     for (; j < G.nb && G.tile0[j] < C + kScanLanes * kCL; ++j) {
       const u32 t0 = G.tile0[j], t1 = G.tile0[j + 1];
-      const bool binv = (rm >> j) & 1u;  // invalid batch: its cells are cleared and count nothing
+      const bool binv = (rm >> j) & 1u;
+      const u32 a = ta > t0 ? ta : t0, b = min(min(ta + kCL, t1), T);
       u64 loc = 0;
-#pragma unroll
-      for (u32 k = 0; k < kCL; ++k) loc += (ta + k >= t0 && ta + k < t1) ? h[k] : 0ull;
+      for (u32 t = a; t < b; ++t) {
+        const u32 c = col[t];
+        if (c) loc += c == kCellWide ? wcol[t] : cell_value(c);
+      }
       if (binv) loc = 0;
-      // inclusive scan over the column's 32 lanes (a half-wave): DPP row moves inside each row of
-      // 16, then rows 1 / 3 take the last lane of rows 0 / 2 (the half-waves never mix)
-      static_assert(kScanLanes == 32, "stage 2 column scans are half-wave DPP scans");
-      u64 inc = loc;
-      inc += dpp_mov<0x111, 0xf>(inc);
-      inc += dpp_mov<0x112, 0xf>(inc);
-      inc += dpp_mov<0x114, 0xf>(inc);
-      inc += dpp_mov<0x118, 0xf>(inc);
-      inc += dpp_mov<0x142, 0xa>(inc);
+      const u64 inc = lane_group_incl_scan(loc);
       u64 run = carry + bsum + inc - loc;
-#pragma unroll
-      for (u32 k = 0; k < kCL; ++k) {
-        if (ta + k >= t0 && ta + k < t1 && h[k]) {
-          if (!binv) ecol[ta + k] = run;
-          col[ta + k] = 0ull;  // clear for the set's next group
-          if (!binv) run += h[k];
+      for (u32 t = a; t < b; ++t) {
+        const u32 c = col[t];
+        if (c) {
+          if (!binv) ecol[t] = run;
+          if (!binv) run += c == kCellWide ? wcol[t] : cell_value(c);
+          col[t] = 0u;
         }
       }
-      bsum += lane_id() < 32u ? bcast_u64(inc, 31) : bcast_u64(inc, 63);  // the half-wave's last lane
-      if (t1 > C + kScanLanes * kCL) break;  // batch j goes on in the next chunk
+      bsum += lane_group_last(inc);
+      if (t1 > C + kScanLanes * kCL) break;
       if (!binv) {
-        if ((bsum & kLow40) > lim16) {
-          // FORMAT.md §3: partition p takes no record of batch j. The same threads that wrote the
-          // cells flag them (program order), absent cells included (stage 3 never reads those).
-          for (u32 B = t0 - t0 % (kScanLanes * kCL); B < t1; B += kScanLanes * kCL)
-#pragma unroll
-            for (u32 k = 0; k < kCL; ++k) {
-              const u32 t = B + kCL * s + k;
-              if (t >= t0 && t < t1) ecol[t] = kExclNoSpace;
-            }
-        } else {
-          carry += bsum;
-        }
+        if ((bsum & kLow40) > lim16) flag_no_space(ecol, s, t0, t1);
+        else carry += bsum;
       }
       bsum = 0;
+      if (s == 0) x.bcum[(u64)j * P + p] = carry;
+    }
+  }
+  return carry;
+}
+
+// Column p of the group: per batch, the exclusive scan of the column over the batch's tiles (thread
+// s holding tiles [kCL s, kCL s + kCL) of the group's first kScanLanes * kCL tiles, h, already
+// loaded), the batches scanned from those registers one after another.
+__device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u32 rm, u32 (&h)[kCL]) {
+  const PipeGroup& G = A.g2;
+  const PipeScratch& x = A.s2;
+  const u32 P = A.st.P, T = G.tiles, GT = A.gt;
+  bool wide = T > kScanLanes * kCL;
+#pragma unroll
+  for (u32 k = 0; k < kCL; ++k) wide |= h[k] == kCellWide;
+  u64 carry = 0;
+  u32 j = 0;
+  if (__any(wide)) {
+    carry = stage2_column_general(A, p, s, rm);
+    j = G.nb;
+  } else {
+    // record bytes / 16 one batch may add to p: its ring less one index interval (FORMAT.md §3)
+    const u64 lim16 = ((1ull << (A.st.ring[p] & 63ull)) - (1ull << A.st.interval_log2)) >> 4;
+    u32* const col = x.hist32 + (u64)p * GT;
+    u64* const ecol = x.excl + (u64)p * GT;
+    const u32 ta = kCL * s;
+    for (; j < G.nb && G.tile0[j] < T; ++j) {
+      const u32 t0 = G.tile0[j], t1 = G.tile0[j + 1];
+      const bool binv = (rm >> j) & 1u;  // invalid batch: its cells are cleared and count nothing
+      // the lane's cells of the batch: k in [klo, khi)
+      const u32 klo = t0 > ta ? min(t0 - ta, kCL) : 0u, khi = t1 > ta ? min(t1 - ta, kCL) : 0u;
+      u32 lc = 0, lb = 0;  // their count, bytes / 16
+#pragma unroll
+      for (u32 k = 0; k < kCL; ++k) {
+        const u32 c = (k >= klo && k < khi) ? h[k] : 0u;
+        lc += c >> kCellCntShift;
+        lb += c & kCellB16;
+      }
+      const u64 loc = binv ? 0ull : ((u64)lc << 40) | lb;
+      const u64 inc = lane_group_incl_scan(loc);
+      u64 run = carry + inc - loc;
+#pragma unroll
+      for (u32 k = 0; k < kCL; ++k) {
+        if (k >= klo && k < khi && h[k]) {
+          if (!binv) ecol[ta + k] = run;
+          run += cell_value(h[k]);
+          col[ta + k] = 0u;  // clear for the set's next group
+        }
+      }
+      const u64 bsum = lane_group_last(inc);
+      if (!binv) {
+        if ((bsum & kLow40) > lim16) flag_no_space(ecol, s, t0, t1);
+        else carry += bsum;
+      }
       if (s == 0) x.bcum[(u64)j * P + p] = carry;
     }
   }
@@ -1166,7 +1266,7 @@ __device__ __forceinline__ void stage2(const PipeArgs& A, u32 wg, u64* s_ex) {
   const u32 ncg = (P + kScanCols - 1) / kScanCols;
   const u32 cstride = A.wg2 * (kPT / kScanLanes);
   u32 cg = (wg * kPT + tid) / kScanLanes;
-  u64 h[kScanCols][kCL];
+  u32 h[kScanCols][kCL];
   if (cg < ncg) load_column_group(x, cg, P, GT, s, T, h);
   // ---- batch rule from stage 1's per-batch sums (every workgroup, since the scans skip invalid
   // batches)

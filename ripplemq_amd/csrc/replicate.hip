@@ -104,6 +104,7 @@ __device__ __forceinline__ u32 source_of_task(const IngestArgs& A, u32 task) {
 struct DirView {
   u32 count, bytes16, tstart, dstart16;
   u64 first, term, commit;
+  u64 lterm;  // (v5) the term of the entry's last entry the follower may count (0: older, unknown)
   bool rebase;
 };
 __device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
@@ -117,6 +118,7 @@ __device__ __forceinline__ DirView dir_of(const RegionView& R, u32 k) {
   d.dstart16 = d1.y;
   d.term = ((u64)d1.w << 32) | d1.z;
   d.commit = ((u64)d2.y << 32) | d2.x;  // the leader's commit (v4)
+  d.lterm = ((u64)d2.w << 32) | d2.z;   // (v5)
   d.rebase = (d.term & kTermRebase) != 0ull;
   d.term &= ~kTermRebase;
   return d;
@@ -172,6 +174,7 @@ __device__ u64 follower_pos(const DevState& st, u32 p, u32 slot, u64 t) {
 }
 
 constexpr u32 kBadCrc = 1u, kBadLog = 2u, kBadStale = 4u, kBadMissed = 8u;
+constexpr u32 kBadUnread = 16u;  // (with kBadLog) the region's header is unreadable: nothing heard from the leader
 
 // A structural fault of source src's region this round (FORMAT.md §9: directory entries that do
 // not tile the table and data sections, a table slot outside its entry, rows out of order): every
@@ -198,7 +201,7 @@ __global__ void ingest_prepare_kernel(IngestArgs A) {
     } else {
       const RegionView R = region_of(A, src);
       if (!R.sane) {
-        bad = kBadLog;
+        bad = kBadLog | kBadUnread;
       } else {
         const DirView d = dir_of(R, k);
         // the entry's slice of the table and of the data section ends where the next entry's
@@ -641,6 +644,9 @@ __device__ __forceinline__ void finish_entry(const IngestArgs& A, u32 e, u64& n_
   for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) bad |= A.bad[q];
   if (own) atomicAdd((unsigned long long*)&A.counters[(own & kBadCrc) && !(own & ~kBadCrc) ? 1 : 2], 1ull);
   A.acc[e] = bad ? 0u : 1u;
+  // an entry of the current term from a leader whose region arrived: the leader is alive (the
+  // election timer restarts), whatever the verdict on its records
+  if (owner && !(A.bad[e] & (kBadMissed | kBadUnread | kBadStale))) st.heard[p] = A.stamp;
   if (bad) {
     A.ackout[2 * e] = st.leo[p] | kAckRefused;
     A.ackout[2 * e + 1] = st.used[p];
@@ -654,6 +660,8 @@ __device__ __forceinline__ void finish_entry(const IngestArgs& A, u32 e, u64& n_
     const u32 ilog = st.interval_log2;
     const u64 old_used = st.used[p];
     if (d.term > st.term[p]) st.term[p] = d.term;
+    st.lterm[p] = d.lterm;  // the entry's last entry term (0: older, unknown)
+    st.mterm[p] = d.term;   // the log matches the term-d.term leader's through the entry's end
     u64 spos = st.start_pos[p];
     if (d.rebase) {
       // the log restarts at the entry's first record: its start, and every index entry of the
@@ -814,9 +822,14 @@ __global__ void notice_apply_kernel(NoticeArgs a) {
   const DevState& st = a.st;
   const u32 p = a.xi_p[e];
   const u64 c = a.in[2 * e], t = a.in[2 * e + 1];
-  if (t < st.term[p]) return;
+  if (t < st.term[p]) return;  // an older term's (or a lost notice, term 0)
   if (t > st.term[p]) st.term[p] = t;
-  learn_commit(st, p, c, a.sets[0].leo[p]);  // (two slots of one partition: the same values)
+  st.heard[p] = a.stamp;
+  // the commit moves over this log only if it was matched in the notice's term; the leader's commit
+  // is learned either way (rmq_become_leader's RMQ_ESTALE). (Two slots of one partition: the same
+  // values.)
+  if (st.mterm[p] == t) learn_commit(st, p, c, a.sets[0].leo[p]);
+  else if (c > st.lcommit[p]) st.lcommit[p] = c;
 }
 
 void launch_notice_fill(const NoticeArgs& a, hipStream_t s) {

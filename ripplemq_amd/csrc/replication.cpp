@@ -193,6 +193,9 @@ int post_round(rmq_engine* e, uint32_t s) {
   a.items_grid = items;
   a.crc = e->d_crc;
   a.counters = r->d_counters;
+  a.stamp = x.round + 1ull;  // (rmq_leader_silent's clock: rounds ingested)
+  if (a.stamp > r->stamp) r->stamp = a.stamp;
+  r->stamp_time[a.stamp % 64] = std::chrono::steady_clock::now();
   launch_ingest(a, tasks, items, e->verify_wgs, r->xchg_s);
   if (a.n_in) r->nitems_par ^= 1u;  // (prepare ran: it cleared the other half)
   HIP_TRY(hipGetLastError());
@@ -587,8 +590,13 @@ int post_notices(rmq_engine* e) {
   a.in = r->d_nin;
   a.n_out = (uint32_t)r->xo_p.size();
   a.n_in = (uint32_t)r->xi_p.size();
+  a.stamp = r->stamp;
   launch_notice_fill(a, e->main_s);  // after the acks applied on the pipeline stream
   HIP_TRY(hipGetLastError());
+  for (uint32_t q = 0; q < W; ++q)  // rmq_fault_cut: these notices are lost (term 0: ignored)
+    if (((r->cut_notice >> q) & 1u) && r->xo_start[q + 1] > r->xo_start[q])
+      HIP_TRY(hipMemsetAsync(r->d_nout + 2ull * r->xo_start[q], 0, 16ull * (r->xo_start[q + 1] - r->xo_start[q]), e->main_s));
+  r->cut_notice = 0;
   HIP_TRY(hipEventRecord(r->ev_notice, e->main_s));
   HIP_TRY(hipStreamWaitEvent(r->xchg_s, r->ev_notice, 0));
   void* sb[kMaxWorld];

@@ -34,7 +34,8 @@ FETCH_RES_DTYPE = np.dtype([
     ("status", "<i4"), ("reserved", "<u4"),
 ])
 STATE_FIELDS = ("log_end_offset", "log_end_pos", "log_start_offset", "log_start_pos", "commit",
-                "high_watermark", "term", "term_start", "leader_commit")
+                "high_watermark", "term", "term_start", "leader_commit", "last_log_term", "voted_term",
+                "voted_for", "led", "heard_round")
 
 
 @dataclass
@@ -61,7 +62,7 @@ class EngineConfig:
 # numpy mirror of rmq_partition_state (bulk read-back)
 STATE_DTYPE = np.dtype({"names": [f for f, _ in A.RmqPartitionState._fields_],
                         "formats": ["<u8"] * 8 + [("<u8", A.RMQ_MAX_RF), ("<u4", A.RMQ_MAX_RF), "<u4", "<u4",
-                                                  "<u8", "<u8"],
+                                                  "<u8", "<u8", "<u8", "<u8", "<u4", "<u4", "<u8"],
                         "offsets": [getattr(A.RmqPartitionState, f).offset for f, _ in A.RmqPartitionState._fields_],
                         "itemsize": C.sizeof(A.RmqPartitionState)})
 
@@ -96,6 +97,9 @@ class Engine:
         self.h = h
         self._keep: dict[int, tuple] = {}
         self._pinned: dict[int, np.ndarray] = {}  # rmq_host_alloc buffers by address
+        # fetches in flight by ticket: the engine holds raw pointers to their arrays (results, output,
+        # page-locked requests) until rmq_fetch_poll answers them or the engine is destroyed
+        self._fetching: dict[int, "FetchTicket"] = {}
         # append_device reuses one argument block: a producer loop calls it once per batch
         self._dbatch = A.RmqBatch(0, A.RMQ_MEM_DEVICE)
         self._dticket = C.c_uint64()
@@ -108,6 +112,7 @@ class Engine:
             self.lib.rmq_destroy(self.h)
             self.h = None
             self._keep.clear()
+            self._fetching.clear()  # (rmq_destroy waited for every fetch)
             for p in list(self._pinned):  # after the engine: no DMA reads them any more
                 self.lib.rmq_host_free(None, C.c_void_p(p))
             self._pinned.clear()
@@ -165,8 +170,32 @@ class Engine:
         """Tests: the next round sent to dst has one byte flipped (rmq_fault_corrupt)."""
         _check(self.lib.rmq_fault_corrupt(self.h, dst, at), "rmq_fault_corrupt")
 
+    def fault_cut(self, dst: int, n: int = 1) -> None:
+        """Tests: as fault_isolate, and the next drain's commit notices to dst are lost (rmq_fault_cut)."""
+        _check(self.lib.rmq_fault_cut(self.h, dst, n), "rmq_fault_cut")
+
     def become_leader(self, pidx: int, term: int) -> None:
         _check(self.lib.rmq_become_leader(self.h, pidx, term), "rmq_become_leader")
+
+    def vote(self, pidx: int, term: int, candidate: int, cand_last_log_term: int, cand_log_end: int) -> bool:
+        """Raft RequestVote on this replica (rmq_vote): True if the vote was granted."""
+        g = C.c_uint32(0)
+        _check(self.lib.rmq_vote(self.h, pidx, term, candidate, cand_last_log_term, cand_log_end, C.byref(g)),
+               "rmq_vote")
+        return bool(g.value)
+
+    def set_vote(self, pidx: int, term: int, voted_for: int) -> None:
+        """Replay of a persisted vote (rmq_set_vote)."""
+        _check(self.lib.rmq_set_vote(self.h, pidx, term, voted_for), "rmq_set_vote")
+
+    def leader_silent(self, silent_rounds: int, timeout_ms: int = 0) -> np.ndarray:
+        """Followed partitions whose leader has been silent (rmq_leader_silent)."""
+        n = C.c_uint32(0)
+        _check(self.lib.rmq_leader_silent(self.h, silent_rounds, timeout_ms, None, 0, C.byref(n)), "rmq_leader_silent")
+        out = np.zeros(max(n.value, 1), np.uint32)
+        _check(self.lib.rmq_leader_silent(self.h, silent_rounds, timeout_ms, _ptr(out), n.value, C.byref(n)),
+               "rmq_leader_silent")
+        return out[:n.value]
 
     # ---- append
     def append_async(self, pidx: np.ndarray, lens: np.ndarray, payload: np.ndarray,
@@ -376,7 +405,9 @@ class Engine:
         t = C.c_uint64()
         _check(self.lib.rmq_fetch_async(self.h, _ptr(req), n, mem, ptr, out_cap, _ptr(res), C.byref(t)),
                "rmq_fetch_async")
-        return FetchTicket(t.value, req, res, out)
+        tk = FetchTicket(t.value, req, res, out)
+        self._fetching[t.value] = tk
+        return tk
 
     def fetch_rows(self, n: int):
         """A page-locked request array ([n, 4] uint32, zeroed) and result array (FETCH_RES_DTYPE[n])
@@ -391,6 +422,7 @@ class Engine:
         rc = self.lib.rmq_fetch_poll(self.h, tk.ticket, 1 if wait else 0, C.byref(used))
         if rc == A.RMQ_PENDING:
             return None
+        self._fetching.pop(tk.ticket, None)
         if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
             raise EngineError(rc, "rmq_fetch_poll")
         return rc, tk.res, int(used.value)

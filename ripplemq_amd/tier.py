@@ -46,7 +46,7 @@ from .engine import EngineError
 
 SEG_SUFFIX = ".seg"
 OFFSETS_FILE = "offsets.bin"   # u64 consumer offsets of the partition (rmq_config.max_consumers)
-META_FILE = "meta.json"        # {"term": t}: the partition's raft_meta
+META_FILE = "meta.json"        # {"term", "voted_term", "voted_for", "cursor"}: the partition's raft_meta
 ENDS_FILE = "durable_ends.bin" # tier root: u64 pairs {partition, durable end} of the last spill
 
 
@@ -177,8 +177,9 @@ class _PartitionFiles:
                 os.fsync(f.fileno())
         os.replace(tmp, os.path.join(self.dir, name))
 
-    def save_state(self, offsets: np.ndarray, term: int, cursor: int, fsync: bool) -> None:
-        """The partition's consumer-offset row and term, each rewritten only when it changed. The
+    def save_state(self, offsets: np.ndarray, term: int, cursor: int, fsync: bool, vote=(0, A.RMQ_NO_VOTE)) -> None:
+        """The partition's consumer-offset row, term and vote (jraft's raft_meta term / votedFor,
+        PartitionRaftServer.java:89), each rewritten only when it changed. The
         tier's own cursor slot is stored as 0 (the durable end is in the ends file and moves with
         every spill: the row then changes only when consumers commit)."""
         row = np.array(offsets, np.uint64)
@@ -190,7 +191,7 @@ class _PartitionFiles:
         if row != self._row:
             self._replace(OFFSETS_FILE, row, fsync)
             self._row = row
-        meta = {"term": int(term), "cursor": int(cursor)}
+        meta = {"term": int(term), "voted_term": int(vote[0]), "voted_for": int(vote[1]), "cursor": int(cursor)}
         if self._meta is None:
             self._meta = self.load_meta()
         if self._meta != meta:
@@ -326,11 +327,12 @@ class DurableLog:
         # offsets and term of the partitions led here (one bulk read of each), then the durable ends
         # of every partition in one file: a reopen trusts the records below them
         rows = self.engine.consumer_table()
-        terms = self.engine.states()["term"]
+        sts = self.engine.states()
         for k, p in enumerate(pidx.tolist()):
             if int(res["status"][k]) == A.RMQ_ENOTLEADER:
                 continue
-            self.parts[p].save_state(rows[p], int(terms[p]), self.cursor, self.fsync)
+            self.parts[p].save_state(rows[p], int(sts["term"][p]), self.cursor, self.fsync,
+                                     vote=(int(sts["voted_term"][p]), int(sts["voted_for"][p])))
         ends = np.array([[p, f.end] for p, f in self.parts.items()], np.uint64).reshape(-1, 2)
         tmp = os.path.join(self.dir, ENDS_FILE + ".tmp")
         with open(tmp, "wb") as f:
@@ -413,6 +415,9 @@ def replay(directory: str, engine, partitions, *, batch_records: int = 65536) ->
         if term > engine.state(p)["term"]:
             engine.become_leader(p, term)
             terms += 1
+        vt, vf = int(meta.get("voted_term", 0)), int(meta.get("voted_for", A.RMQ_NO_VOTE))
+        if vt > engine.state(p)["voted_term"]:  # a vote newer than the term it led (raft_meta votedFor)
+            engine.set_vote(p, vt, vf)
         raw = f.load_offsets_bytes()
         if raw:
             offs = np.frombuffer(raw, np.uint64).copy()

@@ -84,15 +84,16 @@ def mask_commit(region: np.ndarray) -> np.ndarray:
     return r
 
 
-def notice_round(oras):
+def notice_round(oras, lost=()):
     """The commit notices of a drain (FORMAT.md §9 v4): every leader's {commit, term} per entry to
     each follower, which learns its leader's commit. The GPU engines exchange them at every drain
-    that had rounds in flight (rmq_sync, and the drain of a placement change)."""
+    that had rounds in flight (rmq_sync, and the drain of a placement change). lost: (src, dst)
+    pairs whose notices are lost (rmq_fault_cut)."""
     W = len(oras)
     notes = [[oras[s].commit_notice(d) if d != s else None for d in range(W)] for s in range(W)]
     for s in range(W):
         for d in range(W):
-            if d != s and len(notes[s][d]):
+            if d != s and len(notes[s][d]) and (s, d) not in set(map(tuple, lost)):
                 oras[d].apply_notice(s, notes[s][d])
 
 

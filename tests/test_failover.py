@@ -85,6 +85,10 @@ def stale_replica_script(world=3, rf=3, ppr=4):
               ("round", _round(spec, world, 1), {"lost": [(0, 2)]}),
               ("round", _round(spec, world, 2), {"lost": [(0, 2)]}),
               ("place", to2), ("lead", {2: [(p, 2) for p in mine[2]]}),
+              # the placement named rank 2, its become_leader was refused: it serves nothing (a
+              # placement never starts a leadership by itself)
+              ("fetch", {2: (np.array(mine[2], np.uint32), np.zeros(len(mine[2]), np.uint32),
+                             np.full(len(mine[2]), 10, np.uint32))}),
               ("place", to1), ("lead", {1: [(p, 2) for p in mine[1]]}),
               ("round", {r: led_batches(spec, to1[r], r, 2, 66) for r in range(world)}),
               ("round", {r: led_batches(spec, to1[r], r, 2, 67) for r in range(world)}),
@@ -150,6 +154,105 @@ def offset_ticket_script(world=3, rf=3, ppr=4):
     return views, script, BASE, c1
 
 
+def election_script(world=3, rf=3, ppr=4):
+    """Leader election (jraft's election timer and RequestVote,
+    PartitionRaftServer.java:85,89; onLeaderStart, PartitionStateMachine.java:121-126). Rank 0's links
+    to both followers are cut for two rounds (regions and commit notices lost, rmq_fault_cut): ranks 1
+    and 2 report its partitions silent after two rounds, no others, and none after three. Rank 1 runs
+    for leader of each of them in term 2: its own vote and rank 2's (2 of 3); rank 0, whose log holds
+    the two uncommitted rounds, denies it and steps down on the newer term. Rank 2 then runs in the
+    same term and gets no vote. A placement naming rank 2 is refused by become_leader (RMQ_ETERM: it
+    voted for rank 1 in term 2); naming rank 1 succeeds once, a second call at term 2 is refused; the
+    new leaders replicate and rank 0 truncates its uncommitted tail."""
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    spec = StreamSpec(ppr, 300, "uniform", size=(1, 60), config_index=95)
+
+    def to_rank(target):
+        out = []
+        for v in views:
+            ls = v.leader_slot.copy()
+            for p in range(len(v.gp)):
+                if int(v.ranks[p][v.leader_slot[p]]) == 0:
+                    ls[p] = int(np.flatnonzero(v.ranks[p] == target)[0])
+            out.append(RankView(v.rank, v.gp, v.ranks, ls.astype(np.uint32), v.led))
+        return out
+
+    to2, to1 = to_rank(2), to_rank(1)
+    gids = list(range(ppr))  # rank 0's partitions
+    mine = {t: [int(p) for p in range(len(views[t].gp)) if int(views[t].gp[p]) in gids] for t in (1, 2)}
+    cut = {"cut": [(0, 1), (0, 2)]}
+    script = [("round", _round(spec, world, 0)),
+              ("round", _round(spec, world, 1), cut),
+              ("round", _round(spec, world, 2), cut),
+              ("silent", {1: 2, 2: 2}),
+              ("silent", {1: 3, 2: 3}),
+              ("elect", [(1, g, 2) for g in gids]),
+              ("elect", [(2, g, 2) for g in gids]),
+              ("place", to2), ("lead", {2: [(p, 2) for p in mine[2]]}),
+              ("place", to1), ("lead", {1: [(p, 2) for p in mine[1]]}),
+              ("lead", {1: [(p, 2) for p in mine[1]]}),
+              ("round", {r: led_batches(spec, to1[r], r, 2, 68) for r in range(world)}),
+              ("round", {r: led_batches(spec, to1[r], r, 2, 69) for r in range(world)}),
+              ("fetch", {1: (np.array(mine[1], np.uint32), np.zeros(len(mine[1]), np.uint32),
+                             np.full(len(mine[1]), 10_000, np.uint32))})]
+    return views, script, BASE, mine
+
+
+def divergent_notice_script(world=3, rf=3, ppr=4):
+    """A commit notice may not commit a tail its log never matched in the notice's term (Raft: the
+    follower's commit is min(leaderCommit, the last entry verified in the term)). Rank 0's round 1
+    reaches nobody (its records stay in its log, uncommitted), leadership of its partitions moves to
+    replica slot 1 at term 2, and the new leaders' first round to rank 0 is lost while the drain's
+    commit notices reach it: rank 0 adopts term 2 and learns the new commit, but its own commit stays
+    where it was; the next round truncates its tail and its commit follows the leader's."""
+    views = [rank_view(r, world, ppr, rf) for r in range(world)]
+    spec = StreamSpec(ppr, 300, "uniform", size=(1, 60), config_index=96)
+    new = moved_leadership(views)
+    moved = {}
+    for r in range(world):
+        v = new[r]
+        m = [int(p) for p in range(len(v.gp))
+             if v.ranks[p][v.leader_slot[p]] == r and views[r].ranks[p][views[r].leader_slot[p]] != r]
+        if m:
+            moved[r] = m
+    script = [("round", _round(spec, world, 0)),
+              ("state", [0]),
+              ("round", _round(spec, world, 1), {"drop": (0,)}),
+              ("place", new), ("lead", {r: [(p, 2) for p in m] for r, m in moved.items()}),
+              ("round", {r: led_batches(spec, new[r], r, 2, 71) for r in range(world)},
+               {"lost": [(r, 0) for r in moved]}),
+              ("state", [0]),
+              ("round", {r: led_batches(spec, new[r], r, 2, 72) for r in range(world)}),
+              ("state", [0])]
+    return views, script, BASE, ppr
+
+
+def _check_divergent_notice(script, out, ppr):
+    s0, s1, s2 = (out[_k(script, "state", i)][0] for i in range(3))
+    for p in range(ppr):  # rank 0's former partitions (local pidx 0..ppr-1 on rank 0)
+        assert s1[p]["term"] == 2 and s1[p]["leader_commit"] > s0[p]["commit"], (s0[p], s1[p])
+        assert s1[p]["commit"] == s0[p]["commit"], (s0[p], s1[p])  # not over the unmatched tail
+        assert s1[p]["log_end_offset"] > s1[p]["commit"]  # (the tail is there)
+        assert s2[p]["commit"] > s0[p]["commit"] and s2[p]["last_log_term"] == 2, s2[p]
+
+
+def _check_election(script, out, mine):
+    """The election script's outcomes (oracle or GPU alike)."""
+    s1, s3 = _k(script, "silent", 0), _k(script, "silent", 1)
+    assert out[s1][1] == mine[1] and out[s1][2] == mine[2], out[s1]  # exactly rank 0's partitions
+    assert out[s3][1] == [] and out[s3][2] == [], out[s3]
+    e1, e2 = _k(script, "elect", 0), _k(script, "elect", 1)
+    for g in range(len(mine[1])):  # rank 1: its own vote and rank 2's; rank 0 denies
+        assert (g, 1, True) in out[e1][1] and (g, 1, True) in out[e1][2] and (g, 1, False) in out[e1][0]
+    assert all(not granted for r in range(3) for (_, _, granted) in out[e2][r])  # one leader per term
+    l2, l1, l1b = (out[_k(script, "lead", i)] for i in range(3))
+    assert l2[2] and all(st == A.RMQ_ETERM for st in l2[2]), l2
+    assert l1[1] and all(st == A.RMQ_OK for st in l1[1]), l1
+    assert l1b[1] and all(st == A.RMQ_ETERM for st in l1b[1]), l1b
+    rc, res, _ = out[_k(script, "fetch")][1]
+    assert rc == 0 and np.all(res["status"] == 0) and np.all(res["count"] > 0)
+
+
 def _cfgs(views, base):
     return [rank_cfg(EngineConfig(**base), views[r], r) for r in range(len(views))]
 
@@ -202,8 +305,38 @@ def test_stale_replica_cannot_lead(oracle_mod):
         lead2, lead1 = out[_k(script, "lead", 0)][2], out[_k(script, "lead", 1)][1]
         assert lead2 and all(s == A.RMQ_ESTALE for s in lead2), lead2
         assert lead1 and all(s == A.RMQ_OK for s in lead1), lead1
-        rc, res, _ = out[_k(script, "fetch")][1]
+        rc, res, _ = out[_k(script, "fetch", 0)][2]
+        assert np.all(res["status"] == A.RMQ_ENOTLEADER), res  # the refused replica is no leader
+        rc, res, _ = out[_k(script, "fetch", 1)][1]
         assert rc == 0 and np.all(res["status"] == 0) and np.all(res["count"] > 0)
+    finally:
+        _close(oras)
+
+
+def test_leader_election(oracle_mod):
+    views, script, base, mine = election_script()
+    cfgs, oras, out = _oracle_run(oracle_mod, views, script, base)
+    try:
+        _check_election(script, out, mine)
+        for r in range(3):  # rank 0 follows rank 1 in term 2 and holds the new leader's log
+            for p in range(len(views[r].gp)):
+                st = oras[r].state(p)
+                if int(views[r].gp[p]) < 4:
+                    assert st["term"] == 2 and st["is_leader"] == (r == 1), (r, p, st)
+                    # ranks 1 and 2 voted for rank 1 in term 2; rank 0 denied it (its own vote of term 1)
+                    assert (st["voted_term"], st["voted_for"]) == ((2, 1) if r else (1, 0)), (r, p, st)
+        lead = [oras[1].state(p) for p in mine[1]]
+        fol = [oras[0].state(p) for p in range(4)]
+        assert [x["log_end_offset"] for x in lead] == [x["log_end_offset"] for x in fol]
+    finally:
+        _close(oras)
+
+
+def test_notice_does_not_commit_an_unmatched_tail(oracle_mod):
+    views, script, base, ppr = divergent_notice_script()
+    cfgs, oras, out = _oracle_run(oracle_mod, views, script, base)
+    try:
+        _check_divergent_notice(script, out, ppr)
     finally:
         _close(oras)
 
@@ -300,3 +433,17 @@ def test_offset_commit_waits_for_a_quorum_gpu(oracle_mod):
     got, _ = _gpu_vs_oracle(oracle_mod, views, script, base)
     polls = [got[k][0] for k, s in enumerate(script) if s[0] == "poll"]
     assert polls == [A.RMQ_PENDING, A.RMQ_PENDING, A.RMQ_OK, A.RMQ_PENDING, A.RMQ_ENOTLEADER], polls
+
+
+@pytest.mark.gpu
+def test_leader_election_gpu(oracle_mod):
+    views, script, base, mine = election_script()
+    got, _ = _gpu_vs_oracle(oracle_mod, views, script, base)
+    _check_election(script, got, mine)
+
+
+@pytest.mark.gpu
+def test_notice_does_not_commit_an_unmatched_tail_gpu(oracle_mod):
+    views, script, base, ppr = divergent_notice_script()
+    got, _ = _gpu_vs_oracle(oracle_mod, views, script, base)
+    _check_divergent_notice(script, got, ppr)

@@ -9,9 +9,14 @@ RCCL) and on per-rank oracles (tests/repl_sim.py rounds). Steps:
   ("poll", {rank: k})               rmq_poll_commit of the offset ticket that step k's commit got
   ("round", {rank: [batches]}, faults)          the batches form ONE launch group on every rank,
         then rmq_sync (rounds, acks, commit notices); faults = {"drop": ranks, "lost": [(src, dst)],
-        "corrupt": (src, dst, at)}
+        "cut": [(src, dst)] (the region and the drain's commit notices lost), "corrupt": (src, dst, at)}
   ("lead", {rank: [(pidx, term)]})  rmq_become_leader; the status of each call is recorded
   ("fetch", {rank: (pidx, consumer, max)})      rmq_fetch; results and bytes are recorded
+  ("silent", {rank: silent_rounds}) rmq_leader_silent (rounds only); the partitions are recorded
+  ("state", ranks)                  every partition state of those ranks is recorded
+  ("elect", [(candidate, gid, term)])  Raft elections: the candidate's (last_log_term, log end) of
+        global partition gid go as a vote request to every replica of gid in the current placement
+        (the candidate first); every rank records its votes [(gid, candidate, granted)]
 
 run_oracle / run_gpu return the recorded outcomes per step and rank, so a test compares them and
 then every rank's state, rings, index and consumer offsets.
@@ -35,15 +40,29 @@ def _lead(eng, p, t):
         return ex.status
 
 
+def _local(view, gid):
+    hit = np.flatnonzero(view.gp == gid)
+    return int(hit[0]) if hit.size else None
+
+
+def _voters(view, gid, cand):
+    """Replica ranks of global partition gid (the candidate first) in a rank's view of the placement."""
+    p = _local(view, gid)
+    ranks = [int(x) for x in view.ranks[p]]
+    return [cand] + [r for r in ranks if r != cand]
+
+
 def run_oracle(oras, views0, script):
     world = len(oras)
     for r in range(world):
         place(oras[r], views0[r], world)
+    views = list(views0)
     out = []
     for step in script:
         kind = step[0]
         rec = [None] * world
         if kind == "place":
+            views = list(step[1])
             for r in range(world):
                 place(oras[r], step[1][r])
         elif kind == "commit":
@@ -58,9 +77,10 @@ def run_oracle(oras, views0, script):
             for r in range(world):
                 for b in step[1].get(r, []):
                     oras[r].append(b.pidx, b.lens, b.payload)
-            rec = exchange_round(oras, keep_regions=True, drop=f.get("drop", ()), lost=f.get("lost", ()),
-                                 corrupt=f.get("corrupt"))
-            notice_round(oras)
+            cut = list(f.get("cut", ()))
+            rec = exchange_round(oras, keep_regions=True, drop=f.get("drop", ()),
+                                 lost=list(f.get("lost", ())) + cut, corrupt=f.get("corrupt"))
+            notice_round(oras, lost=cut)
         elif kind == "lead":
             for r, items in step[1].items():
                 rec[r] = [_lead(oras[r], p, t) for p, t in items]
@@ -68,6 +88,19 @@ def run_oracle(oras, views0, script):
             for r, (pidx, cons, mx) in step[1].items():
                 rc, res, buf, used = oras[r].fetch(pidx, cons, mx)
                 rec[r] = (rc, res, buf[:used])
+        elif kind == "silent":
+            for r, k in step[1].items():
+                rec[r] = [int(x) for x in oras[r].leader_silent(k)]
+        elif kind == "state":
+            for r in step[1]:
+                rec[r] = [oras[r].state(p) for p in range(len(views[r].gp))]
+        elif kind == "elect":
+            rec = [[] for _ in range(world)]
+            for cand, gid, term in step[1]:
+                st = oras[cand].state(_local(views[cand], gid))
+                for v in _voters(views[cand], gid, cand):
+                    g = oras[v].vote(_local(views[v], gid), term, cand, st["last_log_term"], st["log_end_offset"])
+                    rec[v].append((gid, cand, bool(g)))
         else:
             raise ValueError(kind)
         out.append(rec)
@@ -78,15 +111,19 @@ def run_gpu(engs, hub, views0, script, timeout=240):
     world = len(engs)
     out = [[None] * world for _ in script]
     errs = [None] * world
+    bar = threading.Barrier(world, timeout=timeout)
+    shared = {}
 
     def body(r):
         try:
             e = engs[r]
             e.attach_local(hub)
             place(e, views0[r])
+            views = list(views0)
             for k, step in enumerate(script):
                 kind = step[0]
                 if kind == "place":
+                    views = list(step[1])
                     place(e, step[1][r])
                 elif kind == "commit":
                     if r in step[1]:
@@ -102,6 +139,9 @@ def run_gpu(engs, hub, views0, script, timeout=240):
                     for s, d in f.get("lost", ()):
                         if s == r:
                             e.fault_isolate(d, 1)
+                    for s, d in f.get("cut", ()):
+                        if s == r:
+                            e.fault_cut(d, 1)
                     if f.get("corrupt") and f["corrupt"][0] == r:
                         e.fault_corrupt(f["corrupt"][1], f["corrupt"][2])
                     for b in step[1].get(r, []):
@@ -117,8 +157,31 @@ def run_gpu(engs, hub, views0, script, timeout=240):
                     if r in step[1]:
                         rc, res, buf, used = e.fetch(*step[1][r])
                         out[k][r] = (rc, res, buf[:used])
+                elif kind == "silent":
+                    if r in step[1]:
+                        out[k][r] = [int(x) for x in e.leader_silent(step[1][r])]
+                elif kind == "state":
+                    if r in step[1]:
+                        out[k][r] = [e.state(p) for p in range(len(views[r].gp))]
+                elif kind == "elect":
+                    # one election after another, as the oracle runs them: the candidate publishes its
+                    # log's (last term, end), then each replica votes in order
+                    out[k][r] = []
+                    for cand, gid, term in step[1]:
+                        bar.wait()
+                        if r == cand:
+                            st = e.state(_local(views[r], gid))
+                            shared[(k, gid, cand)] = (st["last_log_term"], st["log_end_offset"])
+                        bar.wait()
+                        lt, leo = shared[(k, gid, cand)]
+                        for v in _voters(views[cand], gid, cand):
+                            if v == r:
+                                g = e.vote(_local(views[r], gid), term, cand, lt, leo)
+                                out[k][r].append((gid, cand, bool(g)))
+                            bar.wait()
         except BaseException as ex:  # noqa: BLE001 - reported below
             errs[r] = ex
+            bar.abort()
 
     ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(world)]
     for t in ts:
@@ -158,3 +221,5 @@ def compare_outcomes(script, got, want):
                 assert g[0] == w[0] and np.array_equal(g[1], w[1]), (k, r, g, w)
             elif step[0] == "poll" and w is not None:
                 assert g == w, (k, r, g, w)
+            elif step[0] in ("silent", "elect", "state") and w is not None:
+                assert g == w, (k, step[0], r, g, w)
