@@ -405,6 +405,16 @@ int rmq_read_consumer_table(rmq_engine* e, uint32_t first, uint32_t n, uint64_t*
 #define RMQ_SCAN_CHECK 1u
 int rmq_scan_records(const uint8_t* buf, uint64_t len, uint64_t first, uint64_t max_records, uint32_t flags,
                      uint64_t* pos_out, uint64_t* count, uint64_t* bytes);
+/* Durable-tier spill (ripplemq_amd/tier.py; jraft's per-group log, PartitionRaftServer.java:53,88-90):
+   run i = buf[buf_pos[i], buf_pos[i] + bytes[i]), count[i] back-to-back FORMAT.md §1 records with
+   header offsets first[i], first[i] + 1, ... (as one rmq_fetch returns a partition's slice), is
+   appended to the open file descriptor fd[i]; pos_out gets, run after run, each record's position
+   inside its run and then the run's end (count[i] + 1 words per run). Runs are checked first
+   (RMQ_EINVAL, nothing written); the writes go over `threads` threads (0: up to 8); fsync_each != 0
+   fsyncs every file. RMQ_EDEVICE on an I/O error (errno set). Needs no engine (or GPU). */
+int rmq_tier_append(uint32_t n, const int32_t* fd, const uint64_t* first, const uint64_t* count,
+                    const uint64_t* buf_pos, const uint64_t* bytes, const uint8_t* buf, uint64_t* pos_out,
+                    uint32_t threads, int fsync_each);
 
 /* ---- device buffers and timing (bench / tests keep inputs resident in HBM) ---- */
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out);

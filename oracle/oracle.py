@@ -303,12 +303,17 @@ class OracleEngine:
         del self._tickets[ticket]
         return A.RMQ_OK if done else A.RMQ_ENOTLEADER
 
-    def fetch(self, pidx, consumer, max_records, out_cap=None, commit=False):
+    def fetch(self, pidx, consumer, max_records, out_cap=None, commit=False, out=None):
         n = len(pidx)
         req = np.zeros((n, 4), np.uint32)
         req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
         res = np.zeros(n, FETCH_RES_DTYPE)
         used = C.c_uint64()
+        if out is not None:  # the caller's buffer (as Engine.fetch)
+            if commit:
+                req[:, 3] = A.RMQ_FETCH_COMMIT
+            rc = self.lib.ro_fetch(self.h, _p(req), n, _p(out), out.size, _p(res), C.byref(used))
+            return rc, res, out, int(used.value)
         if out_cap is None:  # the size query commits nothing
             self.lib.ro_fetch(self.h, _p(req), n, None, 0, _p(res), C.byref(used))
             out_cap = int(used.value)

@@ -164,6 +164,7 @@ _SIGS = {
     "rmq_fault_isolate": (C.c_int, [vp, u32, u32]),
     "rmq_fault_cut": (C.c_int, [vp, u32, u32]),
     "rmq_scan_records": (C.c_int, [vp, u64, u64, u64, u32, vp, C.POINTER(u64), C.POINTER(u64)]),
+    "rmq_tier_append": (C.c_int, [u32, vp, vp, vp, vp, vp, vp, vp, u32, C.c_int]),
 }
 
 _lib = None

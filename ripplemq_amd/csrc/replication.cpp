@@ -473,11 +473,13 @@ void repl_pipe_args(rmq_engine* e, PipeArgs& a, const GroupFlight* s2, const Gro
   Replication* r = e->repl;
   if (!r) return;
   a.lastg = r->d_lastg;               // kept by every launch that applies a group
+  // every rank numbers every round (the follower side stamps its ingest with it), also one that
+  // leads nothing with a remote replica
+  if (s2) r->sets[s2->set].round = r->planned++;
   if (r->xo_p.empty()) return;        // nothing led here has a remote replica
   a.outidx = r->d_outidx;
   if (s2) {
     XchgSet& x = r->sets[s2->set];
-    x.round = r->planned++;
     a.xp2.xo_p = r->d_xo_p;
     a.xp2.xo_slot = r->d_xo_slot;
     a.xp2.xo_start = r->d_xo_start;

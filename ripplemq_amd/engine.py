@@ -330,13 +330,24 @@ class Engine:
             raise EngineError(rc, "rmq_poll_commit (offsets)")
         return rc
 
-    def fetch(self, pidx, consumer, max_records, out_cap: int | None = None, commit: bool = False):
-        """rmq_fetch into a host array (sized by a first call when out_cap is None); commit:
-        RMQ_FETCH_COMMIT on every request (the size query commits nothing)."""
+    def fetch(self, pidx, consumer, max_records, out_cap: int | None = None, commit: bool = False,
+              out: np.ndarray | None = None):
+        """rmq_fetch into a host array (sized by a first call when out_cap is None, or the caller's
+        uint8 `out`, e.g. page-locked from host_empty: one call, RMQ_ENOSPC if it is too small);
+        commit: RMQ_FETCH_COMMIT on every request (the size query commits nothing)."""
         n = len(pidx)
         req = np.zeros((n, 4), np.uint32)
         req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
         res = np.zeros(n, FETCH_RES_DTYPE)
+        if out is not None:
+            if commit:
+                req[:, 3] = A.RMQ_FETCH_COMMIT
+            used = C.c_uint64()
+            rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, _ptr(out), out.size, _ptr(res),
+                                    C.byref(used))
+            if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
+                raise EngineError(rc, "rmq_fetch")
+            return rc, res, out, int(used.value)
         if out_cap is None:
             used = C.c_uint64()
             rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, None, 0, _ptr(res), C.byref(used))

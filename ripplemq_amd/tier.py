@@ -59,6 +59,10 @@ def load_ends(root: str) -> dict[int, int]:
     return {int(p): int(e) for p, e in a}
 
 
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
 def _as_u8(buf) -> np.ndarray:
     if isinstance(buf, np.ndarray):
         return np.ascontiguousarray(buf.view(np.uint8).reshape(-1))
@@ -120,6 +124,7 @@ class _PartitionFiles:
         self.dir = os.path.join(root, f"p{p:06d}")
         self._row = None     # the consumer-offset row / meta last written (no re-read per spill)
         self._meta = None
+        self._fd = -1        # the last segment file, open for appends (spill)
         os.makedirs(self.dir, exist_ok=True)
         self.limit = segment_file_bytes
         self.base = 0
@@ -217,32 +222,52 @@ class _PartitionFiles:
         """Offset after the last durable record."""
         return self.base + len(self.pos) - 1
 
-    def append(self, first: int, data: np.ndarray, count: int, fsync: bool) -> None:
-        if not count:
-            return
+    def append_fd(self, first: int) -> tuple[int, int]:
+        """(fd, logical bytes so far) for a spill that appends records from offset `first`: the last
+        segment file, open for appends, or a new one when it reached the size limit."""
         if not self.seg_first:
             self.base = first
         elif first != self.end:
             raise EngineError(A.RMQ_EINVAL, f"{self.dir}: spill of offset {first} does not continue {self.end}")
-        rp = record_positions(data, count, first)
-        if len(rp) != count + 1 or int(rp[-1]) != len(data):
-            raise EngineError(A.RMQ_EINVAL, f"{self.dir}: {count} records expected in {len(data)} bytes")
-        total = int(self.pos[-1])
+        total = int(self._pos[self._n - 1])
         if not self.seg_first or total - self.seg_pos[-1] >= self.limit:
+            self.close()
             self.seg_first.append(first)
             self.seg_pos.append(total)
-        with open(self._path(self.seg_first[-1]), "ab") as f:
-            f.write(memoryview(np.ascontiguousarray(data)))
-            if fsync:
-                f.flush()
-                os.fsync(f.fileno())
+        if self._fd < 0:
+            self._fd = os.open(self._path(self.seg_first[-1]), os.O_WRONLY | os.O_CREAT | os.O_APPEND, 0o644)
+        return self._fd, total
+
+    def add_positions(self, rp: np.ndarray, total: int) -> None:
+        """The positions of records appended at logical byte `total` (rp: inside their run, then its end)."""
         n0 = self._n - 1  # the end entry is overwritten by the first new record's position
         if n0 + len(rp) > len(self._pos):
             grown = np.zeros(max(n0 + len(rp), 2 * len(self._pos)), np.int64)
             grown[:self._n] = self._pos[:self._n]
             self._pos = grown
-        self._pos[n0:n0 + len(rp)] = rp + total
+        self._pos[n0:n0 + len(rp)] = rp
+        self._pos[n0:n0 + len(rp)] += total
         self._n = n0 + len(rp)
+
+    def close(self) -> None:
+        if self._fd >= 0:
+            os.close(self._fd)
+            self._fd = -1
+
+    def append(self, first: int, data: np.ndarray, count: int, fsync: bool) -> None:
+        """One partition's records (the spill of a single partition; spill() batches them natively)."""
+        if not count:
+            return
+        data = np.ascontiguousarray(np.asarray(data, np.uint8).reshape(-1))
+        fd, total = self.append_fd(first)
+        pos = np.empty(count + 1, np.uint64)
+        rc = A.load().rmq_tier_append(1, _ptr(np.array([fd], np.int32)), _ptr(np.array([first], np.uint64)),
+                                      _ptr(np.array([count], np.uint64)), _ptr(np.zeros(1, np.uint64)),
+                                      _ptr(np.array([data.size], np.uint64)), data.ctypes.data, _ptr(pos), 1,
+                                      1 if fsync else 0)
+        if rc:
+            raise EngineError(rc, f"{self.dir}: {count} records expected in {data.size} bytes")
+        self.add_positions(pos.astype(np.int64), total)
 
     def read_bytes(self, a: int, b: int) -> bytes:
         """Logical bytes [a, b) across the segment files."""
@@ -286,6 +311,8 @@ class DurableLog:
         ends = load_ends(directory)
         self.parts = {int(p): _PartitionFiles(directory, int(p), segment_file_bytes, ends.get(int(p), 0))
                       for p in partitions}
+        self._saved = None  # [partition of parts][row, term, voted term, voted for] as last saved
+        self._buf = None    # the spill's fetch output (reused)
         # a reopened tier continues where its files end: the cursor slot names that offset
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
         ends = np.fromiter((f.end for f in self.parts.values()), np.uint64, len(self.parts))
@@ -295,45 +322,94 @@ class DurableLog:
     def end(self, p: int) -> int:
         return self.parts[p].end
 
+    def close(self) -> None:
+        """Close the open segment files (spill reopens them)."""
+        for f in self.parts.values():
+            f.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
     def spill(self) -> int:
         """Make every committed record durable; returns the number of records written."""
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
         if not len(pidx):
             return 0
         cons = np.full(len(pidx), self.cursor, np.uint32)
-        _, res, buf, _ = self.engine.fetch(pidx, cons, np.full(len(pidx), 0xFFFFFFFF, np.uint32))
+        mx = np.full(len(pidx), 0xFFFFFFFF, np.uint32)
+        # one fetch into a reused buffer (page-locked when the engine offers it), grown when short
+        while True:
+            if self._buf is not None:
+                rc, res, buf, used = self.engine.fetch(pidx, cons, mx, out=self._buf)
+                if rc == A.RMQ_OK:
+                    break
+            else:
+                used = 1 << 20
+            need = max(2 * int(used), 1 << 20)
+            if hasattr(self.engine, "host_empty"):
+                if self._buf is not None:
+                    self.engine.host_release(self._buf)
+                self._buf = self.engine.host_empty(need, np.uint8)
+            else:
+                self._buf = np.zeros(need, np.uint8)
+        status = res["status"].astype(np.int64)
+        bad = np.flatnonzero((status != A.RMQ_OK) & (status != A.RMQ_ENOTLEADER))  # (a follower's tier is
+        if len(bad):                                                                # fed by its own term)
+            p, st = int(pidx[bad[0]]), int(status[bad[0]])
+            raise EngineError(st, f"spill of partition {p} (records lost before they were durable)"
+                              if st == A.RMQ_EOFFSET else f"spill of partition {p}")
+        sel = np.flatnonzero((status == A.RMQ_OK) & (res["count"] > 0))
         moved = 0
-        adv_p, adv_o = [], []
-        for k, p in enumerate(pidx.tolist()):
-            st = int(res["status"][k])
-            if st == A.RMQ_ENOTLEADER:
-                continue  # a follower's tier is fed by its own leader term later
-            if st != A.RMQ_OK:
-                raise EngineError(st, f"spill of partition {p} (records lost before they were durable)"
-                                  if st == A.RMQ_EOFFSET else f"spill of partition {p}")
-            n = int(res["count"][k])
-            if not n:
-                continue
-            pos, nb = int(res["out_pos"][k]), int(res["bytes"][k])
-            first = int(res["start_offset"][k])
-            self.parts[p].append(first, buf[pos:pos + nb], n, self.fsync)
-            moved += n
-            adv_p.append(p)
-            adv_o.append(first + n)
-        if adv_p:
-            self.engine.commit_consumer_offset(np.asarray(adv_p, np.uint32),
-                                               np.full(len(adv_p), self.cursor, np.uint32),
-                                               np.asarray(adv_o, np.uint64))
+        if len(sel):
+            ps = pidx[sel]
+            first = np.ascontiguousarray(res["start_offset"][sel], np.uint64)
+            count = np.ascontiguousarray(res["count"][sel], np.uint64)
+            opos = np.ascontiguousarray(res["out_pos"][sel], np.uint64)
+            nbytes = np.ascontiguousarray(res["bytes"][sel], np.uint64)
+            files = [self.parts[p] for p in ps.tolist()]
+            fds = np.empty(len(sel), np.int32)
+            totals = [0] * len(sel)
+            for i, (f, x) in enumerate(zip(files, first.tolist())):  # continuity, segment roll, fd
+                fds[i], totals[i] = f.append_fd(x)
+            pos = np.empty(int(count.sum()) + len(sel), np.uint64)
+            data = np.ascontiguousarray(buf.view(np.uint8).reshape(-1))
+            rc = A.load().rmq_tier_append(len(sel), _ptr(fds), _ptr(first), _ptr(count), _ptr(opos), _ptr(nbytes),
+                                          data.ctypes.data, _ptr(pos), 8, 1 if self.fsync else 0)
+            if rc:
+                raise EngineError(rc, "spill: segment append (a run does not hold its records, or an I/O error)")
+            pos = pos.view(np.int64)
+            ends = np.cumsum(count.astype(np.int64) + 1)
+            for f, e, c, t in zip(files, ends.tolist(), count.tolist(), totals):
+                f.add_positions(pos[e - c - 1:e], t)
+            moved = int(count.sum())
+            self.engine.commit_consumer_offset(ps.astype(np.uint32), np.full(len(sel), self.cursor, np.uint32),
+                                               first + count)
         # offsets and term of the partitions led here (one bulk read of each), then the durable ends
         # of every partition in one file: a reopen trusts the records below them
-        rows = self.engine.consumer_table()
-        sts = self.engine.states()
-        for k, p in enumerate(pidx.tolist()):
-            if int(res["status"][k]) == A.RMQ_ENOTLEADER:
-                continue
-            self.parts[p].save_state(rows[p], int(sts["term"][p]), self.cursor, self.fsync,
-                                     vote=(int(sts["voted_term"][p]), int(sts["voted_for"][p])))
-        ends = np.array([[p, f.end] for p, f in self.parts.items()], np.uint64).reshape(-1, 2)
+        rows = self.engine.consumer_table()[pidx]
+        sts = self.engine.states()[pidx]
+        if 0 <= self.cursor < rows.shape[1]:
+            rows[:, self.cursor] = 0  # (the tier's own slot: the durable end, in the ends file)
+        key = np.concatenate([rows, sts["term"][:, None], sts["voted_term"][:, None],
+                              sts["voted_for"][:, None].astype(np.uint64)], axis=1)
+        # only the partitions whose row, term or vote changed since the last save (most spills: none)
+        changed = status != A.RMQ_ENOTLEADER
+        if self._saved is not None:
+            changed &= (key != self._saved).any(axis=1)
+        for k in np.flatnonzero(changed).tolist():
+            p = int(pidx[k])
+            self.parts[p].save_state(rows[k], int(sts["term"][k]), self.cursor, self.fsync,
+                                     vote=(int(sts["voted_term"][k]), int(sts["voted_for"][k])))
+        if self._saved is None:
+            self._saved = key.copy()
+        else:
+            self._saved[changed] = key[changed]
+        ends = np.empty((len(self.parts), 2), np.uint64)
+        ends[:, 0] = pidx
+        ends[:, 1] = [f.end for f in self.parts.values()]
         tmp = os.path.join(self.dir, ENDS_FILE + ".tmp")
         with open(tmp, "wb") as f:
             f.write(ends.tobytes())
