@@ -234,6 +234,10 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     const uint32_t slots = pipeline_wgs_per_cu(PT) * e->cu_count, busy = (split ? 0u : a.wg1 + a.wg2) + a.wgp;
     const uint32_t room = slots > busy + e->cu_count ? slots - busy : e->cu_count;
     a.wg3 = e->wg3_all ? want : std::min<uint32_t>(want, room);
+    if (e->s3_pair && !a.outidx) {  // two tasks per wave: every task has its place (no loop)
+      a.s3_pair = 1;
+      a.wg3 = std::max<uint32_t>(1u, (s3->tasks + 2 * wpb - 1) / (2 * wpb));
+    }
     a.wgb = e->big_wgs ? e->big_wgs : 32u * e->cu_count / (PT / 64u);  // 32 large-record waves per CU
     // dispatch order: s3_lead stage-3 workgroups, then ranking, scans and partition threads, then
     // the rest of stage 3, so the ranking/scan chains start before stage 3's last workgroups and
@@ -534,7 +538,7 @@ void free_engine(rmq_engine* e) {
     bufs.push_back(z.used);
   }
   for (const PipeScratch& x : e->scratch) {
-    void* xs[] = {x.hist32, x.hist, x.excl, x.totals, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.bacc, x.nbig, x.bigl};
+    void* xs[] = {x.hist32, x.hist, x.excl, x.totals, x.pk, x.bcum, x.crank, x.pre, x.tsum, x.tile_base, x.binfo, x.bacc, x.nbig, x.bigl};
     for (void* p : xs) bufs.push_back(p);
   }
   delete e->copy_pool;
@@ -683,6 +687,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_AHEAD")) e->max_ahead = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S3_PAIR")) e->s3_pair = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
   if (e->stamps_path || e->steal) e->split = 0;  // (phase stamps and stealing read one launch's roles)
 #define CREATE_TRY(x)      \
@@ -793,6 +798,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     CREATE_TRY(dalloc(&x.hist, TP));
     CREATE_TRY(dalloc(&x.excl, TP));
     CREATE_TRY(dalloc(&x.totals, P));
+    CREATE_TRY(dalloc(&x.pk, (size_t)P * 8));
     CREATE_TRY(dalloc(&x.bcum, (size_t)kMaxGroup * P));
     CREATE_TRY(dalloc(&x.crank, GT * kTileRecs));
     CREATE_TRY(dalloc(&x.pre, GT * kTileRecs));

@@ -226,6 +226,9 @@ struct PipeScratch {
   uint64_t* excl;       // [P][gt] exclusive prefix over the group's accepted cells (bit 63: the
                         //   cell's (batch, partition) is rejected for space, FORMAT.md §3)
   uint64_t* totals;     // [P] group aggregate over accepted cells
+  uint64_t* pk;         // [P][8] what stage 3 reads of partition p for the group, in one 64-byte line
+                        //   (stage 2 writes it): {log end offset, position before the group, totals,
+                        //   ring descriptor, is_leader | local_mask << 8, 0, 0, 0}
   uint64_t* bcum;       // [kMaxGroup][P] aggregate through batch j (accepted cells)
   uint2* crank;         // [tiles * kTileRecs] {rank in tile run | flags << 29, bytes/16 before it in the run}
   uint32_t* pre;        // [tiles * kTileRecs] payload bytes before the record inside its tile
@@ -253,6 +256,7 @@ struct PipeArgs {
   uint32_t rank_mode;      // stage 1: 0 LDS radix sort + segmented scan, 1 wave-ordered hash counters
   uint32_t gt;             // tiles per hist / excl column (group tile capacity)
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
+  uint32_t s3_pair;        // stage-3 waves take two tasks each, their loads interleaved (task, task + wg3 waves)
   uint32_t debug;         // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2, 32 no leader / mask / totals gathers in stage 3

@@ -1239,6 +1239,19 @@ __device__ __forceinline__ void stage2_column(const PipeArgs& A, u32 p, u32 s, u
   for (; j < G.nb; ++j)  // batches without tiles at the group's end
     if (s == 0) x.bcum[(u64)j * P + p] = carry;
   if (s == 0) store_sc1(&x.totals[p], carry);  // sc1: the plan below reads it in this launch
+  if (s == 0) {
+    // stage 3 of the group (next launch) reads p's words in one 64-byte line: the log end before the
+    // group = the state this launch's stage 3 reads plus the group it applies (what the next launch's
+    // stage 3 reads as its state set: plan_decide's B), the totals, the ring, leadership and replicas
+    const u64 t3 = A.g3.nb ? A.s3.totals[p] : 0ull;
+    uint4* pk = reinterpret_cast<uint4*>(x.pk + (u64)p * 8);
+    const u64 boff = A.cur.leo[p] + (t3 >> 40), bpos = A.cur.used[p] + 16ull * (t3 & kLow40);
+    const u64 rd = A.st.ring[p];
+    const u32 fl = A.st.is_leader[p] | (A.st.local_mask[p] << 8);
+    pk[0] = make_uint4((u32)boff, (u32)(boff >> 32), (u32)bpos, (u32)(bpos >> 32));
+    pk[1] = make_uint4((u32)carry, (u32)(carry >> 32), (u32)rd, (u32)(rd >> 32));
+    pk[2] = make_uint4(fl, 0u, 0u, 0u);
+  }
   if (A.xp2.n_out && s == 0 && A.st.is_leader[p]) {  // catch-up verdicts of p's out entries
     const u32 lm = A.st.local_mask[p];
     for (u32 r = 0; r < A.st.RF; ++r) {
@@ -1454,17 +1467,16 @@ __device__ __forceinline__ RecWords rec_words(const PipeArgs& A, u32 jb, u32 i, 
   if (cand) {
     const u32 t = A.g3.tile0[jb] + i / kTR;
     W.ex = A.s3.excl[(u64)p * A.gt + t];
-    W.leo = A.cur.leo[p];
-    W.used = A.cur.used[p];
-    W.rdesc = st.ring[p];
-    if (A.debug & 32u) {  // timing experiment: three of the seven state gathers left out
-      W.lead = 1u;
-      W.lm = (1u << st.RF) - 1u;
-    } else {
-      W.lead = st.is_leader[p];
-      W.tot = A.s3.totals[p];
-      W.lm = st.local_mask[p];
-    }
+    // the partition's words in one 64-byte line (stage 2 wrote them): three 16-byte loads
+    const uint4* pk = reinterpret_cast<const uint4*>(A.s3.pk + (u64)p * 8);
+    const uint4 a = pk[0], b = pk[1], c = pk[2];
+    W.leo = ((u64)a.y << 32) | a.x;
+    W.used = ((u64)a.w << 32) | a.z;
+    W.tot = ((u64)b.y << 32) | b.x;
+    W.rdesc = ((u64)b.w << 32) | b.z;
+    W.lead = c.x & 0xFFu;
+    W.lm = c.x >> 8;
+    (void)st;
   }
   return W;
 }
@@ -2085,6 +2097,35 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
   u32 task = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);
+  if (!XR && A.s3_pair) {
+    // two tasks per wave (task and task + wg3 waves; the engine sizes wg3 so every task has its
+    // place), each load round issued for both before either is waited for: a wave spends most of
+    // its life waiting on its dependent loads (record -> partition state and payload), so two
+    // chains in flight per wave halve the waves and overlap their waits
+    const u32 tb = task + A.wg3 * kPW;
+    const bool ha = task < tasks, hb = tb < tasks;  // (wave-uniform)
+    const TaskPos Ta = task_pos(G, ha ? task : 0u), Tb = task_pos(G, hb ? tb : 0u);
+    const TaskRec Ra = stage3_r1(A, Ta), Rb = stage3_r1(A, Tb);
+    if (!(A.debug & 8u)) {
+      const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+      uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
+      for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
+    }
+    const bool ca = ha && stage3_cand(A, Ta, Ra), cb = hb && stage3_cand(A, Tb, Rb);
+    const TaskState Za = stage3_r2(A, Ta, Ra, ca);
+    const TaskState Zb = stage3_r2(A, Tb, Rb, cb);
+    __syncthreads();
+    uint4 so;
+    if (ha) {
+      stage3_finish<XR>(A, S, Ta, Ra, Za, ca, so);
+      if (lane == 0) G.stats[Ta.jb][task - G.task0[Ta.jb]] = so;
+    }
+    if (hb) {
+      stage3_finish<XR>(A, S, Tb, Rb, Zb, cb, so);
+      if (lane == 0) G.stats[Tb.jb][tb - G.task0[Tb.jb]] = so;
+    }
+    return;
+  }
   // first task: its record and state/payload loads are in flight while the CRC tables fill LDS
   TaskPos T = task_pos(G, task < tasks ? task : 0u);
   TaskRec R = stage3_r1(A, T);
