@@ -46,7 +46,7 @@ sys.path.insert(0, REPO)
 
 # Load the engine (and with it /opt/rocm's HIP runtime) before anything imports torch.
 from ripplemq_amd._abi import RMQ_FETCH_COMMIT  # noqa: E402
-from ripplemq_amd.engine import Engine, EngineConfig, rccl_unique_id  # noqa: E402
+from ripplemq_amd.engine import FETCH_RES_DTYPE, Engine, EngineConfig, rccl_unique_id  # noqa: E402
 from ripplemq_amd.sharding import max_over_ranks, rank_view  # noqa: E402
 from ripplemq_amd.rings import partition_traffic, pool_layout, ring_sizes  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, StreamSpec, make_batch, record_bytes  # noqa: E402
@@ -244,6 +244,34 @@ def host_leg(eng, batches, steps: int) -> dict:
     return res
 
 
+def mixed_engine_leg(cfg: EngineConfig, rings: dict, pool, args) -> dict:
+    """The mixed leg on an engine of its own whose rings retain --mixed-retain batches of each
+    partition's traffic (the bench engine's retain 64, about a millisecond of appends: consumers of
+    max = 10 on hot partitions fall further behind than that within a few fetches and are reset to
+    the log start). The same resident input batches; the rings filled first, untimed."""
+    spec = CONFIGS[args.config]
+    eng = Engine(dataclasses.replace(cfg, segment_bytes=rings["segment_bytes"], pool_bytes=rings["pool_bytes"]))
+    try:
+        if rings["grown"].size:
+            eng.set_segments(rings["grown"], rings["grown_bytes"])
+        d_out = [eng.device_alloc(spec.records * 8) for _ in range(4)]
+
+        def step(k: int) -> int:
+            n, dp, dl, dpay, pb, _ = pool[k % len(pool)]
+            return eng.append_device(n, dp, dl, dpay, pb, d_out[k % len(d_out)])
+
+        for k in range(int(args.mixed_retain) + 64):  # the rings full (and their pages touched)
+            step(k)
+        out = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group)
+        out["rings"] = ring_report(rings, eng.cfg.replication_factor, args.group, spec.partitions)
+        out["retain_batches"] = args.mixed_retain
+        for d in d_out:
+            eng.device_free(d)
+        return out
+    finally:
+        eng.close()
+
+
 def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
     """Appends and consumer fetches at once on one engine (configs[4]: concurrent consumer fetch at
     lagging offsets), driven by ONE host thread as a broker's event loop would: per round `appends`
@@ -423,10 +451,11 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     B_fetch = 2 (16 + L) per returned record (read log, write output) + 8 ceil(log2(index entries))
     per request."""
     P = spec.partitions
-    st = [eng.state(p) for p in range(P)]
-    hw = np.array([s["high_watermark"] for s in st], np.int64)
-    lo = np.array([s["log_start_offset"] for s in st], np.int64)
-    idx_entries = np.maximum(1, np.array([(s["log_end_pos"] - s["log_start_pos"]) // 1024 + 1 for s in st]))
+    st = eng.states()  # one bulk read-back of every partition's state
+    hw = st["high_watermark"].astype(np.int64)
+    lo = st["log_start_offset"].astype(np.int64)
+    span = (st["log_end_pos"] - st["log_start_pos"]).astype(np.int64)
+    idx_entries = np.maximum(1, span // 1024 + 1)
     search_bytes = int((8 * np.ceil(np.log2(idx_entries + 1))).sum()) * consumers
     g = np.random.default_rng(0x52495050)
     pp = np.repeat(np.arange(P, dtype=np.uint32), consumers)
@@ -435,7 +464,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                         "HBM-resident at 4,096 partitions"}
     for mx in (10, 1024):
         hi = spec.size if isinstance(spec.size, int) else spec.size[1]
-        retained = int(sum(s["log_end_pos"] - s["log_start_pos"] for s in st))
+        retained = int(span.sum())
         cap = min(P * consumers * mx * (16 + (hi + 15) // 16 * 16), consumers * retained) + 4096
         d_out = eng.device_alloc(cap)
         recs = nbytes = 0
@@ -456,6 +485,12 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
         rows = [eng.fetch_rows(P * consumers) for _ in range(8)]
         for rq, _ in rows:
             rq[:, 0], rq[:, 1], rq[:, 2] = pp, cc, mx
+        # the kernel measurement's rows in device memory (RMQ_FETCH_DEVICE_ROWS: no PCIe inside the
+        # timed kernels, as the append bench's inputs are resident); the calls below use host rows
+        n_rq = P * consumers
+        d_req, d_res = eng.device_alloc(16 * n_rq), eng.device_alloc(32 * n_rq)
+        eng.h2d(d_req, rows[0][0])
+        res = np.empty(n_rq, FETCH_RES_DTYPE)
         for k in range(rounds):
             lag = (g.random(P * consumers) * (np.repeat(hw - lo, consumers) + 1)).astype(np.int64)
             eng.commit_consumer_offset(pp, cc, (np.repeat(hw, consumers) - lag).astype(np.uint64))
@@ -472,14 +507,15 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
             if os.environ.get("RMQ_BENCH_CALLS"):  # diagnostic: each timed call's wall time
                 print(f"bench: fetch max {mx} call {(time.perf_counter() - t0) * 1e6:.1f} us", file=sys.stderr)
             eng.profile(True)
-            rc, res, used = eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+            rc, _, used = eng.fetch_device(None, None, None, d_out, cap, d_rows=(n_rq, d_req, d_res))
             _, ms_f = eng.profile_query(3)  # the kernels' own dispatch-recorded spans, summed
             eng.profile(False)
+            eng.d2h(res, d_res)
             # kernel time: the same fetch's kernels run REPLAY times back to back between two events
-            # (idempotent; the request and result copies outside), so no copy, host gap or
-            # early-dispatch span enters it, and a rocprofv3 trace shows the same kernels back to back
+            # (idempotent; rows on the device), so no transfer, host gap or early-dispatch span enters
+            # it, and a rocprofv3 trace shows the same kernels back to back
             eng.profile(REPLAY)
-            eng.fetch_device(pp, cc, np.full(P * consumers, mx, np.uint32), d_out, cap)
+            eng.fetch_device(None, None, None, d_out, cap, d_rows=(n_rq, d_req, d_res))
             runs, ms_all = eng.profile_query(4)
             ms_r = ms_all / max(runs, 1)
             eng.profile(False)
@@ -508,6 +544,8 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                 print(f"bench: fetch max {mx} burst issue {t_iss * 1e6:.1f} us total {n_async / bursts[-1] * 1e6:.1f} us "
                       f"records {n_async}", file=sys.stderr)
         eng.device_free(d_out)
+        eng.device_free(d_req)
+        eng.device_free(d_res)
         for rq, rs in rows:
             eng.host_release(rq)
             eng.host_release(rs)
@@ -534,7 +572,58 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                                         "timing": f"per fetch: its kernels run {REPLAY}x back to back between two "
                                                   "HIP events on the fetch stream, divided by the runs",
                                         "kernel_spans_us_summed": t_kern / rounds * 1e6}}
+    out["loop10"] = consumer_loop(eng, spec, pp, cc, hw, lo, g, rounds * 4)
     return out
+
+
+def consumer_loop(eng, spec: StreamSpec, pp, cc, hw, lo, g, loops: int, mx: int = 10) -> dict:
+    """The consumer loop (ConsumerClientImpl.java:61-117): every (partition, consumer) reads max = 10
+    and commits what it read, round after round, through RMQ_FETCH_COMMIT (the commit happens on
+    the device), from a lag of U[0, retained records]. Each fetch reads on from the end of the one
+    before, whose ring position the engine's position cache holds (fetch.hip): the resolve walks
+    from there instead of searching the index. A committing fetch runs once (no replay) and needs
+    host rows (the call checks them): the rows are page-locked and the kernels read and write them
+    across PCIe, so this rate includes that transfer; timed by HIP events around the one run."""
+    n = len(pp)
+    lag = (g.random(n) * (np.repeat(hw - lo, n // len(hw)) + 1)).astype(np.int64)
+    eng.commit_consumer_offset(pp, cc, (np.repeat(hw, n // len(hw)) - lag).astype(np.uint64))
+    hi = spec.size if isinstance(spec.size, int) else spec.size[1]
+    cap = n * mx * (16 + (hi + 15) // 16 * 16) + 4096
+    d_out = eng.device_alloc(cap)
+    rq, rs = eng.fetch_rows(n)
+    rq[:, 0], rq[:, 1], rq[:, 2], rq[:, 3] = pp, cc, mx, RMQ_FETCH_COMMIT
+    eng.sync()
+    eng.fetch_device(None, None, None, d_out, cap, req=rq, res=rs, pinned_rows=True)  # the cache's first entries
+    recs = nbytes = 0
+    t_reg = 0.0
+    t_calls = []
+    for _ in range(loops):
+        eng.profile(True)
+        gc.disable()
+        t0 = time.perf_counter()
+        rc, _, _ = eng.fetch_device(None, None, None, d_out, cap, req=rq, res=rs, pinned_rows=True)
+        t_calls.append(time.perf_counter() - t0)
+        gc.enable()
+        runs, ms = eng.profile_query(4)
+        eng.profile(False)
+        if rc or np.any(rs["status"] != 0):
+            raise SystemExit(f"bench: consumer loop fetch failed rc={rc} statuses={np.unique(rs['status'])}")
+        t_reg += ms / 1e3
+        recs += int(rs["count"].sum())
+        nbytes += int(rs["bytes"].sum())
+    eng.device_free(d_out)
+    eng.host_release(rq)
+    eng.host_release(rs)
+    rec_bytes = recs * (16 + spec.size) if isinstance(spec.size, int) else nbytes
+    alg = 2 * rec_bytes
+    return {"requests": n, "loops": loops, "max_records": mx, "records_per_request": recs / (loops * n),
+            "records_per_s_kernels": recs / t_reg, "records_per_s_call": recs / loops / float(np.median(t_calls)),
+            "call_us_median": float(np.median(t_calls)) * 1e6,
+            "roofline": {"bound": "hbm", "achieved": alg / t_reg / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": alg / t_reg / 1e9 / HBM_PEAK_GBS, "mean_us_per_fetch": t_reg / loops * 1e6,
+                         "timing": "per fetch: HIP events around its kernels (one run; page-locked host rows, "
+                                   "read and written across PCIe by the kernels)",
+                         "bytes": "B_fetch = 2 (16 + L) per returned record (no index search on a cache hit)"}}
 
 
 class SoloGroup:
@@ -623,6 +712,11 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
     batches = [make_batch(spec, 1_000_000 * rank + q) for q in range(args.pool)]
     max_payload = max(int(b.payload.nbytes) for b in batches)
     rings = ring_plan(args, spec, batches, view)
+    # the mixed leg's engine: rings that retain --mixed-retain batches (consumers of max = 10 lag the
+    # appends on hot partitions; the ring is how far they may fall behind before a reset)
+    rings_mixed = (ring_plan(argparse.Namespace(**{**vars(args), "retain_batches": args.mixed_retain}), spec, batches,
+                             view)
+                   if args.concurrent_rounds > 0 and world == 1 else None)
     cfg = EngineConfig(num_partitions=len(view.gp), replication_factor=rf,
                        segment_bytes=rings["segment_bytes"], pool_bytes=rings["pool_bytes"],
                        index_interval=INDEX_INTERVAL, max_batch_records=spec.records,
@@ -775,7 +869,7 @@ def run_rank(args, grp, device: int, attach) -> dict | None:
         if args.fetch_rounds > 0 and world == 1:
             out["fetch"] = fetch_leg(eng, spec, args.fetch_rounds)
         if args.concurrent_rounds > 0 and world == 1:
-            out["mixed"] = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group)
+            out["mixed"] = mixed_engine_leg(cfg, rings_mixed, pool, args)
         if args.tier_rounds > 0 and world == 1:
             out["tier"] = tier_leg(eng, step, spec, args.tier_rounds, args.group)
     if region is not None:
@@ -808,6 +902,8 @@ def main() -> None:
     ap.add_argument("--rings", default="load", choices=["load", "equal"],
                     help="load: ring per partition from its traffic in one shared pool (rmq_set_segments); "
                          "equal: every ring --segment-mb (default 4)")
+    ap.add_argument("--mixed-retain", type=float, default=1024.0,
+                    help="mixed leg: batches of a partition's mean traffic its rings retain (own engine)")
     ap.add_argument("--retain-batches", type=float, default=64.0,
                     help="load policy: batches of a partition's mean traffic its ring retains")
     ap.add_argument("--segment-mb", type=int, default=None,

@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 8u
+#define RMQ_ABI_VERSION 9u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -338,10 +338,15 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
    at once). MessageBatchReadRequestProcessor.java:36-42 answers each read from its own closure;
    this is the batched, pipelined form of that call.
    mem | RMQ_FETCH_PINNED_ROWS (ABI 7; rmq_fetch too): reqs and res are page-locked host memory
-   (rmq_host_alloc or rmq_host_register): the requests go to the device and the result rows come back
-   by DMA with no host copy. The caller then keeps reqs unchanged until the ticket completes (as
-   with pinned batches); res is written by the DMA before the poll that returns the result. */
+   (rmq_host_alloc or rmq_host_register): the fetch kernels read the request rows and write the
+   result rows there themselves, with no copy (rows the runtime cannot map are staged like ordinary
+   ones). The caller then keeps reqs unchanged until the ticket completes (as with pinned batches);
+   res is written before the poll that returns the result.
+   mem | RMQ_FETCH_DEVICE_ROWS (ABI 9; rmq_fetch too): reqs and res are device memory (a broker whose
+   requests arrive on the GPU): no transfer at all. The host never sees these requests, so their
+   flags word must be 0 (RMQ_FETCH_COMMIT needs host rows: the call checks them) and is ignored. */
 #define RMQ_FETCH_PINNED_ROWS 0x100u
+#define RMQ_FETCH_DEVICE_ROWS 0x200u
 int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
                     uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket);
 /* Completion of an rmq_fetch_async ticket: RMQ_PENDING while it runs (wait != 0: block instead), else

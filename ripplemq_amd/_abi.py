@@ -15,9 +15,10 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 8
+RMQ_ABI_VERSION = 9
 RMQ_FETCH_COMMIT = 1
 RMQ_FETCH_PINNED_ROWS = 0x100
+RMQ_FETCH_DEVICE_ROWS = 0x200
 RMQ_MAX_RF = 8
 RMQ_ALL_PARTITIONS = 0xFFFFFFFF
 RMQ_OFFSET_NONE = 0xFFFFFFFFFFFFFFFF

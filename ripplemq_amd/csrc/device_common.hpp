@@ -35,6 +35,7 @@ struct CrcConsts {
   u32 zshift1k[4][256];   // register shift past 1024 zero bytes (a wave's round of 64 pieces)
   u32 inv_pad[16];        // inv_pad[n] = x^(-8n) mod P: "remove n trailing zero bytes"
   u32 sh16[64];           // sh16[e] = x^(8 * 16 * e) mod P: shift past e 16-byte pieces
+  u32 inv_pad16[16];      // inv_pad16[n] = inv_pad[n] * x^16: the low half of a split pad removal
 };
 
 // FORMAT.md §1 record size: 16-byte header + payload padded to kRecAlign.
@@ -70,6 +71,19 @@ __device__ __forceinline__ u32 gf2_mulmod(u32 a, u32 b) {
 #pragma unroll
   for (int k = 31; k >= 0; --k) {
     p ^= b & (0u - ((a >> k) & 1u));
+    b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
+  }
+  return p;
+}
+
+// Half of gf2_mulmod(a, b) for a lane pair: lane 0 takes a's coefficients of x^0..x^15 (bits
+// 31..16) against b, lane 1 those of x^16..x^31 (bits 15..0) against b * x^16; the product is the
+// XOR of the two halves.
+__device__ __forceinline__ u32 gf2_mulmod_half(u32 a16, u32 b) {
+  u32 p = 0;
+#pragma unroll
+  for (int k = 15; k >= 0; --k) {
+    p ^= b & (0u - ((a16 >> k) & 1u));
     b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));
   }
   return p;

@@ -89,6 +89,7 @@ void build_crc_consts(CrcConsts* c) {
   uint32_t x8n = 0x80000000u;  // x^(8n), n = 0..15
   for (uint32_t n = 0; n < 16; ++n) {
     c->inv_pad[n] = n ? host_inverse(x8n) : 0x80000000u;
+    c->inv_pad16[n] = host_mulmod(c->inv_pad[n], x2n[4]);
     x8n = host_mulmod(x8n, x2n[3]);
   }
 }
@@ -520,7 +521,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.pcache, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq,
                              s.lterm, s.mterm, s.heard, e->d_crc,
                              e->d_stats, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   for (rmq_engine::FetchSlot& f : e->fslot) {
@@ -778,6 +779,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_TRY(dalloc(&s.ring, P));
   CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
+  CREATE_TRY(dalloc(&s.pcache, (size_t)P * C * 2));
+  CREATE_HIP(hipMemset(s.pcache, 0xFF, (size_t)P * C * 16));  // every entry empty
   CREATE_TRY(dalloc(&s.cdirty, P));
   CREATE_TRY(dalloc(&s.lcommit, P));
   CREATE_TRY(dalloc(&s.lterm, P));
@@ -1559,7 +1562,7 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
     }
     // the device writes rmq_fetch_res rows (status zero-extended into its reserved word)
     static_assert(sizeof(rmq_fetch_res) == 32, "result rows are four words");
-    if (!f.rows_pinned) std::memcpy(f.res, f.h_res, (size_t)f.n * 32);  // (pinned: DMA'd in place)
+    if (!f.rows_pinned) std::memcpy(f.res, f.h_res, (size_t)f.n * 32);  // (pinned: written in place)
     // some request did not fit iff the bytes needed exceed the output (requests are placed in
     // order: the one holding byte out_cap is cut), so no pass over the rows
     f.rc = __atomic_load_n(f.need, __ATOMIC_ACQUIRE) > f.out_cap ? RMQ_ENOSPC : RMQ_OK;
@@ -1602,14 +1605,14 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
 }  // namespace
 
 namespace {
-// Issue a fetch into the next slot. sync (rmq_fetch: the caller waits at once): the request and
-// result copies on the fetch stream itself, so the call's chain has no cross-stream hops; else on
-// the copy stream and the result stream, overlapping the fetches and launches around it.
+// Issue a fetch into the next slot: its kernels on the pipeline stream, an event after them.
 int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
-                uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket, bool sync) {
+                uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
   if (!e || !ticket) return RMQ_EINVAL;
-  const bool rows_pinned = (mem & RMQ_FETCH_PINNED_ROWS) != 0;
-  mem &= ~RMQ_FETCH_PINNED_ROWS;
+  bool rows_pinned = (mem & RMQ_FETCH_PINNED_ROWS) != 0;
+  const bool rows_dev = (mem & RMQ_FETCH_DEVICE_ROWS) != 0;
+  mem &= ~(RMQ_FETCH_PINNED_ROWS | RMQ_FETCH_DEVICE_ROWS);
+  if (rows_dev && (rows_pinned || mem != RMQ_MEM_DEVICE)) return RMQ_EINVAL;  // (output on the device too)
   if ((n && (!reqs || !res)) || (mem != RMQ_MEM_HOST && mem != RMQ_MEM_DEVICE)) return RMQ_EINVAL;
   if (out_cap && !out) return RMQ_EINVAL;
   if (mem == RMQ_MEM_DEVICE && (reinterpret_cast<uintptr_t>(out) & 15u)) return RMQ_EINVAL;
@@ -1625,7 +1628,7 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
   }
   // RMQ_FETCH_COMMIT: known flags only, one committing request per (partition, consumer)
   bool any = false;
-  {
+  if (!rows_dev) {  // (device rows: never read here; their flags are ignored)
     for (uint32_t r = 0; r < n; ++r) {
       if (reqs[r].flags & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
       any |= (reqs[r].flags & RMQ_FETCH_COMMIT) != 0;
@@ -1657,19 +1660,38 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     *ticket = tk;
     return RMQ_OK;
   }
-  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0, e->fetch_s);
+  int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0, e->main_s);
   if (rc) return rc;
   uint8_t* d_out = mem == RMQ_MEM_HOST ? (out_cap ? f.d_out : nullptr) : out;
-  if (!rows_pinned) std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
+  // The kernels read the request rows from page-locked host memory and write the result rows
+  // there (no copy either way): the caller's own rows (RMQ_FETCH_PINNED_ROWS, if the runtime maps
+  // them), else the slot's staging rows.
+  void* d_rq = nullptr;
+  void* d_rs = nullptr;
+  if (rows_dev) {
+    d_rq = const_cast<rmq_fetch_req*>(reqs);
+    d_rs = res;
+  } else if (rows_pinned && (hipHostGetDevicePointer(&d_rq, const_cast<rmq_fetch_req*>(reqs), 0) != hipSuccess ||
+                      hipHostGetDevicePointer(&d_rs, res, 0) != hipSuccess)) {
+    (void)hipGetLastError();
+    rows_pinned = false;  // not mapped: staged like ordinary rows
+  }
+  if (!rows_pinned && !rows_dev) {
+    std::memcpy(f.h_req, reqs, (size_t)n * sizeof(rmq_fetch_req));
+    d_rq = f.h_req;
+    d_rs = f.h_res;
+  }
   {
-    // Order against the append pipeline without flushing it: the fetch reads the committed state
-    // after the last launch issued so far, and the next launch waits for the fetch, so no ring
-    // bytes or log starts it reads change under it.
+    // Order against the append pipeline without flushing it: on the pipeline's stream, after the
+    // last launch issued so far and before the next, so no ring bytes or log starts it reads change
+    // under it.
     std::lock_guard<std::mutex> g(e->mu);
     FetchArgs a{};
     a.st = e->st;
-    a.req = f.d_req;
+    a.req = static_cast<const uint32_t*>(d_rq);
+    a.req_dev = f.d_req;
     a.res = f.d_res;
+    a.res_host = static_cast<uint64_t*>(d_rs);
     a.aux = f.d_aux;
     a.cpre = f.d_cpre;
     a.csum_lines = f.csum_lines;
@@ -1677,49 +1699,37 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     a.out_cap = out_cap;
     a.need_host = f.need_dev;
     a.n = n;
-    // the requests' copy on the copy stream (it depends on nothing the pipeline or an earlier fetch
-    // writes: it overlaps the running launch and fetch), then the kernels behind the launches
-    // issued so far and the copy
-    hipStream_t in_s = sync ? e->fetch_s : e->copy_s, out_s = sync ? e->fetch_s : e->fetch_out_s;
-    HIP_TRY(hipMemcpyAsync(f.d_req, rows_pinned ? static_cast<const void*>(reqs) : f.h_req,
-                           (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, in_s));
-    if (!sync) HIP_TRY(hipEventRecord(f.ev_in, in_s));
-    HIP_TRY(hipEventRecord(e->ev_main, e->main_s));
-    HIP_TRY(hipStreamWaitEvent(e->fetch_s, e->ev_main, 0));
-    if (!sync) HIP_TRY(hipStreamWaitEvent(e->fetch_s, f.ev_in, 0));
+    a.commits = any ? 1u : 0u;
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     // (profiling replays a fetch's kernels back to back; a committing fetch runs once: each run
     // would commit again and the next would read from the committed offset)
     const uint32_t runs = e->profile && !any ? e->fetch_replay : 1u;
-    if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run, copies outside
-      for (hipEvent_t& x : ev) x = pool_event(e);
-      for (int k = 0; k < 2; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
+    // (a committing fetch records no dispatch spans: the events the kernels' own dispatches record
+    // were measured to hold the second kernel ~10 us behind the first, which its one run would carry)
+    const bool spans = e->profile && !any;
+    if (e->profile) {  // kernel 3: the first run's dispatch spans; 4: every run
+      if (spans) {
+        for (hipEvent_t& x : ev) x = pool_event(e);
+        for (int k = 0; k < 2; ++k) e->prof[3].push_back({ev[2 * k], ev[2 * k + 1]});
+      }
       r0 = pool_event(e);
       r1 = pool_event(e);
       e->prof[4].push_back({r0, r1});
       e->prof_fetch_runs += runs;
-      HIP_TRY(hipEventRecord(r0, e->fetch_s));
+      HIP_TRY(hipEventRecord(r0, e->main_s));
     }
     for (uint32_t k = 0; k < runs; ++k) {
       const size_t half = (size_t)f.csum_lines * kCsumStride;
       a.csum = f.d_csum + half * f.csum_par;
       a.csum_next = f.d_csum + half * (f.csum_par ^ 1u);
       f.csum_par ^= 1u;
-      launch_fetch(a, e->fetch_s, e->profile && k == 0 ? ev : nullptr);
+      launch_fetch(a, e->main_s, spans && k == 0 ? ev : nullptr);
       HIP_TRY(hipGetLastError());
     }
-    if (e->profile) HIP_TRY(hipEventRecord(r1, e->fetch_s));
-    // the next launch waits for the kernels only (not for the result copy to the host)
-    HIP_TRY(hipEventRecord(f.ev_k, e->fetch_s));
-    HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_k, 0));
-    // the result rows on their own stream: the next fetch's kernels do not wait for this copy
-    if (!sync) HIP_TRY(hipStreamWaitEvent(out_s, f.ev_k, 0));
-    // (the bytes needed reach the host by the gather's own store into f.need)
-    HIP_TRY(hipMemcpyAsync(rows_pinned ? static_cast<void*>(res) : static_cast<void*>(f.h_res), f.d_res, (size_t)n * 32,
-                           hipMemcpyDeviceToHost, out_s));
-    HIP_TRY(hipEventRecord(f.ev, out_s));
+    if (e->profile) HIP_TRY(hipEventRecord(r1, e->main_s));
+    HIP_TRY(hipEventRecord(f.ev, e->main_s));  // kernels done: result rows and bytes needed in place
   }
-  f.rows_pinned = rows_pinned;
+  f.rows_pinned = rows_pinned || rows_dev;  // (no copy of the rows at completion)
   f.ticket = tk;
   f.phase = 1;
   f.rc = RMQ_OK;
@@ -1738,7 +1748,7 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
 
 int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
                     uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
-  return fetch_issue(e, reqs, n, mem, out, out_cap, res, ticket, false);
+  return fetch_issue(e, reqs, n, mem, out, out_cap, res, ticket);
 }
 
 int rmq_fetch_poll(rmq_engine* e, uint64_t ticket, uint32_t wait, uint64_t* bytes_used) {
@@ -1766,7 +1776,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
   if (!e) return RMQ_EINVAL;
   if (!n) return RMQ_OK;
   uint64_t t = 0;
-  const int rc = fetch_issue(e, reqs, n, mem, out, out_cap, res, &t, true);
+  const int rc = fetch_issue(e, reqs, n, mem, out, out_cap, res, &t);
   if (rc) return rc;
   return rmq_fetch_poll(e, t, 1, bytes_used);
 }

@@ -47,6 +47,7 @@ struct PartView {
 // A wave resolves two requests (lanes 0..31 and 32..63), and each request's two ends are found
 // together by a quarter-wave each: kQL lanes per searched position.
 constexpr u32 kQL = 16;
+constexpr u64 kWalkMax = 32;  // longest slice walked from a cached position
 constexpr u32 kRPW = 2;  // requests per resolve wave
 
 // Logical byte position of record t (start_off <= t <= leo) in the lane's view, found by the kQL
@@ -77,7 +78,10 @@ __device__ __forceinline__ WinWords load_window(const uint8_t* ring, u64 wb, u32
   return x;
 }
 
-__device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v, u64 t, bool act) {
+// hit: the position cache holds the position of record h_off <= t (h_pos): no index search, the
+// walk starts there.
+__device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v, u64 t, bool act, bool hit,
+                                           u64 h_off, u64 h_pos) {
   const u32 lane = lane_id(), h = lane / kQL, hl = lane % kQL;
   constexpr u32 kWin = kPPL * kQL;  // pieces per header window
   const u32 ilog = st.interval_log2;
@@ -89,7 +93,12 @@ __device__ __forceinline__ u64 record_posq(const DevState& st, const PartView& v
   long ws = lo, step = 1;
   const u64 mask = v.rg.seg - 1;
   u64 sw = ~0ull;  // speculative header window
-  if (open) {
+  if (act && hit) {
+    open = false;
+    c_off = h_off;
+    c_pos = h_pos;
+    sw = h_pos & ~15ull;
+  } else if (open) {
     const double f = (double)(t - v.start_off) / (double)(v.leo - v.start_off);
     const u64 gpos = v.start_pos + (u64)(f * (double)(v.used - v.start_pos));
     const long me = (long)(gpos >> ilog);
@@ -181,7 +190,10 @@ struct Resolved {
 
 __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, bool live) {
   const DevState& st = a.st;
-  const u32 p = live ? a.req[4 * r] : 0u, c = live ? a.req[4 * r + 1] : 0u, mx = live ? a.req[4 * r + 2] : 0u;
+  // the request row, read once from host memory; the device copy for the gather and the cache
+  const uint4 rq = live ? *reinterpret_cast<const uint4*>(a.req + 4ull * r) : make_uint4(0, 0, 0, 0);
+  if (live && (lane_id() & 31u) == 0) *reinterpret_cast<uint4*>(a.req_dev + 4ull * r) = rq;
+  const u32 p = rq.x, c = rq.y, mx = rq.z;
   int status = kOk;
   u64 start = 0, count = 0, end = 0, ring_off = 0;
   // every word of the partition in one round, the leader flag included (a request refused by the
@@ -198,6 +210,8 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
   v.start_pos = okp ? st.start_pos[pp] : 0ull;
   const u32 lm = okp ? st.local_mask[pp] : 0u;
   const u64 desc = okp ? st.ring[pp] : 0ull;
+  const u64* ce = st.pcache + ((u64)pp * st.C + cc) * 2;
+  const u64 h_off = okp ? ce[0] : ~0ull, h_pos = okp ? ce[1] : 0ull;
   v.rg = ring_ref(desc, st.interval_log2, st.icap_mul);
   v.ring = st.logs;
   bool need = false;  // the slice is not empty: both its ends are searched
@@ -228,7 +242,11 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
   }
   // quarter 0 of the half: the slice's first record, quarter 1: one past its last
   const u32 hb = lane_id() & 32u;
-  const u64 pq = record_posq(st, v, (lane_id() & 16u) ? end : off, need);
+  // the position cache (the record after this consumer's last served slice): a consumer reading on
+  // from there skips the index search, and walks from the cached position (a short slice only:
+  // a long one takes the search, which skips most of it)
+  const bool hit = need && h_off == off && h_pos >= v.start_pos && h_pos < v.used && count <= kWalkMax;
+  const u64 pq = record_posq(st, v, (lane_id() & 16u) ? end : off, need, hit, off, h_pos);
   const u64 pos0 = __shfl(pq, (int)hb, 64), pend = __shfl(pq, (int)(hb + 16u), 64);
   return Resolved{start, count, need ? pend - pos0 : 0ull, pos0, (ring_off << 6) | (desc & 63ull), status};
 }
@@ -242,6 +260,14 @@ __global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
   const u64 b2 = bcast_u64(q.bytes, 0) + bcast_u64(q.bytes, 32);  // the wave's two requests
   if (lane == 0) s_b[w] = b2;
   if (live && (lane & 31u) == 0) {
+    // the position cache's next entry for this consumer: the record after the slice (a served
+    // request's partition and consumer are in range; reloaded here rather than held through the
+    // resolve, which would take 8 more VGPRs)
+    if (q.status == kOk && q.count) {
+      u64* ce = a.st.pcache + ((u64)a.req_dev[4 * r] * a.st.C + a.req_dev[4 * r + 1]) * 2;
+      ce[0] = q.start + q.count;
+      ce[1] = q.pos0 + q.bytes;
+    }
     a.res[4 * r + 0] = q.start;
     a.res[4 * r + 2] = q.count | (q.bytes << 32);
     a.res[4 * r + 3] = (u64)(uint32_t)q.status;
@@ -315,24 +341,25 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   if (tid < kGR && rr < a.n) {
     const u64 pos = base + inc - nb;
     s_pos[tid] = pos;
-    a.res[4 * rr + 1] = pos;  // out_pos (one result copy to the host)
+    u64 w0 = a.res[4 * rr], w2 = a.res[4 * rr + 2], w3 = a.res[4 * rr + 3];  // the resolve's words
     const bool nospc = nb && pos + nb > a.out_cap;
+    const int s0 = (int)(uint32_t)w3;
     if (nospc) {  // does not fit: not served (rare); its bytes still count
-      a.res[4 * rr + 2] = 0;
-      a.res[4 * rr + 3] = (u64)(uint32_t)kNoSpc;
+      w2 = 0;
+      w3 = (u64)(uint32_t)kNoSpc;
     }
-    if (rr + 1 == a.n) {  // bytes needed
-      a.res[4ull * a.n] = pos + nb;
+    // the final row, into the caller's page-locked rows (or the slot's staging rows)
+    *reinterpret_cast<ulonglong2*>(a.res_host + 4ull * rr) = make_ulonglong2(w0, pos);
+    *reinterpret_cast<ulonglong2*>(a.res_host + 4ull * rr + 2) = make_ulonglong2(w2, w3);
+    if (rr + 1 == a.n)  // bytes needed
       __hip_atomic_store(a.need_host, pos + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
     // RMQ_FETCH_COMMIT: the consumer's next offset once its records are in the output (or the
     // first retained offset after RMQ_EOFFSET); every request's offset was read by the resolve
     // kernel before (the host refuses two committing requests for one consumer in a call)
-    if (a.req[4 * rr + 3] & 1u) {
-      const int s0 = (int)(uint32_t)a.res[4 * rr + 3];
+    if (a.commits && (a.req_dev[4 * rr + 3] & 1u)) {
       if (!nospc && (s0 == kOk || s0 == kOffset)) {
-        const u32 p = a.req[4 * rr], c = a.req[4 * rr + 1];
-        a.st.cons[(u64)p * a.st.C + c] = a.res[4 * rr] + (s0 == kOk ? (u64)(uint32_t)a.res[4 * rr + 2] : 0ull);
+        const u32 p = a.req_dev[4 * rr], c = a.req_dev[4 * rr + 1];
+        a.st.cons[(u64)p * a.st.C + c] = w0 + (s0 == kOk ? (u64)(uint32_t)w2 : 0ull);
         a.st.cdirty[p] = 1u;  // (with a transport the row travels with the next round)
       }
     }

@@ -140,6 +140,9 @@ struct DevState {
   uint8_t* logs;         // [RF][pool] replica regions; partition p's ring at RingRef.base in each
   uint64_t* ring;        // [P] ring descriptor: byte offset in the pool | log2(ring bytes) (bits 0..5)
   uint64_t* cons;        // [P][C] consumer offsets
+  uint64_t* pcache;      // [P][C][2] fetch position cache {offset, its ring byte position}: the end
+                         //   of each consumer's last served slice (fetch.hip); an entry is always a
+                         //   true pair (committed records never move), offset ~0 = empty
   uint32_t* cdirty;      // [P] consumer offsets changed since the last replication round (FORMAT §9)
   uint64_t* lcommit;     // [P] follower: the newest leader commit learned (rounds, commit notices;
                          //   FORMAT.md §9); a leader's own is `commit`
@@ -286,8 +289,12 @@ struct PipeArgs {
 
 struct FetchArgs {
   DevState st;
-  const uint32_t* req;       // [n][4] {pidx, consumer, max, reserved}
+  const uint32_t* req;       // [n][4] {pidx, consumer, max, flags}: page-locked host rows (read once)
+  uint32_t* req_dev;         // [n][4] the resolve's device copy of them (the gather reads it)
   uint64_t* res;             // [n][4] {start_offset, out_pos, count|bytes<<32, status}, then {bytes needed}
+                             //   (device: resolve -> gather)
+  uint64_t* res_host;        // [n][4] the final result rows, written by the gather into page-locked
+                             //   host memory (no copy node)
   uint64_t* aux;             // [n][2] {source byte position, ring byte offset in logs}
   uint32_t* cpre;            // [n + 1] bytes of each request (resolve -> gather), 16-byte aligned
   uint64_t* csum;            // [n / kFetchChunk + 1][kCsumStride] bytes of each chunk of kFetchChunk
@@ -302,6 +309,7 @@ struct FetchArgs {
                              //   gather with a system-scope store (no copy node for it)
   uint32_t n;
   uint32_t csum_lines;
+  uint32_t commits;          // the host checked read-and-commit requests in the call (else flags ignored)
 };
 constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
 constexpr uint32_t kCsumStride = 16;   // u64 words per chunk sum (128 bytes)

@@ -1731,15 +1731,17 @@ __device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Sme
   acc ^= pair_swap(acc);
 
   // ---- header (lane 1), out offset (lane 0), sparse index (lane 1)
-  uint4 h = make_uint4(0, 0, 0, 0);
-  if (okp && j == 1) {
-    u32 crc = 0;
-    if (L) {  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad))
-      const u32 pad = 16u * m - L;
-      crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
-    }
-    h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
+  // CRC32C = ~(register(M || pad zeros) * x^(-8 pad)); the pair splits the product by halves of
+  // the register's coefficients
+  u32 part = 0;
+  if (okp && L) {
+    const u32 pad = 16u * m - L;
+    part = pad ? gf2_mulmod_half(j ? acc & 0xFFFFu : acc >> 16, j ? A.crc->inv_pad16[pad] : A.crc->inv_pad[pad])
+               : (j ? 0u : acc);
   }
+  part ^= pair_swap(part);
+  uint4 h = make_uint4(0, 0, 0, 0);
+  if (okp && j == 1) h = make_uint4((u32)off, (u32)(off >> 32), L, L ? ~part : 0u);
   if (img) {
     if (j == 1) W.img[w][r32][0] = h;
     // the 4-bit piece count is only meaningful for a stored record (ok implies m <= 7 here); a

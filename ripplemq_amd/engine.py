@@ -364,10 +364,21 @@ class Engine:
         return rc, res, out[:out_cap], int(used.value)
 
     def fetch_device(self, pidx, consumer, max_records, d_out: int, out_cap: int, commit: bool = False,
-                     req: np.ndarray | None = None, res: np.ndarray | None = None, pinned_rows: bool = False):
+                     req: np.ndarray | None = None, res: np.ndarray | None = None, pinned_rows: bool = False,
+                     d_rows: tuple[int, int, int] | None = None):
         """rmq_fetch into a device buffer (16-byte aligned); returns (rc, res, bytes_used). req / res:
         the caller's arrays (pidx / consumer / max_records None leave req's columns as they are);
-        pinned_rows: page-locked ones (fetch_rows), DMA'd with no host copy (RMQ_FETCH_PINNED_ROWS)."""
+        pinned_rows: page-locked ones (fetch_rows), read and written by the kernels in place
+        (RMQ_FETCH_PINNED_ROWS). d_rows = (n, device request rows, device result rows): rows in
+        device memory (RMQ_FETCH_DEVICE_ROWS, flags ignored); res is then None."""
+        if d_rows is not None:
+            n, d_req, d_res = d_rows
+            used = C.c_uint64()
+            rc = self.lib.rmq_fetch(self.h, C.c_void_p(d_req), n, A.RMQ_MEM_DEVICE | A.RMQ_FETCH_DEVICE_ROWS,
+                                    d_out, out_cap, C.c_void_p(d_res), C.byref(used))
+            if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
+                raise EngineError(rc, "rmq_fetch")
+            return rc, None, int(used.value)
         n = len(pidx) if pidx is not None else len(req)
         if req is None:
             req = np.zeros((n, 4), np.uint32)
@@ -393,7 +404,7 @@ class Engine:
         and res (FETCH_RES_DTYPE[n]) may be a caller's arrays reused from call to call; with req
         given, pidx / consumer / max_records None leave those columns as they are (column 3: the
         requests' flags, RMQ_FETCH_COMMIT). pinned_rows: req and res are page-locked (fetch_rows)
-        and go to and from the device by DMA alone (RMQ_FETCH_PINNED_ROWS); req then stays
+        and the kernels read and write them in place (RMQ_FETCH_PINNED_ROWS); req then stays
         unchanged until the ticket completes."""
         n = len(pidx) if pidx is not None else len(req)
         if pinned_rows and (req is None or res is None):

@@ -153,6 +153,95 @@ def test_fetch_commit_matches_oracle(oracle_mod):
         assert ei.value.status == A.RMQ_EINVAL
 
 
+def _cache_script(eng, P, C, spec, moves):
+    """Read-and-commit rounds (position-cache hits), rounds whose consumers the application moved
+    (misses), a plain read (the next fetch re-reads: a miss), slices longer than the walk (search)."""
+    pp = np.repeat(np.arange(P, dtype=np.uint32), C)
+    cc = np.tile(np.arange(C, dtype=np.uint32), P)
+    out = []
+    for k in range(10):
+        b = make_batch(spec, k)
+        eng.append(b.pidx, b.lens, b.payload)
+        if k in moves:
+            eng.commit_consumer_offset(pp[::2], cc[::2], moves[k])
+        mx = np.full(P * C, (3, 10, 40)[k % 3], np.uint32)
+        rc, res, buf, used = eng.fetch(pp, cc, mx, out_cap=1 << 22, commit=k != 5)
+        out.append((rc, res.copy(), bytes(buf[:used])))
+    return out
+
+
+def test_position_cache_hits_and_misses(oracle_mod):
+    """The fetch position cache (fetch.hip: the ring position of the record after each consumer's
+    last served slice): consumers reading on from their last slice walk from the cached position,
+    the others search the index; rings small enough that retention passes cached positions. Every
+    result equals the oracle's, which has no cache."""
+    P, C = 32, 3
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 15, index_interval=256,
+                       max_consumers=C, max_batch_records=4096)
+    spec = StreamSpec(P, 2000, "zipf", size=(1, 200), config_index=48)
+    g = np.random.default_rng(48)
+    moves = {3: g.integers(0, 400, P * C // 2 + (P * C) % 2).astype(np.uint64),
+             7: g.integers(0, 900, P * C // 2 + (P * C) % 2).astype(np.uint64)}
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        got = _cache_script(dev, P, C, spec, moves)
+        want = _cache_script(ora, P, C, spec, moves)
+        for k, (gw, ww) in enumerate(zip(got, want)):
+            assert gw[0] == ww[0], k
+            for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                assert np.array_equal(gw[1][f], ww[1][f]), (k, f)
+            assert gw[2] == ww[2], k
+        assert np.array_equal(dev.consumer_table(), ora.consumer_table())
+        st = np.concatenate([x[1]["status"] for x in got])
+        assert (st == A.RMQ_EOFFSET).any() and (st == A.RMQ_OK).any()
+
+
+def test_device_rows_match_host_rows():
+    """RMQ_FETCH_DEVICE_ROWS (ABI 9): request and result rows in device memory give the results of
+    the same requests from host rows; their flags word is ignored (a read-and-commit flag commits
+    nothing: the host never checked those requests); host outputs are refused with device rows."""
+    P, C = 128, 2
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=C, max_batch_records=8192)
+    spec = StreamSpec(P, 6000, "zipf", size=(1, 400), config_index=49)
+    g = np.random.default_rng(49)
+    with Engine(cfg) as dev:
+        for b in range(4):
+            bt = make_batch(spec, b)
+            dev.append(bt.pidx, bt.lens, bt.payload)
+        n = 3001
+        req = np.zeros((n, 4), np.uint32)
+        req[:, 0] = g.integers(0, P + 2, n)
+        req[:, 1] = g.integers(0, C + 1, n)
+        req[:, 2] = g.integers(0, 300, n)
+        dev.commit_consumer_offset(np.repeat(np.arange(P, dtype=np.uint32), C), np.tile(np.arange(C, dtype=np.uint32), P),
+                                   g.integers(0, 60, P * C).astype(np.uint64))
+        cap = 4 << 20
+        d_out, d_out2 = dev.device_alloc(cap), dev.device_alloc(cap)
+        rc_w, want, used_w = dev.fetch_device(None, None, None, d_out, cap, req=req.copy())
+        table = dev.consumer_table().copy()
+        req[:, 3] = A.RMQ_FETCH_COMMIT  # ignored with device rows
+        d_req, d_res = dev.device_alloc(16 * n), dev.device_alloc(32 * n)
+        dev.h2d(d_req, req)
+        rc, none, used = dev.fetch_device(None, None, None, d_out2, cap, d_rows=(n, d_req, d_res))
+        assert none is None and rc == rc_w and used == used_w
+        got = np.empty(n, want.dtype)
+        dev.d2h(got, d_res)
+        for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+            assert np.array_equal(got[f], want[f]), f
+        a, b = np.empty(used, np.uint8), np.empty(used, np.uint8)
+        dev.d2h(a, d_out)
+        dev.d2h(b, d_out2)
+        assert np.array_equal(a, b)
+        assert np.array_equal(dev.consumer_table(), table)
+        assert (want["count"] > 0).any()
+        out = np.zeros(64, np.uint8)
+        rc = dev.lib.rmq_fetch(dev.h, A.C.c_void_p(d_req), n, A.RMQ_MEM_HOST | A.RMQ_FETCH_DEVICE_ROWS,
+                               out.ctypes.data_as(A.C.c_void_p), 64, A.C.c_void_p(d_res), None)
+        assert rc == A.RMQ_EINVAL
+        for d in (d_out, d_out2, d_req, d_res):
+            dev.device_free(d)
+
+
 def test_pinned_rows_match_sync():
     """RMQ_FETCH_PINNED_ROWS (ABI 7): requests and result rows in page-locked arrays go by DMA alone;
     six fetches in flight (more than the four slots), host and device outputs, one output cut

@@ -7,7 +7,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from ripplemq_amd.engine import FETCH_RES_DTYPE, Engine, EngineConfig  # noqa: E402
 from ripplemq_amd.workload import CONFIGS, make_batch  # noqa: E402
 
