@@ -375,7 +375,7 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
                     "HBM-resident at 4,096 partitions, so it is bounded by what the rings retain)"}
 
 
-def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int = 512, consumers: int = 4) -> dict:
+def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int = 4096, consumers: int = 4) -> dict:
     """The durable tier (ripplemq_amd/tier.py) on the bench engine: the first
     `parts` partitions' committed records spill to segment files (one rmq_fetch per spill, the
     native record scan, one file append per partition) while the workload appends: per round one
@@ -401,6 +401,7 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
         tier = DurableLog(eng, root, pidx, cursor, segment_file_bytes=256 << 20)
         first = tier.spill()  # untimed: the retained windows at the start
         size0 = sum(int(f.pos[-1]) for f in tier.parts.values())
+        tier.phase_s.clear()
         spilled, t_spill, k0 = 0, 0.0, 500_000
         for k in range(rounds):
             for j in range(appends):
@@ -418,6 +419,8 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
             lo, hi = f.base, min(int(st["log_start_offset"][p]), f.end)
             if hi > lo:
                 reqs += [(p, int(o)) for o in g.integers(lo, hi, consumers)]
+        if len(reqs) > 4096:  # a sample of them
+            reqs = [reqs[i] for i in g.choice(len(reqs), 4096, replace=False)]
         recs = rbytes = 0
         t0 = time.perf_counter()
         for p, off in reqs:
@@ -430,7 +433,8 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
     return {"partitions": P, "partition_stride": stride, "rounds": rounds, "appends_per_round": appends,
             "spill": {"records": spilled, "records_per_s": spilled / t_spill if t_spill else None,
                       "gb_per_s": sbytes / t_spill / 1e9 if t_spill else None, "initial_records": first,
-                      "ms_per_spill": t_spill * 1e3 / max(rounds, 1)},
+                      "ms_per_spill": t_spill * 1e3 / max(rounds, 1),
+                      "ms_per_spill_phases": {k: v * 1e3 / max(rounds, 1) for k, v in tier.phase_s.items()}},
             "read_below_rings": {"requests": len(reqs), "records": recs,
                                  "records_per_s": recs / t_read if t_read else None,
                                  "gb_per_s": rbytes / t_read / 1e9 if t_read else None, "max_records": 1024},

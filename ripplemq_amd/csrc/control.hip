@@ -8,6 +8,7 @@
 //   * ring moves (rmq_set_segments): a partition's retained log and index entries into a new ring.
 #include "device_common.hpp"
 #include "kernels.hpp"
+#include <algorithm>
 #include "partition_ops.hpp"
 
 namespace rmq {
@@ -68,6 +69,24 @@ __global__ void row_quorum_all_kernel(DevState st) {
 }
 
 static inline dim3 grid_for(u32 n, u32 b) { return dim3((n + b - 1) / b ? (n + b - 1) / b : 1); }
+
+// rmq_get_partition_states: the state words of partitions [first, first + n) gathered into one
+// page-locked host area in a single pass (field-major: 11 fields, then the match rows), instead of a
+// DMA per field (12 serialized copies measured 0.86 ms for 4,096 partitions).
+__global__ void state_gather_kernel(DevState st, uint64_t* out, u32 first, u32 n, u32 RF) {
+  const u64* const src[11] = {st.leo, st.used, st.start_off, st.start_pos, st.commit, st.hw, st.term,
+                              st.term_start, st.lcommit, st.lterm, st.heard};
+  for (u32 i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+#pragma unroll
+    for (u32 f = 0; f < 11; ++f) out[(u64)f * n + i] = src[f][first + i];
+    for (u32 r = 0; r < RF; ++r) out[11ull * n + (u64)i * RF + r] = st.match[(u64)(first + i) * RF + r];
+  }
+}
+
+void launch_state_gather(const DevState& st, uint64_t* out, uint32_t first, uint32_t n, uint32_t RF, hipStream_t s) {
+  hipLaunchKernelGGL(state_gather_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 1024u)), dim3(256), 0, s, st, out,
+                     first, n, RF);
+}
 
 void launch_row_quorum_all(const DevState& st, hipStream_t s) {
   hipLaunchKernelGGL(row_quorum_all_kernel, grid_for(st.P, 256), dim3(256), 0, s, st);

@@ -524,6 +524,7 @@ void free_engine(rmq_engine* e) {
                              s.local_mask, s.index, s.logs, s.ring, s.cons, s.pcache, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq,
                              s.lterm, s.mterm, s.heard, e->d_crc,
                              e->d_stats, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
+  if (e->state_stage) hipHostFree(e->state_stage);
   for (rmq_engine::FetchSlot& f : e->fslot) {
     void* fs[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum, f.d_out};
     for (void* p : fs) bufs.push_back(p);
@@ -1827,10 +1828,24 @@ int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_part
   uint64_t* const src[] = {s.leo, s.used, s.start_off, s.start_pos, s.commit, s.hw, s.term, s.term_start, s.lcommit,
                            s.lterm, s.heard};
   constexpr int NF = sizeof src / sizeof src[0];
-  std::vector<uint64_t> v((size_t)n * NF), m((size_t)n * RF);
-  for (int f = 0; f < NF; ++f)
-    HIP_TRY(hipMemcpy(v.data() + (size_t)f * n, src[f] + first, (size_t)n * 8, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(m.data(), s.match + (size_t)first * RF, (size_t)n * RF * 8, hipMemcpyDeviceToHost));
+  // every field gathered by one kernel into a page-locked staging area, one wait (12 synchronous
+  // copies into pageable vectors took 0.86 ms for 4,096 partitions)
+  const size_t words = (size_t)P * (NF + RF);
+  if (e->state_stage_words < words) {
+    if (e->state_stage) hipHostFree(e->state_stage);
+    e->state_stage = nullptr;
+    e->state_stage_words = 0;
+    HIP_TRY(hipHostMalloc((void**)&e->state_stage, words * 8, 0));
+    e->state_stage_words = words;
+  }
+  uint64_t* const v = e->state_stage;
+  uint64_t* const m = v + (size_t)n * NF;
+  static_assert(NF == 11, "state_gather_kernel's fields");
+  (void)src;
+  launch_state_gather(s, v, first, n, RF, e->main_s);  // (page-locked: the kernel writes it in place)
+  HIP_TRY(hipGetLastError());
+  rc = stream_wait(e->main_s);
+  if (rc) return rc;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t p = first + i;
     rmq_partition_state& x = o[i];

@@ -431,6 +431,8 @@ struct rmq_engine {
   // step with every role (the split measured slower: 60 vs 49 us per step).
   uint32_t split = 0;
   uint32_t rank_cus = 0;        // RMQ_RANK_CUS=n: rank_s runs on n CUs and main_s on the others
+  uint64_t* state_stage = nullptr;  // page-locked staging of rmq_get_partition_states
+  size_t state_stage_words = 0;
   uint32_t s3_pair = 0;         // RMQ_S3_PAIR=1: stage-3 waves take two tasks each (single-GPU kernel)
   hipStream_t rank_s = nullptr;
   hipEvent_t ev_rank[2] = {nullptr, nullptr};  // rank launch L recorded in slot L & 1

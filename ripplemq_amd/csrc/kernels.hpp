@@ -415,6 +415,7 @@ void preload_fetch_kernels();
 
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);
 void launch_row_quorum_all(const DevState& st, hipStream_t s);
+void launch_state_gather(const DevState& st, uint64_t* out, uint32_t first, uint32_t n, uint32_t RF, hipStream_t s);
 void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, uint32_t verify_wgs, hipStream_t s);
 uint32_t verify_wgs_per_cu();
 uint32_t verify_records_per_task();  // the host sizes the verify tasks with it

@@ -113,53 +113,67 @@ extern "C" int rmq_tier_append(uint32_t n, const int32_t* fd, const uint64_t* fi
                                uint64_t* pos_out, uint32_t threads, int fsync_each) {
   if (!n) return RMQ_OK;
   if (!fd || !first || !count || !buf_pos || !bytes || !buf || !pos_out) return RMQ_EINVAL;
-  // every run: header offsets first, first + 1, ..., exactly count records filling exactly its bytes
-  uint64_t at = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const uint8_t* b = buf + buf_pos[i];
-    uint64_t pos = 0, k = 0;
-    for (; k < count[i] && pos + 16 <= bytes[i]; ++k) {
-      uint64_t off;
-      uint32_t L;
-      std::memcpy(&off, b + pos, 8);
-      std::memcpy(&L, b + pos + 8, 4);
-      const uint64_t rs = 16ull + ((L + 15ull) & ~15ull);
-      if (off != first[i] + k || rs > bytes[i] - pos) break;
-      pos_out[at + k] = pos;
-      pos += rs;
-    }
-    if (k != count[i] || pos != bytes[i]) return RMQ_EINVAL;
-    pos_out[at + k] = pos;
-    at += count[i] + 1;
+  // each run's first slot in pos_out
+  std::vector<uint64_t> at(n);
+  for (uint32_t i = 0, a = 0; i < n; ++i) {
+    at[i] = a;
+    a += count[i] + 1;
   }
-  // the writes, spread over a few threads (independent files)
+  // on a few threads: every run's check (header offsets first, first + 1, ..., exactly count records
+  // filling exactly its bytes), then — none failed — every run's write (independent files)
   std::atomic<uint32_t> next{0};
   std::atomic<int> err{0};
-  auto work = [&]() {
+  auto check = [&]() {
     for (uint32_t i; (i = next.fetch_add(1)) < n && !err.load();) {
       const uint8_t* b = buf + buf_pos[i];
-      uint64_t left = bytes[i];
-      while (left) {
-        const ssize_t w = ::write(fd[i], b, left);
-        if (w < 0) {
-          if (errno == EINTR) continue;
-          err.store(errno ? errno : EIO);
-          return;
-        }
-        b += w;
-        left -= (uint64_t)w;
+      uint64_t pos = 0, k = 0;
+      for (; k < count[i] && pos + 16 <= bytes[i]; ++k) {
+        uint64_t off;
+        uint32_t L;
+        std::memcpy(&off, b + pos, 8);
+        std::memcpy(&L, b + pos + 8, 4);
+        const uint64_t rs = 16ull + ((L + 15ull) & ~15ull);
+        if (off != first[i] + k || rs > bytes[i] - pos) break;
+        pos_out[at[i] + k] = pos;
+        pos += rs;
       }
-      if (fsync_each && ::fsync(fd[i]) != 0) {
+      if (k != count[i] || pos != bytes[i]) {
+        err.store(-1);
+        return;
+      }
+      pos_out[at[i] + k] = pos;
+    }
+  };
+  auto write_run = [&](uint32_t i) {
+    const uint8_t* b = buf + buf_pos[i];
+    uint64_t left = bytes[i];
+    while (left) {
+      const ssize_t w = ::write(fd[i], b, left);
+      if (w < 0) {
+        if (errno == EINTR) continue;
         err.store(errno ? errno : EIO);
         return;
       }
+      b += w;
+      left -= (uint64_t)w;
     }
+    if (fsync_each && ::fsync(fd[i]) != 0) err.store(errno ? errno : EIO);
   };
   const uint32_t t = std::max<uint32_t>(1u, std::min<uint32_t>(threads ? threads : 8u, (n + 7) / 8));
+  // one set of threads for both phases, meeting between them (thread start-up is tens of us each)
+  std::atomic<uint32_t> arrived{0}, next_w{0};
+  auto both = [&]() {
+    check();
+    arrived.fetch_add(1);
+    while (arrived.load() < t) std::this_thread::yield();
+    if (err.load()) return;
+    for (uint32_t i; (i = next_w.fetch_add(1)) < n && !err.load();) write_run(i);
+  };
   std::vector<std::thread> pool;
-  for (uint32_t k = 1; k < t; ++k) pool.emplace_back(work);
-  work();
+  for (uint32_t k = 1; k < t; ++k) pool.emplace_back(both);
+  both();
   for (std::thread& th : pool) th.join();
+  if (err.load() < 0) return RMQ_EINVAL;
   if (err.load()) {
     errno = err.load();
     return RMQ_EDEVICE;  // an I/O error (errno set)

@@ -38,6 +38,7 @@ from __future__ import annotations
 import ctypes as C
 import json
 import os
+import time
 
 import numpy as np
 
@@ -132,6 +133,8 @@ class _PartitionFiles:
         self._n = 1
         self.seg_first: list[int] = []   # first offset of every segment file
         self.seg_pos: list[int] = []     # its first logical byte
+        self._owner = None   # the DurableLog whose spills hold positions not merged here yet
+        self._li = -1        #   and this partition's index there
         names = sorted(int(f[:-len(SEG_SUFFIX)]) for f in os.listdir(self.dir) if f.endswith(SEG_SUFFIX))
         cat, acc = [], 0
         for i, first in enumerate(names):  # reopen: walk the headers of every file, in offset order
@@ -162,6 +165,8 @@ class _PartitionFiles:
     @property
     def pos(self) -> np.ndarray:
         """Logical byte position of every durable record, then the end."""
+        if self._owner is not None:
+            self._owner._merge(self._li)
         return self._pos[:self._n]
 
     def _set_pos(self, v: np.ndarray) -> None:
@@ -229,7 +234,7 @@ class _PartitionFiles:
             self.base = first
         elif first != self.end:
             raise EngineError(A.RMQ_EINVAL, f"{self.dir}: spill of offset {first} does not continue {self.end}")
-        total = int(self._pos[self._n - 1])
+        total = int(self.pos[-1])
         if not self.seg_first or total - self.seg_pos[-1] >= self.limit:
             self.close()
             self.seg_first.append(first)
@@ -313,6 +318,22 @@ class DurableLog:
                       for p in partitions}
         self._saved = None  # [partition of parts][row, term, voted term, voted for] as last saved
         self._buf = None    # the spill's fetch output (reused)
+        # every partition's spill state as arrays (a spill of thousands of partitions runs no
+        # per-partition Python): durable end, logical bytes, first byte of the open segment file
+        # and its descriptor (-1: none open); the record positions of each spill are kept per spill
+        # and merged into a partition's files object when it is read
+        self._files = list(self.parts.values())
+        self._chunks = []   # per spill: (local indices, run starts in pos, counts, bytes before, pos)
+        self._merged = np.zeros(len(self._files), np.int64)  # chunks merged into each files object
+        for k, f in enumerate(self._files):
+            f._owner, f._li = self, k
+        self._end = np.fromiter((f.end for f in self._files), np.int64, len(self._files))
+        self._total = np.fromiter((int(f.pos[-1]) for f in self._files), np.int64, len(self._files))
+        self._segbase = np.fromiter((f.seg_pos[-1] if f.seg_first else -1 for f in self._files), np.int64,
+                                    len(self._files))
+        self._fd = np.full(len(self._files), -1, np.int64)
+        self._limit = int(segment_file_bytes)
+        self.phase_s: dict[str, float] = {}
         # a reopened tier continues where its files end: the cursor slot names that offset
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
         ends = np.fromiter((f.end for f in self.parts.values()), np.uint64, len(self.parts))
@@ -322,10 +343,28 @@ class DurableLog:
     def end(self, p: int) -> int:
         return self.parts[p].end
 
+    def _merge(self, k: int) -> None:
+        """The record positions of partition k's spills not merged into its files object yet."""
+        m = int(self._merged[k])
+        if m == len(self._chunks):
+            return
+        self._merged[k] = len(self._chunks)
+        f = self._files[k]
+        f._owner = None  # (add_positions reads its own arrays)
+        try:
+            for li, starts, counts, before, pos in self._chunks[m:]:
+                j = int(np.searchsorted(li, k))
+                if j < len(li) and li[j] == k:
+                    s0, c = int(starts[j]), int(counts[j])
+                    f.add_positions(pos[s0:s0 + c + 1], int(before[j]))
+        finally:
+            f._owner = self
+
     def close(self) -> None:
         """Close the open segment files (spill reopens them)."""
         for f in self.parts.values():
             f.close()
+        self._fd[:] = -1
 
     def __del__(self):
         try:
@@ -334,7 +373,9 @@ class DurableLog:
             pass
 
     def spill(self) -> int:
-        """Make every committed record durable; returns the number of records written."""
+        """Make every committed record durable; returns the number of records written. The host
+        time of its phases adds up in self.phase_s (fetch, files, commit, state)."""
+        t0 = time.perf_counter()
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
         if not len(pidx):
             return 0
@@ -355,6 +396,7 @@ class DurableLog:
                 self._buf = self.engine.host_empty(need, np.uint8)
             else:
                 self._buf = np.zeros(need, np.uint8)
+        t1 = time.perf_counter()
         status = res["status"].astype(np.int64)
         bad = np.flatnonzero((status != A.RMQ_OK) & (status != A.RMQ_ENOTLEADER))  # (a follower's tier is
         if len(bad):                                                                # fed by its own term)
@@ -369,28 +411,46 @@ class DurableLog:
             count = np.ascontiguousarray(res["count"][sel], np.uint64)
             opos = np.ascontiguousarray(res["out_pos"][sel], np.uint64)
             nbytes = np.ascontiguousarray(res["bytes"][sel], np.uint64)
-            files = [self.parts[p] for p in ps.tolist()]
-            fds = np.empty(len(sel), np.int32)
-            totals = [0] * len(sel)
-            for i, (f, x) in enumerate(zip(files, first.tolist())):  # continuity, segment roll, fd
-                fds[i], totals[i] = f.append_fd(x)
+            # (pidx lists the partitions in local order: sel are their local indices, ascending)
+            gap = np.flatnonzero((self._segbase[sel] >= 0) & (first.astype(np.int64) != self._end[sel]))
+            if len(gap):
+                k = int(sel[gap[0]])
+                raise EngineError(A.RMQ_EINVAL, f"{self._files[k].dir}: spill of offset {int(first[gap[0]])} "
+                                                f"does not continue {int(self._end[k])}")
+            # a new segment file where none is open or the open one reached the size limit (rare)
+            roll = (self._fd[sel] < 0) | ((self._segbase[sel] >= 0) &
+                                          (self._total[sel] - self._segbase[sel] >= self._limit))
+            for j in np.flatnonzero(roll).tolist():
+                k = int(sel[j])
+                f = self._files[k]
+                fd, total = f.append_fd(int(first[j]))  # (a partition's first file starts its log)
+                self._fd[k], self._segbase[k], self._end[k], self._total[k] = fd, f.seg_pos[-1], f.end, total
+            fds = np.ascontiguousarray(self._fd[sel], np.int32)
+            before = self._total[sel].copy()
             pos = np.empty(int(count.sum()) + len(sel), np.uint64)
             data = np.ascontiguousarray(buf.view(np.uint8).reshape(-1))
             rc = A.load().rmq_tier_append(len(sel), _ptr(fds), _ptr(first), _ptr(count), _ptr(opos), _ptr(nbytes),
-                                          data.ctypes.data, _ptr(pos), 8, 1 if self.fsync else 0)
+                                          data.ctypes.data, _ptr(pos), 16, 1 if self.fsync else 0)
             if rc:
                 raise EngineError(rc, "spill: segment append (a run does not hold its records, or an I/O error)")
-            pos = pos.view(np.int64)
             ends = np.cumsum(count.astype(np.int64) + 1)
-            for f, e, c, t in zip(files, ends.tolist(), count.tolist(), totals):
-                f.add_positions(pos[e - c - 1:e], t)
+            self._chunks.append((sel.astype(np.int64), ends - count.astype(np.int64) - 1, count.astype(np.int64),
+                                 before, pos.view(np.int64)))
+            self._end[sel] += count.astype(np.int64)
+            self._total[sel] += nbytes.astype(np.int64)
             moved = int(count.sum())
+            t2 = time.perf_counter()
             self.engine.commit_consumer_offset(ps.astype(np.uint32), np.full(len(sel), self.cursor, np.uint32),
                                                first + count)
+        else:
+            t2 = time.perf_counter()
+        t3 = time.perf_counter()
         # offsets and term of the partitions led here (one bulk read of each), then the durable ends
         # of every partition in one file: a reopen trusts the records below them
         rows = self.engine.consumer_table()[pidx]
+        t3a = time.perf_counter()
         sts = self.engine.states()[pidx]
+        t3b = time.perf_counter()
         if 0 <= self.cursor < rows.shape[1]:
             rows[:, self.cursor] = 0  # (the tier's own slot: the durable end, in the ends file)
         key = np.concatenate([rows, sts["term"][:, None], sts["voted_term"][:, None],
@@ -407,9 +467,10 @@ class DurableLog:
             self._saved = key.copy()
         else:
             self._saved[changed] = key[changed]
+        t3c = time.perf_counter()
         ends = np.empty((len(self.parts), 2), np.uint64)
         ends[:, 0] = pidx
-        ends[:, 1] = [f.end for f in self.parts.values()]
+        ends[:, 1] = self._end
         tmp = os.path.join(self.dir, ENDS_FILE + ".tmp")
         with open(tmp, "wb") as f:
             f.write(ends.tobytes())
@@ -417,6 +478,10 @@ class DurableLog:
                 f.flush()
                 os.fsync(f.fileno())
         os.replace(tmp, os.path.join(self.dir, ENDS_FILE))
+        t4 = time.perf_counter()
+        for k, v in (("fetch", t1 - t0), ("files", t2 - t1), ("commit", t3 - t2), ("table", t3a - t3),
+                     ("states", t3b - t3a), ("save", t3c - t3b), ("ends", t4 - t3c)):
+            self.phase_s[k] = self.phase_s.get(k, 0.0) + v
         return moved
 
     def read(self, p: int, off: int, max_messages: int) -> list[tuple[int, int, bytes]]:
