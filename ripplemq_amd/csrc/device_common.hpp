@@ -50,6 +50,19 @@ typedef u32 u32x4 __attribute__((ext_vector_type(4)));
 #ifndef RMQ_RING_NT
 #define RMQ_RING_NT 1
 #endif
+// A payload block read once per launch (RMQ_PAYLOAD_NT: non-temporal).
+#ifndef RMQ_PAYLOAD_NT
+#define RMQ_PAYLOAD_NT 1
+#endif
+__device__ __forceinline__ uint4 load_payload16(const void* src) {
+#if RMQ_PAYLOAD_NT
+  const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+  return make_uint4(x[0], x[1], x[2], x[3]);
+#else
+  return *reinterpret_cast<const uint4*>(src);
+#endif
+}
+
 __device__ __forceinline__ void store_log16(uint8_t* dst, uint4 v) {
 #if RMQ_RING_NT
   const u32x4 x = {v.x, v.y, v.z, v.w};

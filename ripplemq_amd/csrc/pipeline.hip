@@ -1448,7 +1448,7 @@ __device__ __forceinline__ void round_blocks(const PipeArgs& A, const TaskRec& R
   for (u32 q = 0; q < kBL; ++q) {
     const u64 blk_addr = a0 + 16ull * (kPR * c + j + 2u * q);
     blk[q] = make_uint4(0, 0, 0, 0);
-    if (live && blk_addr < lim && !(A.debug & 4u)) blk[q] = *reinterpret_cast<const uint4*>(blk_addr);
+    if (live && blk_addr < lim && !(A.debug & 4u)) blk[q] = load_payload16(reinterpret_cast<const void*>(blk_addr));
   }
 }
 
@@ -1528,11 +1528,11 @@ __device__ __forceinline__ void big_round(u64 src, u32 L, u32 k0, u32 ph, uint4 
   for (u32 u = 0; u < kBU; ++u) {
     const int jb = (int)(64u * (k0 + u) + lane) - (int)ph;
     const u64 ad = a0 + 16ll * jb;
-    b0[u] = jb >= 0 && ad < lim ? *reinterpret_cast<const uint4*>(ad) : make_uint4(0, 0, 0, 0);
+    b0[u] = jb >= 0 && ad < lim ? load_payload16(reinterpret_cast<const void*>(ad)) : make_uint4(0, 0, 0, 0);
   }
   tail = make_uint4(0, 0, 0, 0);
   const u64 ad = a0 + 16ull * (64u * (k0 + kBU) - ph);
-  if (sa && lane == 63u && ad < lim) tail = *reinterpret_cast<const uint4*>(ad);
+  if (sa && lane == 63u && ad < lim) tail = load_payload16(reinterpret_cast<const void*>(ad));
 }
 
 // The destination phase of a large record at ring position pos: its payload pieces start at piece
