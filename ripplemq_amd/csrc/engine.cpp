@@ -532,8 +532,6 @@ void free_engine(rmq_engine* e) {
     if (f.h_res) hipHostFree(f.h_res);
     if (f.ev) hipEventDestroy(f.ev);
     if (f.ev_copy) hipEventDestroy(f.ev_copy);
-    if (f.ev_k) hipEventDestroy(f.ev_k);
-    if (f.ev_in) hipEventDestroy(f.ev_in);
   }
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -565,7 +563,6 @@ void free_engine(rmq_engine* e) {
     if (ev) hipEventDestroy(ev);
   if (e->ev_pre_rank) hipEventDestroy(e->ev_pre_rank);
   if (e->rank_s) hipStreamDestroy(e->rank_s);
-  if (e->fetch_s) hipStreamDestroy(e->fetch_s);
   if (e->fetch_out_s) hipStreamDestroy(e->fetch_out_s);
   if (e->copy_s) hipStreamDestroy(e->copy_s);
   for (auto& v : e->prof)
@@ -724,7 +721,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
     for (hipEvent_t& ev : e->ev_rank) CREATE_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&e->ev_pre_rank, hipEventDisableTiming));
   }
-  CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_s, hipStreamNonBlocking));
   CREATE_HIP(hipStreamCreateWithFlags(&e->fetch_out_s, hipStreamNonBlocking));
   preload_fetch_kernels();
   CREATE_HIP(hipStreamCreateWithFlags(&e->copy_s, hipStreamNonBlocking));
@@ -732,8 +728,6 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   for (rmq_engine::FetchSlot& f : e->fslot) {
     CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
-    CREATE_HIP(hipEventCreateWithFlags(&f.ev_k, hipEventDisableTiming));
-    CREATE_HIP(hipEventCreateWithFlags(&f.ev_in, hipEventDisableTiming));
   }
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
@@ -1104,7 +1098,7 @@ int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
   if (rc) return rc;
-  HIP_TRY(hipStreamSynchronize(e->fetch_s));
+  // (fetches run on the pipeline stream: the drain waited for them too)
   // new rings first, all or nothing
   std::vector<MigrateItem> items;
   for (uint32_t i = 0; i < n; ++i) {

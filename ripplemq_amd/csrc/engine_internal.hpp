@@ -322,7 +322,6 @@ struct rmq_engine {
   // fetch: its own stream and scratch, serialised by fetch_mu (engine state under mu only while
   // the fetch is ordered against the pipeline stream)
   std::mutex fetch_mu;
-  hipStream_t fetch_s = nullptr;
   hipStream_t fetch_out_s = nullptr;  // fetch results (and host outputs) -> host, after the kernels:
                                       // a fetch's result copy overlaps the next fetch's kernels
   hipStream_t copy_s = nullptr;  // host batches and fetch requests: pinned -> device DMA
@@ -346,11 +345,9 @@ struct rmq_engine {
     uint32_t cap = 0;
     uint8_t* d_out = nullptr;    // device staging of a host output
     uint64_t out_alloc = 0;
-    hipEvent_t ev = nullptr;     // kernels and the result copy done
+    hipEvent_t ev = nullptr;     // its kernels done (result rows and bytes needed in place)
     hipEvent_t ev_copy = nullptr;  // host output copies done
-    hipEvent_t ev_k = nullptr;     // its kernels done (the pipeline stream waits for this one)
-    hipEvent_t ev_in = nullptr;    // its requests on the device (copy stream)
-    bool rows_pinned = false;      // RMQ_FETCH_PINNED_ROWS: the caller's rows are DMA'd directly
+    bool rows_pinned = false;      // the caller's rows read / written in place (pinned or device rows)
     uint64_t* need = nullptr;      // bytes needed: a word of fetch_need_host (the gather stores it)
     uint64_t* need_dev = nullptr;  // its device address
     // the fetch in flight: ticket 0 = idle; phase 1: kernels, 2: host output copies

@@ -259,21 +259,6 @@ class _PartitionFiles:
             os.close(self._fd)
             self._fd = -1
 
-    def append(self, first: int, data: np.ndarray, count: int, fsync: bool) -> None:
-        """One partition's records (the spill of a single partition; spill() batches them natively)."""
-        if not count:
-            return
-        data = np.ascontiguousarray(np.asarray(data, np.uint8).reshape(-1))
-        fd, total = self.append_fd(first)
-        pos = np.empty(count + 1, np.uint64)
-        rc = A.load().rmq_tier_append(1, _ptr(np.array([fd], np.int32)), _ptr(np.array([first], np.uint64)),
-                                      _ptr(np.array([count], np.uint64)), _ptr(np.zeros(1, np.uint64)),
-                                      _ptr(np.array([data.size], np.uint64)), data.ctypes.data, _ptr(pos), 1,
-                                      1 if fsync else 0)
-        if rc:
-            raise EngineError(rc, f"{self.dir}: {count} records expected in {data.size} bytes")
-        self.add_positions(pos.astype(np.int64), total)
-
     def read_bytes(self, a: int, b: int) -> bytes:
         """Logical bytes [a, b) across the segment files."""
         out = []
