@@ -231,6 +231,18 @@ class Engine:
         if self._pinned.pop(p, None) is not None:
             _check(self.lib.rmq_host_free(self.h, C.c_void_p(p)), "rmq_host_free")
 
+    def host_register(self, arr: np.ndarray) -> None:
+        """Page-lock a caller's contiguous array in place (rmq_host_register), so it can serve as
+        pinned batch arrays or pinned fetch rows; undone by host_unregister before it is freed."""
+        if not arr.flags["C_CONTIGUOUS"] or arr.nbytes == 0:
+            raise ValueError("host_register needs a non-empty contiguous array")
+        _check(self.lib.rmq_host_register(self.h, C.c_void_p(arr.__array_interface__["data"][0]), arr.nbytes),
+               "rmq_host_register")
+
+    def host_unregister(self, arr: np.ndarray) -> None:
+        _check(self.lib.rmq_host_unregister(self.h, C.c_void_p(arr.__array_interface__["data"][0])),
+               "rmq_host_unregister")
+
     def append_pinned_async(self, pidx: np.ndarray, lens: np.ndarray, payload: np.ndarray, out: np.ndarray,
                             payload_off: np.ndarray | None = None, payload_bytes: int | None = None) -> int:
         """rmq_append of a batch whose arrays (and `out`, uint64[n]) are page-locked (host_empty):

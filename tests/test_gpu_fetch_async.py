@@ -15,7 +15,7 @@ import pytest
 
 from parity import run_ops
 from ripplemq_amd import _abi as A
-from ripplemq_amd.engine import Engine, EngineConfig, EngineError
+from ripplemq_amd.engine import FETCH_RES_DTYPE, Engine, EngineConfig, EngineError
 from ripplemq_amd.workload import StreamSpec, make_batch
 
 pytestmark = pytest.mark.gpu
@@ -240,6 +240,52 @@ def test_device_rows_match_host_rows():
         assert rc == A.RMQ_EINVAL
         for d in (d_out, d_out2, d_req, d_res):
             dev.device_free(d)
+
+
+def test_pinned_rows_from_registered_and_plain_memory():
+    """RMQ_FETCH_PINNED_ROWS with rows the caller page-locked itself (rmq_host_register: mapped, so
+    the kernels read and write them in place) and with ordinary pageable rows (not mapped: staged
+    like unflagged rows): both give the results of an ordinary fetch of the same requests."""
+    P, C = 200, 2
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=C, max_batch_records=8192)
+    spec = StreamSpec(P, 5000, "zipf", size=(1, 300), config_index=53)
+    g = np.random.default_rng(53)
+    with Engine(cfg) as dev:
+        for b in range(3):
+            bt = make_batch(spec, b)
+            dev.append(bt.pidx, bt.lens, bt.payload)
+        cap = 8 << 20
+        for register in (True, False):
+            n = 2 * P + 13
+            # (rows page-aligned: hipHostRegister locks whole pages)
+            raw_q, raw_s = np.zeros(16 * n + 8192, np.uint8), np.zeros(32 * n + 8192, np.uint8)
+            oq, os_ = (-raw_q.ctypes.data) % 4096, (-raw_s.ctypes.data) % 4096
+            req = raw_q[oq:oq + 16 * n].view(np.uint32).reshape(n, 4)
+            res = raw_s[os_:os_ + 32 * n].view(FETCH_RES_DTYPE)
+            req[:, 0] = g.integers(0, P + 2, n)
+            req[:, 1] = g.integers(0, C, n)
+            req[:, 2] = g.integers(0, 500, n)
+            if register:
+                dev.host_register(req)
+                dev.host_register(res)
+            try:
+                out = np.zeros(cap, np.uint8)
+                tk = dev.fetch_async(None, None, None, out=out, out_cap=cap, req=req, res=res, pinned_rows=True)
+                rc, got, used = dev.fetch_poll(tk, wait=True)
+                rc_w, want, wbuf, used_w = dev.fetch(req[:, 0].copy(), req[:, 1].copy(), req[:, 2].copy(), out_cap=cap)
+                assert rc == rc_w == A.RMQ_OK and used == used_w, register
+                assert got is res
+                for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                    assert np.array_equal(res[f], want[f]), (register, f)
+                assert (res["count"] > 0).any()
+                for r in np.flatnonzero((res["status"] == 0) & (res["bytes"] > 0)):
+                    a, b = int(res["out_pos"][r]), int(res["out_pos"][r] + res["bytes"][r])
+                    assert np.array_equal(out[a:b], wbuf[a:b]), (register, r)
+            finally:
+                if register:
+                    dev.host_unregister(req)
+                    dev.host_unregister(res)
 
 
 def test_pinned_rows_match_sync():
