@@ -532,6 +532,8 @@ void free_engine(rmq_engine* e) {
     if (f.h_res) hipHostFree(f.h_res);
     if (f.ev) hipEventDestroy(f.ev);
     if (f.ev_copy) hipEventDestroy(f.ev_copy);
+    if (f.ev_in) hipEventDestroy(f.ev_in);
+    if (f.ev_k) hipEventDestroy(f.ev_k);
   }
   for (const StateSet& z : e->sets) {
     bufs.push_back(z.leo);
@@ -688,6 +690,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_PAIR")) e->s3_pair = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_FETCH_DMA")) e->fetch_dma = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_FETCH_DMA_IN")) e->fetch_dma_in = (uint32_t)std::atoi(v);
   if (e->stamps_path || e->steal) e->split = 0;  // (phase stamps and stealing read one launch's roles)
 #define CREATE_TRY(x)      \
   do {                     \
@@ -728,6 +732,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   for (rmq_engine::FetchSlot& f : e->fslot) {
     CREATE_HIP(hipEventCreateWithFlags(&f.ev, hipEventDisableTiming));
     CREATE_HIP(hipEventCreateWithFlags(&f.ev_copy, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&f.ev_in, hipEventDisableTiming));
+    CREATE_HIP(hipEventCreateWithFlags(&f.ev_k, hipEventDisableTiming));
   }
 
   const uint32_t P = cfg->num_partitions, RF = cfg->replication_factor, C = cfg->max_consumers;
@@ -1602,7 +1608,7 @@ int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t
 namespace {
 // Issue a fetch into the next slot: its kernels on the pipeline stream, an event after them.
 int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
-                uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
+                uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket, bool sync) {
   if (!e || !ticket) return RMQ_EINVAL;
   bool rows_pinned = (mem & RMQ_FETCH_PINNED_ROWS) != 0;
   const bool rows_dev = (mem & RMQ_FETCH_DEVICE_ROWS) != 0;
@@ -1658,9 +1664,12 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
   int rc = fetch_slot_reserve(f, n, mem == RMQ_MEM_HOST ? out_cap : 0, e->main_s);
   if (rc) return rc;
   uint8_t* d_out = mem == RMQ_MEM_HOST ? (out_cap ? f.d_out : nullptr) : out;
-  // The kernels read the request rows from page-locked host memory and write the result rows
-  // there (no copy either way): the caller's own rows (RMQ_FETCH_PINNED_ROWS, if the runtime maps
-  // them), else the slot's staging rows.
+  // Host rows are page-locked: the caller's own (RMQ_FETCH_PINNED_ROWS, if the runtime maps them),
+  // else the slot's staging rows. The kernels read and write them in place across PCIe (no copy
+  // either way: the lowest latency for one call), or (RMQ_FETCH_DMA, asynchronous calls by
+  // default) the request rows go to the slot's device rows by DMA on the copy stream and the
+  // result rows come back by DMA on the result stream, so the kernels touch device memory only
+  // and a burst's copies overlap the other fetches' kernels.
   void* d_rq = nullptr;
   void* d_rs = nullptr;
   if (rows_dev) {
@@ -1676,11 +1685,22 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     d_rq = f.h_req;
     d_rs = f.h_res;
   }
+  const bool dma = !rows_dev && (e->fetch_dma >= 2 || (e->fetch_dma == 1 && !sync));
+  void* h_rs = rows_pinned ? static_cast<void*>(res) : static_cast<void*>(f.h_res);  // (DMA) result rows' host copy
+  const bool dma_in = dma && e->fetch_dma_in;
+  if (dma_in) {
+    HIP_TRY(hipMemcpyAsync(f.d_req, rows_pinned ? static_cast<const void*>(reqs) : static_cast<const void*>(f.h_req),
+                           (size_t)n * sizeof(rmq_fetch_req), hipMemcpyHostToDevice, e->copy_s));
+    HIP_TRY(hipEventRecord(f.ev_in, e->copy_s));
+    d_rq = f.d_req;
+  }
+  if (dma) d_rs = f.d_res;  // (the gather reads a request's resolve words, then writes its final row there)
   {
     // Order against the append pipeline without flushing it: on the pipeline's stream, after the
     // last launch issued so far and before the next, so no ring bytes or log starts it reads change
     // under it.
     std::lock_guard<std::mutex> g(e->mu);
+    if (dma_in) HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_in, 0));
     FetchArgs a{};
     a.st = e->st;
     a.req = static_cast<const uint32_t*>(d_rq);
@@ -1722,7 +1742,14 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
       HIP_TRY(hipGetLastError());
     }
     if (e->profile) HIP_TRY(hipEventRecord(r1, e->main_s));
-    HIP_TRY(hipEventRecord(f.ev, e->main_s));  // kernels done: result rows and bytes needed in place
+    if (dma) {  // the result rows to the host behind the kernels, off the pipeline stream
+      HIP_TRY(hipEventRecord(f.ev_k, e->main_s));
+      HIP_TRY(hipStreamWaitEvent(e->fetch_out_s, f.ev_k, 0));
+      HIP_TRY(hipMemcpyAsync(h_rs, f.d_res, (size_t)n * sizeof(rmq_fetch_res), hipMemcpyDeviceToHost, e->fetch_out_s));
+      HIP_TRY(hipEventRecord(f.ev, e->fetch_out_s));
+    } else {
+      HIP_TRY(hipEventRecord(f.ev, e->main_s));  // kernels done: result rows and bytes needed in place
+    }
   }
   f.rows_pinned = rows_pinned || rows_dev;  // (no copy of the rows at completion)
   f.ticket = tk;
@@ -1743,7 +1770,7 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
 
 int rmq_fetch_async(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem, uint8_t* out,
                     uint64_t out_cap, rmq_fetch_res* res, uint64_t* ticket) {
-  return fetch_issue(e, reqs, n, mem, out, out_cap, res, ticket);
+  return fetch_issue(e, reqs, n, mem, out, out_cap, res, ticket, false);
 }
 
 int rmq_fetch_poll(rmq_engine* e, uint64_t ticket, uint32_t wait, uint64_t* bytes_used) {
@@ -1771,7 +1798,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
   if (!e) return RMQ_EINVAL;
   if (!n) return RMQ_OK;
   uint64_t t = 0;
-  const int rc = fetch_issue(e, reqs, n, mem, out, out_cap, res, &t);
+  const int rc = fetch_issue(e, reqs, n, mem, out, out_cap, res, &t, true);
   if (rc) return rc;
   return rmq_fetch_poll(e, t, 1, bytes_used);
 }

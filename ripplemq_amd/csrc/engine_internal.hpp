@@ -347,6 +347,8 @@ struct rmq_engine {
     uint64_t out_alloc = 0;
     hipEvent_t ev = nullptr;     // its kernels done (result rows and bytes needed in place)
     hipEvent_t ev_copy = nullptr;  // host output copies done
+    hipEvent_t ev_in = nullptr;    // (DMA rows) request rows on the device
+    hipEvent_t ev_k = nullptr;     // (DMA rows) kernels done: the result rows' copy may start
     bool rows_pinned = false;      // the caller's rows read / written in place (pinned or device rows)
     uint64_t* need = nullptr;      // bytes needed: a word of fetch_need_host (the gather stores it)
     uint64_t* need_dev = nullptr;  // its device address
@@ -431,6 +433,13 @@ struct rmq_engine {
   uint64_t* state_stage = nullptr;  // page-locked staging of rmq_get_partition_states
   size_t state_stage_words = 0;
   uint32_t s3_pair = 0;         // RMQ_S3_PAIR=1: stage-3 waves take two tasks each (single-GPU kernel)
+  // RMQ_FETCH_DMA: host request / result rows of a fetch moved by DMA (request rows on copy_s before
+  // the kernels, result rows on fetch_out_s after them) instead of read and written in place by
+  // the kernels across PCIe: 0 never (default), 1 for rmq_fetch_async, 2 for every fetch. Measured
+  // (round 5, tools/exp_dma.sh): the kernels gain 4-11 us but each fetch's copies and cross-stream
+  // waits add ~100 us (max = 10 bursts 3.3 -> 1.1 G records/s), so in place stays the default
+  uint32_t fetch_dma = 0;
+  uint32_t fetch_dma_in = 1;    // RMQ_FETCH_DMA_IN=0: with DMA, the request rows still read in place
   hipStream_t rank_s = nullptr;
   hipEvent_t ev_rank[2] = {nullptr, nullptr};  // rank launch L recorded in slot L & 1
   hipEvent_t ev_pre_rank = nullptr;            // main_s before a rank launch

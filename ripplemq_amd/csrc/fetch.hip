@@ -190,9 +190,9 @@ struct Resolved {
 
 __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, bool live) {
   const DevState& st = a.st;
-  // the request row, read once from host memory; the device copy for the gather and the cache
+  // the request row, read once (from host memory: a device copy for the gather and the cache)
   const uint4 rq = live ? *reinterpret_cast<const uint4*>(a.req + 4ull * r) : make_uint4(0, 0, 0, 0);
-  if (live && (lane_id() & 31u) == 0) *reinterpret_cast<uint4*>(a.req_dev + 4ull * r) = rq;
+  if (live && (lane_id() & 31u) == 0 && a.req != a.req_dev) *reinterpret_cast<uint4*>(a.req_dev + 4ull * r) = rq;
   const u32 p = rq.x, c = rq.y, mx = rq.z;
   int status = kOk;
   u64 start = 0, count = 0, end = 0, ring_off = 0;
