@@ -188,11 +188,8 @@ struct Resolved {
   int status;
 };
 
-__device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, bool live) {
+__device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, const uint4 rq, bool live) {
   const DevState& st = a.st;
-  // the request row, read once (from host memory: a device copy for the gather and the cache)
-  const uint4 rq = live ? *reinterpret_cast<const uint4*>(a.req + 4ull * r) : make_uint4(0, 0, 0, 0);
-  if (live && (lane_id() & 31u) == 0 && a.req != a.req_dev) *reinterpret_cast<uint4*>(a.req_dev + 4ull * r) = rq;
   const u32 p = rq.x, c = rq.y, mx = rq.z;
   int status = kOk;
   u64 start = 0, count = 0, end = 0, ring_off = 0;
@@ -254,8 +251,21 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, u32 r, b
 __global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
   const u32 lane = lane_id(), w = threadIdx.x >> 6;
   const u32 r = (blockIdx.x * kRW + w) * kRPW + (lane >> 5);
-  const bool live = r < a.n;  // (no early return: the workgroup meets at a barrier below)
-  const Resolved q = resolve_request(a, r, live);
+  const bool live = r < a.n;  // (no early return: the workgroup meets at barriers below)
+  // the workgroup's request rows, read once by one load of consecutive 16-byte rows (host rows:
+  // one PCIe read of 128 bytes instead of a 16-byte read per request), through LDS; the device
+  // copy for the gather and the position cache
+  __shared__ uint4 s_rq[kRW * kRPW];
+  {
+    const u32 r0 = blockIdx.x * kRW * kRPW + threadIdx.x;
+    if (threadIdx.x < kRW * kRPW && r0 < a.n) {
+      const uint4 x = *reinterpret_cast<const uint4*>(a.req + 4ull * r0);
+      s_rq[threadIdx.x] = x;
+      if (a.req != a.req_dev) *reinterpret_cast<uint4*>(a.req_dev + 4ull * r0) = x;
+    }
+  }
+  __syncthreads();
+  const Resolved q = resolve_request(a, live ? s_rq[w * kRPW + (lane >> 5)] : make_uint4(0, 0, 0, 0), live);
   __shared__ u64 s_b[kRW];
   const u64 b2 = bcast_u64(q.bytes, 0) + bcast_u64(q.bytes, 32);  // the wave's two requests
   if (lane == 0) s_b[w] = b2;
@@ -283,6 +293,11 @@ __global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
     for (u32 k = 0; k < kRW; ++k) b += s_b[k];
     if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kRW * kRPW / kFetchChunk) * kCsumStride], (unsigned long long)b);
   }
+}
+
+// Lane src's value (src per lane).
+__device__ __forceinline__ u64 shfl_u64(u64 v, int src) {
+  return ((u64)(u32)__shfl((int)(v >> 32), src, 64) << 32) | (u32)__shfl((int)(u32)v, src, 64);
 }
 
 constexpr u32 kGQ = 4;          // requests per gather wave
@@ -338,6 +353,7 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
   const u64 inc = wave_incl_scan(nb);  // kGR <= 64: one wave holds them all
   __syncthreads();
   const u64 base = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+  u64 f0 = 0, f1 = 0, f2 = 0, f3 = 0;  // the final row of request rr (tid < kGR)
   if (tid < kGR && rr < a.n) {
     const u64 pos = base + inc - nb;
     s_pos[tid] = pos;
@@ -348,9 +364,10 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
       w2 = 0;
       w3 = (u64)(uint32_t)kNoSpc;
     }
-    // the final row, into the caller's page-locked rows (or the slot's staging rows)
-    *reinterpret_cast<ulonglong2*>(a.res_host + 4ull * rr) = make_ulonglong2(w0, pos);
-    *reinterpret_cast<ulonglong2*>(a.res_host + 4ull * rr + 2) = make_ulonglong2(w2, w3);
+    f0 = w0;
+    f1 = pos;
+    f2 = w2;
+    f3 = w3;
     if (rr + 1 == a.n)  // bytes needed
       __hip_atomic_store(a.need_host, pos + nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     // RMQ_FETCH_COMMIT: the consumer's next offset once its records are in the output (or the
@@ -363,6 +380,17 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
         a.st.cdirty[p] = 1u;  // (with a transport the row travels with the next round)
       }
     }
+  }
+  if (w == 0) {
+    // the final rows into the caller's page-locked rows (or the slot's staging rows): lane j
+    // stores half j & 1 of row r0 + j / 2, so one store covers the workgroup's rows contiguously
+    // (host rows: whole PCIe writes, not 16-byte pieces at a 32-byte stride)
+    static_assert(2 * kGR <= 64, "one wave holds the workgroup's rows");
+    const int src = (int)(lane >> 1);
+    const u64 x0 = shfl_u64(f0, src), x1 = shfl_u64(f1, src), x2 = shfl_u64(f2, src), x3 = shfl_u64(f3, src);
+    if (lane < 2 * kGR && r0 + (lane >> 1) < a.n)
+      *reinterpret_cast<ulonglong2*>(a.res_host + 4ull * r0 + 2ull * lane) =
+          (lane & 1u) ? make_ulonglong2(x2, x3) : make_ulonglong2(x0, x1);
   }
   __syncthreads();
   // the wave's requests one after the other (one stream of 16-byte pieces per wave: four requests
