@@ -1,4 +1,5 @@
-# The tier leg alone (and the tier GPU test), twice per spill chunk count. [CHUNKS="1 4"] bash tools/exp_tier.sh <tag>
+# The tier leg alone (and the tier GPU test), twice. bash tools/exp_tier.sh <tag>
+# (round 5's chunked-spill sweep set RMQ_TIER_CHUNKS per run, CHUNKS="1 2 4 8"; the chunked spill was reverted)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
