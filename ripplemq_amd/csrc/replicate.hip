@@ -448,6 +448,20 @@ __device__ __forceinline__ void verify_task(const IngestArgs& A, const u32 (*t8)
   }
 }
 
+// Whether the bytes of a record's last 16-byte piece past its payload (L bytes) are zero.
+__device__ __forceinline__ bool pad_zero(const uint4 t, u32 L) {
+  const u32 nb = L & 15u;  // payload bytes in the last piece (0: it is all payload)
+  u32 z = 0;
+  const u32 w4[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+  for (u32 i = 0; i < 4; ++i) {
+    const u32 lo = 4u * i;  // the word's first byte
+    const u32 keep = nb <= lo ? 0u : nb >= lo + 4u ? 0xFFFFFFFFu : (1u << (8u * (nb - lo))) - 1u;
+    z |= w4[i] & ~keep;
+  }
+  return nb == 0u || z == 0u;
+}
+
 // One task (64 records of one source region) of the verify kernel, by one wave: a lane per record.
 // The lane runs the CRC32C register through the record's payload pieces in order (slicing-by-8 from
 // LDS, two steps per 16-byte piece, no zero-shift tables); records over 1 KB by the whole wave.
@@ -462,6 +476,7 @@ __device__ __forceinline__ void verify_task_lane(const IngestArgs& A, const u32 
   const DevState& st = A.st;
   u32 p = 0, L = 0, m = 0, e = 0;
   u64 pos = 0, off = 0;
+  u64 p_used = 0, p_ring = 0;  // the partition's live log end and ring word (the index writes below)
   bool ok = false, owner = false, reb = false;
   const uint8_t* rec = R.base;
   uint4 hdr = make_uint4(0, 0, 0, 0);
@@ -510,16 +525,25 @@ __device__ __forceinline__ void verify_task_lane(const IngestArgs& A, const u32 
          off == d.first + (i - d.tstart) && rel + 16ull * (1ull + m) <= 16ull * d.bytes16 && chained &&
          A.bad[e] == 0u;
     if (!ok && A.bad[e] == 0u) atomicOr(&A.bad[e], kBadCrc);  // the record's content is wrong
+    // loaded now (in flight with the payload loads below) rather than after the CRC
+    if (ok && owner && !reb) {
+      p_used = st.used[p];
+      p_ring = st.ring[p];
+    }
   }
   const bool big = ok && m > kBigIngest;
   const u32 mm = ok && !big ? m : 0u;
   // the CRC register over the payload pieces in order (zero-padded in the log), from ~0
   u32 acc = 0xFFFFFFFFu;
+  bool padz = true;  // the zero padding after the payload in the record's last piece (small records)
   {
     const uint4 sv[4] = {sp0, sp1, sp2, sp3};
 #pragma unroll
     for (u32 u = 0; u < kVSpec; ++u)
-      if (u < mm) acc = crc_step8(t8, crc_step8(t8, acc, sv[u].x, sv[u].y), sv[u].z, sv[u].w);
+      if (u < mm) {
+        acc = crc_step8(t8, crc_step8(t8, acc, sv[u].x, sv[u].y), sv[u].z, sv[u].w);
+        if (u + 1u == mm) padz = pad_zero(sv[u], L);
+      }
   }
   for (u32 c = kVSpec; __any(c < mm); c += 4) {
     uint4 v[4];
@@ -528,7 +552,10 @@ __device__ __forceinline__ void verify_task_lane(const IngestArgs& A, const u32 
       v[u] = c + u < mm ? *reinterpret_cast<const uint4*>(rec + 16ull + 16ull * (c + u)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (u32 u = 0; u < 4; ++u)
-      if (c + u < mm) acc = crc_step8(t8, crc_step8(t8, acc, v[u].x, v[u].y), v[u].z, v[u].w);
+      if (c + u < mm) {
+        acc = crc_step8(t8, crc_step8(t8, acc, v[u].x, v[u].y), v[u].z, v[u].w);
+        if (c + u + 1u == mm) padz = pad_zero(v[u], L);
+      }
   }
   // records over 1 KB, one at a time by the wave: lane l takes pieces l, l + 64, ... (Horner with
   // the 1 KB shift), shifts past the pieces after its last one, XOR-reduce; the record's lane gets
@@ -570,21 +597,17 @@ __device__ __forceinline__ void verify_task_lane(const IngestArgs& A, const u32 
       crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
     }
     // the zero padding after the payload (FORMAT.md §1) is part of the record
-    if (m && (L & 15u)) {
-      const uint4 t = *reinterpret_cast<const uint4*>(rec + 16ull * m);  // the last piece
-      const u32 nb = L & 15u;
-      const u32 w4[4] = {t.x, t.y, t.z, t.w};
-      for (u32 b = nb; b < 16u; ++b)
-        if ((w4[b >> 2] >> (8u * (b & 3u))) & 0xFFu) crc = ~hdr.w;
-    }
+    // (a large record's last piece is read again: the wave folded its pieces)
+    if (big && m) padz = pad_zero(*reinterpret_cast<const uint4*>(rec + 16ull * m), L);
+    if (!padz) crc = ~hdr.w;
     if (crc == hdr.w) {
       // (a rebase entry's index entries are written by finish, once the entry is accepted: its
       // positions lie past the live log but may share index slots with it)
       if (owner && !reb) {
         // sparse index past the follower's live log: every interval multiple the record crosses
         const u32 ilog = st.interval_log2;
-        const RingRef rg = ring_ref(st, p);
-        const u64 end = pos + 16ull * (1ull + m), live = st.used[p] >> ilog;
+        const RingRef rg = ring_ref(p_ring, ilog, st.icap_mul);
+        const u64 end = pos + 16ull * (1ull + m), live = p_used >> ilog;
         for (u64 q = (pos >> ilog) + 1; (q << ilog) <= end; ++q) {
           if (q <= live) continue;  // inside the live log (a truncation): finish writes it if accepted
           u64* ie = st.index + (rg.ibase + q % rg.icap) * 2;
