@@ -62,11 +62,11 @@ for step in "$@"; do
     local2)
       run 300 "${T}_local2.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
       prof 300 local2_prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_local2_kt" -o kt -- python3 "$R/bench.py" --gpus 2 --transport local --steps 100 --warmup 10 --segment-mb 2 --pool 8 $Q ;;
-    ab2|ab2:*)  # A/B of the 2-rank rehearsal: current library vs variants/NAME/ (default head), two pairs
+    ab2|ab2:*)  # A/B of the 2-rank rehearsal: current library vs variants/NAME/ (default head; NAME+NAME2: several), two rounds
       V=head; [ "$step" != ab2 ] && V=${step#ab2:}
       for k in 1 2; do
-        for v in cur $V; do
-          if [ $v = cur ]; then L=$R/ripplemq_amd/libripplemq_engine.so; else L=$R/variants/$V/libripplemq_engine.so; fi
+        for v in cur ${V//+/ }; do
+          if [ $v = cur ]; then L=$R/ripplemq_amd/libripplemq_engine.so; else L=$R/variants/$v/libripplemq_engine.so; fi
           RMQ_LIB=$L run 300 "${T}_local2_${v}_$k.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
         done
       done ;;
