@@ -10,6 +10,7 @@
 #   bench      default bench line (2000 steps, CPU baseline, fetch, concurrent and host legs)
 #   bench20    two driver-shaped lines (--steps 20 --warmup 5)
 #   steady     one 600-step line without the side legs
+#   kt20       kernel trace of a 20-step line (fill / drain launches)
 #   benchD     config D (RF 5, 64 B..16 KB) line
 #   ab[:NAME]  A/B of the current library against variants/NAME/ (default head; 400- and 20-step lines, 2 pairs)
 #   local2     2-rank rehearsal on one GPU over the in-process transport (+ kernel trace)
@@ -49,6 +50,8 @@ for step in "$@"; do
     bench) run 500 "${T}_bench.json" python bench.py ;;
     bench20) for k in 1 2; do run 200 "${T}_bench20_$k.json" python bench.py --gpus 1 --steps 20 --warmup 5; done ;;
     steady) run 300 "${T}_steady.json" python bench.py --steps 600 --warmup 60 $Q ;;
+    kt20)  # kernel trace of a driver-shaped line (20 steps): the fill and drain launches
+      prof 200 kt20 --kernel-trace -f csv -d "$R/gpurun_out/${T}_kt20" -o kt -- python3 "$R/bench.py" --steps 20 --warmup 5 $Q ;;
     benchD) run 300 "${T}_benchD.json" python bench.py --config D --pool 16 --steps 200 --warmup 20 --no-cpu-baseline --host-steps 0 ;;
     ab|ab:*)  # ab:NAME compares against variants/NAME/ (default head)
       V=head; [ "$step" != ab ] && V=${step#ab:}
