@@ -363,3 +363,50 @@ def test_pinned_rows_match_sync():
                 assert np.array_equal(buf[a:b], wbuf[a:b]), (k, r)
             dev.device_free(d_out)
         dev.sync()
+
+
+@pytest.mark.parametrize("dma_in", ["1", "0"])
+def test_rows_by_dma_match_rows_in_place(monkeypatch, dma_in):
+    """RMQ_FETCH_DMA=2 (a measured knob, off by default): request rows copied to the device and result
+    rows copied back around the kernels (RMQ_FETCH_DMA_IN=0: result rows only) give the results of
+    the default path, where the kernels read and write the rows in place; host and device outputs,
+    synchronous and asynchronous calls, page-locked and staged rows."""
+    P, C = 96, 2
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=C, max_batch_records=8192)
+    spec = StreamSpec(P, 4000, "zipf", size=(1, 300), config_index=57)
+    g = np.random.default_rng(57)
+    n = 2 * P + 7
+    p, c, mx = g.integers(0, P + 2, n), g.integers(0, C, n), g.integers(0, 400, n)
+    cap = 4 << 20
+
+    def run():
+        out = []
+        with Engine(cfg) as dev:
+            for b in range(3):
+                bt = make_batch(spec, b)
+                dev.append(bt.pidx, bt.lens, bt.payload)
+            rc, res, buf, used = dev.fetch(p, c, mx, out_cap=cap)  # staged rows, host output
+            out.append((rc, res.copy(), bytes(buf[:used])))
+            req, rs = dev.fetch_rows(n)
+            req[:, 0], req[:, 1], req[:, 2] = p, c, mx
+            d_out = dev.device_alloc(cap)
+            tk = dev.fetch_async(None, None, None, d_out=d_out, out_cap=cap, req=req, res=rs, pinned_rows=True)
+            rc, res, used = dev.fetch_poll(tk, wait=True)
+            got = np.empty(max(used, 1), np.uint8)
+            if used:
+                dev.d2h(got[:used], d_out)
+            out.append((rc, res.copy(), bytes(got[:used])))
+            dev.device_free(d_out)
+        return out
+
+    want = run()
+    monkeypatch.setenv("RMQ_FETCH_DMA", "2")
+    monkeypatch.setenv("RMQ_FETCH_DMA_IN", dma_in)
+    got = run()
+    for k, (a, b) in enumerate(zip(got, want)):
+        assert a[0] == b[0] == A.RMQ_OK, k
+        for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+            assert np.array_equal(a[1][f], b[1][f]), (k, f)
+        assert a[2] == b[2], k
+    assert (want[0][1]["count"] > 0).any()
