@@ -8,7 +8,8 @@
 // replica (ConsumerOffsetUpdateRequestProcessor.java:59-60, PartitionStateMachine.java:48-49). Here
 // a round carries one launch group of the leader's appends (and any catch-up gap) for every
 // partition the two ranks share, as one region of the exchange, plus the changed consumer-offset
-// rows. Four kernels, in order on the exchange stream:
+// rows. Three launches, in order on the exchange stream (finish and copy share the last one: both
+// only read verify's verdicts):
 //   ingest_prepare (thread per entry): the log end the entry continues — the follower's own, or,
 //     when the entry's first offset lies inside the follower's retained log below its end, that
 //     offset and its position (truncation: the leader's log wins; the position from the sparse
@@ -649,22 +650,32 @@ __global__ __launch_bounds__(kIT, RMQ_VERIFY_WAVES) void ingest_verify_kernel(In
 
 // The verdict and state of entry e (thread per entry); its records and bytes ingested are added
 // to n_rec / n_bytes (the kernel sums them over the wave: one atomic per wave, not per entry).
+// The verdict on entry e once verify has run: its own refusal bits (a structurally broken region
+// refuses all its entries; so does a round whose copy items overflowed: only corrupted regions ask
+// for more than the host's bound, and no entry may be accepted with bytes left uncopied), and those
+// of the partition's other local slot (adjacent entries of the same source: a refusal of either
+// refuses both). Finish and the copy each derive it.
+struct Verdict {
+  u32 own, bad;
+};
+__device__ __forceinline__ Verdict entry_verdict(const IngestArgs& A, u32 e, u32 src, u32 p) {
+  const bool broken = __hip_atomic_load(&A.insane[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+                      *A.n_items > A.items_grid;
+  Verdict v;
+  v.own = A.bad[e] | (broken ? kBadCrc : 0u);
+  v.bad = v.own;
+  for (u32 q = e; q > A.xi_start[src] && A.xi_p[q - 1] == p; --q) v.bad |= A.bad[q - 1];
+  for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) v.bad |= A.bad[q];
+  return v;
+}
+
 __device__ __forceinline__ void finish_entry(const IngestArgs& A, u32 e, u64& n_rec, u64& n_bytes) {
   const u32 src = source_of_entry(A, e);
   const DevState& st = A.st;
   const u32 p = A.xi_p[e], k = e - A.xi_start[src];
   const bool owner = k == 0 || A.xi_p[e - 1] != p;
-  // a structurally broken region refuses all its entries; so does a round whose copy items
-  // overflowed (only corrupted regions ask for more than the host's bound: no entry may be
-  // accepted with bytes left uncopied)
-  const bool broken = __hip_atomic_load(&A.insane[src], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
-                      *A.n_items > A.items_grid;
-  // two local slots of one partition (adjacent entries of the same source): a refusal of either
-  // refuses both
-  const u32 own = A.bad[e] | (broken ? kBadCrc : 0u);
-  u32 bad = own;
-  for (u32 q = e; q > A.xi_start[src] && A.xi_p[q - 1] == p; --q) bad |= A.bad[q - 1];
-  for (u32 q = e + 1; q < A.xi_start[src + 1] && A.xi_p[q] == p; ++q) bad |= A.bad[q];
+  const Verdict vd = entry_verdict(A, e, src, p);
+  const u32 own = vd.own, bad = vd.bad;
   if (own) atomicAdd((unsigned long long*)&A.counters[(own & kBadCrc) && !(own & ~kBadCrc) ? 1 : 2], 1ull);
   A.acc[e] = bad ? 0u : 1u;
   // an entry of the current term from a leader whose region arrived: the leader is alive (the
@@ -761,8 +772,7 @@ __device__ __forceinline__ void finish_entry(const IngestArgs& A, u32 e, u64& n_
   A.ackout[2 * e + 1] = nused;
 }
 
-__global__ void ingest_finish_kernel(IngestArgs A) {
-  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void finish_block(const IngestArgs& A, u32 e) {
   u64 n_rec = 0, n_bytes = 0;
   if (e < A.n_in) finish_entry(A, e, n_rec, n_bytes);
   // every lane of the wave is back here (blockDim is a multiple of 64)
@@ -780,15 +790,15 @@ __global__ void ingest_finish_kernel(IngestArgs A) {
 // {entry, 16 KiB chunk of its data}, 16-byte pieces, four in flight per thread. A work item is a
 // chain of dependent lookups before its first data load, so items are one wave each: up to 32 per
 // CU in flight.
-__global__ __launch_bounds__(kCT) void ingest_copy_kernel(IngestArgs A) {
-  const u32 it = blockIdx.x;
+__device__ __forceinline__ void copy_item(const IngestArgs& A, u32 it) {
   if (it >= *A.n_items) return;
   const u32 e = A.items[2 * it], c = A.items[2 * it + 1];
-  // the verdict and the entry's descriptor (prepare) in one round of loads
-  const u32 ok = A.acc[e];
+  // the verdict (derived here, as finish derives it beside this copy) and the entry's descriptor
+  // (prepare), loaded together
   const u64* cd = A.cdesc + 4ull * e;
   const u64 d0 = cd[0], d1 = cd[1], bused = cd[2], d3 = cd[3];
-  if (!ok) return;
+  const u32 src = source_of_entry(A, e);
+  if (entry_verdict(A, e, src, A.xi_p[e]).bad) return;
   const uint8_t* data = reinterpret_cast<const uint8_t*>(d0);
   uint8_t* const ring = reinterpret_cast<uint8_t*>(d1);
   const u64 seg = 1ull << (d3 & 63ull), segmask = seg - 1ull;
@@ -812,6 +822,17 @@ __global__ __launch_bounds__(kCT) void ingest_copy_kernel(IngestArgs A) {
       if (q >= b0 && q < b1 && x + seg >= gend) store_log16(ring + (x & segmask), v[u]);
     }
   }
+}
+
+// Finish and copy in one launch (both only read verify's verdicts): one-wave workgroups, the
+// first fin_blocks finish entries (a thread each), the rest copy one work item each. The copy no
+// longer waits for finish to end (one kernel less in each round's ingest chain).
+__global__ __launch_bounds__(kCT) void ingest_finish_copy_kernel(IngestArgs A, u32 fin_blocks) {
+  static_assert(kCT == 64, "one-wave workgroups (finish sums its counters per wave)");
+  if (blockIdx.x < fin_blocks)
+    finish_block(A, blockIdx.x * kCT + threadIdx.x);
+  else
+    copy_item(A, blockIdx.x - fin_blocks);
 }
 
 // Acks of one round applied after the pipeline has drained (thread per partition).
@@ -875,8 +896,8 @@ void launch_ingest(const IngestArgs& a, uint32_t tasks, uint32_t items_bound, ui
   if (a.n_in) hipLaunchKernelGGL(ingest_prepare_kernel, dim3((a.n_in + kEntryT - 1) / kEntryT), dim3(kEntryT), 0, s, a);
   if (tasks)
     hipLaunchKernelGGL(ingest_verify_kernel, dim3(std::min<uint32_t>((tasks + kIW - 1) / kIW, verify_wgs)), dim3(kIT), 0, s, a);
-  if (a.n_in) hipLaunchKernelGGL(ingest_finish_kernel, dim3((a.n_in + kEntryT - 1) / kEntryT), dim3(kEntryT), 0, s, a);
-  if (items_bound) hipLaunchKernelGGL(ingest_copy_kernel, dim3(items_bound), dim3(kCT), 0, s, a);
+  const u32 fin = (a.n_in + kCT - 1) / kCT;
+  if (fin + items_bound) hipLaunchKernelGGL(ingest_finish_copy_kernel, dim3(fin + items_bound), dim3(kCT), 0, s, a, fin);
 }
 
 // Fault injection (rmq_fault_corrupt): one byte of a region flipped before it is sent.
