@@ -73,6 +73,9 @@ for step in "$@"; do
           RMQ_LIB=$L run 300 "${T}_local2_${v}_$k.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
         done
       done ;;
+    local2kt:*)  # rehearsal kernel trace with variants/NAME/
+      V=${step#local2kt:}
+      RMQ_LIB=$R/variants/$V/libripplemq_engine.so prof 300 local2_prof_$V --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_local2_kt_$V" -o kt -- python3 "$R/bench.py" --gpus 2 --transport local --steps 100 --warmup 10 --segment-mb 2 --pool 8 $Q ;;
     local4) run 300 "${T}_local4.json" python bench.py --gpus 4 --transport local --steps 100 --warmup 10 --segment-mb 1 --pool 4 --config C $Q ;;
     prof) prof 500 prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_prof" -o kt -- python3 "$R/bench.py" --no-cpu-baseline --host-steps 0 ;;
     pmc)
