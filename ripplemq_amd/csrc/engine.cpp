@@ -244,6 +244,8 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     // the rest of stage 3, so the ranking/scan chains start before stage 3's last workgroups and
     // end with them (RMQ_S3_LEAD=<n>; RMQ_S3_FIRST=0 puts all of stage 3 last)
     a.s3_lead = e->s3_first ? std::min<uint32_t>(a.wg3, e->s3_lead ? e->s3_lead : a.wg3) : 0u;
+    // (only with every stage-3 workgroup first: then its block index is its stage-3 index)
+    a.s3_xcd = e->s3_xcd && a.s3_lead == a.wg3 && !a.s3_pair ? 1u : 0u;
   }
   a.launch_seq = ++e->launch_seq;
   e->st.csnap_slot = (uint32_t)(a.launch_seq & 1ull);  // control kernels after this launch write its slot
@@ -689,6 +691,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_PAIR")) e->s3_pair = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S3_XCD")) e->s3_xcd = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_FETCH_DMA")) e->fetch_dma = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_FETCH_DMA_IN")) e->fetch_dma_in = (uint32_t)std::atoi(v);

@@ -2162,7 +2162,17 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   const u32 tasks = G.task0[G.nb];
   const u32 lane = threadIdx.x & 63;
   // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
-  u32 task = __builtin_amdgcn_readfirstlane(wg * kPW + (threadIdx.x >> 6));
+  u32 slot = wg;
+  if (A.s3_xcd) {
+    // blocks b and b + 8 share an XCD (round-robin placement, speed only): the stage-3 workgroups
+    // of one XCD take one contiguous range of slots, so records next to each other in a batch
+    // (and in their partitions' rings) are stored through one L2
+    const u32 x = wg & 7u, n = A.wg3;
+    u32 before = 0;
+    for (u32 y = 0; y < x; ++y) before += n > y ? (n - y + 7u) >> 3 : 0u;
+    slot = before + (wg >> 3);
+  }
+  u32 task = __builtin_amdgcn_readfirstlane(slot * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);
   if (!XR && A.s3_pair) {
     // two tasks per wave (task and task + wg3 waves; the engine sizes wg3 so every task has its
