@@ -262,7 +262,7 @@ def mixed_engine_leg(cfg: EngineConfig, rings: dict, pool, args) -> dict:
 
         for k in range(int(args.mixed_retain) + 64):  # the rings full (and their pages touched)
             step(k)
-        out = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group)
+        out = mixed_leg(eng, step, spec, args.concurrent_rounds, args.group, fetch_every=args.mixed_fetch_every)
         out["rings"] = ring_report(rings, eng.cfg.replication_factor, args.group, spec.partitions)
         out["retain_batches"] = args.mixed_retain
         for d in d_out:
@@ -272,17 +272,21 @@ def mixed_engine_leg(cfg: EngineConfig, rings: dict, pool, args) -> dict:
         eng.close()
 
 
-def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10) -> dict:
+def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers: int = 4, mx: int = 10,
+              fetch_every: float = 2.0) -> dict:
     """Appends and consumer fetches at once on one engine (configs[4]: concurrent consumer fetch at
     lagging offsets), driven by ONE host thread as a broker's event loop would: per round `appends`
     device-resident batches go to the pipeline, and every (partition, consumer) reads max = 10 and
     commits what it read (ConsumerClientImpl.java:61-117) through rmq_fetch_async with
     RMQ_FETCH_COMMIT: the read-then-commit of each consumer happens on the device, so the next fetch,
-    ordered after it on the fetch stream, reads on from there and two fetches can be in flight
+    ordered after it on the fetch stream, reads on from there and four fetches can be in flight
     without a host round trip between them. Fetches are polled without waiting; every fetch runs
     between two pipeline launches (the next launch waits for it). The broker bounds its own
     run-ahead to eight launch groups (rmq_poll_commit), so a fetch returns within about eight
-    launches. Reports both rates over the same wall time."""
+    launches. The consumers are paced: one read-and-commit pass of every consumer per `fetch_every`
+    rounds of appends (a pass reads up to max records per consumer), so the mix of the two does not
+    depend on how the host's polls happen to fall (unpaced, 106 and 258 passes over 250 rounds on
+    two boxes). Reports both rates over the same wall time."""
     P = spec.partitions
     eng.sync()
     st = eng.states()
@@ -294,7 +298,9 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     lag = (g.random(P * consumers) * (np.repeat(retained, consumers) // 2 + 1)).astype(np.int64)
     off = (np.repeat(hw, consumers) - lag).astype(np.uint64)
     eng.commit_consumer_offset(pp, cc, off)
-    inflight_f = 2
+    # passes in flight: each waits behind the appends queued before it on the pipeline stream (up to
+    # eight launch groups), so two in flight capped the passes at about one per four rounds
+    inflight_f = 4
     rows = [eng.fetch_rows(P * consumers) for _ in range(inflight_f)]  # page-locked request / result rows
     for rq, _ in rows:
         rq[:, 0], rq[:, 1], rq[:, 2], rq[:, 3] = pp, cc, mx, RMQ_FETCH_COMMIT
@@ -317,9 +323,11 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
         resets += int(np.count_nonzero(stt == -6))  # RMQ_EOFFSET: the ring moved past a slow
         # consumer, which resumes at the first retained offset (committed on the device)
 
+    budget = 1.0  # passes the pacing allows so far (one per fetch_every rounds)
+
     def service() -> bool:
-        """Completed fetches in, new ones out (at most two in flight). False if nothing moved."""
-        nonlocal fetches, t_host, nslot
+        """Completed fetches in, new ones out (at most inflight_f in flight). False if nothing moved."""
+        nonlocal fetches, t_host, nslot, budget
         t1 = time.perf_counter()
         moved = False
         while fq:
@@ -329,7 +337,8 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
             take(r)
             fq.popleft()
             moved = True
-        while len(fq) < inflight_f:
+        while len(fq) < inflight_f and budget >= 1.0:
+            budget -= 1.0
             k = nslot % inflight_f
             nslot += 1
             fq.append((eng.fetch_async(None, None, None, d_out=d_out[k], out_cap=cap, req=rows[k][0], res=rows[k][1],
@@ -351,6 +360,7 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
                 elif not service():
                     time.sleep(0)
             inflight.append(step(k0 + k * appends + j))
+        budget += 1.0 / fetch_every
         service()
     while fq:
         take(eng.fetch_poll(fq.popleft()[0], wait=True))
@@ -363,14 +373,16 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
         eng.host_release(rs)
     recs = rounds * appends * spec.records
     return {"append_msgs_per_s": recs / dt, "fetch_records_per_s": fetched / dt, "rounds": rounds,
-            "appends_per_round": appends, "fetches": fetches, "requests_per_fetch": P * consumers,
+            "appends_per_round": appends, "fetches": fetches, "fetch_every_rounds": fetch_every,
+            "requests_per_fetch": P * consumers,
             "max_records": mx, "wall_s": dt, "consumer_host_s": t_host,
             "lag_bound": "U[0, retained records / 2] per partition at the start",
             "consumer_resets": resets,
             "note": "one host thread: appends (device-resident batches, at most 8 launch groups not yet "
                     "complete) and, between them, every consumer's read-and-commit at max = 10 through "
-                    "rmq_fetch_async with RMQ_FETCH_COMMIT (two fetches in flight, polled without "
-                    "waiting); both rates over the same wall time; consumers start lagging the high "
+                    "rmq_fetch_async with RMQ_FETCH_COMMIT (four fetches in flight, polled without "
+                    f"waiting; one pass of every consumer per {fetch_every:g} rounds of appends); both "
+                    "rates over the same wall time; consumers start lagging the high "
                     "watermark by U[0, lag_bound] (configs[4] names U[0, 10^6]: that lag is not "
                     "HBM-resident at 4,096 partitions, so it is bounded by what the rings retain)"}
 
@@ -919,6 +931,8 @@ def main() -> None:
     ap.add_argument("--fetch-rounds", type=int, default=10, help="rounds of the fetch leg (0: skip)")
     ap.add_argument("--concurrent-rounds", type=int, default=250,
                     help="rounds of the append+fetch mixed leg (1 GPU; 0: skip)")
+    ap.add_argument("--mixed-fetch-every", type=float, default=2.0,
+                    help="mixed leg: rounds of appends per read-and-commit pass of every consumer")
     ap.add_argument("--tier-rounds", type=int, default=20,
                     help="rounds of the durable-tier leg (spills + reads below the rings, 1 GPU; 0: skip)")
     ap.add_argument("--host-steps", type=int, default=100,
