@@ -199,6 +199,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
       e->set_reset &= ~(1u << s1->set);
     }
     a.wg1 = e->s1_wgs ? std::min<uint32_t>(s1->tiles, e->s1_wgs) : s1->tiles;
+    a.s1_xcd = e->s1_xcd;
   }
   if (s2) {
     a.g2 = make_group(e, *s2);
@@ -692,6 +693,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_PAIR")) e->s3_pair = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_XCD")) e->s3_xcd = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S1_XCD")) e->s1_xcd = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_FETCH_DMA")) e->fetch_dma = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_FETCH_DMA_IN")) e->fetch_dma_in = (uint32_t)std::atoi(v);

@@ -435,6 +435,7 @@ struct rmq_engine {
   uint32_t s3_pair = 0;         // RMQ_S3_PAIR=1: stage-3 waves take two tasks each (single-GPU kernel)
   uint32_t s3_xcd = 1;          // RMQ_S3_XCD (default 1): stage-3 tasks in contiguous ranges per XCD
                                 //   (blockIdx % 8); round 5: 5.51-5.58 vs 5.43-5.51 G, 3 pairs, r05X8
+  uint32_t s1_xcd = 0;          // RMQ_S1_XCD=1: stage-1 tiles in contiguous ranges per XCD
   // RMQ_FETCH_DMA: host request / result rows of a fetch moved by DMA (request rows on copy_s before
   // the kernels, result rows on fetch_out_s after them) instead of read and written in place by
   // the kernels across PCIe: 0 never (default), 1 for rmq_fetch_async, 2 for every fetch. Measured

@@ -261,6 +261,7 @@ struct PipeArgs {
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
   uint32_t s3_pair;        // stage-3 waves take two tasks each, their loads interleaved (task, task + wg3 waves)
   uint32_t s3_xcd;         // stage-3 task order by XCD: the workgroups sharing an XCD take one contiguous task range
+  uint32_t s1_xcd;         // stage-1 tile order by XCD (the same for the ranking workgroups)
   uint32_t debug;         // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
                            // stores, 2 no CRC lookups, 4 no payload loads, 8 no CRC tables,
                            // 16 skip stages 1-2, 32 no leader / mask / totals gathers in stage 3

@@ -2073,13 +2073,26 @@ __device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
 #define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
+// The rank of block b among the blocks [b0, b0 + n) (b inside it) when the blocks that share an XCD
+// (b and b + 8 under round-robin placement; speed only, never correctness) take one contiguous run
+// of ranks, XCD after XCD: neighbouring work items then share one L2.
+__device__ __forceinline__ u32 xcd_rank(u32 b0, u32 n, u32 b) {
+  const auto below = [](u32 m, u32 y) { return m > y ? (m - y + 7u) >> 3 : 0u; };  // k < m, k % 8 == y
+  const u32 x = b & 7u;
+  u32 r = below(b, x) - below(b0, x);
+  for (u32 y = 0; y < x; ++y) r += below(b0 + n, y) - below(b0, y);
+  return r;
+}
 // Stage 1 of the launch's group, tile by tile: a static share (tiles wg, wg + wg1, ...) or, with
 // RMQ_STEAL, tiles taken from the group's counter (s1.nbig[1]) by the dedicated stage-1 workgroups
 // and by stage-3 workgroups that ran out of tasks, so ranking starts as soon as stage 3 frees a
 // slot instead of when the dispatcher reaches the stage-1 workgroups.
 __device__ __forceinline__ void stage1_tiles(const PipeArgs& A, char* smem, u32 wg, bool take) {
   __shared__ u32 s_t;
-  for (u32 t = wg;;) {
+  // (RMQ_S1_XCD: the tiles of one XCD's workgroups contiguous, so the 32 tiles whose cells share a
+  // 128-byte line of a partition's hist32 column are written through one L2)
+  const u32 t0 = !take && A.s1_xcd ? xcd_rank(A.s3_lead, A.wg1, A.s3_lead + wg) : wg;
+  for (u32 t = t0;;) {
     if (take) {
       if (threadIdx.x == 0) s_t = __hip_atomic_fetch_add(A.s1.nbig + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
@@ -2162,16 +2175,9 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   const u32 tasks = G.task0[G.nb];
   const u32 lane = threadIdx.x & 63;
   // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
-  u32 slot = wg;
-  if (A.s3_xcd) {
-    // blocks b and b + 8 share an XCD (round-robin placement, speed only): the stage-3 workgroups
-    // of one XCD take one contiguous range of slots, so records next to each other in a batch
-    // (and in their partitions' rings) are stored through one L2
-    const u32 x = wg & 7u, n = A.wg3;
-    u32 before = 0;
-    for (u32 y = 0; y < x; ++y) before += n > y ? (n - y + 7u) >> 3 : 0u;
-    slot = before + (wg >> 3);
-  }
+  // (RMQ_S3_XCD: the stage-3 workgroups of one XCD take one contiguous range of slots, so records
+  // next to each other in a batch, and in their partitions' rings, are stored through one L2)
+  const u32 slot = A.s3_xcd ? xcd_rank(0, A.wg3, wg) : wg;
   u32 task = __builtin_amdgcn_readfirstlane(slot * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);
   if (!XR && A.s3_pair) {
