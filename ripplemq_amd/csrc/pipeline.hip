@@ -156,6 +156,17 @@ __device__ __forceinline__ u64 readlane64(u64 v, u32 l) {
 }
 __device__ __forceinline__ u32 readlane32(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
 
+// The rank of block b among the blocks [b0, b0 + n) (b inside it) when the blocks that share an XCD
+// (b and b + 8 under round-robin placement; speed only, never correctness) take one contiguous run
+// of ranks, XCD after XCD: neighbouring work items then share one L2.
+__device__ __forceinline__ u32 xcd_rank(u32 b0, u32 n, u32 b) {
+  const auto below = [](u32 m, u32 y) { return m > y ? (m - y + 7u) >> 3 : 0u; };  // k < m, k % 8 == y
+  const u32 x = b & 7u;
+  u32 r = below(b, x) - below(b0, x);
+  for (u32 y = 0; y < x; ++y) r += below(b0 + n, y) - below(b0, y);
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------
 // Stage 1: rank one tile
 // ------------------------------------------------------------------------------------------
@@ -2073,16 +2084,6 @@ __device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
 #define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
-// The rank of block b among the blocks [b0, b0 + n) (b inside it) when the blocks that share an XCD
-// (b and b + 8 under round-robin placement; speed only, never correctness) take one contiguous run
-// of ranks, XCD after XCD: neighbouring work items then share one L2.
-__device__ __forceinline__ u32 xcd_rank(u32 b0, u32 n, u32 b) {
-  const auto below = [](u32 m, u32 y) { return m > y ? (m - y + 7u) >> 3 : 0u; };  // k < m, k % 8 == y
-  const u32 x = b & 7u;
-  u32 r = below(b, x) - below(b0, x);
-  for (u32 y = 0; y < x; ++y) r += below(b0 + n, y) - below(b0, y);
-  return r;
-}
 // Stage 1 of the launch's group, tile by tile: a static share (tiles wg, wg + wg1, ...) or, with
 // RMQ_STEAL, tiles taken from the group's counter (s1.nbig[1]) by the dedicated stage-1 workgroups
 // and by stage-3 workgroups that ran out of tasks, so ranking starts as soon as stage 3 frees a
