@@ -1635,10 +1635,23 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
   // RMQ_FETCH_COMMIT: known flags only, one committing request per (partition, consumer)
   bool any = false;
   if (!rows_dev) {  // (device rows: never read here; their flags are ignored)
-    for (uint32_t r = 0; r < n; ++r) {
-      if (reqs[r].flags & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
-      any |= (reqs[r].flags & RMQ_FETCH_COMMIT) != 0;
+    // the OR of every row's flags word (the high half of its second 8-byte word), four rows per
+    // step with no early exit: 16,384 rows in a few us instead of a branch per row
+    static_assert(sizeof(rmq_fetch_req) == 16 && offsetof(rmq_fetch_req, flags) == 12, "request rows are four words");
+    typedef uint64_t __attribute__((__may_alias__)) u64a;
+    const u64a* w = reinterpret_cast<const u64a*>(reqs);
+    uint64_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    uint32_t r = 0;
+    for (; r + 4 <= n; r += 4) {
+      a0 |= w[2 * r + 1];
+      a1 |= w[2 * r + 3];
+      a2 |= w[2 * r + 5];
+      a3 |= w[2 * r + 7];
     }
+    for (; r < n; ++r) a0 |= w[2 * r + 1];
+    const uint32_t fl = (uint32_t)((a0 | a1 | a2 | a3) >> 32);
+    if (fl & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
+    any = (fl & RMQ_FETCH_COMMIT) != 0;
     if (any) {
       const size_t slots = (size_t)e->cfg.num_partitions * e->cfg.max_consumers;
       if (e->fetch_stamp.size() != slots) {

@@ -6,6 +6,8 @@ Thin host glue for tests, tools and bench.py: every call goes straight to
 from __future__ import annotations
 
 import ctypes as C
+import os
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -27,6 +29,29 @@ def _check(rc: int, what: str) -> int:
 
 def _ptr(a: np.ndarray | None) -> int | None:
     return None if a is None else a.ctypes.data
+
+
+_PTRS: dict = {}  # id(array) -> (weak reference, data address): arrays a caller reuses call after call
+_PTR_CACHE = os.environ.get("RMQ_PY_PTR_CACHE", "1") != "0"  # (A/B of the cache)
+
+
+def _ptr_reused(a: np.ndarray) -> int:
+    """_ptr of an array passed again and again (a fetch's request and result rows, views of
+    page-locked memory from fetch_rows): numpy's .ctypes.data costs ~1.5 us a call, a checked cache
+    entry ~0.5 us."""
+    if a.base is None or not _PTR_CACHE:  # (an array owning its data can be resized in place: not cached)
+        return a.ctypes.data
+    e = _PTRS.get(id(a))
+    if e is not None and e[0]() is a:
+        return e[1]
+    if len(_PTRS) > 256:
+        _PTRS.clear()
+    p = a.ctypes.data
+    try:
+        _PTRS[id(a)] = (weakref.ref(a), p)
+    except TypeError:  # (an object without weak references: no cache)
+        pass
+    return p
 
 
 FETCH_RES_DTYPE = np.dtype([
@@ -402,7 +427,7 @@ class Engine:
             res = np.zeros(n, FETCH_RES_DTYPE)
         used = C.c_uint64()
         mem = A.RMQ_MEM_DEVICE | (A.RMQ_FETCH_PINNED_ROWS if pinned_rows else 0)
-        rc = self.lib.rmq_fetch(self.h, _ptr(req), n, mem, d_out, out_cap, _ptr(res), C.byref(used))
+        rc = self.lib.rmq_fetch(self.h, _ptr_reused(req), n, mem, d_out, out_cap, _ptr_reused(res), C.byref(used))
         if rc not in (A.RMQ_OK, A.RMQ_ENOSPC):
             raise EngineError(rc, "rmq_fetch")
         return rc, res, int(used.value)
@@ -437,7 +462,7 @@ class Engine:
         if pinned_rows:
             mem |= A.RMQ_FETCH_PINNED_ROWS
         t = C.c_uint64()
-        _check(self.lib.rmq_fetch_async(self.h, _ptr(req), n, mem, ptr, out_cap, _ptr(res), C.byref(t)),
+        _check(self.lib.rmq_fetch_async(self.h, _ptr_reused(req), n, mem, ptr, out_cap, _ptr_reused(res), C.byref(t)),
                "rmq_fetch_async")
         tk = FetchTicket(t.value, req, res, out)
         self._fetching[t.value] = tk

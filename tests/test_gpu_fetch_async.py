@@ -151,6 +151,19 @@ def test_fetch_commit_matches_oracle(oracle_mod):
             dev.fetch(np.zeros(2, np.uint32), np.zeros(2, np.uint32), np.full(2, 5, np.uint32), out_cap=1 << 16,
                       commit=True)
         assert ei.value.status == A.RMQ_EINVAL
+        # an unknown flag bit in any row (first, middle, the last of a count that is not a multiple of
+        # four): the call is refused whole, nothing committed
+        table = dev.consumer_table().copy()
+        d_out = dev.device_alloc(1 << 16)
+        for n, at, bit in ((7, 6, 2), (9, 0, 1 << 31), (16, 9, 4), (1, 0, 8)):
+            req = np.zeros((n, 4), np.uint32)
+            req[:, 0], req[:, 2], req[:, 3] = np.arange(n) % P, 5, A.RMQ_FETCH_COMMIT
+            req[at, 3] |= bit
+            with pytest.raises(EngineError) as ei:
+                dev.fetch_device(None, None, None, d_out, 1 << 16, req=req)
+            assert ei.value.status == A.RMQ_EINVAL, (n, at, bit)
+        assert np.array_equal(dev.consumer_table(), table)
+        dev.device_free(d_out)
 
 
 def _cache_script(eng, P, C, spec, moves):
