@@ -293,11 +293,14 @@ def test_pipelined_groups(oracle_mod, group):
         assert dev.state(5)["log_end_offset"] == 0
 
 
-@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"}])
+@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"},
+                                 {"RMQ_S3_XCD": "0", "RMQ_S1_XCD": "1"}, {"RMQ_S1_XCD": "1", "RMQ_S1_WGS": "37"}])
 def test_pipelined_dispatch_modes(oracle_mod, monkeypatch, env):
     # the non-default dispatch modes (read at rmq_create): resident task waves looping over the
-    # group's tasks, stage-3 workgroups dispatched after the other roles, and few large-record
-    # workgroups (each wave then takes many records of the list)
+    # group's tasks, stage-3 workgroups dispatched after the other roles, few large-record
+    # workgroups (each wave then takes many records of the list), stage-3 tasks in block order
+    # and stage-1 tiles in XCD order (also with fewer stage-1 workgroups than tiles, each then
+    # ranking several)
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     cfg, dev, ora = pair(oracle_mod, num_partitions=4096, replication_factor=3, segment_bytes=1 << 24,
