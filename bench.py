@@ -279,7 +279,7 @@ def mixed_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, consumers:
     device-resident batches go to the pipeline, and every (partition, consumer) reads max = 10 and
     commits what it read (ConsumerClientImpl.java:61-117) through rmq_fetch_async with
     RMQ_FETCH_COMMIT: the read-then-commit of each consumer happens on the device, so the next fetch,
-    ordered after it on the fetch stream, reads on from there and four fetches can be in flight
+    ordered after it on the pipeline stream, reads on from there and four fetches can be in flight
     without a host round trip between them. Fetches are polled without waiting; every fetch runs
     between two pipeline launches (the next launch waits for it). The broker bounds its own
     run-ahead to eight launch groups (rmq_poll_commit), so a fetch returns within about eight
@@ -463,7 +463,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
     (partition, consumer) commits an offset lagging the high watermark by U[0, retained records]
     (config D's lagging consumers, bounded by what retention keeps), then one rmq_fetch of all
     P x consumers requests into a device buffer, at max = 10 (ConsumerClientImpl.java:21) and
-    max = 1024. Timed with HIP events around the fetch kernels on the engine's fetch stream.
+    max = 1024. Timed with HIP events around the fetch kernels on the pipeline stream they run on.
     B_fetch = 2 (16 + L) per returned record (read log, write output) + 8 ceil(log2(index entries))
     per request."""
     P = spec.partitions
@@ -586,7 +586,7 @@ def fetch_leg(eng, spec: StreamSpec, rounds: int, consumers: int = 4) -> dict:
                                         "kernels": "rmq::fetch_resolve (two requests per wave) + fetch_gather (placement fused)",
                                         "mean_us_per_fetch": t_reg / rounds * 1e6,
                                         "timing": f"per fetch: its kernels run {REPLAY}x back to back between two "
-                                                  "HIP events on the fetch stream, divided by the runs",
+                                                  "HIP events on the pipeline stream, divided by the runs",
                                         "kernel_spans_us_summed": t_kern / rounds * 1e6}}
     out["loop10"] = consumer_loop(eng, spec, pp, cc, hw, lo, g, rounds * 4)
     return out

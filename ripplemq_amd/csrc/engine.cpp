@@ -1516,7 +1516,7 @@ int fetch_alloc(void** p, size_t bytes) {
   return RMQ_OK;
 }
 
-int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage, hipStream_t e_fetch_s) {
+int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage, hipStream_t s) {
   if (n > f.cap) {
     void* ds[] = {f.d_req, f.d_res, f.d_aux, f.d_cpre, f.d_csum};
     for (void* p : ds)
@@ -1535,7 +1535,7 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage, hip
     if (!rc) rc = fetch_alloc((void**)&f.d_csum, 2ull * lines * kCsumStride * 8);
     if (rc) return rc;
     // both halves start zeroed (stream-ordered before the slot's first fetch)
-    HIP_TRY(hipMemsetAsync(f.d_csum, 0, 2ull * lines * kCsumStride * 8, e_fetch_s));
+    HIP_TRY(hipMemsetAsync(f.d_csum, 0, 2ull * lines * kCsumStride * 8, s));
     f.csum_lines = lines;
     f.csum_par = 0;
     HIP_TRY(hipHostMalloc((void**)&f.h_req, (size_t)cap * 16, 0));

@@ -21,9 +21,10 @@
 //          (Round 2 placed with a single 1024-thread workgroup between the two: 12.6 us of the
 //          max = 10 fetch of 16,384 requests with the rest of the GPU idle.)
 //
-// The kernels (resolve, gather; the chunk sums a slot's previous gather cleared) run on the engine's fetch stream, after the last pipeline launch the host had
-// issued and before the next one (engine.cpp orders the two streams with events), so the committed
-// state they read is stable and the append pipeline is never flushed for a fetch.
+// The kernels (resolve, gather; the chunk sums a slot's previous gather cleared) run on the
+// pipeline stream itself, after the last pipeline launch the host had issued and before the next
+// one, so the committed state they read is stable and the append pipeline is never flushed for a
+// fetch.
 #include <hip/hip_ext.h>
 
 #include "device_common.hpp"

@@ -353,7 +353,7 @@ def test_pinned_rows_match_sync():
                 a, b = int(res["out_pos"][r]), int(res["out_pos"][r] + res["bytes"][r])
                 assert np.array_equal(got[a:b], wbuf[a:b]), (k, r)
         assert pending[2][1] == A.RMQ_ENOSPC
-        # the synchronous call with page-locked rows (its copies on the fetch stream itself)
+        # the synchronous call with page-locked rows (read and written in place by its kernels)
         for k, cap in ((0, 8 << 20), (1, 1 << 16)):
             n = P * C
             req, res = dev.fetch_rows(n)
