@@ -35,7 +35,8 @@ namespace rmq {
 constexpr int kOk = 0, kNotLeader = -1, kNoPart = -2, kInval = -3, kNoSpc = -4, kOffset = -6;
 constexpr u32 kFW = 4;  // waves per workgroup (gather)
 #ifndef RMQ_RESOLVE_WAVES
-#define RMQ_RESOLVE_WAVES 4
+#define RMQ_RESOLVE_WAVES 8  // round 5 (rows read by one load per workgroup): 8 vs 4 waves, max = 10
+                             // 24.8-25.3 vs 25.1-25.5 us, consumer loop 36.0 vs 36.9-37.6 us; 16: max = 10 27 us
 #endif
 constexpr u32 kRW = RMQ_RESOLVE_WAVES;  // waves per resolve workgroup
 
