@@ -179,7 +179,9 @@ typedef struct rmq_partition_state {
   uint64_t last_log_term;      /* Raft's lastLogTerm: the newest term whose leader-start entry this
                                   replica's log holds (its own term once it leads; on a follower the
                                   term of the last round entry it accepted that reached its leader's
-                                  term start, 0 = unknown older); compared by rmq_vote */
+                                  term start; 0 = unknown, after a catch-up that ended below its
+                                  leader's term start: rmq_vote then compares against an upper bound,
+                                  the leader's term - 1, while a candidacy claims 0) */
   uint64_t voted_term;         /* the term of this replica's last vote (raft_meta votedFor's term) */
   uint32_t voted_for;          /* the rank it voted for in voted_term (RMQ_NO_VOTE: none) */
   uint32_t led;                /* 1: this replica led voted_term (rmq_become_leader succeeded in it) */
@@ -263,7 +265,11 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term);
    when this replica has not voted for another candidate in `term` and the candidate's log is at least
    as up to date, (cand_last_log_term, cand_log_end) >= (last_log_term, log_end_offset) in that order.
    *granted = 1 records the vote (voted_term = term, voted_for = candidate). A candidate votes for
-   itself through this call too, then rmq_become_leader(pidx, term) once a quorum granted. */
+   itself through this call too, then rmq_become_leader(pidx, term) once a quorum granted.
+   Without a transport the batches submitted are applied first. With one nothing is flushed (a flush
+   is collective): the call waits for what is issued only, and a replica that leads pidx with launch
+   groups still in flight answers RMQ_PENDING with nothing changed (the request is delayed: send it
+   again after the next rmq_sync). */
 int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, uint64_t cand_last_log_term,
              uint64_t cand_log_end, uint32_t* granted);
 /* Replay of a persisted vote (raft_meta): voted_term / voted_for of pidx, and the term if newer. */

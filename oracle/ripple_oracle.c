@@ -20,6 +20,7 @@
 #endif
 
 #define RO_POLY 0x82F63B78u /* CRC32C (Castagnoli), reflected */
+#define RO_LTERM_BOUND (1ull << 63) /* lterm flag: the last entry's term is unknown, at most the value */
 
 /* ------------------------------------------------------------------------------------------ */
 /* CRC32C                                                                                      */
@@ -868,7 +869,7 @@ int ro_get_partition_state(ro_engine* e, uint32_t p, rmq_partition_state* o) {
   o->is_leader = s->is_leader;
   o->segment_bytes = s->seg;
   o->leader_commit = s->is_leader ? s->commit : s->lc;
-  o->last_log_term = s->lterm;
+  o->last_log_term = (s->lterm & RO_LTERM_BOUND) ? 0 : s->lterm;
   o->voted_term = s->vterm;
   o->voted_for = s->vfor;
   o->led = s->led;
@@ -1443,7 +1444,10 @@ int ro_ingest(ro_engine* e, uint32_t src, const uint8_t* region, uint64_t size, 
       if (term > s->term) s->term = term;
       uint64_t ltm;
       memcpy(&ltm, d + 40, 8);
-      s->lterm = ltm;   /* the entry's last entry term (0: older, unknown) */
+      /* the entry's last entry term; 0: older than the leader's term start, so the log ends in a
+         term below the leader's: kept as that upper bound (the vote compares against it), reported
+         as 0 (a candidate claims no more than it knows) */
+      s->lterm = ltm ? ltm : RO_LTERM_BOUND | (term ? term - 1 : 0);
       s->mterm = term;  /* the log now matches the term-`term` leader's through the entry's end */
       if (rebase) {
         if (rebase_log(e, s, leo, used)) {
@@ -1612,7 +1616,8 @@ int ro_vote(ro_engine* e, uint32_t p, uint64_t term, uint32_t cand, uint64_t can
       if (s->commit > s->lc) s->lc = s->commit;
     }
   }
-  const int up = cand_lterm > s->lterm || (cand_lterm == s->lterm && cand_leo >= s->leo);
+  const uint64_t lt = s->lterm & ~RO_LTERM_BOUND; /* unknown: its upper bound (a stricter vote) */
+  const int up = cand_lterm > lt || (cand_lterm == lt && cand_leo >= s->leo);
   const int free_vote = s->vterm != term || (!s->led && s->vfor == cand);
   if (up && free_vote) {
     s->vterm = term;

@@ -92,6 +92,30 @@ void launch_row_quorum_all(const DevState& st, hipStream_t s) {
   hipLaunchKernelGGL(row_quorum_all_kernel, grid_for(st.P, 256), dim3(256), 0, s, st);
 }
 
+// Retention of the last applied group for the partitions whose replay its own launch stopped early
+// (rlate[p]: the group added more than a ring less an interval to p, so the index entries retention
+// needed were being written by that launch; pipeline.hip partition_threads): issued by the host
+// before a fetch or a state read that follows that launch, so they see the log start the oracle has
+// after the group's last batch (FORMAT.md §4) rather than the next launch's stage 4 doing it. The
+// flag is cleared, so that stage 4 finds nothing left.
+__global__ void late_retention_kernel(LateArgs a) {
+  const DevState& st = a.st;
+  const u32 p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= st.P || !a.rlate[p] || !st.is_leader[p]) return;
+  u64 bc[kMaxGroup];
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j) bc[j] = j < a.nb ? a.bcum[(u64)j * st.P + p] : 0ull;
+  const RingRef rg = ring_ref(st, p);
+  u64 soff = st.start_off[p], spos = st.start_pos[p];
+  retain_batches(st, rg, bc, a.nb, false, st.used[p], a.totals[p], ~0ull, soff, spos);
+  st.start_off[p] = soff;
+  st.start_pos[p] = spos;
+  a.rlate[p] = 0u;
+}
+void launch_late_retention(const LateArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(late_retention_kernel, grid_for(a.st.P, 256), dim3(256), 0, s, a);
+}
+
 void launch_commit_all(const DevState& st, hipStream_t s) {
   hipLaunchKernelGGL(commit_all_kernel, grid_for(st.P, 256), dim3(256), 0, s, st);
 }

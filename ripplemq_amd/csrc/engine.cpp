@@ -240,6 +240,11 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
       a.s3_pair = 1;
       a.wg3 = std::max<uint32_t>(1u, (s3->tasks + 2 * wpb - 1) / (2 * wpb));
     }
+    if (e->s3_roles && !a.outidx && !e->split) {  // loader / storer waves: a run of tasks per workgroup
+      a.s3_roles = 1;
+      a.s3_pair = 0;
+      a.wg3 = std::max<uint32_t>(1u, std::min<uint32_t>(s3->tasks, e->s3_roles * e->cu_count));
+    }
     a.wgb = e->big_wgs ? e->big_wgs : 32u * e->cu_count / (PT / 64u);  // 32 large-record waves per CU
     // dispatch order: s3_lead stage-3 workgroups, then ranking, scans and partition threads, then
     // the rest of stage 3, so the ranking/scan chains start before stage 3's last workgroups and
@@ -394,9 +399,27 @@ int drain(rmq_engine* e) {
   return RMQ_OK;
 }
 
+// The last applied group's retention, where its own launch stopped early (late_retention_kernel),
+// before a fetch or a state read ordered after that launch; once per applied group.
+int late_retention(rmq_engine* e) {
+  if (!e->has3 || e->late_done == e->g3_seq) return RMQ_OK;
+  LateArgs a{};
+  a.st = e->st;
+  a.bcum = e->scratch[e->g3.set].bcum;
+  a.totals = e->scratch[e->g3.set].totals;
+  a.rlate = e->d_rlate;
+  a.nb = e->g3.nb;
+  launch_late_retention(a, e->main_s);
+  HIP_TRY(hipGetLastError());
+  e->late_done = e->g3_seq;
+  return RMQ_OK;
+}
+
 // Wait for everything issued on the pipeline stream, without flushing batches that are still
 // forming or in the pipeline's earlier stages (reads of committed state, consumer commits).
 int quiesce(rmq_engine* e) {
+  int rc0 = late_retention(e);
+  if (rc0) return rc0;
   int rc = stream_wait(e->main_s);
   if (rc) return rc;
   collect_done(e);
@@ -645,6 +668,7 @@ const char* rmq_strerror(int s) {
     case RMQ_EOFFSET: return "offset out of range";
     case RMQ_ENOMEM: return "out of memory";
     case RMQ_ESTALE: return "replica lags the committed log";
+    case RMQ_ETERM: return "term already led or voted for another candidate";
     default: return "unknown status";
   }
 }
@@ -692,6 +716,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_STAMPS_AT")) e->stamps_at = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_PAIR")) e->s3_pair = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S3_ROLES")) e->s3_roles = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_XCD")) e->s3_xcd = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S1_XCD")) e->s1_xcd = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
@@ -1005,6 +1030,17 @@ int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   return rc;
 }
 
+// Before a vote reads a partition's term and log: without a transport every batch submitted is
+// applied first (drain); with one, a flush would be collective (rmq_sync), so only what is issued is
+// waited for: the pipeline stream and the rounds' ingest on the exchange stream.
+static int vote_settle(rmq_engine* e) {
+  if (!e->repl) return drain(e);
+  int rc = quiesce(e);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->repl->xchg_s));
+  return RMQ_OK;
+}
+
 int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, uint64_t cand_last_log_term,
              uint64_t cand_log_end, uint32_t* granted) {
   if (!e || !granted) return RMQ_EINVAL;
@@ -1012,12 +1048,16 @@ int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, ui
   std::lock_guard<std::mutex> g(e->mu);
   if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = vote_settle(e);
   if (rc) return rc;
+  // with a transport nothing is flushed (a flush is collective): a leader of pidx whose groups in
+  // flight may still add its records answers RMQ_PENDING and changes nothing (a delayed RequestVote)
+  if (e->repl && e->is_leader[pidx] && (e->forming.nb || e->has1 || e->has2)) return RMQ_PENDING;
   uint64_t cur = 0, lterm = 0, leo = 0;
   HIP_TRY(hipMemcpy(&cur, e->st.term + pidx, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&lterm, e->st.lterm + pidx, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&leo, e->st.leo + pidx, 8, hipMemcpyDeviceToHost));
+  lterm &= ~kLtermBound;  // an unknown last log term: its upper bound (a stricter vote)
   if (term < cur) return RMQ_OK;  // a candidate of an older term
   if (term > cur) {  // Raft: a newer term is adopted; a leader steps down
     e->term[pidx] = term;
@@ -1050,7 +1090,7 @@ int rmq_set_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t voted_for
   std::lock_guard<std::mutex> g(e->mu);
   if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
-  int rc = drain(e);
+  int rc = vote_settle(e);
   if (rc) return rc;
   uint64_t cur = 0;
   HIP_TRY(hipMemcpy(&cur, e->st.term + pidx, 8, hipMemcpyDeviceToHost));
@@ -1719,6 +1759,8 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     // under it.
     std::lock_guard<std::mutex> g(e->mu);
     if (dma_in) HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_in, 0));
+    rc = late_retention(e);  // (the log starts the fetch reads: every batch applied so far retained)
+    if (rc) return rc;
     FetchArgs a{};
     a.st = e->st;
     a.req = static_cast<const uint32_t*>(d_rq);
@@ -1847,6 +1889,7 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   if (o->is_leader) o->leader_commit = o->commit;
   else HIP_TRY(hipMemcpy(&o->leader_commit, s.lcommit + p, 8, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(&o->last_log_term, s.lterm + p, 8, hipMemcpyDeviceToHost));
+  if (o->last_log_term & kLtermBound) o->last_log_term = 0;  // unknown: a candidate claims none
   HIP_TRY(hipMemcpy(&o->heard_round, s.heard + p, 8, hipMemcpyDeviceToHost));
   o->voted_term = e->vterm[p];
   o->voted_for = e->vfor[p];
@@ -1905,7 +1948,7 @@ int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_part
     x.is_leader = e->is_leader[p];
     x.segment_bytes = 1ull << (e->ring[p] & 63ull);
     x.leader_commit = x.is_leader ? x.commit : v[8ull * n + i];
-    x.last_log_term = v[9ull * n + i];
+    x.last_log_term = (v[9ull * n + i] & kLtermBound) ? 0ull : v[9ull * n + i];
     x.heard_round = v[10ull * n + i];
     x.voted_term = e->vterm[p];
     x.voted_for = e->vfor[p];

@@ -433,6 +433,8 @@ struct rmq_engine {
   uint64_t* state_stage = nullptr;  // page-locked staging of rmq_get_partition_states
   size_t state_stage_words = 0;
   uint32_t s3_pair = 0;         // RMQ_S3_PAIR=1: stage-3 waves take two tasks each (single-GPU kernel)
+  uint64_t late_done = 0;       // the applied group (by launch) whose late retention ran (late_retention)
+  uint32_t s3_roles = 0;        // RMQ_S3_ROLES=k: stage 3 in loader / storer waves, k workgroups per CU (single-GPU kernel)
   uint32_t s3_xcd = 1;          // RMQ_S3_XCD (default 1): stage-3 tasks in contiguous ranges per XCD
                                 //   (blockIdx % 8); round 5: 5.51-5.58 vs 5.43-5.51 G, 3 pairs, r05X8
   uint32_t s1_xcd = 0;          // RMQ_S1_XCD=1: stage-1 tiles in contiguous ranges per XCD

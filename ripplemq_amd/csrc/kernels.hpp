@@ -154,7 +154,7 @@ struct DevState {
   // consumer-offset rows on a quorum (rmq_commit_consumer_offset tickets, FORMAT.md §8)
   // leader election: Raft's lastLogTerm, the term this log was last verified in
   // against its leader's, and the round stamp of the last entry or notice heard from the leader
-  uint64_t* lterm;       // [P]
+  uint64_t* lterm;       // [P] last log term; kLtermBound | t: unknown, at most t (a partial catch-up)
   uint64_t* mterm;       // [P]
   uint64_t* heard;       // [P]
   uint64_t* cver;        // [P] leader: version of the partition's row (one per commit call touching it)
@@ -171,6 +171,12 @@ struct DevState {
 // Where partition p's ring and index live (FORMAT.md §2, §5). A ring of S bytes sits at a multiple
 // of S inside each replica region; its index ring holds icap_mul * S / I entries at a proportional
 // offset of the index pool, so rings and index rings never overlap.
+// DevState::lterm of a follower whose last entry's term is unknown (a partial catch-up that ended below
+// its leader's term start, FORMAT.md §9 v5): the flag and an upper bound, the leader's term - 1. A vote
+// compares against the bound (stricter: only liveness can suffer), a candidate claims 0 (never more
+// than it has).
+constexpr uint64_t kLtermBound = 1ull << 63;
+
 struct RingRef {
   uint64_t base;   // byte offset of the ring inside a replica region
   uint64_t seg;    // ring bytes (power of two)
@@ -260,6 +266,7 @@ struct PipeArgs {
   uint32_t gt;             // tiles per hist / excl column (group tile capacity)
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
   uint32_t s3_pair;        // stage-3 waves take two tasks each, their loads interleaved (task, task + wg3 waves)
+  uint32_t s3_roles;       // stage 3 in loader / storer waves (RMQ_S3_ROLES): each workgroup a run of tasks
   uint32_t s3_xcd;         // stage-3 task order by XCD: the workgroups sharing an XCD take one contiguous task range
   uint32_t s1_xcd;         // stage-1 tile order by XCD (the same for the ranking workgroups)
   uint32_t debug;         // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
@@ -326,6 +333,16 @@ struct ConsumerCommitArgs {  // one item per (partition, consumer): the host res
   const uint64_t* ver;     // the partition's new row version (the same for every item of a partition)
   uint32_t n;
   uint32_t pad;
+};
+
+// The last applied group's retention for partitions whose replay its launch stopped early
+// (late_retention_kernel): the group's batch aggregates and totals, and the per-partition flags.
+struct LateArgs {
+  DevState st;
+  const uint64_t* bcum;  // [kMaxGroup][P] the group's aggregate through each batch
+  const uint64_t* totals;
+  uint32_t* rlate;
+  uint32_t nb;
 };
 
 struct AckArgs {
@@ -411,6 +428,7 @@ void launch_pipeline(const PipeArgs& a, hipStream_t s, hipEvent_t start = nullpt
 uint32_t pipeline_wgs_per_cu(uint32_t threads);  // resident workgroups per CU of that size
 void launch_commit_all(const DevState& st, hipStream_t s);
 void launch_ack(const AckArgs& a, hipStream_t s);
+void launch_late_retention(const LateArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
 void preload_fetch_kernels();

@@ -5,6 +5,9 @@
 
 namespace rmq {
 
+constexpr u64 kLow40 = (1ull << 40) - 1ull;  // bytes/16 field of a {count << 40 | bytes/16} aggregate
+
+
 // Raft quorum commit (jraft BallotBox semantics; restated from the Raft paper since
 // jraft-core 1.3.15 is not in the container): N = k-th largest matchIndex of the partition's
 // replica row, k = RF/2 + 1 (the median for odd RF), held in registers and ordered by a
@@ -124,6 +127,64 @@ __device__ __forceinline__ void learn_commit(const DevState& st, u32 p, u64 lc, 
   c = c < leo ? c : leo;
   st.commit[p] = c;
   st.hw[p] = c;
+}
+
+// Retention after each batch of a group (FORMAT.md §4), batch by batch: after batch j the start
+// moves to index entry ceil((fin_j - seg) / I) when fin_j - start > seg, fin_j = the log end after
+// batch j: used0 + 16 (bc_j bytes) when used0 is the log end before the group (pre), else
+// used0 - 16 (tot - bc_j bytes) (used0 after it); bc = the group's aggregates through each batch
+// (a batch that appended nothing of p cannot move it). The start only grows, so a batch with
+// fin_j - start0 <= seg never moves it: the positions of the others' entries are loaded together,
+// the batches replayed in order in registers, and the offset of the last entry taken loaded after
+// (the same index entry: one cache line). An entry at or past position `lim` may be written by
+// the running launch: it is not read, the replay stops at its batch and the function returns
+// false (the next launch's stage 4 finishes the group; replaying applied batches moves nothing).
+__device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef& rg, const u64 (&bc)[kMaxGroup], u32 nb,
+                                               bool pre, u64 used0, u64 tot, u64 lim, u64& soff, u64& spos) {
+  const u32 ilog = st.interval_log2;
+  u64 ep[kMaxGroup];
+  u32 cand = 0, late = 0;  // bit j: batch j may move the start / its entry is not readable yet
+  u64 prev = 0;
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j) {
+    ep[j] = 0ull;
+    const bool app = j < nb && (bc[j] >> 40) != (prev >> 40);
+    const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
+    if (app && fin - spos > rg.seg) {
+      const u64 ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
+      cand |= 1u << j;
+      if ((ms << ilog) > lim) late |= 1u << j;
+      else ep[j] = st.index[(rg.ibase + ms % rg.icap) * 2 + 1];
+    }
+    prev = j < nb ? bc[j] : prev;
+  }
+  bool done = true;
+  int last = -1;
+  u64 sp = spos;
+#pragma unroll
+  for (u32 j = 0; j < kMaxGroup; ++j) {
+    const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
+    if (done && ((cand >> j) & 1u) && fin - sp > rg.seg) {
+      if ((late >> j) & 1u) {
+        done = false;
+      } else {
+        sp = ep[j];
+        last = (int)j;
+      }
+    }
+  }
+  if (last >= 0) {
+    u64 ms = 0;
+#pragma unroll
+    for (u32 j = 0; j < kMaxGroup; ++j)
+      if ((int)j == last) {
+        const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
+        ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
+      }
+    soff = st.index[(rg.ibase + ms % rg.icap) * 2];
+    spos = sp;
+  }
+  return done;
 }
 
 }  // namespace rmq

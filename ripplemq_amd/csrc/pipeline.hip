@@ -67,7 +67,6 @@ constexpr u32 kRankMask = (1u << kFlagShift) - 1u;
 // stage-1 flags (leadership is per partition, so it cannot change another partition's ranks:
 // stage 3 checks it)
 constexpr u32 kFlNoPart = 1u, kFlInvalid = 4u, kFlJunk = 7u;
-constexpr u64 kLow40 = (1ull << 40) - 1ull;
 constexpr u64 kOne40 = 1ull << 40;
 constexpr u64 kCnt23 = (1ull << 23) - 1ull;  // count field of an excl value (bits 40..62)
 constexpr u64 kExclNoSpace = 1ull << 63;     // excl flag: the cell's (batch, partition) is rejected
@@ -1876,64 +1875,6 @@ __device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Sme
   }
 }
 
-// Retention after each batch of a group (FORMAT.md §4), batch by batch: after batch j the start
-// moves to index entry ceil((fin_j - seg) / I) when fin_j - start > seg, fin_j = the log end after
-// batch j: used0 + 16 (bc_j bytes) when used0 is the log end before the group (pre), else
-// used0 - 16 (tot - bc_j bytes) (used0 after it); bc = the group's aggregates through each batch
-// (a batch that appended nothing of p cannot move it). The start only grows, so a batch with
-// fin_j - start0 <= seg never moves it: the positions of the others' entries are loaded together,
-// the batches replayed in order in registers, and the offset of the last entry taken loaded after
-// (the same index entry: one cache line). An entry at or past position `lim` may be written by
-// the running launch: it is not read, the replay stops at its batch and the function returns
-// false (the next launch's stage 4 finishes the group; replaying applied batches moves nothing).
-__device__ __forceinline__ bool retain_batches(const DevState& st, const RingRef& rg, const u64 (&bc)[kMaxGroup], u32 nb,
-                                               bool pre, u64 used0, u64 tot, u64 lim, u64& soff, u64& spos) {
-  const u32 ilog = st.interval_log2;
-  u64 ep[kMaxGroup];
-  u32 cand = 0, late = 0;  // bit j: batch j may move the start / its entry is not readable yet
-  u64 prev = 0;
-#pragma unroll
-  for (u32 j = 0; j < kMaxGroup; ++j) {
-    ep[j] = 0ull;
-    const bool app = j < nb && (bc[j] >> 40) != (prev >> 40);
-    const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
-    if (app && fin - spos > rg.seg) {
-      const u64 ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
-      cand |= 1u << j;
-      if ((ms << ilog) > lim) late |= 1u << j;
-      else ep[j] = st.index[(rg.ibase + ms % rg.icap) * 2 + 1];
-    }
-    prev = j < nb ? bc[j] : prev;
-  }
-  bool done = true;
-  int last = -1;
-  u64 sp = spos;
-#pragma unroll
-  for (u32 j = 0; j < kMaxGroup; ++j) {
-    const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
-    if (done && ((cand >> j) & 1u) && fin - sp > rg.seg) {
-      if ((late >> j) & 1u) {
-        done = false;
-      } else {
-        sp = ep[j];
-        last = (int)j;
-      }
-    }
-  }
-  if (last >= 0) {
-    u64 ms = 0;
-#pragma unroll
-    for (u32 j = 0; j < kMaxGroup; ++j)
-      if ((int)j == last) {
-        const u64 fin = pre ? used0 + 16ull * (bc[j] & kLow40) : used0 - 16ull * ((tot - bc[j]) & kLow40);
-        ms = (fin - rg.seg + (1ull << ilog) - 1) >> ilog;
-      }
-    soff = st.index[(rg.ibase + ms % rg.icap) * 2];
-    spos = sp;
-  }
-  return done;
-}
-
 // Thread per partition: stage 3's state advance, retention of the group it applies, and stage 4.
 // Everything these read is loaded first, in one round (speculatively: a partition this engine
 // does not lead, or one without records, discards it), so the chain is that round, the index
@@ -2081,6 +2022,288 @@ __device__ __forceinline__ void stage3_catchup(const PipeArgs& A, u32 wg) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Stage 3 in two roles (RMQ_S3_ROLES, single-GPU kernel): loader waves and a storer wave
+// ------------------------------------------------------------------------------------------
+// On gfx950 `vmcnt` counts stores as well as loads, and a wave's slot is held until its stores are
+// acknowledged (s_endpgm waits for them): a wave that loads, checksums and stores its task keeps its
+// slot through the store latency, and a wave that loops over tasks waits for the previous task's
+// stores before the next task's loads return. Here a workgroup takes a contiguous run of tasks and
+// splits the work by wave: kS3Loaders loader waves load each task's record words, partition line and
+// payload, compute the CRCs and build the task's log image in an LDS buffer, with no global stores
+// (so each loader prefetches its next task's record words while it checksums the current one, and
+// no load ever waits behind a store); the storer wave takes the images in task order and issues only
+// stores: ring pieces, out offsets, sparse-index entries and statistics. It never waits on vmcnt.
+// The hand-off is a ring of kS3Bufs LDS buffers with one sequence word each: a loader publishes task
+// i in buffer i % kS3Bufs as 2i + 1 once its image writes have completed (lgkmcnt(0)); the storer
+// reads the buffer into registers and releases it as 2i + 2. Every wait is for a smaller task index,
+// so the smallest unfinished task always progresses (no deadlock), and every wave ends when its
+// share of the run is done.
+#ifndef RMQ_S3_LOADERS
+#define RMQ_S3_LOADERS 3
+#endif
+constexpr u32 kS3Loaders = RMQ_S3_LOADERS;
+constexpr u32 kS3Storers = kPW > kS3Loaders ? kPW - kS3Loaders : 1u;
+constexpr u32 kS3Bufs = 4;
+struct Stage3RSmem {
+  u32 t8[8][256];
+  u32 z[2][4][256];
+  uint4 img[kS3Bufs][kTaskRecs][8];   // the task's records as laid out in the log (<= 128 B each)
+  uint4 info[kS3Bufs][kTaskRecs][2];  // {pos, off}, {ring descriptor, flags, payload pieces}
+  uint4 stat[kS3Bufs];                // the task's statistics
+  u32 seq[kS3Bufs];                   // 2i + 1: task i published; 2i + 2: task i taken
+};
+static_assert(sizeof(Stage3RSmem) <= kSmemBytes, "the role-split stage 3 fits the launch's LDS");
+// info flags
+constexpr u32 kRfImg = 8u;            // bits 8..11: payload pieces the storer stores from the image
+constexpr u32 kRfSt = 1u << 12;       // the storer stores the header (and the image's pieces)
+constexpr u32 kRfDead = 13u;          // bits 13..17: leading dead pieces (0 = header), clipped at 31
+constexpr u32 kRfOk = 1u << 18;       // appended: out offset = off, index entries
+constexpr u32 kRfIn = 1u << 19;       // a record of the batch: an out offset is written
+
+__device__ __forceinline__ u32 lds_seq(const u32* s) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+// Wait until the sequence word reaches v (LDS only: no vmcnt wait), then order later LDS accesses
+// after it. The wait is bounded (about a second): a broken hand-off ends in wrong results that the
+// parity tests catch, never in waves that do not finish.
+__device__ __forceinline__ void lds_wait_seq(const u32* s, u32 v) {
+  for (u32 k = 0; lds_seq(s) < v && k < (1u << 24); ++k) __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+// Every LDS write (and read) of this wave has completed, then the sequence word is set.
+__device__ __forceinline__ void lds_post_seq(u32* s, u32 v) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(s, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Loader: the task's CRCs and log image into buffer bi (stage3_finish without the stores; records of
+// 8-64 payload pieces, which do not fit the image, store their payload pieces here themselves).
+__device__ __forceinline__ void stage3_build(const PipeArgs& A, Stage3RSmem& S, const TaskPos& T, const TaskRec& R,
+                                             const TaskState& Z, bool cand, u32 bi) {
+  const PipeBatch& b = A.g3.b[T.jb];
+  const DevState& st = A.st;
+  const u32 lane = threadIdx.x & 63, j = lane & 1u, r32 = lane >> 1;
+  const u32 RF = st.RF;
+  const u32 i = task_rec(T);
+  const bool in = i < b.n;
+  const u32 L = R.L;
+  const u32 fl = R.cr.x >> kFlagShift;
+  const u32 rej = batch_rej(A, T);
+  const bool ns = (Z.lm & kNoSpace) != 0u;
+  const bool lead = (Z.lm & kLead) != 0u;
+  const u32 lm8 = Z.lm & 0xFFu;
+  const bool ok = cand && lead && !ns;
+  const u32 m = (L + 15u) >> 4;
+  const bool big = ok && m > kBigPieces;  // the large-record waves store it
+  const bool okp = ok && !big;
+  const RingRef rg = ring_ref(Z.rdesc, st.interval_log2, st.icap_mul);
+  const u64 segmask = rg.seg - 1ull;
+  const u64 pos = Z.pos;
+  uint8_t* const ring = st.logs + rg.base;
+  const u32 lmw = (A.debug & 1u) ? 0u : lm8;
+  const u32 sa = (u32)(R.src & 15u);
+  const u32 nr = okp ? (m + kPR - 1u) / kPR : 0u;
+  const bool img = __all(!okp || m <= 7u);
+  u32 acc = 0;
+  uint4 blk[kBL];
+#pragma unroll
+  for (u32 q = 0; q < kBL; ++q) blk[q] = Z.blk[q];
+  for (u32 c = 0; __any(c < nr); ++c) {
+    if (c) round_blocks(A, R, c, c < nr, blk);
+#pragma unroll
+    for (u32 q = 0; q < 4; ++q) {
+      const uint4 pb = pair_swap4(j ? blk[q] : blk[q + 1]);
+      const u32 jp = kPR * c + j + 2u * q;
+      if (c < nr && jp < m) {
+        const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
+        uint4 v = extract_piece(blk[q], pb, sa, nb);
+        uint4 vc = v;
+        if (jp == 0) vc.x ^= 0xFFFFFFFFu;
+        acc = crc_zshift(S.z[1], acc) ^ ((A.debug & 2u) ? vc.x : crc_piece16(S.t8, vc));
+        if (img) {
+          S.img[bi][r32][jp + 1] = v;
+        } else {
+          uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
+          if (jp + 1u >= Z.dead)
+            for (u32 r = 0; r < RF; ++r)
+              if ((lmw >> r) & 1u) store_log16(dst + r * st.rstride, v);
+        }
+      }
+    }
+  }
+  if (okp && m > j && ((m - 1u - j) & 1u)) acc = crc_zshift(S.z[0], acc);
+  acc ^= pair_swap(acc);
+  u32 part = 0;
+  if (okp && L) {
+    const u32 pad = 16u * m - L;
+    part = pad ? gf2_mulmod_half(j ? acc & 0xFFFFu : acc >> 16, j ? A.crc->inv_pad16[pad] : A.crc->inv_pad[pad])
+               : (j ? 0u : acc);
+  }
+  part ^= pair_swap(part);
+  if (j == 1) {
+    S.img[bi][r32][0] = okp ? make_uint4((u32)Z.off, (u32)(Z.off >> 32), L, L ? ~part : 0u) : make_uint4(0, 0, 0, 0);
+  } else {
+    const u32 f = (okp ? (lmw | ((img ? m : 0u) << kRfImg) | kRfSt) : 0u) | (min(Z.dead, 31u) << kRfDead) |
+                  (ok ? kRfOk : 0u) | (in ? kRfIn : 0u);
+    S.info[bi][r32][0] = make_uint4((u32)pos, (u32)(pos >> 32), (u32)Z.off, (u32)(Z.off >> 32));
+    S.info[bi][r32][1] = make_uint4((u32)Z.rdesc, (u32)(Z.rdesc >> 32), f, m);
+  }
+  const bool h0 = j == 0;
+  const u32 n_in = (u32)__popcll(__ballot(h0 && in));
+  const u32 n_app = (u32)__popcll(__ballot(h0 && ok));
+  const u32 n_nl = (u32)__popcll(__ballot(h0 && cand && !lead));
+  const u32 n_np = rej ? 0u : (u32)__popcll(__ballot(h0 && in && fl == kFlNoPart));
+  const u32 n_inv = (rej & kRejInvalid) ? n_in : 0u;
+  const u32 n_ns = (u32)__popcll(__ballot(h0 && cand && lead && ns));
+  if (lane == 0) S.stat[bi] = make_uint4(n_app, n_nl, n_np, n_ns | (n_inv << 16));
+}
+
+// Storer: task `task` from buffer bi (published as sequence ti): everything into registers, the
+// buffer released, then the stores.
+__device__ __forceinline__ void stage3_store(const PipeArgs& A, Stage3RSmem& S, u32 task, u32 bi, u32 ti) {
+  const PipeGroup& G = A.g3;
+  const DevState& st = A.st;
+  const u32 lane = threadIdx.x & 63;
+  const TaskPos T = task_pos(G, task);
+  const PipeBatch& b = G.b[T.jb];
+  constexpr u32 kS4 = kTaskRecs * 8u / 64u;  // (record, piece) slots per lane
+  uint4 v[kS4], i0[kS4], i1[kS4];
+#pragma unroll
+  for (u32 s4 = 0; s4 < kS4; ++s4) {
+    const u32 idx = lane + 64u * s4, rr = idx >> 3, k = idx & 7u;
+    v[s4] = S.img[bi][rr][k];
+    i0[s4] = S.info[bi][rr][0];
+    i1[s4] = S.info[bi][rr][1];
+  }
+  const u32 rr = lane & (kTaskRecs - 1u);  // lanes 0..31: record lane's out offset and index entries
+  const uint4 r0 = S.info[bi][rr][0], r1 = S.info[bi][rr][1];
+  const uint4 so = S.stat[bi];
+  lds_post_seq(&S.seq[bi], 2u * ti + 2u);
+  const u64 rstride = st.rstride;
+#pragma unroll
+  for (u32 s4 = 0; s4 < kS4; ++s4) {
+    const u32 k = (lane + 64u * s4) & 7u;
+    const u32 f = i1[s4].z;
+    if ((f & kRfSt) && k <= ((f >> kRfImg) & 0xFu) && k >= ((f >> kRfDead) & 31u)) {
+      const u64 rpos = ((u64)i0[s4].y << 32) | i0[s4].x;
+      const RingRef rg = ring_ref(((u64)i1[s4].y << 32) | i1[s4].x, st.interval_log2, st.icap_mul);
+      uint8_t* dst = st.logs + rg.base + ((rpos + 16ull * k) & (rg.seg - 1ull));
+      for (u32 r = 0; r < st.RF; ++r)
+        if ((f >> r) & 1u) store_log16(dst + r * rstride, v[s4]);
+    }
+  }
+  if (lane < kTaskRecs) {
+    const u32 f = r1.z;
+    const u64 off = ((u64)r0.w << 32) | r0.z;
+    if (f & kRfIn) b.out_offsets[T.i0 + lane] = (f & kRfOk) ? off : ~0ull;
+    if (f & kRfOk) {
+      const u32 ilog = st.interval_log2;
+      const u64 pos = ((u64)r0.y << 32) | r0.x;
+      const u64 end = pos + 16ull * (1ull + r1.w);
+      const RingRef rg = ring_ref(((u64)r1.y << 32) | r1.x, ilog, st.icap_mul);
+      for (u64 mm = (pos >> ilog) + 1; (mm << ilog) <= end; ++mm) {
+        u64* e = st.index + (rg.ibase + mm % rg.icap) * 2;
+        e[0] = off + 1;
+        e[1] = end;
+      }
+    }
+  }
+  if (lane == 0) G.stats[T.jb][task - G.task0[T.jb]] = so;
+}
+
+// The CRC tables into LDS by the loader waves: every 16-byte block loaded before any is written
+// (one load round trip instead of one per block a thread copies).
+__device__ __forceinline__ void roles_tables(const PipeArgs& A, Stage3RSmem& S) {
+  static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
+  constexpr u32 kN = (sizeof(S.t8) + sizeof(S.z)) / 16u, kT = kS3Loaders * 64u, kPer = (kN + kT - 1u) / kT;
+  const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
+  uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
+  uint4 v[kPer];
+#pragma unroll
+  for (u32 q = 0; q < kPer; ++q) v[q] = src[min(threadIdx.x + q * kT, kN - 1u)];  // (unconditional: registers)
+#pragma unroll
+  for (u32 q = 0; q < kPer; ++q)
+    if (threadIdx.x + q * kT < kN) dst[threadIdx.x + q * kT] = v[q];
+}
+
+// A workgroup's run of tasks [slot * tasks / wg3, (slot + 1) * tasks / wg3) in two roles.
+__device__ __forceinline__ void stage3_roles(const PipeArgs& A, Stage3RSmem& S, u32 slot) {
+  const PipeGroup& G = A.g3;
+  const u32 tasks = G.task0[G.nb];
+  const u32 t0 = (u32)((u64)slot * tasks / A.wg3), n = (u32)((u64)(slot + 1u) * tasks / A.wg3) - t0;
+  const u32 w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  PIPE_STAMP(0);
+  if (w < kS3Loaders && w < n) {
+    // the first task's record words are in flight while the tables fill LDS
+    u32 i = w;
+    TaskPos T = task_pos(G, t0 + i);
+    TaskRec R = stage3_r1(A, T);
+    if (!(A.debug & 8u)) roles_tables(A, S);
+    bool cand = stage3_cand(A, T, R);
+    TaskState Z = stage3_r2(A, T, R, cand);
+    if (threadIdx.x < kS3Bufs) S.seq[threadIdx.x] = 0u;
+    __syncthreads();
+    PIPE_STAMP(1);
+    u64 waited = 0, tw = 0;  // (stamps: time spent waiting for a free buffer, for its loads)
+    for (;;) {
+      const u32 in_ = i + kS3Loaders;
+      const bool more = in_ < n;  // (wave-uniform)
+      TaskPos Tn = T;
+      TaskRec Rn = R;
+      if (more) {  // the next task's record words, issued before this task's stores... of which there are none
+        Tn = task_pos(G, t0 + in_);
+        Rn = stage3_r1(A, Tn);
+      }
+      const u32 bi = i % kS3Bufs;
+      if (A.stamps) tw = __builtin_amdgcn_s_memrealtime();
+      if (i >= kS3Bufs) lds_wait_seq(&S.seq[bi], 2u * (i - kS3Bufs) + 2u);
+      if (A.stamps) {
+        waited += __builtin_amdgcn_s_memrealtime() - tw;
+        if (i == w) PIPE_STAMP(2);
+      }
+      stage3_build(A, S, T, R, Z, cand, bi);
+      lds_post_seq(&S.seq[bi], 2u * i + 1u);
+      if (!more) break;
+      i = in_;
+      T = Tn;
+      R = Rn;
+      cand = stage3_cand(A, T, R);
+      Z = stage3_r2(A, T, R, cand);
+    }
+    if (A.stamps) {
+      PIPE_STAMP(3);
+      if ((threadIdx.x & 63) == 0) A.stamps[((u64)blockIdx.x * kPW + w) * 8 + 4] = waited;
+    }
+    return;
+  }
+  if (w < kS3Loaders) {  // a loader without a task: the tables and the barrier only
+    if (!(A.debug & 8u)) roles_tables(A, S);
+    if (threadIdx.x < kS3Bufs) S.seq[threadIdx.x] = 0u;
+    __syncthreads();
+    return;
+  }
+  __syncthreads();
+  PIPE_STAMP(1);
+  u64 waited = 0;  // (stamps: time spent waiting for a published image)
+  for (u32 i = w - kS3Loaders; i < n; i += kS3Storers) {
+    const u32 bi = i % kS3Bufs;
+    const u64 tw = A.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    lds_wait_seq(&S.seq[bi], 2u * i + 1u);
+    if (A.stamps) {
+      waited += __builtin_amdgcn_s_memrealtime() - tw;
+      if (i == w - kS3Loaders) PIPE_STAMP(2);
+    }
+    stage3_store(A, S, t0 + i, bi, i);
+  }
+  if (A.stamps) {
+    PIPE_STAMP(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PIPE_STAMP(5);
+    if ((threadIdx.x & 63) == 0) A.stamps[((u64)blockIdx.x * kPW + w) * 8 + 4] = waited;
+  }
+}
+
 #ifndef RMQ_PIPE_WAVES_PER_SIMD
 #define RMQ_PIPE_WAVES_PER_SIMD 4  // <= 128 VGPRs, no spills: 2 resident workgroups per CU
 #endif
@@ -2179,6 +2402,10 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   // (RMQ_S3_XCD: the stage-3 workgroups of one XCD take one contiguous range of slots, so records
   // next to each other in a batch, and in their partitions' rings, are stored through one L2)
   const u32 slot = A.s3_xcd ? xcd_rank(0, A.wg3, wg) : wg;
+  if (!XR && A.s3_roles) {
+    stage3_roles(A, *reinterpret_cast<Stage3RSmem*>(smem_raw), slot);
+    return;
+  }
   u32 task = __builtin_amdgcn_readfirstlane(slot * kPW + (threadIdx.x >> 6));
   PIPE_STAMP(0);
   if (!XR && A.s3_pair) {

@@ -694,7 +694,10 @@ __device__ __forceinline__ void finish_entry(const IngestArgs& A, u32 e, u64& n_
     const u32 ilog = st.interval_log2;
     const u64 old_used = st.used[p];
     if (d.term > st.term[p]) st.term[p] = d.term;
-    st.lterm[p] = d.lterm;  // the entry's last entry term (0: older, unknown)
+    // the entry's last entry term; 0: older than the leader's term start, unknown here, so the log
+    // ends in a term below the leader's (the vote's bound, never 0: a replica whose log ends in
+    // term-t entries must not grant a candidate of an older last term)
+    st.lterm[p] = d.lterm ? d.lterm : kLtermBound | (d.term ? d.term - 1ull : 0ull);
     st.mterm[p] = d.term;   // the log matches the term-d.term leader's through the entry's end
     u64 spos = st.start_pos[p];
     if (d.rebase) {

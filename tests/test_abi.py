@@ -2,12 +2,15 @@
 its struct layouts match the ctypes mirror, and compute entry points fail loudly (no fallback)."""
 import ctypes as C
 import os
+import re
 import subprocess
 
 import pytest
 
 from ripplemq_amd import _abi as A
 from ripplemq_amd.engine import Engine, EngineConfig, EngineError
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -54,6 +57,13 @@ def test_struct_layouts_match_ctypes(tmp_path):
 
 def test_strerror_and_defaults(lib):
     assert lib.rmq_strerror(A.RMQ_ENOTLEADER) == b"Not leader"
+    # every status the header declares has its own message
+    hdr = open(os.path.join(REPO, "include", "ripplemq_engine.h")).read()
+    codes = dict((m.group(1), int(m.group(2))) for m in re.finditer(r"\b(RMQ_(?:OK|PENDING|E[A-Z]+))\s*=\s*(-?\d+)", hdr))
+    assert "RMQ_ETERM" in codes and "RMQ_ESTALE" in codes, codes
+    msgs = {name: lib.rmq_strerror(v) for name, v in codes.items()}
+    assert all(m and m != b"unknown status" for m in msgs.values()), msgs
+    assert len(set(msgs.values())) == len(msgs), msgs
     assert lib.rmq_abi_version() == A.RMQ_ABI_VERSION
     c = A.RmqConfig()
     lib.rmq_config_default(C.byref(c), 4096, 3)

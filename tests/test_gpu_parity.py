@@ -294,7 +294,9 @@ def test_pipelined_groups(oracle_mod, group):
 
 
 @pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"},
-                                 {"RMQ_S3_XCD": "0", "RMQ_S1_XCD": "1"}, {"RMQ_S1_XCD": "1", "RMQ_S1_WGS": "37"}])
+                                 {"RMQ_S3_XCD": "0", "RMQ_S1_XCD": "1"}, {"RMQ_S1_XCD": "1", "RMQ_S1_WGS": "37"},
+                                 {"RMQ_S3_ROLES": "0"}, {"RMQ_S3_ROLES": "1", "RMQ_S3_XCD": "0"},
+                                 {"RMQ_S3_ROLES": "4"}])
 def test_pipelined_dispatch_modes(oracle_mod, monkeypatch, env):
     # the non-default dispatch modes (read at rmq_create): resident task waves looping over the
     # group's tasks, stage-3 workgroups dispatched after the other roles, few large-record
@@ -310,6 +312,35 @@ def test_pipelined_dispatch_modes(oracle_mod, monkeypatch, env):
         _pipelined(dev, ora, [make_batch(spec, b) for b in range(6)])
         hot = np.argsort([-ora.state(p)["log_end_offset"] for p in range(4096)])
         compare_state(dev, ora, cfg, parts=list(hot[:16]) + list(range(0, 4096, 257)))
+
+
+@pytest.mark.parametrize("roles", ["0", "1", "3"])
+def test_stage3_roles_mixed_sizes(oracle_mod, monkeypatch, roles):
+    # stage 3 in loader / storer waves (RMQ_S3_ROLES) against the oracle: records of 0 B to 3 KB
+    # (image tasks, tasks whose loader stores medium records' pieces itself, large-record waves),
+    # launch groups with retention and ring wrap, a no-space partition, a partition not led and
+    # unknown partitions
+    monkeypatch.setenv("RMQ_S3_ROLES", roles)
+    cfg, dev, ora = pair(oracle_mod, num_partitions=300, replication_factor=3, segment_bytes=1 << 18,
+                         index_interval=256, max_batch_records=20000, pipeline_depth=4)
+    with dev, ora:
+        for e in (dev, ora):
+            e.set_replicas(9, [1, 0, 2], 0)
+        short = StreamSpec(300, 20000, "zipf", size=(0, 112), config_index=31, invalid_frac=0.005)
+        mixed = StreamSpec(300, 6000, "uniform", size=(0, 3000), config_index=32)
+        batches = [make_batch(short if b % 3 else mixed, b) for b in range(10)]
+        nsp = make_batch(StreamSpec(300, 3000, "uniform", size=100, config_index=33), 0)
+        nsp.pidx[:2500] = 5  # 2500 x 128 B > ring - I: partition 5 takes none of this batch's records
+        batches.insert(4, nsp)
+        _pipelined(dev, ora, batches)
+        # a fetch right after the last launch: the log starts of groups that outgrew a ring
+        # (late_retention before the fetch kernels), consumers at offset 0 (RMQ_EOFFSET below a start)
+        pidx = np.arange(300, dtype=np.uint32)
+        rd, resd, bd, _ = dev.fetch(pidx, np.zeros(300, np.uint32), np.full(300, 50, np.uint32))
+        ro, reso, bo, _ = ora.fetch(pidx, np.zeros(300, np.uint32), np.full(300, 50, np.uint32))
+        assert rd == ro and np.array_equal(resd, reso) and np.array_equal(bd, bo), "fetch differs"
+        compare_state(dev, ora, cfg, full_rings=True)
+        assert max(ora.state(p)["log_start_offset"] for p in range(300)) > 0, "scenario must exercise retention"
 
 
 def test_config_B_pipelined(oracle_mod):
