@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define RMQ_ABI_VERSION 9u
+#define RMQ_ABI_VERSION 10u
 #define RMQ_MAX_RF 8u
 #define RMQ_ALL_PARTITIONS 0xFFFFFFFFu
 #define RMQ_OFFSET_NONE 0xFFFFFFFFFFFFFFFFull /* out_offsets value of a rejected record */
@@ -146,6 +146,15 @@ typedef struct rmq_fetch_req {
    (ConsumerClientImpl.java:61-117) in one device pass. At most one committing request per
    (partition, consumer) in a call (RMQ_EINVAL otherwise). */
 #define RMQ_FETCH_COMMIT 1u
+/* rmq_fetch_req.flags (ABI 10): read this engine's own replica of pidx, whether it leads the
+   partition or follows it: the slice starts at the partition's replica cursor (rmq_set_replica_cursor;
+   the consumer field only keys the position cache and must be < max_consumers) and ends at the
+   replica's commit (its high_watermark: on a follower the part of its log below the leader commit
+   it learned). With RMQ_FETCH_COMMIT the replica cursor moves to start_offset + count (local to this
+   engine, never replicated; one committing replica request per partition in a call). This is how a
+   replica's durable tier reads its own log: jraft keeps the whole log on every node
+   (PartitionRaftServer.java:53,88-90), so a follower persists what it holds, not only a leader. */
+#define RMQ_FETCH_REPLICA 2u
 
 typedef struct rmq_fetch_res {
   uint64_t start_offset;       /* reference: MessageBatchReadResponse.offset (the consumer offset);
@@ -328,6 +337,10 @@ int rmq_sync(rmq_engine* e);
    one polls as RMQ_EINVAL. */
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                                const uint64_t* offset, uint32_t n, int32_t* status, uint64_t* ticket);
+/* ABI 10: the replica cursors of n partitions (where RMQ_FETCH_REPLICA reads start): a durable
+   tier's end after it reopens its files. Local to this engine (no round carries it); ordered with
+   the pipeline stream like a consumer-offset commit. */
+int rmq_set_replica_cursor(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* offset);
 
 /* Batched consumer fetch: for each request, off = committed consumer offset (default 0),
    returns records [off, min(off + max, high_watermark)) (PartitionStateMachine.java:85-110).

@@ -45,6 +45,7 @@ def load() -> C.CDLL:
         "ro_ack": (C.c_int, [vp, vp, vp, vp, u32]),
         "ro_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp]),
         "ro_fetch": (C.c_int, [vp, vp, u32, vp, u64, vp, C.POINTER(u64)]),
+        "ro_set_replica_cursor": (C.c_int, [vp, u32, vp, vp]),
         "ro_get_partition_state": (C.c_int, [vp, u32, C.POINTER(A.RmqPartitionState)]),
         "ro_get_partition_states": (C.c_int, [vp, u32, u32, vp]),
         "ro_commit_notice": (C.c_int, [vp, u32, vp]),
@@ -303,22 +304,30 @@ class OracleEngine:
         del self._tickets[ticket]
         return A.RMQ_OK if done else A.RMQ_ENOTLEADER
 
-    def fetch(self, pidx, consumer, max_records, out_cap=None, commit=False, out=None):
+    def set_replica_cursor(self, pidx, offset):
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        offset = np.ascontiguousarray(offset, np.uint64)
+        rc = self.lib.ro_set_replica_cursor(self.h, len(pidx), _p(pidx), _p(offset))
+        if rc:
+            raise EngineError(rc, "oracle set_replica_cursor")
+
+    def fetch(self, pidx, consumer, max_records, out_cap=None, commit=False, out=None, replica=False):
         n = len(pidx)
         req = np.zeros((n, 4), np.uint32)
         req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
+        req[:, 3] = A.RMQ_FETCH_REPLICA if replica else 0
         res = np.zeros(n, FETCH_RES_DTYPE)
         used = C.c_uint64()
         if out is not None:  # the caller's buffer (as Engine.fetch)
             if commit:
-                req[:, 3] = A.RMQ_FETCH_COMMIT
+                req[:, 3] |= A.RMQ_FETCH_COMMIT
             rc = self.lib.ro_fetch(self.h, _p(req), n, _p(out), out.size, _p(res), C.byref(used))
             return rc, res, out, int(used.value)
         if out_cap is None:  # the size query commits nothing
             self.lib.ro_fetch(self.h, _p(req), n, None, 0, _p(res), C.byref(used))
             out_cap = int(used.value)
         if commit:
-            req[:, 3] = A.RMQ_FETCH_COMMIT
+            req[:, 3] |= A.RMQ_FETCH_COMMIT
         out = np.zeros(max(out_cap, 1), np.uint8)
         rc = self.lib.ro_fetch(self.h, _p(req), n, _p(out), out_cap, _p(res), C.byref(used))
         return rc, res, out[:out_cap], int(used.value)

@@ -137,6 +137,7 @@ typedef struct {
      vote (term, candidate) and whether this replica led that term */
   uint64_t lterm, mterm, heard, vterm;
   uint32_t vfor, led;
+  uint64_t rcur; /* replica cursor: where an RMQ_FETCH_REPLICA read starts (local, never replicated) */
 } ro_part;
 
 struct ro_engine {
@@ -776,18 +777,36 @@ int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t
 
 /* PartitionStateMachine.handleBatchRead: off = consumerOffsets.getOrDefault(id, 0);
    returns messages[off, min(off + max, size)) with size = applied (committed) records. */
+/* The lowest replica slot this engine stores (the engine reads a replica read from it; the bytes of
+   every local slot are equal), else the leader's. */
+static uint32_t local_slot(const ro_engine* e, const ro_part* s) {
+  for (uint32_t r = 0; r < e->cfg.replication_factor; ++r)
+    if (s->ranks[r] == e->cfg.rank) return r;
+  return s->leader_slot;
+}
+
+int ro_set_replica_cursor(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* offset) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (pidx[i] >= e->cfg.num_partitions) return RMQ_ENOPART;
+  for (uint32_t i = 0; i < n; ++i) e->parts[pidx[i]].rcur = offset[i];
+  return RMQ_OK;
+}
+
 int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, uint64_t out_cap,
              rmq_fetch_res* res, uint64_t* bytes_used) {
   uint64_t cursor = 0;
   int rc = RMQ_OK;
-  /* RMQ_FETCH_COMMIT: at most one committing request per (partition, consumer) */
+  /* RMQ_FETCH_COMMIT: at most one committing request per (partition, consumer); with
+     RMQ_FETCH_REPLICA (the partition's replica cursor) one per partition */
   for (uint32_t r = 0; r < n; ++r) {
-    if (reqs[r].flags & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
+    if (reqs[r].flags & ~(RMQ_FETCH_COMMIT | RMQ_FETCH_REPLICA)) return RMQ_EINVAL;
     if (!(reqs[r].flags & RMQ_FETCH_COMMIT) || reqs[r].pidx >= e->cfg.num_partitions ||
         reqs[r].consumer >= e->cfg.max_consumers)
       continue;
+    const uint32_t rep = reqs[r].flags & RMQ_FETCH_REPLICA;
     for (uint32_t q = 0; q < r; ++q)
-      if ((reqs[q].flags & RMQ_FETCH_COMMIT) && reqs[q].pidx == reqs[r].pidx && reqs[q].consumer == reqs[r].consumer)
+      if ((reqs[q].flags & RMQ_FETCH_COMMIT) && (reqs[q].flags & RMQ_FETCH_REPLICA) == rep &&
+          reqs[q].pidx == reqs[r].pidx && (rep || reqs[q].consumer == reqs[r].consumer))
         return RMQ_EINVAL;
   }
   for (uint32_t r = 0; r < n; ++r) {
@@ -800,7 +819,8 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
       continue;
     }
     ro_part* s = &e->parts[p];
-    if (!s->is_leader) {
+    const int rep = (reqs[r].flags & RMQ_FETCH_REPLICA) != 0; /* this engine's own replica */
+    if (!s->is_leader && !rep) {
       x->status = RMQ_ENOTLEADER;
       continue;
     }
@@ -808,7 +828,7 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
       x->status = RMQ_EINVAL;
       continue;
     }
-    uint64_t off = s->cons[reqs[r].consumer];
+    uint64_t off = rep ? s->rcur : s->cons[reqs[r].consumer];
     x->start_offset = off;
     uint64_t lim = off + reqs[r].max_records;
     if (lim < off) lim = UINT64_MAX;
@@ -828,7 +848,7 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
       rc = RMQ_ENOSPC;
       continue;
     }
-    if (out) ring_read(s->seg, ring_of(e, s->leader_slot, p), p0, out + cursor, nb);
+    if (out) ring_read(s->seg, ring_of(e, rep ? local_slot(e, s) : s->leader_slot, p), p0, out + cursor, nb);
     x->count = (uint32_t)(end - off);
     x->bytes = (uint32_t)nb;
     cursor += nb;
@@ -838,8 +858,13 @@ int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, 
     const rmq_fetch_res* x = &res[r];
     if (!(reqs[r].flags & RMQ_FETCH_COMMIT) || (x->status != RMQ_OK && x->status != RMQ_EOFFSET)) continue;
     ro_part* s = &e->parts[reqs[r].pidx];
-    s->cons[reqs[r].consumer] = x->start_offset + (x->status == RMQ_OK ? x->count : 0);
-    s->dirty = 1;
+    const uint64_t nx = x->start_offset + (x->status == RMQ_OK ? x->count : 0);
+    if (reqs[r].flags & RMQ_FETCH_REPLICA) {
+      s->rcur = nx; /* local: no round carries it */
+    } else {
+      s->cons[reqs[r].consumer] = nx;
+      s->dirty = 1;
+    }
   }
   if (bytes_used) *bytes_used = cursor;
   return rc;

@@ -62,6 +62,7 @@ int ro_set_segments(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint64
 int ro_ack(ro_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n);
 int ro_commit_consumer_offset(ro_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                               const uint64_t* offset, uint32_t n, int32_t* status);
+int ro_set_replica_cursor(ro_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* offset);
 int ro_fetch(ro_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint8_t* out, uint64_t out_cap,
              rmq_fetch_res* res, uint64_t* bytes_used);
 

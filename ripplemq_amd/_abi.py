@@ -15,8 +15,9 @@ REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "ripplemq_engine.h")
 LIB_PATH = os.environ.get("RMQ_LIB") or os.path.join(HERE, "libripplemq_engine.so")
 
-RMQ_ABI_VERSION = 9
+RMQ_ABI_VERSION = 10
 RMQ_FETCH_COMMIT = 1
+RMQ_FETCH_REPLICA = 2
 RMQ_FETCH_PINNED_ROWS = 0x100
 RMQ_FETCH_DEVICE_ROWS = 0x200
 RMQ_MAX_RF = 8
@@ -133,6 +134,7 @@ _SIGS = {
     "rmq_ticket_stats": (C.c_int, [vp, u64, C.POINTER(RmqAppendStats)]),
     "rmq_sync": (C.c_int, [vp]),
     "rmq_commit_consumer_offset": (C.c_int, [vp, vp, vp, vp, u32, vp, C.POINTER(u64)]),
+    "rmq_set_replica_cursor": (C.c_int, [vp, u32, vp, vp]),
     "rmq_fetch": (C.c_int, [vp, vp, u32, u32, vp, u64, vp, C.POINTER(u64)]),
     "rmq_fetch_async": (C.c_int, [vp, vp, u32, u32, vp, u64, vp, C.POINTER(u64)]),
     "rmq_fetch_poll": (C.c_int, [vp, u64, u32, C.POINTER(u64)]),

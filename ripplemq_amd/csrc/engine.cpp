@@ -547,7 +547,7 @@ void free_engine(rmq_engine* e) {
   repl_free(e);
   DevState& s = e->st;
   std::vector<void*> bufs = {s.start_off, s.start_pos, s.commit, s.hw, s.term_start, s.term, s.match, s.is_leader,
-                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.pcache, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq,
+                             s.local_mask, s.index, s.logs, s.ring, s.cons, s.pcache, s.rcur, s.cdirty, s.lcommit, s.csnap, s.cver, s.cq,
                              s.lterm, s.mterm, s.heard, e->d_crc,
                              e->d_stats, e->d_ctl32, e->d_ctl64, e->d_stamps, e->d_rlate};
   if (e->state_stage) hipHostFree(e->state_stage);
@@ -811,6 +811,7 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   CREATE_HIP(hipMemcpy(s.ring, e->ring.data(), (size_t)P * 8, hipMemcpyHostToDevice));
   CREATE_TRY(dalloc(&s.cons, (size_t)P * C));
   CREATE_TRY(dalloc(&s.pcache, (size_t)P * C * 2));
+  CREATE_TRY(dalloc(&s.rcur, (size_t)P));  // (dalloc zero-fills: every replica cursor at offset 0)
   CREATE_HIP(hipMemset(s.pcache, 0xFF, (size_t)P * C * 16));  // every entry empty
   CREATE_TRY(dalloc(&s.cdirty, P));
   CREATE_TRY(dalloc(&s.lcommit, P));
@@ -1435,6 +1436,23 @@ int rmq_sync(rmq_engine* e) {
   return drain(e);
 }
 
+int rmq_set_replica_cursor(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* offset) {
+  if (!e || (n && (!pidx || !offset))) return RMQ_EINVAL;
+  std::lock_guard<std::mutex> g(e->mu);
+  const uint32_t P = e->cfg.num_partitions;
+  for (uint32_t i = 0; i < n; ++i)
+    if (pidx[i] >= P) return RMQ_ENOPART;
+  if (!n) return RMQ_OK;
+  HIP_TRY(hipSetDevice(e->device));
+  int rc = quiesce(e);  // (fetches on the pipeline stream read and commit the cursors)
+  if (rc) return rc;
+  std::vector<uint64_t> cur(P);
+  HIP_TRY(hipMemcpy(cur.data(), e->st.rcur, P * 8ull, hipMemcpyDeviceToHost));
+  for (uint32_t i = 0; i < n; ++i) cur[pidx[i]] = offset[i];
+  HIP_TRY(hipMemcpy(e->st.rcur, cur.data(), P * 8ull, hipMemcpyHostToDevice));
+  return RMQ_OK;
+}
+
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                                const uint64_t* offset, uint32_t n, int32_t* status, uint64_t* ticket) {
   if (!e) return RMQ_EINVAL;
@@ -1673,7 +1691,7 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     e->fetch_done.push_back({old, (uint64_t)(int64_t)rc, used});
   }
   // RMQ_FETCH_COMMIT: known flags only, one committing request per (partition, consumer)
-  bool any = false;
+  bool any = false, replica = false;
   if (!rows_dev) {  // (device rows: never read here; their flags are ignored)
     // the OR of every row's flags word (the high half of its second 8-byte word), four rows per
     // step with no early exit: 16,384 rows in a few us instead of a branch per row
@@ -1690,23 +1708,28 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     }
     for (; r < n; ++r) a0 |= w[2 * r + 1];
     const uint32_t fl = (uint32_t)((a0 | a1 | a2 | a3) >> 32);
-    if (fl & ~RMQ_FETCH_COMMIT) return RMQ_EINVAL;
+    if (fl & ~(RMQ_FETCH_COMMIT | RMQ_FETCH_REPLICA)) return RMQ_EINVAL;
     any = (fl & RMQ_FETCH_COMMIT) != 0;
+    replica = (fl & RMQ_FETCH_REPLICA) != 0;
     if (any) {
       const size_t slots = (size_t)e->cfg.num_partitions * e->cfg.max_consumers;
       if (e->fetch_stamp.size() != slots) {
         e->fetch_stamp.assign(slots, 0u);
+        e->fetch_stamp_rep.assign(e->cfg.num_partitions, 0u);
         e->fetch_gen = 0;
       }
       if (++e->fetch_gen == 0) {
         std::fill(e->fetch_stamp.begin(), e->fetch_stamp.end(), 0u);
+        std::fill(e->fetch_stamp_rep.begin(), e->fetch_stamp_rep.end(), 0u);
         e->fetch_gen = 1;
       }
       for (uint32_t r = 0; r < n; ++r) {
         const rmq_fetch_req& q = reqs[r];
         if (!(q.flags & RMQ_FETCH_COMMIT) || q.pidx >= e->cfg.num_partitions || q.consumer >= e->cfg.max_consumers)
           continue;
-        uint32_t& sl = e->fetch_stamp[(size_t)q.pidx * e->cfg.max_consumers + q.consumer];
+        // a replica read commits the partition's replica cursor: one per partition (any consumer key)
+        uint32_t& sl = (q.flags & RMQ_FETCH_REPLICA) ? e->fetch_stamp_rep[q.pidx]
+                                                     : e->fetch_stamp[(size_t)q.pidx * e->cfg.max_consumers + q.consumer];
         if (sl == e->fetch_gen) return RMQ_EINVAL;
         sl = e->fetch_gen;
       }
@@ -1775,6 +1798,7 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     a.need_host = f.need_dev;
     a.n = n;
     a.commits = any ? 1u : 0u;
+    a.replica = replica ? 1u : 0u;
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     // (profiling replays a fetch's kernels back to back; a committing fetch runs once: each run
     // would commit again and the next would read from the committed offset)

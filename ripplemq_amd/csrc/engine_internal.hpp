@@ -367,6 +367,7 @@ struct rmq_engine {
   uint64_t* fetch_need_host = nullptr;  // [kFetchSlots] coherent pinned words (FetchSlot::need)
   uint64_t fetch_seq = 0;        // tickets
   std::vector<uint32_t> fetch_stamp;  // RMQ_FETCH_COMMIT duplicate check ([P][C] generation stamps)
+  std::vector<uint32_t> fetch_stamp_rep;  // the same for replica reads ([P]: one replica cursor each)
   uint32_t fetch_gen = 0;
   std::deque<std::array<uint64_t, 3>> fetch_done;  // {ticket, rc, bytes used} completed, not yet polled
   // consumer-offset commits: staging slots (pinned items -> device by one copy on the pipeline

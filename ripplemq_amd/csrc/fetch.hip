@@ -200,7 +200,9 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, const ui
   const bool okp = live && p < st.P;
   const u32 pp = okp ? p : 0u, cc = c < st.C ? c : 0u;
   const u32 lead = okp ? st.is_leader[pp] : 0u;
-  const u64 off = okp ? st.cons[(u64)pp * st.C + cc] : 0ull;
+  // RMQ_FETCH_REPLICA: this engine's own replica, from its replica cursor, leader or follower
+  const bool rep = a.replica && (rq.w & kFetchReplica);
+  const u64 off = okp ? (rep ? st.rcur[pp] : st.cons[(u64)pp * st.C + cc]) : 0ull;
   const u64 hw = okp ? st.hw[pp] : 0ull;
   PartView v;
   v.leo = okp ? st.leo[pp] : 0ull;
@@ -209,15 +211,16 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, const ui
   v.start_pos = okp ? st.start_pos[pp] : 0ull;
   const u32 lm = okp ? st.local_mask[pp] : 0u;
   const u64 desc = okp ? st.ring[pp] : 0ull;
-  const u64* ce = st.pcache + ((u64)pp * st.C + cc) * 2;
-  const u64 h_off = okp ? ce[0] : ~0ull, h_pos = okp ? ce[1] : 0ull;
+  const ulonglong2 ce = okp ? *reinterpret_cast<const ulonglong2*>(st.pcache + ((u64)pp * st.C + cc) * 2)
+                            : make_ulonglong2(~0ull, 0ull);
+  const u64 h_off = ce.x, h_pos = ce.y;
   v.rg = ring_ref(desc, st.interval_log2, st.icap_mul);
   v.ring = st.logs;
   bool need = false;  // the slice is not empty: both its ends are searched
   if (!live) {
   } else if (p >= st.P) {
     status = kNoPart;
-  } else if (!lead) {
+  } else if (!lead && !rep) {
     status = kNotLeader;
   } else if (c >= st.C) {
     status = kInval;
@@ -276,9 +279,10 @@ __global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
     // request's partition and consumer are in range; reloaded here rather than held through the
     // resolve, which would take 8 more VGPRs)
     if (q.status == kOk && q.count) {
+      // one 16-byte store: requests of one (partition, consumer) in one call (allowed when none
+      // commits) each write a true {offset, position} pair, and a pair is never torn between two
       u64* ce = a.st.pcache + ((u64)a.req_dev[4 * r] * a.st.C + a.req_dev[4 * r + 1]) * 2;
-      ce[0] = q.start + q.count;
-      ce[1] = q.pos0 + q.bytes;
+      *reinterpret_cast<ulonglong2*>(ce) = make_ulonglong2(q.start + q.count, q.pos0 + q.bytes);
     }
     a.res[4 * r + 0] = q.start;
     a.res[4 * r + 2] = q.count | (q.bytes << 32);
@@ -378,8 +382,13 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
     if (a.commits && (a.req_dev[4 * rr + 3] & 1u)) {
       if (!nospc && (s0 == kOk || s0 == kOffset)) {
         const u32 p = a.req_dev[4 * rr], c = a.req_dev[4 * rr + 1];
-        a.st.cons[(u64)p * a.st.C + c] = w0 + (s0 == kOk ? (u64)(uint32_t)w2 : 0ull);
-        a.st.cdirty[p] = 1u;  // (with a transport the row travels with the next round)
+        const u64 nx = w0 + (s0 == kOk ? (u64)(uint32_t)w2 : 0ull);
+        if (a.replica && (a.req_dev[4 * rr + 3] & kFetchReplica)) {
+          a.st.rcur[p] = nx;  // the replica cursor (local: no round carries it)
+        } else {
+          a.st.cons[(u64)p * a.st.C + c] = nx;
+          a.st.cdirty[p] = 1u;  // (with a transport the row travels with the next round)
+        }
       }
     }
   }

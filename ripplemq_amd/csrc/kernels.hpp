@@ -144,6 +144,7 @@ struct DevState {
                          //   of each consumer's last served slice (fetch.hip); an entry is always a
                          //   true pair (committed records never move), offset ~0 = empty
   uint32_t* cdirty;      // [P] consumer offsets changed since the last replication round (FORMAT §9)
+  uint64_t* rcur;        // [P] replica cursor: where an RMQ_FETCH_REPLICA read starts (local, not replicated)
   uint64_t* lcommit;     // [P] follower: the newest leader commit learned (rounds, commit notices;
                          //   FORMAT.md §9); a leader's own is `commit`
   uint64_t* csnap;       // [2][P] leader commit at the end of launch L, in slot L & 1 (partition threads
@@ -319,8 +320,10 @@ struct FetchArgs {
   uint32_t n;
   uint32_t csum_lines;
   uint32_t commits;          // the host checked read-and-commit requests in the call (else flags ignored)
+  uint32_t replica;          // the host checked RMQ_FETCH_REPLICA requests in the call (else flags ignored)
 };
 constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
+constexpr uint32_t kFetchReplica = 2u;  // rmq_fetch_req.flags RMQ_FETCH_REPLICA
 constexpr uint32_t kCsumStride = 16;   // u64 words per chunk sum (128 bytes)
 
 

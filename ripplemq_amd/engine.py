@@ -209,6 +209,12 @@ class Engine:
                "rmq_vote")
         return bool(g.value)
 
+    def set_replica_cursor(self, pidx, offset) -> None:
+        """Where RMQ_FETCH_REPLICA reads of these partitions start (rmq_set_replica_cursor)."""
+        pidx = np.ascontiguousarray(pidx, np.uint32)
+        offset = np.ascontiguousarray(offset, np.uint64)
+        _check(self.lib.rmq_set_replica_cursor(self.h, len(pidx), _ptr(pidx), _ptr(offset)), "rmq_set_replica_cursor")
+
     def set_vote(self, pidx: int, term: int, voted_for: int) -> None:
         """Replay of a persisted vote (rmq_set_vote)."""
         _check(self.lib.rmq_set_vote(self.h, pidx, term, voted_for), "rmq_set_vote")
@@ -368,17 +374,19 @@ class Engine:
         return rc
 
     def fetch(self, pidx, consumer, max_records, out_cap: int | None = None, commit: bool = False,
-              out: np.ndarray | None = None):
+              out: np.ndarray | None = None, replica: bool = False):
         """rmq_fetch into a host array (sized by a first call when out_cap is None, or the caller's
         uint8 `out`, e.g. page-locked from host_empty: one call, RMQ_ENOSPC if it is too small);
-        commit: RMQ_FETCH_COMMIT on every request (the size query commits nothing)."""
+        commit: RMQ_FETCH_COMMIT on every request (the size query commits nothing); replica:
+        RMQ_FETCH_REPLICA (this engine's own replica from its replica cursor, leader or follower)."""
         n = len(pidx)
         req = np.zeros((n, 4), np.uint32)
         req[:, 0], req[:, 1], req[:, 2] = pidx, consumer, max_records
+        req[:, 3] = A.RMQ_FETCH_REPLICA if replica else 0
         res = np.zeros(n, FETCH_RES_DTYPE)
         if out is not None:
             if commit:
-                req[:, 3] = A.RMQ_FETCH_COMMIT
+                req[:, 3] |= A.RMQ_FETCH_COMMIT
             used = C.c_uint64()
             rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, _ptr(out), out.size, _ptr(res),
                                     C.byref(used))
@@ -392,7 +400,7 @@ class Engine:
                 raise EngineError(rc, "rmq_fetch")
             out_cap = int(used.value)
         if commit:
-            req[:, 3] = A.RMQ_FETCH_COMMIT
+            req[:, 3] |= A.RMQ_FETCH_COMMIT
         out = np.zeros(max(out_cap, 1), np.uint8)
         used = C.c_uint64()
         rc = self.lib.rmq_fetch(self.h, _ptr(req), n, A.RMQ_MEM_HOST, _ptr(out), out_cap, _ptr(res), C.byref(used))

@@ -7,10 +7,13 @@ The engine's replica rings keep a retained window only (FORMAT.md §4): a fetch 
 ``RMQ_EOFFSET``. This module is the tier that restores the reference's semantics on the host side:
 
 * ``DurableLog.spill()`` moves every committed record not yet durable into per-partition segment
-  files with ONE ``rmq_fetch`` for all partitions: the durable end of each partition is a consumer
-  offset of its own (a reserved consumer slot, ``cursor``), so the fetch kernel returns exactly the
-  records ``[durable end, high watermark)`` and the cursor advances with one
-  ``rmq_commit_consumer_offset``. A segment file holds the records exactly as the rings do (FORMAT.md
+  files with ONE ``rmq_fetch`` for all partitions, led or followed: replica reads
+  (``RMQ_FETCH_REPLICA | RMQ_FETCH_COMMIT``) start at each partition's replica cursor (the durable
+  end, local to the engine) and end at the replica's commit, so the fetch kernel returns exactly the
+  records ``[durable end, commit)`` of this engine's own replica and moves the cursor on the device.
+  jraft keeps the whole log on every node (``PartitionRaftServer.java:53,88-90``): a follower's tier
+  persists its replica too, so a leader moved to it serves consumers below its rings from its own
+  files. A segment file holds the records exactly as the rings do (FORMAT.md
   §1: 16-byte header {offset, length, CRC32C} + payload padded to 16 bytes), named by its first
   offset (``p<pidx>/<first offset>.seg``), rolled at ``segment_file_bytes``.
 * ``DurableLog.read(p, off, max)`` serves ``[off, min(off + max, durable end))`` from the files
@@ -27,7 +30,8 @@ The engine's replica rings keep a retained window only (FORMAT.md §4): a fetch 
   ``p<pidx>/meta.json``, each replaced atomically (write, fsync if asked, rename) when it changed;
   ``replay`` restores both after the records (the term through ``rmq_become_leader``, so only
   appends of the restored term advance the commit). Offsets and terms are durable at spill
-  granularity, like the records.
+  granularity, like the records; a vote is durable before it is answered (``save_vote``, Raft's
+  votedFor in raft_meta, ``PartitionRaftServer.java:89``).
 
 Spill must run at least once per retained window of every partition (rings hold ``retain``
 batches of their traffic, ``ripplemq_amd/rings.py``); a cursor below a ring's start raises, since
@@ -187,7 +191,8 @@ class _PartitionFiles:
                 os.fsync(f.fileno())
         os.replace(tmp, os.path.join(self.dir, name))
 
-    def save_state(self, offsets: np.ndarray, term: int, cursor: int, fsync: bool, vote=(0, A.RMQ_NO_VOTE)) -> None:
+    def save_state(self, offsets: np.ndarray, term: int, cursor: int, fsync: bool, vote=(0, A.RMQ_NO_VOTE),
+                   led: int = 1) -> None:
         """The partition's consumer-offset row, term and vote (jraft's raft_meta term / votedFor,
         PartitionRaftServer.java:89), each rewritten only when it changed. The
         tier's own cursor slot is stored as 0 (the durable end is in the ends file and moves with
@@ -201,7 +206,13 @@ class _PartitionFiles:
         if row != self._row:
             self._replace(OFFSETS_FILE, row, fsync)
             self._row = row
-        meta = {"term": int(term), "voted_term": int(vote[0]), "voted_for": int(vote[1]), "cursor": int(cursor)}
+        self.save_meta(term, vote, cursor, fsync, led)
+
+    def save_meta(self, term: int, vote, cursor: int, fsync: bool, led: int = 1) -> None:
+        """meta.json (term, vote, whether this replica led the vote's term, cursor) when it changed:
+        written to a temporary file and renamed."""
+        meta = {"term": int(term), "voted_term": int(vote[0]), "voted_for": int(vote[1]), "led": int(led),
+                "cursor": int(cursor)}
         if self._meta is None:
             self._meta = self.load_meta()
         if self._meta != meta:
@@ -290,7 +301,8 @@ def split_records(data: bytes) -> list[tuple[int, int, bytes]]:
 
 
 class DurableLog:
-    """Segment files of the partitions ``partitions`` of one engine (their leader), fed by spill."""
+    """Segment files of the partitions ``partitions`` of one engine (every partition it holds a
+    replica of, led or followed), fed by spill from the engine's own replica."""
 
     def __init__(self, engine, directory: str, partitions, cursor: int, *,
                  segment_file_bytes: int = 64 << 20, fsync: bool = False):
@@ -319,14 +331,22 @@ class DurableLog:
         self._fd = np.full(len(self._files), -1, np.int64)
         self._limit = int(segment_file_bytes)
         self.phase_s: dict[str, float] = {}
-        # a reopened tier continues where its files end: the cursor slot names that offset
+        # a reopened tier continues where its files end: the replica cursors name that offset
+        # (`cursor` only keys the replica reads' position cache; no consumer slot is used)
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
         ends = np.fromiter((f.end for f in self.parts.values()), np.uint64, len(self.parts))
-        if len(pidx) and ends.any():
-            self.engine.commit_consumer_offset(pidx, np.full(len(pidx), self.cursor, np.uint32), ends)
+        if len(pidx):
+            self.engine.set_replica_cursor(pidx, ends)
 
     def end(self, p: int) -> int:
         return self.parts[p].end
+
+    def save_vote(self, p: int, term: int, voted_for: int) -> None:
+        """Raft's votedFor (and currentTerm) of partition p, durable BEFORE the vote is answered
+        (jraft's raft_meta, PartitionRaftServer.java:89): meta.json is replaced (fsync'd when the tier
+        fsyncs) so that a replica that restarts cannot vote twice in one term."""
+        f = self.parts[int(p)]
+        f.save_meta(term, (term, voted_for), self.cursor, self.fsync, led=0)
 
     def _merge(self, k: int) -> None:
         """The record positions of partition k's spills not merged into its files object yet."""
@@ -369,9 +389,11 @@ class DurableLog:
         # one fetch into a reused buffer (page-locked when the engine offers it), grown when short
         while True:
             if self._buf is not None:
-                rc, res, buf, used = self.engine.fetch(pidx, cons, mx, out=self._buf)
+                rc, res, buf, used = self.engine.fetch(pidx, cons, mx, out=self._buf, commit=True, replica=True)
                 if rc == A.RMQ_OK:
                     break
+                # (RMQ_ENOSPC: the requests that fitted moved their cursors; every one reads again)
+                self.engine.set_replica_cursor(pidx, self._end.astype(np.uint64))
             else:
                 used = 1 << 20
             need = max(2 * int(used), 1 << 20)
@@ -383,8 +405,8 @@ class DurableLog:
                 self._buf = np.zeros(need, np.uint8)
         t1 = time.perf_counter()
         status = res["status"].astype(np.int64)
-        bad = np.flatnonzero((status != A.RMQ_OK) & (status != A.RMQ_ENOTLEADER))  # (a follower's tier is
-        if len(bad):                                                                # fed by its own term)
+        bad = np.flatnonzero(status != A.RMQ_OK)
+        if len(bad):
             p, st = int(pidx[bad[0]]), int(status[bad[0]])
             raise EngineError(st, f"spill of partition {p} (records lost before they were durable)"
                               if st == A.RMQ_EOFFSET else f"spill of partition {p}")
@@ -417,6 +439,12 @@ class DurableLog:
             rc = A.load().rmq_tier_append(len(sel), _ptr(fds), _ptr(first), _ptr(count), _ptr(opos), _ptr(nbytes),
                                           data.ctypes.data, _ptr(pos), 16, 1 if self.fsync else 0)
             if rc:
+                # some runs may already be (partly) in their files: cut every file back to its size
+                # before the call, so the records the next spill writes again are not doubled. The
+                # replica cursors moved with the fetch: put them back to the durable ends too.
+                for j in range(len(sel)):
+                    os.ftruncate(int(fds[j]), int(before[j] - self._segbase[sel[j]]))
+                self.engine.set_replica_cursor(ps, self._end[sel].astype(np.uint64))
                 raise EngineError(rc, "spill: segment append (a run does not hold its records, or an I/O error)")
             ends = np.cumsum(count.astype(np.int64) + 1)
             self._chunks.append((sel.astype(np.int64), ends - count.astype(np.int64) - 1, count.astype(np.int64),
@@ -425,8 +453,6 @@ class DurableLog:
             self._total[sel] += nbytes.astype(np.int64)
             moved = int(count.sum())
             t2 = time.perf_counter()
-            self.engine.commit_consumer_offset(ps.astype(np.uint32), np.full(len(sel), self.cursor, np.uint32),
-                                               first + count)
         else:
             t2 = time.perf_counter()
         t3 = time.perf_counter()
@@ -439,15 +465,18 @@ class DurableLog:
         if 0 <= self.cursor < rows.shape[1]:
             rows[:, self.cursor] = 0  # (the tier's own slot: the durable end, in the ends file)
         key = np.concatenate([rows, sts["term"][:, None], sts["voted_term"][:, None],
-                              sts["voted_for"][:, None].astype(np.uint64)], axis=1)
-        # only the partitions whose row, term or vote changed since the last save (most spills: none)
-        changed = status != A.RMQ_ENOTLEADER
+                              sts["voted_for"][:, None].astype(np.uint64), sts["led"][:, None].astype(np.uint64)],
+                             axis=1)
+        # only the partitions whose row, term or vote changed since the last save (most spills: none);
+        # every partition held here, led or followed (a follower's term and vote are its raft_meta)
+        changed = np.ones(len(pidx), bool)
         if self._saved is not None:
             changed &= (key != self._saved).any(axis=1)
         for k in np.flatnonzero(changed).tolist():
             p = int(pidx[k])
             self.parts[p].save_state(rows[k], int(sts["term"][k]), self.cursor, self.fsync,
-                                     vote=(int(sts["voted_term"][k]), int(sts["voted_for"][k])))
+                                     vote=(int(sts["voted_term"][k]), int(sts["voted_for"][k])),
+                                     led=int(sts["led"][k]))
         if self._saved is None:
             self._saved = key.copy()
         else:
@@ -538,19 +567,18 @@ def replay(directory: str, engine, partitions, *, batch_records: int = 65536) ->
     for p, f in files.items():
         meta = f.load_meta()
         term = int(meta.get("term", 0))
-        if term > engine.state(p)["term"]:
+        vt, vf = int(meta.get("voted_term", 0)), int(meta.get("voted_for", A.RMQ_NO_VOTE))
+        led = int(meta.get("led", 1))  # (a meta without the flag came from a leader's spill)
+        if led and term > engine.state(p)["term"]:
             engine.become_leader(p, term)
             terms += 1
-        vt, vf = int(meta.get("voted_term", 0)), int(meta.get("voted_for", A.RMQ_NO_VOTE))
-        if vt > engine.state(p)["voted_term"]:  # a vote newer than the term it led (raft_meta votedFor)
-            engine.set_vote(p, vt, vf)
+        if vt > engine.state(p)["voted_term"]:  # a vote newer than any term it led (raft_meta votedFor):
+            engine.set_vote(p, vt, vf)          # restored as a vote, never as a leadership
+            terms += 0 if led else 1
         raw = f.load_offsets_bytes()
         if raw:
             offs = np.frombuffer(raw, np.uint64).copy()
             n = min(len(offs), engine.cfg.max_consumers)
-            c = int(meta.get("cursor", -1))
-            if 0 <= c < n:
-                offs[c] = f.end  # the tier's cursor: the durable end
             rc, st = engine.commit_consumer_offset(np.full(n, p, np.uint32), np.arange(n, dtype=np.uint32), offs[:n])
             if rc:
                 raise EngineError(rc, f"replay of partition {p}: consumer offsets")

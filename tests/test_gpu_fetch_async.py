@@ -208,6 +208,45 @@ def test_position_cache_hits_and_misses(oracle_mod):
         assert (st == A.RMQ_EOFFSET).any() and (st == A.RMQ_OK).any()
 
 
+def _dup_rows_script(eng, P, C, spec, seed):
+    """Fetch calls where every (partition, consumer) appears eight times with different max values
+    (allowed: none commits); then each consumer moves to the end of one of its slices and reads on."""
+    g = np.random.default_rng(seed)
+    for b in range(3):
+        bt = make_batch(spec, b)
+        eng.append(bt.pidx, bt.lens, bt.payload)
+    pc = np.repeat(np.arange(P, dtype=np.uint32), C), np.tile(np.arange(C, dtype=np.uint32), P)
+    eng.commit_consumer_offset(pc[0], pc[1], g.integers(0, 50, P * C).astype(np.uint64))
+    out = []
+    for k in range(12):
+        pidx, cons = np.tile(pc[0], 8), np.tile(pc[1], 8)
+        mx = g.integers(1, 40, pidx.size).astype(np.uint32)
+        rc, res, buf, used = eng.fetch(pidx, cons, mx, out_cap=1 << 23)
+        out.append((rc, res.copy(), bytes(buf[:used])))
+        pick = g.integers(0, 8, P * C) * (P * C) + np.arange(P * C)
+        nxt = res["start_offset"][pick] + res["count"][pick]
+        eng.commit_consumer_offset(pc[0], pc[1], nxt.astype(np.uint64))
+    return out
+
+
+def test_position_cache_duplicate_rows(oracle_mod):
+    """requests of one (partition, consumer) in one call each leave a position-cache
+    entry; the entry is one 16-byte store, so the next call, reading on from one of the slices,
+    walks from a true {offset, position} pair. Every result equals the oracle's (no cache)."""
+    P, C = 16, 2
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 20, index_interval=256,
+                       max_consumers=C, max_batch_records=4096)
+    spec = StreamSpec(P, 3000, "uniform", size=(1, 300), config_index=57)
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        got, want = _dup_rows_script(dev, P, C, spec, 57), _dup_rows_script(ora, P, C, spec, 57)
+        for k, (gw, ww) in enumerate(zip(got, want)):
+            assert gw[0] == ww[0], k
+            for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                assert np.array_equal(gw[1][f], ww[1][f]), (k, f)
+            assert gw[2] == ww[2], k
+        assert all((x[1]["count"] > 0).any() for x in got)
+
+
 def test_device_rows_match_host_rows():
     """RMQ_FETCH_DEVICE_ROWS (ABI 9): request and result rows in device memory give the results of
     the same requests from host rows; their flags word is ignored (a read-and-commit flag commits

@@ -16,7 +16,10 @@ RCCL) and on per-rank oracles (tests/repl_sim.py rounds). Steps:
   ("state", ranks)                  every partition state of those ranks is recorded
   ("elect", [(candidate, gid, term)])  Raft elections: the candidate's (last_log_term, log end) of
         global partition gid go as a vote request to every replica of gid in the current placement
-        (the candidate first); every rank records its votes [(gid, candidate, granted)]
+        (the candidate first); every rank records its votes [(gid, candidate, granted)]; with durable
+        tiers a granted vote is saved (DurableLog.save_vote) before it counts
+  ("spill", ranks)                  DurableLog.spill of those ranks' tiers (records moved)
+  ("tier_read", {rank: (gid, off, max)})  records [off, off + max) of gid from that rank's tier files
 
 run_oracle / run_gpu return the recorded outcomes per step and rank, so a test compares them and
 then every rank's state, rings, index and consumer offsets.
@@ -52,8 +55,16 @@ def _voters(view, gid, cand):
     return [cand] + [r for r in ranks if r != cand]
 
 
-def run_oracle(oras, views0, script):
+def _vote(eng, tier, p, term, cand, lt, leo):
+    g = bool(eng.vote(p, term, cand, lt, leo))
+    if g and tier is not None:
+        tier.save_vote(p, term, cand)  # durable before the grant is answered (raft_meta votedFor)
+    return g
+
+
+def run_oracle(oras, views0, script, tiers=None):
     world = len(oras)
+    tiers = tiers or [None] * world
     for r in range(world):
         place(oras[r], views0[r], world)
     views = list(views0)
@@ -99,16 +110,24 @@ def run_oracle(oras, views0, script):
             for cand, gid, term in step[1]:
                 st = oras[cand].state(_local(views[cand], gid))
                 for v in _voters(views[cand], gid, cand):
-                    g = oras[v].vote(_local(views[v], gid), term, cand, st["last_log_term"], st["log_end_offset"])
-                    rec[v].append((gid, cand, bool(g)))
+                    g = _vote(oras[v], tiers[v], _local(views[v], gid), term, cand, st["last_log_term"],
+                              st["log_end_offset"])
+                    rec[v].append((gid, cand, g))
+        elif kind == "spill":
+            for r in step[1]:
+                rec[r] = tiers[r].spill()
+        elif kind == "tier_read":
+            for r, (gid, off, mx) in step[1].items():
+                rec[r] = tiers[r].read_images(_local(views[r], gid), off, mx)
         else:
             raise ValueError(kind)
         out.append(rec)
     return out
 
 
-def run_gpu(engs, hub, views0, script, timeout=240):
+def run_gpu(engs, hub, views0, script, timeout=240, tiers=None):
     world = len(engs)
+    tiers = tiers or [None] * world
     out = [[None] * world for _ in script]
     errs = [None] * world
     bar = threading.Barrier(world, timeout=timeout)
@@ -176,9 +195,16 @@ def run_gpu(engs, hub, views0, script, timeout=240):
                         lt, leo = shared[(k, gid, cand)]
                         for v in _voters(views[cand], gid, cand):
                             if v == r:
-                                g = e.vote(_local(views[r], gid), term, cand, lt, leo)
-                                out[k][r].append((gid, cand, bool(g)))
+                                g = _vote(e, tiers[r], _local(views[r], gid), term, cand, lt, leo)
+                                out[k][r].append((gid, cand, g))
                             bar.wait()
+                elif kind == "spill":
+                    if r in step[1]:
+                        out[k][r] = tiers[r].spill()
+                elif kind == "tier_read":
+                    if r in step[1]:
+                        gid, off, mx = step[1][r]
+                        out[k][r] = tiers[r].read_images(_local(views[r], gid), off, mx)
         except BaseException as ex:  # noqa: BLE001 - reported below
             errs[r] = ex
             bar.abort()
@@ -221,5 +247,5 @@ def compare_outcomes(script, got, want):
                 assert g[0] == w[0] and np.array_equal(g[1], w[1]), (k, r, g, w)
             elif step[0] == "poll" and w is not None:
                 assert g == w, (k, r, g, w)
-            elif step[0] in ("silent", "elect", "state") and w is not None:
+            elif step[0] in ("silent", "elect", "state", "spill", "tier_read") and w is not None:
                 assert g == w, (k, step[0], r, g, w)

@@ -1,5 +1,6 @@
 # Counters of the split pipeline's launches (diagnostic; RMQ_SPLIT=2: apply and rank launches one
-# after the other, so each dispatch is one role set). Run through gpurun:
+# after the other, so each dispatch is one role set; SPLIT=0 keeps the one launch, e.g. with
+# RMQ_S3_ROLES). Run through gpurun:
 #   bash tools/pmc_apply.sh <tag> [sq|mem]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; R=$GRAFT_REPO_ROOT
@@ -17,5 +18,5 @@ fi
 k=0
 for set in "${SETS[@]}"; do
   k=$((k+1))
-  (cd /tmp && export TMPDIR=/tmp && RMQ_SPLIT=2 timeout -s KILL 90 rocprofv3 --pmc $set -f csv -d "$R/gpurun_out/${T}_pmc$k" -o pm -- python3 "$R/bench.py" --steps 60 --warmup 10 $Q) > "$R/gpurun_out/${T}_pmc$k.log" 2>&1 || { echo "pass $k failed"; tail -5 "$R/gpurun_out/${T}_pmc$k.log"; }
+  (cd /tmp && export TMPDIR=/tmp && RMQ_SPLIT=${SPLIT:-2} timeout -s KILL 90 rocprofv3 --pmc $set -f csv -d "$R/gpurun_out/${T}_pmc$k" -o pm -- python3 "$R/bench.py" --steps 60 --warmup 10 $Q) > "$R/gpurun_out/${T}_pmc$k.log" 2>&1 || { echo "pass $k failed"; tail -5 "$R/gpurun_out/${T}_pmc$k.log"; }
 done
