@@ -109,6 +109,17 @@ int check_err(rmq_engine* e) {
   return q == hipSuccess || q == hipErrorNotReady ? RMQ_OK : hip_fail(q);
 }
 
+int fetch_flush(rmq_engine* e);
+// The engine lock of every call: held-back asynchronous fetches go to the pipeline stream first, so
+// whatever the call issues is ordered after them (their contract); a launch error stays sticky on the
+// stream and surfaces at the next check.
+struct EngineLock {
+  std::lock_guard<std::mutex> g;
+  explicit EngineLock(rmq_engine* e) : g(e->mu) {
+    if (!e->fpend.empty() && hipSetDevice(e->device) == hipSuccess) (void)fetch_flush(e);
+  }
+};
+
 // Wait for everything issued on stream s. A blocking hipStreamSynchronize returns ~10 us after the
 // last kernel ends (interrupt wake-up); a sync sits on the producer's path (rmq_sync, a poll that
 // needs commit indices), so poll the stream for up to 20 ms first, then block.
@@ -252,6 +263,7 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     a.s3_lead = e->s3_first ? std::min<uint32_t>(a.wg3, e->s3_lead ? e->s3_lead : a.wg3) : 0u;
     // (only with every stage-3 workgroup first: then its block index is its stage-3 index)
     a.s3_xcd = e->s3_xcd && a.s3_lead == a.wg3 && !a.s3_pair ? 1u : 0u;
+    a.s3_stage = e->s3_stage;
   }
   a.launch_seq = ++e->launch_seq;
   e->st.csnap_slot = (uint32_t)(a.launch_seq & 1ull);  // control kernels after this launch write its slot
@@ -415,6 +427,27 @@ int late_retention(rmq_engine* e) {
   return RMQ_OK;
 }
 
+// The asynchronous fetches held back (fetch_issue) as ONE resolve + gather pair (kFetchBatch tickets
+// at most), each ticket's completion event after it. Called (under mu) by the next fetch that cannot
+// join them, by every other call that takes the engine lock (EngineLock: whatever it issues on the
+// pipeline stream stays ordered after the fetches issued before it), and by a poll of a held ticket.
+int fetch_flush(rmq_engine* e) {
+  if (e->fpend.empty()) return RMQ_OK;
+  int rc = late_retention(e);
+  if (rc) return rc;
+  FetchArgs t[kFetchBatch];
+  uint32_t nt = 0;
+  for (uint32_t i : e->fpend) t[nt++] = e->fslot[i].args;
+  launch_fetch_batch(t, nt, e->main_s);
+  HIP_TRY(hipGetLastError());
+  for (uint32_t i : e->fpend) {
+    HIP_TRY(hipEventRecord(e->fslot[i].ev, e->main_s));
+    e->fslot[i].pending = false;
+  }
+  e->fpend.clear();
+  return RMQ_OK;
+}
+
 // Wait for everything issued on the pipeline stream, without flushing batches that are still
 // forming or in the pipeline's earlier stages (reads of committed state, consumer commits).
 int quiesce(rmq_engine* e) {
@@ -539,6 +572,7 @@ void free_engine(rmq_engine* e) {
   if (e->main_s) {
     // every submitted batch is applied before the memory goes away; with a replication transport
     // a flush is collective, so the application must have called rmq_sync on every rank
+    (void)fetch_flush(e);
     if (!e->repl) flush(e);
     hipStreamSynchronize(e->main_s);
     if (e->rank_s) hipStreamSynchronize(e->rank_s);
@@ -717,6 +751,8 @@ int rmq_create(const rmq_config* cfg, rmq_engine** out) {
   if (const char* v = std::getenv("RMQ_SPLIT")) e->split = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_PAIR")) e->s3_pair = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_ROLES")) e->s3_roles = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_S3_STAGE")) e->s3_stage = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("RMQ_FETCH_COALESCE")) e->fetch_coalesce = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S3_XCD")) e->s3_xcd = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_S1_XCD")) e->s1_xcd = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("RMQ_RANK_CUS")) e->rank_cus = (uint32_t)std::atoi(v);
@@ -953,7 +989,7 @@ int set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_
 
 int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* ranks, uint32_t rf, uint32_t leader_slot) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
   if (!ranks || rf != e->cfg.replication_factor || leader_slot >= rf) return RMQ_EINVAL;
   return set_placement(e, 1, &pidx, nullptr, ranks, &leader_slot);
@@ -962,13 +998,13 @@ int rmq_set_replicas(rmq_engine* e, uint32_t pidx, const uint32_t* ranks, uint32
 int rmq_set_placement(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* key, const uint32_t* ranks,
                       const uint32_t* leader_slot) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   return set_placement(e, n, pidx, key, ranks, leader_slot);
 }
 
 int rmq_become_leader(rmq_engine* e, uint32_t pidx, uint64_t term) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
   if (pidx != RMQ_ALL_PARTITIONS && pidx >= P) return RMQ_ENOPART;
   const uint32_t lo = pidx == RMQ_ALL_PARTITIONS ? 0 : pidx, hi = pidx == RMQ_ALL_PARTITIONS ? P : pidx + 1;
@@ -1046,7 +1082,7 @@ int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, ui
              uint64_t cand_log_end, uint32_t* granted) {
   if (!e || !granted) return RMQ_EINVAL;
   *granted = 0;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
   int rc = vote_settle(e);
@@ -1088,7 +1124,7 @@ int rmq_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t candidate, ui
 
 int rmq_set_vote(rmq_engine* e, uint32_t pidx, uint64_t term, uint32_t voted_for) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (pidx >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
   int rc = vote_settle(e);
@@ -1109,7 +1145,7 @@ int rmq_leader_silent(rmq_engine* e, uint32_t silent_rounds, uint32_t timeout_ms
                       uint32_t* n) {
   if (!e || !n || (cap && !out_pidx)) return RMQ_EINVAL;
   *n = 0;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
   HIP_TRY(hipSetDevice(e->device));
   if (e->repl) HIP_TRY(hipStreamSynchronize(e->repl->xchg_s));  // (the rounds' ingest writes the words)
@@ -1139,7 +1175,7 @@ int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint
   if (!n) return RMQ_OK;
   if (!pidx || !seg) return RMQ_EINVAL;
   std::lock_guard<std::mutex> fg(e->fetch_mu);  // no fetch reads a ring while it moves
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   const uint32_t P = e->cfg.num_partitions, ilog = e->st.interval_log2;
   std::vector<uint8_t> seen(P, 0);
   for (uint32_t i = 0; i < n; ++i) {
@@ -1218,7 +1254,7 @@ int rmq_set_segments(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint
 
 int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_t* ticket) {
   if (!e || !b || !ticket) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   const uint32_t n = b->n;
   if (n > e->cfg.max_batch_records) return RMQ_ENOSPC;
   if (b->payload_bytes > e->cfg.max_batch_bytes) return RMQ_ENOSPC;
@@ -1327,7 +1363,7 @@ int rmq_append(rmq_engine* e, const rmq_batch* b, uint64_t* out_offsets, uint64_
 
 int rmq_ack(rmq_engine* e, const uint32_t* pidx, const uint32_t* slot, const uint64_t* match, uint32_t n) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (!n) return RMQ_OK;
   if (!pidx || !slot || !match) return RMQ_EINVAL;
   for (uint32_t i = 0; i < n; ++i) {
@@ -1376,7 +1412,7 @@ int poll_offsets(rmq_engine* e, uint64_t ticket) {
 
 int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64_t* hw_out) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (ticket & RMQ_TICKET_OFFSETS) {
     HIP_TRY(hipSetDevice(e->device));
     return poll_offsets(e, ticket);
@@ -1406,7 +1442,7 @@ int rmq_poll_commit(rmq_engine* e, uint64_t ticket, uint64_t* commit_out, uint64
 
 int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out) {
   if (!e || !out) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (!ticket || ticket > e->last_ticket || e->last_ticket - ticket >= kStatsRing) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = wait_ticket(e, ticket);
@@ -1431,14 +1467,14 @@ int rmq_ticket_stats(rmq_engine* e, uint64_t ticket, rmq_append_stats* out) {
 
 int rmq_sync(rmq_engine* e) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   HIP_TRY(hipSetDevice(e->device));
   return drain(e);
 }
 
 int rmq_set_replica_cursor(rmq_engine* e, uint32_t n, const uint32_t* pidx, const uint64_t* offset) {
   if (!e || (n && (!pidx || !offset))) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   const uint32_t P = e->cfg.num_partitions;
   for (uint32_t i = 0; i < n; ++i)
     if (pidx[i] >= P) return RMQ_ENOPART;
@@ -1456,7 +1492,7 @@ int rmq_set_replica_cursor(rmq_engine* e, uint32_t n, const uint32_t* pidx, cons
 int rmq_commit_consumer_offset(rmq_engine* e, const uint32_t* pidx, const uint32_t* consumer,
                                const uint64_t* offset, uint32_t n, int32_t* status, uint64_t* ticket) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (ticket) *ticket = 0;
   if (!n) return RMQ_OK;
   if (!pidx || !consumer || !offset) return RMQ_EINVAL;
@@ -1615,6 +1651,13 @@ int fetch_slot_reserve(rmq_engine::FetchSlot& f, uint32_t n, uint64_t stage, hip
 // (wait: block instead); else its result, with the caller's res (and host output) filled and the
 // slot idle again.
 int fetch_slot_step(rmq_engine* e, rmq_engine::FetchSlot& f, bool wait, uint64_t* bytes_used) {
+  if (f.phase == 1) {
+    std::lock_guard<std::mutex> g(e->mu);  // a held-back ticket is launched (with the others held) when polled
+    if (f.pending) {
+      const int rc = fetch_flush(e);
+      if (rc) return rc;
+    }
+  }
   if (f.phase == 1) {
     if (wait) {
       const int rc = event_wait(f.ev);
@@ -1780,10 +1823,20 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     // Order against the append pipeline without flushing it: on the pipeline's stream, after the
     // last launch issued so far and before the next, so no ring bytes or log starts it reads change
     // under it.
-    std::lock_guard<std::mutex> g(e->mu);
+    std::lock_guard<std::mutex> g(e->mu);  // (not EngineLock: this decides about the held-back fetches)
+    // an asynchronous fetch that commits nothing waits to go with the next ones (up to kFetchBatch
+    // tickets in one resolve + gather pair: the requests of different tickets never depend on one
+    // another); anything else launches the held ones first, then itself
+    const bool hold = !sync && !any && !dma && !e->profile && e->fetch_coalesce > 1;
+    if (!hold) {
+      rc = fetch_flush(e);
+      if (rc) return rc;
+    }
     if (dma_in) HIP_TRY(hipStreamWaitEvent(e->main_s, f.ev_in, 0));
-    rc = late_retention(e);  // (the log starts the fetch reads: every batch applied so far retained)
-    if (rc) return rc;
+    if (!hold) {
+      rc = late_retention(e);  // (the log starts the fetch reads: every batch applied so far retained)
+      if (rc) return rc;
+    }
     FetchArgs a{};
     a.st = e->st;
     a.req = static_cast<const uint32_t*>(d_rq);
@@ -1799,10 +1852,23 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
     a.n = n;
     a.commits = any ? 1u : 0u;
     a.replica = replica ? 1u : 0u;
+    if (hold) {
+      const size_t half = (size_t)f.csum_lines * kCsumStride;
+      a.csum = f.d_csum + half * f.csum_par;
+      a.csum_next = f.d_csum + half * (f.csum_par ^ 1u);
+      f.csum_par ^= 1u;
+      f.args = a;
+      f.pending = true;
+      e->fpend.push_back(e->fslot_next);
+      if (e->fpend.size() >= std::min<uint32_t>(kFetchBatch, e->fetch_coalesce)) {
+        rc = fetch_flush(e);
+        if (rc) return rc;
+      }
+    }
     hipEvent_t ev[4] = {}, r0 = nullptr, r1 = nullptr;
     // (profiling replays a fetch's kernels back to back; a committing fetch runs once: each run
     // would commit again and the next would read from the committed offset)
-    const uint32_t runs = e->profile && !any ? e->fetch_replay : 1u;
+    const uint32_t runs = hold ? 0u : e->profile && !any ? e->fetch_replay : 1u;
     // (a committing fetch records no dispatch spans: the events the kernels' own dispatches record
     // were measured to hold the second kernel ~10 us behind the first, which its one run would carry)
     const bool spans = e->profile && !any;
@@ -1826,7 +1892,9 @@ int fetch_issue(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t m
       HIP_TRY(hipGetLastError());
     }
     if (e->profile) HIP_TRY(hipEventRecord(r1, e->main_s));
-    if (dma) {  // the result rows to the host behind the kernels, off the pipeline stream
+    if (hold) {
+      // (the completion event: recorded when fetch_flush launches the kernels)
+    } else if (dma) {  // the result rows to the host behind the kernels, off the pipeline stream
       HIP_TRY(hipEventRecord(f.ev_k, e->main_s));
       HIP_TRY(hipStreamWaitEvent(e->fetch_out_s, f.ev_k, 0));
       HIP_TRY(hipMemcpyAsync(h_rs, f.d_res, (size_t)n * sizeof(rmq_fetch_res), hipMemcpyDeviceToHost, e->fetch_out_s));
@@ -1889,7 +1957,7 @@ int rmq_fetch(rmq_engine* e, const rmq_fetch_req* reqs, uint32_t n, uint32_t mem
 
 int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
   if (!e || !o) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
   int rc = quiesce(e);
@@ -1923,7 +1991,7 @@ int rmq_get_partition_state(rmq_engine* e, uint32_t p, rmq_partition_state* o) {
 
 int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_partition_state* o) {
   if (!e || (n && !o)) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   const uint32_t P = e->cfg.num_partitions, RF = e->cfg.replication_factor;
   if (first > P || n > P - first) return RMQ_ENOPART;
   if (!n) return RMQ_OK;
@@ -1983,7 +2051,7 @@ int rmq_get_partition_states(rmq_engine* e, uint32_t first, uint32_t n, rmq_part
 
 int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t p, uint64_t ring_off, uint64_t len, uint8_t* out) {
   if (!e || (len && !out)) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   const RingRef rg = ring_ref(e->ring[p], e->st.interval_log2, e->st.icap_mul);
   if (replica >= e->cfg.replication_factor || ring_off > rg.seg || len > rg.seg - ring_off) return RMQ_EINVAL;
@@ -1998,7 +2066,7 @@ int rmq_read_segment(rmq_engine* e, uint32_t replica, uint32_t p, uint64_t ring_
 
 int rmq_read_index(rmq_engine* e, uint32_t p, uint64_t m_first, uint64_t count, uint64_t* out) {
   if (!e || (count && !out)) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   const RingRef rg = ring_ref(e->ring[p], e->st.interval_log2, e->st.icap_mul);
   const uint32_t icap = rg.icap;
@@ -2018,7 +2086,7 @@ int rmq_read_index(rmq_engine* e, uint32_t p, uint64_t m_first, uint64_t count, 
 
 int rmq_read_consumer_offsets(rmq_engine* e, uint32_t p, uint64_t* out) {
   if (!e || !out) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (p >= e->cfg.num_partitions) return RMQ_ENOPART;
   HIP_TRY(hipSetDevice(e->device));
   int rc = quiesce(e);
@@ -2030,7 +2098,7 @@ int rmq_read_consumer_offsets(rmq_engine* e, uint32_t p, uint64_t* out) {
 
 int rmq_read_consumer_table(rmq_engine* e, uint32_t first, uint32_t n, uint64_t* out) {
   if (!e || (n && !out)) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (first > e->cfg.num_partitions || n > e->cfg.num_partitions - first) return RMQ_ENOPART;
   if (!n) return RMQ_OK;
   HIP_TRY(hipSetDevice(e->device));
@@ -2043,7 +2111,7 @@ int rmq_read_consumer_table(rmq_engine* e, uint32_t first, uint32_t n, uint64_t*
 
 int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out) {
   if (!e || !out) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   HIP_TRY(hipSetDevice(e->device));
   *out = nullptr;
   HIP_TRY(hipMalloc(out, bytes ? bytes : 1));
@@ -2052,7 +2120,7 @@ int rmq_device_alloc(rmq_engine* e, uint64_t bytes, void** out) {
 
 int rmq_device_free(rmq_engine* e, void* p) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   HIP_TRY(hipSetDevice(e->device));
   int rc = settle(e);
   if (rc) return rc;
@@ -2062,7 +2130,7 @@ int rmq_device_free(rmq_engine* e, void* p) {
 
 int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int kind) {
   if (!e || (bytes && (!dst || !src))) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   HIP_TRY(hipSetDevice(e->device));
   const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice
                         : kind == 1 ? hipMemcpyDeviceToHost
@@ -2075,7 +2143,7 @@ int rmq_memcpy(rmq_engine* e, void* dst, const void* src, uint64_t bytes, int ki
 
 int rmq_profile_enable(rmq_engine* e, int enable) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   HIP_TRY(hipSetDevice(e->device));
   int rc = settle(e);
   if (rc) return rc;
@@ -2099,7 +2167,7 @@ int rmq_profile_enable(rmq_engine* e, int enable) {
 
 int rmq_profile_query(rmq_engine* e, int kernel, uint64_t* launches, double* total_ms) {
   if (!e || kernel < 0 || kernel > 4) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   HIP_TRY(hipSetDevice(e->device));
   int rc = settle(e);
   if (rc) return rc;
@@ -2135,7 +2203,7 @@ int rmq_rccl_unique_id(uint8_t* out) {
 
 int rmq_attach_rccl(rmq_engine* e, const uint8_t* comm_id, uint32_t world) {
   if (!e || !comm_id || world < 2 || world > kMaxWorld) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (e->repl) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
@@ -2162,7 +2230,7 @@ void rmq_local_hub_destroy(rmq_local_hub* h) { delete h; }
 
 int rmq_attach_local(rmq_engine* e, rmq_local_hub* h) {
   if (!e || !h) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (e->repl) return RMQ_EINVAL;
   HIP_TRY(hipSetDevice(e->device));
   int rc = drain(e);
@@ -2175,7 +2243,7 @@ int rmq_attach_local(rmq_engine* e, rmq_local_hub* h) {
 
 int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
   if (!e || !out) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   std::memset(out, 0, sizeof *out);
   if (!e->repl) return RMQ_OK;
   const Replication* r = e->repl;
@@ -2204,7 +2272,7 @@ int rmq_replication_stats(rmq_engine* e, rmq_repl_stats* out) {
 
 int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (!e->repl) return RMQ_EINVAL;
   e->repl->drop_from = e->last_ticket + 1;
   e->repl->drop_n = n;
@@ -2214,14 +2282,14 @@ int rmq_fault_drop_rounds(rmq_engine* e, uint32_t n) {
 int rmq_fault_cut(rmq_engine* e, uint32_t dst, uint32_t n) {
   int rc = rmq_fault_isolate(e, dst, n);
   if (rc) return rc;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   e->repl->cut_notice |= 1u << dst;
   return RMQ_OK;
 }
 
 int rmq_fault_isolate(rmq_engine* e, uint32_t dst, uint32_t n) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (!e->repl || dst >= e->repl->world || dst == e->repl->rank) return RMQ_EINVAL;
   e->repl->iso_from[dst] = e->last_ticket + 1;
   e->repl->iso_n[dst] = n;
@@ -2230,7 +2298,7 @@ int rmq_fault_isolate(rmq_engine* e, uint32_t dst, uint32_t n) {
 
 int rmq_fault_corrupt(rmq_engine* e, uint32_t dst, int64_t at) {
   if (!e) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   if (!e->repl || dst >= e->repl->world || dst == e->repl->rank) return RMQ_EINVAL;
   e->repl->flip[dst] = true;
   e->repl->flip_at[dst] = at;
@@ -2239,7 +2307,7 @@ int rmq_fault_corrupt(rmq_engine* e, uint32_t dst, int64_t at) {
 
 int rmq_read_outbox(rmq_engine* e, uint32_t dst, uint8_t* out, uint64_t cap, uint64_t* size) {
   if (!e || !size) return RMQ_EINVAL;
-  std::lock_guard<std::mutex> g(e->mu);
+  EngineLock g(e);
   *size = 0;
   Replication* r = e->repl;
   if (!r || dst >= r->world) return RMQ_EINVAL;

@@ -253,16 +253,31 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, const ui
   return Resolved{start, count, need ? pend - pos0 : 0ull, pos0, (ring_off << 6) | (desc & 63ull), status};
 }
 
-__global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
+// The ticket of workgroup b (wg0: first workgroup of each ticket) and b's index inside it; the
+// arguments are read in place from the kernarg segment (an indexed by-value copy could go to scratch).
+__device__ __forceinline__ const FetchArgs& ticket_of(const u32* wg0, u32& b) {
+  const FetchBatch& B = *(const FetchBatch*)__builtin_amdgcn_kernarg_segment_ptr();
+  u32 k = 0;
+#pragma unroll
+  for (u32 i = 1; i < kFetchBatch; ++i) k += (i < B.nt && b >= wg0[i]) ? 1u : 0u;
+  b -= wg0[k];
+  return B.t[k];
+}
+
+__global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchBatch batch) {
+  (void)batch;
+  const FetchBatch& B = *(const FetchBatch*)__builtin_amdgcn_kernarg_segment_ptr();
+  u32 bid = blockIdx.x;
+  const FetchArgs& a = ticket_of(B.rwg0, bid);
   const u32 lane = lane_id(), w = threadIdx.x >> 6;
-  const u32 r = (blockIdx.x * kRW + w) * kRPW + (lane >> 5);
+  const u32 r = (bid * kRW + w) * kRPW + (lane >> 5);
   const bool live = r < a.n;  // (no early return: the workgroup meets at barriers below)
   // the workgroup's request rows, read once by one load of consecutive 16-byte rows (host rows:
   // one PCIe read of 128 bytes instead of a 16-byte read per request), through LDS; the device
   // copy for the gather and the position cache
   __shared__ uint4 s_rq[kRW * kRPW];
   {
-    const u32 r0 = blockIdx.x * kRW * kRPW + threadIdx.x;
+    const u32 r0 = bid * kRW * kRPW + threadIdx.x;
     if (threadIdx.x < kRW * kRPW && r0 < a.n) {
       const uint4 x = *reinterpret_cast<const uint4*>(a.req + 4ull * r0);
       s_rq[threadIdx.x] = x;
@@ -297,7 +312,7 @@ __global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchArgs a) {
   if (threadIdx.x == 0) {
     u64 b = 0;
     for (u32 k = 0; k < kRW; ++k) b += s_b[k];
-    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(blockIdx.x * kRW * kRPW / kFetchChunk) * kCsumStride], (unsigned long long)b);
+    if (b) atomicAdd((unsigned long long*)&a.csum[(u64)(bid * kRW * kRPW / kFetchChunk) * kCsumStride], (unsigned long long)b);
   }
 }
 
@@ -312,19 +327,24 @@ constexpr u32 kGR = kFW * kGQ;  // requests per gather workgroup
 // Placement + gather: workgroup per kGR consecutive requests. Two rounds of loads: the wave's
 // request words with the placement sums, then (requests of at most 128 pieces) the records' pieces,
 // issued before the placement barriers; only the stores wait for the output positions.
-__global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchArgs a) {
+__global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchBatch batch) {
+  (void)batch;
+  const FetchBatch& B = *(const FetchBatch*)__builtin_amdgcn_kernarg_segment_ptr();
+  u32 bid = blockIdx.x;
+  const FetchArgs& a = ticket_of(B.gwg0, bid);
+  const u32 nwg = (a.n + kGR - 1) / kGR;  // the ticket's gather workgroups
   __shared__ u64 s_red[kFW];
   __shared__ u64 s_pos[kGR];
   const DevState& st = a.st;
   const u32 tid = threadIdx.x, lane = lane_id(), w = tid >> 6;
-  const u32 r0 = blockIdx.x * kGR, c0 = r0 / kFetchChunk;
+  const u32 r0 = bid * kGR, c0 = r0 / kFetchChunk;
   // the wave's kGQ requests (lanes 0..kGQ-1 read one each)
   const u32 rq = r0 + w * kGQ + (lane < kGQ ? lane : 0u);
   const bool qv = lane < kGQ && rq < a.n;
   const u64 q_pos = qv ? a.aux[2 * rq + 0] : 0ull, q_ring = qv ? a.aux[2 * rq + 1] : 0ull;
   const u64 q_nb = qv ? a.cpre[rq] : 0ull;
   // the next fetch's chunk sums (its resolve runs after this kernel on the same stream)
-  for (u32 k = blockIdx.x * 64 * kFW + tid; k < a.csum_lines; k += gridDim.x * 64 * kFW) a.csum_next[(u64)k * kCsumStride] = 0;
+  for (u32 k = bid * 64 * kFW + tid; k < a.csum_lines; k += nwg * 64 * kFW) a.csum_next[(u64)k * kCsumStride] = 0;
   // bytes of every request before r0: the chunk sums before its chunk, then its chunk's requests
   u64 v = 0;
   for (u32 k = tid; k < c0; k += 64 * kFW) v += a.csum[(u64)k * kCsumStride];
@@ -456,13 +476,33 @@ void preload_fetch_kernels() {
   (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel));
 }
 
+static void launch_batch(const FetchBatch& b, hipStream_t s, const hipEvent_t* e) {
+  if (!b.rwg0[b.nt]) return;
+  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3(b.rwg0[b.nt]), dim3(64 * kRW), 0, s, e ? e[0] : nullptr,
+                        e ? e[1] : nullptr, 0, b);
+  hipExtLaunchKernelGGL(fetch_gather_kernel, dim3(b.gwg0[b.nt]), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
+                        e ? e[3] : nullptr, 0, b);
+}
+
+void launch_fetch_batch(const FetchArgs* t, uint32_t nt, hipStream_t s) {
+  FetchBatch b{};
+  b.nt = nt;
+  for (uint32_t k = 0; k < nt; ++k) {
+    b.t[k] = t[k];
+    b.rwg0[k + 1] = b.rwg0[k] + (t[k].n + kRW * kRPW - 1) / (kRW * kRPW);
+    b.gwg0[k + 1] = b.gwg0[k] + (t[k].n + kGR - 1) / kGR;
+  }
+  launch_batch(b, s, nullptr);
+}
+
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev) {
   if (!a.n) return;
-  const hipEvent_t* e = ev;
-  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3((a.n + kRW * kRPW - 1) / (kRW * kRPW)), dim3(64 * kRW), 0, s, e ? e[0] : nullptr,
-                        e ? e[1] : nullptr, 0, a);
-  hipExtLaunchKernelGGL(fetch_gather_kernel, dim3((a.n + kGR - 1) / kGR), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
-                        e ? e[3] : nullptr, 0, a);
+  FetchBatch b{};
+  b.nt = 1;
+  b.t[0] = a;
+  b.rwg0[1] = (a.n + kRW * kRPW - 1) / (kRW * kRPW);
+  b.gwg0[1] = (a.n + kGR - 1) / kGR;
+  launch_batch(b, s, ev);
 }
 
 }  // namespace rmq

@@ -268,6 +268,7 @@ struct PipeArgs {
   uint32_t s3_lead;        // stage-3 workgroups placed before the other roles along blockIdx.x
   uint32_t s3_pair;        // stage-3 waves take two tasks each, their loads interleaved (task, task + wg3 waves)
   uint32_t s3_roles;       // stage 3 in loader / storer waves (RMQ_S3_ROLES): each workgroup a run of tasks
+  uint32_t s3_stage;       // stage 3 loads a packed task's payload span by coalesced loads through LDS (RMQ_S3_STAGE)
   uint32_t s3_xcd;         // stage-3 task order by XCD: the workgroups sharing an XCD take one contiguous task range
   uint32_t s1_xcd;         // stage-1 tile order by XCD (the same for the ranking workgroups)
   uint32_t debug;         // diagnostic only (RMQ_DEBUG, results invalid): 1 no payload ring
@@ -323,6 +324,16 @@ struct FetchArgs {
   uint32_t replica;          // the host checked RMQ_FETCH_REPLICA requests in the call (else flags ignored)
 };
 constexpr uint32_t kFetchChunk = 256;  // requests per chunk sum (placement)
+// Up to kFetchBatch asynchronous fetches (tickets) are launched as one resolve + gather pair: ticket k
+// owns the kernels' workgroups [wg0, wg0 + its own count) (no workgroup straddles two tickets), and
+// reads its own arguments, rows, scratch and output.
+constexpr uint32_t kFetchBatch = 4;
+struct FetchBatch {
+  FetchArgs t[kFetchBatch];
+  uint32_t rwg0[kFetchBatch + 1];  // first resolve workgroup of each ticket (then the total)
+  uint32_t gwg0[kFetchBatch + 1];  // first gather workgroup of each ticket
+  uint32_t nt;
+};
 constexpr uint32_t kFetchReplica = 2u;  // rmq_fetch_req.flags RMQ_FETCH_REPLICA
 constexpr uint32_t kCsumStride = 16;   // u64 words per chunk sum (128 bytes)
 
@@ -434,6 +445,7 @@ void launch_ack(const AckArgs& a, hipStream_t s);
 void launch_late_retention(const LateArgs& a, hipStream_t s);
 void launch_become_leader(const DevState& st, uint32_t pidx, hipStream_t s);
 void launch_fetch(const FetchArgs& a, hipStream_t s, const hipEvent_t* ev4);
+void launch_fetch_batch(const FetchArgs* t, uint32_t nt, hipStream_t s);  // nt <= kFetchBatch tickets, one pair
 void preload_fetch_kernels();
 
 void launch_consumer_commit(const ConsumerCommitArgs& a, hipStream_t s);

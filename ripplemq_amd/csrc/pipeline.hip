@@ -1414,8 +1414,19 @@ struct TaskState {
   u32 lm;          // local replica mask | kLead | kNoSpace
   u32 dead;        // leading pieces (0 = header) a later piece of the group overwrites
   u32 rel16, rk;   // replication: 16-byte units and records into the partition's group run
-  uint4 blk[kBL];
+  uint4 blk[kBL];  // the lane's first round of payload blocks, or (staged) blk[0..3] = the task's span
+  u32 nblk;        // staged: 16-byte blocks of the task's payload span from base `sbase` (wave-uniform;
+  u64 sbase;       //   0: not staged)
 };
+
+// A task's records are packed back to back in the batch payload (no payload_off: one tile, so one
+// contiguous span): the wave loads the span's 16-byte blocks with coalesced loads (lane l: blocks
+// l, l + 64, ...; about 2 L1->L2 requests per 128-byte record instead of one per 32 bytes a lane
+// pair loads), through its LDS image area, and each lane pair reads its record's blocks from there.
+constexpr u32 kSpanPer = 4;  // blocks per lane: spans of up to 4 KB (32 records of <= 112 B take 3.6 KB)
+#ifndef RMQ_SPAN_AUX
+#define RMQ_SPAN_AUX 2  // the span loads' cache policy: nt (read once per launch, like load_payload16)
+#endif
 
 // Record i of batch jb of the group in stage 3 (every lane: its own record, or its pair's).
 __device__ __forceinline__ TaskRec stage3_r1_at(const PipeArgs& A, u32 jb, u32 i) {
@@ -1505,14 +1516,42 @@ __device__ __forceinline__ void rec_place(const RecWords& W, const TaskRec& R, u
   lmo = W.lm | (W.lead ? kLead : 0u) | ((W.ex & kExclNoSpace) ? kNoSpace : 0u);
 }
 
-__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos& T, const TaskRec& R, bool cand) {
+__device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos& T, const TaskRec& R, bool cand,
+                                               bool stage = false) {
   TaskState S;
   S.pos = S.off = 0ull;
   S.lm = S.dead = S.rel16 = S.rk = 0u;
+  S.nblk = 0u;
+  S.sbase = 0ull;
   const RecWords W = rec_words(A, T.jb, task_rec(T), R.p, cand);
   S.rdesc = W.rdesc;
-  // first round of payload blocks, speculatively (leadership is checked before any store)
-  round_blocks(A, R, 0u, cand, S.blk);
+  // first round of payload blocks, speculatively (leadership is checked before any store): the
+  // task's whole span by coalesced loads when it is packed and fits, else the lane pair's blocks
+  const PipeBatch& b = A.g3.b[T.jb];
+  if (stage && !b.poff && T.i0 < b.n && !(A.debug & 4u)) {
+    const u32 last = 2u * (min(kTaskRecs, b.n - T.i0) - 1u);  // lane of the task's last record
+    const u64 s0 = readlane64(R.src, 0) & ~15ull;
+    const u64 e1 = readlane64(R.src, last) + readlane32(R.L, last);
+    const u64 nb = (e1 - s0 + 15ull) >> 4;
+    if (nb <= 64ull * kSpanPer) {
+      S.nblk = __builtin_amdgcn_readfirstlane((u32)nb);
+      S.sbase = ((u64)__builtin_amdgcn_readfirstlane((u32)(s0 >> 32)) << 32) | __builtin_amdgcn_readfirstlane((u32)s0);
+    }
+  }
+  if (S.nblk) {
+    // buffer loads through a descriptor of the span (bounds-checked: blocks past it read 0), one
+    // 32-bit offset for all four (the span base is wave-uniform)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(S.sbase), 0, (int)(16u * S.nblk), 0x00020000);
+    const u32 vo = 16u * (threadIdx.x & 63u);
+#pragma unroll
+    for (u32 u = 0; u < kSpanPer; ++u) {
+      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 1024u * u, 0, RMQ_SPAN_AUX);
+      S.blk[u] = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    S.blk[kBL - 1] = make_uint4(0, 0, 0, 0);
+  } else {
+    round_blocks(A, R, 0u, cand, S.blk);
+  }
   if (cand) rec_place(W, R, S.pos, S.off, S.dead, S.lm, S.rk, S.rel16);
   return S;
 }
@@ -1774,6 +1813,23 @@ __device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Sme
   uint4 blk[kBL];
 #pragma unroll
   for (u32 q = 0; q < kBL; ++q) blk[q] = Z.blk[q];
+  if (!XR && Z.nblk) {
+    // the task's payload span through the wave's image area: every lane's blocks in, then each
+    // lane pair's record blocks out (before any image write reuses the area)
+    uint4* sg = &W.img[w][0][0];
+    static_assert(sizeof(S.img[0]) >= 64u * kSpanPer * 16u, "a wave's image area holds the staged span");
+#pragma unroll
+    for (u32 u = 0; u < kSpanPer; ++u)
+      if (lane + 64u * u < Z.nblk) sg[lane + 64u * u] = Z.blk[u];
+    __builtin_amdgcn_wave_barrier();
+    const u32 b0 = (u32)(((R.src & ~15ull) - Z.sbase) >> 4) + j;
+#pragma unroll
+    for (u32 q = 0; q < kBL; ++q) {
+      const u32 k = b0 + 2u * q;
+      blk[q] = k < Z.nblk ? sg[k] : make_uint4(0, 0, 0, 0);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
   for (u32 c = 0; __any(c < nr); ++c) {
     if (c) round_blocks(A, R, c, c < nr, blk);
 #pragma unroll
@@ -2449,7 +2505,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];  // zk: large-record waves
   }
   bool cand = task < tasks && stage3_cand(A, T, R);
-  TaskState Z = stage3_r2(A, T, R, cand);
+  TaskState Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u);
   __syncthreads();
   PIPE_STAMP(1);
   while (task < tasks) {
@@ -2463,7 +2519,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
       T = task_pos(G, task);
       R = stage3_r1(A, T);
       cand = stage3_cand(A, T, R);
-      Z = stage3_r2(A, T, R, cand);
+      Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u);
     }
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -71,6 +71,75 @@ def test_async_fetch_matches_sync_while_appending():
         dev.sync()
 
 
+def test_coalesced_async_fetches(oracle_mod):
+    """Asynchronous fetches that commit nothing are held back and launched together, up to four
+    tickets in one resolve + gather pair (engine.cpp fetch_flush); a committing fetch, any other call,
+    a fifth ticket or a poll launches the held ones first. Every ticket's results, bytes and the
+    consumer table equal the oracle's, which runs the same calls one after the other."""
+    P, C = 64, 4
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 18, index_interval=256,
+                       max_consumers=C, max_batch_records=4096, pipeline_depth=2)
+    spec = StreamSpec(P, 3000, "zipf", size=(1, 300), config_index=58)
+    g = np.random.default_rng(58)
+    pp = np.arange(P, dtype=np.uint32)
+    # (kind, args): "f" async fetch (consumer, max, commit, device output), "a" append, "s" sync fetch
+    ops = [("a", 0), ("a", 1), ("f", (0, 10, False, True)), ("f", (1, 50, False, False)), ("f", (2, 1000, False, True)),
+           ("f", (3, 7, False, False)),                      # the fourth: the four go as one pair
+           ("f", (1, 20, False, True)), ("f", (2, 5, False, False)),
+           ("f", (1, 30, True, False)),                      # commits: the two held go first, then it
+           ("f", (1, 40, False, True)), ("f", (0, 9, False, False)), ("f", (3, 64, False, True)),
+           ("a", 2),                                          # an append launches the three held
+           ("f", (2, 11, True, True)), ("f", (0, 12, False, False)), ("f", (1, 13, False, False)),
+           ("s", (3, 100))]                                   # a synchronous fetch: held ones first
+    offs = g.integers(0, 200, P * C).astype(np.uint64)
+    with Engine(cfg) as dev, oracle_mod.OracleEngine(cfg) as ora:
+        for e in (dev, ora):
+            e.commit_consumer_offset(np.repeat(pp, C), np.tile(np.arange(C, dtype=np.uint32), P), offs)
+        want, got, held = [], [], []
+        for kind, x in ops:
+            if kind == "a":
+                b = make_batch(spec, x)
+                dev.append_async(b.pidx, b.lens, b.payload)
+                ora.append(b.pidx, b.lens, b.payload)
+                continue
+            c, mx = x[0], x[1]
+            commit = kind == "f" and x[2]
+            rc, res, buf, used = ora.fetch(pp, np.full(P, c, np.uint32), np.full(P, mx, np.uint32),
+                                           out_cap=4 << 20, commit=commit)
+            want.append((res.copy(), bytes(buf[:used])))
+            if kind == "s":
+                rc, res, buf, used = dev.fetch(pp, np.full(P, c, np.uint32), np.full(P, mx, np.uint32), out_cap=4 << 20)
+                got.append((res.copy(), bytes(buf[:used])))
+                continue
+            req = np.zeros((P, 4), np.uint32)
+            req[:, 3] = A.RMQ_FETCH_COMMIT if commit else 0
+            if x[3]:
+                d_out = dev.device_alloc(4 << 20)
+                tk = dev.fetch_async(pp, np.full(P, c, np.uint32), np.full(P, mx, np.uint32), d_out=d_out,
+                                     out_cap=4 << 20, req=req)
+            else:
+                d_out = None
+                tk = dev.fetch_async(pp, np.full(P, c, np.uint32), np.full(P, mx, np.uint32),
+                                     out=np.zeros(4 << 20, np.uint8), out_cap=4 << 20, req=req)
+            held.append((len(got), tk, d_out))
+            got.append(None)
+        for k, tk, d_out in held:
+            rc, res, used = dev.fetch_poll(tk, wait=True)
+            if d_out is None:
+                data = bytes(tk.out[:used])
+            else:
+                h = np.empty(used, np.uint8)
+                dev.d2h(h, d_out)
+                data = bytes(h)
+                dev.device_free(d_out)
+            got[k] = (res.copy(), data)
+        for k, ((gr, gb), (wr, wb)) in enumerate(zip(got, want)):
+            for f in ("status", "start_offset", "count", "bytes", "out_pos"):
+                assert np.array_equal(gr[f], wr[f]), (k, f)
+            assert gb == wb, k
+        assert np.array_equal(dev.consumer_table(), ora.consumer_table())
+
+
 def test_async_fetch_empty_and_unknown():
     cfg = EngineConfig(num_partitions=8, replication_factor=1, segment_bytes=1 << 16, index_interval=256,
                        max_consumers=1, max_batch_records=1024)

@@ -22,6 +22,11 @@
 #   legs       fetch / mixed / tier legs of a short line
 #   calls      host-side cost per fetch call (tools/fetch_calls.py)
 #   fetchkt    rocprofv3 kernel trace of the fetch leg (replayed kernels)
+#   envab:VAR=v[,CFG]  GPU tests with an environment knob, then three off/on pairs of lines
+#   group      launch-group size sweep;  Dprof  config D line, stamps and apply-launch trace
+#   roles      phase stamps of the role-split stage 3 and of the default launch
+#   sq / memc  SQ / memory-pipeline counters of the apply launches (tools/pmc_apply.sh)
+#   knob:VAR=v1,v2  steady and 20-step lines per value;  dbg:B1,B2  timing-only RMQ_DEBUG lines
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -109,6 +114,36 @@ for step in "$@"; do
     xstamps)  # phase stamps of one launch of the 2-rank rehearsal (transport kernel, 8 waves/workgroup)
       RMQ_STAMPS=gpurun_out/${T}_xst.csv RMQ_STAMPS_AT=60 run 300 "${T}_xstamped.json" python bench.py --gpus 2 --transport local --steps 200 --warmup 20 --segment-mb 2 --pool 8 $Q
       python tools/pipe_stamps.py "gpurun_out/${T}_xst.csv" > "gpurun_out/${T}_xstamps.txt" 2>&1 ;;
+    envab:*)  # envab:VAR=v[,CFG]: GPU tests with the knob set, then three pairs of 400- and 20-step lines off / on
+      kv=${step#envab:}; CF=B; case $kv in *,*) CF=${kv#*,}; kv=${kv%%,*};; esac
+      run 900 "${T}_envab_pytest.log" env "$kv" python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "parity or golden or pipelined or config or large or world8 or replication"
+      for k in 1 2 3; do
+        run 200 "${T}_envab_off_$k.json" python bench.py --config $CF --steps 400 --warmup 40 $Q
+        run 200 "${T}_envab_on_$k.json" env "$kv" python bench.py --config $CF --steps 400 --warmup 40 $Q
+        run 200 "${T}_envab_off20_$k.json" python bench.py --config $CF --steps 20 --warmup 5 $Q
+        run 200 "${T}_envab_on20_$k.json" env "$kv" python bench.py --config $CF --steps 20 --warmup 5 $Q
+      done
+      python3 tools/show_lines.py gpurun_out/${T}_envab_*.json ;;
+    group)  # launch-group size sweep (20- and 600-step lines, two rounds)
+      for k in 1 2; do
+        for g in 4 5 6 8; do
+          run 200 "${T}_g${g}_20_$k.json" python bench.py --steps 20 --warmup 8 --group $g $Q
+          run 200 "${T}_g${g}_600_$k.json" python bench.py --steps 600 --warmup 60 --group $g $Q
+        done
+      done ;;
+    Dprof)  # config D: a line, phase stamps of one launch, the apply launches' kernel trace
+      DQ="--config D --pool 16 --no-cpu-baseline --fetch-rounds 0 --concurrent-rounds 0 --host-steps 0 --tier-rounds 0"
+      run 200 "${T}_D.json" python bench.py --steps 400 --warmup 40 $DQ
+      RMQ_STAMPS=gpurun_out/${T}_Dst.csv RMQ_STAMPS_AT=60 run 200 "${T}_Dstamped.json" python bench.py --steps 200 --warmup 40 $DQ
+      python tools/pipe_stamps.py "gpurun_out/${T}_Dst.csv" > "gpurun_out/${T}_Dstamps.txt" 2>&1 || true
+      RMQ_SPLIT=2 prof 200 Dkt --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_Dkt" -o kt -- python3 "$R/bench.py" --steps 200 --warmup 20 $DQ ;;
+    roles)  # phase stamps of the role-split stage 3 (RMQ_S3_ROLES=4) and of the default launch
+      RMQ_S3_ROLES=4 RMQ_STAMPS=gpurun_out/${T}_rst.csv RMQ_STAMPS_AT=50 run 200 "${T}_rstamped.json" python bench.py --steps 300 --warmup 30 $Q
+      RMQ_STAMPS=gpurun_out/${T}_st0.csv RMQ_STAMPS_AT=50 run 200 "${T}_stamped0.json" python bench.py --steps 300 --warmup 30 $Q
+      python tools/roles_stamps.py "gpurun_out/${T}_rst.csv" > "gpurun_out/${T}_roles_stamps.txt" 2>&1
+      python tools/pipe_stamps.py "gpurun_out/${T}_st0.csv" >> "gpurun_out/${T}_roles_stamps.txt" 2>&1 ;;
+    sq|memc)  # SQ / memory-pipeline counters of the apply launches (tools/pmc_apply.sh)
+      bash tools/pmc_apply.sh "${T}_$step" $([ $step = sq ] && echo sq || echo mem) ;;
     *) echo "[gpu.sh] unknown step $step"; exit 2 ;;
   esac
 done
