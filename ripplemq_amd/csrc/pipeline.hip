@@ -1534,8 +1534,8 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
     const u64 e1 = readlane64(R.src, last) + readlane32(R.L, last);
     const u64 nb = (e1 - s0 + 15ull) >> 4;
     if (nb <= 64ull * kSpanPer) {
-      S.nblk = __builtin_amdgcn_readfirstlane((u32)nb);
-      S.sbase = ((u64)__builtin_amdgcn_readfirstlane((u32)(s0 >> 32)) << 32) | __builtin_amdgcn_readfirstlane((u32)s0);
+      S.nblk = (u32)nb;  // (s0, e1: read lanes, wave-uniform)
+      S.sbase = s0;
     }
   }
   if (S.nblk) {

@@ -97,9 +97,9 @@ def test_coalesced_async_fetches(oracle_mod):
             e.commit_consumer_offset(np.repeat(pp, C), np.tile(np.arange(C, dtype=np.uint32), P), offs)
         want, got, held = [], [], []
         for kind, x in ops:
-            if kind == "a":
+            if kind == "a":  # (applied before it returns, as the oracle's)
                 b = make_batch(spec, x)
-                dev.append_async(b.pidx, b.lens, b.payload)
+                dev.append(b.pidx, b.lens, b.payload)
                 ora.append(b.pidx, b.lens, b.payload)
                 continue
             c, mx = x[0], x[1]
@@ -224,7 +224,7 @@ def test_fetch_commit_matches_oracle(oracle_mod):
         # four): the call is refused whole, nothing committed
         table = dev.consumer_table().copy()
         d_out = dev.device_alloc(1 << 16)
-        for n, at, bit in ((7, 6, 2), (9, 0, 1 << 31), (16, 9, 4), (1, 0, 8)):
+        for n, at, bit in ((7, 6, 4), (9, 0, 1 << 31), (16, 9, 8), (1, 0, 16)):  # (2: RMQ_FETCH_REPLICA, ABI 10)
             req = np.zeros((n, 4), np.uint32)
             req[:, 0], req[:, 2], req[:, 3] = np.arange(n) % P, 5, A.RMQ_FETCH_COMMIT
             req[at, 3] |= bit

@@ -1,12 +1,12 @@
 # Counters of the split pipeline's launches (diagnostic; RMQ_SPLIT=2: apply and rank launches one
 # after the other, so each dispatch is one role set; SPLIT=0 keeps the one launch, e.g. with
-# RMQ_S3_ROLES). Run through gpurun:
+# RMQ_S3_ROLES; CFG=D: config D). Run through gpurun:
 #   bash tools/pmc_apply.sh <tag> [sq|mem]
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; R=$GRAFT_REPO_ROOT
 T=${1:-r05g}
 WHAT=${2:-sq}
-Q="--no-cpu-baseline --fetch-rounds 0 --concurrent-rounds 0 --host-steps 0 --tier-rounds 0"
+Q="${CFG:+--config $CFG --pool 16} --no-cpu-baseline --fetch-rounds 0 --concurrent-rounds 0 --host-steps 0 --tier-rounds 0"
 if [ "$WHAT" = sq ]; then
   SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
         "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR")
