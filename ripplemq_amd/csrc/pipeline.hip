@@ -1590,63 +1590,70 @@ __device__ __forceinline__ void big_round(u64 src, u32 L, u32 k0, u32 ph, uint4 
 // tools/replica_bench, 3.80 vs 4.71 TB/s).
 __device__ __forceinline__ u32 big_phase(u64 pos) { return (u32)((pos >> 4) + 1ull) & 7u; }
 
-// first / first_tail: round 0, loaded by the caller (while the record before was stored).
-__device__ __forceinline__ void big_record(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256], u64 src, u32 L, u64 pos,
-                           u64 off, u32 dead, uint8_t* ring, u64 segmask, u32 lm, const u64* xdst, u32 nx,
-                           const uint4 (&first)[kBU], uint4 first_tail) {
+// A large record's wave-uniform place (broadcast from the lane that resolved it).
+struct BigRec {
+  u64 src, pos, off, ring, segm;
+  u64 x[kMaxRemote];
+  u32 L, dead, lm, nx, ph, m;
+};
+
+// Round k0 of a large record, its blocks b0 / tail loaded: CRC fold into acc and the stores.
+__device__ __forceinline__ void big_store_round(const PipeArgs& A, const Stage3Smem& S, const u32 (*zk)[256],
+                                                const BigRec& R, u32 k0, const uint4 (&b0)[kBU], uint4 tail, u32& acc) {
   const u32 lane = threadIdx.x & 63, RF = A.st.RF;
   const u64 rstride = A.st.rstride;
-  const u32 m = (L + 15u) >> 4, sa = (u32)(src & 15u), ph = big_phase(pos);
-  u32 acc = 0;
-  for (u32 k0 = 0; 64u * k0 < m + ph; k0 += kBU) {
-    uint4 b0[kBU], tail;
-    if (k0 == 0) {
+  const u32 sa = (u32)(R.src & 15u);
+  uint8_t* ring = reinterpret_cast<uint8_t*>(R.ring);
 #pragma unroll
-      for (u32 u = 0; u < kBU; ++u) b0[u] = first[u];
-      tail = first_tail;
-    } else {
-      big_round(src, L, k0, ph, b0, tail);
+  for (u32 u = 0; u < kBU; ++u) {
+    const u32 jp = 64u * (k0 + u) + lane - R.ph;  // (wraps below 0: then past m, skipped)
+    uint4 b1;
+    b1.x = (u32)__shfl_down((int)b0[u].x, 1, 64);
+    b1.y = (u32)__shfl_down((int)b0[u].y, 1, 64);
+    b1.z = (u32)__shfl_down((int)b0[u].z, 1, 64);
+    b1.w = (u32)__shfl_down((int)b0[u].w, 1, 64);
+    if (lane == 63u) {
+      const u32 un = u + 1 < kBU ? u + 1 : u;  // unrolled: a constant
+      b1 = u + 1 < kBU ? make_uint4(readlane32(b0[un].x, 0), readlane32(b0[un].y, 0), readlane32(b0[un].z, 0),
+                                    readlane32(b0[un].w, 0))
+                       : tail;
     }
+    if (jp < R.m) {
+      const u32 nb = R.L - 16u * jp < 16u ? R.L - 16u * jp : 16u;
+      const uint4 v = extract_piece(b0[u], b1, sa, nb);
+      acc = crc_zshift(zk, acc) ^ piece_crc(A, S, v, jp);
+      uint8_t* dst = ring + ((R.pos + 16ull + 16ull * jp) & R.segm);
+      if (jp + 1u >= R.dead)
+        for (u32 r = 0; r < RF; ++r)
+          if ((R.lm >> r) & 1u) store_log16(dst + r * rstride, v);
 #pragma unroll
-    for (u32 u = 0; u < kBU; ++u) {
-      const u32 jp = 64u * (k0 + u) + lane - ph;  // (wraps below 0: then past m, skipped)
-      uint4 b1;
-      b1.x = (u32)__shfl_down((int)b0[u].x, 1, 64);
-      b1.y = (u32)__shfl_down((int)b0[u].y, 1, 64);
-      b1.z = (u32)__shfl_down((int)b0[u].z, 1, 64);
-      b1.w = (u32)__shfl_down((int)b0[u].w, 1, 64);
-      if (lane == 63u) {
-        const u32 un = u + 1 < kBU ? u + 1 : u;  // unrolled: a constant
-        b1 = u + 1 < kBU ? make_uint4(readlane32(b0[un].x, 0), readlane32(b0[un].y, 0), readlane32(b0[un].z, 0),
-                                      readlane32(b0[un].w, 0))
-                         : tail;
-      }
-      if (jp < m) {
-        const u32 nb = L - 16u * jp < 16u ? L - 16u * jp : 16u;
-        const uint4 v = extract_piece(b0[u], b1, sa, nb);
-        acc = crc_zshift(zk, acc) ^ piece_crc(A, S, v, jp);
-        uint8_t* dst = ring + ((pos + 16ull + 16ull * jp) & segmask);
-        if (jp + 1u >= dead)
-          for (u32 r = 0; r < RF; ++r)
-            if ((lm >> r) & 1u) store_log16(dst + r * rstride, v);
-        for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(xdst[q]) + 16ull + 16ull * jp, v);
-      }
+      for (u32 q = 0; q < kMaxRemote; ++q)
+        if (q < R.nx) store_log16(reinterpret_cast<uint8_t*>(R.x[q]) + 16ull + 16ull * jp, v);
     }
   }
-  // lane l's pieces are l - ph (mod 64) apart by 64; e pieces follow its last one in the record
-  if (((lane + 64u - ph) & 63u) < m) {
-    const u32 e = (m - 1u - lane + ph) & 63u;
+}
+
+// After a large record's last round: lane l's pieces are l - ph (mod 64) apart by 64 and e pieces
+// follow its last one, so its register is shifted past them; the wave XOR-reduces and lane 0
+// writes the header.
+__device__ __forceinline__ void big_close(const PipeArgs& A, const BigRec& R, u32 acc) {
+  const u32 lane = threadIdx.x & 63, RF = A.st.RF;
+  if (((lane + 64u - R.ph) & 63u) < R.m) {
+    const u32 e = (R.m - 1u - lane + R.ph) & 63u;
     if (e) acc = gf2_mulmod(acc, A.crc->sh16[e]);
   }
   acc = wave_xor_all(acc);
   if (lane == 0) {
-    const u32 pad = 16u * m - L;
+    const u32 pad = 16u * R.m - R.L;
     const u32 crc = ~(pad ? gf2_mulmod(A.crc->inv_pad[pad], acc) : acc);
-    const uint4 h = make_uint4((u32)off, (u32)(off >> 32), L, crc);
-    if (dead == 0u)
+    const uint4 h = make_uint4((u32)R.off, (u32)(R.off >> 32), R.L, crc);
+    uint8_t* ring = reinterpret_cast<uint8_t*>(R.ring);
+    if (R.dead == 0u)
       for (u32 r = 0; r < RF; ++r)
-        if ((lm >> r) & 1u) store_log16(ring + (pos & segmask) + r * rstride, h);
-    for (u32 q = 0; q < nx; ++q) store_log16(reinterpret_cast<uint8_t*>(xdst[q]), h);
+        if ((R.lm >> r) & 1u) store_log16(ring + (R.pos & R.segm) + r * A.st.rstride, h);
+#pragma unroll
+    for (u32 q = 0; q < kMaxRemote; ++q)
+      if (q < R.nx) store_log16(reinterpret_cast<uint8_t*>(R.x[q]), h);
   }
 }
 
@@ -1719,34 +1726,58 @@ __device__ __forceinline__ void stage3_big_waves(const PipeArgs& A, Stage3Smem& 
         }
       }
     }
-    // each record's first round of payload loads is issued before the record ahead of it is
-    // processed (a record of a few KB is one round: one load latency per record otherwise)
+    // the wave's (record, round) units in order, each unit's payload loads issued before the unit
+    // ahead of it is folded and stored: the next round of the same record, or the first round of
+    // the next one (one load latency per round otherwise, behind the previous round's stores)
     u64 bm = __ballot(ok);
-    uint4 nb[kBU], ntail = make_uint4(0, 0, 0, 0);
+    if (!bm) continue;
+    auto take = [&](u32 k) {
+      BigRec R;
+      R.src = bcast_u64(src, k);
+      R.pos = bcast_u64(pos, k);
+      R.off = bcast_u64(off, k);
+      R.ring = bcast_u64(ringb, k);
+      R.segm = bcast_u64(segm, k);
+      R.L = readlane32(L, k);
+      R.dead = readlane32(dead, k);
+      R.lm = readlane32(lm, k);
+      R.nx = XR ? readlane32(nx, k) : 0u;
 #pragma unroll
-    for (u32 u = 0; u < kBU; ++u) nb[u] = ntail;
-    if (bm) {
-      const u32 k = (u32)__builtin_ctzll(bm);
-      big_round(bcast_u64(src, k), readlane32(L, k), 0u, big_phase(bcast_u64(pos, k)), nb, ntail);
-    }
-    for (; bm; ) {
-      const u32 k = (u32)__builtin_ctzll(bm);
-      bm &= bm - 1ull;
+      for (u32 q = 0; q < kMaxRemote; ++q) R.x[q] = XR ? bcast_u64(xdst[q], k) : 0ull;
+      R.ph = big_phase(R.pos);
+      R.m = (R.L + 15u) >> 4;
+      return R;
+    };
+    u32 k = (u32)__builtin_ctzll(bm);
+    bm &= bm - 1ull;
+    BigRec cur = take(k);
+    uint4 nb[kBU], ntail;
+    big_round(cur.src, cur.L, 0u, cur.ph, nb, ntail);
+    u32 k0 = 0, acc = 0;
+    for (;;) {
       uint4 cb[kBU];
 #pragma unroll
       for (u32 u = 0; u < kBU; ++u) cb[u] = nb[u];
       const uint4 ctail = ntail;
-      if (bm) {
-        const u32 k2 = (u32)__builtin_ctzll(bm);
-        big_round(bcast_u64(src, k2), readlane32(L, k2), 0u, big_phase(bcast_u64(pos, k2)), nb, ntail);
+      const bool more = 64u * (k0 + kBU) < cur.m + cur.ph, last = !more && !bm;
+      BigRec nxt = cur;
+      if (more) {
+        big_round(cur.src, cur.L, k0 + kBU, cur.ph, nb, ntail);
+      } else if (bm) {
+        nxt = take((u32)__builtin_ctzll(bm));
+        bm &= bm - 1ull;
+        big_round(nxt.src, nxt.L, 0u, nxt.ph, nb, ntail);
       }
-      u64 xk[kMaxRemote];
-      const u32 nxk = XR ? readlane32(nx, k) : 0u;
-#pragma unroll
-      for (u32 q = 0; q < kMaxRemote; ++q) xk[q] = XR ? bcast_u64(xdst[q], k) : 0ull;
-      big_record(A, S, XR ? A.crc->zshift1k : S.zk, bcast_u64(src, k), readlane32(L, k), bcast_u64(pos, k),
-                 bcast_u64(off, k), readlane32(dead, k), reinterpret_cast<uint8_t*>(bcast_u64(ringb, k)),
-                 bcast_u64(segm, k), readlane32(lm, k), xk, nxk, cb, ctail);
+      big_store_round(A, S, XR ? A.crc->zshift1k : S.zk, cur, k0, cb, ctail, acc);
+      if (more) {
+        k0 += kBU;
+        continue;
+      }
+      big_close(A, cur, acc);
+      if (last) break;
+      cur = nxt;
+      k0 = 0;
+      acc = 0;
     }
   }
 }

@@ -14,7 +14,7 @@
 #   benchD     config D (RF 5, 64 B..16 KB) line
 #   ab[:NAME]  A/B of the current library against variants/NAME/ (default head; 400- and 20-step lines, 2 pairs)
 #   local2     2-rank rehearsal on one GPU over the in-process transport (+ kernel trace)
-#   local4     4-rank rehearsal (config C shape)
+#   local4     4-rank rehearsal (config C shape);  local8  the same with 8 ranks
 #   ab2[:NAME] A/B of the 2-rank rehearsal against variants/NAME/ (default head)
 #   prof       rocprofv3 --kernel-trace --stats of the default line (kernel stats CSV)
 #   pmc        rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate runs) of a 300-step line
@@ -82,6 +82,8 @@ for step in "$@"; do
       V=${step#local2kt:}
       RMQ_LIB=$R/variants/$V/libripplemq_engine.so prof 300 local2_prof_$V --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_local2_kt_$V" -o kt -- python3 "$R/bench.py" --gpus 2 --transport local --steps 100 --warmup 10 --segment-mb 2 --pool 8 $Q ;;
     local4) run 300 "${T}_local4.json" python bench.py --gpus 4 --transport local --steps 100 --warmup 10 --segment-mb 1 --pool 4 --config C $Q ;;
+    local8)  # the N = 8 bench path (8 ranks, configs[3]'s shape) as threads on one GPU
+      run 400 "${T}_local8.json" python bench.py --gpus 8 --transport local --steps 60 --warmup 6 --segment-mb 1 --pool 4 --config C $Q ;;
     prof) prof 500 prof --kernel-trace --stats -f csv -d "$R/gpurun_out/${T}_prof" -o kt -- python3 "$R/bench.py" --no-cpu-baseline --host-steps 0 ;;
     pmc)
       prof 150 pmc_fetch --pmc FETCH_SIZE -f csv -d "$R/gpurun_out/${T}_pmc_fetch" -o pf -- python3 "$R/bench.py" --steps 300 --warmup 50 $Q
