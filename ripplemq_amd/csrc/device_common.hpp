@@ -36,6 +36,7 @@ struct CrcConsts {
   u32 inv_pad[16];        // inv_pad[n] = x^(-8n) mod P: "remove n trailing zero bytes"
   u32 sh16[64];           // sh16[e] = x^(8 * 16 * e) mod P: shift past e 16-byte pieces
   u32 inv_pad16[16];      // inv_pad16[n] = inv_pad[n] * x^16: the low half of a split pad removal
+  u32 nib[16][32];        // the 16 tables of table and zshift in order by nibble: t[b] = nib[q][b & 15] ^ nib[q][16 + (b >> 4)]
 };
 
 // FORMAT.md §1 record size: 16-byte header + payload padded to kRecAlign.
@@ -112,6 +113,24 @@ __device__ __forceinline__ u32 crc_step8(const u32 (*t)[256], u32 c, u32 lo, u32
 // Register shift past 16 << k zero bytes (k = 0, 1) by a 4 x 256 table (linearity in the register).
 __device__ __forceinline__ u32 crc_zshift(const u32 (*z)[256], u32 c) {
   return z[0][c & 0xFF] ^ z[1][(c >> 8) & 0xFF] ^ z[2][(c >> 16) & 0xFF] ^ z[3][c >> 24];
+}
+
+// The 16 KB of table and zshift (sixteen 256-entry tables, contiguous at `tabs`) built in LDS from
+// their 2 KB of nibble tables: every table is GF(2)-linear in its byte, so entry b is
+// nib[q][b & 15] ^ nib[q][16 + (b >> 4)]. Copying the 16 KB from L2 was two of the ~4.8 L1->L2 read
+// requests per record of the stage-3 launch (profiles/r06_stage3_counters.txt); the nibble tables
+// are a quarter of one. `scratch`: 2 KB of LDS nothing else touches until the caller's next
+// barrier. Holds one workgroup barrier (every thread of the workgroup must call it).
+template <u32 kThreads>
+__device__ __forceinline__ void crc_tables_lds(const CrcConsts* crc, u32* tabs, u32* scratch) {
+  static_assert(sizeof(CrcConsts::nib) == 128 * 16 && kThreads >= 128, "one 16-byte block per thread");
+  if (threadIdx.x < 128u)
+    reinterpret_cast<uint4*>(scratch)[threadIdx.x] = reinterpret_cast<const uint4*>(&crc->nib[0][0])[threadIdx.x];
+  __syncthreads();
+  for (u32 b = threadIdx.x; b < 256u; b += kThreads) {
+#pragma unroll
+    for (u32 q = 0; q < 16u; ++q) tabs[256u * q + b] = scratch[32u * q + (b & 15u)] ^ scratch[32u * q + 16u + (b >> 4)];
+  }
 }
 
 // CRC register of one 16-byte piece (two slicing-by-8 steps from a zero register).

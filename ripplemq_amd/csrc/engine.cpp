@@ -92,6 +92,15 @@ void build_crc_consts(CrcConsts* c) {
     c->inv_pad16[n] = host_mulmod(c->inv_pad[n], x2n[4]);
     x8n = host_mulmod(x8n, x2n[3]);
   }
+  // nibble tables of the sixteen LDS tables of stage 3 (table[0..7], then zshift[0][0..3],
+  // zshift[1][0..3], as laid out in LDS): each is GF(2)-linear in its byte
+  for (uint32_t q = 0; q < 16; ++q) {
+    const uint32_t* t = q < 8 ? c->table[q] : c->zshift[(q - 8) / 4][(q - 8) % 4];
+    for (uint32_t n = 0; n < 16; ++n) {
+      c->nib[q][n] = t[n];
+      c->nib[q][16 + n] = t[n << 4];
+    }
+  }
 }
 
 bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }

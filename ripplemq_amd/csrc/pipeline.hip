@@ -2504,11 +2504,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
     const bool ha = task < tasks, hb = tb < tasks;  // (wave-uniform)
     const TaskPos Ta = task_pos(G, ha ? task : 0u), Tb = task_pos(G, hb ? tb : 0u);
     const TaskRec Ra = stage3_r1(A, Ta), Rb = stage3_r1(A, Tb);
-    if (!(A.debug & 8u)) {
-      const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
-      uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-      for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];
-    }
+    if (!(A.debug & 8u)) crc_tables_lds<kPT>(A.crc, &S.t8[0][0], reinterpret_cast<u32*>(&S.img[0][0][0]));
     const bool ca = ha && stage3_cand(A, Ta, Ra), cb = hb && stage3_cand(A, Tb, Rb);
     const TaskState Za = stage3_r2(A, Ta, Ra, ca);
     const TaskState Zb = stage3_r2(A, Tb, Rb, cb);
@@ -2528,12 +2524,10 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   TaskPos T = task_pos(G, task < tasks ? task : 0u);
   TaskRec R = stage3_r1(A, T);
   if (!(A.debug & 8u)) {
-    // slicing and zero-shift tables are contiguous in CrcConsts and in Stage3Smem: 16-byte copies
+    // the slicing and zero-shift tables (contiguous in Stage3Smem) from their nibble tables, through
+    // the image area (first written after the barrier below)
     static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
-    static_assert(offsetof(CrcConsts, zshift) == sizeof(A.crc->table), "table and zshift adjacent");
-    const uint4* src = reinterpret_cast<const uint4*>(&A.crc->table[0][0]);
-    uint4* dst = reinterpret_cast<uint4*>(&S.t8[0][0]);
-    for (u32 k = threadIdx.x; k < (sizeof(S.t8) + sizeof(S.z)) / 16u; k += kPT) dst[k] = src[k];  // zk: large-record waves
+    crc_tables_lds<kPT>(A.crc, &S.t8[0][0], reinterpret_cast<u32*>(&S.img[0][0][0]));
   }
   bool cand = task < tasks && stage3_cand(A, T, R);
   TaskState Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u);
