@@ -120,17 +120,26 @@ __device__ __forceinline__ u32 crc_zshift(const u32 (*z)[256], u32 c) {
 // nib[q][b & 15] ^ nib[q][16 + (b >> 4)]. Copying the 16 KB from L2 was two of the ~4.8 L1->L2 read
 // requests per record of the stage-3 launch (profiles/r06_stage3_counters.txt); the nibble tables
 // are a quarter of one. `scratch`: 2 KB of LDS nothing else touches until the caller's next
-// barrier. Holds one workgroup barrier (every thread of the workgroup must call it).
+// barrier. crc_nib_lds holds one workgroup barrier (every thread of the workgroup must call it).
 template <u32 kThreads>
-__device__ __forceinline__ void crc_tables_lds(const CrcConsts* crc, u32* tabs, u32* scratch) {
+__device__ __forceinline__ void crc_nib_lds(const CrcConsts* crc, u32* scratch) {
   static_assert(sizeof(CrcConsts::nib) == 128 * 16 && kThreads >= 128, "one 16-byte block per thread");
   if (threadIdx.x < 128u)
     reinterpret_cast<uint4*>(scratch)[threadIdx.x] = reinterpret_cast<const uint4*>(&crc->nib[0][0])[threadIdx.x];
   __syncthreads();
+}
+template <u32 kThreads>
+__device__ __forceinline__ void crc_expand_lds(u32* tabs, const u32* scratch) {
   for (u32 b = threadIdx.x; b < 256u; b += kThreads) {
 #pragma unroll
     for (u32 q = 0; q < 16u; ++q) tabs[256u * q + b] = scratch[32u * q + (b & 15u)] ^ scratch[32u * q + 16u + (b >> 4)];
   }
+}
+// (both halves; the caller may issue loads between them)
+template <u32 kThreads>
+__device__ __forceinline__ void crc_tables_lds(const CrcConsts* crc, u32* tabs, u32* scratch) {
+  crc_nib_lds<kThreads>(crc, scratch);
+  crc_expand_lds<kThreads>(tabs, scratch);
 }
 
 // CRC register of one 16-byte piece (two slicing-by-8 steps from a zero register).

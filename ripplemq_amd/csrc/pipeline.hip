@@ -1517,7 +1517,7 @@ __device__ __forceinline__ void rec_place(const RecWords& W, const TaskRec& R, u
 }
 
 __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos& T, const TaskRec& R, bool cand,
-                                               bool stage = false) {
+                                               bool stage = false, RecWords* defer = nullptr) {
   TaskState S;
   S.pos = S.off = 0ull;
   S.lm = S.dead = S.rel16 = S.rk = 0u;
@@ -1552,7 +1552,10 @@ __device__ __forceinline__ TaskState stage3_r2(const PipeArgs& A, const TaskPos&
   } else {
     round_blocks(A, R, 0u, cand, S.blk);
   }
-  if (cand) rec_place(W, R, S.pos, S.off, S.dead, S.lm, S.rk, S.rel16);
+  if (defer)
+    *defer = W;  // placed by the caller (rec_place) after work that does not wait for these loads
+  else if (cand)
+    rec_place(W, R, S.pos, S.off, S.dead, S.lm, S.rk, S.rel16);
   return S;
 }
 
@@ -2523,14 +2526,16 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   // first task: its record and state/payload loads are in flight while the CRC tables fill LDS
   TaskPos T = task_pos(G, task < tasks ? task : 0u);
   TaskRec R = stage3_r1(A, T);
-  if (!(A.debug & 8u)) {
-    // the slicing and zero-shift tables (contiguous in Stage3Smem) from their nibble tables, through
-    // the image area (first written after the barrier below)
-    static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
-    crc_tables_lds<kPT>(A.crc, &S.t8[0][0], reinterpret_cast<u32*>(&S.img[0][0][0]));
-  }
+  // the slicing and zero-shift tables (contiguous in Stage3Smem) from their nibble tables, through
+  // the image area (first written after the barrier below); the expansion runs while the record's
+  // state and payload loads are in flight
+  static_assert(offsetof(Stage3Smem, z) == sizeof(S.t8), "t8 and z adjacent in LDS");
+  if (!(A.debug & 8u)) crc_nib_lds<kPT>(A.crc, reinterpret_cast<u32*>(&S.img[0][0][0]));
   bool cand = task < tasks && stage3_cand(A, T, R);
-  TaskState Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u);
+  RecWords W0;
+  TaskState Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u, &W0);
+  if (!(A.debug & 8u)) crc_expand_lds<kPT>(&S.t8[0][0], reinterpret_cast<const u32*>(&S.img[0][0][0]));
+  if (cand) rec_place(W0, R, Z.pos, Z.off, Z.dead, Z.lm, Z.rk, Z.rel16);
   __syncthreads();
   PIPE_STAMP(1);
   while (task < tasks) {
