@@ -404,13 +404,13 @@ def tier_leg(eng, step, spec: StreamSpec, rounds: int, appends: int, parts: int 
     stride = max(1, spec.partitions // parts)  # every stride-th partition: an even sample of the Zipf ranks
     pidx = np.arange(0, spec.partitions, stride, dtype=np.uint32)
     P = len(pidx)
-    cursor = eng.cfg.max_consumers - 1  # the tier's durability cursor (a consumer slot of its own)
+    cursor = eng.cfg.max_consumers - 1  # keys the replica reads' position cache
     eng.sync()
     st = eng.states()[pidx]
-    eng.commit_consumer_offset(pidx, np.full(P, cursor, np.uint32), st["log_start_offset"])
     root = tempfile.mkdtemp(prefix="rmq_tier_", dir=os.environ.get("RMQ_TIER_DIR"))
     try:
-        tier = DurableLog(eng, root, pidx, cursor, segment_file_bytes=256 << 20)
+        # attached to a running engine: each partition's files start at its current log start
+        tier = DurableLog(eng, root, pidx, cursor, segment_file_bytes=256 << 20, start=st["log_start_offset"])
         first = tier.spill()  # untimed: the retained windows at the start
         size0 = sum(int(f.pos[-1]) for f in tier.parts.values())
         tier.phase_s.clear()

@@ -305,7 +305,7 @@ class DurableLog:
     replica of, led or followed), fed by spill from the engine's own replica."""
 
     def __init__(self, engine, directory: str, partitions, cursor: int, *,
-                 segment_file_bytes: int = 64 << 20, fsync: bool = False):
+                 segment_file_bytes: int = 64 << 20, fsync: bool = False, start=None):
         self.engine = engine
         self.dir = directory
         self.cursor = int(cursor)
@@ -331,12 +331,20 @@ class DurableLog:
         self._fd = np.full(len(self._files), -1, np.int64)
         self._limit = int(segment_file_bytes)
         self.phase_s: dict[str, float] = {}
+        # `start` (one offset per partition, in `partitions` order): a tier attached to an engine
+        # that already holds records begins a partition without files at that offset (its log start:
+        # the records below it were never durable and are gone from the ring)
+        if start is not None:
+            fresh = np.fromiter((not f.seg_first for f in self._files), bool, len(self._files))
+            st = np.asarray(start, np.int64).reshape(-1)
+            if st.size != len(self._files):
+                raise ValueError("start: one offset per partition")
+            self._end[fresh] = np.maximum(self._end[fresh], st[fresh])
         # a reopened tier continues where its files end: the replica cursors name that offset
         # (`cursor` only keys the replica reads' position cache; no consumer slot is used)
         pidx = np.fromiter(self.parts, np.uint32, len(self.parts))
-        ends = np.fromiter((f.end for f in self.parts.values()), np.uint64, len(self.parts))
         if len(pidx):
-            self.engine.set_replica_cursor(pidx, ends)
+            self.engine.set_replica_cursor(pidx, self._end.astype(np.uint64))
 
     def end(self, p: int) -> int:
         return self.parts[p].end

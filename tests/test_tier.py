@@ -189,3 +189,35 @@ def test_native_record_scan_matches_the_format(oracle_mod):
     pad[int(want[2]) + 16 + 15] = 7  # record 2 (15 B payload): its pad byte, records follow
     with pytest.raises(Exception):
         whole_records(pad, 0)
+
+
+def test_tier_attached_to_a_running_engine(oracle_mod, tmp_path):
+    """A tier opened on an engine whose rings already dropped records (bench.py's tier leg): its
+    files start at each partition's log start (`start=`); without it the first spill asks for
+    offset 0, which is gone, and refuses with RMQ_EOFFSET instead of spilling a gap."""
+    from ripplemq_amd import _abi as A
+    from ripplemq_amd.engine import EngineError
+    cfg = EngineConfig(num_partitions=P, replication_factor=2, segment_bytes=1 << 13, index_interval=256,
+                       max_consumers=4, max_batch_records=4096)
+    g = np.random.default_rng(7)
+    msgs = {p: [] for p in range(P)}
+    with oracle_mod.OracleEngine(cfg) as eng:
+        for _ in range(30):
+            pidx = g.integers(0, P, 50).astype(np.uint32)
+            lens = g.integers(1, 120, 50).astype(np.uint32)
+            pay = g.integers(0, 256, int(lens.sum())).astype(np.uint8)
+            eng.append(pidx, lens, pay)
+            pos = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+            for i, p in enumerate(pidx.tolist()):
+                msgs[p].append(bytes(pay[pos[i]:pos[i + 1]]))
+        starts = np.array([eng.state(p)["log_start_offset"] for p in range(P)], np.int64)
+        assert starts.min() > 0
+        with pytest.raises(EngineError) as ex:
+            DurableLog(eng, str(tmp_path / "plain"), range(P), 3).spill()
+        assert ex.value.status == A.RMQ_EOFFSET
+        tier = DurableLog(eng, str(tmp_path / "late"), range(P), 3, start=starts)
+        assert tier.spill() == sum(len(msgs[p]) for p in range(P)) - int(starts.sum())
+        for p in range(P):
+            assert tier.end(p) == len(msgs[p])
+            got = [m for _, _, m in tier.read(p, int(starts[p]), len(msgs[p]))]
+            assert got == msgs[p][int(starts[p]):], p
