@@ -436,9 +436,9 @@ struct rmq_engine {
   uint64_t* state_stage = nullptr;  // page-locked staging of rmq_get_partition_states
   size_t state_stage_words = 0;
   uint32_t s3_pair = 0;         // RMQ_S3_PAIR=1: stage-3 waves take two tasks each (single-GPU kernel)
-  uint64_t late_done = 0;
+  uint64_t late_done = 0;       // the applied group (by launch) whose late retention ran (late_retention)
   std::vector<uint32_t> fpend;  // slots of asynchronous fetches whose kernels wait for fetch_flush (under mu)
-  uint32_t fetch_coalesce = kFetchBatch;  // RMQ_FETCH_COALESCE: asynchronous fetches launched together (1: none)       // the applied group (by launch) whose late retention ran (late_retention)
+  uint32_t fetch_coalesce = kFetchBatch;  // RMQ_FETCH_COALESCE: asynchronous fetches launched together (1: none)
   uint32_t s3_stage = 1;        // RMQ_S3_STAGE (default 1): stage-3 payload spans by coalesced loads through LDS
   uint32_t s3_roles = 0;        // RMQ_S3_ROLES=k: stage 3 in loader / storer waves, k workgroups per CU (single-GPU kernel)
   uint32_t s3_xcd = 1;          // RMQ_S3_XCD (default 1): stage-3 tasks in contiguous ranges per XCD
