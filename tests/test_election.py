@@ -139,3 +139,72 @@ def test_election_gpu(oracle_mod):
         for e in engs:
             e.close()
         hub.close()
+
+
+@pytest.mark.gpu
+def test_vote_with_groups_in_flight_gpu():
+    """rmq_vote is not collective: a leader whose launch groups are still forming or in
+    flight answers RMQ_PENDING (the Python call: not granted) and changes nothing — no flush, which
+    with a transport every rank would have to join; after the next collective sync the same
+    RequestVote of a newer term is granted and the leader steps down."""
+    import threading
+
+    from repl_sim import place
+    from ripplemq_amd.engine import Engine, LocalHub
+
+    views = [rank_view(r, WORLD, PPR, RF) for r in range(WORLD)]
+    cfgs = [rank_cfg(EngineConfig(**BASE), views[r], r) for r in range(WORLD)]
+    hub = LocalHub(WORLD)
+    engs = [Engine(c) for c in cfgs]
+    bar = threading.Barrier(WORLD, timeout=120)
+    seen = {}
+    errs = []
+
+    def body(r):
+        try:
+            e = engs[r]
+            e.attach_local(hub)
+            place(e, views[r])
+            bs = led_batches(SPEC, views[r], r, 1, _salt(0) + 1000 * r)
+            led = int(np.flatnonzero(views[r].ranks[np.arange(PPR), views[r].leader_slot] == r)[0])
+            bar.wait()
+            if r == 0:
+                for b in bs:
+                    e.append_async(b.pidx, b.lens, b.payload)  # a group forming on rank 0 only
+                t0 = e.lib.rmq_vote  # (the raw status, through the Python wrapper's argument types)
+                import ctypes as C
+                g = C.c_uint32(7)
+                seen["rc"] = t0(e.h, led, 5, 1, 99, 1 << 40, C.byref(g))
+                seen["granted"] = g.value
+            bar.wait()
+            if r != 0:
+                e.append_async(np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint8))
+            e.sync()  # collective: the round carries rank 0's group
+            bar.wait()
+            if r == 0:
+                before = e.state(led)
+                seen["before"] = (before["term"], before["is_leader"])
+                seen["again"] = e.vote(led, 5, 1, 99, 1 << 40)
+                after = e.state(led)
+                seen["after"] = (after["term"], after["is_leader"])
+            bar.wait()
+        except BaseException as ex:  # noqa: BLE001 - reported below
+            errs.append((r, ex))
+            bar.abort()
+
+    ts = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(WORLD)]
+    try:
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(240)
+            assert not t.is_alive(), "a rank hung"
+        assert not errs, errs
+        from ripplemq_amd import _abi as A
+        assert seen["rc"] == A.RMQ_PENDING and seen["granted"] == 0, seen
+        assert seen["before"] == (1, 1), seen  # nothing changed by the pending vote
+        assert seen["again"] is True and seen["after"] == (5, 0), seen
+    finally:
+        for e in engs:
+            e.close()
+        hub.close()

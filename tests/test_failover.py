@@ -126,6 +126,46 @@ def fresh_replica_script(seg=1 << 16, world=4, rf=3, ppr=2):
     return views, script, dict(BASE, segment_bytes=seg), (f, g)
 
 
+def unknown_term_vote_script(world=4, rf=3, ppr=2):
+    """A follower filled by a PARTIAL catch-up that ends below the leader's term start does not
+    know the term of its last entry (the round word carries 0); it must keep an upper bound of it
+    (the term before the leader's), never 0, or it would grant a candidate of an older last term
+    with a shorter log (Raft's election restriction). Partition 0 (rank 0) runs four
+    term-1 rounds, rank 0 starts term 2, replica slot 2 moves to the empty rank f; the catch-up
+    reserve (one round bound: small batches here) covers only a prefix of f's gap, below term 2's
+    start. Then f answers RequestVotes of term 3 from a candidate whose last log term is 1: one log
+    shorter than f's (refused), one as long (granted, term 4)."""
+    views, script, base, (f, g) = fresh_replica_script(1 << 16, world, rf, ppr)
+    base = dict(base, max_batch_records=64, max_batch_bytes=4096)
+    spec = StreamSpec(ppr, 60, "uniform", size=(50, 100), config_index=95)
+    new = script[3][1]
+    lead = [("lead", {0: [(0, 2)]})]
+    script = [("round", _round(spec, world, k)) for k in range(4)] + lead + [("place", new)]
+    script += [("round", _round(spec, world, 4)), ("state", [f]), ("round", _round(spec, world, 5)), ("state", [f])]
+    script += [("vote", {f: [(g, 3, 1, 1, -1), (g, 4, 1, 1, 0)]}), ("state", [f])]
+    return views, script, base, (f, g)
+
+
+def _check_unknown_term_vote(script, out, f):
+    ks = [k for k, s in enumerate(script) if s[0] == "state"]
+    fp = len(out[ks[0]][f]) - 1  # rank f's slot of partition 0 (its last local partition)
+    first, second = out[ks[0]][f][fp], out[ks[1]][f][fp]
+    assert first["log_end_offset"] == 0  # refused: its log did not match
+    # the partial catch-up: some records, below the term start, the last term unknown (reported 0)
+    assert 0 < second["log_end_offset"] and second["last_log_term"] == 0, second
+    votes = out[[k for k, s in enumerate(script) if s[0] == "vote"][0]][f]
+    assert votes == [False, True], votes
+
+
+def test_unknown_last_term_votes_strictly(oracle_mod):
+    views, script, base, (f, g) = unknown_term_vote_script()
+    cfgs, oras, out = _oracle_run(oracle_mod, views, script, base)
+    try:
+        _check_unknown_term_vote(script, out, f)
+    finally:
+        _close(oras)
+
+
 def offset_ticket_script(world=3, rf=3, ppr=4):
     """Consumer-offset completion (ConsumerOffsetUpdateRequestProcessor.java:40-49,60: the reply comes
     from the Raft closure, after the commit). Rank 0 commits offsets (ticket T1): pending until a
@@ -411,6 +451,13 @@ def test_new_leader_serves_committed_records_gpu(oracle_mod):
     for rec in got[_k(script, "fetch", 0)]:
         if rec is not None:
             assert np.all(rec[1]["count"] > 0), rec[1]
+
+
+@pytest.mark.gpu
+def test_unknown_last_term_votes_strictly_gpu(oracle_mod):
+    views, script, base, (f, g) = unknown_term_vote_script()
+    got, _ = _gpu_vs_oracle(oracle_mod, views, script, base)
+    _check_unknown_term_vote(script, got, f)
 
 
 @pytest.mark.gpu

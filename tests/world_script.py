@@ -18,6 +18,8 @@ RCCL) and on per-rank oracles (tests/repl_sim.py rounds). Steps:
         global partition gid go as a vote request to every replica of gid in the current placement
         (the candidate first); every rank records its votes [(gid, candidate, granted)]; with durable
         tiers a granted vote is saved (DurableLog.save_vote) before it counts
+  ("vote", {rank: [(gid, term, cand, last_log_term, dleo)]})  RequestVotes with explicit candidate
+        logs (log end = the voter's own log end + dleo); the grants are recorded
   ("spill", ranks)                  DurableLog.spill of those ranks' tiers (records moved)
   ("tier_read", {rank: (gid, off, max)})  records [off, off + max) of gid from that rank's tier files
 
@@ -60,6 +62,11 @@ def _vote(eng, tier, p, term, cand, lt, leo):
     if g and tier is not None:
         tier.save_vote(p, term, cand)  # durable before the grant is answered (raft_meta votedFor)
     return g
+
+
+def _vote_rel(eng, tier, p, term, cand, lt, dleo):
+    """A RequestVote whose candidate log ends dleo records from the voter's own log end."""
+    return _vote(eng, tier, p, term, cand, lt, int(eng.state(p)["log_end_offset"]) + int(dleo))
 
 
 def run_oracle(oras, views0, script, tiers=None):
@@ -113,6 +120,10 @@ def run_oracle(oras, views0, script, tiers=None):
                     g = _vote(oras[v], tiers[v], _local(views[v], gid), term, cand, st["last_log_term"],
                               st["log_end_offset"])
                     rec[v].append((gid, cand, g))
+        elif kind == "vote":
+            for r, items in step[1].items():
+                rec[r] = [_vote_rel(oras[r], tiers[r], _local(views[r], gid), term, cand, lt, dleo)
+                          for gid, term, cand, lt, dleo in items]
         elif kind == "spill":
             for r in step[1]:
                 rec[r] = tiers[r].spill()
@@ -198,6 +209,10 @@ def run_gpu(engs, hub, views0, script, timeout=240, tiers=None):
                                 g = _vote(e, tiers[r], _local(views[r], gid), term, cand, lt, leo)
                                 out[k][r].append((gid, cand, g))
                             bar.wait()
+                elif kind == "vote":
+                    if r in step[1]:
+                        out[k][r] = [_vote_rel(e, tiers[r], _local(views[r], gid), term, cand, lt, dleo)
+                                     for gid, term, cand, lt, dleo in step[1][r]]
                 elif kind == "spill":
                     if r in step[1]:
                         out[k][r] = tiers[r].spill()
@@ -247,5 +262,5 @@ def compare_outcomes(script, got, want):
                 assert g[0] == w[0] and np.array_equal(g[1], w[1]), (k, r, g, w)
             elif step[0] == "poll" and w is not None:
                 assert g == w, (k, r, g, w)
-            elif step[0] in ("silent", "elect", "state", "spill", "tier_read") and w is not None:
+            elif step[0] in ("silent", "elect", "vote", "state", "spill", "tier_read") and w is not None:
                 assert g == w, (k, step[0], r, g, w)
