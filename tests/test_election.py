@@ -166,7 +166,8 @@ def test_vote_with_groups_in_flight_gpu():
             e.attach_local(hub)
             place(e, views[r])
             bs = led_batches(SPEC, views[r], r, 1, _salt(0) + 1000 * r)
-            led = int(np.flatnonzero(views[r].ranks[np.arange(PPR), views[r].leader_slot] == r)[0])
+            v = views[r]
+            led = int(np.flatnonzero(v.ranks[np.arange(len(v.gp)), v.leader_slot] == r)[0])
             bar.wait()
             if r == 0:
                 for b in bs:
