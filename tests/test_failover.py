@@ -130,18 +130,18 @@ def unknown_term_vote_script(world=4, rf=3, ppr=2):
     """A follower filled by a PARTIAL catch-up that ends below the leader's term start does not
     know the term of its last entry (the round word carries 0); it must keep an upper bound of it
     (the term before the leader's), never 0, or it would grant a candidate of an older last term
-    with a shorter log (Raft's election restriction). Partition 0 (rank 0) runs four
+    with a shorter log (Raft's election restriction). Partition 0 (rank 0) runs five
     term-1 rounds, rank 0 starts term 2, replica slot 2 moves to the empty rank f; the catch-up
     reserve (one round bound: small batches here) covers only a prefix of f's gap, below term 2's
     start. Then f answers RequestVotes of term 3 from a candidate whose last log term is 1: one log
     shorter than f's (refused), one as long (granted, term 4)."""
     views, script, base, (f, g) = fresh_replica_script(1 << 16, world, rf, ppr)
-    base = dict(base, max_batch_records=64, max_batch_bytes=4096)
+    base = dict(base, max_batch_records=64, max_batch_bytes=8192)
     spec = StreamSpec(ppr, 60, "uniform", size=(50, 100), config_index=95)
     new = script[3][1]
     lead = [("lead", {0: [(0, 2)]})]
-    script = [("round", _round(spec, world, k)) for k in range(4)] + lead + [("place", new)]
-    script += [("round", _round(spec, world, 4)), ("state", [f]), ("round", _round(spec, world, 5)), ("state", [f])]
+    script = [("round", _round(spec, world, k)) for k in range(5)] + lead + [("place", new)]
+    script += [("round", _round(spec, world, 5)), ("state", [f]), ("round", _round(spec, world, 6)), ("state", [f])]
     script += [("vote", {f: [(g, 3, 1, 1, -1), (g, 4, 1, 1, 0)]}), ("state", [f])]
     return views, script, base, (f, g)
 
