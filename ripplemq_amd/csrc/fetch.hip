@@ -27,6 +27,8 @@
 // fetch.
 #include <hip/hip_ext.h>
 
+#include <type_traits>
+
 #include "device_common.hpp"
 #include "kernels.hpp"
 
@@ -255,7 +257,11 @@ __device__ __forceinline__ Resolved resolve_request(const FetchArgs& a, const ui
 
 // The ticket of workgroup b (wg0: first workgroup of each ticket) and b's index inside it; the
 // arguments are read in place from the kernarg segment (an indexed by-value copy could go to scratch).
+// kMulti false: a launch of one ticket (every synchronous fetch, every fetch that commits): its
+// arguments at fixed kernarg offsets, as before batches existed.
+template <bool kMulti>
 __device__ __forceinline__ const FetchArgs& ticket_of(const u32* wg0, u32& b) {
+  if (!kMulti) return *(const FetchArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   const FetchBatch& B = *(const FetchBatch*)__builtin_amdgcn_kernarg_segment_ptr();
   u32 k = 0;
 #pragma unroll
@@ -264,11 +270,16 @@ __device__ __forceinline__ const FetchArgs& ticket_of(const u32* wg0, u32& b) {
   return B.t[k];
 }
 
-__global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchBatch batch) {
+template <bool kMulti>
+using FetchKArgs = typename std::conditional<kMulti, FetchBatch, FetchArgs>::type;  // (t[0] first in both)
+static_assert(offsetof(FetchBatch, t) == 0, "a batch's first ticket at the kernarg base");
+
+template <bool kMulti>
+__global__ __launch_bounds__(64 * kRW) void fetch_resolve_kernel(FetchKArgs<kMulti> batch) {
   (void)batch;
   const FetchBatch& B = *(const FetchBatch*)__builtin_amdgcn_kernarg_segment_ptr();
   u32 bid = blockIdx.x;
-  const FetchArgs& a = ticket_of(B.rwg0, bid);
+  const FetchArgs& a = ticket_of<kMulti>(B.rwg0, bid);
   const u32 lane = lane_id(), w = threadIdx.x >> 6;
   const u32 r = (bid * kRW + w) * kRPW + (lane >> 5);
   const bool live = r < a.n;  // (no early return: the workgroup meets at barriers below)
@@ -327,11 +338,12 @@ constexpr u32 kGR = kFW * kGQ;  // requests per gather workgroup
 // Placement + gather: workgroup per kGR consecutive requests. Two rounds of loads: the wave's
 // request words with the placement sums, then (requests of at most 128 pieces) the records' pieces,
 // issued before the placement barriers; only the stores wait for the output positions.
-__global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchBatch batch) {
+template <bool kMulti>
+__global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchKArgs<kMulti> batch) {
   (void)batch;
   const FetchBatch& B = *(const FetchBatch*)__builtin_amdgcn_kernarg_segment_ptr();
   u32 bid = blockIdx.x;
-  const FetchArgs& a = ticket_of(B.gwg0, bid);
+  const FetchArgs& a = ticket_of<kMulti>(B.gwg0, bid);
   const u32 nwg = (a.n + kGR - 1) / kGR;  // the ticket's gather workgroups
   __shared__ u64 s_red[kFW];
   __shared__ u64 s_pos[kGR];
@@ -472,15 +484,24 @@ __global__ __launch_bounds__(64 * kFW) void fetch_gather_kernel(FetchBatch batch
 // loads it: ~20 ms inside the first rmq_fetch, profiles/r03q_prof).
 void preload_fetch_kernels() {
   hipFuncAttributes fa;
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_resolve_kernel));
-  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_resolve_kernel<false>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel<false>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_resolve_kernel<true>));
+  (void)hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&fetch_gather_kernel<true>));
 }
 
 static void launch_batch(const FetchBatch& b, hipStream_t s, const hipEvent_t* e) {
   if (!b.rwg0[b.nt]) return;
-  hipExtLaunchKernelGGL(fetch_resolve_kernel, dim3(b.rwg0[b.nt]), dim3(64 * kRW), 0, s, e ? e[0] : nullptr,
+  if (b.nt == 1) {  // one ticket: the 4x smaller kernarg, fixed offsets
+    hipExtLaunchKernelGGL(fetch_resolve_kernel<false>, dim3(b.rwg0[1]), dim3(64 * kRW), 0, s, e ? e[0] : nullptr,
+                          e ? e[1] : nullptr, 0, b.t[0]);
+    hipExtLaunchKernelGGL(fetch_gather_kernel<false>, dim3(b.gwg0[1]), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
+                          e ? e[3] : nullptr, 0, b.t[0]);
+    return;
+  }
+  hipExtLaunchKernelGGL(fetch_resolve_kernel<true>, dim3(b.rwg0[b.nt]), dim3(64 * kRW), 0, s, e ? e[0] : nullptr,
                         e ? e[1] : nullptr, 0, b);
-  hipExtLaunchKernelGGL(fetch_gather_kernel, dim3(b.gwg0[b.nt]), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
+  hipExtLaunchKernelGGL(fetch_gather_kernel<true>, dim3(b.gwg0[b.nt]), dim3(64 * kFW), 0, s, e ? e[2] : nullptr,
                         e ? e[3] : nullptr, 0, b);
 }
 
