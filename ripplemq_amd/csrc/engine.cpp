@@ -267,11 +267,13 @@ int launch_stages(rmq_engine* e, const GroupFlight* s1, const GroupFlight* s2, c
     }
     a.wgb = e->big_wgs ? e->big_wgs : 32u * e->cu_count / (PT / 64u);  // 32 large-record waves per CU
     // dispatch order: s3_lead stage-3 workgroups, then ranking, scans and partition threads, then
-    // the rest of stage 3, so the ranking/scan chains start before stage 3's last workgroups and
-    // end with them (RMQ_S3_LEAD=<n>; RMQ_S3_FIRST=0 puts all of stage 3 last)
-    a.s3_lead = e->s3_first ? std::min<uint32_t>(a.wg3, e->s3_lead ? e->s3_lead : a.wg3) : 0u;
-    // (only with every stage-3 workgroup first: then its block index is its stage-3 index)
-    a.s3_xcd = e->s3_xcd && a.s3_lead == a.wg3 && !a.s3_pair ? 1u : 0u;
+    // the rest of stage 3. Round 6 default: all of stage 3 last, so the ranking and scan chains
+    // start with the launch instead of in its tail, when the first stage-3 workgroups retire
+    // (42.5-43.3 vs 43.7-44.0 us per launch, 20-step 34.4-34.7 vs 35.6-35.8, profiles/r06_dispatch_order.txt;
+    // round 2's +2.8 % for stage 3 first no longer holds); RMQ_S3_FIRST=1 all first, RMQ_S3_LEAD=<n> n first
+    a.s3_lead = e->s3_lead ? std::min<uint32_t>(a.wg3, e->s3_lead) : e->s3_first ? a.wg3 : 0u;
+    // (with every stage-3 workgroup first or every one last: one contiguous range of blocks)
+    a.s3_xcd = e->s3_xcd && (a.s3_lead == a.wg3 || a.s3_lead == 0u) && !a.s3_pair ? 1u : 0u;
     a.s3_stage = e->s3_stage;
   }
   a.launch_seq = ++e->launch_seq;

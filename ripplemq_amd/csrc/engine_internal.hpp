@@ -421,7 +421,7 @@ struct rmq_engine {
   uint32_t wg3_all = 1;
   uint32_t s1_wgs = 0;    // RMQ_S1_WGS: stage-1 workgroups per launch (0: one per tile; fewer loop over tiles)
   uint32_t s2_wgs = 0;    // RMQ_S2_WGS: cap on stage-2 workgroups (0: one thread group per column)
-  uint32_t s3_first = 1;  // stage-3 workgroups first in dispatch order (RMQ_S3_FIRST=0: last)
+  uint32_t s3_first = 0;  // RMQ_S3_FIRST=1: stage-3 workgroups first in dispatch order (round 6 default: last, -2.5 %)
   uint32_t s3_lead = 0;   // stage-3 workgroups before the other roles (RMQ_S3_LEAD; 0: all of them)
   uint32_t debug = 0;  // RMQ_DEBUG (timing experiments only; results are invalid when set)
   // Split launches (single-GPU kernel, no transport): each pipeline step is two launches of the

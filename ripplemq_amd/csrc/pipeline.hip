@@ -2491,7 +2491,8 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   // the task index is wave-uniform: keep it (and the batch lookups) in scalar registers
   // (RMQ_S3_XCD: the stage-3 workgroups of one XCD take one contiguous range of slots, so records
   // next to each other in a batch, and in their partitions' rings, are stored through one L2)
-  const u32 slot = A.s3_xcd ? xcd_rank(0, A.wg3, wg) : wg;
+  // (stage 3 first: its blocks are [0, wg3); last: [other, other + wg3))
+  const u32 slot = A.s3_xcd ? xcd_rank(A.s3_lead ? 0u : A.wg1 + A.wg2 + A.wgp, A.wg3, blockIdx.x) : wg;
   if (!XR && A.s3_roles) {
     stage3_roles(A, *reinterpret_cast<Stage3RSmem*>(smem_raw), slot);
     return;

@@ -293,7 +293,7 @@ def test_pipelined_groups(oracle_mod, group):
         assert dev.state(5)["log_end_offset"] == 0
 
 
-@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "0"}, {"RMQ_BIG_WGS": "3"},
+@pytest.mark.parametrize("env", [{"RMQ_WG3_ALL": "0"}, {"RMQ_S3_FIRST": "1"}, {"RMQ_S3_LEAD": "5"}, {"RMQ_BIG_WGS": "3"},
                                  {"RMQ_S3_XCD": "0", "RMQ_S1_XCD": "1"}, {"RMQ_S1_XCD": "1", "RMQ_S1_WGS": "37"},
                                  {"RMQ_S3_ROLES": "0"}, {"RMQ_S3_ROLES": "1", "RMQ_S3_XCD": "0"},
                                  {"RMQ_S3_ROLES": "4"}])
