@@ -285,7 +285,7 @@ struct rmq_engine {
   uint32_t max_ahead = 0;  // RMQ_AHEAD: pipeline launches queued at most (0: unbounded; a bound of
                            // 4 or 8 cost 4-6 % at config B, profiles/r04i_*: bound it in the app)
   uint32_t steal = 0;      // RMQ_STEAL=1: stage-3 workgroups take stage-1 tiles when out of tasks
-  uint32_t prio = 0;  // RMQ_PRIO: stage-1/2 and partition waves at s_setprio 3
+  uint32_t prio = 1;  // RMQ_PRIO (round 6 default 1; 0 off): stage-1/2 and partition waves at s_setprio 3
                            // (5.20 -> 4.00 G msgs/s: stage 2 and the second half of stage 3 start later)
   PipeScratch scratch[kSets]{};
   std::vector<Staging> staging;
