@@ -27,6 +27,8 @@
 #   roles      phase stamps of the role-split stage 3 and of the default launch
 #   sq / memc  SQ / memory-pipeline counters of the apply launches (tools/pmc_apply.sh)
 #   knob:VAR=v1,v2  steady and 20-step lines per value;  dbg:B1,B2  timing-only RMQ_DEBUG lines
+#   coalesce   fetch legs with asynchronous fetch coalescing on / off;  caps:S1:S2,...  ranking caps
+#   fetchab3:V:OLD  fetch legs of the current library, variants/V and the older tree variants/OLD/tree
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -144,6 +146,28 @@ for step in "$@"; do
       RMQ_STAMPS=gpurun_out/${T}_st0.csv RMQ_STAMPS_AT=50 run 200 "${T}_stamped0.json" python bench.py --steps 300 --warmup 30 $Q
       python tools/roles_stamps.py "gpurun_out/${T}_rst.csv" > "gpurun_out/${T}_roles_stamps.txt" 2>&1
       python tools/pipe_stamps.py "gpurun_out/${T}_st0.csv" >> "gpurun_out/${T}_roles_stamps.txt" 2>&1 ;;
+    coalesce)  # fetch legs with asynchronous fetch coalescing on (default) and off, three pairs
+      FQ="--steps 100 --warmup 10 --no-cpu-baseline --concurrent-rounds 0 --host-steps 0 --tier-rounds 0"
+      for k in 1 2 3; do
+        run 200 "${T}_on_$k.json" python bench.py $FQ
+        RMQ_FETCH_COALESCE=1 run 200 "${T}_off_$k.json" python bench.py $FQ
+      done ;;
+    caps:*)  # caps:S1:S2,S1:S2,...  ranking workgroup caps (RMQ_S1_WGS / RMQ_S2_WGS, 0 = none), 400- and 20-step lines, two rounds
+      for k in 1 2; do
+        for c in $(echo "${step#caps:}" | tr , ' '); do
+          s1=${c%%:*}; s2=${c##*:}
+          RMQ_S1_WGS=$s1 RMQ_S2_WGS=$s2 run 200 "${T}_${s1}_${s2}_400_$k.json" python bench.py --steps 400 --warmup 40 $Q
+          RMQ_S1_WGS=$s1 RMQ_S2_WGS=$s2 run 200 "${T}_${s1}_${s2}_20_$k.json" python bench.py --steps 20 --warmup 5 $Q
+        done
+      done ;;
+    fetchab3:*)  # fetchab3:V:OLD  fetch legs of the current library, variants/V and a whole older tree variants/OLD/tree
+      V=${step#fetchab3:}; O=${V#*:}; V=${V%%:*}
+      FQ="--steps 100 --warmup 10 --no-cpu-baseline --concurrent-rounds 0 --host-steps 0 --tier-rounds 0"
+      for k in 1 2; do
+        run 200 "${T}_cur_$k.json" python bench.py $FQ
+        RMQ_LIB=$R/variants/$V/libripplemq_engine.so run 200 "${T}_${V}_$k.json" python bench.py $FQ
+        (cd variants/$O/tree && timeout -k 10 200 python bench.py $FQ) > "gpurun_out/${T}_${O}_$k.json" 2> "gpurun_out/${T}_${O}_$k.json.err" || { echo "[gpu.sh] FAILED $O $k"; exit 1; }
+      done ;;
     sq|memc)  # SQ / memory-pipeline counters of the apply launches (tools/pmc_apply.sh)
       bash tools/pmc_apply.sh "${T}_$step" $([ $step = sq ] && echo sq || echo mem) ;;
     *) echo "[gpu.sh] unknown step $step"; exit 2 ;;
