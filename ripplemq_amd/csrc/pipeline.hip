@@ -1847,7 +1847,7 @@ __device__ __forceinline__ void stage3_finish(const PipeArgs& A, const Stage3Sme
   uint4 blk[kBL];
 #pragma unroll
   for (u32 q = 0; q < kBL; ++q) blk[q] = Z.blk[q];
-  if (!XR && Z.nblk) {
+  if (Z.nblk) {
     // the task's payload span through the wave's image area: every lane's blocks in, then each
     // lane pair's record blocks out (before any image write reuses the area)
     uint4* sg = &W.img[w][0][0];
@@ -2534,7 +2534,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
   if (!(A.debug & 8u)) crc_nib_lds<kPT>(A.crc, reinterpret_cast<u32*>(&S.img[0][0][0]));
   bool cand = task < tasks && stage3_cand(A, T, R);
   RecWords W0;
-  TaskState Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u, &W0);
+  TaskState Z = stage3_r2(A, T, R, cand, A.s3_stage != 0u, &W0);
   if (!(A.debug & 8u)) crc_expand_lds<kPT>(&S.t8[0][0], reinterpret_cast<const u32*>(&S.img[0][0][0]));
   if (cand) rec_place(W0, R, Z.pos, Z.off, Z.dead, Z.lm, Z.rk, Z.rel16);
   __syncthreads();
@@ -2550,7 +2550,7 @@ __global__ __launch_bounds__(kPT, RMQ_PIPE_WAVES_PER_SIMD) void pipeline_kernel(
       T = task_pos(G, task);
       R = stage3_r1(A, T);
       cand = stage3_cand(A, T, R);
-      Z = stage3_r2(A, T, R, cand, !XR && A.s3_stage != 0u);
+      Z = stage3_r2(A, T, R, cand, A.s3_stage != 0u);
     }
   }
   if (A.stamps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
